@@ -1,0 +1,806 @@
+/*
+ * gsr_oracle.c -- CPU restatement of the differentiable 3DGS rasterizer.
+ * TEST INFRASTRUCTURE ONLY (see gsr_oracle.h).  Compiled with
+ * -ffp-contract=off and no fast-math so that every float feeding a tile key is
+ * produced by the same IEEE operations, in the same order, as the HIP kernels
+ * (bit-exact keys and sort order are part of the parity contract).
+ *
+ * Reference anchors (the reference has no rasterizer):
+ *   - quaternion -> R, (w,x,y,z), w first ........ src/utils/general_utils.cpp:24-37
+ *   - L = R diag(s) ............................. src/utils/general_utils.cpp:91-97
+ *   - Sigma = L L^T, stripped [xx,xy,xz,yy,yz,zz] src/scene/gaussian_model.cpp:23-26,
+ *                                                 src/utils/general_utils.cpp:54-59
+ *   - camera matrices (column-major here) ....... src/scene/camera.cpp:66-71,
+ *                                                 src/utils/graphics_utils.cpp:10-72
+ *   - activations applied by the caller ......... src/scene/gaussian_model.cpp:270-298
+ * Rasterizer stages restate SURVEY.md Appendix B (published 3DGS/EWA algorithm):
+ *   B.1 preprocess  -> preprocess_one()
+ *   B.2 binning     -> bin_instances()
+ *   B.3 blend fwd   -> blend_tile()
+ *   B.4 blend bwd   -> blend_tile_backward()
+ *   B.5 preprocess backward -> preprocess_backward_one()
+ */
+#include "gsr_oracle.h"
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include <float.h>
+
+#define TILE 16
+
+static const float SH_C0 = 0.28209479177387814f;
+static const float SH_C1 = 0.4886025119029199f;
+static const float SH_C2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f,
+                               -1.0925484305920792f, 0.5462742152960396f};
+static const float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f,
+                               0.3731763325901154f, -0.4570457994644658f, 1.445305721320277f,
+                               -0.5900435899266435f};
+
+struct gsro_state {
+    gsro_camera cam;
+    int P, D, M_rest;
+    float bg[3];
+    int tile_y0, tile_y1;
+    int grid_x, grid_y;
+    /* inputs (borrowed pointers, valid until backward) */
+    const float *means3D, *sh_dc, *sh_rest, *colors_precomp, *opacities, *scales, *rotations,
+        *cov3D_precomp;
+    float scale_mod;
+    /* per-Gaussian preprocess */
+    int* radii;
+    float* xy;       /* P*2 */
+    float* depth;    /* P */
+    float* conic_o;  /* P*4 */
+    float* rgb;      /* P*3 */
+    uint8_t* clamped;/* P*3 */
+    uint32_t* tiles_touched; /* band-clipped */
+    int* rect;       /* P*4: minx, miny, maxx, maxy (full image) */
+    uint32_t* inst_start; /* P: first emission index of g */
+    /* instances */
+    int K;
+    uint32_t* s_tile;  /* K sorted */
+    uint32_t* s_depth; /* K sorted depth bits */
+    uint32_t* s_gid;   /* K sorted */
+    uint32_t* s_j;     /* K sorted emission index */
+    uint32_t* ranges;  /* num_tiles*2 */
+    /* pixels */
+    float* final_T;
+    uint32_t* n_contrib;
+    uint64_t pairs;
+};
+
+/* ------------------------------------------------------------------ */
+/* reference math restatements                                          */
+/* ------------------------------------------------------------------ */
+
+/* general_utils.cpp:12-40: normalise q, then R with r = q[0] as real part. */
+void gsro_build_rotation(const float* q_in, float* R) {
+    float n = sqrtf(q_in[0] * q_in[0] + q_in[1] * q_in[1] + q_in[2] * q_in[2] + q_in[3] * q_in[3]);
+    float r = q_in[0] / n, x = q_in[1] / n, y = q_in[2] / n, z = q_in[3] / n;
+    R[0] = 1.f - 2.f * (y * y + z * z);
+    R[1] = 2.f * (x * y - r * z);
+    R[2] = 2.f * (x * z + r * y);
+    R[3] = 2.f * (x * y + r * z);
+    R[4] = 1.f - 2.f * (x * x + z * z);
+    R[5] = 2.f * (y * z - r * x);
+    R[6] = 2.f * (x * z - r * y);
+    R[7] = 2.f * (y * z + r * x);
+    R[8] = 1.f - 2.f * (x * x + y * y);
+}
+
+/* Rotation from an (assumed unit) quaternion, no re-normalisation: the
+ * rasterizer receives get_rotation() output (gaussian_model.cpp:276-280). */
+static void rot_from_quat(const float* q, float* R) {
+    float r = q[0], x = q[1], y = q[2], z = q[3];
+    R[0] = 1.f - 2.f * (y * y + z * z);
+    R[1] = 2.f * (x * y - r * z);
+    R[2] = 2.f * (x * z + r * y);
+    R[3] = 2.f * (x * y + r * z);
+    R[4] = 1.f - 2.f * (x * x + z * z);
+    R[5] = 2.f * (y * z - r * x);
+    R[6] = 2.f * (x * z - r * y);
+    R[7] = 2.f * (y * z + r * x);
+    R[8] = 1.f - 2.f * (x * x + y * y);
+}
+
+/* Sigma = L L^T, L = R diag(mod*s); order [xx,xy,xz,yy,yz,zz] (general_utils.cpp:54-59) */
+static void cov3d_from_R(const float* R, const float* s, float mod, float* c) {
+    float sx = mod * s[0], sy = mod * s[1], sz = mod * s[2];
+    float L[9];
+    for (int i = 0; i < 3; ++i) {
+        L[3 * i + 0] = R[3 * i + 0] * sx;
+        L[3 * i + 1] = R[3 * i + 1] * sy;
+        L[3 * i + 2] = R[3 * i + 2] * sz;
+    }
+#define SIG(i, j) (L[3 * (i) + 0] * L[3 * (j) + 0] + L[3 * (i) + 1] * L[3 * (j) + 1] + L[3 * (i) + 2] * L[3 * (j) + 2])
+    c[0] = SIG(0, 0);
+    c[1] = SIG(0, 1);
+    c[2] = SIG(0, 2);
+    c[3] = SIG(1, 1);
+    c[4] = SIG(1, 2);
+    c[5] = SIG(2, 2);
+#undef SIG
+}
+
+/* gaussian_model.cpp:18-28 + general_utils.cpp:88-99 (normalising build_rotation) */
+void gsro_covariance(const float* s, float mod, const float* q, float* cov6) {
+    float R[9];
+    gsro_build_rotation(q, R);
+    cov3d_from_R(R, s, mod, cov6);
+}
+
+/* ------------------------------------------------------------------ */
+/* B.1 preprocess                                                        */
+/* ------------------------------------------------------------------ */
+static inline float ndc2pix(float v, int S) { return ((v + 1.0f) * (float)S - 1.0f) * 0.5f; }
+
+static inline int imin(int a, int b) { return a < b ? a : b; }
+static inline int imax(int a, int b) { return a > b ? a : b; }
+
+static void sh_basis(int D, float x, float y, float z, float* b) {
+    b[0] = SH_C0;
+    if (D < 1) return;
+    b[1] = -SH_C1 * y;
+    b[2] = SH_C1 * z;
+    b[3] = -SH_C1 * x;
+    if (D < 2) return;
+    float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    b[4] = SH_C2[0] * xy;
+    b[5] = SH_C2[1] * yz;
+    b[6] = SH_C2[2] * (2.0f * zz - xx - yy);
+    b[7] = SH_C2[3] * xz;
+    b[8] = SH_C2[4] * (xx - yy);
+    if (D < 3) return;
+    b[9] = SH_C3[0] * y * (3.0f * xx - yy);
+    b[10] = SH_C3[1] * xy * z;
+    b[11] = SH_C3[2] * y * (4.0f * zz - xx - yy);
+    b[12] = SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy);
+    b[13] = SH_C3[4] * x * (4.0f * zz - xx - yy);
+    b[14] = SH_C3[5] * z * (xx - yy);
+    b[15] = SH_C3[6] * x * (xx - 3.0f * yy);
+}
+
+static void view_dir(const gsro_camera* cam, const float* p, float* dir, float* len_out) {
+    float dx = p[0] - cam->campos[0], dy = p[1] - cam->campos[1], dz = p[2] - cam->campos[2];
+    float len = sqrtf(dx * dx + dy * dy + dz * dz);
+    dir[0] = dx / len;
+    dir[1] = dy / len;
+    dir[2] = dz / len;
+    *len_out = len;
+}
+
+static void preprocess_one(gsro_state* st, int g) {
+    const gsro_camera* cam = &st->cam;
+    const float* V = cam->viewmatrix;
+    const float* Pm = cam->projmatrix;
+    const float* p = st->means3D + 3 * g;
+    st->radii[g] = 0;
+    st->tiles_touched[g] = 0;
+    /* view-space point, transformPoint4x3 */
+    float tx = V[0] * p[0] + V[4] * p[1] + V[8] * p[2] + V[12];
+    float ty = V[1] * p[0] + V[5] * p[1] + V[9] * p[2] + V[13];
+    float tz = V[2] * p[0] + V[6] * p[1] + V[10] * p[2] + V[14];
+    if (tz <= 0.2f) return;
+    /* homogeneous projection, transformPoint4x4 */
+    float hx = Pm[0] * p[0] + Pm[4] * p[1] + Pm[8] * p[2] + Pm[12];
+    float hy = Pm[1] * p[0] + Pm[5] * p[1] + Pm[9] * p[2] + Pm[13];
+    float hw = Pm[3] * p[0] + Pm[7] * p[1] + Pm[11] * p[2] + Pm[15];
+    float pw = 1.0f / (hw + 0.0000001f);
+    float px = hx * pw, py = hy * pw;
+    /* 3D covariance */
+    float c3[6];
+    if (st->cov3D_precomp) {
+        memcpy(c3, st->cov3D_precomp + 6 * g, sizeof(c3));
+    } else {
+        float R[9];
+        rot_from_quat(st->rotations + 4 * g, R);
+        cov3d_from_R(R, st->scales + 3 * g, st->scale_mod, c3);
+    }
+    /* EWA 2D covariance */
+    float W = (float)cam->width, H = (float)cam->height;
+    float fx = W / (2.0f * cam->tanfovx);
+    float fy = H / (2.0f * cam->tanfovy);
+    float limx = 1.3f * cam->tanfovx, limy = 1.3f * cam->tanfovy;
+    float txtz = tx / tz, tytz = ty / tz;
+    float cx = fminf(limx, fmaxf(-limx, txtz)) * tz;
+    float cy = fminf(limy, fmaxf(-limy, tytz)) * tz;
+    float tz2 = tz * tz;
+    float J00 = fx / tz, J02 = -(fx * cx) / tz2;
+    float J11 = fy / tz, J12 = -(fy * cy) / tz2;
+    /* T = J * Wv, Wv rows = (V0,V4,V8),(V1,V5,V9),(V2,V6,V10) */
+    float T0[3], T1[3];
+    for (int k = 0; k < 3; ++k) {
+        T0[k] = J00 * V[4 * k + 0] + J02 * V[4 * k + 2];
+        T1[k] = J11 * V[4 * k + 1] + J12 * V[4 * k + 2];
+    }
+    float S[9] = {c3[0], c3[1], c3[2], c3[1], c3[3], c3[4], c3[2], c3[4], c3[5]};
+    float U0[3], U1[3];
+    for (int j = 0; j < 3; ++j) {
+        U0[j] = T0[0] * S[0 + j] + T0[1] * S[3 + j] + T0[2] * S[6 + j];
+        U1[j] = T1[0] * S[0 + j] + T1[1] * S[3 + j] + T1[2] * S[6 + j];
+    }
+    float a = (U0[0] * T0[0] + U0[1] * T0[1] + U0[2] * T0[2]) + 0.3f;
+    float b = U0[0] * T1[0] + U0[1] * T1[1] + U0[2] * T1[2];
+    float c = (U1[0] * T1[0] + U1[1] * T1[1] + U1[2] * T1[2]) + 0.3f;
+    float det = a * c - b * b;
+    if (det == 0.0f) return;
+    float det_inv = 1.0f / det;
+    float cA = c * det_inv, cB = -b * det_inv, cC = a * det_inv;
+    float mid = 0.5f * (a + c);
+    float disc = fmaxf(0.1f, mid * mid - det);
+    float sq = sqrtf(disc);
+    float l1 = mid + sq, l2 = mid - sq;
+    int radius = (int)ceilf(3.0f * sqrtf(fmaxf(l1, l2)));
+    float xs = ndc2pix(px, cam->width), ys = ndc2pix(py, cam->height);
+    int gx = st->grid_x, gy = st->grid_y;
+    float rf = (float)radius;
+    int minx = imin(gx, imax(0, (int)((xs - rf) / (float)TILE)));
+    int miny = imin(gy, imax(0, (int)((ys - rf) / (float)TILE)));
+    int maxx = imin(gx, imax(0, (int)((xs + rf + (float)(TILE - 1)) / (float)TILE)));
+    int maxy = imin(gy, imax(0, (int)((ys + rf + (float)(TILE - 1)) / (float)TILE)));
+    if ((maxx - minx) * (maxy - miny) == 0) return;
+    /* colour */
+    float* rgb = st->rgb + 3 * g;
+    if (st->colors_precomp) {
+        rgb[0] = st->colors_precomp[3 * g + 0];
+        rgb[1] = st->colors_precomp[3 * g + 1];
+        rgb[2] = st->colors_precomp[3 * g + 2];
+        st->clamped[3 * g + 0] = st->clamped[3 * g + 1] = st->clamped[3 * g + 2] = 0;
+    } else {
+        float dir[3], len;
+        view_dir(cam, p, dir, &len);
+        float basis[16];
+        sh_basis(st->D, dir[0], dir[1], dir[2], basis);
+        int nb = (st->D + 1) * (st->D + 1);
+        for (int ch = 0; ch < 3; ++ch) {
+            float r = basis[0] * st->sh_dc[3 * g + ch];
+            const float* rest = st->sh_rest + (size_t)g * st->M_rest * 3;
+            for (int k = 1; k < nb; ++k) r = r + basis[k] * rest[3 * (k - 1) + ch];
+            r = r + 0.5f;
+            st->clamped[3 * g + ch] = r < 0.0f;
+            rgb[ch] = fmaxf(r, 0.0f);
+        }
+    }
+    /* band-clipped tile count */
+    int by0 = imax(miny, st->tile_y0), by1 = imin(maxy, st->tile_y1);
+    int band_rows = by1 > by0 ? by1 - by0 : 0;
+    st->radii[g] = radius;
+    st->depth[g] = tz;
+    st->xy[2 * g + 0] = xs;
+    st->xy[2 * g + 1] = ys;
+    st->conic_o[4 * g + 0] = cA;
+    st->conic_o[4 * g + 1] = cB;
+    st->conic_o[4 * g + 2] = cC;
+    st->conic_o[4 * g + 3] = st->opacities[g];
+    st->rect[4 * g + 0] = minx;
+    st->rect[4 * g + 1] = miny;
+    st->rect[4 * g + 2] = maxx;
+    st->rect[4 * g + 3] = maxy;
+    st->tiles_touched[g] = (uint32_t)((maxx - minx) * band_rows);
+}
+
+/* ------------------------------------------------------------------ */
+/* B.2 binning: canonical order (tile, depth_bits, gid), rect row-major  */
+/* ------------------------------------------------------------------ */
+typedef struct { uint32_t tile, dbits, gid, j; } inst_t;
+
+static int inst_cmp(const void* a_, const void* b_) {
+    const inst_t* a = (const inst_t*)a_;
+    const inst_t* b = (const inst_t*)b_;
+    if (a->tile != b->tile) return a->tile < b->tile ? -1 : 1;
+    if (a->dbits != b->dbits) return a->dbits < b->dbits ? -1 : 1;
+    if (a->gid != b->gid) return a->gid < b->gid ? -1 : 1;
+    return 0;
+}
+
+static int bin_instances(gsro_state* st) {
+    int P = st->P;
+    uint64_t K = 0;
+    for (int g = 0; g < P; ++g) {
+        st->inst_start[g] = (uint32_t)K;
+        K += st->tiles_touched[g];
+    }
+    if (K > 0x7fffffffULL) return -1;
+    st->K = (int)K;
+    inst_t* inst = (inst_t*)malloc(sizeof(inst_t) * (K ? K : 1));
+    if (!inst) return -2;
+#pragma omp parallel for schedule(dynamic, 1024)
+    for (int g = 0; g < P; ++g) {
+        if (st->tiles_touched[g] == 0) continue;
+        const int* r = st->rect + 4 * g;
+        uint32_t db;
+        memcpy(&db, &st->depth[g], 4);
+        uint32_t j = st->inst_start[g];
+        int y0 = imax(r[1], st->tile_y0), y1 = imin(r[3], st->tile_y1);
+        for (int y = y0; y < y1; ++y)
+            for (int x = r[0]; x < r[2]; ++x) {
+                inst[j].tile = (uint32_t)(y * st->grid_x + x);
+                inst[j].dbits = db;
+                inst[j].gid = (uint32_t)g;
+                inst[j].j = j;
+                ++j;
+            }
+    }
+    qsort(inst, K, sizeof(inst_t), inst_cmp);
+    st->s_tile = (uint32_t*)malloc(4 * (K ? K : 1));
+    st->s_depth = (uint32_t*)malloc(4 * (K ? K : 1));
+    st->s_gid = (uint32_t*)malloc(4 * (K ? K : 1));
+    st->s_j = (uint32_t*)malloc(4 * (K ? K : 1));
+    int nt = st->grid_x * st->grid_y;
+    st->ranges = (uint32_t*)calloc((size_t)nt * 2, 4);
+    for (uint64_t i = 0; i < K; ++i) {
+        st->s_tile[i] = inst[i].tile;
+        st->s_depth[i] = inst[i].dbits;
+        st->s_gid[i] = inst[i].gid;
+        st->s_j[i] = inst[i].j;
+        uint32_t t = inst[i].tile;
+        if (i == 0 || inst[i - 1].tile != t) st->ranges[2 * t] = (uint32_t)i;
+        if (i == K - 1 || inst[i + 1].tile != t) st->ranges[2 * t + 1] = (uint32_t)(i + 1);
+    }
+    free(inst);
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* B.3 blend forward                                                     */
+/* ------------------------------------------------------------------ */
+static uint64_t blend_tile(gsro_state* st, int tile, float* out_color) {
+    int W = st->cam.width, H = st->cam.height;
+    int tx = tile % st->grid_x, ty = tile / st->grid_x;
+    uint32_t beg = st->ranges[2 * tile], end = st->ranges[2 * tile + 1];
+    uint64_t pairs = 0;
+    for (int ly = 0; ly < TILE; ++ly)
+        for (int lx = 0; lx < TILE; ++lx) {
+            int pxi = tx * TILE + lx, pyi = ty * TILE + ly;
+            if (pxi >= W || pyi >= H) continue;
+            float pfx = (float)pxi, pfy = (float)pyi;
+            float T = 1.0f, C[3] = {0, 0, 0};
+            uint32_t contributor = 0, last = 0;
+            for (uint32_t i = beg; i < end; ++i) {
+                contributor++;
+                pairs++;
+                uint32_t g = st->s_gid[i];
+                const float* co = st->conic_o + 4 * g;
+                float dx = st->xy[2 * g] - pfx, dy = st->xy[2 * g + 1] - pfy;
+                float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                if (power > 0.0f) continue;
+                float alpha = fminf(0.99f, co[3] * expf(power));
+                if (alpha < 1.0f / 255.0f) continue;
+                float test_T = T * (1.0f - alpha);
+                if (test_T < 0.0001f) break;
+                const float* c = st->rgb + 3 * g;
+                for (int ch = 0; ch < 3; ++ch) C[ch] += c[ch] * alpha * T;
+                T = test_T;
+                last = contributor;
+            }
+            size_t pix = (size_t)pyi * W + pxi;
+            st->final_T[pix] = T;
+            st->n_contrib[pix] = last;
+            for (int ch = 0; ch < 3; ++ch) out_color[(size_t)ch * H * W + pix] = C[ch] + T * st->bg[ch];
+        }
+    return pairs;
+}
+
+int gsro_forward(const gsro_camera* cam, int P, int D, int M_rest, const float* bg,
+                 const float* means3D, const float* sh_dc, const float* sh_rest,
+                 const float* colors_precomp, const float* opacities, const float* scales,
+                 float scale_mod, const float* rotations, const float* cov3D_precomp, int tile_y0,
+                 int tile_y1, float* out_color, int* radii, gsro_state** state_out) {
+    if (P < 0 || D < 0 || D > 3 || (!colors_precomp && (D + 1) * (D + 1) - 1 > M_rest)) return -1;
+    if (!colors_precomp && !sh_dc) return -1;
+    if (!cov3D_precomp && (!scales || !rotations)) return -1;
+    gsro_state* st = (gsro_state*)calloc(1, sizeof(gsro_state));
+    st->cam = *cam;
+    st->P = P;
+    st->D = D;
+    st->M_rest = M_rest;
+    memcpy(st->bg, bg, sizeof(st->bg));
+    st->grid_x = (cam->width + TILE - 1) / TILE;
+    st->grid_y = (cam->height + TILE - 1) / TILE;
+    st->tile_y0 = imax(0, tile_y0);
+    st->tile_y1 = imin(st->grid_y, tile_y1);
+    st->means3D = means3D;
+    st->sh_dc = sh_dc;
+    st->sh_rest = sh_rest;
+    st->colors_precomp = colors_precomp;
+    st->opacities = opacities;
+    st->scales = scales;
+    st->rotations = rotations;
+    st->cov3D_precomp = cov3D_precomp;
+    st->scale_mod = scale_mod;
+    size_t Pn = P ? (size_t)P : 1;
+    st->radii = (int*)calloc(Pn, 4);
+    st->xy = (float*)calloc(Pn * 2, 4);
+    st->depth = (float*)calloc(Pn, 4);
+    st->conic_o = (float*)calloc(Pn * 4, 4);
+    st->rgb = (float*)calloc(Pn * 3, 4);
+    st->clamped = (uint8_t*)calloc(Pn * 3, 1);
+    st->tiles_touched = (uint32_t*)calloc(Pn, 4);
+    st->rect = (int*)calloc(Pn * 4, 4);
+    st->inst_start = (uint32_t*)calloc(Pn, 4);
+#pragma omp parallel for schedule(static)
+    for (int g = 0; g < P; ++g) preprocess_one(st, g);
+    int rc = bin_instances(st);
+    if (rc) {
+        gsro_free(st);
+        return rc;
+    }
+    size_t npix = (size_t)cam->width * cam->height;
+    st->final_T = (float*)malloc(4 * npix);
+    st->n_contrib = (uint32_t*)malloc(4 * npix);
+    /* pixels outside the band: background, T = 1 */
+    for (size_t i = 0; i < npix; ++i) {
+        st->final_T[i] = 1.0f;
+        st->n_contrib[i] = 0;
+        for (int ch = 0; ch < 3; ++ch) out_color[ch * npix + i] = st->bg[ch];
+    }
+    uint64_t pairs = 0;
+    int t0 = st->tile_y0 * st->grid_x, t1 = st->tile_y1 * st->grid_x;
+#pragma omp parallel for schedule(dynamic, 4) reduction(+ : pairs)
+    for (int t = t0; t < t1; ++t) pairs += blend_tile(st, t, out_color);
+    st->pairs = pairs;
+    memcpy(radii, st->radii, sizeof(int) * (size_t)P);
+    *state_out = st;
+    return st->K;
+}
+
+/* ------------------------------------------------------------------ */
+/* B.4 blend backward: per-instance partial (9 floats) summed over the   */
+/* tile's pixels in row-major pixel order; partial indexed by emission j */
+/* ------------------------------------------------------------------ */
+#define NPART 9 /* mean2D.x, mean2D.y, conic A, B, C, opacity, r, g, b */
+
+static void blend_tile_backward(gsro_state* st, int tile, const float* dL_dpix, float* partial) {
+    int W = st->cam.width, H = st->cam.height;
+    int tx = tile % st->grid_x, ty = tile / st->grid_x;
+    uint32_t beg = st->ranges[2 * tile], end = st->ranges[2 * tile + 1];
+    const float ddelx_dx = 0.5f * (float)W, ddely_dy = 0.5f * (float)H;
+    size_t npix = (size_t)W * H;
+    for (int ly = 0; ly < TILE; ++ly)
+        for (int lx = 0; lx < TILE; ++lx) {
+            int pxi = tx * TILE + lx, pyi = ty * TILE + ly;
+            if (pxi >= W || pyi >= H) continue;
+            size_t pix = (size_t)pyi * W + pxi;
+            float pfx = (float)pxi, pfy = (float)pyi;
+            const float T_final = st->final_T[pix];
+            float T = T_final;
+            uint32_t last = st->n_contrib[pix];
+            float dpix[3] = {dL_dpix[pix], dL_dpix[npix + pix], dL_dpix[2 * npix + pix]};
+            float accum[3] = {0, 0, 0}, last_color[3] = {0, 0, 0}, last_alpha = 0.0f;
+            float bg_dot = st->bg[0] * dpix[0] + st->bg[1] * dpix[1] + st->bg[2] * dpix[2];
+            for (int64_t i = (int64_t)beg + last - 1; i >= (int64_t)beg; --i) {
+                uint32_t g = st->s_gid[i];
+                const float* co = st->conic_o + 4 * g;
+                float dx = st->xy[2 * g] - pfx, dy = st->xy[2 * g + 1] - pfy;
+                float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                if (power > 0.0f) continue;
+                float G = expf(power);
+                float alpha = fminf(0.99f, co[3] * G);
+                if (alpha < 1.0f / 255.0f) continue;
+                T = T / (1.0f - alpha);
+                float dchannel_dcolor = alpha * T;
+                const float* c = st->rgb + 3 * g;
+                float* pp = partial + (size_t)NPART * st->s_j[i];
+                float dL_dalpha = 0.0f;
+                for (int ch = 0; ch < 3; ++ch) {
+                    accum[ch] = last_alpha * last_color[ch] + (1.0f - last_alpha) * accum[ch];
+                    last_color[ch] = c[ch];
+                    dL_dalpha += (c[ch] - accum[ch]) * dpix[ch];
+                    pp[6 + ch] += dchannel_dcolor * dpix[ch];
+                }
+                dL_dalpha *= T;
+                last_alpha = alpha;
+                dL_dalpha += (-T_final / (1.0f - alpha)) * bg_dot;
+                float dL_dG = co[3] * dL_dalpha;
+                float gdx = G * dx, gdy = G * dy;
+                float dG_ddelx = -gdx * co[0] - gdy * co[1];
+                float dG_ddely = -gdy * co[2] - gdx * co[1];
+                pp[0] += dL_dG * dG_ddelx * ddelx_dx;
+                pp[1] += dL_dG * dG_ddely * ddely_dy;
+                pp[2] += -0.5f * gdx * dx * dL_dG;
+                pp[3] += -gdx * dy * dL_dG; /* full d/dB of -B dx dy */
+                pp[4] += -0.5f * gdy * dy * dL_dG;
+                pp[5] += G * dL_dalpha;
+            }
+        }
+}
+
+/* ------------------------------------------------------------------ */
+/* B.5 preprocess backward                                               */
+/* ------------------------------------------------------------------ */
+static void preprocess_backward_one(gsro_state* st, int g, const float* g2d, float* dL_dmeans3D,
+                                    float* dL_dsh_dc, float* dL_dsh_rest, float* dL_dscales,
+                                    float* dL_drot, float* dL_dcov3D, float* dL_dcolors) {
+    const gsro_camera* cam = &st->cam;
+    const float* V = cam->viewmatrix;
+    const float* Pm = cam->projmatrix;
+    const float* p = st->means3D + 3 * g;
+    double dm[3] = {0, 0, 0};
+    float dmf[3];
+    /* --- mean2D (NDC) -> mean3D through the projection --- */
+    {
+        float hx = Pm[0] * p[0] + Pm[4] * p[1] + Pm[8] * p[2] + Pm[12];
+        float hy = Pm[1] * p[0] + Pm[5] * p[1] + Pm[9] * p[2] + Pm[13];
+        float hw = Pm[3] * p[0] + Pm[7] * p[1] + Pm[11] * p[2] + Pm[15];
+        float mw = 1.0f / (hw + 0.0000001f);
+        float mw2 = mw * mw;
+        for (int k = 0; k < 3; ++k) {
+            float d = (Pm[4 * k + 0] * mw - Pm[4 * k + 3] * hx * mw2) * g2d[0] +
+                      (Pm[4 * k + 1] * mw - Pm[4 * k + 3] * hy * mw2) * g2d[1];
+            dmf[k] = d;
+        }
+    }
+    /* --- colour -> SH (and view direction) --- */
+    float drgb[3] = {g2d[6], g2d[7], g2d[8]};
+    float dmean_dir[3] = {0, 0, 0};
+    if (st->colors_precomp) {
+        if (dL_dcolors)
+            for (int ch = 0; ch < 3; ++ch) dL_dcolors[3 * g + ch] = drgb[ch];
+    } else {
+        int D = st->D;
+        float dres[3];
+        for (int ch = 0; ch < 3; ++ch) dres[ch] = st->clamped[3 * g + ch] ? 0.0f : drgb[ch];
+        float dir[3], len;
+        view_dir(cam, p, dir, &len);
+        float x = dir[0], y = dir[1], z = dir[2];
+        float basis[16];
+        sh_basis(D, x, y, z, basis);
+        int nb = (D + 1) * (D + 1);
+        const float* sh0 = st->sh_dc + 3 * g;
+        const float* rest = st->sh_rest + (size_t)g * st->M_rest * 3;
+        for (int ch = 0; ch < 3; ++ch) dL_dsh_dc[3 * g + ch] = basis[0] * dres[ch];
+        if (dL_dsh_rest) {
+            float* drest = dL_dsh_rest + (size_t)g * st->M_rest * 3;
+            for (int k = 1; k < nb; ++k)
+                for (int ch = 0; ch < 3; ++ch) drest[3 * (k - 1) + ch] = basis[k] * dres[ch];
+        }
+        /* d basis / d (x,y,z) */
+        float db[16][3];
+        memset(db, 0, sizeof(db));
+        if (D >= 1) {
+            db[1][1] = -SH_C1;
+            db[2][2] = SH_C1;
+            db[3][0] = -SH_C1;
+        }
+        if (D >= 2) {
+            float xx = x * x, yy = y * y, zz = z * z;
+            db[4][0] = SH_C2[0] * y; db[4][1] = SH_C2[0] * x;
+            db[5][1] = SH_C2[1] * z; db[5][2] = SH_C2[1] * y;
+            db[6][0] = SH_C2[2] * -2.f * x; db[6][1] = SH_C2[2] * -2.f * y; db[6][2] = SH_C2[2] * 4.f * z;
+            db[7][0] = SH_C2[3] * z; db[7][2] = SH_C2[3] * x;
+            db[8][0] = SH_C2[4] * 2.f * x; db[8][1] = SH_C2[4] * -2.f * y;
+            if (D >= 3) {
+                db[9][0] = SH_C3[0] * 6.f * x * y;
+                db[9][1] = SH_C3[0] * 3.f * (xx - yy);
+                db[10][0] = SH_C3[1] * y * z; db[10][1] = SH_C3[1] * x * z; db[10][2] = SH_C3[1] * x * y;
+                db[11][0] = SH_C3[2] * -2.f * x * y;
+                db[11][1] = SH_C3[2] * (4.f * zz - xx - 3.f * yy);
+                db[11][2] = SH_C3[2] * 8.f * y * z;
+                db[12][0] = SH_C3[3] * -6.f * x * z;
+                db[12][1] = SH_C3[3] * -6.f * y * z;
+                db[12][2] = SH_C3[3] * (6.f * zz - 3.f * xx - 3.f * yy);
+                db[13][0] = SH_C3[4] * (4.f * zz - 3.f * xx - yy);
+                db[13][1] = SH_C3[4] * -2.f * x * y;
+                db[13][2] = SH_C3[4] * 8.f * x * z;
+                db[14][0] = SH_C3[5] * 2.f * x * z;
+                db[14][1] = SH_C3[5] * -2.f * y * z;
+                db[14][2] = SH_C3[5] * (xx - yy);
+                db[15][0] = SH_C3[6] * 3.f * (xx - yy);
+                db[15][1] = SH_C3[6] * -6.f * x * y;
+            }
+        }
+        float ddir[3] = {0, 0, 0};
+        for (int k = 1; k < nb; ++k) {
+            float s = rest[3 * (k - 1) + 0] * dres[0] + rest[3 * (k - 1) + 1] * dres[1] +
+                      rest[3 * (k - 1) + 2] * dres[2];
+            for (int a = 0; a < 3; ++a) ddir[a] += db[k][a] * s;
+        }
+        (void)sh0;
+        /* dir = v / |v|: dv = (ddir - dir (dir . ddir)) / |v| */
+        float dd = dir[0] * ddir[0] + dir[1] * ddir[1] + dir[2] * ddir[2];
+        for (int a = 0; a < 3; ++a) dmean_dir[a] = (ddir[a] - dir[a] * dd) / len;
+    }
+    /* --- conic -> cov2D -> (cov3D, view-space mean) --- */
+    float c3[6], R[9], s_eff[3] = {0, 0, 0};
+    const float* q = NULL;
+    if (st->cov3D_precomp) {
+        memcpy(c3, st->cov3D_precomp + 6 * g, sizeof(c3));
+    } else {
+        q = st->rotations + 4 * g;
+        rot_from_quat(q, R);
+        cov3d_from_R(R, st->scales + 3 * g, st->scale_mod, c3);
+        for (int k = 0; k < 3; ++k) s_eff[k] = st->scale_mod * st->scales[3 * g + k];
+    }
+    float tx = V[0] * p[0] + V[4] * p[1] + V[8] * p[2] + V[12];
+    float ty = V[1] * p[0] + V[5] * p[1] + V[9] * p[2] + V[13];
+    float tz = V[2] * p[0] + V[6] * p[1] + V[10] * p[2] + V[14];
+    float Wf = (float)cam->width, Hf = (float)cam->height;
+    float fx = Wf / (2.0f * cam->tanfovx), fy = Hf / (2.0f * cam->tanfovy);
+    float limx = 1.3f * cam->tanfovx, limy = 1.3f * cam->tanfovy;
+    float txtz = tx / tz, tytz = ty / tz;
+    float cx = fminf(limx, fmaxf(-limx, txtz)) * tz;
+    float cy = fminf(limy, fmaxf(-limy, tytz)) * tz;
+    float xmul = (txtz < -limx || txtz > limx) ? 0.0f : 1.0f;
+    float ymul = (tytz < -limy || tytz > limy) ? 0.0f : 1.0f;
+    float tz2 = tz * tz, tz3 = tz2 * tz;
+    float J00 = fx / tz, J02 = -(fx * cx) / tz2, J11 = fy / tz, J12 = -(fy * cy) / tz2;
+    float T0[3], T1[3];
+    for (int k = 0; k < 3; ++k) {
+        T0[k] = J00 * V[4 * k + 0] + J02 * V[4 * k + 2];
+        T1[k] = J11 * V[4 * k + 1] + J12 * V[4 * k + 2];
+    }
+    float S[9] = {c3[0], c3[1], c3[2], c3[1], c3[3], c3[4], c3[2], c3[4], c3[5]};
+    float ST0[3], ST1[3];
+    for (int i = 0; i < 3; ++i) {
+        ST0[i] = S[3 * i + 0] * T0[0] + S[3 * i + 1] * T0[1] + S[3 * i + 2] * T0[2];
+        ST1[i] = S[3 * i + 0] * T1[0] + S[3 * i + 1] * T1[1] + S[3 * i + 2] * T1[2];
+    }
+    float a = (ST0[0] * T0[0] + ST0[1] * T0[1] + ST0[2] * T0[2]) + 0.3f;
+    float b = ST0[0] * T1[0] + ST0[1] * T1[1] + ST0[2] * T1[2];
+    float c = (ST1[0] * T1[0] + ST1[1] * T1[1] + ST1[2] * T1[2]) + 0.3f;
+    float det = a * c - b * b;
+    float dA = g2d[2], dB = g2d[3], dC = g2d[4];
+    float inv2 = 1.0f / (det * det);
+    float dL_da = inv2 * (-c * c * dA + b * c * dB - b * b * dC);
+    float dL_db = inv2 * (2.f * b * c * dA - (a * c + b * b) * dB + 2.f * a * b * dC);
+    float dL_dc = inv2 * (-b * b * dA + a * b * dB - a * a * dC);
+    /* dL/dSigma (unique-entry convention, off-diagonals doubled) */
+    float dS[6];
+    dS[0] = T0[0] * T0[0] * dL_da + T0[0] * T1[0] * dL_db + T1[0] * T1[0] * dL_dc;
+    dS[3] = T0[1] * T0[1] * dL_da + T0[1] * T1[1] * dL_db + T1[1] * T1[1] * dL_dc;
+    dS[5] = T0[2] * T0[2] * dL_da + T0[2] * T1[2] * dL_db + T1[2] * T1[2] * dL_dc;
+    dS[1] = 2.f * T0[0] * T0[1] * dL_da + (T0[0] * T1[1] + T0[1] * T1[0]) * dL_db + 2.f * T1[0] * T1[1] * dL_dc;
+    dS[2] = 2.f * T0[0] * T0[2] * dL_da + (T0[0] * T1[2] + T0[2] * T1[0]) * dL_db + 2.f * T1[0] * T1[2] * dL_dc;
+    dS[4] = 2.f * T0[1] * T0[2] * dL_da + (T0[1] * T1[2] + T0[2] * T1[1]) * dL_db + 2.f * T1[1] * T1[2] * dL_dc;
+    /* dL/dT */
+    float dT0[3], dT1[3];
+    for (int i = 0; i < 3; ++i) {
+        dT0[i] = 2.f * ST0[i] * dL_da + ST1[i] * dL_db;
+        dT1[i] = 2.f * ST1[i] * dL_dc + ST0[i] * dL_db;
+    }
+    /* dL/dJ */
+    float dJ00 = 0, dJ02 = 0, dJ11 = 0, dJ12 = 0;
+    for (int i = 0; i < 3; ++i) {
+        dJ00 += dT0[i] * V[4 * i + 0];
+        dJ02 += dT0[i] * V[4 * i + 2];
+        dJ11 += dT1[i] * V[4 * i + 1];
+        dJ12 += dT1[i] * V[4 * i + 2];
+    }
+    float dtx = xmul * (-fx / tz2) * dJ02;
+    float dty = ymul * (-fy / tz2) * dJ12;
+    float dtz = (-fx / tz2) * dJ00 + (-fy / tz2) * dJ11 + (2.f * fx * cx / tz3) * dJ02 +
+                (2.f * fy * cy / tz3) * dJ12;
+    (void)J00; (void)J02; (void)J11; (void)J12;
+    /* view-space mean -> world mean: dL/dp_k = sum_r V[4k+r] dt_r */
+    for (int k = 0; k < 3; ++k) {
+        float d = V[4 * k + 0] * dtx + V[4 * k + 1] * dty + V[4 * k + 2] * dtz;
+        dm[k] = (double)dmf[k] + (double)d + (double)dmean_dir[k];
+    }
+    for (int k = 0; k < 3; ++k) dL_dmeans3D[3 * g + k] = (float)dm[k];
+    /* --- cov3D -> scale, rotation --- */
+    if (st->cov3D_precomp) {
+        if (dL_dcov3D) memcpy(dL_dcov3D + 6 * g, dS, sizeof(dS));
+    } else {
+        /* full symmetric gradient G (off-diagonals halved); dL/dL = 2 G L */
+        float Gm[9] = {dS[0], 0.5f * dS[1], 0.5f * dS[2], 0.5f * dS[1], dS[3], 0.5f * dS[4],
+                       0.5f * dS[2], 0.5f * dS[4], dS[5]};
+        float L[9], dLm[9];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) L[3 * i + j] = R[3 * i + j] * s_eff[j];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                dLm[3 * i + j] = 2.f * (Gm[3 * i + 0] * L[0 + j] + Gm[3 * i + 1] * L[3 + j] + Gm[3 * i + 2] * L[6 + j]);
+        float dR[9];
+        for (int j = 0; j < 3; ++j) {
+            float acc = 0;
+            for (int i = 0; i < 3; ++i) {
+                acc += dLm[3 * i + j] * R[3 * i + j];
+                dR[3 * i + j] = dLm[3 * i + j] * s_eff[j];
+            }
+            dL_dscales[3 * g + j] = st->scale_mod * acc;
+        }
+        float r = q[0], x = q[1], y = q[2], z = q[3];
+        float dq[4];
+        dq[0] = 2.f * (-z * dR[1] + y * dR[2] + z * dR[3] - x * dR[5] - y * dR[6] + x * dR[7]);
+        dq[1] = 2.f * (y * dR[1] + z * dR[2] + y * dR[3] - 2.f * x * dR[4] - r * dR[5] + z * dR[6] + r * dR[7] - 2.f * x * dR[8]);
+        dq[2] = 2.f * (-2.f * y * dR[0] + x * dR[1] + r * dR[2] + x * dR[3] + z * dR[5] - r * dR[6] + z * dR[7] - 2.f * y * dR[8]);
+        dq[3] = 2.f * (-2.f * z * dR[0] - r * dR[1] + x * dR[2] + r * dR[3] - 2.f * z * dR[4] + y * dR[5] + x * dR[6] + y * dR[7]);
+        for (int k = 0; k < 4; ++k) dL_drot[4 * g + k] = dq[k];
+    }
+}
+
+int gsro_backward(gsro_state* st, const float* dL_dpix, float* dL_dmeans2D, float* dL_dconic,
+                  float* dL_dopacity, float* dL_dcolors, float* dL_dmeans3D, float* dL_dsh_dc,
+                  float* dL_dsh_rest, float* dL_dscales, float* dL_drotations, float* dL_dcov3D) {
+    int P = st->P, K = st->K;
+    float* partial = (float*)calloc((size_t)NPART * (K ? K : 1), 4);
+    if (!partial) return -2;
+    int t0 = st->tile_y0 * st->grid_x, t1 = st->tile_y1 * st->grid_x;
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int t = t0; t < t1; ++t) blend_tile_backward(st, t, dL_dpix, partial);
+    float* g2d_all = (float*)calloc((size_t)NPART * (P ? P : 1), 4);
+#pragma omp parallel for schedule(static)
+    for (int g = 0; g < P; ++g) {
+        float* g2d = g2d_all + (size_t)NPART * g;
+        /* fixed order: emission order (rect row-major) */
+        for (uint32_t j = st->inst_start[g]; j < st->inst_start[g] + st->tiles_touched[g]; ++j)
+            for (int k = 0; k < NPART; ++k) g2d[k] += partial[(size_t)NPART * j + k];
+    }
+    free(partial);
+    int Mr = st->M_rest;
+#pragma omp parallel for schedule(static)
+    for (int g = 0; g < P; ++g) {
+        float* g2d = g2d_all + (size_t)NPART * g;
+        if (dL_dmeans2D) {
+            dL_dmeans2D[3 * g + 0] = g2d[0];
+            dL_dmeans2D[3 * g + 1] = g2d[1];
+            dL_dmeans2D[3 * g + 2] = 0.0f;
+        }
+        if (dL_dconic) {
+            dL_dconic[3 * g + 0] = g2d[2];
+            dL_dconic[3 * g + 1] = g2d[3];
+            dL_dconic[3 * g + 2] = g2d[4];
+        }
+        if (dL_dopacity) dL_dopacity[g] = g2d[5];
+        /* defaults: zero everything this Gaussian owns */
+        for (int k = 0; k < 3; ++k) dL_dmeans3D[3 * g + k] = 0.0f;
+        if (!st->colors_precomp) {
+            for (int k = 0; k < 3; ++k) dL_dsh_dc[3 * g + k] = 0.0f;
+            if (dL_dsh_rest)
+                for (int k = 0; k < 3 * Mr; ++k) dL_dsh_rest[(size_t)g * Mr * 3 + k] = 0.0f;
+        } else if (dL_dcolors) {
+            for (int k = 0; k < 3; ++k) dL_dcolors[3 * g + k] = 0.0f;
+        }
+        if (!st->cov3D_precomp) {
+            for (int k = 0; k < 3; ++k) dL_dscales[3 * g + k] = 0.0f;
+            for (int k = 0; k < 4; ++k) dL_drotations[4 * g + k] = 0.0f;
+        } else if (dL_dcov3D) {
+            for (int k = 0; k < 6; ++k) dL_dcov3D[6 * g + k] = 0.0f;
+        }
+        if (st->radii[g] <= 0) continue;
+        preprocess_backward_one(st, g, g2d, dL_dmeans3D, dL_dsh_dc, dL_dsh_rest, dL_dscales,
+                                dL_drotations, dL_dcov3D, dL_dcolors);
+    }
+    free(g2d_all);
+    return 0;
+}
+
+void gsro_free(gsro_state* st) {
+    if (!st) return;
+    free(st->radii); free(st->xy); free(st->depth); free(st->conic_o); free(st->rgb);
+    free(st->clamped); free(st->tiles_touched); free(st->rect); free(st->inst_start);
+    free(st->s_tile); free(st->s_depth); free(st->s_gid); free(st->s_j); free(st->ranges);
+    free(st->final_T); free(st->n_contrib);
+    free(st);
+}
+
+int gsro_num_rendered(const gsro_state* st) { return st->K; }
+
+void gsro_get_sorted(const gsro_state* st, uint32_t* tile, uint32_t* depth_bits, uint32_t* gid) {
+    size_t n = (size_t)st->K * 4;
+    if (tile) memcpy(tile, st->s_tile, n);
+    if (depth_bits) memcpy(depth_bits, st->s_depth, n);
+    if (gid) memcpy(gid, st->s_gid, n);
+}
+
+void gsro_get_ranges(const gsro_state* st, uint32_t* ranges) {
+    memcpy(ranges, st->ranges, (size_t)st->grid_x * st->grid_y * 2 * 4);
+}
+
+void gsro_get_pixel_state(const gsro_state* st, float* final_T, uint32_t* n_contrib) {
+    size_t n = (size_t)st->cam.width * st->cam.height * 4;
+    if (final_T) memcpy(final_T, st->final_T, n);
+    if (n_contrib) memcpy(n_contrib, st->n_contrib, n);
+}
+
+void gsro_get_preprocess(const gsro_state* st, float* xy, float* depth, float* conic_o, float* rgb,
+                         uint32_t* tiles_touched) {
+    size_t P = (size_t)st->P;
+    if (xy) memcpy(xy, st->xy, P * 8);
+    if (depth) memcpy(depth, st->depth, P * 4);
+    if (conic_o) memcpy(conic_o, st->conic_o, P * 16);
+    if (rgb) memcpy(rgb, st->rgb, P * 12);
+    if (tiles_touched) memcpy(tiles_touched, st->tiles_touched, P * 4);
+}
+
+uint64_t gsro_forward_pairs(const gsro_state* st) { return st->pairs; }
