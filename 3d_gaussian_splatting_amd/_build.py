@@ -1,0 +1,137 @@
+"""In-tree build of the native libraries (gfx950 only).
+
+  lib/libgsr_hip.so      hipcc --offload-arch=gfx950: the CDNA4 kernels + the C ABI
+  lib/_gsr_torch*.so     libtorch render() + autograd Function (C++), links libgsr_hip.so
+
+Per-file flags: gsr_preprocess.hip is compiled with -ffp-contract=off so its key-feeding
+arithmetic is bit-identical to the CPU oracle; the blend / backward files keep hipcc's
+default FMA contraction (their outputs are compared within tolerance, not bitwise).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "lib")
+ROOT = os.path.dirname(PKG)
+ARCH = "gfx950"
+
+HIP_SOURCES = {
+    "gsr_preprocess.hip": ["-ffp-contract=off"],
+    "gsr_sort.hip": [],
+    "gsr_blend.hip": [],
+    "gsr_preprocess_bwd.hip": [],
+    "gsr_api.cpp": [],
+}
+COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fno-fast-math",
+          "-Wall", "-Wno-unused-function", "-I" + os.path.join(ROOT, "include")]
+
+
+def _hipcc() -> str:
+    p = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(p):
+        raise RuntimeError("hipcc not found")
+    return p
+
+
+def _stamp(paths, extra=""):
+    h = hashlib.sha256(extra.encode())
+    for p in sorted(paths):
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def _headers():
+    out = [os.path.join(ROOT, "include", "gsr", "gsr.h")]
+    out += [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    return out
+
+
+def build_hip(verbose: bool = False, force: bool = False) -> str:
+    os.makedirs(LIB, exist_ok=True)
+    so = os.path.join(LIB, "libgsr_hip.so")
+    srcs = [os.path.join(CSRC, f) for f in HIP_SOURCES]
+    stamp = _stamp(srcs + _headers(), " ".join(COMMON))
+    stamp_file = so + ".stamp"
+    if not force and os.path.exists(so) and os.path.exists(stamp_file) and open(stamp_file).read() == stamp:
+        return so
+    hipcc = _hipcc()
+    objs = []
+
+    def compile_one(name):
+        src = os.path.join(CSRC, name)
+        obj = os.path.join(LIB, name + ".o")
+        lang = ["-x", "hip"] if name.endswith(".cpp") else []
+        cmd = [hipcc] + COMMON + HIP_SOURCES[name] + lang + ["-c", src, "-o", obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {name}:\n{r.stdout}\n{r.stderr}")
+        if verbose and r.stderr.strip():
+            print(r.stderr)
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(HIP_SOURCES))) as ex:
+        objs = list(ex.map(compile_one, HIP_SOURCES))
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", so] + objs
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    for o in objs:
+        os.remove(o)
+    with open(stamp_file, "w") as fh:
+        fh.write(stamp)
+    return so
+
+
+def torch_ext_name() -> str:
+    return "_gsr_torch" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so")
+
+
+def build_torch_ext(verbose: bool = False, force: bool = False) -> str:
+    """Compile csrc/torch/gsr_torch.cpp against libtorch (host C++, no device code) and link
+    it to libgsr_hip.so with an $ORIGIN rpath, into lib/."""
+    import torch
+    from torch.utils import cpp_extension
+
+    os.makedirs(LIB, exist_ok=True)
+    out = os.path.join(LIB, torch_ext_name())
+    src = os.path.join(CSRC, "torch", "gsr_torch.cpp")
+    tinc = cpp_extension.include_paths()
+    flags = ["-O2", "-std=c++17", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__=1",
+             "-DTORCH_EXTENSION_NAME=_gsr_torch", "-DTORCH_API_INCLUDE_EXTENSION_H",
+             f"-D_GLIBCXX_USE_CXX11_ABI={int(torch._C._GLIBCXX_USE_CXX11_ABI)}",
+             "-I" + os.path.join(ROOT, "include"), "-I/opt/rocm/include",
+             "-I" + sysconfig.get_paths()["include"]] + ["-I" + p for p in tinc]
+    tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    libs = ["-L" + LIB, "-lgsr_hip", "-Wl,-rpath,$ORIGIN", "-L" + tlib, "-lc10", "-ltorch",
+            "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-Wl,-rpath," + tlib]
+    stamp = _stamp([src] + _headers(), " ".join(flags))
+    stamp_file = out + ".stamp"
+    if not force and os.path.exists(out) and os.path.exists(stamp_file) and open(stamp_file).read() == stamp:
+        return out
+    cxx = shutil.which("g++") or "c++"
+    cmd = [cxx] + flags + [src, "-o", out] + libs
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"torch extension build failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    with open(stamp_file, "w") as fh:
+        fh.write(stamp)
+    return out
+
+
+def build_all(verbose: bool = False, force: bool = False):
+    so = build_hip(verbose, force)
+    ext = build_torch_ext(verbose, force)
+    return so, ext
+
+
+if __name__ == "__main__":
+    print(build_all(verbose=True, force="--force" in sys.argv))

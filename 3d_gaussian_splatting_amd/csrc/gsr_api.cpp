@@ -1,0 +1,477 @@
+// gsr_api.cpp -- the C ABI (include/gsr/gsr.h) over the CDNA4 kernels.
+//
+// Stage order (forward): F1 preprocess -> depth sort (P keys) -> scan of tiles_touched in
+// depth-rank order -> ONE device->host read of K -> F3 duplicate -> tile-key sort (K keys)
+// -> F5 finalize (sorted gid + tile ranges) -> F6 blend.  Backward: B1 blend backward ->
+// B2 preprocess backward (or B1 -> per-Gaussian grad2d for the multi-GPU all-reduce).
+// No persistent allocations; every scratch buffer comes from the caller's callbacks.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "gsr_kernels.h"
+
+using namespace gsr;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define GSR_CHECK_HIP(expr, stage)                                                             \
+    do {                                                                                       \
+        int _e = (int)(expr);                                                                  \
+        if (_e != 0) return fail(-10, "%s: %s", stage, hipGetErrorString((hipError_t)_e));    \
+        if (debug) {                                                                           \
+            hipError_t _s = hipStreamSynchronize(stream);                                      \
+            if (_s != hipSuccess) return fail(-11, "%s (sync): %s", stage, hipGetErrorString(_s)); \
+        }                                                                                      \
+    } while (0)
+
+// ---- optional stage profiler ----
+struct Profiler {
+    std::mutex mu;
+    uint32_t mask = 0;
+    std::vector<hipEvent_t> pool;
+    struct Rec {
+        int stage;
+        hipEvent_t a, b;
+    };
+    std::vector<Rec> pending;
+    double ms[GSR_NUM_STAGES] = {};
+    uint32_t counts[GSR_NUM_STAGES] = {};
+    hipEvent_t get() {
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e = nullptr;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        return e;
+    }
+};
+Profiler& prof() {
+    static Profiler p;
+    return p;
+}
+
+// RAII bracket of one stage on `stream` (no-op unless the stage is enabled)
+struct StageTimer {
+    int stage;
+    hipStream_t stream;
+    hipEvent_t a = nullptr, b = nullptr;
+    StageTimer(int s, hipStream_t st) : stage(s), stream(st) {
+        Profiler& p = prof();
+        if (!(__atomic_load_n(&p.mask, __ATOMIC_RELAXED) & (1u << s))) return;
+        std::lock_guard<std::mutex> lk(p.mu);
+        a = p.get();
+        b = p.get();
+        if (a && b) hipEventRecord(a, stream);
+    }
+    ~StageTimer() {
+        if (!a || !b) return;
+        hipEventRecord(b, stream);
+        Profiler& p = prof();
+        std::lock_guard<std::mutex> lk(p.mu);
+        p.pending.push_back({stage, a, b});
+    }
+};
+
+#define GSR_STAGE(id, expr, name)          \
+    do {                                   \
+        StageTimer _timer((id), stream);   \
+        GSR_CHECK_HIP(expr, name);         \
+    } while (0)
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+int validate(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs) {
+    if (!cam || !gs || !rs) return fail(-1, "null camera/gaussians/settings");
+    if (cam->width <= 0 || cam->height <= 0) return fail(-1, "bad image size %dx%d", cam->width, cam->height);
+    if ((long long)div_up(cam->width, kTile) >= 65535 || (long long)div_up(cam->height, kTile) >= 65535)
+        return fail(-1, "image too large");
+    if (gs->P < 0) return fail(-1, "negative P");
+    if (gs->P == 0) return 0;
+    if (!gs->means3D || !gs->opacities) return fail(-1, "means3D/opacities required");
+    if (gs->sh_degree < 0 || gs->sh_degree > 3) return fail(-1, "sh_degree must be 0..3");
+    if (!gs->colors_precomp) {
+        if (!gs->sh_dc) return fail(-1, "sh_dc required without colors_precomp");
+        const int need = (gs->sh_degree + 1) * (gs->sh_degree + 1) - 1;
+        if (need > 0 && (!gs->sh_rest || gs->sh_rest_coeffs < need))
+            return fail(-1, "sh_rest must hold >= %d coefficients for degree %d", need, gs->sh_degree);
+        if (gs->sh_rest_coeffs > 15) return fail(-1, "sh_rest_coeffs > 15");
+    }
+    if (!gs->cov3D_precomp) {
+        if (!gs->scales || !gs->rotations) return fail(-1, "scales/rotations required without cov3D_precomp");
+        if (!aligned16(gs->rotations)) return fail(-1, "rotations must be 16-byte aligned");
+    }
+    return 0;
+}
+
+gsr::GaussIn gauss_in(const gsr_gaussians* gs) {
+    GaussIn in;
+    in.P = gs->P;
+    in.D = gs->sh_degree;
+    in.M_rest = gs->sh_rest ? gs->sh_rest_coeffs : 0;
+    in.smod = gs->scale_modifier;
+    in.means3D = gs->means3D;
+    in.sh_dc = gs->sh_dc;
+    in.sh_rest = gs->sh_rest;
+    in.colors = gs->colors_precomp;
+    in.opac = gs->opacities;
+    in.scales = gs->scales;
+    in.rots = gs->rotations;
+    in.cov3D = gs->cov3D_precomp;
+    return in;
+}
+
+void band(const gsr_camera* cam, const gsr_raster_settings* rs, int* y0, int* y1) {
+    const int gy = div_up(cam->height, kTile);
+    *y0 = rs->tile_y0 < 0 ? 0 : (rs->tile_y0 > gy ? gy : rs->tile_y0);
+    *y1 = rs->tile_y1 > gy ? gy : rs->tile_y1;
+    if (*y1 < *y0) *y1 = *y0;
+}
+
+struct Views {
+    uint32_t *depth_key, *tiles, *flags, *inst_start, *offsets, *gid_by_rank;
+    float4* rec;
+    uint2* ranges;
+    float* final_T;
+    uint32_t* n_contrib;
+    uint32_t *sorted_tile, *sorted_j, *sorted_gid, *inst_gid;
+};
+
+Views views(const gsr_camera* cam, int P, const gsr_buffers* b) {
+    Views v{};
+    GeomLayout gl(P);
+    ImgLayout il(cam->width, cam->height);
+    v.depth_key = at<uint32_t>(b->geom, gl.depth_key);
+    v.tiles = at<uint32_t>(b->geom, gl.tiles);
+    v.flags = at<uint32_t>(b->geom, gl.flags);
+    v.rec = at<float4>(b->geom, gl.rec);
+    v.inst_start = at<uint32_t>(b->geom, gl.inst_start);
+    v.offsets = at<uint32_t>(b->geom, gl.offsets);
+    // 32-bit depth key = 4 passes (even) -> result in the A buffers
+    v.gid_by_rank = at<uint32_t>(b->geom, gl.sA_v);
+    v.ranges = at<uint2>(b->image, il.ranges);
+    v.final_T = at<float>(b->image, il.final_T);
+    v.n_contrib = at<uint32_t>(b->image, il.n_contrib);
+    if (b->binning) {
+        BinLayout bl(b->num_rendered);
+        const int tiles = div_up(cam->width, kTile) * div_up(cam->height, kTile);
+        const bool odd = (tile_passes(tiles) & 1) != 0;
+        v.sorted_tile = at<uint32_t>(b->binning, odd ? bl.kB : bl.kA);
+        v.sorted_j = at<uint32_t>(b->binning, odd ? bl.vB : bl.vA);
+        v.sorted_gid = at<uint32_t>(b->binning, bl.sorted_gid);
+        v.inst_gid = at<uint32_t>(b->binning, bl.inst_gid);
+    }
+    return v;
+}
+
+__global__ void fill_background(float* out_color, float* final_T, uint32_t* n_contrib, int npix,
+                                float bg0, float bg1, float bg2) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= npix) return;
+    out_color[i] = bg0;
+    out_color[npix + i] = bg1;
+    out_color[2 * (size_t)npix + i] = bg2;
+    final_T[i] = 1.0f;
+    n_contrib[i] = 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gsr_abi_version(void) { return GSR_ABI_VERSION; }
+const char* gsr_last_error(void) { return g_err.c_str(); }
+
+size_t gsr_geom_bytes(int32_t P) { return GeomLayout(P).total; }
+size_t gsr_binning_bytes(int32_t K) { return BinLayout(K).total; }
+size_t gsr_image_bytes(int32_t w, int32_t h) { return ImgLayout(w, h).total; }
+size_t gsr_scratch_bytes(int32_t K) { return (size_t)(K > 0 ? K : 1) * kPart * sizeof(float); }
+
+int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
+                float* out_color, int32_t* radii, gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_binning,
+                gsr_alloc_fn alloc_image, void* ctx, gsr_buffers* bufs, void* stream_) {
+    g_err.clear();
+    if (int e = validate(cam, gs, rs)) return e;
+    if (!out_color || (gs->P > 0 && !radii) || !bufs || !alloc_geom || !alloc_binning || !alloc_image)
+        return fail(-1, "null output / allocator");
+    hipStream_t stream = (hipStream_t)stream_;
+    const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
+    const int P = gs->P;
+    const int W = cam->width, H = cam->height;
+    const int gx = div_up(W, kTile), gy = div_up(H, kTile);
+    int ty0, ty1;
+    band(cam, rs, &ty0, &ty1);
+    std::memset(bufs, 0, sizeof *bufs);
+    bufs->geom = alloc_geom(ctx, GeomLayout(P).total);
+    bufs->image = alloc_image(ctx, ImgLayout(W, H).total);
+    if (!bufs->geom || !bufs->image) return fail(-2, "allocation failed (geometry/image)");
+    GeomLayout gl(P);
+    ImgLayout il(W, H);
+    uint32_t* depth_key = at<uint32_t>(bufs->geom, gl.depth_key);
+    uint32_t* tiles = at<uint32_t>(bufs->geom, gl.tiles);
+    uint32_t* flags = at<uint32_t>(bufs->geom, gl.flags);
+    float4* rec = at<float4>(bufs->geom, gl.rec);
+    uint32_t* offsets = at<uint32_t>(bufs->geom, gl.offsets);
+    uint32_t* inst_start = at<uint32_t>(bufs->geom, gl.inst_start);
+    uint2* ranges = at<uint2>(bufs->image, il.ranges);
+    float* final_T = at<float>(bufs->image, il.final_T);
+    uint32_t* n_contrib = at<uint32_t>(bufs->image, il.n_contrib);
+
+    if (ty0 > 0 || ty1 < gy) {
+        const int npix = W * H;
+        hipLaunchKernelGGL(fill_background, dim3(div_up(npix, 256)), dim3(256), 0, stream, out_color,
+                           final_T, n_contrib, npix, rs->bg[0], rs->bg[1], rs->bg[2]);
+        GSR_STAGE(GSR_STAGE_MISC, hipGetLastError(), "fill_background");
+    }
+    GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(ranges, 0, sizeof(uint2) * (size_t)gx * gy, stream), "memset ranges");
+
+    long long K = 0;
+    if (P > 0) {
+        PreOut po{radii, depth_key, tiles, flags, rec};
+        GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess(*cam, gauss_in(gs), ty0, ty1, po, stream), "preprocess");
+        int which = -1;
+        GSR_STAGE(GSR_STAGE_DEPTH_SORT, radix_sort(depth_key, nullptr, at<uint32_t>(bufs->geom, gl.sB_k),
+                                 at<uint32_t>(bufs->geom, gl.sB_v), at<uint32_t>(bufs->geom, gl.sA_k),
+                                 at<uint32_t>(bufs->geom, gl.sA_v), P, 32, at<uint32_t>(bufs->geom, gl.hist),
+                                 &which, stream),
+                      "depth sort");
+        if (which != 1) return fail(-12, "depth sort ended in an unexpected buffer");
+        const uint32_t* gid_by_rank = at<uint32_t>(bufs->geom, gl.sA_v);
+        GSR_STAGE(GSR_STAGE_SCAN, inclusive_scan_gather(tiles, gid_by_rank, offsets, P,
+                                            at<uint32_t>(bufs->geom, gl.partials), stream),
+                      "scan");
+        uint32_t k32 = 0;
+        GSR_STAGE(GSR_STAGE_MISC, hipMemcpyAsync(&k32, offsets + (P - 1), sizeof k32, hipMemcpyDeviceToHost, stream),
+                      "read num_rendered");
+        GSR_CHECK_HIP(hipStreamSynchronize(stream), "sync num_rendered");
+        K = k32;
+        if (K > INT32_MAX) return fail(-3, "num_rendered overflow (%lld)", K);
+        bufs->num_rendered = (int32_t)K;
+        bufs->binning = alloc_binning(ctx, BinLayout(K).total);
+        if (!bufs->binning) return fail(-2, "allocation failed (binning, K=%lld)", K);
+        BinLayout bl(K);
+        uint32_t* kA = at<uint32_t>(bufs->binning, bl.kA);
+        uint32_t* vA = at<uint32_t>(bufs->binning, bl.vA);
+        uint32_t* kB = at<uint32_t>(bufs->binning, bl.kB);
+        uint32_t* vB = at<uint32_t>(bufs->binning, bl.vB);
+        uint32_t* inst_gid = at<uint32_t>(bufs->binning, bl.inst_gid);
+        uint32_t* sorted_gid = at<uint32_t>(bufs->binning, bl.sorted_gid);
+        GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate(gid_by_rank, offsets, tiles, rec, P, gx, ty0, ty1, inst_start, kA,
+                                       inst_gid, stream),
+                      "duplicate");
+        if (K > 0) {
+            int w2 = -1;
+            GSR_STAGE(GSR_STAGE_TILE_SORT, radix_sort(kA, nullptr, kB, vB, kA, vA, K, tile_bits(gx * gy),
+                                     at<uint32_t>(bufs->binning, bl.hist), &w2, stream),
+                          "tile sort");
+            const bool odd = (tile_passes(gx * gy) & 1) != 0;
+            if ((w2 == 0) != odd) return fail(-12, "tile sort ended in an unexpected buffer");
+            GSR_STAGE(GSR_STAGE_FINALIZE, launch_finalize(odd ? kB : kA, odd ? vB : vA, inst_gid, K, sorted_gid, ranges, stream),
+                          "finalize");
+        }
+    } else {
+        bufs->binning = alloc_binning(ctx, BinLayout(0).total);
+    }
+    const Views v = views(cam, P, bufs);
+    GSR_STAGE(GSR_STAGE_BLEND_FWD, launch_blend_forward(*cam, rs->bg, ty0, ty1, ranges, v.sorted_gid, rec, out_color, final_T,
+                                       n_contrib, stream),
+                  "blend forward");
+    return 0;
+}
+
+static int backward_impl(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
+                         const gsr_buffers* bufs, const float* dL_dpix, gsr_alloc_fn alloc_scratch,
+                         void* ctx, const gsr_grads* grads, float* grad2d, void* stream_) {
+    if (int e = validate(cam, gs, rs)) return e;
+    if (!bufs || !bufs->geom || !bufs->image || !dL_dpix) return fail(-1, "missing forward buffers / dL_dpix");
+    hipStream_t stream = (hipStream_t)stream_;
+    const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
+    const int P = gs->P;
+    if (P == 0) return 0;
+    int ty0, ty1;
+    band(cam, rs, &ty0, &ty1);
+    const Views v = views(cam, P, bufs);
+    const long long K = bufs->num_rendered;
+    float* partial = nullptr;
+    if (K > 0) {
+        if (!alloc_scratch) return fail(-1, "null scratch allocator");
+        partial = static_cast<float*>(alloc_scratch(ctx, gsr_scratch_bytes((int32_t)K)));
+        if (!partial) return fail(-2, "allocation failed (scratch, K=%lld)", K);
+        GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.sorted_j, v.rec,
+                                            v.final_T, v.n_contrib, dL_dpix, partial, stream),
+                      "blend backward");
+    }
+    if (grad2d) {
+        if (K > 0) {
+            GSR_STAGE(GSR_STAGE_GATHER, launch_gather_grad2d(v.inst_start, v.tiles, partial, P, grad2d, stream), "gather grad2d");
+        } else {
+            GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(grad2d, 0, sizeof(float) * kPart * (size_t)P, stream), "zero grad2d");
+        }
+        return 0;
+    }
+    return 0;
+}
+
+static int check_grads(const gsr_gaussians* gs, const gsr_grads* g) {
+    if (!g || !g->dL_dmeans2D || !g->dL_dopacity || !g->dL_dmeans3D) return fail(-1, "missing gradient outputs");
+    if (gs->colors_precomp ? !g->dL_dcolors : !g->dL_dsh_dc) return fail(-1, "missing colour/SH gradient output");
+    if (!gs->colors_precomp && gs->sh_rest && !g->dL_dsh_rest) return fail(-1, "missing sh_rest gradient output");
+    if (gs->cov3D_precomp ? !g->dL_dcov3D : (!g->dL_dscales || !g->dL_drotations))
+        return fail(-1, "missing cov3D / scale / rotation gradient output");
+    return 0;
+}
+
+static GradOut grad_out(const gsr_grads* g) {
+    GradOut o;
+    o.means2D = g->dL_dmeans2D;
+    o.conic = g->dL_dconic;
+    o.opac = g->dL_dopacity;
+    o.colors = g->dL_dcolors;
+    o.means3D = g->dL_dmeans3D;
+    o.sh_dc = g->dL_dsh_dc;
+    o.sh_rest = g->dL_dsh_rest;
+    o.scales = g->dL_dscales;
+    o.rots = g->dL_drotations;
+    o.cov3D = g->dL_dcov3D;
+    return o;
+}
+
+int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
+                 const gsr_buffers* bufs, const float* dL_dpix, gsr_alloc_fn alloc_scratch, void* ctx,
+                 const gsr_grads* grads, void* stream_) {
+    g_err.clear();
+    if (int e = validate(cam, gs, rs)) return e;
+    if (gs->P == 0) return 0;
+    if (int e = check_grads(gs, grads)) return e;
+    hipStream_t stream = (hipStream_t)stream_;
+    const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
+    if (!bufs || !bufs->geom || !bufs->image || !dL_dpix) return fail(-1, "missing forward buffers / dL_dpix");
+    int ty0, ty1;
+    band(cam, rs, &ty0, &ty1);
+    const Views v = views(cam, gs->P, bufs);
+    const long long K = bufs->num_rendered;
+    float* partial = nullptr;
+    if (K > 0) {
+        if (!alloc_scratch) return fail(-1, "null scratch allocator");
+        partial = static_cast<float*>(alloc_scratch(ctx, gsr_scratch_bytes((int32_t)K)));
+        if (!partial) return fail(-2, "allocation failed (scratch, K=%lld)", K);
+        GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.sorted_j, v.rec,
+                                            v.final_T, v.n_contrib, dL_dpix, partial, stream),
+                      "blend backward");
+    }
+    // K == 0: no partials and no grad2d -> the kernel uses zero 2D gradients
+    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), v.depth_key, v.flags, v.inst_start, v.tiles,
+                                             partial, nullptr, grad_out(grads), stream),
+                  "preprocess backward");
+    return 0;
+}
+
+int gsr_backward_blend(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
+                       const gsr_buffers* bufs, const float* dL_dpix, gsr_alloc_fn alloc_scratch, void* ctx,
+                       float* grad2d, void* stream) {
+    g_err.clear();
+    if (!grad2d && gs && gs->P > 0) return fail(-1, "null grad2d");
+    return backward_impl(cam, gs, rs, bufs, dL_dpix, alloc_scratch, ctx, nullptr, grad2d, stream);
+}
+
+int gsr_backward_preprocess(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
+                            const gsr_buffers* bufs, const float* grad2d, const gsr_grads* grads,
+                            void* stream_) {
+    g_err.clear();
+    if (int e = validate(cam, gs, rs)) return e;
+    if (gs->P == 0) return 0;
+    if (int e = check_grads(gs, grads)) return e;
+    if (!bufs || !bufs->geom || !grad2d) return fail(-1, "missing forward buffers / grad2d");
+    hipStream_t stream = (hipStream_t)stream_;
+    const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
+    GeomLayout gl(gs->P);
+    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), at<uint32_t>(bufs->geom, gl.depth_key),
+                                             at<uint32_t>(bufs->geom, gl.flags),
+                                             at<uint32_t>(bufs->geom, gl.inst_start),
+                                             at<uint32_t>(bufs->geom, gl.tiles), nullptr, grad2d,
+                                             grad_out(grads), stream),
+                  "preprocess backward");
+    return 0;
+}
+
+int gsr_profile_enable(uint32_t stage_mask) {
+    Profiler& p = prof();
+    std::lock_guard<std::mutex> lk(p.mu);
+    for (auto& r : p.pending) {
+        hipEventSynchronize(r.b);
+        p.pool.push_back(r.a);
+        p.pool.push_back(r.b);
+    }
+    p.pending.clear();
+    for (int i = 0; i < GSR_NUM_STAGES; ++i) p.ms[i] = 0.0, p.counts[i] = 0;
+    __atomic_store_n(&p.mask, stage_mask, __ATOMIC_RELAXED);
+    return 0;
+}
+
+int gsr_profile_read(double* ms, uint32_t* counts) {
+    Profiler& p = prof();
+    std::lock_guard<std::mutex> lk(p.mu);
+    for (auto& r : p.pending) {
+        float t = 0.f;
+        if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&t, r.a, r.b) == hipSuccess) {
+            p.ms[r.stage] += t;
+            p.counts[r.stage] += 1;
+        }
+        p.pool.push_back(r.a);
+        p.pool.push_back(r.b);
+    }
+    p.pending.clear();
+    for (int i = 0; i < GSR_NUM_STAGES; ++i) {
+        if (ms) ms[i] = p.ms[i];
+        if (counts) counts[i] = p.counts[i];
+        p.ms[i] = 0.0;
+        p.counts[i] = 0;
+    }
+    return 0;
+}
+
+const char* gsr_stage_name(int stage) {
+    static const char* names[GSR_NUM_STAGES] = {"preprocess", "depth_sort", "scan", "duplicate", "tile_sort",
+                                               "finalize", "blend_fwd", "blend_bwd", "preprocess_bwd",
+                                               "gather_grad2d", "misc"};
+    return (stage >= 0 && stage < GSR_NUM_STAGES) ? names[stage] : "?";
+}
+
+const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, int what) {
+    if (!cam || !bufs || !bufs->geom || !bufs->image) return nullptr;
+    const Views v = views(cam, P, bufs);
+    switch (what) {
+        case GSR_VIEW_RADII_SORTED_GID: return v.sorted_gid;
+        case GSR_VIEW_SORTED_TILE: return v.sorted_tile;
+        case GSR_VIEW_RANGES: return v.ranges;
+        case GSR_VIEW_FINAL_T: return v.final_T;
+        case GSR_VIEW_N_CONTRIB: return v.n_contrib;
+        case GSR_VIEW_DEPTH_KEY: return v.depth_key;
+        case GSR_VIEW_TILES_TOUCHED: return v.tiles;
+        case GSR_VIEW_RECORDS: return v.rec;
+        default: return nullptr;
+    }
+}
+
+}  // extern "C"

@@ -1,0 +1,97 @@
+// gsr_internal.h -- buffer layouts and launch helpers shared by the C-ABI (gsr_api.cpp)
+// and the kernels.  HBM layout (DESIGN.md "Data layout"):
+//
+//   geometry (per Gaussian, P):   depth_key u32 | tiles u32 | flags u32 | rec float4[3]
+//                                 | inst_start u32 | offsets u32 | sort ping-pong 4 x u32
+//                                 | radix histogram (256 x blocks) | scan partials
+//   binning  (per instance, K):   tile key/val ping-pong 4 x u32 | inst_gid u32 | sorted_gid u32
+//                                 | radix histogram
+//   image    (per pixel):         ranges uint2[tiles] | final_T f32 | n_contrib u32
+//   scratch  (backward, per K):   partial float[GSR_GRAD2D_STRIDE]  (indexed by emission j)
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/gsr/gsr.h"
+
+namespace gsr {
+
+constexpr int kTile = GSR_TILE;
+constexpr int kSortBlock = 256;             // threads per radix-sort / scan block
+constexpr int kSortItems = 16;              // items per thread
+constexpr int kSortTile = kSortBlock * kSortItems;  // 4096 items per block
+constexpr int kRecFloats = 12;              // 3 x float4 per Gaussian record
+constexpr int kPart = GSR_GRAD2D_STRIDE;    // floats per partial / grad2d entry
+
+inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
+inline int div_up(long long a, long long b) { return (int)((a + b - 1) / b); }
+inline int sort_blocks(long long n) { return n > 0 ? div_up(n, kSortTile) : 0; }
+
+struct GeomLayout {
+    size_t depth_key, tiles, flags, rec, inst_start, offsets, sA_k, sA_v, sB_k, sB_v, hist,
+        partials, total;
+    GeomLayout(int P) {
+        size_t o = 0, n = (size_t)(P > 0 ? P : 1);
+        auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
+        depth_key = take(4 * n);
+        tiles = take(4 * n);
+        flags = take(4 * n);
+        rec = take(16 * 3 * n);
+        inst_start = take(4 * n);
+        offsets = take(4 * n);
+        sA_k = take(4 * n);
+        sA_v = take(4 * n);
+        sB_k = take(4 * n);
+        sB_v = take(4 * n);
+        hist = take(4 * (256 * (size_t)(sort_blocks(n) + 1) + 256));
+        partials = take(4 * ((size_t)sort_blocks(n) + 16));
+        total = o;
+    }
+};
+
+struct BinLayout {
+    size_t kA, vA, kB, vB, inst_gid, sorted_gid, hist, total;
+    BinLayout(long long K) {
+        size_t o = 0, n = (size_t)(K > 0 ? K : 1);
+        auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
+        kA = take(4 * n);
+        vA = take(4 * n);
+        kB = take(4 * n);
+        vB = take(4 * n);
+        inst_gid = take(4 * n);
+        sorted_gid = take(4 * n);
+        hist = take(4 * (256 * (size_t)(sort_blocks(n) + 1) + 256));
+        total = o;
+    }
+};
+
+struct ImgLayout {
+    size_t ranges, final_T, n_contrib, total;
+    ImgLayout(int W, int H) {
+        size_t o = 0;
+        auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
+        size_t tiles = (size_t)div_up(W, kTile) * div_up(H, kTile);
+        size_t pix = (size_t)W * H;
+        ranges = take(8 * (tiles ? tiles : 1));
+        final_T = take(4 * (pix ? pix : 1));
+        n_contrib = take(4 * (pix ? pix : 1));
+        total = o;
+    }
+};
+
+// number of 8-bit LSD passes to sort tile ids of a grid with `tiles` tiles
+inline int tile_bits(int tiles) {
+    int b = 1;
+    while ((1ll << b) < tiles) ++b;
+    return b;
+}
+inline int tile_passes(int tiles) { return (tile_bits(tiles) + 7) / 8; }
+
+template <class T>
+inline T* at(void* base, size_t off) { return reinterpret_cast<T*>(static_cast<char*>(base) + off); }
+template <class T>
+inline const T* at(const void* base, size_t off) {
+    return reinterpret_cast<const T*>(static_cast<const char*>(base) + off);
+}
+
+}  // namespace gsr

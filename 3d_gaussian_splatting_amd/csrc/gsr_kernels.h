@@ -1,0 +1,74 @@
+// gsr_kernels.h -- host-side launchers of the CDNA4 kernels (one per pipeline stage).
+// Every launcher enqueues on `stream` and returns hipGetLastError() as an int.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "gsr_internal.h"
+
+namespace gsr {
+
+struct GaussIn {
+    int P, D, M_rest;
+    float smod;
+    const float *means3D, *sh_dc, *sh_rest, *colors, *opac, *scales, *rots, *cov3D;
+};
+
+struct PreOut {
+    int32_t* radii;
+    uint32_t* depth_key;
+    uint32_t* tiles;
+    uint32_t* flags;
+    float4* rec;
+};
+
+// F1: projection, EWA cov2D, conic, radius, tile rect, SH->RGB (bit-exact vs the oracle)
+int launch_preprocess(const gsr_camera& cam, const GaussIn& in, int ty0, int ty1, const PreOut& out,
+                      hipStream_t s);
+
+// LSD radix sort of (u32 key, u32 value) by key bits [0, nbits); vals_in == nullptr means the
+// identity permutation.  Ping-pongs between (k0,v0) and (k1,v1); returns in *which (0/1) where
+// the sorted data ended.  hist: 256*(blocks+1)+256 u32.
+int radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* k0, uint32_t* v0,
+               uint32_t* k1, uint32_t* v1, long long n, int nbits, uint32_t* hist, int* which,
+               hipStream_t s);
+
+// inclusive scan out[r] = sum_{q<=r} in[idx ? idx[q] : q]; partials: blocks+16 u32
+int inclusive_scan_gather(const uint32_t* in, const uint32_t* idx, uint32_t* out, int n,
+                          uint32_t* partials, hipStream_t s);
+
+// F3: emit (tile key, owner gid) for every (Gaussian, tile in band) in depth-rank order
+int launch_duplicate(const uint32_t* gid_by_rank, const uint32_t* offsets, const uint32_t* tiles,
+                     const float4* rec, int P, int grid_x, int ty0, int ty1, uint32_t* inst_start,
+                     uint32_t* tkey, uint32_t* inst_gid, hipStream_t s);
+
+// F5: sorted_gid[i] = inst_gid[sorted_j[i]]; ranges[tile] = [start, end)
+int launch_finalize(const uint32_t* sorted_tile, const uint32_t* sorted_j, const uint32_t* inst_gid,
+                    long long K, uint32_t* sorted_gid, uint2* ranges, hipStream_t s);
+
+// F6: per-tile front-to-back blend
+int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
+                         const uint2* ranges, const uint32_t* sorted_gid, const float4* rec,
+                         float* out_color, float* final_T, uint32_t* n_contrib, hipStream_t s);
+
+// B1: per-tile back-to-front gradients -> per-instance partial[j] (kPart floats)
+int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
+                          const uint2* ranges, const uint32_t* sorted_gid, const uint32_t* sorted_j,
+                          const float4* rec, const float* final_T, const uint32_t* n_contrib,
+                          const float* dL_dpix, float* partial, hipStream_t s);
+
+// sum partials per Gaussian (emission order) -> grad2d (kPart floats per Gaussian)
+int launch_gather_grad2d(const uint32_t* inst_start, const uint32_t* tiles, const float* partial,
+                         int P, float* grad2d, hipStream_t s);
+
+struct GradOut {
+    float *means2D, *conic, *opac, *colors, *means3D, *sh_dc, *sh_rest, *scales, *rots, *cov3D;
+};
+
+// B2: chain rule to the leaves.  Source of the 2D gradients: either per-instance partials
+// (partial != nullptr: summed in emission order here) or a grad2d buffer.
+int launch_preprocess_backward(const gsr_camera& cam, const GaussIn& in, const uint32_t* depth_key,
+                               const uint32_t* flags, const uint32_t* inst_start,
+                               const uint32_t* tiles, const float* partial, const float* grad2d,
+                               const GradOut& out, hipStream_t s);
+
+}  // namespace gsr

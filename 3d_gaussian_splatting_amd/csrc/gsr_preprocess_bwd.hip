@@ -1,0 +1,362 @@
+// gsr_preprocess_bwd.hip -- B2: per-Gaussian chain rule from the 2D gradients (mean2D, conic,
+// opacity, colour) to the leaves (means3D, SH, scales, rotations, or the precomputed colour /
+// cov3D), on gfx950.  One thread per Gaussian; every output element is written (zeros for
+// culled Gaussians) so the caller can hand in uninitialised tensors.
+//
+// The per-Gaussian 2D gradient is the sum of its per-(tile, instance) partials in emission
+// order (rect row-major), read from the contiguous range [inst_start[g], +tiles[g]) -- a fixed
+// order, so results are bitwise reproducible run to run.
+//
+// Derivation (restated; same formulas as oracle/gsr_oracle.c
+// preprocess_backward_one): conic (A,B,C) = inv([[a,b],[b,c]]), cov2D = T Sigma T^T with
+// T = J W, J the EWA Jacobian (x/y terms zeroed outside the 1.3 tan(fov) clamp), Sigma = L L^T,
+// L = R(q) diag(mod s) (src/utils/general_utils.cpp:24-37,91-97), SH basis derivatives w.r.t.
+// the normalised view direction, NDC mean through the homogeneous divide.
+//
+// Roofline: HBM-bound (V*(80+12M) + N*(60+12M) bytes).
+#include "gsr_kernels.h"
+
+namespace gsr {
+namespace {
+
+__constant__ float kC2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f,
+                             -1.0925484305920792f, 0.5462742152960396f};
+__constant__ float kC3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f,
+                             0.3731763325901154f, -0.4570457994644658f, 1.445305721320277f,
+                             -0.5900435899266435f};
+constexpr float kC0 = 0.28209479177387814f;
+constexpr float kC1 = 0.4886025119029199f;
+
+__global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __restrict__ inst_start,
+                                                            const uint32_t* __restrict__ tiles,
+                                                            const float* __restrict__ partial, int P,
+                                                            float* __restrict__ grad2d) {
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= P) return;
+    float a[kPart];
+#pragma unroll
+    for (int k = 0; k < kPart; ++k) a[k] = 0.f;
+    const uint32_t j0 = inst_start[g], nt = tiles[g];
+    for (uint32_t j = j0; j < j0 + nt; ++j) {
+        const float4* src = reinterpret_cast<const float4*>(partial + (size_t)kPart * j);
+        const float4 v0 = src[0], v1 = src[1], v2 = src[2];
+        a[0] += v0.x; a[1] += v0.y; a[2] += v0.z; a[3] += v0.w;
+        a[4] += v1.x; a[5] += v1.y; a[6] += v1.z; a[7] += v1.w;
+        a[8] += v2.x;
+    }
+    float4* dst = reinterpret_cast<float4*>(grad2d + (size_t)kPart * g);
+    dst[0] = make_float4(a[0], a[1], a[2], a[3]);
+    dst[1] = make_float4(a[4], a[5], a[6], a[7]);
+    dst[2] = make_float4(a[8], 0.f, 0.f, 0.f);
+}
+
+__global__ __launch_bounds__(256) void preprocess_backward_kernel(
+    const gsr_camera cam, const GaussIn in, const uint32_t* __restrict__ depth_key,
+    const uint32_t* __restrict__ flags, const uint32_t* __restrict__ inst_start,
+    const uint32_t* __restrict__ tiles, const float* __restrict__ partial,
+    const float* __restrict__ grad2d, GradOut out) {
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= in.P) return;
+    const bool visible = depth_key[g] != 0xFFFFFFFFu;
+    // ---- 2D gradients ----
+    float g2[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) g2[k] = 0.f;
+    if (visible) {
+        if (partial) {
+            const uint32_t j0 = inst_start[g], nt = tiles[g];
+            for (uint32_t j = j0; j < j0 + nt; ++j) {
+                const float4* src = reinterpret_cast<const float4*>(partial + (size_t)kPart * j);
+                const float4 v0 = src[0], v1 = src[1], v2 = src[2];
+                g2[0] += v0.x; g2[1] += v0.y; g2[2] += v0.z; g2[3] += v0.w;
+                g2[4] += v1.x; g2[5] += v1.y; g2[6] += v1.z; g2[7] += v1.w;
+                g2[8] += v2.x;
+            }
+        } else if (grad2d) {
+            const float4* src = reinterpret_cast<const float4*>(grad2d + (size_t)kPart * g);
+            const float4 v0 = src[0], v1 = src[1], v2 = src[2];
+            g2[0] = v0.x; g2[1] = v0.y; g2[2] = v0.z; g2[3] = v0.w;
+            g2[4] = v1.x; g2[5] = v1.y; g2[6] = v1.z; g2[7] = v1.w;
+            g2[8] = v2.x;
+        }
+    }
+    out.means2D[3 * g + 0] = g2[0];
+    out.means2D[3 * g + 1] = g2[1];
+    out.means2D[3 * g + 2] = 0.f;
+    if (out.conic) {
+        out.conic[3 * g + 0] = g2[2];
+        out.conic[3 * g + 1] = g2[3];
+        out.conic[3 * g + 2] = g2[4];
+    }
+    out.opac[g] = g2[5];
+
+    const float* V = cam.viewmatrix;
+    const float* Pm = cam.projmatrix;
+    const float p0 = in.means3D[3 * g + 0], p1 = in.means3D[3 * g + 1], p2 = in.means3D[3 * g + 2];
+    const float p[3] = {p0, p1, p2};
+    float dm[3] = {0.f, 0.f, 0.f};
+    const int D = in.D;
+    const int nb = (D + 1) * (D + 1);
+
+    if (!visible) {
+        if (in.colors) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) out.colors[3 * g + k] = 0.f;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) out.sh_dc[3 * g + k] = 0.f;
+            if (in.sh_rest)
+                for (int k = 0; k < 3 * in.M_rest; ++k) out.sh_rest[(size_t)g * in.M_rest * 3 + k] = 0.f;
+        }
+        out.means3D[3 * g + 0] = 0.f;
+        out.means3D[3 * g + 1] = 0.f;
+        out.means3D[3 * g + 2] = 0.f;
+        if (in.cov3D) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) out.cov3D[6 * g + k] = 0.f;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) out.scales[3 * g + k] = 0.f;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) out.rots[4 * g + k] = 0.f;
+        }
+        return;
+    }
+    // ---- colour -> SH / view direction ----
+    if (in.colors) {
+        out.colors[3 * g + 0] = g2[6];
+        out.colors[3 * g + 1] = g2[7];
+        out.colors[3 * g + 2] = g2[8];
+    } else {
+        const uint32_t cl = flags[g];
+        const float dres[3] = {(cl & 1u) ? 0.f : g2[6], (cl & 2u) ? 0.f : g2[7], (cl & 4u) ? 0.f : g2[8]};
+        const float vx = p0 - cam.campos[0], vy = p1 - cam.campos[1], vz = p2 - cam.campos[2];
+        const float len = sqrtf(vx * vx + vy * vy + vz * vz);
+        const float x = vx / len, y = vy / len, z = vz / len;
+        float basis[16], dbx[16], dby[16], dbz[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) basis[k] = dbx[k] = dby[k] = dbz[k] = 0.f;
+        basis[0] = kC0;
+        if (D >= 1) {
+            basis[1] = -kC1 * y; basis[2] = kC1 * z; basis[3] = -kC1 * x;
+            dby[1] = -kC1; dbz[2] = kC1; dbx[3] = -kC1;
+        }
+        if (D >= 2) {
+            const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+            basis[4] = kC2[0] * xy;
+            basis[5] = kC2[1] * yz;
+            basis[6] = kC2[2] * (2.0f * zz - xx - yy);
+            basis[7] = kC2[3] * xz;
+            basis[8] = kC2[4] * (xx - yy);
+            dbx[4] = kC2[0] * y; dby[4] = kC2[0] * x;
+            dby[5] = kC2[1] * z; dbz[5] = kC2[1] * y;
+            dbx[6] = kC2[2] * -2.f * x; dby[6] = kC2[2] * -2.f * y; dbz[6] = kC2[2] * 4.f * z;
+            dbx[7] = kC2[3] * z; dbz[7] = kC2[3] * x;
+            dbx[8] = kC2[4] * 2.f * x; dby[8] = kC2[4] * -2.f * y;
+            if (D >= 3) {
+                basis[9] = kC3[0] * y * (3.0f * xx - yy);
+                basis[10] = kC3[1] * xy * z;
+                basis[11] = kC3[2] * y * (4.0f * zz - xx - yy);
+                basis[12] = kC3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy);
+                basis[13] = kC3[4] * x * (4.0f * zz - xx - yy);
+                basis[14] = kC3[5] * z * (xx - yy);
+                basis[15] = kC3[6] * x * (xx - 3.0f * yy);
+                dbx[9] = kC3[0] * 6.f * xy; dby[9] = kC3[0] * 3.f * (xx - yy);
+                dbx[10] = kC3[1] * yz; dby[10] = kC3[1] * xz; dbz[10] = kC3[1] * xy;
+                dbx[11] = kC3[2] * -2.f * xy; dby[11] = kC3[2] * (4.f * zz - xx - 3.f * yy); dbz[11] = kC3[2] * 8.f * yz;
+                dbx[12] = kC3[3] * -6.f * xz; dby[12] = kC3[3] * -6.f * yz; dbz[12] = kC3[3] * (6.f * zz - 3.f * xx - 3.f * yy);
+                dbx[13] = kC3[4] * (4.f * zz - 3.f * xx - yy); dby[13] = kC3[4] * -2.f * xy; dbz[13] = kC3[4] * 8.f * xz;
+                dbx[14] = kC3[5] * 2.f * xz; dby[14] = kC3[5] * -2.f * yz; dbz[14] = kC3[5] * (xx - yy);
+                dbx[15] = kC3[6] * 3.f * (xx - yy); dby[15] = kC3[6] * -6.f * xy;
+            }
+        }
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) out.sh_dc[3 * g + ch] = basis[0] * dres[ch];
+        float ddx = 0.f, ddy = 0.f, ddz = 0.f;
+        if (in.sh_rest) {
+            const float* rest = in.sh_rest + (size_t)g * in.M_rest * 3;
+            float* drest = out.sh_rest + (size_t)g * in.M_rest * 3;
+#pragma unroll
+            for (int k = 1; k < 16; ++k) {
+                if (k > in.M_rest) break;
+                if (k < nb) {
+                    const float c0 = rest[3 * (k - 1) + 0], c1 = rest[3 * (k - 1) + 1], c2 = rest[3 * (k - 1) + 2];
+                    drest[3 * (k - 1) + 0] = basis[k] * dres[0];
+                    drest[3 * (k - 1) + 1] = basis[k] * dres[1];
+                    drest[3 * (k - 1) + 2] = basis[k] * dres[2];
+                    const float sdot = c0 * dres[0] + c1 * dres[1] + c2 * dres[2];
+                    ddx += dbx[k] * sdot;
+                    ddy += dby[k] * sdot;
+                    ddz += dbz[k] * sdot;
+                } else {
+                    drest[3 * (k - 1) + 0] = 0.f;
+                    drest[3 * (k - 1) + 1] = 0.f;
+                    drest[3 * (k - 1) + 2] = 0.f;
+                }
+            }
+        }
+        const float dd = x * ddx + y * ddy + z * ddz;
+        dm[0] += (ddx - x * dd) / len;
+        dm[1] += (ddy - y * dd) / len;
+        dm[2] += (ddz - z * dd) / len;
+    }
+    // ---- mean2D (NDC) -> mean3D ----
+    {
+        const float hx = Pm[0] * p0 + Pm[4] * p1 + Pm[8] * p2 + Pm[12];
+        const float hy = Pm[1] * p0 + Pm[5] * p1 + Pm[9] * p2 + Pm[13];
+        const float hw = Pm[3] * p0 + Pm[7] * p1 + Pm[11] * p2 + Pm[15];
+        const float mw = 1.0f / (hw + 0.0000001f);
+        const float mw2 = mw * mw;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            dm[k] += (Pm[4 * k + 0] * mw - Pm[4 * k + 3] * hx * mw2) * g2[0] +
+                     (Pm[4 * k + 1] * mw - Pm[4 * k + 3] * hy * mw2) * g2[1];
+    }
+    // ---- conic -> cov2D -> (cov3D, view-space mean) ----
+    float c3[6], R[9], se[3] = {0.f, 0.f, 0.f};
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (in.cov3D) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) c3[k] = in.cov3D[6 * g + k];
+    } else {
+        q = *reinterpret_cast<const float4*>(in.rots + 4 * g);
+        const float r = q.x, x = q.y, y = q.z, z = q.w;
+        R[0] = 1.f - 2.f * (y * y + z * z);
+        R[1] = 2.f * (x * y - r * z);
+        R[2] = 2.f * (x * z + r * y);
+        R[3] = 2.f * (x * y + r * z);
+        R[4] = 1.f - 2.f * (x * x + z * z);
+        R[5] = 2.f * (y * z - r * x);
+        R[6] = 2.f * (x * z - r * y);
+        R[7] = 2.f * (y * z + r * x);
+        R[8] = 1.f - 2.f * (x * x + y * y);
+        se[0] = in.smod * in.scales[3 * g + 0];
+        se[1] = in.smod * in.scales[3 * g + 1];
+        se[2] = in.smod * in.scales[3 * g + 2];
+        float L[9];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) L[3 * i + j] = R[3 * i + j] * se[j];
+        c3[0] = L[0] * L[0] + L[1] * L[1] + L[2] * L[2];
+        c3[1] = L[0] * L[3] + L[1] * L[4] + L[2] * L[5];
+        c3[2] = L[0] * L[6] + L[1] * L[7] + L[2] * L[8];
+        c3[3] = L[3] * L[3] + L[4] * L[4] + L[5] * L[5];
+        c3[4] = L[3] * L[6] + L[4] * L[7] + L[5] * L[8];
+        c3[5] = L[6] * L[6] + L[7] * L[7] + L[8] * L[8];
+    }
+    const float tx = V[0] * p0 + V[4] * p1 + V[8] * p2 + V[12];
+    const float ty = V[1] * p0 + V[5] * p1 + V[9] * p2 + V[13];
+    const float tz = V[2] * p0 + V[6] * p1 + V[10] * p2 + V[14];
+    const float Wf = (float)cam.width, Hf = (float)cam.height;
+    const float fx = Wf / (2.0f * cam.tanfovx), fy = Hf / (2.0f * cam.tanfovy);
+    const float limx = 1.3f * cam.tanfovx, limy = 1.3f * cam.tanfovy;
+    const float txtz = tx / tz, tytz = ty / tz;
+    const float cx = fminf(limx, fmaxf(-limx, txtz)) * tz;
+    const float cy = fminf(limy, fmaxf(-limy, tytz)) * tz;
+    const float xmul = (txtz < -limx || txtz > limx) ? 0.f : 1.f;
+    const float ymul = (tytz < -limy || tytz > limy) ? 0.f : 1.f;
+    const float tz2 = tz * tz, tz3 = tz2 * tz;
+    const float J00 = fx / tz, J02 = -(fx * cx) / tz2, J11 = fy / tz, J12 = -(fy * cy) / tz2;
+    float T0[3], T1[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        T0[k] = J00 * V[4 * k + 0] + J02 * V[4 * k + 2];
+        T1[k] = J11 * V[4 * k + 1] + J12 * V[4 * k + 2];
+    }
+    const float S[9] = {c3[0], c3[1], c3[2], c3[1], c3[3], c3[4], c3[2], c3[4], c3[5]};
+    float ST0[3], ST1[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        ST0[i] = S[3 * i + 0] * T0[0] + S[3 * i + 1] * T0[1] + S[3 * i + 2] * T0[2];
+        ST1[i] = S[3 * i + 0] * T1[0] + S[3 * i + 1] * T1[1] + S[3 * i + 2] * T1[2];
+    }
+    const float a = (ST0[0] * T0[0] + ST0[1] * T0[1] + ST0[2] * T0[2]) + 0.3f;
+    const float b = ST0[0] * T1[0] + ST0[1] * T1[1] + ST0[2] * T1[2];
+    const float c = (ST1[0] * T1[0] + ST1[1] * T1[1] + ST1[2] * T1[2]) + 0.3f;
+    const float det = a * c - b * b;
+    const float dA = g2[2], dB = g2[3], dC = g2[4];
+    const float inv2 = 1.0f / (det * det);
+    const float dL_da = inv2 * (-c * c * dA + b * c * dB - b * b * dC);
+    const float dL_db = inv2 * (2.f * b * c * dA - (a * c + b * b) * dB + 2.f * a * b * dC);
+    const float dL_dc = inv2 * (-b * b * dA + a * b * dB - a * a * dC);
+    float dS[6];
+    dS[0] = T0[0] * T0[0] * dL_da + T0[0] * T1[0] * dL_db + T1[0] * T1[0] * dL_dc;
+    dS[3] = T0[1] * T0[1] * dL_da + T0[1] * T1[1] * dL_db + T1[1] * T1[1] * dL_dc;
+    dS[5] = T0[2] * T0[2] * dL_da + T0[2] * T1[2] * dL_db + T1[2] * T1[2] * dL_dc;
+    dS[1] = 2.f * T0[0] * T0[1] * dL_da + (T0[0] * T1[1] + T0[1] * T1[0]) * dL_db + 2.f * T1[0] * T1[1] * dL_dc;
+    dS[2] = 2.f * T0[0] * T0[2] * dL_da + (T0[0] * T1[2] + T0[2] * T1[0]) * dL_db + 2.f * T1[0] * T1[2] * dL_dc;
+    dS[4] = 2.f * T0[1] * T0[2] * dL_da + (T0[1] * T1[2] + T0[2] * T1[1]) * dL_db + 2.f * T1[1] * T1[2] * dL_dc;
+    float dJ00 = 0.f, dJ02 = 0.f, dJ11 = 0.f, dJ12 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float dT0 = 2.f * ST0[i] * dL_da + ST1[i] * dL_db;
+        const float dT1 = 2.f * ST1[i] * dL_dc + ST0[i] * dL_db;
+        dJ00 += dT0 * V[4 * i + 0];
+        dJ02 += dT0 * V[4 * i + 2];
+        dJ11 += dT1 * V[4 * i + 1];
+        dJ12 += dT1 * V[4 * i + 2];
+    }
+    const float dtx = xmul * (-fx / tz2) * dJ02;
+    const float dty = ymul * (-fy / tz2) * dJ12;
+    const float dtz = (-fx / tz2) * dJ00 + (-fy / tz2) * dJ11 + (2.f * fx * cx / tz3) * dJ02 +
+                      (2.f * fy * cy / tz3) * dJ12;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) dm[k] += V[4 * k + 0] * dtx + V[4 * k + 1] * dty + V[4 * k + 2] * dtz;
+    out.means3D[3 * g + 0] = dm[0];
+    out.means3D[3 * g + 1] = dm[1];
+    out.means3D[3 * g + 2] = dm[2];
+    (void)p;
+    // ---- cov3D -> scale, rotation ----
+    if (in.cov3D) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) out.cov3D[6 * g + k] = dS[k];
+        return;
+    }
+    const float Gm[9] = {dS[0], 0.5f * dS[1], 0.5f * dS[2], 0.5f * dS[1], dS[3], 0.5f * dS[4],
+                         0.5f * dS[2], 0.5f * dS[4], dS[5]};
+    float L[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) L[3 * i + j] = R[3 * i + j] * se[j];
+    float dR[9];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const float dl = 2.f * (Gm[3 * i + 0] * L[0 + j] + Gm[3 * i + 1] * L[3 + j] + Gm[3 * i + 2] * L[6 + j]);
+            acc += dl * R[3 * i + j];
+            dR[3 * i + j] = dl * se[j];
+        }
+        out.scales[3 * g + j] = in.smod * acc;
+    }
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    out.rots[4 * g + 0] = 2.f * (-z * dR[1] + y * dR[2] + z * dR[3] - x * dR[5] - y * dR[6] + x * dR[7]);
+    out.rots[4 * g + 1] = 2.f * (y * dR[1] + z * dR[2] + y * dR[3] - 2.f * x * dR[4] - r * dR[5] + z * dR[6] + r * dR[7] - 2.f * x * dR[8]);
+    out.rots[4 * g + 2] = 2.f * (-2.f * y * dR[0] + x * dR[1] + r * dR[2] + x * dR[3] + z * dR[5] - r * dR[6] + z * dR[7] - 2.f * y * dR[8]);
+    out.rots[4 * g + 3] = 2.f * (-2.f * z * dR[0] - r * dR[1] + x * dR[2] + r * dR[3] - 2.f * z * dR[4] + y * dR[5] + x * dR[6] + y * dR[7]);
+}
+
+}  // namespace
+
+int launch_gather_grad2d(const uint32_t* inst_start, const uint32_t* tiles, const float* partial,
+                         int P, float* grad2d, hipStream_t s) {
+    if (P <= 0) return 0;
+    hipLaunchKernelGGL(gather_grad2d_kernel, dim3(div_up(P, 256)), dim3(256), 0, s, inst_start, tiles,
+                       partial, P, grad2d);
+    return (int)hipGetLastError();
+}
+
+int launch_preprocess_backward(const gsr_camera& cam, const GaussIn& in, const uint32_t* depth_key,
+                               const uint32_t* flags, const uint32_t* inst_start,
+                               const uint32_t* tiles, const float* partial, const float* grad2d,
+                               const GradOut& out, hipStream_t s) {
+    if (in.P <= 0) return 0;
+    hipLaunchKernelGGL(preprocess_backward_kernel, dim3(div_up(in.P, 256)), dim3(256), 0, s, cam, in,
+                       depth_key, flags, inst_start, tiles, partial, grad2d, out);
+    return (int)hipGetLastError();
+}
+
+}  // namespace gsr

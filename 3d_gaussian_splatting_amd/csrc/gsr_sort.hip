@@ -1,0 +1,364 @@
+// gsr_sort.hip -- binning on gfx950: scan, duplicateWithKeys, LSD radix sort, tile ranges.
+//
+// Canonical instance order is (tile, depth bits, gid) (SURVEY §8a notes).  It is reached
+// with far fewer sorted bytes than one 45-bit key sort over K instances:
+//   1. depth sort of the P Gaussians: stable LSD over the 32-bit depth key, values = gid
+//      (identity input, so ties keep gid order)            -> gid_by_rank
+//   2. inclusive scan of tiles_touched in rank order        -> offsets (K = last)
+//   3. duplicate: rank r emits its band-clipped rect row-major at offsets[r-1]: the instance
+//      array is then already in (depth bits, gid, rect order) order
+//   4. stable LSD over the ceil(log2 tiles)-bit tile key only (2 passes at 1080p),
+//      values = emission index j                             -> sorted_j
+//   5. finalize: sorted_gid = inst_gid[sorted_j], tile ranges from key boundaries
+// Sorted bytes at 1M/1080p: 4 passes x 1M x 8 B + 2 passes x 6.5M x 8 B, vs 6 passes x 6.5M
+// x 12 B for a 45-bit (tile|depth) key sort.
+//
+// Radix sort = reduce-then-scan per 8-bit digit: upsweep (per-block digit counts), column
+// scan (per digit over blocks), downsweep (stable wave64 ranking: 8 ballots give each lane
+// its peer mask, popcount below it is its rank in the round; per-wave running counters in
+// LDS; digit base = scanned counts).  All integer work: HBM-bound, no MFMA.
+#include "gsr_kernels.h"
+
+namespace gsr {
+namespace {
+
+constexpr int kB = kSortBlock;       // 256 threads = 4 waves
+constexpr int kI = kSortItems;       // 16 rounds per wave
+constexpr int kWaves = kB / 64;
+constexpr int kWaveItems = kI * 64;  // 1024 contiguous items per wave
+
+__device__ inline uint64_t lanemask_lt() {
+    const int lane = threadIdx.x & 63;
+    return (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+}
+
+// lanes (among `active`) holding the same digit as this lane
+__device__ inline uint64_t match_digit(uint32_t d, int nbits, uint64_t active) {
+    uint64_t peers = active;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        if (b < nbits) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+    }
+    return peers;
+}
+
+// ---- upsweep: per-block digit histogram, written digit-major hist[d * nb + b] ----
+__global__ __launch_bounds__(kB) void radix_upsweep(const uint32_t* __restrict__ keys, long long n,
+                                                    int shift, int nbits, int nb,
+                                                    uint32_t* __restrict__ hist) {
+    __shared__ uint32_t cnt[kWaves][256];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) cnt[k][tid] = 0;
+    __syncthreads();
+    const uint32_t mask = (1u << nbits) - 1u;
+    const long long base = (long long)blockIdx.x * kSortTile + (long long)w * kWaveItems;
+    for (int r = 0; r < kI; ++r) {
+        const long long idx = base + r * 64 + lane;
+        const bool valid = idx < n;
+        const uint32_t d = valid ? (keys[idx] >> shift) & mask : 0u;
+        const uint64_t active = __ballot(valid);
+        if (active == 0) break;
+        const uint64_t peers = match_digit(d, nbits, active);
+        if (valid && (peers & lanemask_lt()) == 0) cnt[w][d] += (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) s += cnt[k][tid];
+    hist[(size_t)tid * nb + blockIdx.x] = s;
+}
+
+// ---- column scan: block d turns hist[d*nb .. +nb) into an exclusive scan; totals[d] ----
+__global__ __launch_bounds__(kB) void radix_colscan(uint32_t* __restrict__ hist, int nb,
+                                                    uint32_t* __restrict__ totals) {
+    __shared__ uint32_t wsum[kWaves];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    uint32_t* col = hist + (size_t)blockIdx.x * nb;
+    uint32_t carry = 0;
+    for (int base = 0; base < nb; base += kB) {
+        const int i = base + tid;
+        const uint32_t v = i < nb ? col[i] : 0u;
+        // inclusive wave scan
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        uint32_t pre = 0;
+#pragma unroll
+        for (int k = 0; k < kWaves; ++k) pre += (k < w) ? wsum[k] : 0u;
+        if (i < nb) col[i] = carry + pre + x - v;
+        uint32_t tot = 0;
+#pragma unroll
+        for (int k = 0; k < kWaves; ++k) tot += wsum[k];
+        __syncthreads();
+        carry += tot;
+    }
+    if (tid == 0) totals[blockIdx.x] = carry;
+}
+
+// ---- downsweep: stable scatter ----
+__global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict__ keys_in,
+                                                      const uint32_t* __restrict__ vals_in,
+                                                      uint32_t* __restrict__ keys_out,
+                                                      uint32_t* __restrict__ vals_out, long long n,
+                                                      int shift, int nbits, int nb,
+                                                      const uint32_t* __restrict__ hist,
+                                                      const uint32_t* __restrict__ totals) {
+    __shared__ uint32_t wcnt[kWaves][256];
+    __shared__ uint32_t dbase[256];
+    __shared__ uint32_t wsum[kWaves];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const uint32_t mask = (1u << nbits) - 1u;
+    // digit base: exclusive scan of totals + this block's scanned count
+    {
+        const uint32_t v = totals[tid];
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+#pragma unroll
+        for (int k = 0; k < kWaves; ++k) wcnt[k][tid] = 0;
+        __syncthreads();
+        uint32_t pre = 0;
+#pragma unroll
+        for (int k = 0; k < kWaves; ++k) pre += (k < w) ? wsum[k] : 0u;
+        dbase[tid] = pre + x - v + hist[(size_t)tid * nb + blockIdx.x];
+    }
+    __syncthreads();
+    const long long base = (long long)blockIdx.x * kSortTile + (long long)w * kWaveItems;
+    uint32_t key[kI], val[kI], rank[kI];
+    const uint64_t lt = lanemask_lt();
+#pragma unroll
+    for (int r = 0; r < kI; ++r) {
+        const long long idx = base + r * 64 + lane;
+        const bool valid = idx < n;
+        key[r] = valid ? keys_in[idx] : 0xFFFFFFFFu;
+        val[r] = valid ? (vals_in ? vals_in[idx] : (uint32_t)idx) : 0u;
+        const uint32_t d = (key[r] >> shift) & mask;
+        const uint64_t active = __ballot(valid);
+        const uint64_t peers = match_digit(d, nbits, active);
+        const uint32_t old = wcnt[w][d];
+        rank[r] = old + (uint32_t)__popcll(peers & lt);
+        if (valid && (peers & lt) == 0) wcnt[w][d] = old + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    {
+        uint32_t off = dbase[tid];
+#pragma unroll
+        for (int k = 0; k < kWaves; ++k) {
+            const uint32_t c = wcnt[k][tid];
+            wcnt[k][tid] = off;
+            off += c;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kI; ++r) {
+        const long long idx = base + r * 64 + lane;
+        if (idx < n) {
+            const uint32_t d = (key[r] >> shift) & mask;
+            const uint32_t pos = wcnt[w][d] + rank[r];
+            keys_out[pos] = key[r];
+            vals_out[pos] = val[r];
+        }
+    }
+}
+
+// ---- scan (gathered input): reduce / partial scan / downsweep ----
+__device__ inline uint32_t block_exclusive_scan(uint32_t v, uint32_t* wsum, uint32_t* total) {
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+    const int nw = blockDim.x >> 6;
+    for (int k = 0; k < nw; ++k) {
+        pre += (k < w) ? wsum[k] : 0u;
+        tot += wsum[k];
+    }
+    __syncthreads();
+    *total = tot;
+    return pre + x - v;
+}
+
+__global__ __launch_bounds__(kB) void scan_reduce(const uint32_t* __restrict__ in,
+                                                  const uint32_t* __restrict__ idx, int n,
+                                                  uint32_t* __restrict__ partials) {
+    __shared__ uint32_t wsum[kWaves];
+    const int base = blockIdx.x * kSortTile;
+    uint32_t s = 0;
+#pragma unroll
+    for (int r = 0; r < kI; ++r) {
+        const int i = base + r * kB + threadIdx.x;
+        if (i < n) s += in[idx ? idx[i] : i];
+    }
+    uint32_t tot;
+    block_exclusive_scan(s, wsum, &tot);
+    if (threadIdx.x == 0) partials[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(1024) void scan_partials(uint32_t* __restrict__ partials, int nb) {
+    __shared__ uint32_t wsum[16];
+    uint32_t carry = 0;
+    for (int base = 0; base < nb; base += 1024) {
+        const int i = base + threadIdx.x;
+        const uint32_t v = i < nb ? partials[i] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_exclusive_scan(v, wsum, &tot);
+        if (i < nb) partials[i] = carry + ex;
+        carry += tot;
+    }
+}
+
+__global__ __launch_bounds__(kB) void scan_downsweep(const uint32_t* __restrict__ in,
+                                                     const uint32_t* __restrict__ idx, int n,
+                                                     const uint32_t* __restrict__ partials,
+                                                     uint32_t* __restrict__ out) {
+    __shared__ uint32_t buf[kSortTile + kSortTile / 32];
+    __shared__ uint32_t wsum[kWaves];
+    const int base = blockIdx.x * kSortTile;
+    const int tid = threadIdx.x;
+    auto pad = [](int i) { return i + (i >> 5); };
+#pragma unroll
+    for (int r = 0; r < kI; ++r) {
+        const int i = r * kB + tid;
+        const int g = base + i;
+        buf[pad(i)] = g < n ? in[idx ? idx[g] : g] : 0u;
+    }
+    __syncthreads();
+    uint32_t v[kI];
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kI; ++k) {
+        v[k] = buf[pad(tid * kI + k)];
+        s += v[k];
+        v[k] = s;  // thread-local inclusive
+    }
+    uint32_t tot;
+    const uint32_t ex = block_exclusive_scan(s, wsum, &tot) + partials[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < kI; ++k) buf[pad(tid * kI + k)] = v[k] + ex;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kI; ++r) {
+        const int i = r * kB + tid;
+        if (base + i < n) out[base + i] = buf[pad(i)];
+    }
+}
+
+// ---- F3 duplicate ----
+__global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restrict__ gid_by_rank,
+                                                        const uint32_t* __restrict__ offsets,
+                                                        const uint32_t* __restrict__ tiles,
+                                                        const float4* __restrict__ rec, int P,
+                                                        int grid_x, int ty0, int ty1,
+                                                        uint32_t* __restrict__ inst_start,
+                                                        uint32_t* __restrict__ tkey,
+                                                        uint32_t* __restrict__ inst_gid) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= P) return;
+    const uint32_t g = gid_by_rank[r];
+    const uint32_t nt = tiles[g];
+    const uint32_t end = offsets[r];
+    uint32_t j = end - nt;
+    inst_start[g] = j;
+    if (nt == 0) return;
+    const float4 r2 = rec[3 * (size_t)g + 2];
+    const uint32_t rmin = __float_as_uint(r2.z), rmax = __float_as_uint(r2.w);
+    const int minx = rmin & 0xFFFF, miny = rmin >> 16, maxx = rmax & 0xFFFF, maxy = rmax >> 16;
+    const int y0 = miny > ty0 ? miny : ty0, y1 = maxy < ty1 ? maxy : ty1;
+    for (int y = y0; y < y1; ++y)
+        for (int x = minx; x < maxx; ++x) {
+            tkey[j] = (uint32_t)(y * grid_x + x);
+            inst_gid[j] = g;
+            ++j;
+        }
+}
+
+// ---- F5 finalize ----
+__global__ __launch_bounds__(256) void finalize_kernel(const uint32_t* __restrict__ stile,
+                                                       const uint32_t* __restrict__ sj,
+                                                       const uint32_t* __restrict__ inst_gid,
+                                                       long long K, uint32_t* __restrict__ sgid,
+                                                       uint2* __restrict__ ranges) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= K) return;
+    sgid[i] = inst_gid[sj[i]];
+    const uint32_t t = stile[i];
+    if (i == 0 || stile[i - 1] != t) ranges[t].x = (uint32_t)i;
+    if (i == K - 1 || stile[i + 1] != t) ranges[t].y = (uint32_t)(i + 1);
+}
+
+}  // namespace
+
+int radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* k0, uint32_t* v0,
+               uint32_t* k1, uint32_t* v1, long long n, int nbits, uint32_t* hist, int* which,
+               hipStream_t s) {
+    *which = -1;
+    if (n <= 0) return 0;
+    const int nb = sort_blocks(n);
+    uint32_t* totals = hist + (size_t)256 * (nb + 1);
+    const uint32_t* kin = keys_in;
+    const uint32_t* vin = vals_in;
+    int dst = 0;
+    for (int shift = 0; shift < nbits; shift += 8) {
+        const int bits = (nbits - shift) < 8 ? (nbits - shift) : 8;
+        uint32_t* ko = dst == 0 ? k0 : k1;
+        uint32_t* vo = dst == 0 ? v0 : v1;
+        hipLaunchKernelGGL(radix_upsweep, dim3(nb), dim3(kB), 0, s, kin, n, shift, bits, nb, hist);
+        hipLaunchKernelGGL(radix_colscan, dim3(256), dim3(kB), 0, s, hist, nb, totals);
+        hipLaunchKernelGGL(radix_downsweep, dim3(nb), dim3(kB), 0, s, kin, vin, ko, vo, n, shift, bits, nb,
+                           hist, totals);
+        kin = ko;
+        vin = vo;
+        *which = dst;
+        dst ^= 1;
+    }
+    return (int)hipGetLastError();
+}
+
+int inclusive_scan_gather(const uint32_t* in, const uint32_t* idx, uint32_t* out, int n,
+                          uint32_t* partials, hipStream_t s) {
+    if (n <= 0) return 0;
+    const int nb = sort_blocks(n);
+    hipLaunchKernelGGL(scan_reduce, dim3(nb), dim3(kB), 0, s, in, idx, n, partials);
+    hipLaunchKernelGGL(scan_partials, dim3(1), dim3(1024), 0, s, partials, nb);
+    hipLaunchKernelGGL(scan_downsweep, dim3(nb), dim3(kB), 0, s, in, idx, n, partials, out);
+    return (int)hipGetLastError();
+}
+
+int launch_duplicate(const uint32_t* gid_by_rank, const uint32_t* offsets, const uint32_t* tiles,
+                     const float4* rec, int P, int grid_x, int ty0, int ty1, uint32_t* inst_start,
+                     uint32_t* tkey, uint32_t* inst_gid, hipStream_t s) {
+    if (P <= 0) return 0;
+    hipLaunchKernelGGL(duplicate_kernel, dim3(div_up(P, 256)), dim3(256), 0, s, gid_by_rank, offsets,
+                       tiles, rec, P, grid_x, ty0, ty1, inst_start, tkey, inst_gid);
+    return (int)hipGetLastError();
+}
+
+int launch_finalize(const uint32_t* sorted_tile, const uint32_t* sorted_j, const uint32_t* inst_gid,
+                    long long K, uint32_t* sorted_gid, uint2* ranges, hipStream_t s) {
+    if (K <= 0) return 0;
+    hipLaunchKernelGGL(finalize_kernel, dim3(div_up(K, 256)), dim3(256), 0, s, sorted_tile, sorted_j,
+                       inst_gid, K, sorted_gid, ranges);
+    return (int)hipGetLastError();
+}
+
+}  // namespace gsr

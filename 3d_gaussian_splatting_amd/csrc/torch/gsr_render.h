@@ -1,0 +1,110 @@
+// gsr_render.h -- libtorch render() surface for the reference's C++ training loop.
+//
+// The reference (seiya-kumada/3d_gaussian_splatting) has no renderer; its loop body is a stub
+// at src/utils/train_utils.cpp:128-145.  This header gives that loop the call it is missing:
+//
+//     auto out = gsr::render(cam, *gaussians, pipeline_params, background);
+//     auto loss = l1(out.render, gt);  loss.backward();
+//
+// `Model` is the reference's GaussianModel (src/scene/gaussian_model.h): render() only uses
+// its public getters (get_xyz / get_opacity / get_scaling / get_rotation / get_covariance,
+// gaussian_model.h:85-90), get_core_params() for active_sh_degree_ and the raw SH leaves
+// (features_dc_ / features_rest_, gaussian_model.h:12-14 -- passed separately so the
+// get_features() cat copy, gaussian_model.cpp:289-292, is never made) and get_max_sh_degree().
+// `Pipe` is PipelineParams (src/arguments/params.h:93-106): convert_SHs_python_,
+// compute_cov3D_python_, debug_.
+#pragma once
+#include <torch/torch.h>
+
+#include <array>
+#include <optional>
+
+#include "gsr/gsr.h"
+
+namespace gsr {
+
+// POD view the rasterizer consumes (f32, column-major matrices: the reference Camera's
+// row-vector-convention tensors flattened row-major, src/scene/camera.cpp:66-71).
+struct RasterCamera {
+    int width = 0, height = 0;
+    float tanfovx = 0.f, tanfovy = 0.f;
+    std::array<float, 16> viewmatrix{};
+    std::array<float, 16> projmatrix{};
+    std::array<float, 3> campos{};
+    float znear = 0.01f, zfar = 100.f;
+
+    // From the reference Camera's device tensors (world_view_transform_, full_proj_transform_,
+    // camera_center_: camera.cpp:66-71) -- one host copy per camera, not per iteration.
+    static RasterCamera from_tensors(int width, int height, double FoVx, double FoVy,
+                                     const torch::Tensor& world_view_transform,
+                                     const torch::Tensor& full_proj_transform,
+                                     const torch::Tensor& camera_center);
+    gsr_camera to_c() const;
+};
+
+struct RasterSettings {
+    std::array<float, 3> bg{0.f, 0.f, 0.f};
+    float scale_modifier = 1.f;
+    int sh_degree = 0;
+    int tile_y0 = 0, tile_y1 = INT32_MAX;  // tile-row band (multi-GPU sharding)
+    bool debug = false;
+};
+
+struct RenderOutput {
+    torch::Tensor render;             // (3,H,W)
+    torch::Tensor viewspace_points;   // (P,3) zeros requiring grad: receives dL/dmeans2D
+    torch::Tensor visibility_filter;  // (P,) bool, radii > 0
+    torch::Tensor radii;              // (P,) int32
+};
+
+// Differentiable rasterization (RasterizeGaussians autograd Function).  Absent optional
+// inputs are undefined tensors.  Returns {color (3,H,W), radii (P,) int32}.
+std::vector<torch::Tensor> rasterize_gaussians(
+    const RasterCamera& cam, const RasterSettings& rs, const torch::Tensor& means3D,
+    const torch::Tensor& means2D, const torch::Tensor& sh_dc, const torch::Tensor& sh_rest,
+    const torch::Tensor& colors_precomp, const torch::Tensor& opacities, const torch::Tensor& scales,
+    const torch::Tensor& rotations, const torch::Tensor& cov3D_precomp);
+
+// torch-op SH evaluation (PipelineParams::convert_SHs_python_ path): colours for
+// directions (P,3) and coefficients (P,M,3) at degree D; +0.5 and clamp at 0 as in-kernel.
+torch::Tensor eval_sh_colors(int D, const torch::Tensor& sh, const torch::Tensor& dirs);
+
+template <class Model, class Pipe>
+RenderOutput render(const RasterCamera& cam, Model& pc, const Pipe& pipe, const torch::Tensor& bg,
+                    float scaling_modifier = 1.f,
+                    std::optional<torch::Tensor> override_color = std::nullopt) {
+    const auto& xyz = pc.get_xyz();
+    auto screenspace = torch::zeros_like(xyz).requires_grad_(true);
+    RasterSettings rs;
+    auto bgc = bg.to(torch::kCPU, torch::kFloat32).contiguous();
+    for (int c = 0; c < 3; ++c) rs.bg[c] = bgc.data_ptr<float>()[c];
+    rs.scale_modifier = scaling_modifier;
+    auto& core = pc.get_core_params();
+    rs.sh_degree = core.active_sh_degree_;
+    rs.debug = pipe.debug_;
+    torch::Tensor scales, rotations, cov3D, sh_dc, sh_rest, colors;
+    if (pipe.compute_cov3D_python_) {
+        cov3D = pc.get_covariance(scaling_modifier);
+    } else {
+        scales = pc.get_scaling();
+        rotations = pc.get_rotation();
+    }
+    if (override_color) {
+        colors = *override_color;
+    } else if (pipe.convert_SHs_python_) {
+        auto feats = pc.get_features();  // (P, M, 3)
+        auto cpos = torch::from_blob(const_cast<float*>(cam.campos.data()), {1, 3}, torch::kFloat32)
+                        .to(xyz.device());
+        auto dirs = xyz - cpos;
+        dirs = dirs / dirs.norm(2, 1, true);
+        colors = eval_sh_colors(core.active_sh_degree_, feats, dirs);
+    } else {
+        sh_dc = core.features_dc_;
+        sh_rest = core.features_rest_;
+    }
+    auto outs = rasterize_gaussians(cam, rs, xyz, screenspace, sh_dc, sh_rest, colors, pc.get_opacity(),
+                                    scales, rotations, cov3D);
+    return RenderOutput{outs[0], screenspace, outs[1] > 0, outs[1]};
+}
+
+}  // namespace gsr

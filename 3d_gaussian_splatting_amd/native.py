@@ -1,0 +1,157 @@
+"""Loader for the native libraries + a ctypes binding of the C ABI (include/gsr/gsr.h).
+
+Product path, no fallback: if lib/libgsr_hip.so or the libtorch extension is missing this
+module raises -- it never substitutes a CPU implementation.
+
+``CAbi`` is the ctypes stub a Python (or any FFI) caller binds: the parity tests drive the
+HIP kernels through it directly (gsr_forward / gsr_backward / gsr_backward_blend /
+gsr_backward_preprocess / gsr_view), with device memory owned by torch tensors.
+"""
+from __future__ import annotations
+
+import ctypes
+import importlib.machinery
+import importlib.util
+import os
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(PKG, "lib")
+HIP_LIB = os.path.join(LIB_DIR, "libgsr_hip.so")
+
+GSR_FLAG_DEBUG = 1
+GSR_GRAD2D_STRIDE = 12
+VIEW_SORTED_GID, VIEW_SORTED_TILE, VIEW_RANGES, VIEW_FINAL_T, VIEW_N_CONTRIB, VIEW_DEPTH_KEY, \
+    VIEW_TILES_TOUCHED, VIEW_RECORDS = range(1, 9)
+EXPORTS = ["gsr_abi_version", "gsr_last_error", "gsr_forward", "gsr_backward", "gsr_backward_blend",
+           "gsr_backward_preprocess", "gsr_view", "gsr_geom_bytes", "gsr_binning_bytes",
+           "gsr_image_bytes", "gsr_scratch_bytes", "gsr_profile_enable", "gsr_profile_read",
+           "gsr_stage_name"]
+STAGES = ["preprocess", "depth_sort", "scan", "duplicate", "tile_sort", "finalize", "blend_fwd", "blend_bwd",
+          "preprocess_bwd", "gather_grad2d", "misc"]
+
+
+class Camera(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("tanfovx", ctypes.c_float), ("tanfovy", ctypes.c_float),
+                ("viewmatrix", ctypes.c_float * 16), ("projmatrix", ctypes.c_float * 16),
+                ("campos", ctypes.c_float * 3)]
+
+
+class Gaussians(ctypes.Structure):
+    _fields_ = [("P", ctypes.c_int32), ("sh_degree", ctypes.c_int32), ("sh_rest_coeffs", ctypes.c_int32),
+                ("scale_modifier", ctypes.c_float)] + [
+        (n, ctypes.c_void_p) for n in ("means3D", "sh_dc", "sh_rest", "colors_precomp", "opacities",
+                                       "scales", "rotations", "cov3D_precomp")]
+
+
+class Settings(ctypes.Structure):
+    _fields_ = [("bg", ctypes.c_float * 3), ("tile_y0", ctypes.c_int32), ("tile_y1", ctypes.c_int32),
+                ("flags", ctypes.c_uint32)]
+
+
+class Grads(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in (
+        "dL_dmeans2D", "dL_dconic", "dL_dopacity", "dL_dcolors", "dL_dmeans3D", "dL_dsh_dc",
+        "dL_dsh_rest", "dL_dscales", "dL_drotations", "dL_dcov3D")]
+
+
+class Buffers(ctypes.Structure):
+    _fields_ = [("geom", ctypes.c_void_p), ("binning", ctypes.c_void_p), ("image", ctypes.c_void_p),
+                ("num_rendered", ctypes.c_int32)]
+
+
+ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+
+_hip = None
+_ext = None
+
+
+def hip_library_path() -> str:
+    return HIP_LIB
+
+
+def load_hip() -> ctypes.CDLL:
+    """dlopen libgsr_hip.so (after torch, so the process has ONE HIP runtime)."""
+    global _hip
+    if _hip is None:
+        import torch  # noqa: F401  (loads torch's libamdhip64.so.7 first)
+        if not os.path.exists(HIP_LIB):
+            raise RuntimeError(f"{HIP_LIB} missing: run __graft_entry__.build() (no CPU fallback)")
+        L = ctypes.CDLL(HIP_LIB, mode=ctypes.RTLD_GLOBAL)
+        vp, i32 = ctypes.c_void_p, ctypes.c_int32
+        L.gsr_abi_version.restype = ctypes.c_int
+        L.gsr_last_error.restype = ctypes.c_char_p
+        L.gsr_forward.restype = ctypes.c_int
+        L.gsr_forward.argtypes = [ctypes.POINTER(Camera), ctypes.POINTER(Gaussians), ctypes.POINTER(Settings),
+                                  vp, vp, ALLOC_FN, ALLOC_FN, ALLOC_FN, vp, ctypes.POINTER(Buffers), vp]
+        L.gsr_backward.restype = ctypes.c_int
+        L.gsr_backward.argtypes = [ctypes.POINTER(Camera), ctypes.POINTER(Gaussians), ctypes.POINTER(Settings),
+                                   ctypes.POINTER(Buffers), vp, ALLOC_FN, vp, ctypes.POINTER(Grads), vp]
+        L.gsr_backward_blend.restype = ctypes.c_int
+        L.gsr_backward_blend.argtypes = [ctypes.POINTER(Camera), ctypes.POINTER(Gaussians),
+                                         ctypes.POINTER(Settings), ctypes.POINTER(Buffers), vp, ALLOC_FN, vp,
+                                         vp, vp]
+        L.gsr_backward_preprocess.restype = ctypes.c_int
+        L.gsr_backward_preprocess.argtypes = [ctypes.POINTER(Camera), ctypes.POINTER(Gaussians),
+                                              ctypes.POINTER(Settings), ctypes.POINTER(Buffers), vp,
+                                              ctypes.POINTER(Grads), vp]
+        L.gsr_view.restype = vp
+        L.gsr_view.argtypes = [ctypes.POINTER(Camera), i32, ctypes.POINTER(Buffers), ctypes.c_int]
+        for n in ("gsr_geom_bytes", "gsr_binning_bytes", "gsr_scratch_bytes"):
+            getattr(L, n).restype = ctypes.c_size_t
+            getattr(L, n).argtypes = [i32]
+        L.gsr_profile_enable.restype = ctypes.c_int
+        L.gsr_profile_enable.argtypes = [ctypes.c_uint32]
+        L.gsr_profile_read.restype = ctypes.c_int
+        L.gsr_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32)]
+        L.gsr_stage_name.restype = ctypes.c_char_p
+        L.gsr_stage_name.argtypes = [ctypes.c_int]
+        L.gsr_image_bytes.restype = ctypes.c_size_t
+        L.gsr_image_bytes.argtypes = [i32, i32]
+        _hip = L
+    return _hip
+
+
+def load_torch_ext():
+    """Import lib/_gsr_torch*.so (the libtorch RasterizeGaussians layer)."""
+    global _ext
+    if _ext is None:
+        import torch  # noqa: F401
+        load_hip()
+        from . import _build
+        path = os.path.join(LIB_DIR, _build.torch_ext_name())
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run __graft_entry__.build() (no CPU fallback)")
+        loader = importlib.machinery.ExtensionFileLoader("_gsr_torch", path)
+        spec = importlib.util.spec_from_file_location("_gsr_torch", path, loader=loader)
+        mod = importlib.util.module_from_spec(spec)
+        loader.exec_module(mod)
+        _ext = mod
+    return _ext
+
+
+def camera_struct(cam) -> Camera:
+    c = Camera()
+    c.width, c.height = int(cam.width), int(cam.height)
+    c.tanfovx, c.tanfovy = float(cam.tanfovx), float(cam.tanfovy)
+    c.viewmatrix[:] = [float(v) for v in cam.viewmatrix]
+    c.projmatrix[:] = [float(v) for v in cam.projmatrix]
+    c.campos[:] = [float(v) for v in cam.campos]
+    return c
+
+
+def profile_enable(mask: int = (1 << len(STAGES)) - 1) -> None:
+    load_hip().gsr_profile_enable(mask)
+
+
+def profile_read() -> dict:
+    """{stage: (total_ms, launches)} accumulated since profile_enable (syncs the events)."""
+    L = load_hip()
+    ms = (ctypes.c_double * len(STAGES))()
+    cnt = (ctypes.c_uint32 * len(STAGES))()
+    L.gsr_profile_read(ms, cnt)
+    return {STAGES[i]: (float(ms[i]), int(cnt[i])) for i in range(len(STAGES))}
+
+
+def last_error() -> str:
+    return load_hip().gsr_last_error().decode()

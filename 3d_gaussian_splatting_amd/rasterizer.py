@@ -1,0 +1,255 @@
+"""Python mirror of the rasterizer surface.
+
+Two entry points, both ending in the same HIP kernels:
+
+* ``CAbiRasterizer`` -- drives the C ABI (include/gsr/gsr.h) through ctypes with torch-owned
+  device memory: what a ctypes / cgo / JNI binding of libgsr_hip.so looks like.  The GPU parity
+  tests and bench.py use it so every call crosses the C boundary.
+* ``render()`` / ``rasterize_gaussians()`` -- the libtorch RasterizeGaussians autograd Function
+  (lib/_gsr_torch*.so), i.e. the C++ render() surface (csrc/torch/gsr_render.h) the
+  reference's training loop would call at src/utils/train_utils.cpp:137-144.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import torch
+
+from . import native
+from .graphics import RasterCamera
+
+INT32_MAX = 2**31 - 1
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _f32(t, shape=None, device=None):
+    if t is None:
+        return None
+    t = torch.as_tensor(t, dtype=torch.float32, device=device)
+    if shape is not None:
+        t = t.reshape(shape)
+    return t.contiguous()
+
+
+class _Allocator:
+    """Allocation callbacks for the C ABI: uint8 tensors kept alive by the owner."""
+
+    def __init__(self, device):
+        self.device = device
+        self.tensors = []
+        self.cb = native.ALLOC_FN(self._alloc)
+
+    def _alloc(self, _ctx, nbytes):
+        t = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=self.device)
+        self.tensors.append(t)
+        return t.data_ptr()
+
+
+@dataclass
+class ForwardState:
+    cam: RasterCamera
+    inputs: dict
+    settings: native.Settings
+    gauss: native.Gaussians
+    buffers: native.Buffers
+    color: torch.Tensor
+    radii: torch.Tensor
+    allocs: list = field(default_factory=list)
+
+    @property
+    def num_rendered(self) -> int:
+        return int(self.buffers.num_rendered)
+
+    def _owner(self, ptr: int):
+        for a in self.allocs:
+            for t in a.tensors:
+                base = t.data_ptr()
+                if base <= ptr < base + t.numel():
+                    return t, ptr - base
+        raise KeyError("pointer not inside a forward buffer")
+
+    def view(self, what: int, dtype: torch.dtype, count: int) -> torch.Tensor:
+        """Copy of an internal array (gsr_view) as a torch tensor."""
+        L = native.load_hip()
+        c = native.camera_struct(self.cam)
+        p = L.gsr_view(ctypes.byref(c), self.gauss.P, ctypes.byref(self.buffers), what)
+        if not p or count == 0:
+            return torch.empty(0, dtype=dtype, device=self.color.device)
+        t, off = self._owner(p)
+        nbytes = count * torch.empty(0, dtype=dtype).element_size()
+        return t[off:off + nbytes].view(dtype).clone()
+
+
+class CAbiRasterizer:
+    """Thin ctypes front-end of gsr_forward / gsr_backward*."""
+
+    def __init__(self, device="cuda"):
+        self.device = torch.device(device)
+        self.L = native.load_hip()
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise RuntimeError(f"{what} failed ({rc}): {native.last_error()}")
+
+    def forward(self, cam: RasterCamera, means3D, opacities, scales=None, rotations=None, sh_dc=None,
+                sh_rest=None, sh_degree=0, colors_precomp=None, cov3D_precomp=None, scale_modifier=1.0,
+                bg=(0.0, 0.0, 0.0), tile_rows=None, debug=False) -> ForwardState:
+        dev = self.device
+        means3D = _f32(means3D, device=dev)
+        P = int(means3D.shape[0])
+        inputs = dict(means3D=means3D.reshape(P, 3), opacities=_f32(opacities, (P,), dev),
+                      scales=_f32(scales, (P, 3), dev) if scales is not None else None,
+                      rotations=_f32(rotations, (P, 4), dev) if rotations is not None else None,
+                      sh_dc=_f32(sh_dc, (P, 1, 3), dev) if sh_dc is not None else None,
+                      sh_rest=_f32(sh_rest, device=dev) if sh_rest is not None else None,
+                      colors_precomp=_f32(colors_precomp, (P, 3), dev) if colors_precomp is not None else None,
+                      cov3D_precomp=_f32(cov3D_precomp, (P, 6), dev) if cov3D_precomp is not None else None)
+        if inputs["sh_rest"] is not None:
+            inputs["sh_rest"] = inputs["sh_rest"].reshape(P, -1, 3).contiguous()
+            if inputs["sh_rest"].shape[1] == 0:
+                inputs["sh_rest"] = None
+        g = native.Gaussians()
+        g.P, g.sh_degree, g.scale_modifier = P, int(sh_degree), float(scale_modifier)
+        g.sh_rest_coeffs = 0 if inputs["sh_rest"] is None else int(inputs["sh_rest"].shape[1])
+        for k in ("means3D", "sh_dc", "sh_rest", "colors_precomp", "opacities", "scales", "rotations",
+                  "cov3D_precomp"):
+            setattr(g, k, None if inputs[k] is None else inputs[k].data_ptr())
+        s = native.Settings()
+        s.bg[:] = [float(v) for v in bg]
+        s.tile_y0, s.tile_y1 = (0, INT32_MAX) if tile_rows is None else (int(tile_rows[0]), int(tile_rows[1]))
+        s.flags = native.GSR_FLAG_DEBUG if debug else 0
+        color = torch.empty((3, cam.height, cam.width), dtype=torch.float32, device=dev)
+        radii = torch.empty((P,), dtype=torch.int32, device=dev)
+        ag, ab, ai = _Allocator(dev), _Allocator(dev), _Allocator(dev)
+        bufs = native.Buffers()
+        c = native.camera_struct(cam)
+        rc = self.L.gsr_forward(ctypes.byref(c), ctypes.byref(g), ctypes.byref(s), _ptr(color),
+                                _ptr(radii) if P else None, ag.cb, ab.cb, ai.cb, None, ctypes.byref(bufs),
+                                self._stream())
+        self._check(rc, "gsr_forward")
+        return ForwardState(cam=cam, inputs=inputs, settings=s, gauss=g, buffers=bufs, color=color,
+                            radii=radii, allocs=[ag, ab, ai])
+
+    def _grad_tensors(self, st: ForwardState):
+        P = st.gauss.P
+        dev = self.device
+        e = lambda *shape: torch.empty(shape, dtype=torch.float32, device=dev)
+        out = dict(means2D=e(P, 3), conic=e(P, 3), opacities=e(P, 1), means3D=e(P, 3))
+        inp = st.inputs
+        if inp["colors_precomp"] is not None:
+            out["colors"] = e(P, 3)
+        else:
+            out["sh_dc"] = e(P, 1, 3)
+            if inp["sh_rest"] is not None:
+                out["sh_rest"] = torch.empty_like(inp["sh_rest"])
+        if inp["cov3D_precomp"] is not None:
+            out["cov3D"] = e(P, 6)
+        else:
+            out["scales"], out["rotations"] = e(P, 3), e(P, 4)
+        gg = native.Grads()
+        names = dict(means2D="dL_dmeans2D", conic="dL_dconic", opacities="dL_dopacity", colors="dL_dcolors",
+                     means3D="dL_dmeans3D", sh_dc="dL_dsh_dc", sh_rest="dL_dsh_rest", scales="dL_dscales",
+                     rotations="dL_drotations", cov3D="dL_dcov3D")
+        for k, v in out.items():
+            setattr(gg, names[k], v.data_ptr())
+        return out, gg
+
+    def backward(self, st: ForwardState, dL_dpix) -> dict:
+        dpix = _f32(dL_dpix, (3, st.cam.height, st.cam.width), self.device)
+        out, gg = self._grad_tensors(st)
+        scratch = _Allocator(self.device)
+        c = native.camera_struct(st.cam)
+        rc = self.L.gsr_backward(ctypes.byref(c), ctypes.byref(st.gauss), ctypes.byref(st.settings),
+                                 ctypes.byref(st.buffers), _ptr(dpix), scratch.cb, None, ctypes.byref(gg),
+                                 self._stream())
+        self._check(rc, "gsr_backward")
+        return out
+
+    def backward_blend(self, st: ForwardState, dL_dpix) -> torch.Tensor:
+        dpix = _f32(dL_dpix, (3, st.cam.height, st.cam.width), self.device)
+        grad2d = torch.empty((st.gauss.P, native.GSR_GRAD2D_STRIDE), dtype=torch.float32, device=self.device)
+        scratch = _Allocator(self.device)
+        c = native.camera_struct(st.cam)
+        rc = self.L.gsr_backward_blend(ctypes.byref(c), ctypes.byref(st.gauss), ctypes.byref(st.settings),
+                                       ctypes.byref(st.buffers), _ptr(dpix), scratch.cb, None, _ptr(grad2d),
+                                       self._stream())
+        self._check(rc, "gsr_backward_blend")
+        return grad2d
+
+    def backward_preprocess(self, st: ForwardState, grad2d: torch.Tensor) -> dict:
+        out, gg = self._grad_tensors(st)
+        grad2d = grad2d.contiguous()
+        c = native.camera_struct(st.cam)
+        rc = self.L.gsr_backward_preprocess(ctypes.byref(c), ctypes.byref(st.gauss), ctypes.byref(st.settings),
+                                            ctypes.byref(st.buffers), _ptr(grad2d), ctypes.byref(gg),
+                                            self._stream())
+        self._check(rc, "gsr_backward_preprocess")
+        return out
+
+
+# ------------------------------------------------------------------------------------------
+# autograd surface (libtorch extension)
+# ------------------------------------------------------------------------------------------
+def ext_camera(cam: RasterCamera):
+    ext = native.load_torch_ext()
+    return ext.RasterCamera(cam.width, cam.height, float(cam.tanfovx), float(cam.tanfovy),
+                            [float(v) for v in cam.viewmatrix], [float(v) for v in cam.projmatrix],
+                            [float(v) for v in cam.campos])
+
+
+def rasterize_gaussians(cam: RasterCamera, means3D, means2D, opacities, sh_dc=None, sh_rest=None,
+                        colors_precomp=None, scales=None, rotations=None, cov3D_precomp=None,
+                        sh_degree=0, scale_modifier=1.0, bg=(0.0, 0.0, 0.0), tile_rows=None, debug=False):
+    """RasterizeGaussians.apply: returns (color (3,H,W), radii (P,) int32); differentiable in
+    every tensor input (means2D receives the screen-space gradient)."""
+    ext = native.load_torch_ext()
+    y0, y1 = (0, INT32_MAX) if tile_rows is None else tile_rows
+    rs = ext.RasterSettings([float(v) for v in bg], float(scale_modifier), int(sh_degree), int(y0), int(y1),
+                            bool(debug))
+    return ext.rasterize_gaussians(ext_camera(cam), rs, means3D, means2D, sh_dc, sh_rest, colors_precomp,
+                                   opacities, scales, rotations, cov3D_precomp)
+
+
+@dataclass
+class PipelineParams:
+    """Mirror of src/arguments/params.h:93-106."""
+    convert_SHs_python: bool = False
+    compute_cov3D_python: bool = False
+    debug: bool = False
+
+
+def render(viewpoint_camera: RasterCamera, pc, pipe: PipelineParams, bg_color, scaling_modifier=1.0,
+           override_color=None) -> dict:
+    """render(): same contract as the C++ gsr::render template (csrc/torch/gsr_render.h) for a
+    model exposing the reference GaussianModel getters (see model.GaussianModel)."""
+    from .general import eval_sh
+    xyz = pc.get_xyz
+    screenspace = torch.zeros_like(xyz, requires_grad=True)
+    bg = [float(v) for v in torch.as_tensor(bg_color).flatten().tolist()]
+    scales = rotations = cov3D = sh_dc = sh_rest = colors = None
+    if pipe.compute_cov3D_python:
+        cov3D = pc.get_covariance(scaling_modifier)
+    else:
+        scales, rotations = pc.get_scaling, pc.get_rotation
+    if override_color is not None:
+        colors = override_color
+    elif pipe.convert_SHs_python:
+        campos = torch.as_tensor(viewpoint_camera.campos, device=xyz.device)
+        dirs = xyz - campos
+        dirs = dirs / dirs.norm(dim=1, keepdim=True)
+        colors = torch.clamp_min(eval_sh(pc.active_sh_degree, pc.get_features, dirs) + 0.5, 0.0)
+    else:
+        sh_dc, sh_rest = pc.features_dc, pc.features_rest
+    color, radii = rasterize_gaussians(viewpoint_camera, xyz, screenspace, pc.get_opacity, sh_dc=sh_dc,
+                                       sh_rest=sh_rest, colors_precomp=colors, scales=scales,
+                                       rotations=rotations, cov3D_precomp=cov3D,
+                                       sh_degree=0 if colors is not None else pc.active_sh_degree,
+                                       scale_modifier=scaling_modifier, bg=bg, debug=pipe.debug)
+    return dict(render=color, viewspace_points=screenspace, visibility_filter=radii > 0, radii=radii)

@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Benchmark: forward+backward of the MI355X 3DGS rasterizer (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1m_1080p|100k_800|5m_1080p]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One step = gsr_forward + gsr_backward (through the C ABI) of the whole synthetic scene:
+1M Gaussians, 1920x1080, SH degree 3 (BASELINE configs[2], the roofline run; inputs already
+resident in HBM).  N > 1: screen-space tile-row bands, one per rank (RCCL): replicated
+preprocess, band-local binning/blend, all-gather of the image bands, blend-backward on the
+band, all-reduce of the per-Gaussian 2D gradients, replicated preprocess-backward.  The
+whole image is rendered once per step for the job, so value = steps/s of the job
+("scaling": "strong").  Rank 0 prints ONE JSON line.
+
+roofline: the dominant kernel's algorithmic HBM bytes (SURVEY §8d formulas) per
+launch / its mean launch time from HIP events recorded on the launch stream over the timed
+region (gsr_profile_*), against 8.0 TB/s.  cpu_baseline: the CPU oracle (oracle/, a C port
+of the same algorithm) timed on this host's cores for ONE forward+backward of the same
+workload (rank 0, N = 1), which also gives the PSNR / gradient error of the GPU result.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+PKG = "3d_gaussian_splatting_amd"
+gr = importlib.import_module(f"{PKG}.graphics")
+sc = importlib.import_module(f"{PKG}.scene")
+R = importlib.import_module(f"{PKG}.rasterizer")
+native = importlib.import_module(f"{PKG}.native")
+
+CONFIGS = {
+    "1k_256": dict(P=1_000, W=256, H=256, D=0),
+    "100k_800": dict(P=100_000, W=800, H=800, D=3),
+    "1m_1080p": dict(P=1_000_000, W=1920, H=1080, D=3),
+    "5m_1080p": dict(P=5_000_000, W=1920, H=1080, D=3),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def algorithmic_bytes(P, V, K, pix, tiles, M):
+    """SURVEY §8d compulsory traffic per stage (bytes), M = (D+1)^2 SH coefficients."""
+    return {
+        "preprocess": P * (44 + 8) + V * (12 * M + 40),
+        "scan": P * 8,
+        "duplicate": V * 20 + K * 12,
+        "tile_sort": K * 24,
+        "finalize": K * 8 + tiles * 8,
+        "blend_fwd": tiles * 8 + K * 40 + pix * 20,
+        "blend_bwd": tiles * 8 + K * 40 + pix * 20 + V * 36,
+        "preprocess_bwd": V * (80 + 12 * M) + P * (60 + 12 * M),
+    }
+
+
+def pmc_traffic(kernel_prefix):
+    """HBM bytes per launch of `kernel_prefix` from the committed rocprofv3 PMC passes
+    (profiles/*pmc*.json written by tools/pmc_summary.py), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        data = json.load(fh)
+    for name, rec in data.get("kernels", {}).items():
+        if kernel_prefix in name:
+            return rec.get("hbm_bytes_per_launch")
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="1m_1080p", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stage-events", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    cfg = CONFIGS[args.config]
+    P, W, H, D = cfg["P"], cfg["W"], cfg["H"], cfg["D"]
+    cam = gr.synthetic_camera(W, H)
+    scene = sc.make_scene(cam, P, max_sh_degree=max(D, 0), seed=0)
+    dpix_np = sc.make_dL_dpix(cam, seed=1)
+    rast = R.CAbiRasterizer(dev)
+    t = lambda a: torch.tensor(a, device=dev)
+    inputs = dict(means3D=t(scene.means3D), opacities=t(scene.opacities), scales=t(scene.scales),
+                  rotations=t(scene.rotations), sh_dc=t(scene.sh_dc), sh_rest=t(scene.sh_rest))
+    dpix = t(dpix_np)
+    gx, gy = cam.grid
+    if world > 1:
+        rows = [(r * gy) // world for r in range(world + 1)]
+        band = (rows[rank], rows[rank + 1])
+        band_px = max(rows[i + 1] - rows[i] for i in range(world)) * 16
+        gather_buf = torch.zeros((world, 3, band_px, W), device=dev)
+    else:
+        band = None
+
+    def step():
+        st = rast.forward(cam, **inputs, sh_degree=D, tile_rows=band)
+        if world > 1:
+            y0, y1 = band[0] * 16, min(band[1] * 16, H)
+            mine = torch.zeros((3, band_px, W), device=dev)
+            mine[:, :y1 - y0] = st.color[:, y0:y1]
+            dist.all_gather_into_tensor(gather_buf.view(-1), mine.view(-1))
+            g2 = rast.backward_blend(st, dpix)
+            dist.all_reduce(g2)
+            g = rast.backward_preprocess(st, g2)
+        else:
+            g = rast.backward(st, dpix)
+        return st, g
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    if not args.no_stage_events:
+        native.profile_enable()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st, g = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    stages = native.profile_read() if not args.no_stage_events else {}
+    if dist:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    ms_per_step = 1e3 * elapsed / args.steps
+    value = args.steps / elapsed  # whole-image forward+backward iterations per second (job)
+
+    K = st.num_rendered
+    V = int((st.radii > 0).sum())
+    tiles = gx * gy
+    M = (D + 1) ** 2
+    if world > 1:  # K is band-local; count the band's pixels and tiles
+        pix_local = (min(band[1] * 16, H) - band[0] * 16) * W
+        tiles_local = (band[1] - band[0]) * gx
+    else:
+        pix_local, tiles_local = W * H, tiles
+    alg = algorithmic_bytes(P, V, K, pix_local, tiles_local, M)
+    result = {
+        "metric": "forward+backward iters/s at 1080p, 1M Gaussians; PSNR vs CPU ref",
+        "value": round(value, 3), "unit": "iters/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"{args.config}: {P} Gaussians, {W}x{H}, SH degree {D}, fwd+bwd",
+                   "gaussians": P, "width": W, "height": H, "sh_degree": D,
+                   "parallelism": f"tile-row bands x{world}" if world > 1 else "single GPU"},
+        "mpixel_per_s": round(W * H * value / 1e6, 2),
+        "counts": {"visible": V, "num_rendered": K, "tiles": tiles},
+    }
+    if stages and rank == 0:
+        per = {k: (ms / max(n, 1), n // args.steps if args.steps else 0) for k, (ms, n) in stages.items() if n}
+        result["stage_ms"] = {k: round(ms / args.steps, 4) for k, (ms, n) in stages.items() if n}
+        cand = {k: v for k, v in per.items() if k in alg}
+        dom = max(cand, key=lambda k: cand[k][0] * max(cand[k][1], 1))
+        mean_ms = per[dom][0]
+        launches_per_stage = max(per[dom][1], 1)
+        bytes_launch = alg[dom] / launches_per_stage
+        achieved = bytes_launch / (mean_ms * 1e-3) / 1e9
+        kernel_name = {"blend_fwd": "blend_forward_kernel", "blend_bwd": "blend_backward_kernel",
+                       "preprocess": "preprocess_kernel", "preprocess_bwd": "preprocess_backward_kernel"}.get(dom, dom)
+        traffic = pmc_traffic(kernel_name)
+        result["roofline"] = {"bound": "hbm", "kernel": kernel_name, "achieved": round(achieved, 2),
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                              "traffic": traffic, "mean_launch_ms": round(mean_ms, 4),
+                              "algorithmic_bytes_per_launch": int(bytes_launch)}
+        total_alg = sum(alg.values())
+        result["pipeline_roofline"] = {
+            "algorithmic_bytes_per_step": int(total_alg),
+            "achieved_GBs": round(total_alg / (ms_per_step * 1e-3) / 1e9, 2),
+            "frac_of_8TBs": round(total_alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import gsr_oracle  # cpu_baseline leg only: the checker / reported baseline
+        cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        os.environ.setdefault("OMP_NUM_THREADS", str(cores))
+        c0 = time.perf_counter()
+        f = gsr_oracle.forward(cam, scene.means3D, scene.opacities, scene.scales, scene.rotations, scene.sh_dc,
+                               scene.sh_rest, sh_degree=D)
+        gc = f.state.backward(dpix_np)
+        cpu_s = time.perf_counter() - c0
+        col = st.color.cpu().numpy().astype(np.float64)
+        mse = float(np.mean((col - f.color) ** 2))
+        rel = {}
+        for k in ("means3D", "opacities", "scales", "rotations", "sh_dc", "sh_rest"):
+            a = g[k].cpu().numpy().reshape(gc[k].shape).astype(np.float64)
+            rel[k] = float(np.linalg.norm(a - gc[k]) / max(np.linalg.norm(gc[k]), 1e-30))
+        result["cpu_baseline"] = {"value": round(1.0 / cpu_s, 5), "unit": "iters/s", "cores": cores,
+                                  "kind": "port", "sample": f"1 forward+backward of the full {args.config} "
+                                  f"workload on the CPU oracle ({cpu_s:.2f} s, OpenMP {cores} threads)"}
+        result["parity"] = {"psnr_db_vs_cpu": round(10 * math.log10(1.0 / mse), 2) if mse > 0 else float("inf"),
+                            "rgb_rel_l2": float(np.linalg.norm(col - f.color) / np.linalg.norm(f.color)),
+                            "grad_rel_l2_max": max(rel.values()),
+                            "num_rendered_equal": int(f.num_rendered) == K}
+    if rank == 0:
+        print(json.dumps(result))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
