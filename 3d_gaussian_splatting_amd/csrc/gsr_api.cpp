@@ -248,7 +248,7 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
 
     long long K = 0;
     if (P > 0) {
-        PreOut po{radii, depth_key, tiles, flags, rec};
+        PreOut po{radii, depth_key, tiles, flags, rec, at<uint2>(bufs->geom, gl.rect)};
         GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess(*cam, gauss_in(gs), ty0, ty1, po, stream), "preprocess");
         int which = -1;
         GSR_STAGE(GSR_STAGE_DEPTH_SORT, radix_sort(depth_key, nullptr, at<uint32_t>(bufs->geom, gl.sB_k),
@@ -277,7 +277,7 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
         uint32_t* vB = at<uint32_t>(bufs->binning, bl.vB);
         uint32_t* inst_gid = at<uint32_t>(bufs->binning, bl.inst_gid);
         uint32_t* sorted_gid = at<uint32_t>(bufs->binning, bl.sorted_gid);
-        GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate(gid_by_rank, offsets, tiles, rec, P, gx, ty0, ty1, inst_start, kA,
+        GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate(gid_by_rank, offsets, tiles, at<uint2>(bufs->geom, gl.rect), P, gx, ty0, ty1, inst_start, kA,
                                        inst_gid, stream),
                       "duplicate");
         if (K > 0) {

@@ -65,6 +65,22 @@ struct BlendGeom {
     float bg0, bg1, bg2;
 };
 
+// Which of the tile's four 16x4 pixel stripes (slot p = rows 4p..4p+3) the record's
+// alpha >= 1/255 footprint box can touch.  Exact culling: a pixel outside the (padded) box
+// fails the alpha test, so skipping it changes no output bit.
+__device__ inline uint32_t stripe_mask(const float4 r0, const float4 r2, float bx0, float by0) {
+    const float ex = r2.y, ey = r2.z;
+    if (!(ex >= 0.0f) || r0.x + ex < bx0 || r0.x - ex > bx0 + 15.0f) return 0u;
+    const float ylo = r0.y - ey, yhi = r0.y + ey;
+    uint32_t m = 0;
+#pragma unroll
+    for (int p = 0; p < kPPL; ++p) {
+        const float s0 = by0 + 4.0f * p;
+        m |= (yhi >= s0 && ylo <= s0 + 3.0f) ? (1u << p) : 0u;
+    }
+    return m;
+}
+
 __global__ __launch_bounds__(64) void blend_forward_kernel(const BlendGeom geo,
                                                            const uint2* __restrict__ ranges,
                                                            const uint32_t* __restrict__ sorted_gid,
@@ -78,6 +94,7 @@ __global__ __launch_bounds__(64) void blend_forward_kernel(const BlendGeom geo,
     const int lane = threadIdx.x;
     const int px = tx * kTile + (lane & 15);
     const float pfx = (float)px;
+    const float bx0 = (float)(tx * kTile), by0 = (float)(ty * kTile);
     float pfy[kPPL], T[kPPL], C0[kPPL], C1[kPPL], C2[kPPL];
     uint32_t last[kPPL];
     bool done[kPPL];
@@ -93,48 +110,55 @@ __global__ __launch_bounds__(64) void blend_forward_kernel(const BlendGeom geo,
     const uint2 range = ranges[tile];
     const int n = (int)(range.y - range.x);
     for (int base = 0; base < n; base += 64) {
-        bool alldone = true;
+        uint32_t live = 0;  // stripes with at least one unfinished pixel (wave-uniform)
 #pragma unroll
-        for (int p = 0; p < kPPL; ++p) alldone &= done[p];
-        if (__all(alldone)) break;
+        for (int p = 0; p < kPPL; ++p) live |= __all(done[p]) ? 0u : (1u << p);
+        if (live == 0) break;
+        uint32_t smask = 0;
         if (base + lane < n) {
             const uint32_t g = sorted_gid[range.x + base + lane];
             const float4* r = rec + 3 * (size_t)g;
-            srec[3 * lane + 0] = r[0];
-            srec[3 * lane + 1] = r[1];
-            srec[3 * lane + 2] = r[2];
+            const float4 r0 = r[0], r1 = r[1], r2 = r[2];
+            srec[3 * lane + 0] = r0;
+            srec[3 * lane + 1] = r1;
+            srec[3 * lane + 2] = r2;
+            smask = stripe_mask(r0, r2, bx0, by0);
         }
         __syncthreads();
-        const int cnt = (n - base) < 64 ? (n - base) : 64;
-        for (int k = 0; k < cnt; ++k) {
-            const float4 r0 = srec[3 * k + 0];  // x, y, A, B
-            const float4 r1 = srec[3 * k + 1];  // C, opacity, r, g
-            const float4 r2 = srec[3 * k + 2];  // b, depth, rect
+        uint64_t todo = __ballot((smask & live) != 0u);
+        int visited = 0;
+        while (todo) {
+            const int k = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)smask, k) & live;
+            const float4 r0 = srec[3 * k + 0];  // x, y, a', b'
+            const float4 r1 = srec[3 * k + 1];  // c', opacity, r, g
+            const float rb = srec[3 * k + 2].x; // b
+            const uint32_t idx = (uint32_t)(base + k + 1);
 #pragma unroll
             for (int p = 0; p < kPPL; ++p) {
-                if (done[p]) continue;
+                if (!(m & (1u << p))) continue;  // wave-uniform
                 const float dx = r0.x - pfx, dy = r0.y - pfy[p];
-                const float power = -0.5f * (r0.z * dx * dx + r1.x * dy * dy) - r0.w * dx * dy;
-                if (power > 0.0f) continue;
-                const float alpha = fminf(0.99f, r1.y * __expf(power));
-                if (alpha < 1.0f / 255.0f) continue;
-                const float test_T = T[p] * (1.0f - alpha);
-                if (test_T < 0.0001f) {
-                    done[p] = true;
-                    continue;
-                }
-                const float w = alpha * T[p];
-                C0[p] += r1.z * w;
-                C1[p] += r1.w * w;
-                C2[p] += r2.x * w;
-                T[p] = test_T;
-                last[p] = (uint32_t)(base + k + 1);
+                const float pw = fmaf(r0.z * dx, dx, fmaf(r0.w * dx, dy, r1.x * dy * dy));
+                const float alpha = fminf(0.99f, r1.y * __builtin_amdgcn_exp2f(pw));
+                const bool valid = !done[p] && pw <= 0.0f && alpha >= (1.0f / 255.0f);
+                const float tT = T[p] * (1.0f - alpha);
+                const bool term = valid && tT < 0.0001f;
+                const bool contrib = valid && !term;
+                done[p] = done[p] || term;
+                const float w = contrib ? alpha * T[p] : 0.0f;
+                C0[p] = fmaf(r1.z, w, C0[p]);
+                C1[p] = fmaf(r1.w, w, C1[p]);
+                C2[p] = fmaf(rb, w, C2[p]);
+                T[p] = contrib ? tT : T[p];
+                last[p] = contrib ? idx : last[p];
             }
-            if ((k & 7) == 7) {
-                bool ad = true;
+            if ((++visited & 7) == 0) {
+                uint32_t lv = 0;
 #pragma unroll
-                for (int p = 0; p < kPPL; ++p) ad &= done[p];
-                if (__all(ad)) break;
+                for (int p = 0; p < kPPL; ++p) lv |= __all(done[p]) ? 0u : (1u << p);
+                live = lv;
+                if (live == 0) break;
             }
         }
         __syncthreads();
@@ -170,25 +194,26 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
     const int lane = threadIdx.x;
     const int px = tx * kTile + (lane & 15);
     const float pfx = (float)px;
+    const float bx0 = (float)(tx * kTile), by0 = (float)(ty * kTile);
     const size_t npix = (size_t)geo.W * geo.H;
-    const float ddelx_dx = 0.5f * (float)geo.W, ddely_dy = 0.5f * (float)geo.H;
-    float pfy[kPPL], T[kPPL], Tf[kPPL], dp0[kPPL], dp1[kPPL], dp2[kPPL], bgd[kPPL];
+    const float hw = 0.5f * (float)geo.W, hh = 0.5f * (float)geo.H;
+    // per-pixel state (4 pixels per lane)
+    float T[kPPL], dp0[kPPL], dp1[kPPL], dp2[kPPL], cbg[kPPL];
     float ac0[kPPL], ac1[kPPL], ac2[kPPL], lc0[kPPL], lc1[kPPL], lc2[kPPL], la[kPPL];
     uint32_t lastc[kPPL];
     uint32_t maxlast = 0;
 #pragma unroll
     for (int p = 0; p < kPPL; ++p) {
         const int py = ty * kTile + (lane >> 4) + 4 * p;
-        pfy[p] = (float)py;
         const bool in = px < geo.W && py < geo.H;
         const size_t pix = in ? (size_t)py * geo.W + px : 0;
-        Tf[p] = in ? final_T[pix] : 1.0f;
-        T[p] = Tf[p];
+        const float Tf = in ? final_T[pix] : 1.0f;
+        T[p] = Tf;
         lastc[p] = in ? n_contrib[pix] : 0u;
         dp0[p] = in ? dL_dpix[pix] : 0.0f;
         dp1[p] = in ? dL_dpix[npix + pix] : 0.0f;
         dp2[p] = in ? dL_dpix[2 * npix + pix] : 0.0f;
-        bgd[p] = geo.bg0 * dp0[p] + geo.bg1 * dp1[p] + geo.bg2 * dp2[p];
+        cbg[p] = -Tf * (geo.bg0 * dp0[p] + geo.bg1 * dp1[p] + geo.bg2 * dp2[p]);
         ac0[p] = ac1[p] = ac2[p] = lc0[p] = lc1[p] = lc2[p] = la[p] = 0.0f;
         maxlast = maxlast > lastc[p] ? maxlast : lastc[p];
     }
@@ -198,82 +223,89 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
     for (int top = n; top > 0; top -= 64) {
         const int lo = top > 64 ? top - 64 : 0;
         const int cnt = top - lo;
-        const int e_l = top - 1 - lane;  // entry of this lane's batch slot (descending)
-        uint32_t jl = 0;
+        const int e_l = top - 1 - lane;  // this lane's entry (descending)
+        uint32_t jl = 0, smask = 0;
         if (lane < cnt) {
             jl = sorted_j[range.x + e_l];
             if (e_l < (int)maxlast) {
                 const uint32_t g = sorted_gid[range.x + e_l];
                 const float4* r = rec + 3 * (size_t)g;
-                srec[3 * lane + 0] = r[0];
-                srec[3 * lane + 1] = r[1];
-                srec[3 * lane + 2] = r[2];
+                const float4 r0 = r[0], r1 = r[1], r2 = r[2];
+                srec[3 * lane + 0] = r0;
+                srec[3 * lane + 1] = r1;
+                srec[3 * lane + 2] = r2;
+                smask = stripe_mask(r0, r2, bx0, by0);
             }
         }
         sout[3 * lane + 0] = make_float4(0.f, 0.f, 0.f, 0.f);
         sout[3 * lane + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
         sout[3 * lane + 2] = make_float4(0.f, 0.f, 0.f, 0.f);
         __syncthreads();
-        if (lo < (int)maxlast) {
-            const int kstart = top > (int)maxlast ? top - (int)maxlast : 0;
-            for (int k = kstart; k < cnt; ++k) {
-                const uint32_t e = (uint32_t)(top - 1 - k);
-                const float4 r0 = srec[3 * k + 0];
-                const float4 r1 = srec[3 * k + 1];
-                const float4 r2 = srec[3 * k + 2];
-                float gmx = 0.f, gmy = 0.f, gA = 0.f, gB = 0.f, gC = 0.f, go = 0.f, gr = 0.f, gg = 0.f,
-                      gb = 0.f;
-                bool any = false;
+        uint64_t todo = __ballot(smask != 0u);
+        while (todo) {
+            const int k = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)smask, k);
+            const uint32_t e = (uint32_t)(top - 1 - k);
+            const float4 r0 = srec[3 * k + 0];  // x, y, a', b'
+            const float4 r1 = srec[3 * k + 1];  // c', o, r, g
+            const float rb = srec[3 * k + 2].x;
+            // moments of s = G * o * dL/dalpha over the tile's pixels
+            float Sx = 0.f, Sy = 0.f, Sxx = 0.f, Sxy = 0.f, Syy = 0.f, S0 = 0.f, gr = 0.f, gg = 0.f, gb = 0.f;
+            bool any = false;
 #pragma unroll
-                for (int p = 0; p < kPPL; ++p) {
-                    if (e >= lastc[p]) continue;
-                    const float dx = r0.x - pfx, dy = r0.y - pfy[p];
-                    const float power = -0.5f * (r0.z * dx * dx + r1.x * dy * dy) - r0.w * dx * dy;
-                    if (power > 0.0f) continue;
-                    const float G = __expf(power);
-                    const float alpha = fminf(0.99f, r1.y * G);
-                    if (alpha < 1.0f / 255.0f) continue;
+            for (int p = 0; p < kPPL; ++p) {
+                if (!(m & (1u << p))) continue;  // wave-uniform
+                const float dx = r0.x - pfx, dy = r0.y - (by0 + (float)((lane >> 4) + 4 * p));
+                const float pw = fmaf(r0.z * dx, dx, fmaf(r0.w * dx, dy, r1.x * dy * dy));
+                const float G = __builtin_amdgcn_exp2f(pw);
+                const float alpha = fminf(0.99f, r1.y * G);
+                const bool valid = e < lastc[p] && pw <= 0.0f && alpha >= (1.0f / 255.0f);
+                if (valid) {
                     any = true;
-                    const float one_m = 1.0f - alpha;
-                    T[p] = T[p] / one_m;
-                    const float dchannel = alpha * T[p];
-                    ac0[p] = la[p] * lc0[p] + (1.0f - la[p]) * ac0[p];
-                    ac1[p] = la[p] * lc1[p] + (1.0f - la[p]) * ac1[p];
-                    ac2[p] = la[p] * lc2[p] + (1.0f - la[p]) * ac2[p];
+                    const float inv = __builtin_amdgcn_rcpf(1.0f - alpha);
+                    T[p] = T[p] * inv;
+                    const float dch = alpha * T[p];
+                    ac0[p] = fmaf(la[p], lc0[p] - ac0[p], ac0[p]);
+                    ac1[p] = fmaf(la[p], lc1[p] - ac1[p], ac1[p]);
+                    ac2[p] = fmaf(la[p], lc2[p] - ac2[p], ac2[p]);
                     lc0[p] = r1.z;
                     lc1[p] = r1.w;
-                    lc2[p] = r2.x;
-                    float dL_dalpha = (r1.z - ac0[p]) * dp0[p] + (r1.w - ac1[p]) * dp1[p] + (r2.x - ac2[p]) * dp2[p];
-                    gr += dchannel * dp0[p];
-                    gg += dchannel * dp1[p];
-                    gb += dchannel * dp2[p];
-                    dL_dalpha *= T[p];
+                    lc2[p] = rb;
                     la[p] = alpha;
-                    dL_dalpha += (-Tf[p] / one_m) * bgd[p];
-                    const float dL_dG = r1.y * dL_dalpha;
-                    const float gdx = G * dx, gdy = G * dy;
-                    gmx += dL_dG * (-gdx * r0.z - gdy * r0.w) * ddelx_dx;
-                    gmy += dL_dG * (-gdy * r1.x - gdx * r0.w) * ddely_dy;
-                    gA += -0.5f * gdx * dx * dL_dG;
-                    gB += -gdx * dy * dL_dG;
-                    gC += -0.5f * gdy * dy * dL_dG;
-                    go += G * dL_dalpha;
+                    float dLda = (r1.z - ac0[p]) * dp0[p];
+                    dLda = fmaf(r1.w - ac1[p], dp1[p], dLda);
+                    dLda = fmaf(rb - ac2[p], dp2[p], dLda);
+                    gr = fmaf(dch, dp0[p], gr);
+                    gg = fmaf(dch, dp1[p], gg);
+                    gb = fmaf(dch, dp2[p], gb);
+                    dLda = fmaf(dLda, T[p], cbg[p] * inv);
+                    const float GdL = G * dLda;
+                    S0 += GdL;
+                    const float s = r1.y * GdL;
+                    const float sx = s * dx, sy = s * dy;
+                    Sx += sx;
+                    Sy += sy;
+                    Sxx = fmaf(sx, dx, Sxx);
+                    Sxy = fmaf(sx, dy, Sxy);
+                    Syy = fmaf(sy, dy, Syy);
                 }
-                if (__any(any)) {
-                    gmx = wave_sum(gmx);
-                    gmy = wave_sum(gmy);
-                    gA = wave_sum(gA);
-                    gB = wave_sum(gB);
-                    gC = wave_sum(gC);
-                    go = wave_sum(go);
-                    gr = wave_sum(gr);
-                    gg = wave_sum(gg);
-                    gb = wave_sum(gb);
-                    if (lane == 0) {
-                        sout[3 * k + 0] = make_float4(gmx, gmy, gA, gB);
-                        sout[3 * k + 1] = make_float4(gC, go, gr, gg);
-                        sout[3 * k + 2] = make_float4(gb, 0.f, 0.f, 0.f);
-                    }
+            }
+            if (__any(any)) {
+                Sx = wave_sum(Sx);
+                Sy = wave_sum(Sy);
+                Sxx = wave_sum(Sxx);
+                Sxy = wave_sum(Sxy);
+                Syy = wave_sum(Syy);
+                S0 = wave_sum(S0);
+                gr = wave_sum(gr);
+                gg = wave_sum(gg);
+                gb = wave_sum(gb);
+                if (lane == 0) {
+                    const float A = -2.0f * kLn2 * r0.z, B = -kLn2 * r0.w, C = -2.0f * kLn2 * r1.x;
+                    sout[3 * k + 0] = make_float4((-A * Sx - B * Sy) * hw, (-C * Sy - B * Sx) * hh, -0.5f * Sxx, -Sxy);
+                    sout[3 * k + 1] = make_float4(-0.5f * Syy, S0, gr, gg);
+                    sout[3 * k + 2] = make_float4(gb, 0.f, 0.f, 0.f);
                 }
             }
         }

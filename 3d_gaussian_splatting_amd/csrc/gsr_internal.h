@@ -1,7 +1,7 @@
 // gsr_internal.h -- buffer layouts and launch helpers shared by the C-ABI (gsr_api.cpp)
 // and the kernels.  HBM layout (DESIGN.md "Data layout"):
 //
-//   geometry (per Gaussian, P):   depth_key u32 | tiles u32 | flags u32 | rec float4[3]
+//   geometry (per Gaussian, P):   depth_key u32 | tiles u32 | flags u32 | rec float4[3] | rect uint2
 //                                 | inst_start u32 | offsets u32 | sort ping-pong 4 x u32
 //                                 | radix histogram (256 x blocks) | scan partials
 //   binning  (per instance, K):   tile key/val ping-pong 4 x u32 | inst_gid u32 | sorted_gid u32
@@ -28,7 +28,7 @@ inline int div_up(long long a, long long b) { return (int)((a + b - 1) / b); }
 inline int sort_blocks(long long n) { return n > 0 ? div_up(n, kSortTile) : 0; }
 
 struct GeomLayout {
-    size_t depth_key, tiles, flags, rec, inst_start, offsets, sA_k, sA_v, sB_k, sB_v, hist,
+    size_t depth_key, tiles, flags, rec, rect, inst_start, offsets, sA_k, sA_v, sB_k, sB_v, hist,
         partials, total;
     GeomLayout(int P) {
         size_t o = 0, n = (size_t)(P > 0 ? P : 1);
@@ -37,6 +37,7 @@ struct GeomLayout {
         tiles = take(4 * n);
         flags = take(4 * n);
         rec = take(16 * 3 * n);
+        rect = take(8 * n);
         inst_start = take(4 * n);
         offsets = take(4 * n);
         sA_k = take(4 * n);

@@ -18,7 +18,8 @@ struct PreOut {
     uint32_t* depth_key;
     uint32_t* tiles;
     uint32_t* flags;
-    float4* rec;
+    float4* rec;   // blend records: {x, y, a', b'}, {c', o, r, g}, {b, ext_x, ext_y, 0}
+    uint2* rect;   // tile rect: (minx | miny << 16, maxx | maxy << 16), full image
 };
 
 // F1: projection, EWA cov2D, conic, radius, tile rect, SH->RGB (bit-exact vs the oracle)
@@ -38,7 +39,7 @@ int inclusive_scan_gather(const uint32_t* in, const uint32_t* idx, uint32_t* out
 
 // F3: emit (tile key, owner gid) for every (Gaussian, tile in band) in depth-rank order
 int launch_duplicate(const uint32_t* gid_by_rank, const uint32_t* offsets, const uint32_t* tiles,
-                     const float4* rec, int P, int grid_x, int ty0, int ty1, uint32_t* inst_start,
+                     const uint2* rect, int P, int grid_x, int ty0, int ty1, uint32_t* inst_start,
                      uint32_t* tkey, uint32_t* inst_gid, hipStream_t s);
 
 // F5: sorted_gid[i] = inst_gid[sorted_j[i]]; ranges[tile] = [start, end)
@@ -55,6 +56,9 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
                           const uint2* ranges, const uint32_t* sorted_gid, const uint32_t* sorted_j,
                           const float4* rec, const float* final_T, const uint32_t* n_contrib,
                           const float* dL_dpix, float* partial, hipStream_t s);
+
+// record layout constants shared by preprocess and the blend kernels
+constexpr float kLn2 = 0.6931471805599453f;  // conic A = -2 ln2 a', B = -ln2 b', C = -2 ln2 c' 
 
 // sum partials per Gaussian (emission order) -> grad2d (kPart floats per Gaussian)
 int launch_gather_grad2d(const uint32_t* inst_start, const uint32_t* tiles, const float* partial,

@@ -29,10 +29,22 @@ constexpr float kSH_C1 = 0.4886025119029199f;
 __device__ inline int imin(int a, int b) { return a < b ? a : b; }
 __device__ inline int imax(int a, int b) { return a > b ? a : b; }
 
+// The block's SH-rest rows (256 Gaussians x M_rest x 3 floats, contiguous in HBM) are staged
+// through LDS with coalesced dword loads: read straight from HBM, each lane's 180-B row at a
+// 180-B lane stride would touch ~90 cache lines per load instruction and thrash L1.
 __global__ __launch_bounds__(256) void preprocess_kernel(const gsr_camera cam, const GaussIn in,
                                                          int grid_x, int grid_y, int ty0, int ty1,
                                                          PreOut out) {
+    extern __shared__ __attribute__((aligned(16))) float sh_lds[];
     const int g = blockIdx.x * 256 + threadIdx.x;
+    const int M3 = in.M_rest * 3;
+    if (in.sh_rest && !in.colors && in.D > 0) {  // block-uniform
+        const size_t base = (size_t)blockIdx.x * 256 * M3;
+        const int rows = in.P - blockIdx.x * 256 < 256 ? in.P - blockIdx.x * 256 : 256;
+        const int cnt = rows * M3;
+        for (int i = threadIdx.x; i < cnt; i += 256) sh_lds[i] = in.sh_rest[base + i];
+        __syncthreads();
+    }
     if (g >= in.P) return;
     const float* V = cam.viewmatrix;
     const float* Pm = cam.projmatrix;
@@ -164,7 +176,7 @@ __global__ __launch_bounds__(256) void preprocess_kernel(const gsr_camera cam, c
                         }
                     }
                     const int nb = (D + 1) * (D + 1);
-                    const float* rest = in.sh_rest + (size_t)g * in.M_rest * 3;
+                    const float* rest = sh_lds + threadIdx.x * M3;
 #pragma unroll
                     for (int ch = 0; ch < 3; ++ch) {
                         float r = basis[0] * in.sh_dc[3 * g + ch];
@@ -181,12 +193,21 @@ __global__ __launch_bounds__(256) void preprocess_kernel(const gsr_camera cam, c
                 radius_out = radius;
                 key_out = __float_as_uint(tz);
                 tiles_out = (uint32_t)((maxx - minx) * band_rows);
-                const uint32_t rmin = (uint32_t)minx | ((uint32_t)miny << 16);
-                const uint32_t rmax = (uint32_t)maxx | ((uint32_t)maxy << 16);
+                // Blend record (SURVEY B.3 power with -0.5 and log2(e) folded in, so the blend
+                // evaluates exp2 directly) + the half-extents of the alpha >= 1/255 footprint:
+                // d^T Q d <= t, t = 2 ln(255 o)  =>  |dx| <= sqrt(t a), |dy| <= sqrt(t c),
+                // padded (x1.02 + 0.5 px) so the per-stripe cull never drops a contributing pixel.
+                const float opac = in.opac[g];
+                const float kL2E = 1.4426950408889634f;
+                const float tthr = 2.0f * logf(255.0f * opac);
+                const float ex = tthr > 0.0f ? sqrtf(tthr * a) * 1.02f + 0.5f : -1.0f;
+                const float ey = tthr > 0.0f ? sqrtf(tthr * c) * 1.02f + 0.5f : -1.0f;
                 float4* rec = out.rec + 3 * (size_t)g;
-                rec[0] = make_float4(xs, ys, cA, cB);
-                rec[1] = make_float4(cC, in.opac[g], rgb[0], rgb[1]);
-                rec[2] = make_float4(rgb[2], tz, __uint_as_float(rmin), __uint_as_float(rmax));
+                rec[0] = make_float4(xs, ys, -0.5f * kL2E * cA, -kL2E * cB);
+                rec[1] = make_float4(-0.5f * kL2E * cC, opac, rgb[0], rgb[1]);
+                rec[2] = make_float4(rgb[2], ex, ey, 0.0f);
+                out.rect[g] = make_uint2((uint32_t)minx | ((uint32_t)miny << 16),
+                                         (uint32_t)maxx | ((uint32_t)maxy << 16));
                 out.flags[g] = clamped;
             }
         }
@@ -202,7 +223,8 @@ int launch_preprocess(const gsr_camera& cam, const GaussIn& in, int ty0, int ty1
                       hipStream_t s) {
     if (in.P <= 0) return 0;
     const int gx = div_up(cam.width, kTile), gy = div_up(cam.height, kTile);
-    hipLaunchKernelGGL(preprocess_kernel, dim3(div_up(in.P, 256)), dim3(256), 0, s, cam, in, gx, gy,
+    const size_t lds = (in.sh_rest && !in.colors && in.D > 0) ? sizeof(float) * 256 * 3 * in.M_rest : 0;
+    hipLaunchKernelGGL(preprocess_kernel, dim3(div_up(in.P, 256)), dim3(256), lds, s, cam, in, gx, gy,
                        ty0, ty1, out);
     return (int)hipGetLastError();
 }

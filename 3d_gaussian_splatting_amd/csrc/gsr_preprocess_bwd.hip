@@ -50,13 +50,16 @@ __global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __re
     dst[2] = make_float4(a[8], 0.f, 0.f, 0.f);
 }
 
-__global__ __launch_bounds__(256) void preprocess_backward_kernel(
-    const gsr_camera cam, const GaussIn in, const uint32_t* __restrict__ depth_key,
-    const uint32_t* __restrict__ flags, const uint32_t* __restrict__ inst_start,
-    const uint32_t* __restrict__ tiles, const float* __restrict__ partial,
-    const float* __restrict__ grad2d, GradOut out) {
-    const int g = blockIdx.x * 256 + threadIdx.x;
-    if (g >= in.P) return;
+// One Gaussian's chain rule.  `lrest`: this thread's SH-rest row staged in LDS (read, then
+// overwritten in place with the row's gradient), or nullptr when there is no SH-rest input.
+__device__ void preprocess_backward_one(const gsr_camera& cam, const GaussIn& in, int g,
+                                        const uint32_t* __restrict__ depth_key,
+                                        const uint32_t* __restrict__ flags,
+                                        const uint32_t* __restrict__ inst_start,
+                                        const uint32_t* __restrict__ tiles,
+                                        const float* __restrict__ partial,
+                                        const float* __restrict__ grad2d, const GradOut& out,
+                                        float* lrest) {
     const bool visible = depth_key[g] != 0xFFFFFFFFu;
     // ---- 2D gradients ----
     float g2[9];
@@ -105,8 +108,8 @@ __global__ __launch_bounds__(256) void preprocess_backward_kernel(
         } else {
 #pragma unroll
             for (int k = 0; k < 3; ++k) out.sh_dc[3 * g + k] = 0.f;
-            if (in.sh_rest)
-                for (int k = 0; k < 3 * in.M_rest; ++k) out.sh_rest[(size_t)g * in.M_rest * 3 + k] = 0.f;
+            if (lrest)
+                for (int k = 0; k < 3 * in.M_rest; ++k) lrest[k] = 0.f;
         }
         out.means3D[3 * g + 0] = 0.f;
         out.means3D[3 * g + 1] = 0.f;
@@ -173,9 +176,9 @@ __global__ __launch_bounds__(256) void preprocess_backward_kernel(
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) out.sh_dc[3 * g + ch] = basis[0] * dres[ch];
         float ddx = 0.f, ddy = 0.f, ddz = 0.f;
-        if (in.sh_rest) {
-            const float* rest = in.sh_rest + (size_t)g * in.M_rest * 3;
-            float* drest = out.sh_rest + (size_t)g * in.M_rest * 3;
+        if (lrest) {
+            const float* rest = lrest;
+            float* drest = lrest;
 #pragma unroll
             for (int k = 1; k < 16; ++k) {
                 if (k > in.M_rest) break;
@@ -339,6 +342,30 @@ __global__ __launch_bounds__(256) void preprocess_backward_kernel(
     out.rots[4 * g + 3] = 2.f * (-2.f * z * dR[0] - r * dR[1] + x * dR[2] + r * dR[3] - 2.f * z * dR[4] + y * dR[5] + x * dR[6] + y * dR[7]);
 }
 
+__global__ __launch_bounds__(256) void preprocess_backward_kernel(
+    const gsr_camera cam, const GaussIn in, const uint32_t* __restrict__ depth_key,
+    const uint32_t* __restrict__ flags, const uint32_t* __restrict__ inst_start,
+    const uint32_t* __restrict__ tiles, const float* __restrict__ partial,
+    const float* __restrict__ grad2d, GradOut out) {
+    extern __shared__ __attribute__((aligned(16))) float sh_lds[];
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    const int M3 = in.M_rest * 3;
+    const bool stage = in.sh_rest != nullptr && !in.colors;  // block-uniform
+    const int rows = in.P - blockIdx.x * 256 < 256 ? in.P - blockIdx.x * 256 : 256;
+    const size_t base = (size_t)blockIdx.x * 256 * M3;
+    if (stage) {  // coalesced staging of the block's SH-rest rows (see preprocess_kernel)
+        for (int i = threadIdx.x; i < rows * M3; i += 256) sh_lds[i] = in.sh_rest[base + i];
+        __syncthreads();
+    }
+    if (g < in.P)
+        preprocess_backward_one(cam, in, g, depth_key, flags, inst_start, tiles, partial, grad2d, out,
+                                stage ? sh_lds + threadIdx.x * M3 : nullptr);
+    if (stage) {  // coalesced write-back of the SH-rest gradient rows
+        __syncthreads();
+        for (int i = threadIdx.x; i < rows * M3; i += 256) out.sh_rest[base + i] = sh_lds[i];
+    }
+}
+
 }  // namespace
 
 int launch_gather_grad2d(const uint32_t* inst_start, const uint32_t* tiles, const float* partial,
@@ -354,7 +381,8 @@ int launch_preprocess_backward(const gsr_camera& cam, const GaussIn& in, const u
                                const uint32_t* tiles, const float* partial, const float* grad2d,
                                const GradOut& out, hipStream_t s) {
     if (in.P <= 0) return 0;
-    hipLaunchKernelGGL(preprocess_backward_kernel, dim3(div_up(in.P, 256)), dim3(256), 0, s, cam, in,
+    const size_t lds = (in.sh_rest && !in.colors) ? sizeof(float) * 256 * 3 * in.M_rest : 0;
+    hipLaunchKernelGGL(preprocess_backward_kernel, dim3(div_up(in.P, 256)), dim3(256), lds, s, cam, in,
                        depth_key, flags, inst_start, tiles, partial, grad2d, out);
     return (int)hipGetLastError();
 }

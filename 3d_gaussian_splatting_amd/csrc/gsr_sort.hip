@@ -267,7 +267,7 @@ __global__ __launch_bounds__(kB) void scan_downsweep(const uint32_t* __restrict_
 __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restrict__ gid_by_rank,
                                                         const uint32_t* __restrict__ offsets,
                                                         const uint32_t* __restrict__ tiles,
-                                                        const float4* __restrict__ rec, int P,
+                                                        const uint2* __restrict__ rect, int P,
                                                         int grid_x, int ty0, int ty1,
                                                         uint32_t* __restrict__ inst_start,
                                                         uint32_t* __restrict__ tkey,
@@ -280,8 +280,8 @@ __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restri
     uint32_t j = end - nt;
     inst_start[g] = j;
     if (nt == 0) return;
-    const float4 r2 = rec[3 * (size_t)g + 2];
-    const uint32_t rmin = __float_as_uint(r2.z), rmax = __float_as_uint(r2.w);
+    const uint2 rr = rect[g];
+    const uint32_t rmin = rr.x, rmax = rr.y;
     const int minx = rmin & 0xFFFF, miny = rmin >> 16, maxx = rmax & 0xFFFF, maxy = rmax >> 16;
     const int y0 = miny > ty0 ? miny : ty0, y1 = maxy < ty1 ? maxy : ty1;
     for (int y = y0; y < y1; ++y)
@@ -345,11 +345,11 @@ int inclusive_scan_gather(const uint32_t* in, const uint32_t* idx, uint32_t* out
 }
 
 int launch_duplicate(const uint32_t* gid_by_rank, const uint32_t* offsets, const uint32_t* tiles,
-                     const float4* rec, int P, int grid_x, int ty0, int ty1, uint32_t* inst_start,
+                     const uint2* rect, int P, int grid_x, int ty0, int ty1, uint32_t* inst_start,
                      uint32_t* tkey, uint32_t* inst_gid, hipStream_t s) {
     if (P <= 0) return 0;
     hipLaunchKernelGGL(duplicate_kernel, dim3(div_up(P, 256)), dim3(256), 0, s, gid_by_rank, offsets,
-                       tiles, rec, P, grid_x, ty0, ty1, inst_start, tkey, inst_gid);
+                       tiles, rect, P, grid_x, ty0, ty1, inst_start, tkey, inst_gid);
     return (int)hipGetLastError();
 }
 

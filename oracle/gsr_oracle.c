@@ -66,6 +66,7 @@ struct gsro_state {
     /* pixels */
     float* final_T;
     uint32_t* n_contrib;
+    uint32_t* examined; /* list entries examined per pixel (work statistics) */
     uint64_t pairs;
 };
 
@@ -376,6 +377,7 @@ static uint64_t blend_tile(gsro_state* st, int tile, float* out_color) {
             size_t pix = (size_t)pyi * W + pxi;
             st->final_T[pix] = T;
             st->n_contrib[pix] = last;
+            st->examined[pix] = contributor;
             for (int ch = 0; ch < 3; ++ch) out_color[(size_t)ch * H * W + pix] = C[ch] + T * st->bg[ch];
         }
     return pairs;
@@ -428,6 +430,7 @@ int gsro_forward(const gsro_camera* cam, int P, int D, int M_rest, const float* 
     size_t npix = (size_t)cam->width * cam->height;
     st->final_T = (float*)malloc(4 * npix);
     st->n_contrib = (uint32_t*)malloc(4 * npix);
+    st->examined = (uint32_t*)calloc(npix, 4);
     /* pixels outside the band: background, T = 1 */
     for (size_t i = 0; i < npix; ++i) {
         st->final_T[i] = 1.0f;
@@ -770,7 +773,7 @@ void gsro_free(gsro_state* st) {
     free(st->radii); free(st->xy); free(st->depth); free(st->conic_o); free(st->rgb);
     free(st->clamped); free(st->tiles_touched); free(st->rect); free(st->inst_start);
     free(st->s_tile); free(st->s_depth); free(st->s_gid); free(st->s_j); free(st->ranges);
-    free(st->final_T); free(st->n_contrib);
+    free(st->final_T); free(st->n_contrib); free(st->examined);
     free(st);
 }
 
@@ -804,3 +807,7 @@ void gsro_get_preprocess(const gsro_state* st, float* xy, float* depth, float* c
 }
 
 uint64_t gsro_forward_pairs(const gsro_state* st) { return st->pairs; }
+
+void gsro_get_examined(const gsro_state* st, uint32_t* examined) {
+    memcpy(examined, st->examined, (size_t)st->cam.width * st->cam.height * 4);
+}

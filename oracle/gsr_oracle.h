@@ -86,6 +86,8 @@ void gsro_get_preprocess(const gsro_state* st, float* xy, float* depth, float* c
                          float* rgb, uint32_t* tiles_touched);
 /* count of (pixel, list entry) evaluations the forward made (VALU-bound proxy) */
 uint64_t gsro_forward_pairs(const gsro_state* st);
+/* per pixel: list entries examined by the forward before termination */
+void gsro_get_examined(const gsro_state* st, uint32_t* examined);
 
 #ifdef __cplusplus
 }

@@ -53,6 +53,7 @@ def lib():
         L.gsro_get_pixel_state.argtypes = [vp, fp, up]
         L.gsro_get_preprocess.argtypes = [vp, fp, fp, fp, fp, up]
         L.gsro_forward_pairs.argtypes = [vp]
+        L.gsro_get_examined.argtypes = [vp, up]
         L.gsro_forward_pairs.restype = ctypes.c_uint64
         L.gsro_build_rotation.argtypes = [fp, fp]
         L.gsro_covariance.argtypes = [fp, ctypes.c_float, fp, fp]
@@ -138,6 +139,12 @@ class OracleState:
         tt = np.zeros(P, np.uint32)
         lib().gsro_get_preprocess(self.ptr, _f(xy), _f(depth), _f(co), _f(rgb), _u(tt))
         return dict(xy=xy, depth=depth, conic_o=co, rgb=rgb, tiles_touched=tt)
+
+    def examined(self):
+        H, W = self.cam.height, self.cam.width
+        e = np.zeros(H * W, np.uint32)
+        lib().gsro_get_examined(self.ptr, _u(e))
+        return e.reshape(H, W)
 
     def forward_pairs(self) -> int:
         return int(lib().gsro_forward_pairs(self.ptr))
