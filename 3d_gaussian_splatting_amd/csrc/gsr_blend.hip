@@ -21,6 +21,8 @@
 //
 // Roofline: VALU-bound (exp + ~20 flops per pixel x record pair); HBM traffic per tile is
 // the gathered 48-B records + per-pixel I/O.
+#include <cstdlib>
+
 #include "gsr_kernels.h"
 
 namespace gsr {
@@ -35,20 +37,45 @@ __device__ inline int xcd_tile(int b, int nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
 }
 
-template <int CTRL, int ROW_MASK = 0xF>
+template <int CTRL>
 __device__ inline float dpp_f(float x) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, ROW_MASK, 0xF, false));
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
 }
 
-// sum over the 64 lanes (every lane must be active); result is wave-uniform
-__device__ inline float wave_sum(float x) {
-    x += dpp_f<0xB1>(x);         // quad_perm [1,0,3,2]
-    x += dpp_f<0x4E>(x);         // quad_perm [2,3,0,1]
-    x += dpp_f<0x141>(x);        // row_half_mirror
-    x += dpp_f<0x140>(x);        // row_mirror
-    x += dpp_f<0x142, 0xA>(x);   // row_bcast:15
-    x += dpp_f<0x143, 0xC>(x);   // row_bcast:31
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+// Row-level (16-lane) all-reduce of N independent values, step-interleaved so consecutive
+// DPP reads never hit the VGPR written by the instruction right before (no s_nop hazards).
+template <int N>
+__device__ inline void row_reduce(float (&v)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] += dpp_f<0xB1>(v[i]);   // quad_perm [1,0,3,2]
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] += dpp_f<0x4E>(v[i]);   // quad_perm [2,3,0,1]
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] += dpp_f<0x141>(v[i]);  // row_half_mirror
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] += dpp_f<0x140>(v[i]);  // row_mirror
+}
+
+__device__ inline float fsum_pair(uint2 r) { return __uint_as_float(r.x) + __uint_as_float(r.y); }
+
+// gfx950 reduce-scatter of four row-reduced values: afterwards lanes of row 0/1/2/3 hold the
+// 64-lane totals of a/b/c/d.  v_permlane16_swap swaps VDST rows 1,3 with VSRC rows 0,2;
+// v_permlane32_swap swaps VDST lanes 32-63 with VSRC lanes 0-31.
+__device__ inline float scatter4(float a, float b, float c, float d) {
+    auto ab = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    auto cd = __builtin_amdgcn_permlane16_swap(__float_as_uint(c), __float_as_uint(d), false, false);
+    const float x = __uint_as_float(ab[0]) + __uint_as_float(ab[1]);  // rows: a01 b01 a23 b23
+    const float y = __uint_as_float(cd[0]) + __uint_as_float(cd[1]);  // rows: c01 d01 c23 d23
+    auto xy = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+    return __uint_as_float(xy[0]) + __uint_as_float(xy[1]);           // rows: a b c d
+}
+
+// full 64-lane all-reduce of a row-reduced value (every lane gets the total)
+__device__ inline float allreduce_rows(float a) {
+    auto s16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(a), false, false);
+    const float x = __uint_as_float(s16[0]) + __uint_as_float(s16[1]);
+    auto s32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(s32[0]) + __uint_as_float(s32[1]);
 }
 
 __device__ inline uint32_t wave_max_u32(uint32_t x) {
@@ -81,6 +108,9 @@ __device__ inline uint32_t stripe_mask(const float4 r0, const float4 r2, float b
     return m;
 }
 
+// SLOT_CULL: skip culled 16x4 stripes with a wave-uniform branch (fewer VALU ops) or
+// evaluate all four stripes predicated (independent chains the scheduler can interleave).
+template <bool SLOT_CULL>
 __global__ __launch_bounds__(64) void blend_forward_kernel(const BlendGeom geo,
                                                            const uint2* __restrict__ ranges,
                                                            const uint32_t* __restrict__ sorted_gid,
@@ -137,11 +167,12 @@ __global__ __launch_bounds__(64) void blend_forward_kernel(const BlendGeom geo,
             const uint32_t idx = (uint32_t)(base + k + 1);
 #pragma unroll
             for (int p = 0; p < kPPL; ++p) {
-                if (!(m & (1u << p))) continue;  // wave-uniform
+                if (SLOT_CULL && !(m & (1u << p))) continue;  // wave-uniform
                 const float dx = r0.x - pfx, dy = r0.y - pfy[p];
                 const float pw = fmaf(r0.z * dx, dx, fmaf(r0.w * dx, dy, r1.x * dy * dy));
                 const float alpha = fminf(0.99f, r1.y * __builtin_amdgcn_exp2f(pw));
-                const bool valid = !done[p] && pw <= 0.0f && alpha >= (1.0f / 255.0f);
+                const bool valid = (SLOT_CULL || (m & (1u << p))) && !done[p] && pw <= 0.0f &&
+                                   alpha >= (1.0f / 255.0f);
                 const float tT = T[p] * (1.0f - alpha);
                 const bool term = valid && tT < 0.0001f;
                 const bool contrib = valid && !term;
@@ -178,6 +209,7 @@ __global__ __launch_bounds__(64) void blend_forward_kernel(const BlendGeom geo,
     }
 }
 
+template <bool SLOT_CULL>
 __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
                                                             const uint2* __restrict__ ranges,
                                                             const uint32_t* __restrict__ sorted_gid,
@@ -188,7 +220,7 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
                                                             const float* __restrict__ dL_dpix,
                                                             float* __restrict__ partial) {
     __shared__ float4 srec[64 * 3];
-    __shared__ float4 sout[64 * 3];
+    __shared__ float smom[64 * 12];  // per batch entry: Sx Sy Sxx Sxy | Syy S0 gr gg | gb - - -
     const int tile = xcd_tile(blockIdx.x, geo.nwg) + geo.ty0 * geo.grid_x;
     const int tx = tile % geo.grid_x, ty = tile / geo.grid_x;
     const int lane = threadIdx.x;
@@ -220,26 +252,29 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
     maxlast = wave_max_u32(maxlast);
     const uint2 range = ranges[tile];
     const int n = (int)(range.y - range.x);
+    const int row = lane >> 4;
     for (int top = n; top > 0; top -= 64) {
         const int lo = top > 64 ? top - 64 : 0;
         const int cnt = top - lo;
         const int e_l = top - 1 - lane;  // this lane's entry (descending)
         uint32_t jl = 0, smask = 0;
+        float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0;  // this lane's record (conic)
         if (lane < cnt) {
             jl = sorted_j[range.x + e_l];
             if (e_l < (int)maxlast) {
                 const uint32_t g = sorted_gid[range.x + e_l];
                 const float4* r = rec + 3 * (size_t)g;
-                const float4 r0 = r[0], r1 = r[1], r2 = r[2];
-                srec[3 * lane + 0] = r0;
-                srec[3 * lane + 1] = r1;
+                q0 = r[0];
+                q1 = r[1];
+                const float4 r2 = r[2];
+                srec[3 * lane + 0] = q0;
+                srec[3 * lane + 1] = q1;
                 srec[3 * lane + 2] = r2;
-                smask = stripe_mask(r0, r2, bx0, by0);
+                smask = stripe_mask(q0, r2, bx0, by0);
             }
         }
-        sout[3 * lane + 0] = make_float4(0.f, 0.f, 0.f, 0.f);
-        sout[3 * lane + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
-        sout[3 * lane + 2] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int c = 0; c < 12; ++c) smom[lane * 12 + c] = 0.0f;
         __syncthreads();
         uint64_t todo = __ballot(smask != 0u);
         while (todo) {
@@ -250,17 +285,18 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
             const float4 r0 = srec[3 * k + 0];  // x, y, a', b'
             const float4 r1 = srec[3 * k + 1];  // c', o, r, g
             const float rb = srec[3 * k + 2].x;
-            // moments of s = G * o * dL/dalpha over the tile's pixels
-            float Sx = 0.f, Sy = 0.f, Sxx = 0.f, Sxy = 0.f, Syy = 0.f, S0 = 0.f, gr = 0.f, gg = 0.f, gb = 0.f;
+            // moments of s = G * o * dL/dalpha over the tile's pixels (+ colour sums)
+            float v[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
             bool any = false;
 #pragma unroll
             for (int p = 0; p < kPPL; ++p) {
-                if (!(m & (1u << p))) continue;  // wave-uniform
-                const float dx = r0.x - pfx, dy = r0.y - (by0 + (float)((lane >> 4) + 4 * p));
+                if (SLOT_CULL && !(m & (1u << p))) continue;  // wave-uniform
+                const float dx = r0.x - pfx, dy = r0.y - (by0 + (float)(row + 4 * p));
                 const float pw = fmaf(r0.z * dx, dx, fmaf(r0.w * dx, dy, r1.x * dy * dy));
                 const float G = __builtin_amdgcn_exp2f(pw);
                 const float alpha = fminf(0.99f, r1.y * G);
-                const bool valid = e < lastc[p] && pw <= 0.0f && alpha >= (1.0f / 255.0f);
+                const bool valid = (SLOT_CULL || (m & (1u << p))) && e < lastc[p] && pw <= 0.0f &&
+                                   alpha >= (1.0f / 255.0f);
                 if (valid) {
                     any = true;
                     const float inv = __builtin_amdgcn_rcpf(1.0f - alpha);
@@ -276,51 +312,55 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
                     float dLda = (r1.z - ac0[p]) * dp0[p];
                     dLda = fmaf(r1.w - ac1[p], dp1[p], dLda);
                     dLda = fmaf(rb - ac2[p], dp2[p], dLda);
-                    gr = fmaf(dch, dp0[p], gr);
-                    gg = fmaf(dch, dp1[p], gg);
-                    gb = fmaf(dch, dp2[p], gb);
+                    v[6] = fmaf(dch, dp0[p], v[6]);
+                    v[7] = fmaf(dch, dp1[p], v[7]);
+                    v[8] = fmaf(dch, dp2[p], v[8]);
                     dLda = fmaf(dLda, T[p], cbg[p] * inv);
                     const float GdL = G * dLda;
-                    S0 += GdL;
-                    const float s = r1.y * GdL;
-                    const float sx = s * dx, sy = s * dy;
-                    Sx += sx;
-                    Sy += sy;
-                    Sxx = fmaf(sx, dx, Sxx);
-                    Sxy = fmaf(sx, dy, Sxy);
-                    Syy = fmaf(sy, dy, Syy);
+                    v[5] += GdL;
+                    const float sv = r1.y * GdL;
+                    const float sx = sv * dx, sy = sv * dy;
+                    v[0] += sx;
+                    v[1] += sy;
+                    v[2] = fmaf(sx, dx, v[2]);
+                    v[3] = fmaf(sx, dy, v[3]);
+                    v[4] = fmaf(sy, dy, v[4]);
                 }
             }
             if (__any(any)) {
-                Sx = wave_sum(Sx);
-                Sy = wave_sum(Sy);
-                Sxx = wave_sum(Sxx);
-                Sxy = wave_sum(Sxy);
-                Syy = wave_sum(Syy);
-                S0 = wave_sum(S0);
-                gr = wave_sum(gr);
-                gg = wave_sum(gg);
-                gb = wave_sum(gb);
-                if (lane == 0) {
-                    const float A = -2.0f * kLn2 * r0.z, B = -kLn2 * r0.w, C = -2.0f * kLn2 * r1.x;
-                    sout[3 * k + 0] = make_float4((-A * Sx - B * Sy) * hw, (-C * Sy - B * Sx) * hh, -0.5f * Sxx, -Sxy);
-                    sout[3 * k + 1] = make_float4(-0.5f * Syy, S0, gr, gg);
-                    sout[3 * k + 2] = make_float4(gb, 0.f, 0.f, 0.f);
+                row_reduce(v);
+                const float t0 = scatter4(v[0], v[1], v[2], v[3]);  // rows: Sx Sy Sxx Sxy
+                const float t1 = scatter4(v[4], v[5], v[6], v[7]);  // rows: Syy S0 gr gg
+                const float t2 = allreduce_rows(v[8]);              // gb everywhere
+                if ((lane & 15) == 0) {
+                    smom[k * 12 + row] = t0;
+                    smom[k * 12 + 4 + row] = t1;
+                    if (row == 0) smom[k * 12 + 8] = t2;
                 }
             }
         }
         __syncthreads();
         if (lane < cnt) {
+            // raw moments -> 2D gradients with this entry's own conic
+            const float* mo = smom + lane * 12;
+            const float Sx = mo[0], Sy = mo[1], Sxx = mo[2], Sxy = mo[3], Syy = mo[4], S0 = mo[5];
+            const float A = -2.0f * kLn2 * q0.z, B = -kLn2 * q0.w, C = -2.0f * kLn2 * q1.x;
             float4* dst = reinterpret_cast<float4*>(partial + (size_t)kPart * jl);
-            dst[0] = sout[3 * lane + 0];
-            dst[1] = sout[3 * lane + 1];
-            dst[2] = sout[3 * lane + 2];
+            dst[0] = make_float4((-A * Sx - B * Sy) * hw, (-C * Sy - B * Sx) * hh, -0.5f * Sxx, -Sxy);
+            dst[1] = make_float4(-0.5f * Syy, S0, mo[6], mo[7]);
+            dst[2] = make_float4(mo[8], 0.f, 0.f, 0.f);
         }
         __syncthreads();
     }
 }
 
 }  // namespace
+
+// Kernel-variant selector for A/B timing (bench/ablation only; default = shipped variant).
+static int variant(const char* name, int dflt) {
+    const char* v = std::getenv(name);
+    return v ? std::atoi(v) : dflt;
+}
 
 static BlendGeom make_geo(const gsr_camera& cam, const float bg[3], int ty0, int ty1) {
     BlendGeom g;
@@ -340,8 +380,12 @@ int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int 
                          float* out_color, float* final_T, uint32_t* n_contrib, hipStream_t s) {
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1);
     if (geo.nwg <= 0) return 0;
-    hipLaunchKernelGGL(blend_forward_kernel, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid, rec,
-                       out_color, final_T, n_contrib);
+    if (variant("GSR_FWD_VARIANT", 0) == 1)
+        hipLaunchKernelGGL(blend_forward_kernel<false>, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid,
+                           rec, out_color, final_T, n_contrib);
+    else
+        hipLaunchKernelGGL(blend_forward_kernel<true>, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid,
+                           rec, out_color, final_T, n_contrib);
     return (int)hipGetLastError();
 }
 
@@ -351,8 +395,12 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
                           const float* dL_dpix, float* partial, hipStream_t s) {
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1);
     if (geo.nwg <= 0) return 0;
-    hipLaunchKernelGGL(blend_backward_kernel, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid,
-                       sorted_j, rec, final_T, n_contrib, dL_dpix, partial);
+    if (variant("GSR_BWD_VARIANT", 0) == 1)
+        hipLaunchKernelGGL(blend_backward_kernel<false>, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid,
+                           sorted_j, rec, final_T, n_contrib, dL_dpix, partial);
+    else
+        hipLaunchKernelGGL(blend_backward_kernel<true>, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid,
+                           sorted_j, rec, final_T, n_contrib, dL_dpix, partial);
     return (int)hipGetLastError();
 }
 
