@@ -155,7 +155,9 @@ struct Views {
     uint2* ranges;
     float* final_T;
     uint32_t* n_contrib;
-    uint32_t *sorted_tile, *sorted_j, *sorted_gid, *inst_gid;
+    float* accum;
+    uint32_t *sorted_tile, *sorted_gid, *inst_gid;
+    uint2* rect;
 };
 
 Views views(const gsr_camera* cam, int P, const gsr_buffers* b) {
@@ -168,27 +170,31 @@ Views views(const gsr_camera* cam, int P, const gsr_buffers* b) {
     v.rec = at<float4>(b->geom, gl.rec);
     v.inst_start = at<uint32_t>(b->geom, gl.inst_start);
     v.offsets = at<uint32_t>(b->geom, gl.offsets);
+    v.rect = at<uint2>(b->geom, gl.rect);
     // 32-bit depth key = 4 passes (even) -> result in the A buffers
     v.gid_by_rank = at<uint32_t>(b->geom, gl.sA_v);
     v.ranges = at<uint2>(b->image, il.ranges);
     v.final_T = at<float>(b->image, il.final_T);
     v.n_contrib = at<uint32_t>(b->image, il.n_contrib);
+    v.accum = at<float>(b->image, il.accum);
     if (b->binning) {
         BinLayout bl(b->num_rendered);
         const int tiles = div_up(cam->width, kTile) * div_up(cam->height, kTile);
         const bool odd = (tile_passes(tiles) & 1) != 0;
         v.sorted_tile = at<uint32_t>(b->binning, odd ? bl.kB : bl.kA);
-        v.sorted_j = at<uint32_t>(b->binning, odd ? bl.vB : bl.vA);
-        v.sorted_gid = at<uint32_t>(b->binning, bl.sorted_gid);
+        v.sorted_gid = at<uint32_t>(b->binning, odd ? bl.vB : bl.vA);
         v.inst_gid = at<uint32_t>(b->binning, bl.inst_gid);
     }
     return v;
 }
 
-__global__ void fill_background(float* out_color, float* final_T, uint32_t* n_contrib, int npix,
-                                float bg0, float bg1, float bg2) {
+__global__ void fill_background(float* out_color, float* final_T, uint32_t* n_contrib, float* accum,
+                                int npix, float bg0, float bg1, float bg2) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= npix) return;
+    accum[i] = 0.0f;
+    accum[npix + i] = 0.0f;
+    accum[2 * (size_t)npix + i] = 0.0f;
     out_color[i] = bg0;
     out_color[npix + i] = bg1;
     out_color[2 * (size_t)npix + i] = bg2;
@@ -241,7 +247,8 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
     if (ty0 > 0 || ty1 < gy) {
         const int npix = W * H;
         hipLaunchKernelGGL(fill_background, dim3(div_up(npix, 256)), dim3(256), 0, stream, out_color,
-                           final_T, n_contrib, npix, rs->bg[0], rs->bg[1], rs->bg[2]);
+                           final_T, n_contrib, at<float>(bufs->image, il.accum), npix, rs->bg[0], rs->bg[1],
+                           rs->bg[2]);
         GSR_STAGE(GSR_STAGE_MISC, hipGetLastError(), "fill_background");
     }
     GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(ranges, 0, sizeof(uint2) * (size_t)gx * gy, stream), "memset ranges");
@@ -276,18 +283,17 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
         uint32_t* kB = at<uint32_t>(bufs->binning, bl.kB);
         uint32_t* vB = at<uint32_t>(bufs->binning, bl.vB);
         uint32_t* inst_gid = at<uint32_t>(bufs->binning, bl.inst_gid);
-        uint32_t* sorted_gid = at<uint32_t>(bufs->binning, bl.sorted_gid);
         GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate(gid_by_rank, offsets, tiles, at<uint2>(bufs->geom, gl.rect), P, gx, ty0, ty1, inst_start, kA,
                                        inst_gid, stream),
                       "duplicate");
         if (K > 0) {
             int w2 = -1;
-            GSR_STAGE(GSR_STAGE_TILE_SORT, radix_sort(kA, nullptr, kB, vB, kA, vA, K, tile_bits(gx * gy),
+            GSR_STAGE(GSR_STAGE_TILE_SORT, radix_sort(kA, inst_gid, kB, vB, kA, vA, K, tile_bits(gx * gy),
                                      at<uint32_t>(bufs->binning, bl.hist), &w2, stream),
                           "tile sort");
             const bool odd = (tile_passes(gx * gy) & 1) != 0;
             if ((w2 == 0) != odd) return fail(-12, "tile sort ended in an unexpected buffer");
-            GSR_STAGE(GSR_STAGE_FINALIZE, launch_finalize(odd ? kB : kA, odd ? vB : vA, inst_gid, K, sorted_gid, ranges, stream),
+            GSR_STAGE(GSR_STAGE_FINALIZE, launch_finalize(odd ? kB : kA, K, ranges, stream),
                           "finalize");
         }
     } else {
@@ -295,7 +301,7 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
     }
     const Views v = views(cam, P, bufs);
     GSR_STAGE(GSR_STAGE_BLEND_FWD, launch_blend_forward(*cam, rs->bg, ty0, ty1, ranges, v.sorted_gid, rec, out_color, final_T,
-                                       n_contrib, stream),
+                                       n_contrib, v.accum, stream),
                   "blend forward");
     return 0;
 }
@@ -318,8 +324,8 @@ static int backward_impl(const gsr_camera* cam, const gsr_gaussians* gs, const g
         if (!alloc_scratch) return fail(-1, "null scratch allocator");
         partial = static_cast<float*>(alloc_scratch(ctx, gsr_scratch_bytes((int32_t)K)));
         if (!partial) return fail(-2, "allocation failed (scratch, K=%lld)", K);
-        GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.sorted_j, v.rec,
-                                            v.final_T, v.n_contrib, dL_dpix, partial, stream),
+        GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.inst_start, v.rect, v.rec,
+                                            v.final_T, v.n_contrib, v.accum, dL_dpix, partial, stream),
                       "blend backward");
     }
     if (grad2d) {
@@ -376,8 +382,8 @@ int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raste
         if (!alloc_scratch) return fail(-1, "null scratch allocator");
         partial = static_cast<float*>(alloc_scratch(ctx, gsr_scratch_bytes((int32_t)K)));
         if (!partial) return fail(-2, "allocation failed (scratch, K=%lld)", K);
-        GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.sorted_j, v.rec,
-                                            v.final_T, v.n_contrib, dL_dpix, partial, stream),
+        GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.inst_start, v.rect, v.rec,
+                                            v.final_T, v.n_contrib, v.accum, dL_dpix, partial, stream),
                       "blend backward");
     }
     // K == 0: no partials and no grad2d -> the kernel uses zero 2D gradients

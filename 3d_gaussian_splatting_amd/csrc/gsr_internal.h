@@ -4,9 +4,9 @@
 //   geometry (per Gaussian, P):   depth_key u32 | tiles u32 | flags u32 | rec float4[3] | rect uint2
 //                                 | inst_start u32 | offsets u32 | sort ping-pong 4 x u32
 //                                 | radix histogram (256 x blocks) | scan partials
-//   binning  (per instance, K):   tile key/val ping-pong 4 x u32 | inst_gid u32 | sorted_gid u32
-//                                 | radix histogram
-//   image    (per pixel):         ranges uint2[tiles] | final_T f32 | n_contrib u32
+//   binning  (per instance, K):   tile key/val ping-pong 4 x u32 (values = Gaussian id)
+//                                 | inst_gid u32 (emission order) | radix histogram
+//   image    (per pixel):         ranges uint2[tiles] | final_T f32 | n_contrib u32 | accum 3 x f32
 //   scratch  (backward, per K):   partial float[GSR_GRAD2D_STRIDE]  (indexed by emission j)
 #pragma once
 #include <stddef.h>
@@ -51,7 +51,7 @@ struct GeomLayout {
 };
 
 struct BinLayout {
-    size_t kA, vA, kB, vB, inst_gid, sorted_gid, hist, total;
+    size_t kA, vA, kB, vB, inst_gid, hist, total;
     BinLayout(long long K) {
         size_t o = 0, n = (size_t)(K > 0 ? K : 1);
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
@@ -60,14 +60,13 @@ struct BinLayout {
         kB = take(4 * n);
         vB = take(4 * n);
         inst_gid = take(4 * n);
-        sorted_gid = take(4 * n);
         hist = take(4 * (256 * (size_t)(sort_blocks(n) + 1) + 256));
         total = o;
     }
 };
 
 struct ImgLayout {
-    size_t ranges, final_T, n_contrib, total;
+    size_t ranges, final_T, n_contrib, accum, total;
     ImgLayout(int W, int H) {
         size_t o = 0;
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
@@ -76,6 +75,7 @@ struct ImgLayout {
         ranges = take(8 * (tiles ? tiles : 1));
         final_T = take(4 * (pix ? pix : 1));
         n_contrib = take(4 * (pix ? pix : 1));
+        accum = take(12 * (pix ? pix : 1));  // colour sum without background, 3 x H x W
         total = o;
     }
 };

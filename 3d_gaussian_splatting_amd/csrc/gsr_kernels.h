@@ -42,20 +42,22 @@ int launch_duplicate(const uint32_t* gid_by_rank, const uint32_t* offsets, const
                      const uint2* rect, int P, int grid_x, int ty0, int ty1, uint32_t* inst_start,
                      uint32_t* tkey, uint32_t* inst_gid, hipStream_t s);
 
-// F5: sorted_gid[i] = inst_gid[sorted_j[i]]; ranges[tile] = [start, end)
-int launch_finalize(const uint32_t* sorted_tile, const uint32_t* sorted_j, const uint32_t* inst_gid,
-                    long long K, uint32_t* sorted_gid, uint2* ranges, hipStream_t s);
+// F5: ranges[tile] = [start, end) of the sorted tile keys
+int launch_finalize(const uint32_t* sorted_tile, long long K, uint2* ranges, hipStream_t s);
 
 // F6: per-tile front-to-back blend
 int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
                          const uint2* ranges, const uint32_t* sorted_gid, const float4* rec,
-                         float* out_color, float* final_T, uint32_t* n_contrib, hipStream_t s);
+                         float* out_color, float* final_T, uint32_t* n_contrib, float* accum,
+                         hipStream_t s);
 
-// B1: per-tile back-to-front gradients -> per-instance partial[j] (kPart floats)
+// B1: per-tile back-to-front gradients -> per-instance partial[j] (kPart floats), where the
+// emission index j = inst_start[g] + row-major index of the tile in g's band-clipped rect
 int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
-                          const uint2* ranges, const uint32_t* sorted_gid, const uint32_t* sorted_j,
-                          const float4* rec, const float* final_T, const uint32_t* n_contrib,
-                          const float* dL_dpix, float* partial, hipStream_t s);
+                          const uint2* ranges, const uint32_t* sorted_gid, const uint32_t* inst_start,
+                          const uint2* rect, const float4* rec, const float* final_T,
+                          const uint32_t* n_contrib, const float* accum, const float* dL_dpix,
+                          float* partial, hipStream_t s);
 
 // record layout constants shared by preprocess and the blend kernels
 constexpr float kLn2 = 0.6931471805599453f;  // conic A = -2 ln2 a', B = -ln2 b', C = -2 ln2 c' 

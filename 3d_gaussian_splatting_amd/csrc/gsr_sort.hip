@@ -8,8 +8,10 @@
 //   3. duplicate: rank r emits its band-clipped rect row-major at offsets[r-1]: the instance
 //      array is then already in (depth bits, gid, rect order) order
 //   4. stable LSD over the ceil(log2 tiles)-bit tile key only (2 passes at 1080p),
-//      values = emission index j                             -> sorted_j
-//   5. finalize: sorted_gid = inst_gid[sorted_j], tile ranges from key boundaries
+//      values = the instance's Gaussian id                   -> sorted_gid
+//   5. finalize: tile ranges from key boundaries
+// (B1 recovers an instance's emission index j from its Gaussian's rect, so no permutation
+// array is carried through the sort.)
 // Sorted bytes at 1M/1080p: 4 passes x 1M x 8 B + 2 passes x 6.5M x 8 B, vs 6 passes x 6.5M
 // x 12 B for a 45-bit (tile|depth) key sort.
 //
@@ -105,7 +107,7 @@ __global__ __launch_bounds__(kB) void radix_colscan(uint32_t* __restrict__ hist,
     if (tid == 0) totals[blockIdx.x] = carry;
 }
 
-// ---- downsweep: stable scatter ----
+// ---- downsweep: stable scatter, reordered through LDS so global writes are coalesced ----
 __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict__ keys_in,
                                                       const uint32_t* __restrict__ vals_in,
                                                       uint32_t* __restrict__ keys_out,
@@ -114,11 +116,16 @@ __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ hist,
                                                       const uint32_t* __restrict__ totals) {
     __shared__ uint32_t wcnt[kWaves][256];
-    __shared__ uint32_t dbase[256];
+    __shared__ uint32_t gbase[256];   // global position of this block's first item of digit d
+    __shared__ uint32_t lbase[256];   // block-local position of the first item of digit d
     __shared__ uint32_t wsum[kWaves];
+    __shared__ uint32_t skey[kSortTile];
+    __shared__ uint32_t sval[kSortTile];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const uint32_t mask = (1u << nbits) - 1u;
-    // digit base: exclusive scan of totals + this block's scanned count
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) wcnt[k][tid] = 0;
+    // global digit base: exclusive scan of totals + this block's scanned count
     {
         const uint32_t v = totals[tid];
         uint32_t x = v;
@@ -128,16 +135,15 @@ __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict
             if (lane >= o) x += y;
         }
         if (lane == 63) wsum[w] = x;
-#pragma unroll
-        for (int k = 0; k < kWaves; ++k) wcnt[k][tid] = 0;
         __syncthreads();
         uint32_t pre = 0;
 #pragma unroll
         for (int k = 0; k < kWaves; ++k) pre += (k < w) ? wsum[k] : 0u;
-        dbase[tid] = pre + x - v + hist[(size_t)tid * nb + blockIdx.x];
+        gbase[tid] = pre + x - v + hist[(size_t)tid * nb + blockIdx.x];
     }
     __syncthreads();
-    const long long base = (long long)blockIdx.x * kSortTile + (long long)w * kWaveItems;
+    const long long bbase = (long long)blockIdx.x * kSortTile;
+    const long long base = bbase + (long long)w * kWaveItems;
     uint32_t key[kI], val[kI], rank[kI];
     const uint64_t lt = lanemask_lt();
 #pragma unroll
@@ -146,6 +152,11 @@ __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict
         const bool valid = idx < n;
         key[r] = valid ? keys_in[idx] : 0xFFFFFFFFu;
         val[r] = valid ? (vals_in ? vals_in[idx] : (uint32_t)idx) : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < kI; ++r) {
+        const long long idx = base + r * 64 + lane;
+        const bool valid = idx < n;
         const uint32_t d = (key[r] >> shift) & mask;
         const uint64_t active = __ballot(valid);
         const uint64_t peers = match_digit(d, nbits, active);
@@ -155,13 +166,27 @@ __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict
     }
     __syncthreads();
     {
-        uint32_t off = dbase[tid];
+        // per digit: wave prefixes (in place) and the block count; block-local digit starts
+        uint32_t c = 0;
 #pragma unroll
         for (int k = 0; k < kWaves; ++k) {
-            const uint32_t c = wcnt[k][tid];
-            wcnt[k][tid] = off;
-            off += c;
+            const uint32_t t = wcnt[k][tid];
+            wcnt[k][tid] = c;
+            c += t;
         }
+        uint32_t x = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        __syncthreads();  // wsum reuse
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        uint32_t pre = 0;
+#pragma unroll
+        for (int k = 0; k < kWaves; ++k) pre += (k < w) ? wsum[k] : 0u;
+        lbase[tid] = pre + x - c;
     }
     __syncthreads();
 #pragma unroll
@@ -169,10 +194,20 @@ __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict
         const long long idx = base + r * 64 + lane;
         if (idx < n) {
             const uint32_t d = (key[r] >> shift) & mask;
-            const uint32_t pos = wcnt[w][d] + rank[r];
-            keys_out[pos] = key[r];
-            vals_out[pos] = val[r];
+            const uint32_t lp = lbase[d] + wcnt[w][d] + rank[r];
+            skey[lp] = key[r];
+            sval[lp] = val[r];
         }
+    }
+    __syncthreads();
+    const int count = (n - bbase) < kSortTile ? (int)(n - bbase) : kSortTile;
+#pragma unroll 4
+    for (int i = tid; i < count; i += kB) {
+        const uint32_t k = skey[i];
+        const uint32_t d = (k >> shift) & mask;
+        const uint32_t pos = gbase[d] + (uint32_t)i - lbase[d];
+        keys_out[pos] = k;
+        vals_out[pos] = sval[i];
     }
 }
 
@@ -263,7 +298,8 @@ __global__ __launch_bounds__(kB) void scan_downsweep(const uint32_t* __restrict_
     }
 }
 
-// ---- F3 duplicate ----
+// ---- F3 duplicate: wave-cooperative expansion (one wave = 64 consecutive ranks, whose
+// instances are contiguous; lanes write consecutive instances -> coalesced stores) ----
 __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restrict__ gid_by_rank,
                                                         const uint32_t* __restrict__ offsets,
                                                         const uint32_t* __restrict__ tiles,
@@ -272,35 +308,59 @@ __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restri
                                                         uint32_t* __restrict__ inst_start,
                                                         uint32_t* __restrict__ tkey,
                                                         uint32_t* __restrict__ inst_gid) {
-    const int r = blockIdx.x * 256 + threadIdx.x;
-    if (r >= P) return;
-    const uint32_t g = gid_by_rank[r];
-    const uint32_t nt = tiles[g];
-    const uint32_t end = offsets[r];
-    uint32_t j = end - nt;
-    inst_start[g] = j;
-    if (nt == 0) return;
-    const uint2 rr = rect[g];
-    const uint32_t rmin = rr.x, rmax = rr.y;
-    const int minx = rmin & 0xFFFF, miny = rmin >> 16, maxx = rmax & 0xFFFF, maxy = rmax >> 16;
-    const int y0 = miny > ty0 ? miny : ty0, y1 = maxy < ty1 ? maxy : ty1;
-    for (int y = y0; y < y1; ++y)
-        for (int x = minx; x < maxx; ++x) {
-            tkey[j] = (uint32_t)(y * grid_x + x);
-            inst_gid[j] = g;
-            ++j;
-        }
+    __shared__ uint32_t s_start[kWaves][64], s_g[kWaves][64], s_w[kWaves][64], s_x0[kWaves][64],
+        s_y0[kWaves][64];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int r = blockIdx.x * 256 + tid;
+    const bool valid = r < P;
+    uint32_t g = 0, nt = 0, end = 0;
+    if (valid) {
+        g = gid_by_rank[r];
+        nt = tiles[g];
+        end = offsets[r];
+        inst_start[g] = end - nt;
+    }
+    uint32_t minx = 0, maxx = 0, y0 = 0;
+    if (nt) {
+        const uint2 rr = rect[g];
+        minx = rr.x & 0xFFFF;
+        maxx = rr.y & 0xFFFF;
+        const uint32_t miny = rr.x >> 16;
+        y0 = miny > (uint32_t)ty0 ? miny : (uint32_t)ty0;
+    }
+    const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane((int)(end - nt));
+    const uint64_t vmask = __ballot(valid);
+    if (vmask == 0) return;
+    const int last_lane = 63 - __builtin_clzll(vmask);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)end, last_lane) - first;
+    s_start[w][lane] = valid ? end - nt - first : 0xFFFFFFFFu;
+    s_g[w][lane] = g;
+    s_w[w][lane] = maxx - minx;
+    s_x0[w][lane] = minx;
+    s_y0[w][lane] = y0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (uint32_t i = lane; i < total; i += 64) {
+        // owner = last lane whose start <= i (lanes with no instances never own one)
+        int o = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1)
+            if (s_start[w][o + step] <= i) o += step;
+        const uint32_t local = i - s_start[w][o];
+        const uint32_t wd = s_w[w][o];
+        const uint32_t dy = local / wd, dx = local - dy * wd;
+        tkey[first + i] = (s_y0[w][o] + dy) * (uint32_t)grid_x + s_x0[w][o] + dx;
+        inst_gid[first + i] = s_g[w][o];
+    }
+    (void)ty1;
 }
 
-// ---- F5 finalize ----
-__global__ __launch_bounds__(256) void finalize_kernel(const uint32_t* __restrict__ stile,
-                                                       const uint32_t* __restrict__ sj,
-                                                       const uint32_t* __restrict__ inst_gid,
-                                                       long long K, uint32_t* __restrict__ sgid,
+// ---- F5 finalize: tile ranges from the sorted keys ----
+__global__ __launch_bounds__(256) void finalize_kernel(const uint32_t* __restrict__ stile, long long K,
                                                        uint2* __restrict__ ranges) {
     const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
     if (i >= K) return;
-    sgid[i] = inst_gid[sj[i]];
     const uint32_t t = stile[i];
     if (i == 0 || stile[i - 1] != t) ranges[t].x = (uint32_t)i;
     if (i == K - 1 || stile[i + 1] != t) ranges[t].y = (uint32_t)(i + 1);
@@ -353,11 +413,9 @@ int launch_duplicate(const uint32_t* gid_by_rank, const uint32_t* offsets, const
     return (int)hipGetLastError();
 }
 
-int launch_finalize(const uint32_t* sorted_tile, const uint32_t* sorted_j, const uint32_t* inst_gid,
-                    long long K, uint32_t* sorted_gid, uint2* ranges, hipStream_t s) {
+int launch_finalize(const uint32_t* sorted_tile, long long K, uint2* ranges, hipStream_t s) {
     if (K <= 0) return 0;
-    hipLaunchKernelGGL(finalize_kernel, dim3(div_up(K, 256)), dim3(256), 0, s, sorted_tile, sorted_j,
-                       inst_gid, K, sorted_gid, ranges);
+    hipLaunchKernelGGL(finalize_kernel, dim3(div_up(K, 256)), dim3(256), 0, s, sorted_tile, K, ranges);
     return (int)hipGetLastError();
 }
 
