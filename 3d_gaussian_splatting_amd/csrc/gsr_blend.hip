@@ -614,6 +614,289 @@ __global__ __launch_bounds__(64) void blend_backward_f2b_kernel(const BlendGeom 
     }
 }
 
+
+// Forward with the record gathers software-pipelined: batch b+1's records (and batch b+2's
+// Gaussian ids) are loaded into registers while batch b is blended from LDS, so the
+// gather latency (L2 / Infinity Cache / HBM, 500-900 cycles) is off the critical path.
+__global__ __launch_bounds__(64) void blend_forward_v3_kernel(const BlendGeom geo,
+                                                              const uint2* __restrict__ ranges,
+                                                              const uint32_t* __restrict__ sorted_gid,
+                                                              const float4* __restrict__ rec,
+                                                              float* __restrict__ out_color,
+                                                              float* __restrict__ final_T,
+                                                              uint32_t* __restrict__ n_contrib,
+                                                              float* __restrict__ accum) {
+    __shared__ float4 srec[64 * 3];
+    const int tile = xcd_tile(blockIdx.x, geo.nwg) + geo.ty0 * geo.grid_x;
+    const int tx = tile % geo.grid_x, ty = tile / geo.grid_x;
+    const int lane = threadIdx.x;
+    const int px = tx * kTile + (lane & 15);
+    const float pfx = (float)px;
+    const float bx0 = (float)(tx * kTile), by0 = (float)(ty * kTile);
+    float pfy[kPPL], T[kPPL], Tf[kPPL], C0[kPPL], C1[kPPL], C2[kPPL];
+    uint32_t last[kPPL];
+#pragma unroll
+    for (int p = 0; p < kPPL; ++p) {
+        const int py = ty * kTile + (lane >> 4) + 4 * p;
+        pfy[p] = (float)py;
+        T[p] = (px < geo.W && py < geo.H) ? 1.0f : 0.0f;
+        Tf[p] = 1.0f;
+        C0[p] = C1[p] = C2[p] = 0.0f;
+        last[p] = 0;
+    }
+    const uint2 range = ranges[tile];
+    const int n = (int)(range.y - range.x);
+    // prologue: ids of batches 0 and 1, records of batch 0
+    uint32_t g_next = (64 + lane < n) ? sorted_gid[range.x + 64 + lane] : 0u;
+    float4 p0 = make_float4(0.f, 0.f, 0.f, 0.f), p1 = p0, p2 = p0;
+    if (lane < n) {
+        const float4* r = rec + 3 * (size_t)sorted_gid[range.x + lane];
+        p0 = r[0];
+        p1 = r[1];
+        p2 = r[2];
+    }
+    for (int base = 0; base < n; base += 64) {
+        uint32_t live = 0;
+#pragma unroll
+        for (int p = 0; p < kPPL; ++p) live |= __all(T[p] == 0.0f) ? 0u : (1u << p);
+        if (live == 0) break;
+        uint32_t smask = 0;
+        if (base + lane < n) {
+            srec[3 * lane + 0] = p0;
+            srec[3 * lane + 1] = p1;
+            srec[3 * lane + 2] = p2;
+            smask = stripe_mask(p0, p2, bx0, by0);
+        }
+        __syncthreads();
+        // prefetch: records of batch base+64, id of batch base+128
+        if (base + 64 + lane < n) {
+            const float4* r = rec + 3 * (size_t)g_next;
+            p0 = r[0];
+            p1 = r[1];
+            p2 = r[2];
+        }
+        g_next = (base + 128 + lane < n) ? sorted_gid[range.x + base + 128 + lane] : 0u;
+        uint64_t todo = __ballot((smask & live) != 0u);
+        int visited = 0;
+        while (todo) {
+            const int k = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)smask, k) & live;
+            const float4 r0 = srec[3 * k + 0];
+            const float4 r1 = srec[3 * k + 1];
+            const float rb = srec[3 * k + 2].x;
+            const uint32_t idx = (uint32_t)(base + k + 1);
+#pragma unroll
+            for (int p = 0; p < kPPL; ++p) {
+                if (!(m & (1u << p))) continue;  // wave-uniform
+                const float dx = r0.x - pfx, dy = r0.y - pfy[p];
+                const float pw = fmaf(r0.z * dx, dx, fmaf(r0.w * dx, dy, r1.x * dy * dy));
+                float a = fminf(0.99f, r1.y * __builtin_amdgcn_exp2f(pw));
+                a = pw <= 0.0f ? a : 0.0f;
+                a = a >= (1.0f / 255.0f) ? a : 0.0f;
+                const float tT = T[p] * (1.0f - a);
+                const bool ok = tT >= 0.0001f;
+                const float w = ok ? a * T[p] : 0.0f;
+                C0[p] = fmaf(r1.z, w, C0[p]);
+                C1[p] = fmaf(r1.w, w, C1[p]);
+                C2[p] = fmaf(rb, w, C2[p]);
+                const bool used = w > 0.0f;
+                last[p] = used ? idx : last[p];
+                Tf[p] = used ? tT : Tf[p];
+                T[p] = a > 0.0f ? (ok ? tT : 0.0f) : T[p];
+            }
+            if ((++visited & 7) == 0) {
+                uint32_t lv = 0;
+#pragma unroll
+                for (int p = 0; p < kPPL; ++p) lv |= __all(T[p] == 0.0f) ? 0u : (1u << p);
+                live = lv;
+                if (live == 0) break;
+            }
+        }
+        __syncthreads();
+    }
+    const size_t npix = (size_t)geo.W * geo.H;
+#pragma unroll
+    for (int p = 0; p < kPPL; ++p) {
+        const int py = ty * kTile + (lane >> 4) + 4 * p;
+        if (px < geo.W && py < geo.H) {
+            const size_t pix = (size_t)py * geo.W + px;
+            final_T[pix] = Tf[p];
+            n_contrib[pix] = last[p];
+            accum[pix] = C0[p];
+            accum[npix + pix] = C1[p];
+            accum[2 * npix + pix] = C2[p];
+            out_color[pix] = C0[p] + Tf[p] * geo.bg0;
+            out_color[npix + pix] = C1[p] + Tf[p] * geo.bg1;
+            out_color[2 * npix + pix] = C2[p] + Tf[p] * geo.bg2;
+        }
+    }
+}
+
+template <bool SLOT_CULL>
+__global__ __launch_bounds__(64) void blend_backward_f2b_pf_kernel(const BlendGeom geo,
+                                                                const uint2* __restrict__ ranges,
+                                                                const uint32_t* __restrict__ sorted_gid,
+                                                                const uint32_t* __restrict__ inst_start,
+                                                                const uint2* __restrict__ rect,
+                                                                const float4* __restrict__ rec,
+                                                                const float* __restrict__ final_T,
+                                                                const uint32_t* __restrict__ n_contrib,
+                                                                const float* __restrict__ accum,
+                                                                const float* __restrict__ dL_dpix,
+                                                                float* __restrict__ partial) {
+    __shared__ float4 srec[64 * 3];
+    __shared__ float smom[64 * 12];
+    const int tile = xcd_tile(blockIdx.x, geo.nwg) + geo.ty0 * geo.grid_x;
+    const int tx = tile % geo.grid_x, ty = tile / geo.grid_x;
+    const int lane = threadIdx.x;
+    const int px = tx * kTile + (lane & 15);
+    const float pfx = (float)px;
+    const float bx0 = (float)(tx * kTile), by0 = (float)(ty * kTile);
+    const size_t npix = (size_t)geo.W * geo.H;
+    const float hw = 0.5f * (float)geo.W, hh = 0.5f * (float)geo.H;
+    const int row = lane >> 4;
+    float T[kPPL], Sp[kPPL], cb[kPPL], dp0[kPPL], dp1[kPPL], dp2[kPPL];
+    uint32_t lastc[kPPL];
+    uint32_t maxlast = 0;
+#pragma unroll
+    for (int p = 0; p < kPPL; ++p) {
+        const int py = ty * kTile + row + 4 * p;
+        const bool in = px < geo.W && py < geo.H;
+        const size_t pix = in ? (size_t)py * geo.W + px : 0;
+        const float Tfin = in ? final_T[pix] : 1.0f;
+        lastc[p] = in ? n_contrib[pix] : 0u;
+        dp0[p] = in ? dL_dpix[pix] : 0.0f;
+        dp1[p] = in ? dL_dpix[npix + pix] : 0.0f;
+        dp2[p] = in ? dL_dpix[2 * npix + pix] : 0.0f;
+        const float sdp = in ? accum[pix] * dp0[p] + accum[npix + pix] * dp1[p] + accum[2 * npix + pix] * dp2[p]
+                             : 0.0f;
+        cb[p] = sdp + Tfin * (geo.bg0 * dp0[p] + geo.bg1 * dp1[p] + geo.bg2 * dp2[p]);
+        T[p] = 1.0f;
+        Sp[p] = 0.0f;
+        maxlast = maxlast > lastc[p] ? maxlast : lastc[p];
+    }
+    maxlast = wave_max_u32(maxlast);
+    const uint2 range = ranges[tile];
+    const int n = (int)(range.y - range.x);
+    // prologue: batch 0's id, rect, inst_start and record; batch 1's id (software pipeline)
+    uint32_t g_cur = lane < n ? sorted_gid[range.x + lane] : 0u;
+    uint32_t g_next = (64 + lane < n) ? sorted_gid[range.x + 64 + lane] : 0u;
+    uint2 rr_p = make_uint2(0u, 0u);
+    uint32_t is_p = 0;
+    float4 p0 = make_float4(0.f, 0.f, 0.f, 0.f), p1 = p0, p2 = p0;
+    if (lane < n) {
+        rr_p = rect[g_cur];
+        is_p = inst_start[g_cur];
+        if (lane < (int)maxlast) {
+            const float4* r = rec + 3 * (size_t)g_cur;
+            p0 = r[0];
+            p1 = r[1];
+            p2 = r[2];
+        }
+    }
+    for (int base = 0; base < n; base += 64) {
+        const int cnt = (n - base) < 64 ? (n - base) : 64;
+        const int e_l = base + lane;
+        uint32_t jl = 0, smask = 0;
+        const float4 q0 = p0, q1 = p1;
+        if (lane < cnt) {
+            const int minx = rr_p.x & 0xFFFF, miny = rr_p.x >> 16, maxx = rr_p.y & 0xFFFF;
+            const int y0 = miny > geo.ty0 ? miny : geo.ty0;
+            jl = is_p + (uint32_t)((ty - y0) * (maxx - minx) + (tx - minx));
+            if (e_l < (int)maxlast) {
+                srec[3 * lane + 0] = p0;
+                srec[3 * lane + 1] = p1;
+                srec[3 * lane + 2] = p2;
+                smask = stripe_mask(p0, p2, bx0, by0);
+            }
+        }
+        // prefetch batch base+64 (rect, inst_start, record) and the id of batch base+128
+        {
+            const int e_n = base + 64 + lane;
+            if (e_n < n) {
+                rr_p = rect[g_next];
+                is_p = inst_start[g_next];
+                if (e_n < (int)maxlast) {
+                    const float4* r = rec + 3 * (size_t)g_next;
+                    p0 = r[0];
+                    p1 = r[1];
+                    p2 = r[2];
+                }
+            }
+            g_next = (base + 128 + lane < n) ? sorted_gid[range.x + base + 128 + lane] : 0u;
+        }
+#pragma unroll
+        for (int c = 0; c < 12; ++c) smom[lane * 12 + c] = 0.0f;
+        __syncthreads();
+        uint64_t todo = __ballot(smask != 0u);
+        while (todo) {
+            const int k = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)smask, k);
+            const uint32_t e = (uint32_t)(base + k);
+            const float4 r0 = srec[3 * k + 0];
+            const float4 r1 = srec[3 * k + 1];
+            const float rb = srec[3 * k + 2].x;
+            float v[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            bool any = false;
+#pragma unroll
+            for (int p = 0; p < kPPL; ++p) {
+                if (SLOT_CULL && !(m & (1u << p))) continue;  // wave-uniform
+                const float dx = r0.x - pfx, dy = r0.y - (by0 + (float)(row + 4 * p));
+                const float pw = fmaf(r0.z * dx, dx, fmaf(r0.w * dx, dy, r1.x * dy * dy));
+                const float G = __builtin_amdgcn_exp2f(pw);
+                const float oG = r1.y * G;
+                const float alpha = fminf(0.99f, oG);
+                const bool valid = (SLOT_CULL || (m & (1u << p))) && e < lastc[p] && pw <= 0.0f &&
+                                   alpha >= (1.0f / 255.0f);
+                if (valid) {
+                    any = true;
+                    const float w = alpha * T[p];
+                    const float cdp = fmaf(r1.z, dp0[p], fmaf(r1.w, dp1[p], rb * dp2[p]));
+                    Sp[p] = fmaf(w, cdp, Sp[p]);
+                    const float one_m = 1.0f - alpha;
+                    const float dLda = fmaf(T[p], cdp, -(cb[p] - Sp[p]) * __builtin_amdgcn_rcpf(one_m));
+                    T[p] = T[p] * one_m;
+                    v[6] = fmaf(w, dp0[p], v[6]);
+                    v[7] = fmaf(w, dp1[p], v[7]);
+                    v[8] = fmaf(w, dp2[p], v[8]);
+                    v[5] = fmaf(G, dLda, v[5]);
+                    const float sv = oG * dLda;
+                    const float sx = sv * dx, sy = sv * dy;
+                    v[0] += sx;
+                    v[1] += sy;
+                    v[2] = fmaf(sx, dx, v[2]);
+                    v[3] = fmaf(sx, dy, v[3]);
+                    v[4] = fmaf(sy, dy, v[4]);
+                }
+            }
+            if (__any(any)) {
+                row_reduce(v);
+                const float t0 = scatter4(v[0], v[1], v[2], v[3]);
+                const float t1 = scatter4(v[4], v[5], v[6], v[7]);
+                const float t2 = allreduce_rows(v[8]);
+                if ((lane & 15) == 0) {
+                    smom[k * 12 + row] = t0;
+                    smom[k * 12 + 4 + row] = t1;
+                    if (row == 0) smom[k * 12 + 8] = t2;
+                }
+            }
+        }
+        __syncthreads();
+        if (lane < cnt) {
+            const float* mo = smom + lane * 12;
+            const float Sx = mo[0], Sy = mo[1], Sxx = mo[2], Sxy = mo[3], Syy = mo[4], S0 = mo[5];
+            const float A = -2.0f * kLn2 * q0.z, B = -kLn2 * q0.w, C = -2.0f * kLn2 * q1.x;
+            float4* dst = reinterpret_cast<float4*>(partial + (size_t)kPart * jl);
+            dst[0] = make_float4((-A * Sx - B * Sy) * hw, (-C * Sy - B * Sx) * hh, -0.5f * Sxx, -Sxy);
+            dst[1] = make_float4(-0.5f * Syy, S0, mo[6], mo[7]);
+            dst[2] = make_float4(mo[8], 0.f, 0.f, 0.f);
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 // Kernel-variant selector for A/B timing (bench/ablation only; default = shipped variant).
@@ -642,7 +925,10 @@ int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int 
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1);
     if (geo.nwg <= 0) return 0;
     const int v = variant("GSR_FWD_VARIANT", 2);
-    if (v == 2)
+    if (v == 3)
+        hipLaunchKernelGGL(blend_forward_v3_kernel, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid, rec,
+                           out_color, final_T, n_contrib, accum);
+    else if (v == 2)
         hipLaunchKernelGGL(blend_forward_v2_kernel, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid, rec,
                            out_color, final_T, n_contrib, accum);
     else if (v == 1)
@@ -662,7 +948,10 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1);
     if (geo.nwg <= 0) return 0;
     const int v = variant("GSR_BWD_VARIANT", 2);
-    if (v == 2)
+    if (v == 3)
+        hipLaunchKernelGGL(blend_backward_f2b_pf_kernel<true>, dim3(geo.nwg), dim3(64), 0, s, geo, ranges,
+                           sorted_gid, inst_start, rect, rec, final_T, n_contrib, accum, dL_dpix, partial);
+    else if (v == 2)
         hipLaunchKernelGGL(blend_backward_f2b_kernel<true>, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid,
                            inst_start, rect, rec, final_T, n_contrib, accum, dL_dpix, partial);
     else if (v == 1)
