@@ -897,6 +897,297 @@ __global__ __launch_bounds__(64) void blend_backward_f2b_pf_kernel(const BlendGe
     }
 }
 
+
+// ---- mask-specialised bodies: every active stripe of a record in ONE basic block ----
+struct FwdState {
+    float T[kPPL], Tf[kPPL], C0[kPPL], C1[kPPL], C2[kPPL];
+    uint32_t last[kPPL];
+};
+
+template <uint32_t M>
+__device__ __forceinline__ void fwd_record(FwdState& st, const float (&pfy)[kPPL], float pfx, const float4 r0,
+                                           const float4 r1, float rb, uint32_t idx) {
+#pragma unroll
+    for (int p = 0; p < kPPL; ++p) {
+        {
+            if (!((M >> p) & 1u)) continue;
+            const float dx = r0.x - pfx, dy = r0.y - pfy[p];
+            const float pw = fmaf(r0.z * dx, dx, fmaf(r0.w * dx, dy, r1.x * dy * dy));
+            float a = fminf(0.99f, r1.y * __builtin_amdgcn_exp2f(pw));
+            a = pw <= 0.0f ? a : 0.0f;
+            a = a >= (1.0f / 255.0f) ? a : 0.0f;
+            const float tT = st.T[p] * (1.0f - a);
+            const bool ok = tT >= 0.0001f;
+            const float w = ok ? a * st.T[p] : 0.0f;
+            st.C0[p] = fmaf(r1.z, w, st.C0[p]);
+            st.C1[p] = fmaf(r1.w, w, st.C1[p]);
+            st.C2[p] = fmaf(rb, w, st.C2[p]);
+            const bool used = w > 0.0f;
+            st.last[p] = used ? idx : st.last[p];
+            st.Tf[p] = used ? tT : st.Tf[p];
+            st.T[p] = a > 0.0f ? (ok ? tT : 0.0f) : st.T[p];
+        }
+    }
+}
+
+__device__ __forceinline__ void fwd_dispatch(uint32_t m, FwdState& st, const float (&pfy)[kPPL], float pfx,
+                                             const float4 r0, const float4 r1, float rb, uint32_t idx) {
+    switch (m) {
+#define GSR_FWD_CASE(M) \
+    case M: fwd_record<M>(st, pfy, pfx, r0, r1, rb, idx); break;
+        GSR_FWD_CASE(1) GSR_FWD_CASE(2) GSR_FWD_CASE(3) GSR_FWD_CASE(4) GSR_FWD_CASE(5)
+        GSR_FWD_CASE(6) GSR_FWD_CASE(7) GSR_FWD_CASE(8) GSR_FWD_CASE(9) GSR_FWD_CASE(10)
+        GSR_FWD_CASE(11) GSR_FWD_CASE(12) GSR_FWD_CASE(13) GSR_FWD_CASE(14) GSR_FWD_CASE(15)
+#undef GSR_FWD_CASE
+        default: break;
+    }
+}
+
+__global__ __launch_bounds__(64) void blend_forward_v4_kernel(const BlendGeom geo,
+                                                              const uint2* __restrict__ ranges,
+                                                              const uint32_t* __restrict__ sorted_gid,
+                                                              const float4* __restrict__ rec,
+                                                              float* __restrict__ out_color,
+                                                              float* __restrict__ final_T,
+                                                              uint32_t* __restrict__ n_contrib,
+                                                              float* __restrict__ accum) {
+    __shared__ float4 srec[64 * 3];
+    const int tile = xcd_tile(blockIdx.x, geo.nwg) + geo.ty0 * geo.grid_x;
+    const int tx = tile % geo.grid_x, ty = tile / geo.grid_x;
+    const int lane = threadIdx.x;
+    const int px = tx * kTile + (lane & 15);
+    const float pfx = (float)px;
+    const float bx0 = (float)(tx * kTile), by0 = (float)(ty * kTile);
+    float pfy[kPPL];
+    FwdState st;
+#pragma unroll
+    for (int p = 0; p < kPPL; ++p) {
+        const int py = ty * kTile + (lane >> 4) + 4 * p;
+        pfy[p] = (float)py;
+        st.T[p] = (px < geo.W && py < geo.H) ? 1.0f : 0.0f;
+        st.Tf[p] = 1.0f;
+        st.C0[p] = st.C1[p] = st.C2[p] = 0.0f;
+        st.last[p] = 0;
+    }
+    const uint2 range = ranges[tile];
+    const int n = (int)(range.y - range.x);
+    for (int base = 0; base < n; base += 64) {
+        uint32_t live = 0;
+#pragma unroll
+        for (int p = 0; p < kPPL; ++p) live |= __all(st.T[p] == 0.0f) ? 0u : (1u << p);
+        if (live == 0) break;
+        uint32_t smask = 0;
+        if (base + lane < n) {
+            const uint32_t g = sorted_gid[range.x + base + lane];
+            const float4* r = rec + 3 * (size_t)g;
+            const float4 r0 = r[0], r1 = r[1], r2 = r[2];
+            srec[3 * lane + 0] = r0;
+            srec[3 * lane + 1] = r1;
+            srec[3 * lane + 2] = r2;
+            smask = stripe_mask(r0, r2, bx0, by0);
+        }
+        __syncthreads();
+        uint64_t todo = __ballot((smask & live) != 0u);
+        int visited = 0;
+        while (todo) {
+            const int k = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)smask, k) & live;
+            const float4 r0 = srec[3 * k + 0];
+            const float4 r1 = srec[3 * k + 1];
+            const float rb = srec[3 * k + 2].x;
+            fwd_dispatch(m, st, pfy, pfx, r0, r1, rb, (uint32_t)(base + k + 1));
+            if ((++visited & 7) == 0) {
+                uint32_t lv = 0;
+#pragma unroll
+                for (int p = 0; p < kPPL; ++p) lv |= __all(st.T[p] == 0.0f) ? 0u : (1u << p);
+                live = lv;
+                if (live == 0) break;
+            }
+        }
+        __syncthreads();
+    }
+    const size_t npix = (size_t)geo.W * geo.H;
+#pragma unroll
+    for (int p = 0; p < kPPL; ++p) {
+        const int py = ty * kTile + (lane >> 4) + 4 * p;
+        if (px < geo.W && py < geo.H) {
+            const size_t pix = (size_t)py * geo.W + px;
+            final_T[pix] = st.Tf[p];
+            n_contrib[pix] = st.last[p];
+            accum[pix] = st.C0[p];
+            accum[npix + pix] = st.C1[p];
+            accum[2 * npix + pix] = st.C2[p];
+            out_color[pix] = st.C0[p] + st.Tf[p] * geo.bg0;
+            out_color[npix + pix] = st.C1[p] + st.Tf[p] * geo.bg1;
+            out_color[2 * npix + pix] = st.C2[p] + st.Tf[p] * geo.bg2;
+        }
+    }
+}
+
+// ---- backward, mask-specialised ----
+struct BwdState {
+    float T[kPPL], Sp[kPPL], cb[kPPL], dp0[kPPL], dp1[kPPL], dp2[kPPL];
+    uint32_t lastc[kPPL];
+};
+
+template <uint32_t M>
+__device__ __forceinline__ bool bwd_record(BwdState& st, float (&v)[9], float pfx, float by0, int row,
+                                           const float4 r0, const float4 r1, float rb, uint32_t e) {
+    bool any = false;
+#pragma unroll
+    for (int p = 0; p < kPPL; ++p) {
+        if (!((M >> p) & 1u)) continue;
+        const float dx = r0.x - pfx, dy = r0.y - (by0 + (float)(row + 4 * p));
+        const float pw = fmaf(r0.z * dx, dx, fmaf(r0.w * dx, dy, r1.x * dy * dy));
+        const float G = __builtin_amdgcn_exp2f(pw);
+        const float oG = r1.y * G;
+        const float alpha = fminf(0.99f, oG);
+        const bool valid = e < st.lastc[p] && pw <= 0.0f && alpha >= (1.0f / 255.0f);
+        // predicated (no divergent branch): invalid pairs contribute exact zeros
+        const float a = valid ? alpha : 0.0f;
+        const float w = a * st.T[p];
+        const float cdp = fmaf(r1.z, st.dp0[p], fmaf(r1.w, st.dp1[p], rb * st.dp2[p]));
+        st.Sp[p] = fmaf(w, cdp, st.Sp[p]);
+        const float one_m = 1.0f - a;
+        const float dLda = fmaf(st.T[p], cdp, -(st.cb[p] - st.Sp[p]) * __builtin_amdgcn_rcpf(one_m));
+        st.T[p] = st.T[p] * one_m;
+        v[6] = fmaf(w, st.dp0[p], v[6]);
+        v[7] = fmaf(w, st.dp1[p], v[7]);
+        v[8] = fmaf(w, st.dp2[p], v[8]);
+        const float Gv = valid ? G : 0.0f;
+        v[5] = fmaf(Gv, dLda, v[5]);
+        const float sv = r1.y * Gv * dLda;
+        const float sx = sv * dx, sy = sv * dy;
+        v[0] += sx;
+        v[1] += sy;
+        v[2] = fmaf(sx, dx, v[2]);
+        v[3] = fmaf(sx, dy, v[3]);
+        v[4] = fmaf(sy, dy, v[4]);
+        any = any || valid;
+    }
+    return any;
+}
+
+__device__ __forceinline__ bool bwd_dispatch(uint32_t m, BwdState& st, float (&v)[9], float pfx, float by0,
+                                             int row, const float4 r0, const float4 r1, float rb, uint32_t e) {
+    switch (m) {
+#define GSR_BWD_CASE(M) \
+    case M: return bwd_record<M>(st, v, pfx, by0, row, r0, r1, rb, e);
+        GSR_BWD_CASE(1) GSR_BWD_CASE(2) GSR_BWD_CASE(3) GSR_BWD_CASE(4) GSR_BWD_CASE(5)
+        GSR_BWD_CASE(6) GSR_BWD_CASE(7) GSR_BWD_CASE(8) GSR_BWD_CASE(9) GSR_BWD_CASE(10)
+        GSR_BWD_CASE(11) GSR_BWD_CASE(12) GSR_BWD_CASE(13) GSR_BWD_CASE(14) GSR_BWD_CASE(15)
+#undef GSR_BWD_CASE
+        default: return false;
+    }
+}
+
+__global__ __launch_bounds__(64) void blend_backward_v4_kernel(const BlendGeom geo,
+                                                               const uint2* __restrict__ ranges,
+                                                               const uint32_t* __restrict__ sorted_gid,
+                                                               const uint32_t* __restrict__ inst_start,
+                                                               const uint2* __restrict__ rect,
+                                                               const float4* __restrict__ rec,
+                                                               const float* __restrict__ final_T,
+                                                               const uint32_t* __restrict__ n_contrib,
+                                                               const float* __restrict__ accum,
+                                                               const float* __restrict__ dL_dpix,
+                                                               float* __restrict__ partial) {
+    __shared__ float4 srec[64 * 3];
+    __shared__ float smom[64 * 12];
+    const int tile = xcd_tile(blockIdx.x, geo.nwg) + geo.ty0 * geo.grid_x;
+    const int tx = tile % geo.grid_x, ty = tile / geo.grid_x;
+    const int lane = threadIdx.x;
+    const int px = tx * kTile + (lane & 15);
+    const float pfx = (float)px;
+    const float bx0 = (float)(tx * kTile), by0 = (float)(ty * kTile);
+    const size_t npix = (size_t)geo.W * geo.H;
+    const float hw = 0.5f * (float)geo.W, hh = 0.5f * (float)geo.H;
+    const int row = lane >> 4;
+    BwdState st;
+    uint32_t maxlast = 0;
+#pragma unroll
+    for (int p = 0; p < kPPL; ++p) {
+        const int py = ty * kTile + row + 4 * p;
+        const bool in = px < geo.W && py < geo.H;
+        const size_t pix = in ? (size_t)py * geo.W + px : 0;
+        const float Tfin = in ? final_T[pix] : 1.0f;
+        st.lastc[p] = in ? n_contrib[pix] : 0u;
+        st.dp0[p] = in ? dL_dpix[pix] : 0.0f;
+        st.dp1[p] = in ? dL_dpix[npix + pix] : 0.0f;
+        st.dp2[p] = in ? dL_dpix[2 * npix + pix] : 0.0f;
+        const float sdp = in ? accum[pix] * st.dp0[p] + accum[npix + pix] * st.dp1[p] +
+                                   accum[2 * npix + pix] * st.dp2[p]
+                             : 0.0f;
+        st.cb[p] = sdp + Tfin * (geo.bg0 * st.dp0[p] + geo.bg1 * st.dp1[p] + geo.bg2 * st.dp2[p]);
+        st.T[p] = 1.0f;
+        st.Sp[p] = 0.0f;
+        maxlast = maxlast > st.lastc[p] ? maxlast : st.lastc[p];
+    }
+    maxlast = wave_max_u32(maxlast);
+    const uint2 range = ranges[tile];
+    const int n = (int)(range.y - range.x);
+    for (int base = 0; base < n; base += 64) {
+        const int cnt = (n - base) < 64 ? (n - base) : 64;
+        const int e_l = base + lane;
+        uint32_t jl = 0, smask = 0;
+        float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0;
+        if (lane < cnt) {
+            const uint32_t g = sorted_gid[range.x + e_l];
+            const uint2 rr = rect[g];
+            const int minx = rr.x & 0xFFFF, miny = rr.x >> 16, maxx = rr.y & 0xFFFF;
+            const int y0 = miny > geo.ty0 ? miny : geo.ty0;
+            jl = inst_start[g] + (uint32_t)((ty - y0) * (maxx - minx) + (tx - minx));
+            if (e_l < (int)maxlast) {
+                const float4* r = rec + 3 * (size_t)g;
+                q0 = r[0];
+                q1 = r[1];
+                const float4 r2 = r[2];
+                srec[3 * lane + 0] = q0;
+                srec[3 * lane + 1] = q1;
+                srec[3 * lane + 2] = r2;
+                smask = stripe_mask(q0, r2, bx0, by0);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 12; ++c) smom[lane * 12 + c] = 0.0f;
+        __syncthreads();
+        uint64_t todo = __ballot(smask != 0u);
+        while (todo) {
+            const int k = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)smask, k);
+            const float4 r0 = srec[3 * k + 0];
+            const float4 r1 = srec[3 * k + 1];
+            const float rb = srec[3 * k + 2].x;
+            float v[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            const bool any = bwd_dispatch(m, st, v, pfx, by0, row, r0, r1, rb, (uint32_t)(base + k));
+            if (__any(any)) {
+                row_reduce(v);
+                const float t0 = scatter4(v[0], v[1], v[2], v[3]);
+                const float t1 = scatter4(v[4], v[5], v[6], v[7]);
+                const float t2 = allreduce_rows(v[8]);
+                if ((lane & 15) == 0) {
+                    smom[k * 12 + row] = t0;
+                    smom[k * 12 + 4 + row] = t1;
+                    if (row == 0) smom[k * 12 + 8] = t2;
+                }
+            }
+        }
+        __syncthreads();
+        if (lane < cnt) {
+            const float* mo = smom + lane * 12;
+            const float Sx = mo[0], Sy = mo[1], Sxx = mo[2], Sxy = mo[3], Syy = mo[4], S0 = mo[5];
+            const float A = -2.0f * kLn2 * q0.z, B = -kLn2 * q0.w, C = -2.0f * kLn2 * q1.x;
+            float4* dst = reinterpret_cast<float4*>(partial + (size_t)kPart * jl);
+            dst[0] = make_float4((-A * Sx - B * Sy) * hw, (-C * Sy - B * Sx) * hh, -0.5f * Sxx, -Sxy);
+            dst[1] = make_float4(-0.5f * Syy, S0, mo[6], mo[7]);
+            dst[2] = make_float4(mo[8], 0.f, 0.f, 0.f);
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 // Kernel-variant selector for A/B timing (bench/ablation only; default = shipped variant).
@@ -925,7 +1216,10 @@ int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int 
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1);
     if (geo.nwg <= 0) return 0;
     const int v = variant("GSR_FWD_VARIANT", 2);
-    if (v == 3)
+    if (v == 4)
+        hipLaunchKernelGGL(blend_forward_v4_kernel, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid, rec,
+                           out_color, final_T, n_contrib, accum);
+    else if (v == 3)
         hipLaunchKernelGGL(blend_forward_v3_kernel, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid, rec,
                            out_color, final_T, n_contrib, accum);
     else if (v == 2)
@@ -948,7 +1242,10 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1);
     if (geo.nwg <= 0) return 0;
     const int v = variant("GSR_BWD_VARIANT", 2);
-    if (v == 3)
+    if (v == 4)
+        hipLaunchKernelGGL(blend_backward_v4_kernel, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid,
+                           inst_start, rect, rec, final_T, n_contrib, accum, dL_dpix, partial);
+    else if (v == 3)
         hipLaunchKernelGGL(blend_backward_f2b_pf_kernel<true>, dim3(geo.nwg), dim3(64), 0, s, geo, ranges,
                            sorted_gid, inst_start, rect, rec, final_T, n_contrib, accum, dL_dpix, partial);
     else if (v == 2)

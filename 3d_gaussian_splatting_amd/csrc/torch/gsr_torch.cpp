@@ -6,7 +6,11 @@
 // allocator, created inside the C ABI's allocation callbacks and kept in the autograd context
 // until backward -- the library itself allocates nothing persistent.
 #include <c10/hip/HIPStream.h>
+#ifdef GSR_NO_PYBIND
+#include <torch/torch.h>
+#else
 #include <torch/extension.h>
+#endif
 
 #include <cmath>
 #include <stdexcept>
@@ -308,8 +312,9 @@ torch::Tensor eval_sh_colors(int D, const torch::Tensor& sh, const torch::Tensor
 }  // namespace gsr
 
 // ------------------------------------------------------------------------------------------
-// Python binding
+// Python binding (compile with -DGSR_NO_PYBIND when linking into a C++ executable)
 // ------------------------------------------------------------------------------------------
+#ifndef GSR_NO_PYBIND
 namespace py = pybind11;
 
 static gsr::RasterCamera cam_from_py(int w, int h, float tx, float ty, const std::vector<float>& v,
@@ -366,3 +371,4 @@ PYBIND11_MODULE(_gsr_torch, m) {
     m.def("eval_sh_colors", &gsr::eval_sh_colors);
     m.def("abi_version", []() { return gsr_abi_version(); });
 }
+#endif  // GSR_NO_PYBIND
