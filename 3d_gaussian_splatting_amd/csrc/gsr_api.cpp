@@ -330,7 +330,7 @@ static int backward_impl(const gsr_camera* cam, const gsr_gaussians* gs, const g
     }
     if (grad2d) {
         if (K > 0) {
-            GSR_STAGE(GSR_STAGE_GATHER, launch_gather_grad2d(v.inst_start, v.tiles, partial, P, grad2d, stream), "gather grad2d");
+            GSR_STAGE(GSR_STAGE_GATHER, launch_gather_grad2d(v.gid_by_rank, v.offsets, partial, P, grad2d, stream), "gather grad2d");
         } else {
             GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(grad2d, 0, sizeof(float) * kPart * (size_t)P, stream), "zero grad2d");
         }
@@ -373,22 +373,27 @@ int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raste
     hipStream_t stream = (hipStream_t)stream_;
     const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
     if (!bufs || !bufs->geom || !bufs->image || !dL_dpix) return fail(-1, "missing forward buffers / dL_dpix");
+    if (!alloc_scratch) return fail(-1, "null scratch allocator");
     int ty0, ty1;
     band(cam, rs, &ty0, &ty1);
-    const Views v = views(cam, gs->P, bufs);
+    const int P = gs->P;
+    const Views v = views(cam, P, bufs);
     const long long K = bufs->num_rendered;
-    float* partial = nullptr;
+    // two scratch blocks: per-instance partials (K x 48 B) and per-Gaussian grad2d (P x 48 B)
+    float* partial = static_cast<float*>(alloc_scratch(ctx, gsr_scratch_bytes((int32_t)K)));
+    float* grad2d = static_cast<float*>(alloc_scratch(ctx, sizeof(float) * kPart * (size_t)P));
+    if (!partial || !grad2d) return fail(-2, "allocation failed (scratch, K=%lld, P=%d)", K, P);
     if (K > 0) {
-        if (!alloc_scratch) return fail(-1, "null scratch allocator");
-        partial = static_cast<float*>(alloc_scratch(ctx, gsr_scratch_bytes((int32_t)K)));
-        if (!partial) return fail(-2, "allocation failed (scratch, K=%lld)", K);
         GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.inst_start, v.rect, v.rec,
                                             v.final_T, v.n_contrib, v.accum, dL_dpix, partial, stream),
                       "blend backward");
+        GSR_STAGE(GSR_STAGE_GATHER, launch_gather_grad2d(v.gid_by_rank, v.offsets, partial, P, grad2d, stream),
+                  "gather grad2d");
+    } else {
+        GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(grad2d, 0, sizeof(float) * kPart * (size_t)P, stream), "zero grad2d");
     }
-    // K == 0: no partials and no grad2d -> the kernel uses zero 2D gradients
     GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), v.depth_key, v.flags, v.inst_start, v.tiles,
-                                             partial, nullptr, grad_out(grads), stream),
+                                             nullptr, grad2d, grad_out(grads), stream),
                   "preprocess backward");
     return 0;
 }

@@ -1188,6 +1188,122 @@ __global__ __launch_bounds__(64) void blend_backward_v4_kernel(const BlendGeom g
     }
 }
 
+
+// Forward with NW waves per 16x16 tile (PPL = 4/NW pixels per lane; wave w owns rows
+// [w*16/NW, (w+1)*16/NW)).  The block stages 64*NW records per batch (one per thread) and
+// their per-stripe masks in LDS; each wave sweeps the records touching its own stripes.
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void blend_forward_nw_kernel(const BlendGeom geo,
+                                                                   const uint2* __restrict__ ranges,
+                                                                   const uint32_t* __restrict__ sorted_gid,
+                                                                   const float4* __restrict__ rec,
+                                                                   float* __restrict__ out_color,
+                                                                   float* __restrict__ final_T,
+                                                                   uint32_t* __restrict__ n_contrib,
+                                                                   float* __restrict__ accum) {
+    constexpr int PPL = kPPL / NW;
+    constexpr int BATCH = 64 * NW;
+    __shared__ float4 srec[BATCH * 3];
+    __shared__ uint32_t smk[BATCH];
+    const int tile = xcd_tile(blockIdx.x, geo.nwg) + geo.ty0 * geo.grid_x;
+    const int tx = tile % geo.grid_x, ty = tile / geo.grid_x;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int px = tx * kTile + (lane & 15);
+    const float pfx = (float)px;
+    const float bx0 = (float)(tx * kTile), by0 = (float)(ty * kTile);
+    // wave w owns global stripes [w*PPL, (w+1)*PPL)
+    float pfy[PPL], T[PPL], Tf[PPL], C0[PPL], C1[PPL], C2[PPL];
+    uint32_t last[PPL];
+#pragma unroll
+    for (int p = 0; p < PPL; ++p) {
+        const int py = ty * kTile + (lane >> 4) + 4 * (w * PPL + p);
+        pfy[p] = (float)py;
+        T[p] = (px < geo.W && py < geo.H) ? 1.0f : 0.0f;
+        Tf[p] = 1.0f;
+        C0[p] = C1[p] = C2[p] = 0.0f;
+        last[p] = 0;
+    }
+    const uint2 range = ranges[tile];
+    const int n = (int)(range.y - range.x);
+    for (int base = 0; base < n; base += BATCH) {
+        uint32_t live = 0;
+#pragma unroll
+        for (int p = 0; p < PPL; ++p) live |= __all(T[p] == 0.0f) ? 0u : (1u << p);
+        if (__syncthreads_or(live != 0) == 0) break;
+        if (base + tid < n) {
+            const uint32_t g = sorted_gid[range.x + base + tid];
+            const float4* r = rec + 3 * (size_t)g;
+            const float4 r0 = r[0], r1 = r[1], r2 = r[2];
+            srec[3 * tid + 0] = r0;
+            srec[3 * tid + 1] = r1;
+            srec[3 * tid + 2] = r2;
+            smk[tid] = stripe_mask(r0, r2, bx0, by0);
+        } else {
+            smk[tid] = 0u;
+        }
+        __syncthreads();
+        const int cnt = (n - base) < BATCH ? (n - base) : BATCH;
+        int visited = 0;
+        for (int c0 = 0; c0 < cnt && live; c0 += 64) {
+            const uint32_t mine = (smk[c0 + lane] >> (w * PPL)) & ((1u << PPL) - 1u);
+            uint64_t todo = __ballot((mine & live) != 0u && c0 + lane < cnt);
+            while (todo) {
+                const int kk = __builtin_ctzll(todo);
+                todo &= todo - 1;
+                const int k = c0 + kk;
+                const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)mine, kk) & live;
+                const float4 r0 = srec[3 * k + 0];
+                const float4 r1 = srec[3 * k + 1];
+                const float rb = srec[3 * k + 2].x;
+                const uint32_t idx = (uint32_t)(base + k + 1);
+#pragma unroll
+                for (int p = 0; p < PPL; ++p) {
+                    if (!(m & (1u << p))) continue;  // wave-uniform
+                    const float dx = r0.x - pfx, dy = r0.y - pfy[p];
+                    const float pw = fmaf(r0.z * dx, dx, fmaf(r0.w * dx, dy, r1.x * dy * dy));
+                    float a = fminf(0.99f, r1.y * __builtin_amdgcn_exp2f(pw));
+                    a = pw <= 0.0f ? a : 0.0f;
+                    a = a >= (1.0f / 255.0f) ? a : 0.0f;
+                    const float tT = T[p] * (1.0f - a);
+                    const bool ok = tT >= 0.0001f;
+                    const float wgt = ok ? a * T[p] : 0.0f;
+                    C0[p] = fmaf(r1.z, wgt, C0[p]);
+                    C1[p] = fmaf(r1.w, wgt, C1[p]);
+                    C2[p] = fmaf(rb, wgt, C2[p]);
+                    const bool used = wgt > 0.0f;
+                    last[p] = used ? idx : last[p];
+                    Tf[p] = used ? tT : Tf[p];
+                    T[p] = a > 0.0f ? (ok ? tT : 0.0f) : T[p];
+                }
+                if ((++visited & 7) == 0) {
+                    uint32_t lv = 0;
+#pragma unroll
+                    for (int p = 0; p < PPL; ++p) lv |= __all(T[p] == 0.0f) ? 0u : (1u << p);
+                    live = lv;
+                    if (live == 0) break;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    const size_t npix = (size_t)geo.W * geo.H;
+#pragma unroll
+    for (int p = 0; p < PPL; ++p) {
+        const int py = ty * kTile + (lane >> 4) + 4 * (w * PPL + p);
+        if (px < geo.W && py < geo.H) {
+            const size_t pix = (size_t)py * geo.W + px;
+            final_T[pix] = Tf[p];
+            n_contrib[pix] = last[p];
+            accum[pix] = C0[p];
+            accum[npix + pix] = C1[p];
+            accum[2 * npix + pix] = C2[p];
+            out_color[pix] = C0[p] + Tf[p] * geo.bg0;
+            out_color[npix + pix] = C1[p] + Tf[p] * geo.bg1;
+            out_color[2 * npix + pix] = C2[p] + Tf[p] * geo.bg2;
+        }
+    }
+}
+
 }  // namespace
 
 // Kernel-variant selector for A/B timing (bench/ablation only; default = shipped variant).
@@ -1215,8 +1331,17 @@ int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int 
                          hipStream_t s) {
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1);
     if (geo.nwg <= 0) return 0;
-    const int v = variant("GSR_FWD_VARIANT", 2);
-    if (v == 4)
+    const int v = variant("GSR_FWD_VARIANT", 5);
+    if (v == 5)
+        hipLaunchKernelGGL(blend_forward_nw_kernel<2>, dim3(geo.nwg), dim3(128), 0, s, geo, ranges, sorted_gid,
+                           rec, out_color, final_T, n_contrib, accum);
+    else if (v == 6)
+        hipLaunchKernelGGL(blend_forward_nw_kernel<4>, dim3(geo.nwg), dim3(256), 0, s, geo, ranges, sorted_gid,
+                           rec, out_color, final_T, n_contrib, accum);
+    else if (v == 7)
+        hipLaunchKernelGGL(blend_forward_nw_kernel<1>, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid,
+                           rec, out_color, final_T, n_contrib, accum);
+    else if (v == 4)
         hipLaunchKernelGGL(blend_forward_v4_kernel, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid, rec,
                            out_color, final_T, n_contrib, accum);
     else if (v == 3)

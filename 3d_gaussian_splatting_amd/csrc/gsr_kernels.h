@@ -62,8 +62,9 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
 // record layout constants shared by preprocess and the blend kernels
 constexpr float kLn2 = 0.6931471805599453f;  // conic A = -2 ln2 a', B = -ln2 b', C = -2 ln2 c' 
 
-// sum partials per Gaussian (emission order) -> grad2d (kPart floats per Gaussian)
-int launch_gather_grad2d(const uint32_t* inst_start, const uint32_t* tiles, const float* partial,
+// sum partials per Gaussian (emission order) -> grad2d (kPart floats per Gaussian; zeros for
+// culled Gaussians).  gid_by_rank / offsets: depth-sort permutation and inclusive tile scan.
+int launch_gather_grad2d(const uint32_t* gid_by_rank, const uint32_t* offsets, const float* partial,
                          int P, float* grad2d, hipStream_t s);
 
 struct GradOut {

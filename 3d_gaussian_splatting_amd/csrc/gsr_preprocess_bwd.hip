@@ -3,9 +3,9 @@
 // cov3D), on gfx950.  One thread per Gaussian; every output element is written (zeros for
 // culled Gaussians) so the caller can hand in uninitialised tensors.
 //
-// The per-Gaussian 2D gradient is the sum of its per-(tile, instance) partials in emission
-// order (rect row-major), read from the contiguous range [inst_start[g], +tiles[g]) -- a fixed
-// order, so results are bitwise reproducible run to run.
+// The per-Gaussian 2D gradient (grad2d) is the sum of its per-(tile, instance) partials in
+// emission order (rect row-major), read from the contiguous range [inst_start[g], +tiles[g])
+// by gather_grad2d_kernel -- a fixed order, so results are bitwise reproducible run to run.
 //
 // Derivation (restated; same formulas as oracle/gsr_oracle.c
 // preprocess_backward_one): conic (A,B,C) = inv([[a,b],[b,c]]), cov2D = T Sigma T^T with
@@ -27,24 +27,40 @@ __constant__ float kC3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.457045
 constexpr float kC0 = 0.28209479177387814f;
 constexpr float kC1 = 0.4886025119029199f;
 
-__global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __restrict__ inst_start,
-                                                            const uint32_t* __restrict__ tiles,
+// Per-Gaussian sum of its per-(tile, instance) partials in emission order.  Threads walk the
+// Gaussians in depth-rank order, so a wave's segments [offsets[r-1], offsets[r]) are adjacent
+// and together cover one contiguous stretch of the partial array (every fetched line is fully
+// used); loads are issued four instances at a time (independent, predicated) so each thread
+// keeps 12 dwordx4 loads in flight.  The 48 B result lands at grad2d[gid].
+__global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __restrict__ gid_by_rank,
+                                                            const uint32_t* __restrict__ offsets,
                                                             const float* __restrict__ partial, int P,
                                                             float* __restrict__ grad2d) {
-    const int g = blockIdx.x * 256 + threadIdx.x;
-    if (g >= P) return;
-    float a[kPart];
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= P) return;
+    float a[9];
 #pragma unroll
-    for (int k = 0; k < kPart; ++k) a[k] = 0.f;
-    const uint32_t j0 = inst_start[g], nt = tiles[g];
-    for (uint32_t j = j0; j < j0 + nt; ++j) {
-        const float4* src = reinterpret_cast<const float4*>(partial + (size_t)kPart * j);
-        const float4 v0 = src[0], v1 = src[1], v2 = src[2];
-        a[0] += v0.x; a[1] += v0.y; a[2] += v0.z; a[3] += v0.w;
-        a[4] += v1.x; a[5] += v1.y; a[6] += v1.z; a[7] += v1.w;
-        a[8] += v2.x;
+    for (int k = 0; k < 9; ++k) a[k] = 0.f;
+    const uint32_t j0 = r ? offsets[r - 1] : 0u;
+    const uint32_t nt = offsets[r] - j0;
+    const float4* src = reinterpret_cast<const float4*>(partial) + 3 * (size_t)j0;
+    for (uint32_t i = 0; i < nt; i += 4) {
+        float4 v[4][3];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const bool ok = i + u < nt;
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                v[u][c] = ok ? src[3 * (i + u) + c] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {  // emission order: u = 0, 1, 2, 3
+            a[0] += v[u][0].x; a[1] += v[u][0].y; a[2] += v[u][0].z; a[3] += v[u][0].w;
+            a[4] += v[u][1].x; a[5] += v[u][1].y; a[6] += v[u][1].z; a[7] += v[u][1].w;
+            a[8] += v[u][2].x;
+        }
     }
-    float4* dst = reinterpret_cast<float4*>(grad2d + (size_t)kPart * g);
+    float4* dst = reinterpret_cast<float4*>(grad2d + (size_t)kPart * gid_by_rank[r]);
     dst[0] = make_float4(a[0], a[1], a[2], a[3]);
     dst[1] = make_float4(a[4], a[5], a[6], a[7]);
     dst[2] = make_float4(a[8], 0.f, 0.f, 0.f);
@@ -66,16 +82,7 @@ __device__ void preprocess_backward_one(const gsr_camera& cam, const GaussIn& in
 #pragma unroll
     for (int k = 0; k < 9; ++k) g2[k] = 0.f;
     if (visible) {
-        if (partial) {
-            const uint32_t j0 = inst_start[g], nt = tiles[g];
-            for (uint32_t j = j0; j < j0 + nt; ++j) {
-                const float4* src = reinterpret_cast<const float4*>(partial + (size_t)kPart * j);
-                const float4 v0 = src[0], v1 = src[1], v2 = src[2];
-                g2[0] += v0.x; g2[1] += v0.y; g2[2] += v0.z; g2[3] += v0.w;
-                g2[4] += v1.x; g2[5] += v1.y; g2[6] += v1.z; g2[7] += v1.w;
-                g2[8] += v2.x;
-            }
-        } else if (grad2d) {
+        {
             const float4* src = reinterpret_cast<const float4*>(grad2d + (size_t)kPart * g);
             const float4 v0 = src[0], v1 = src[1], v2 = src[2];
             g2[0] = v0.x; g2[1] = v0.y; g2[2] = v0.z; g2[3] = v0.w;
@@ -368,10 +375,10 @@ __global__ __launch_bounds__(256) void preprocess_backward_kernel(
 
 }  // namespace
 
-int launch_gather_grad2d(const uint32_t* inst_start, const uint32_t* tiles, const float* partial,
+int launch_gather_grad2d(const uint32_t* gid_by_rank, const uint32_t* offsets, const float* partial,
                          int P, float* grad2d, hipStream_t s) {
     if (P <= 0) return 0;
-    hipLaunchKernelGGL(gather_grad2d_kernel, dim3(div_up(P, 256)), dim3(256), 0, s, inst_start, tiles,
+    hipLaunchKernelGGL(gather_grad2d_kernel, dim3(div_up(P, 256)), dim3(256), 0, s, gid_by_rank, offsets,
                        partial, P, grad2d);
     return (int)hipGetLastError();
 }

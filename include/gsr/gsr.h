@@ -114,8 +114,9 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
                 gsr_alloc_fn alloc_binning, gsr_alloc_fn alloc_image, void* alloc_ctx,
                 gsr_buffers* bufs, void* stream);
 
-/* Full backward (B1 + B2).  dL_dout_color: 3 x H x W.  scratch: asked for once through
- * alloc_scratch (per-instance partial gradients), valid for the duration of the call. */
+/* Full backward (B1 + gather + B2).  dL_dout_color: 3 x H x W.  scratch: asked for twice
+ * through alloc_scratch (gsr_scratch_bytes(K) for per-instance partial gradients, then
+ * 48 * P bytes for the per-Gaussian screen-space gradient), valid for the duration of the call. */
 int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
                  const gsr_buffers* bufs, const float* dL_dout_color, gsr_alloc_fn alloc_scratch,
                  void* alloc_ctx, const gsr_grads* grads, void* stream);
@@ -158,8 +159,8 @@ const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, 
 #define GSR_STAGE_FINALIZE 5       /* F5 sorted gid + tile ranges */
 #define GSR_STAGE_BLEND_FWD 6      /* F6 */
 #define GSR_STAGE_BLEND_BWD 7      /* B1 */
-#define GSR_STAGE_PREPROCESS_BWD 8 /* B2 (incl. the per-Gaussian partial sum) */
-#define GSR_STAGE_GATHER 9         /* per-Gaussian grad2d sum (multi-GPU path) */
+#define GSR_STAGE_PREPROCESS_BWD 8 /* B2 */
+#define GSR_STAGE_GATHER 9         /* per-Gaussian grad2d sum of the B1 partials */
 #define GSR_STAGE_MISC 10          /* memsets, background fill, num_rendered read */
 #define GSR_NUM_STAGES 11
 int gsr_profile_enable(uint32_t stage_mask);
