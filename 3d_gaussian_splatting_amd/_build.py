@@ -26,7 +26,7 @@ ARCH = "gfx950"
 HIP_SOURCES = {
     "gsr_preprocess.hip": ["-ffp-contract=off"],
     "gsr_sort.hip": [],
-    "gsr_blend.hip": [],
+    "gsr_blend.hip": ["-ffp-contract=off"],  # F6 and B1 must evaluate alpha / T identically
     "gsr_preprocess_bwd.hip": [],
     "gsr_api.cpp": [],
 }

@@ -154,7 +154,6 @@ struct Views {
     float4* rec;
     uint2* ranges;
     float* final_T;
-    uint32_t* n_contrib;
     float* accum;
     uint32_t *sorted_tile, *sorted_gid, *inst_gid;
     uint2* rect;
@@ -175,7 +174,6 @@ Views views(const gsr_camera* cam, int P, const gsr_buffers* b) {
     v.gid_by_rank = at<uint32_t>(b->geom, gl.sA_v);
     v.ranges = at<uint2>(b->image, il.ranges);
     v.final_T = at<float>(b->image, il.final_T);
-    v.n_contrib = at<uint32_t>(b->image, il.n_contrib);
     v.accum = at<float>(b->image, il.accum);
     if (b->binning) {
         BinLayout bl(b->num_rendered);
@@ -188,7 +186,7 @@ Views views(const gsr_camera* cam, int P, const gsr_buffers* b) {
     return v;
 }
 
-__global__ void fill_background(float* out_color, float* final_T, uint32_t* n_contrib, float* accum,
+__global__ void fill_background(float* out_color, float* final_T, float* accum,
                                 int npix, float bg0, float bg1, float bg2) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= npix) return;
@@ -199,7 +197,6 @@ __global__ void fill_background(float* out_color, float* final_T, uint32_t* n_co
     out_color[npix + i] = bg1;
     out_color[2 * (size_t)npix + i] = bg2;
     final_T[i] = 1.0f;
-    n_contrib[i] = 0;
 }
 
 }  // namespace
@@ -212,7 +209,7 @@ const char* gsr_last_error(void) { return g_err.c_str(); }
 size_t gsr_geom_bytes(int32_t P) { return GeomLayout(P).total; }
 size_t gsr_binning_bytes(int32_t K) { return BinLayout(K).total; }
 size_t gsr_image_bytes(int32_t w, int32_t h) { return ImgLayout(w, h).total; }
-size_t gsr_scratch_bytes(int32_t K) { return (size_t)(K > 0 ? K : 1) * kPart * sizeof(float); }
+size_t gsr_scratch_bytes(int32_t K) { return PartLayout(K).total; }
 
 int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
                 float* out_color, int32_t* radii, gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_binning,
@@ -242,12 +239,11 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
     uint32_t* inst_start = at<uint32_t>(bufs->geom, gl.inst_start);
     uint2* ranges = at<uint2>(bufs->image, il.ranges);
     float* final_T = at<float>(bufs->image, il.final_T);
-    uint32_t* n_contrib = at<uint32_t>(bufs->image, il.n_contrib);
 
     if (ty0 > 0 || ty1 < gy) {
         const int npix = W * H;
         hipLaunchKernelGGL(fill_background, dim3(div_up(npix, 256)), dim3(256), 0, stream, out_color,
-                           final_T, n_contrib, at<float>(bufs->image, il.accum), npix, rs->bg[0], rs->bg[1],
+                           final_T, at<float>(bufs->image, il.accum), npix, rs->bg[0], rs->bg[1],
                            rs->bg[2]);
         GSR_STAGE(GSR_STAGE_MISC, hipGetLastError(), "fill_background");
     }
@@ -301,7 +297,7 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
     }
     const Views v = views(cam, P, bufs);
     GSR_STAGE(GSR_STAGE_BLEND_FWD, launch_blend_forward(*cam, rs->bg, ty0, ty1, ranges, v.sorted_gid, rec, out_color, final_T,
-                                       n_contrib, v.accum, stream),
+                                       v.accum, stream),
                   "blend forward");
     return 0;
 }
@@ -325,12 +321,12 @@ static int backward_impl(const gsr_camera* cam, const gsr_gaussians* gs, const g
         partial = static_cast<float*>(alloc_scratch(ctx, gsr_scratch_bytes((int32_t)K)));
         if (!partial) return fail(-2, "allocation failed (scratch, K=%lld)", K);
         GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.inst_start, v.rect, v.rec,
-                                            v.final_T, v.n_contrib, v.accum, dL_dpix, partial, stream),
+                                            v.final_T, v.accum, dL_dpix, partial, K, stream),
                       "blend backward");
     }
     if (grad2d) {
         if (K > 0) {
-            GSR_STAGE(GSR_STAGE_GATHER, launch_gather_grad2d(v.gid_by_rank, v.offsets, partial, P, grad2d, stream), "gather grad2d");
+            GSR_STAGE(GSR_STAGE_GATHER, launch_gather_grad2d(v.gid_by_rank, v.offsets, partial, K, P, grad2d, stream), "gather grad2d");
         } else {
             GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(grad2d, 0, sizeof(float) * kPart * (size_t)P, stream), "zero grad2d");
         }
@@ -385,15 +381,15 @@ int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raste
     if (!partial || !grad2d) return fail(-2, "allocation failed (scratch, K=%lld, P=%d)", K, P);
     if (K > 0) {
         GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.inst_start, v.rect, v.rec,
-                                            v.final_T, v.n_contrib, v.accum, dL_dpix, partial, stream),
+                                            v.final_T, v.accum, dL_dpix, partial, K, stream),
                       "blend backward");
-        GSR_STAGE(GSR_STAGE_GATHER, launch_gather_grad2d(v.gid_by_rank, v.offsets, partial, P, grad2d, stream),
+        GSR_STAGE(GSR_STAGE_GATHER, launch_gather_grad2d(v.gid_by_rank, v.offsets, partial, K, P, grad2d, stream),
                   "gather grad2d");
     } else {
         GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(grad2d, 0, sizeof(float) * kPart * (size_t)P, stream), "zero grad2d");
     }
-    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), v.depth_key, v.flags, v.inst_start, v.tiles,
-                                             nullptr, grad2d, grad_out(grads), stream),
+    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), v.depth_key, v.flags, grad2d,
+                                             grad_out(grads), stream),
                   "preprocess backward");
     return 0;
 }
@@ -418,9 +414,7 @@ int gsr_backward_preprocess(const gsr_camera* cam, const gsr_gaussians* gs, cons
     const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
     GeomLayout gl(gs->P);
     GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), at<uint32_t>(bufs->geom, gl.depth_key),
-                                             at<uint32_t>(bufs->geom, gl.flags),
-                                             at<uint32_t>(bufs->geom, gl.inst_start),
-                                             at<uint32_t>(bufs->geom, gl.tiles), nullptr, grad2d,
+                                             at<uint32_t>(bufs->geom, gl.flags), grad2d,
                                              grad_out(grads), stream),
                   "preprocess backward");
     return 0;
@@ -477,7 +471,7 @@ const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, 
         case GSR_VIEW_SORTED_TILE: return v.sorted_tile;
         case GSR_VIEW_RANGES: return v.ranges;
         case GSR_VIEW_FINAL_T: return v.final_T;
-        case GSR_VIEW_N_CONTRIB: return v.n_contrib;
+        case GSR_VIEW_N_CONTRIB: return nullptr;  // retired: B1 re-derives termination from T
         case GSR_VIEW_DEPTH_KEY: return v.depth_key;
         case GSR_VIEW_TILES_TOUCHED: return v.tiles;
         case GSR_VIEW_RECORDS: return v.rec;

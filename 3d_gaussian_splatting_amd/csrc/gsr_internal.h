@@ -6,8 +6,8 @@
 //                                 | radix histogram (256 x blocks) | scan partials
 //   binning  (per instance, K):   tile key/val ping-pong 4 x u32 (values = Gaussian id)
 //                                 | inst_gid u32 (emission order) | radix histogram
-//   image    (per pixel):         ranges uint2[tiles] | final_T f32 | n_contrib u32 | accum 3 x f32
-//   scratch  (backward, per K):   partial float[GSR_GRAD2D_STRIDE]  (indexed by emission j)
+//   image    (per pixel):         ranges uint2[tiles] | final_T f32 | accum 3 x f32
+//   scratch  (backward, per K):   partial moments float4[2] | partial float  (indexed by emission j)
 #pragma once
 #include <stddef.h>
 #include <stdint.h>
@@ -66,7 +66,7 @@ struct BinLayout {
 };
 
 struct ImgLayout {
-    size_t ranges, final_T, n_contrib, accum, total;
+    size_t ranges, final_T, accum, total;
     ImgLayout(int W, int H) {
         size_t o = 0;
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
@@ -74,9 +74,21 @@ struct ImgLayout {
         size_t pix = (size_t)W * H;
         ranges = take(8 * (tiles ? tiles : 1));
         final_T = take(4 * (pix ? pix : 1));
-        n_contrib = take(4 * (pix ? pix : 1));
         accum = take(12 * (pix ? pix : 1));  // colour sum without background, 3 x H x W
         total = o;
+    }
+};
+
+// B1 output, one entry per (tile, instance) at emission index j: 8 floats (two float4:
+// d mean2D x/y, d conic A/B/C, d opacity, d colour r/g) and a ninth float (d colour b) in a
+// separate array, so the entry is 36 B and every store/load stays 16-B aligned.
+struct PartLayout {
+    size_t p8, p1, total;
+    explicit PartLayout(long long K) {
+        const size_t n = (size_t)(K > 0 ? K : 1);
+        p8 = 0;
+        p1 = align_up(32 * n);
+        total = p1 + align_up(4 * n);
     }
 };
 

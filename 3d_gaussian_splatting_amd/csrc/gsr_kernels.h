@@ -18,7 +18,7 @@ struct PreOut {
     uint32_t* depth_key;
     uint32_t* tiles;
     uint32_t* flags;
-    float4* rec;   // blend records: {x, y, a', b'}, {c', o, r, g}, {b, ext_x, ext_y, 0}
+    float4* rec;   // blend records: {x, y, a', b'}, {c', o, r, g}, {b, ext_x, ext_y, log2 o}
     uint2* rect;   // tile rect: (minx | miny << 16, maxx | maxy << 16), full image
 };
 
@@ -45,19 +45,19 @@ int launch_duplicate(const uint32_t* gid_by_rank, const uint32_t* offsets, const
 // F5: ranges[tile] = [start, end) of the sorted tile keys
 int launch_finalize(const uint32_t* sorted_tile, long long K, uint2* ranges, hipStream_t s);
 
-// F6: per-tile front-to-back blend
+// F6: per-tile front-to-back blend -> colour, final T, colour sum without background
 int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
                          const uint2* ranges, const uint32_t* sorted_gid, const float4* rec,
-                         float* out_color, float* final_T, uint32_t* n_contrib, float* accum,
-                         hipStream_t s);
+                         float* out_color, float* final_T, float* accum, hipStream_t s);
 
-// B1: per-tile back-to-front gradients -> per-instance partial[j] (kPart floats), where the
-// emission index j = inst_start[g] + row-major index of the tile in g's band-clipped rect
+// B1: per-tile front-to-back gradients -> per-instance partial entry j (PartLayout), where the
+// emission index j = inst_start[g] + row-major index of the tile in g's band-clipped rect.
+// `partial` is the base of a PartLayout(K) block.
 int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
                           const uint2* ranges, const uint32_t* sorted_gid, const uint32_t* inst_start,
                           const uint2* rect, const float4* rec, const float* final_T,
-                          const uint32_t* n_contrib, const float* accum, const float* dL_dpix,
-                          float* partial, hipStream_t s);
+                          const float* accum, const float* dL_dpix, float* partial, long long K,
+                          hipStream_t s);
 
 // record layout constants shared by preprocess and the blend kernels
 constexpr float kLn2 = 0.6931471805599453f;  // conic A = -2 ln2 a', B = -ln2 b', C = -2 ln2 c' 
@@ -65,17 +65,15 @@ constexpr float kLn2 = 0.6931471805599453f;  // conic A = -2 ln2 a', B = -ln2 b'
 // sum partials per Gaussian (emission order) -> grad2d (kPart floats per Gaussian; zeros for
 // culled Gaussians).  gid_by_rank / offsets: depth-sort permutation and inclusive tile scan.
 int launch_gather_grad2d(const uint32_t* gid_by_rank, const uint32_t* offsets, const float* partial,
-                         int P, float* grad2d, hipStream_t s);
+                         long long K, int P, float* grad2d, hipStream_t s);
 
 struct GradOut {
     float *means2D, *conic, *opac, *colors, *means3D, *sh_dc, *sh_rest, *scales, *rots, *cov3D;
 };
 
-// B2: chain rule to the leaves.  Source of the 2D gradients: either per-instance partials
-// (partial != nullptr: summed in emission order here) or a grad2d buffer.
+// B2: chain rule to the leaves from the per-Gaussian 2D gradients (grad2d, kPart floats each)
 int launch_preprocess_backward(const gsr_camera& cam, const GaussIn& in, const uint32_t* depth_key,
-                               const uint32_t* flags, const uint32_t* inst_start,
-                               const uint32_t* tiles, const float* partial, const float* grad2d,
-                               const GradOut& out, hipStream_t s);
+                               const uint32_t* flags, const float* grad2d, const GradOut& out,
+                               hipStream_t s);
 
 }  // namespace gsr

@@ -194,7 +194,8 @@ __global__ __launch_bounds__(256) void preprocess_kernel(const gsr_camera cam, c
                 key_out = __float_as_uint(tz);
                 tiles_out = (uint32_t)((maxx - minx) * band_rows);
                 // Blend record (SURVEY B.3 power with -0.5 and log2(e) folded in, so the blend
-                // evaluates exp2 directly) + the half-extents of the alpha >= 1/255 footprint:
+                // evaluates exp2 directly; log2(o) rides along so o * G is one exp2) + the
+                // half-extents of the alpha >= 1/255 footprint:
                 // d^T Q d <= t, t = 2 ln(255 o)  =>  |dx| <= sqrt(t a), |dy| <= sqrt(t c),
                 // padded (x1.02 + 0.5 px) so the per-stripe cull never drops a contributing pixel.
                 const float opac = in.opac[g];
@@ -205,7 +206,7 @@ __global__ __launch_bounds__(256) void preprocess_kernel(const gsr_camera cam, c
                 float4* rec = out.rec + 3 * (size_t)g;
                 rec[0] = make_float4(xs, ys, -0.5f * kL2E * cA, -kL2E * cB);
                 rec[1] = make_float4(-0.5f * kL2E * cC, opac, rgb[0], rgb[1]);
-                rec[2] = make_float4(rgb[2], ex, ey, 0.0f);
+                rec[2] = make_float4(rgb[2], ex, ey, log2f(opac));
                 out.rect[g] = make_uint2((uint32_t)minx | ((uint32_t)miny << 16),
                                          (uint32_t)maxx | ((uint32_t)maxy << 16));
                 out.flags[g] = clamped;

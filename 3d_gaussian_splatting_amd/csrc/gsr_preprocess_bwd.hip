@@ -27,39 +27,43 @@ __constant__ float kC3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.457045
 constexpr float kC0 = 0.28209479177387814f;
 constexpr float kC1 = 0.4886025119029199f;
 
-// Per-Gaussian sum of its per-(tile, instance) partials in emission order.  Threads walk the
-// Gaussians in depth-rank order, so a wave's segments [offsets[r-1], offsets[r]) are adjacent
-// and together cover one contiguous stretch of the partial array (every fetched line is fully
-// used); loads are issued four instances at a time (independent, predicated) so each thread
-// keeps 12 dwordx4 loads in flight.  The 48 B result lands at grad2d[gid].
+// Per-Gaussian sum of its per-(tile, instance) partials in emission order.  A block owns 256
+// consecutive depth ranks; their segments [offsets[r-1], offsets[r]) tile one contiguous
+// stretch of the partial arrays, which the block streams through LDS in coalesced windows of
+// kGatherWin entries.  Each thread then adds the part of its own segment that lies in the
+// window, in order, from LDS.  The 48-B result lands at grad2d[gid].
+constexpr int kGatherWin = 512;
+
 __global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __restrict__ gid_by_rank,
                                                             const uint32_t* __restrict__ offsets,
-                                                            const float* __restrict__ partial, int P,
+                                                            const float4* __restrict__ p8,
+                                                            const float* __restrict__ p1, int P,
                                                             float* __restrict__ grad2d) {
-    const int r = blockIdx.x * 256 + threadIdx.x;
-    if (r >= P) return;
+    __shared__ float4 w8[2 * kGatherWin];
+    __shared__ float w1[kGatherWin];
+    const int r0 = blockIdx.x * 256, r = r0 + threadIdx.x;
+    const int rl = (P - r0 < 256 ? P - r0 : 256) + r0;  // one past the block's last rank
+    const uint32_t J0 = r0 ? offsets[r0 - 1] : 0u, J1 = offsets[rl - 1];
+    const uint32_t s = r < P ? (r ? offsets[r - 1] : 0u) : 0u;
+    const uint32_t e = r < P ? offsets[r] : 0u;
     float a[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) a[k] = 0.f;
-    const uint32_t j0 = r ? offsets[r - 1] : 0u;
-    const uint32_t nt = offsets[r] - j0;
-    const float4* src = reinterpret_cast<const float4*>(partial) + 3 * (size_t)j0;
-    for (uint32_t i = 0; i < nt; i += 4) {
-        float4 v[4][3];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const bool ok = i + u < nt;
-#pragma unroll
-            for (int c = 0; c < 3; ++c)
-                v[u][c] = ok ? src[3 * (i + u) + c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (uint32_t W = J0; W < J1; W += kGatherWin) {
+        const uint32_t n = J1 - W < (uint32_t)kGatherWin ? J1 - W : (uint32_t)kGatherWin;
+        for (uint32_t i = threadIdx.x; i < 2 * n; i += 256) w8[i] = p8[2 * (size_t)W + i];
+        for (uint32_t i = threadIdx.x; i < n; i += 256) w1[i] = p1[(size_t)W + i];
+        __syncthreads();
+        const uint32_t lo = s > W ? s : W, hi = e < W + n ? e : W + n;
+        for (uint32_t j = lo; j < hi; ++j) {
+            const float4 u = w8[2 * (j - W)], v = w8[2 * (j - W) + 1];
+            a[0] += u.x; a[1] += u.y; a[2] += u.z; a[3] += u.w;
+            a[4] += v.x; a[5] += v.y; a[6] += v.z; a[7] += v.w;
+            a[8] += w1[j - W];
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {  // emission order: u = 0, 1, 2, 3
-            a[0] += v[u][0].x; a[1] += v[u][0].y; a[2] += v[u][0].z; a[3] += v[u][0].w;
-            a[4] += v[u][1].x; a[5] += v[u][1].y; a[6] += v[u][1].z; a[7] += v[u][1].w;
-            a[8] += v[u][2].x;
-        }
+        __syncthreads();
     }
+    if (r >= P) return;
     float4* dst = reinterpret_cast<float4*>(grad2d + (size_t)kPart * gid_by_rank[r]);
     dst[0] = make_float4(a[0], a[1], a[2], a[3]);
     dst[1] = make_float4(a[4], a[5], a[6], a[7]);
@@ -71,9 +75,6 @@ __global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __re
 __device__ void preprocess_backward_one(const gsr_camera& cam, const GaussIn& in, int g,
                                         const uint32_t* __restrict__ depth_key,
                                         const uint32_t* __restrict__ flags,
-                                        const uint32_t* __restrict__ inst_start,
-                                        const uint32_t* __restrict__ tiles,
-                                        const float* __restrict__ partial,
                                         const float* __restrict__ grad2d, const GradOut& out,
                                         float* lrest) {
     const bool visible = depth_key[g] != 0xFFFFFFFFu;
@@ -351,9 +352,7 @@ __device__ void preprocess_backward_one(const gsr_camera& cam, const GaussIn& in
 
 __global__ __launch_bounds__(256) void preprocess_backward_kernel(
     const gsr_camera cam, const GaussIn in, const uint32_t* __restrict__ depth_key,
-    const uint32_t* __restrict__ flags, const uint32_t* __restrict__ inst_start,
-    const uint32_t* __restrict__ tiles, const float* __restrict__ partial,
-    const float* __restrict__ grad2d, GradOut out) {
+    const uint32_t* __restrict__ flags, const float* __restrict__ grad2d, GradOut out) {
     extern __shared__ __attribute__((aligned(16))) float sh_lds[];
     const int g = blockIdx.x * 256 + threadIdx.x;
     const int M3 = in.M_rest * 3;
@@ -365,7 +364,7 @@ __global__ __launch_bounds__(256) void preprocess_backward_kernel(
         __syncthreads();
     }
     if (g < in.P)
-        preprocess_backward_one(cam, in, g, depth_key, flags, inst_start, tiles, partial, grad2d, out,
+        preprocess_backward_one(cam, in, g, depth_key, flags, grad2d, out,
                                 stage ? sh_lds + threadIdx.x * M3 : nullptr);
     if (stage) {  // coalesced write-back of the SH-rest gradient rows
         __syncthreads();
@@ -376,21 +375,23 @@ __global__ __launch_bounds__(256) void preprocess_backward_kernel(
 }  // namespace
 
 int launch_gather_grad2d(const uint32_t* gid_by_rank, const uint32_t* offsets, const float* partial,
-                         int P, float* grad2d, hipStream_t s) {
+                         long long K, int P, float* grad2d, hipStream_t s) {
     if (P <= 0) return 0;
+    const PartLayout pl(K);
+    const char* base = reinterpret_cast<const char*>(partial);
     hipLaunchKernelGGL(gather_grad2d_kernel, dim3(div_up(P, 256)), dim3(256), 0, s, gid_by_rank, offsets,
-                       partial, P, grad2d);
+                       reinterpret_cast<const float4*>(base + pl.p8), reinterpret_cast<const float*>(base + pl.p1),
+                       P, grad2d);
     return (int)hipGetLastError();
 }
 
 int launch_preprocess_backward(const gsr_camera& cam, const GaussIn& in, const uint32_t* depth_key,
-                               const uint32_t* flags, const uint32_t* inst_start,
-                               const uint32_t* tiles, const float* partial, const float* grad2d,
-                               const GradOut& out, hipStream_t s) {
+                               const uint32_t* flags, const float* grad2d, const GradOut& out,
+                               hipStream_t s) {
     if (in.P <= 0) return 0;
     const size_t lds = (in.sh_rest && !in.colors) ? sizeof(float) * 256 * 3 * in.M_rest : 0;
     hipLaunchKernelGGL(preprocess_backward_kernel, dim3(div_up(in.P, 256)), dim3(256), lds, s, cam, in,
-                       depth_key, flags, inst_start, tiles, partial, grad2d, out);
+                       depth_key, flags, grad2d, out);
     return (int)hipGetLastError();
 }
 

@@ -140,10 +140,12 @@ int gsr_backward_preprocess(const gsr_camera* cam, const gsr_gaussians* gs,
 #define GSR_VIEW_SORTED_TILE 2      /* uint32[K]: tile id of sorted instance i             */
 #define GSR_VIEW_RANGES 3           /* uint32[2*tiles]: [start,end) per tile               */
 #define GSR_VIEW_FINAL_T 4          /* float[H*W]                                          */
-#define GSR_VIEW_N_CONTRIB 5        /* uint32[H*W]                                         */
+#define GSR_VIEW_N_CONTRIB 5        /* retired (always NULL): the blend no longer keeps a   
+                                       per-pixel contributor count; B1 re-derives the      
+                                       termination point from T                             */
 #define GSR_VIEW_DEPTH_KEY 6        /* uint32[P]: depth bits, 0xFFFFFFFF when culled       */
 #define GSR_VIEW_TILES_TOUCHED 7    /* uint32[P]                                           */
-#define GSR_VIEW_RECORDS 8          /* float4[3*P]: {x,y,a',b'},{c',o,r,g},{b,ext_x,ext_y,0};
+#define GSR_VIEW_RECORDS 8          /* float4[3*P]: {x,y,a',b'},{c',o,r,g},{b,ext_x,ext_y,log2 o};
                                        a',b',c' = -log2(e) * (A/2, B, C/2) of the conic */
 const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, int what);
 
