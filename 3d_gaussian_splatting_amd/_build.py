@@ -26,7 +26,8 @@ ARCH = "gfx950"
 HIP_SOURCES = {
     "gsr_preprocess.hip": ["-ffp-contract=off"],
     "gsr_sort.hip": [],
-    "gsr_blend.hip": ["-ffp-contract=off"],  # F6 and B1 must evaluate alpha / T identically
+    # F6 and B1 must evaluate alpha / T identically; no SLP packing (it splits DPP-fused adds)
+    "gsr_blend.hip": ["-ffp-contract=off", "-fno-slp-vectorize"],
     "gsr_preprocess_bwd.hip": [],
     "gsr_api.cpp": [],
 }

@@ -21,9 +21,15 @@
 // round-robin dispatch, speed only), so each XCD gets a contiguous band of tile rows and
 // its L2 keeps the records those neighbouring tiles share.
 //
-// B1 reduces each record's 9 gradient terms over the tile's 256 pixels in registers
-// (interleaved DPP row reduction + permlane16/32 swaps) and writes ONE 36-B partial per
-// (tile, instance) with plain stores, indexed by the instance's emission index j.  The
+// B1 reduces each record's 9 gradient terms over the tile's 256 pixels: 4 pixels per lane in
+// registers, a 2-step quad DPP reduction, then the 16 quad partials wait in LDS and are summed
+// four records at a time (one (record, value) output per lane) -- ~40% fewer VALU ops than a
+// full 64-lane DPP/permlane reduction per record.  It writes ONE 36-B partial per
+// (tile, instance) with plain stores, indexed by the instance's emission index j.
+//
+// Measured and rejected (scripts/ablate.py): packing two stripes per VGPR pair
+// (v_pk_fma_f32) -- register shuffles and scalar/pair path splits cost more than the packed
+// issue saved (F6 0.31 -> 0.38 ms); 4 waves per tile; record prefetch into registers.  The
 // per-Gaussian sum happens later in fixed emission order (gsr_preprocess_bwd.hip), so
 // gradients are deterministic and no float atomics are issued.
 #include <cstdlib>
@@ -219,6 +225,23 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
     }
 }
 
+// Deferred B1 reduction: 16 quad partials of 9 values for each of `parked` records wait in
+// LDS; lane (slot, c) sums the 16 partials of one (record, value) output in fixed quad order.
+constexpr int kPark = 4;
+__device__ __forceinline__ void park_flush(const float* qpark, const int* qrec, int parked, float* smom,
+                                           int lane) {
+    __syncthreads();  // one-wave block: orders the quad leaders' LDS writes before the reads
+    if (lane < parked * 9) {
+        const int slot = lane / 9, c = lane - 9 * slot;
+        const float* q = qpark + slot * 16 * 12 + c;
+        float t[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) t[i & 3] += q[i * 12];
+        smom[qrec[slot] * 12 + c] = (t[0] + t[1]) + (t[2] + t[3]);
+    }
+    __syncthreads();
+}
+
 // B1 front to back.  With S = the forward's colour sum (no background) and the running
 // Sp = sum over processed contributors of w * (c . dL/dpix), the colour behind entry k is
 // (S . dL/dpix - Sp) / (1 - alpha_k) after T_k, so
@@ -229,6 +252,7 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
 // Per record the lane accumulates sv = o G dL/dalpha moments along its column
 // (sum sv, sum sv dy, sum sv dy^2) and applies dx afterwards:
 //   Sx = dx sum sv, Sxx = dx^2 sum sv, Sxy = dx sum sv dy.
+template <bool DEFER>
 __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
                                                             const uint2* __restrict__ ranges,
                                                             const uint32_t* __restrict__ sorted_gid,
@@ -242,6 +266,8 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
                                                             float* __restrict__ part1) {
     __shared__ float4 srec[64 * 3];
     __shared__ float smom[64 * 12];
+    __shared__ float qpark[DEFER ? kPark * 16 * 12 : 1];  // [slot][quad][9 of 12]
+    __shared__ int qrec[DEFER ? kPark : 1];
     const int tile = xcd_tile(blockIdx.x, geo.nwg) + geo.ty0 * geo.grid_x;
     const int tx = tile % geo.grid_x, ty = tile / geo.grid_x;
     const int lane = threadIdx.x;
@@ -299,7 +325,7 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
         for (int c = 0; c < 12; ++c) smom[lane * 12 + c] = 0.0f;
         __syncthreads();
         uint64_t todo = __ballot((smask & live) != 0u);
-        int visited = 0;
+        int visited = 0, parked = 0;
         while (todo) {
             const int k = __builtin_ctzll(todo);
             todo &= todo - 1;
@@ -342,14 +368,33 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
             if (__any(any)) {
                 const float sx = s0 * dx;
                 float v[9] = {sx, sy, sx * dx, sy * dx, syy, s0, g0, g1, g2};
-                row_reduce(v);
-                const float t0 = scatter4(v[0], v[1], v[2], v[3]);
-                const float t1 = scatter4(v[4], v[5], v[6], v[7]);
-                const float t2 = allreduce_rows(v[8]);
-                if ((lane & 15) == 0) {
-                    smom[k * 12 + row] = t0;
-                    smom[k * 12 + 4 + row] = t1;
-                    if (row == 0) smom[k * 12 + 8] = t2;
+                if (DEFER) {
+                    // quad partials -> LDS; summed kPark records at a time by park_flush
+#pragma unroll
+                    for (int i = 0; i < 9; ++i) v[i] += dpp_f<0xB1>(v[i]);  // quad_perm [1,0,3,2]
+#pragma unroll
+                    for (int i = 0; i < 9; ++i) v[i] += dpp_f<0x4E>(v[i]);  // quad_perm [2,3,0,1]
+                    if ((lane & 3) == 0) {
+                        float* dst = qpark + (parked * 16 + (lane >> 2)) * 12;
+                        *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+                        *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
+                        dst[8] = v[8];
+                    }
+                    if (lane == 0) qrec[parked] = k;
+                    if (++parked == kPark) {
+                        park_flush(qpark, qrec, parked, smom, lane);
+                        parked = 0;
+                    }
+                } else {
+                    row_reduce(v);
+                    const float t0 = scatter4(v[0], v[1], v[2], v[3]);
+                    const float t1 = scatter4(v[4], v[5], v[6], v[7]);
+                    const float t2 = allreduce_rows(v[8]);
+                    if ((lane & 15) == 0) {
+                        smom[k * 12 + row] = t0;
+                        smom[k * 12 + 4 + row] = t1;
+                        if (row == 0) smom[k * 12 + 8] = t2;
+                    }
                 }
             }
             if ((++visited & 7) == 0) {
@@ -360,6 +405,7 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
                 if (live == 0) break;
             }
         }
+        if (DEFER && parked) park_flush(qpark, qrec, parked, smom, lane);
         __syncthreads();
         if (lane < cnt) {
             // moments -> d mean2D (NDC), d conic, d opacity (sum G dL/dalpha = sum sv / o), d colour
@@ -374,6 +420,7 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
         __syncthreads();
     }
 }
+
 
 }  // namespace
 
@@ -423,9 +470,15 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
     if (geo.nwg <= 0) return 0;
     const PartLayout pl(K);
     char* base = reinterpret_cast<char*>(partial);
-    hipLaunchKernelGGL(blend_backward_kernel, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid,
-                       inst_start, rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(base + pl.p8),
-                       reinterpret_cast<float*>(base + pl.p1));
+    // 1: deferred quad/LDS reduction (shipped); 0: full per-record DPP/permlane reduction
+    if (variant("GSR_BWD_VARIANT", 1) == 0)
+        hipLaunchKernelGGL(blend_backward_kernel<false>, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid,
+                           inst_start, rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(base + pl.p8),
+                           reinterpret_cast<float*>(base + pl.p1));
+    else
+        hipLaunchKernelGGL(blend_backward_kernel<true>, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid,
+                           inst_start, rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(base + pl.p8),
+                           reinterpret_cast<float*>(base + pl.p1));
     return (int)hipGetLastError();
 }
 
