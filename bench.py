@@ -39,6 +39,7 @@ gr = importlib.import_module(f"{PKG}.graphics")
 sc = importlib.import_module(f"{PKG}.scene")
 R = importlib.import_module(f"{PKG}.rasterizer")
 native = importlib.import_module(f"{PKG}.native")
+bands = importlib.import_module(f"{PKG}.bands")
 
 CONFIGS = {
     "1k_256": dict(P=1_000, W=256, H=256, D=0),
@@ -47,6 +48,9 @@ CONFIGS = {
     "5m_1080p": dict(P=5_000_000, W=1920, H=1080, D=3),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
+# wave64 VALU issue: 256 CUs x 4 SIMDs, one instruction per 4 cycles per SIMD, 2.4 GHz peak
+# clock (MI355X_MICROARCH 'vector-instruction ISSUE cost'; scripts/ubench/pk_rate.hip)
+VALU_ISSUE_PER_S = 256 * 4 * 2.4e9 / 4
 
 
 def algorithmic_bytes(P, V, K, pix, tiles, M):
@@ -63,18 +67,19 @@ def algorithmic_bytes(P, V, K, pix, tiles, M):
     }
 
 
-def pmc_traffic(kernel_prefix):
-    """HBM bytes per launch of `kernel_prefix` from the committed rocprofv3 PMC passes
-    (profiles/*pmc*.json written by tools/pmc_summary.py), or None."""
+def pmc_record(kernel_prefix):
+    """Per-launch PMC figures of `kernel_prefix` (HBM bytes, VALU instructions) from the
+    committed rocprofv3 passes (profiles/pmc_traffic.json, written by
+    scripts/pmc_summary.py --traffic), or {}."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
-        return None
+        return {}
     with open(path) as fh:
         data = json.load(fh)
     for name, rec in data.get("kernels", {}).items():
-        if kernel_prefix in name:
-            return rec.get("hbm_bytes_per_launch")
-    return None
+        if name.startswith(kernel_prefix):
+            return rec
+    return {}
 
 
 def main():
@@ -109,23 +114,14 @@ def main():
                   rotations=t(scene.rotations), sh_dc=t(scene.sh_dc), sh_rest=t(scene.sh_rest))
     dpix = t(dpix_np)
     gx, gy = cam.grid
-    if world > 1:
-        rows = [(r * gy) // world for r in range(world + 1)]
-        band = (rows[rank], rows[rank + 1])
-        band_px = max(rows[i + 1] - rows[i] for i in range(world)) * 16
-        gather_buf = torch.zeros((world, 3, band_px, W), device=dev)
-    else:
-        band = None
+    band = bands.band_rows(gy, world, rank) if world > 1 else None
 
     def step():
         st = rast.forward(cam, **inputs, sh_degree=D, tile_rows=band)
         if world > 1:
-            y0, y1 = band[0] * 16, min(band[1] * 16, H)
-            mine = torch.zeros((3, band_px, W), device=dev)
-            mine[:, :y1 - y0] = st.color[:, y0:y1]
-            dist.all_gather_into_tensor(gather_buf.view(-1), mine.view(-1))
+            bands.gather_image(st.color, band, gy, dist)  # full image on every rank
             g2 = rast.backward_blend(st, dpix)
-            dist.all_reduce(g2)
+            bands.reduce_grad2d(g2, dist)
             g = rast.backward_preprocess(st, g2)
         else:
             g = rast.backward(st, dpix)
@@ -188,11 +184,20 @@ def main():
         achieved = bytes_launch / (mean_ms * 1e-3) / 1e9
         kernel_name = {"blend_fwd": "blend_forward_kernel", "blend_bwd": "blend_backward_kernel",
                        "preprocess": "preprocess_kernel", "preprocess_bwd": "preprocess_backward_kernel"}.get(dom, dom)
-        traffic = pmc_traffic(kernel_name)
+        pmc = pmc_record(kernel_name)
         result["roofline"] = {"bound": "hbm", "kernel": kernel_name, "achieved": round(achieved, 2),
                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                              "traffic": traffic, "mean_launch_ms": round(mean_ms, 4),
+                              "traffic": pmc.get("hbm_bytes_per_launch"), "mean_launch_ms": round(mean_ms, 4),
                               "algorithmic_bytes_per_launch": int(bytes_launch)}
+        if "valu_insts_per_launch" in pmc:
+            # F6/B1 are VALU-issue-bound, not HBM-bound (DESIGN.md "Rooflines"): share of the
+            # chip's VALU issue slots (1024 SIMDs x one wave64 op per 4 cycles at 2.4 GHz) that
+            # the kernel's measured instruction count fills over its measured duration.
+            slots = VALU_ISSUE_PER_S * mean_ms * 1e-3
+            result["roofline"]["valu_issue"] = {
+                "insts_per_launch": pmc["valu_insts_per_launch"],
+                "frac": round(pmc["valu_insts_per_launch"] / slots, 4),
+                "peak_insts_per_s": VALU_ISSUE_PER_S}
         total_alg = sum(alg.values())
         result["pipeline_roofline"] = {
             "algorithmic_bytes_per_step": int(total_alg),

@@ -55,17 +55,21 @@ def main():
         print(k.ljust(width), " ".join(
             (f"{table[k][c]:18.4g}" if c in table[k] else " " * 18) for c in counters))
     if args.traffic:
-        out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes",
+        out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU, separate passes",
                "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving)",
                "kernels": {}}
         for k in kernels:
             t = table[k]
+            rec = {}
             if "FETCH_SIZE" in t and "WRITE_SIZE" in t:
-                out["kernels"][k] = {
-                    "fetch_size_kib": round(t["FETCH_SIZE"], 3),
-                    "write_size_kib": round(t["WRITE_SIZE"], 3),
-                    "hbm_bytes_per_launch": int((2 * t["FETCH_SIZE"] + t["WRITE_SIZE"]) * 1024),
-                }
+                rec.update(fetch_size_kib=round(t["FETCH_SIZE"], 3), write_size_kib=round(t["WRITE_SIZE"], 3),
+                           hbm_bytes_per_launch=int((2 * t["FETCH_SIZE"] + t["WRITE_SIZE"]) * 1024))
+            if "SQ_INSTS_VALU" in t:  # wave-level VALU instructions per launch (issue-bound kernels)
+                rec["valu_insts_per_launch"] = int(t["SQ_INSTS_VALU"])
+            if "SQ_INSTS_VALU_TRANS_F32" in t:
+                rec["valu_trans_insts_per_launch"] = int(t["SQ_INSTS_VALU_TRANS_F32"])
+            if rec:
+                out["kernels"][k] = rec
         with open(args.traffic, "w") as fh:
             json.dump(out, fh, indent=1)
         print("wrote", args.traffic)
