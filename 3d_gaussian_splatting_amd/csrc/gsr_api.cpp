@@ -388,7 +388,7 @@ int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raste
     } else {
         GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(grad2d, 0, sizeof(float) * kPart * (size_t)P, stream), "zero grad2d");
     }
-    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), v.depth_key, v.flags, grad2d,
+    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), 0, P, v.depth_key, v.flags, grad2d,
                                              grad_out(grads), stream),
                   "preprocess backward");
     return 0;
@@ -402,22 +402,30 @@ int gsr_backward_blend(const gsr_camera* cam, const gsr_gaussians* gs, const gsr
     return backward_impl(cam, gs, rs, bufs, dL_dpix, alloc_scratch, ctx, nullptr, grad2d, stream);
 }
 
-int gsr_backward_preprocess(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
-                            const gsr_buffers* bufs, const float* grad2d, const gsr_grads* grads,
-                            void* stream_) {
+int gsr_backward_preprocess_range(const gsr_camera* cam, const gsr_gaussians* gs,
+                                  const gsr_raster_settings* rs, const gsr_buffers* bufs, int32_t g0,
+                                  int32_t g1, const float* grad2d, const gsr_grads* grads, void* stream_) {
     g_err.clear();
     if (int e = validate(cam, gs, rs)) return e;
-    if (gs->P == 0) return 0;
+    if (g0 < 0 || g1 > gs->P || g0 > g1) return fail(-1, "bad Gaussian range [%d, %d) for P=%d", g0, g1, gs->P);
+    if (g0 == g1) return 0;
     if (int e = check_grads(gs, grads)) return e;
     if (!bufs || !bufs->geom || !grad2d) return fail(-1, "missing forward buffers / grad2d");
     hipStream_t stream = (hipStream_t)stream_;
     const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
     GeomLayout gl(gs->P);
-    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), at<uint32_t>(bufs->geom, gl.depth_key),
+    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), g0, g1, at<uint32_t>(bufs->geom, gl.depth_key),
                                              at<uint32_t>(bufs->geom, gl.flags), grad2d,
                                              grad_out(grads), stream),
                   "preprocess backward");
     return 0;
+}
+
+int gsr_backward_preprocess(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
+                            const gsr_buffers* bufs, const float* grad2d, const gsr_grads* grads,
+                            void* stream) {
+    if (!gs) return fail(-1, "null gaussians");
+    return gsr_backward_preprocess_range(cam, gs, rs, bufs, 0, gs->P, grad2d, grads, stream);
 }
 
 int gsr_profile_enable(uint32_t stage_mask) {

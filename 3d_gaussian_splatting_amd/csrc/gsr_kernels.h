@@ -71,9 +71,10 @@ struct GradOut {
     float *means2D, *conic, *opac, *colors, *means3D, *sh_dc, *sh_rest, *scales, *rots, *cov3D;
 };
 
-// B2: chain rule to the leaves from the per-Gaussian 2D gradients (grad2d, kPart floats each)
-int launch_preprocess_backward(const gsr_camera& cam, const GaussIn& in, const uint32_t* depth_key,
-                               const uint32_t* flags, const float* grad2d, const GradOut& out,
-                               hipStream_t s);
+// B2: chain rule to the leaves for Gaussians [g0, g1) from their 2D gradients (grad2d, kPart
+// floats each).  Inputs are indexed by g; grad2d and all outputs by g - g0.
+int launch_preprocess_backward(const gsr_camera& cam, const GaussIn& in, int g0, int g1,
+                               const uint32_t* depth_key, const uint32_t* flags, const float* grad2d,
+                               const GradOut& out, hipStream_t s);
 
 }  // namespace gsr

@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __re
 
 // One Gaussian's chain rule.  `lrest`: this thread's SH-rest row staged in LDS (read, then
 // overwritten in place with the row's gradient), or nullptr when there is no SH-rest input.
-__device__ void preprocess_backward_one(const gsr_camera& cam, const GaussIn& in, int g,
+__device__ void preprocess_backward_one(const gsr_camera& cam, const GaussIn& in, int g, int o,
                                         const uint32_t* __restrict__ depth_key,
                                         const uint32_t* __restrict__ flags,
                                         const float* __restrict__ grad2d, const GradOut& out,
@@ -84,22 +84,22 @@ __device__ void preprocess_backward_one(const gsr_camera& cam, const GaussIn& in
     for (int k = 0; k < 9; ++k) g2[k] = 0.f;
     if (visible) {
         {
-            const float4* src = reinterpret_cast<const float4*>(grad2d + (size_t)kPart * g);
+            const float4* src = reinterpret_cast<const float4*>(grad2d + (size_t)kPart * o);
             const float4 v0 = src[0], v1 = src[1], v2 = src[2];
             g2[0] = v0.x; g2[1] = v0.y; g2[2] = v0.z; g2[3] = v0.w;
             g2[4] = v1.x; g2[5] = v1.y; g2[6] = v1.z; g2[7] = v1.w;
             g2[8] = v2.x;
         }
     }
-    out.means2D[3 * g + 0] = g2[0];
-    out.means2D[3 * g + 1] = g2[1];
-    out.means2D[3 * g + 2] = 0.f;
+    out.means2D[3 * o + 0] = g2[0];
+    out.means2D[3 * o + 1] = g2[1];
+    out.means2D[3 * o + 2] = 0.f;
     if (out.conic) {
-        out.conic[3 * g + 0] = g2[2];
-        out.conic[3 * g + 1] = g2[3];
-        out.conic[3 * g + 2] = g2[4];
+        out.conic[3 * o + 0] = g2[2];
+        out.conic[3 * o + 1] = g2[3];
+        out.conic[3 * o + 2] = g2[4];
     }
-    out.opac[g] = g2[5];
+    out.opac[o] = g2[5];
 
     const float* V = cam.viewmatrix;
     const float* Pm = cam.projmatrix;
@@ -112,32 +112,32 @@ __device__ void preprocess_backward_one(const gsr_camera& cam, const GaussIn& in
     if (!visible) {
         if (in.colors) {
 #pragma unroll
-            for (int k = 0; k < 3; ++k) out.colors[3 * g + k] = 0.f;
+            for (int k = 0; k < 3; ++k) out.colors[3 * o + k] = 0.f;
         } else {
 #pragma unroll
-            for (int k = 0; k < 3; ++k) out.sh_dc[3 * g + k] = 0.f;
+            for (int k = 0; k < 3; ++k) out.sh_dc[3 * o + k] = 0.f;
             if (lrest)
                 for (int k = 0; k < 3 * in.M_rest; ++k) lrest[k] = 0.f;
         }
-        out.means3D[3 * g + 0] = 0.f;
-        out.means3D[3 * g + 1] = 0.f;
-        out.means3D[3 * g + 2] = 0.f;
+        out.means3D[3 * o + 0] = 0.f;
+        out.means3D[3 * o + 1] = 0.f;
+        out.means3D[3 * o + 2] = 0.f;
         if (in.cov3D) {
 #pragma unroll
-            for (int k = 0; k < 6; ++k) out.cov3D[6 * g + k] = 0.f;
+            for (int k = 0; k < 6; ++k) out.cov3D[6 * o + k] = 0.f;
         } else {
 #pragma unroll
-            for (int k = 0; k < 3; ++k) out.scales[3 * g + k] = 0.f;
+            for (int k = 0; k < 3; ++k) out.scales[3 * o + k] = 0.f;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) out.rots[4 * g + k] = 0.f;
+            for (int k = 0; k < 4; ++k) out.rots[4 * o + k] = 0.f;
         }
         return;
     }
     // ---- colour -> SH / view direction ----
     if (in.colors) {
-        out.colors[3 * g + 0] = g2[6];
-        out.colors[3 * g + 1] = g2[7];
-        out.colors[3 * g + 2] = g2[8];
+        out.colors[3 * o + 0] = g2[6];
+        out.colors[3 * o + 1] = g2[7];
+        out.colors[3 * o + 2] = g2[8];
     } else {
         const uint32_t cl = flags[g];
         const float dres[3] = {(cl & 1u) ? 0.f : g2[6], (cl & 2u) ? 0.f : g2[7], (cl & 4u) ? 0.f : g2[8]};
@@ -182,7 +182,7 @@ __device__ void preprocess_backward_one(const gsr_camera& cam, const GaussIn& in
             }
         }
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch) out.sh_dc[3 * g + ch] = basis[0] * dres[ch];
+        for (int ch = 0; ch < 3; ++ch) out.sh_dc[3 * o + ch] = basis[0] * dres[ch];
         float ddx = 0.f, ddy = 0.f, ddz = 0.f;
         if (lrest) {
             const float* rest = lrest;
@@ -314,14 +314,14 @@ __device__ void preprocess_backward_one(const gsr_camera& cam, const GaussIn& in
                       (2.f * fy * cy / tz3) * dJ12;
 #pragma unroll
     for (int k = 0; k < 3; ++k) dm[k] += V[4 * k + 0] * dtx + V[4 * k + 1] * dty + V[4 * k + 2] * dtz;
-    out.means3D[3 * g + 0] = dm[0];
-    out.means3D[3 * g + 1] = dm[1];
-    out.means3D[3 * g + 2] = dm[2];
+    out.means3D[3 * o + 0] = dm[0];
+    out.means3D[3 * o + 1] = dm[1];
+    out.means3D[3 * o + 2] = dm[2];
     (void)p;
     // ---- cov3D -> scale, rotation ----
     if (in.cov3D) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) out.cov3D[6 * g + k] = dS[k];
+        for (int k = 0; k < 6; ++k) out.cov3D[6 * o + k] = dS[k];
         return;
     }
     const float Gm[9] = {dS[0], 0.5f * dS[1], 0.5f * dS[2], 0.5f * dS[1], dS[3], 0.5f * dS[4],
@@ -341,34 +341,35 @@ __device__ void preprocess_backward_one(const gsr_camera& cam, const GaussIn& in
             acc += dl * R[3 * i + j];
             dR[3 * i + j] = dl * se[j];
         }
-        out.scales[3 * g + j] = in.smod * acc;
+        out.scales[3 * o + j] = in.smod * acc;
     }
     const float r = q.x, x = q.y, y = q.z, z = q.w;
-    out.rots[4 * g + 0] = 2.f * (-z * dR[1] + y * dR[2] + z * dR[3] - x * dR[5] - y * dR[6] + x * dR[7]);
-    out.rots[4 * g + 1] = 2.f * (y * dR[1] + z * dR[2] + y * dR[3] - 2.f * x * dR[4] - r * dR[5] + z * dR[6] + r * dR[7] - 2.f * x * dR[8]);
-    out.rots[4 * g + 2] = 2.f * (-2.f * y * dR[0] + x * dR[1] + r * dR[2] + x * dR[3] + z * dR[5] - r * dR[6] + z * dR[7] - 2.f * y * dR[8]);
-    out.rots[4 * g + 3] = 2.f * (-2.f * z * dR[0] - r * dR[1] + x * dR[2] + r * dR[3] - 2.f * z * dR[4] + y * dR[5] + x * dR[6] + y * dR[7]);
+    out.rots[4 * o + 0] = 2.f * (-z * dR[1] + y * dR[2] + z * dR[3] - x * dR[5] - y * dR[6] + x * dR[7]);
+    out.rots[4 * o + 1] = 2.f * (y * dR[1] + z * dR[2] + y * dR[3] - 2.f * x * dR[4] - r * dR[5] + z * dR[6] + r * dR[7] - 2.f * x * dR[8]);
+    out.rots[4 * o + 2] = 2.f * (-2.f * y * dR[0] + x * dR[1] + r * dR[2] + x * dR[3] + z * dR[5] - r * dR[6] + z * dR[7] - 2.f * y * dR[8]);
+    out.rots[4 * o + 3] = 2.f * (-2.f * z * dR[0] - r * dR[1] + x * dR[2] + r * dR[3] - 2.f * z * dR[4] + y * dR[5] + x * dR[6] + y * dR[7]);
 }
 
+// Gaussians [g0, g0 + n): inputs indexed by g, grad2d and every output by o = g - g0.
 __global__ __launch_bounds__(256) void preprocess_backward_kernel(
-    const gsr_camera cam, const GaussIn in, const uint32_t* __restrict__ depth_key,
+    const gsr_camera cam, const GaussIn in, int g0, int n, const uint32_t* __restrict__ depth_key,
     const uint32_t* __restrict__ flags, const float* __restrict__ grad2d, GradOut out) {
     extern __shared__ __attribute__((aligned(16))) float sh_lds[];
-    const int g = blockIdx.x * 256 + threadIdx.x;
+    const int o = blockIdx.x * 256 + threadIdx.x;
     const int M3 = in.M_rest * 3;
     const bool stage = in.sh_rest != nullptr && !in.colors;  // block-uniform
-    const int rows = in.P - blockIdx.x * 256 < 256 ? in.P - blockIdx.x * 256 : 256;
-    const size_t base = (size_t)blockIdx.x * 256 * M3;
+    const int rows = n - blockIdx.x * 256 < 256 ? n - blockIdx.x * 256 : 256;
+    const size_t obase = (size_t)blockIdx.x * 256 * M3, ibase = (size_t)g0 * M3 + obase;
     if (stage) {  // coalesced staging of the block's SH-rest rows (see preprocess_kernel)
-        for (int i = threadIdx.x; i < rows * M3; i += 256) sh_lds[i] = in.sh_rest[base + i];
+        for (int i = threadIdx.x; i < rows * M3; i += 256) sh_lds[i] = in.sh_rest[ibase + i];
         __syncthreads();
     }
-    if (g < in.P)
-        preprocess_backward_one(cam, in, g, depth_key, flags, grad2d, out,
+    if (o < n)
+        preprocess_backward_one(cam, in, g0 + o, o, depth_key, flags, grad2d, out,
                                 stage ? sh_lds + threadIdx.x * M3 : nullptr);
     if (stage) {  // coalesced write-back of the SH-rest gradient rows
         __syncthreads();
-        for (int i = threadIdx.x; i < rows * M3; i += 256) out.sh_rest[base + i] = sh_lds[i];
+        for (int i = threadIdx.x; i < rows * M3; i += 256) out.sh_rest[obase + i] = sh_lds[i];
     }
 }
 
@@ -385,12 +386,13 @@ int launch_gather_grad2d(const uint32_t* gid_by_rank, const uint32_t* offsets, c
     return (int)hipGetLastError();
 }
 
-int launch_preprocess_backward(const gsr_camera& cam, const GaussIn& in, const uint32_t* depth_key,
-                               const uint32_t* flags, const float* grad2d, const GradOut& out,
-                               hipStream_t s) {
-    if (in.P <= 0) return 0;
+int launch_preprocess_backward(const gsr_camera& cam, const GaussIn& in, int g0, int g1,
+                               const uint32_t* depth_key, const uint32_t* flags, const float* grad2d,
+                               const GradOut& out, hipStream_t s) {
+    const int n = g1 - g0;
+    if (n <= 0) return 0;
     const size_t lds = (in.sh_rest && !in.colors) ? sizeof(float) * 256 * 3 * in.M_rest : 0;
-    hipLaunchKernelGGL(preprocess_backward_kernel, dim3(div_up(in.P, 256)), dim3(256), lds, s, cam, in,
+    hipLaunchKernelGGL(preprocess_backward_kernel, dim3(div_up(n, 256)), dim3(256), lds, s, cam, in, g0, n,
                        depth_key, flags, grad2d, out);
     return (int)hipGetLastError();
 }

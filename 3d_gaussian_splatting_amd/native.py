@@ -23,7 +23,7 @@ GSR_GRAD2D_STRIDE = 12
 VIEW_SORTED_GID, VIEW_SORTED_TILE, VIEW_RANGES, VIEW_FINAL_T, VIEW_N_CONTRIB, VIEW_DEPTH_KEY, \
     VIEW_TILES_TOUCHED, VIEW_RECORDS = range(1, 9)
 EXPORTS = ["gsr_abi_version", "gsr_last_error", "gsr_forward", "gsr_backward", "gsr_backward_blend",
-           "gsr_backward_preprocess", "gsr_view", "gsr_geom_bytes", "gsr_binning_bytes",
+           "gsr_backward_preprocess", "gsr_backward_preprocess_range", "gsr_view", "gsr_geom_bytes", "gsr_binning_bytes",
            "gsr_image_bytes", "gsr_scratch_bytes", "gsr_profile_enable", "gsr_profile_read",
            "gsr_stage_name"]
 STAGES = ["preprocess", "depth_sort", "scan", "duplicate", "tile_sort", "finalize", "blend_fwd", "blend_bwd",
@@ -95,6 +95,10 @@ def load_hip() -> ctypes.CDLL:
         L.gsr_backward_preprocess.argtypes = [ctypes.POINTER(Camera), ctypes.POINTER(Gaussians),
                                               ctypes.POINTER(Settings), ctypes.POINTER(Buffers), vp,
                                               ctypes.POINTER(Grads), vp]
+        L.gsr_backward_preprocess_range.restype = ctypes.c_int
+        L.gsr_backward_preprocess_range.argtypes = [ctypes.POINTER(Camera), ctypes.POINTER(Gaussians),
+                                                    ctypes.POINTER(Settings), ctypes.POINTER(Buffers), i32, i32,
+                                                    vp, ctypes.POINTER(Grads), vp]
         L.gsr_view.restype = vp
         L.gsr_view.argtypes = [ctypes.POINTER(Camera), i32, ctypes.POINTER(Buffers), ctypes.c_int]
         for n in ("gsr_geom_bytes", "gsr_binning_bytes", "gsr_scratch_bytes"):

@@ -137,8 +137,8 @@ class CAbiRasterizer:
         return ForwardState(cam=cam, inputs=inputs, settings=s, gauss=g, buffers=bufs, color=color,
                             radii=radii, allocs=[ag, ab, ai])
 
-    def _grad_tensors(self, st: ForwardState):
-        P = st.gauss.P
+    def _grad_tensors(self, st: ForwardState, P: int | None = None):
+        P = st.gauss.P if P is None else P
         dev = self.device
         e = lambda *shape: torch.empty(shape, dtype=torch.float32, device=dev)
         out = dict(means2D=e(P, 3), conic=e(P, 3), opacities=e(P, 1), means3D=e(P, 3))
@@ -148,7 +148,7 @@ class CAbiRasterizer:
         else:
             out["sh_dc"] = e(P, 1, 3)
             if inp["sh_rest"] is not None:
-                out["sh_rest"] = torch.empty_like(inp["sh_rest"])
+                out["sh_rest"] = inp["sh_rest"].new_empty((P,) + tuple(inp["sh_rest"].shape[1:]))
         if inp["cov3D_precomp"] is not None:
             out["cov3D"] = e(P, 6)
         else:
@@ -172,9 +172,17 @@ class CAbiRasterizer:
         self._check(rc, "gsr_backward")
         return out
 
-    def backward_blend(self, st: ForwardState, dL_dpix) -> torch.Tensor:
+    def backward_blend(self, st: ForwardState, dL_dpix, out: torch.Tensor | None = None) -> torch.Tensor:
+        """B1 + per-Gaussian sum -> grad2d (P x 12).  `out`: optional contiguous (>= P) x 12
+        tensor to write into (e.g. a buffer padded for a reduce-scatter)."""
         dpix = _f32(dL_dpix, (3, st.cam.height, st.cam.width), self.device)
-        grad2d = torch.empty((st.gauss.P, native.GSR_GRAD2D_STRIDE), dtype=torch.float32, device=self.device)
+        if out is None:
+            grad2d = torch.empty((st.gauss.P, native.GSR_GRAD2D_STRIDE), dtype=torch.float32, device=self.device)
+        else:
+            if not (out.is_contiguous() and out.dtype == torch.float32 and out.shape[0] >= st.gauss.P
+                    and out.shape[1] == native.GSR_GRAD2D_STRIDE):
+                raise ValueError("backward_blend: out must be a contiguous f32 (>= P) x 12 tensor")
+            grad2d = out
         scratch = _Allocator(self.device)
         c = native.camera_struct(st.cam)
         rc = self.L.gsr_backward_blend(ctypes.byref(c), ctypes.byref(st.gauss), ctypes.byref(st.settings),
@@ -191,6 +199,18 @@ class CAbiRasterizer:
                                             ctypes.byref(st.buffers), _ptr(grad2d), ctypes.byref(gg),
                                             self._stream())
         self._check(rc, "gsr_backward_preprocess")
+        return out
+
+    def backward_preprocess_range(self, st: ForwardState, g0: int, g1: int, grad2d: torch.Tensor) -> dict:
+        """B2 on Gaussians [g0, g1): `grad2d` holds that slice's rows; the returned gradients
+        are the slice's (g1 - g0 rows)."""
+        out, gg = self._grad_tensors(st, g1 - g0)
+        grad2d = grad2d.contiguous()
+        c = native.camera_struct(st.cam)
+        rc = self.L.gsr_backward_preprocess_range(ctypes.byref(c), ctypes.byref(st.gauss), ctypes.byref(st.settings),
+                                                  ctypes.byref(st.buffers), int(g0), int(g1), _ptr(grad2d),
+                                                  ctypes.byref(gg), self._stream())
+        self._check(rc, "gsr_backward_preprocess_range")
         return out
 
 

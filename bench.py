@@ -8,8 +8,9 @@
 One step = gsr_forward + gsr_backward (through the C ABI) of the whole synthetic scene:
 1M Gaussians, 1920x1080, SH degree 3 (BASELINE configs[2], the roofline run; inputs already
 resident in HBM).  N > 1: screen-space tile-row bands, one per rank (RCCL): replicated
-preprocess, band-local binning/blend, all-gather of the image bands, blend-backward on the
-band, all-reduce of the per-Gaussian 2D gradients, replicated preprocess-backward.  The
+preprocess, band-local binning/blend, asynchronous all-gather of the image bands (overlaps
+the blend backward), blend-backward on the band, reduce-scatter of the per-Gaussian 2D
+gradients, preprocess-backward on the rank's Gaussian slice (leaf gradients sharded).  The
 whole image is rendered once per step for the job, so value = steps/s of the job
 ("scaling": "strong").  Rank 0 prints ONE JSON line.
 
@@ -90,18 +91,23 @@ def main():
     ap.add_argument("--config", default="1m_1080p", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stage-events", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL, one GPU per rank) or gloo (rehearsal: ranks may share a GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local_rank % max(ndev, 1))
+    torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
-    torch.cuda.set_device(dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     cfg = CONFIGS[args.config]
     P, W, H, D = cfg["P"], cfg["W"], cfg["H"], cfg["D"]
@@ -115,14 +121,18 @@ def main():
     dpix = t(dpix_np)
     gx, gy = cam.grid
     band = bands.band_rows(gy, world, rank) if world > 1 else None
+    if world > 1:
+        g0, g1 = bands.gaussian_slice(P, world, rank)
+        g2_padded = torch.zeros((bands.padded_rows(P, world), native.GSR_GRAD2D_STRIDE), device=dev)
 
     def step():
         st = rast.forward(cam, **inputs, sh_degree=D, tile_rows=band)
         if world > 1:
-            bands.gather_image(st.color, band, gy, dist)  # full image on every rank
-            g2 = rast.backward_blend(st, dpix)
-            bands.reduce_grad2d(g2, dist)
-            g = rast.backward_preprocess(st, g2)
+            img = bands.ImageGather(st.color, band, gy, dist)  # overlaps the blend backward
+            rast.backward_blend(st, dpix, out=g2_padded)
+            mine = bands.reduce_scatter_grad2d(g2_padded, dist)
+            g = rast.backward_preprocess_range(st, g0, g1, mine[: g1 - g0])  # leaf grads of my slice
+            img.wait()  # full image on every rank
         else:
             g = rast.backward(st, dpix)
         return st, g
@@ -189,7 +199,7 @@ def main():
                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                               "traffic": pmc.get("hbm_bytes_per_launch"), "mean_launch_ms": round(mean_ms, 4),
                               "algorithmic_bytes_per_launch": int(bytes_launch)}
-        if "valu_insts_per_launch" in pmc:
+        if "valu_insts_per_launch" in pmc and world == 1:  # PMC counts are of the N = 1 launch
             # F6/B1 are VALU-issue-bound, not HBM-bound (DESIGN.md "Rooflines"): share of the
             # chip's VALU issue slots (1024 SIMDs x one wave64 op per 4 cycles at 2.4 GHz) that
             # the kernel's measured instruction count fills over its measured duration.

@@ -17,6 +17,7 @@
  *   gsr_backward           <- loss.backward() into it  (B1+B2, a17-a18)
  *   gsr_backward_blend     <- B1 + per-Gaussian sum only (multi-GPU: all-reduce between)
  *   gsr_backward_preprocess<- B2 only, from per-Gaussian 2D gradients
+ *   gsr_backward_preprocess_range <- B2 on one Gaussian slice (multi-GPU, after reduce-scatter)
  *
  * Conventions
  *   - Every pointer in gsr_gaussians / gsr_grads / outputs is caller-owned DEVICE memory
@@ -133,6 +134,14 @@ int gsr_backward_blend(const gsr_camera* cam, const gsr_gaussians* gs,
 int gsr_backward_preprocess(const gsr_camera* cam, const gsr_gaussians* gs,
                             const gsr_raster_settings* rs, const gsr_buffers* bufs,
                             const float* grad2d, const gsr_grads* grads, void* stream);
+
+/* B2 on the Gaussian slice [g0, g1) only (multi-GPU: each rank owns a slice after a
+ * reduce-scatter of grad2d).  grad2d holds the slice's (g1 - g0) rows, and every output in
+ * `grads` is the slice's own array (row g - g0); the inputs in `gs` stay full-size. */
+int gsr_backward_preprocess_range(const gsr_camera* cam, const gsr_gaussians* gs,
+                                  const gsr_raster_settings* rs, const gsr_buffers* bufs,
+                                  int32_t g0, int32_t g1, const float* grad2d,
+                                  const gsr_grads* grads, void* stream);
 
 /* Introspection for tests / the benchmark (all device pointers into the caller's buffers,
  * or NULL when not applicable).  `what`: see gsr_view_* below. */

@@ -4,9 +4,10 @@
 
 Checks (SURVEY §8e parity rules):
 * the all-gathered band images equal the single-process full render bit for bit;
-* the sum over ranks of the band-local 2D gradients (mean2D, conic, opacity, colour -- what
-  gsr_backward_blend returns as grad2d) equals the full-image 2D gradients, and so do the
-  leaf gradients after the chain rule (B2 is linear in grad2d), within 1e-5 relative L2;
+* the reduce-scatter of the band-local 2D gradients (mean2D, conic, opacity, colour -- what
+  gsr_backward_blend returns as grad2d) gives each rank its Gaussian slice of the full-image
+  2D gradients (slices re-assembled here to compare), and the leaf gradients after the chain
+  rule (B2 is linear in grad2d) sum to the full-image ones, within 1e-5 relative L2;
 * bands partition the tile rows for every world size up to 8 and uneven heights.
 """
 import os
@@ -55,10 +56,17 @@ def _worker(rank, port, outdir):
         gy = (H + 15) // 16
         band = bands.band_rows(gy, WORLD, rank)
         f, g = _render(cam, scene, dpix, tile_rows=band)
-        full = bands.gather_image(torch.from_numpy(f.color), band, gy, dist)
-        grad2d = torch.from_numpy(np.concatenate(
-            [g["means2D"][:, :2], g["conic"], g["opacities"], g["colors"]], axis=1).copy())
-        bands.reduce_grad2d(grad2d, dist)
+        img = bands.ImageGather(torch.from_numpy(f.color), band, gy, dist)
+        P = g["means2D"].shape[0]
+        g2d = np.concatenate([g["means2D"][:, :2], g["conic"], g["opacities"], g["colors"]], axis=1)
+        padded = torch.zeros((bands.padded_rows(P, WORLD), g2d.shape[1]))
+        padded[:P] = torch.from_numpy(g2d)
+        g0, g1 = bands.gaussian_slice(P, WORLD, rank)
+        mine = bands.reduce_scatter_grad2d(padded, dist)[: g1 - g0].clone()
+        slices = [torch.zeros_like(padded[: padded.shape[0] // WORLD]) for _ in range(WORLD)]
+        dist.all_gather(slices, torch.nn.functional.pad(mine, (0, 0, 0, slices[0].shape[0] - mine.shape[0])))
+        grad2d = torch.cat(slices)[:P]
+        full = img.wait()
         leaf = {k: torch.from_numpy(g[k].copy()) for k in ("means3D", "scales", "rotations", "sh_dc", "sh_rest",
                                                           "opacities")}
         for v in leaf.values():
