@@ -13,7 +13,9 @@ bit-identical to the same rows of a single-GPU render.  The exchange is two coll
   (``gaussian_slice``) and runs B2 on that slice only (``gsr_backward_preprocess_range``),
   so the leaf gradients -- and an optimizer step after them -- are sharded by Gaussian.
 
-``ImageGather`` starts the image all-gather asynchronously so it overlaps the blend backward.
+``exchange_grad2d`` is the sparse form of the reduce-scatter: only a band's candidate
+Gaussians carry gradient, so only their rows travel.  ``ImageGather`` starts the image
+all-gather asynchronously so it overlaps the blend backward.
 
 Both work on any torch.distributed backend (RCCL on the GPU box, gloo in the CPU tests).
 """
@@ -60,6 +62,46 @@ def reduce_scatter_grad2d(grad2d_padded: torch.Tensor, dist, group=None) -> torc
         return grad2d_padded[rank * S:(rank + 1) * S]
     out = grad2d_padded.new_empty((S,) + tuple(grad2d_padded.shape[1:]))
     dist.reduce_scatter_tensor(out, grad2d_padded, group=group)
+    return out
+
+
+def exchange_grad2d(grad2d: torch.Tensor, cand: torch.Tensor, P: int, dist, group=None) -> torch.Tensor:
+    """Sparse reduce-scatter of the 2D gradients: a band only produced rows for its candidate
+    Gaussians (``cand``: their ids, e.g. ``GSR_VIEW_GID_BY_RANK``), so each rank sends just
+    those rows, bucketed by owning rank (``gaussian_slice``), in one all_to_all.  The owner
+    places every received row in a per-source dense slab and sums the slabs, so the result
+    is the same fixed-order sum whatever the arrival order.  Returns this rank's slice
+    (ceil(P / world) rows x 12).  The gid rides in padding column 9 of each row."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    S = -(-P // world)
+    width = grad2d.shape[1]
+    if width < 10:
+        raise ValueError("exchange_grad2d: rows need a padding column 9 (GSR_GRAD2D_STRIDE = 12)")
+    dev = grad2d.device
+    cand = cand.to(torch.int64)
+    owner = torch.div(cand, S, rounding_mode="floor")
+    order = torch.argsort(owner, stable=True)
+    cs = cand[order]
+    rows = grad2d.index_select(0, cs)
+    rows[:, 9] = cs.to(torch.int32).view(torch.float32)
+    send = torch.bincount(owner, minlength=world)
+    # gloo has no device all-to-all: stage through host memory there
+    host = dist.get_backend(group) == "gloo" and dev.type != "cpu"
+    xdev = torch.device("cpu") if host else dev
+    send_x = send.to(xdev)
+    recv_x = torch.empty_like(send_x)
+    dist.all_to_all_single(recv_x, send_x, group=group)
+    sc, rc = send_x.tolist(), recv_x.tolist()
+    got = torch.empty((sum(rc), width), dtype=rows.dtype, device=xdev)
+    dist.all_to_all_single(got, rows.to(xdev), rc, sc, group=group)
+    got = got.to(dev)
+    gid = got[:, 9].contiguous().view(torch.int32).to(torch.int64) - rank * S
+    src = torch.repeat_interleave(torch.arange(world, device=dev), torch.tensor(rc, device=dev))
+    dense = grad2d.new_zeros((world, S, width))
+    dense[src, gid] = got
+    out = dense.sum(0)
+    out[:, 9] = 0.0
     return out
 
 

@@ -253,21 +253,43 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
     if (P > 0) {
         PreOut po{radii, depth_key, tiles, flags, rec, at<uint2>(bufs->geom, gl.rect)};
         GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess(*cam, gauss_in(gs), ty0, ty1, po, stream), "preprocess");
-        int which = -1;
-        GSR_STAGE(GSR_STAGE_DEPTH_SORT, radix_sort(depth_key, nullptr, at<uint32_t>(bufs->geom, gl.sB_k),
+        // A band ranks only its candidates (Gaussians with tiles in the band): the depth sort,
+        // scan, duplicate and gather then scale with the band, not with P.
+        const bool banded = ty0 > 0 || ty1 < gy;
+        int NR = P;
+        const uint32_t* sort_keys = depth_key;
+        const uint32_t* sort_vals = nullptr;
+        if (banded) {
+            uint32_t* cnt = at<uint32_t>(bufs->geom, gl.counters);
+            GSR_STAGE(GSR_STAGE_DEPTH_SORT, compact_candidates(tiles, depth_key, P, at<uint32_t>(bufs->geom, gl.partials),
+                                                               offsets, inst_start, cnt, stream),
+                      "band candidates");
+            uint32_t n32 = 0;
+            GSR_STAGE(GSR_STAGE_MISC, hipMemcpyAsync(&n32, cnt, sizeof n32, hipMemcpyDeviceToHost, stream),
+                      "read candidate count");
+            GSR_CHECK_HIP(hipStreamSynchronize(stream), "sync candidate count");
+            NR = (int)n32;
+            sort_keys = offsets;  // free until the scan; inst_start until duplicate
+            sort_vals = inst_start;
+        }
+        bufs->num_ranked = NR;
+        int which = NR > 0 ? -1 : 1;
+        GSR_STAGE(GSR_STAGE_DEPTH_SORT, radix_sort(sort_keys, sort_vals, at<uint32_t>(bufs->geom, gl.sB_k),
                                  at<uint32_t>(bufs->geom, gl.sB_v), at<uint32_t>(bufs->geom, gl.sA_k),
-                                 at<uint32_t>(bufs->geom, gl.sA_v), P, 32, at<uint32_t>(bufs->geom, gl.hist),
+                                 at<uint32_t>(bufs->geom, gl.sA_v), NR, 32, at<uint32_t>(bufs->geom, gl.hist),
                                  &which, stream),
                       "depth sort");
-        if (which != 1) return fail(-12, "depth sort ended in an unexpected buffer");
+        if (NR > 0 && which != 1) return fail(-12, "depth sort ended in an unexpected buffer");
         const uint32_t* gid_by_rank = at<uint32_t>(bufs->geom, gl.sA_v);
-        GSR_STAGE(GSR_STAGE_SCAN, inclusive_scan_gather(tiles, gid_by_rank, offsets, P,
-                                            at<uint32_t>(bufs->geom, gl.partials), stream),
-                      "scan");
         uint32_t k32 = 0;
-        GSR_STAGE(GSR_STAGE_MISC, hipMemcpyAsync(&k32, offsets + (P - 1), sizeof k32, hipMemcpyDeviceToHost, stream),
+        if (NR > 0) {
+            GSR_STAGE(GSR_STAGE_SCAN, inclusive_scan_gather(tiles, gid_by_rank, offsets, NR,
+                                                at<uint32_t>(bufs->geom, gl.partials), stream),
+                      "scan");
+            GSR_STAGE(GSR_STAGE_MISC, hipMemcpyAsync(&k32, offsets + (NR - 1), sizeof k32, hipMemcpyDeviceToHost, stream),
                       "read num_rendered");
-        GSR_CHECK_HIP(hipStreamSynchronize(stream), "sync num_rendered");
+            GSR_CHECK_HIP(hipStreamSynchronize(stream), "sync num_rendered");
+        }
         K = k32;
         if (K > INT32_MAX) return fail(-3, "num_rendered overflow (%lld)", K);
         bufs->num_rendered = (int32_t)K;
@@ -279,7 +301,7 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
         uint32_t* kB = at<uint32_t>(bufs->binning, bl.kB);
         uint32_t* vB = at<uint32_t>(bufs->binning, bl.vB);
         uint32_t* inst_gid = at<uint32_t>(bufs->binning, bl.inst_gid);
-        GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate(gid_by_rank, offsets, tiles, at<uint2>(bufs->geom, gl.rect), P, gx, ty0, ty1, inst_start, kA,
+        GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate(gid_by_rank, offsets, tiles, at<uint2>(bufs->geom, gl.rect), NR, gx, ty0, ty1, inst_start, kA,
                                        inst_gid, stream),
                       "duplicate");
         if (K > 0) {
@@ -300,6 +322,17 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
                                        v.accum, stream),
                   "blend forward");
     return 0;
+}
+
+// Per-Gaussian grad2d for all P: the gather covers the ranked Gaussians (a band's candidates);
+// the rest touched no tile of the band and get zeros.
+static int gather_all(const Views& v, const gsr_buffers* bufs, const float* partial, long long K, int P,
+                      float* grad2d, hipStream_t stream) {
+    const int NR = bufs->num_ranked > 0 ? bufs->num_ranked : P;
+    if (NR < P) {
+        if (hipError_t e = hipMemsetAsync(grad2d, 0, sizeof(float) * kPart * (size_t)P, stream)) return (int)e;
+    }
+    return launch_gather_grad2d(v.gid_by_rank, v.offsets, partial, K, NR, grad2d, stream);
 }
 
 static int backward_impl(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
@@ -326,7 +359,7 @@ static int backward_impl(const gsr_camera* cam, const gsr_gaussians* gs, const g
     }
     if (grad2d) {
         if (K > 0) {
-            GSR_STAGE(GSR_STAGE_GATHER, launch_gather_grad2d(v.gid_by_rank, v.offsets, partial, K, P, grad2d, stream), "gather grad2d");
+            GSR_STAGE(GSR_STAGE_GATHER, gather_all(v, bufs, partial, K, P, grad2d, stream), "gather grad2d");
         } else {
             GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(grad2d, 0, sizeof(float) * kPart * (size_t)P, stream), "zero grad2d");
         }
@@ -383,7 +416,7 @@ int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raste
         GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.inst_start, v.rect, v.rec,
                                             v.final_T, v.accum, dL_dpix, partial, K, stream),
                       "blend backward");
-        GSR_STAGE(GSR_STAGE_GATHER, launch_gather_grad2d(v.gid_by_rank, v.offsets, partial, K, P, grad2d, stream),
+        GSR_STAGE(GSR_STAGE_GATHER, gather_all(v, bufs, partial, K, P, grad2d, stream),
                   "gather grad2d");
     } else {
         GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(grad2d, 0, sizeof(float) * kPart * (size_t)P, stream), "zero grad2d");
@@ -483,6 +516,7 @@ const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, 
         case GSR_VIEW_DEPTH_KEY: return v.depth_key;
         case GSR_VIEW_TILES_TOUCHED: return v.tiles;
         case GSR_VIEW_RECORDS: return v.rec;
+        case GSR_VIEW_GID_BY_RANK: return v.gid_by_rank;
         default: return nullptr;
     }
 }

@@ -29,7 +29,7 @@ inline int sort_blocks(long long n) { return n > 0 ? div_up(n, kSortTile) : 0; }
 
 struct GeomLayout {
     size_t depth_key, tiles, flags, rec, rect, inst_start, offsets, sA_k, sA_v, sB_k, sB_v, hist,
-        partials, total;
+        partials, counters, total;
     GeomLayout(int P) {
         size_t o = 0, n = (size_t)(P > 0 ? P : 1);
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
@@ -46,6 +46,7 @@ struct GeomLayout {
         sB_v = take(4 * n);
         hist = take(4 * (256 * (size_t)(sort_blocks(n) + 1) + 256));
         partials = take(4 * ((size_t)sort_blocks(n) + 16));
+        counters = take(64);  // [0]: band candidate count
         total = o;
     }
 };

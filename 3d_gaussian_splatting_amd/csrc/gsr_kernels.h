@@ -37,6 +37,11 @@ int radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* k0, u
 int inclusive_scan_gather(const uint32_t* in, const uint32_t* idx, uint32_t* out, int n,
                           uint32_t* partials, hipStream_t s);
 
+// Band candidates: the Gaussians with tiles[g] != 0, in gid order -> (depth key, gid) pairs
+// and their count (device u32).  partials: sort_blocks(n) + 16 u32.
+int compact_candidates(const uint32_t* tiles, const uint32_t* depth_key, int n, uint32_t* partials,
+                       uint32_t* keys_out, uint32_t* gids_out, uint32_t* count_out, hipStream_t s);
+
 // F3: emit (tile key, owner gid) for every (Gaussian, tile in band) in depth-rank order
 int launch_duplicate(const uint32_t* gid_by_rank, const uint32_t* offsets, const uint32_t* tiles,
                      const uint2* rect, int P, int grid_x, int ty0, int ty1, uint32_t* inst_start,

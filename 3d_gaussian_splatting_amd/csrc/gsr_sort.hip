@@ -300,6 +300,63 @@ __global__ __launch_bounds__(kB) void scan_downsweep(const uint32_t* __restrict_
 
 // ---- F3 duplicate: wave-cooperative expansion (one wave = 64 consecutive ranks, whose
 // instances are contiguous; lanes write consecutive instances -> coalesced stores) ----
+// ---- band candidates: order-preserving compaction of the Gaussians with tiles in the band ----
+// A block owns kSortTile consecutive gids; wave w handles the contiguous 1024-gid run
+// [w*1024, (w+1)*1024) of it in 16 rounds of 64 lanes, so ballot prefix counts keep gid order.
+__global__ __launch_bounds__(kB) void compact_count(const uint32_t* __restrict__ tiles, int n,
+                                                   uint32_t* __restrict__ partials) {
+    __shared__ uint32_t wsum[kWaves];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int base = blockIdx.x * kSortTile + w * kWaveItems;
+    uint32_t c = 0;
+#pragma unroll
+    for (int r = 0; r < kI; ++r) {
+        const int g = base + r * 64 + lane;
+        c += __popcll(__ballot(g < n && tiles[g] != 0u));
+    }
+    if (lane == 0) wsum[w] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int k = 0; k < kWaves; ++k) t += wsum[k];
+        partials[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(kB) void compact_scatter(const uint32_t* __restrict__ tiles,
+                                                     const uint32_t* __restrict__ depth_key, int n,
+                                                     const uint32_t* __restrict__ partials,
+                                                     uint32_t* __restrict__ keys_out,
+                                                     uint32_t* __restrict__ gids_out,
+                                                     uint32_t* __restrict__ count_out) {
+    __shared__ uint32_t wsum[kWaves];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int base = blockIdx.x * kSortTile + w * kWaveItems;
+    uint32_t c = 0;
+#pragma unroll
+    for (int r = 0; r < kI; ++r) {
+        const int g = base + r * 64 + lane;
+        c += __popcll(__ballot(g < n && tiles[g] != 0u));
+    }
+    if (lane == 0) wsum[w] = c;
+    __syncthreads();
+    uint32_t pos = partials[blockIdx.x];
+    for (int k = 0; k < w; ++k) pos += wsum[k];
+#pragma unroll
+    for (int r = 0; r < kI; ++r) {
+        const int g = base + r * 64 + lane;
+        const bool keep = g < n && tiles[g] != 0u;
+        const uint64_t m = __ballot(keep);
+        if (keep) {
+            const uint32_t at = pos + (uint32_t)__popcll(m & lanemask_lt());
+            keys_out[at] = depth_key[g];
+            gids_out[at] = (uint32_t)g;
+        }
+        pos += (uint32_t)__popcll(m);
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kB - 1) *count_out = pos;
+}
+
 __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restrict__ gid_by_rank,
                                                         const uint32_t* __restrict__ offsets,
                                                         const uint32_t* __restrict__ tiles,
@@ -401,6 +458,17 @@ int inclusive_scan_gather(const uint32_t* in, const uint32_t* idx, uint32_t* out
     hipLaunchKernelGGL(scan_reduce, dim3(nb), dim3(kB), 0, s, in, idx, n, partials);
     hipLaunchKernelGGL(scan_partials, dim3(1), dim3(1024), 0, s, partials, nb);
     hipLaunchKernelGGL(scan_downsweep, dim3(nb), dim3(kB), 0, s, in, idx, n, partials, out);
+    return (int)hipGetLastError();
+}
+
+int compact_candidates(const uint32_t* tiles, const uint32_t* depth_key, int n, uint32_t* partials,
+                       uint32_t* keys_out, uint32_t* gids_out, uint32_t* count_out, hipStream_t s) {
+    if (n <= 0) return 0;
+    const int nb = sort_blocks(n);
+    hipLaunchKernelGGL(compact_count, dim3(nb), dim3(kB), 0, s, tiles, n, partials);
+    hipLaunchKernelGGL(scan_partials, dim3(1), dim3(1024), 0, s, partials, nb);
+    hipLaunchKernelGGL(compact_scatter, dim3(nb), dim3(kB), 0, s, tiles, depth_key, n, partials, keys_out,
+                       gids_out, count_out);
     return (int)hipGetLastError();
 }
 

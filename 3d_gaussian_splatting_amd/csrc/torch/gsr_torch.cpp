@@ -97,6 +97,7 @@ void* cur_stream() { return (void*)c10::hip::getCurrentHIPStream().stream(); }
 struct FwdResult {
     torch::Tensor color, radii, geom, binning, image;
     int32_t K;
+    int32_t NR;  // num_ranked
 };
 
 FwdResult forward_impl(const RasterCamera& cam, const RasterSettings& rs, const torch::Tensor& means3D,
@@ -127,16 +128,18 @@ FwdResult forward_impl(const RasterCamera& cam, const RasterSettings& rs, const 
     r.binning = bin.keep.empty() ? torch::Tensor() : bin.keep.at(0);
     r.image = img.keep.at(0);
     r.K = b.num_rendered;
+    r.NR = b.num_ranked;
     return r;
 }
 
 gsr_buffers buffers_of(const torch::Tensor& geom, const torch::Tensor& binning, const torch::Tensor& image,
-                       int32_t K) {
+                       int32_t K, int32_t NR) {
     gsr_buffers b{};
     b.geom = geom.data_ptr();
     b.binning = binning.defined() ? binning.data_ptr() : nullptr;
     b.image = image.data_ptr();
     b.num_rendered = K;
+    b.num_ranked = NR;
     return b;
 }
 
@@ -154,6 +157,7 @@ class RasterizeGaussians : public torch::autograd::Function<RasterizeGaussians> 
         ctx->save_for_backward({means3D, sh_dc, sh_rest, colors, opac, scales, rots, cov3D, r.geom, r.binning,
                                 r.image});
         ctx->saved_data["K"] = (int64_t)r.K;
+        ctx->saved_data["NR"] = (int64_t)r.NR;
         ctx->saved_data["cam_w"] = (int64_t)cam.width;
         ctx->saved_data["cam_h"] = (int64_t)cam.height;
         ctx->saved_data["cam_tx"] = (double)cam.tanfovx;
@@ -194,6 +198,7 @@ class RasterizeGaussians : public torch::autograd::Function<RasterizeGaussians> 
         rs.tile_y1 = (int)ctx->saved_data["ty1"].toInt();
         rs.debug = ctx->saved_data["debug"].toBool();
         const int32_t K = (int32_t)ctx->saved_data["K"].toInt();
+        const int32_t NR = (int32_t)ctx->saved_data["NR"].toInt();
         auto dL_dcolor = grad_out[0].contiguous();
         const int64_t P = means3D.size(0);
         auto fo = means3D.options();
@@ -228,7 +233,7 @@ class RasterizeGaussians : public torch::autograd::Function<RasterizeGaussians> 
         const gsr_camera c = cam.to_c();
         const gsr_gaussians g = make_gaussians(rs, means3D, sh_dc, sh_rest, colors, opac, scales, rots, cov3D);
         const gsr_raster_settings s = make_settings(rs);
-        const gsr_buffers b = buffers_of(geom, binning, image, K);
+        const gsr_buffers b = buffers_of(geom, binning, image, K, NR);
         AllocCtx scratch{means3D.device(), {}};
         check(gsr_backward(&c, &g, &s, &b, dL_dcolor.data_ptr<float>(), alloc_cb, &scratch, &gg, cur_stream()),
               "gsr_backward");

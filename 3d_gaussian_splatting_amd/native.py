@@ -21,7 +21,7 @@ HIP_LIB = os.path.join(LIB_DIR, "libgsr_hip.so")
 GSR_FLAG_DEBUG = 1
 GSR_GRAD2D_STRIDE = 12
 VIEW_SORTED_GID, VIEW_SORTED_TILE, VIEW_RANGES, VIEW_FINAL_T, VIEW_N_CONTRIB, VIEW_DEPTH_KEY, \
-    VIEW_TILES_TOUCHED, VIEW_RECORDS = range(1, 9)
+    VIEW_TILES_TOUCHED, VIEW_RECORDS, VIEW_GID_BY_RANK = range(1, 10)
 EXPORTS = ["gsr_abi_version", "gsr_last_error", "gsr_forward", "gsr_backward", "gsr_backward_blend",
            "gsr_backward_preprocess", "gsr_backward_preprocess_range", "gsr_view", "gsr_geom_bytes", "gsr_binning_bytes",
            "gsr_image_bytes", "gsr_scratch_bytes", "gsr_profile_enable", "gsr_profile_read",
@@ -57,7 +57,7 @@ class Grads(ctypes.Structure):
 
 class Buffers(ctypes.Structure):
     _fields_ = [("geom", ctypes.c_void_p), ("binning", ctypes.c_void_p), ("image", ctypes.c_void_p),
-                ("num_rendered", ctypes.c_int32)]
+                ("num_rendered", ctypes.c_int32), ("num_ranked", ctypes.c_int32)]
 
 
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)

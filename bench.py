@@ -9,8 +9,9 @@ One step = gsr_forward + gsr_backward (through the C ABI) of the whole synthetic
 1M Gaussians, 1920x1080, SH degree 3 (BASELINE configs[2], the roofline run; inputs already
 resident in HBM).  N > 1: screen-space tile-row bands, one per rank (RCCL): replicated
 preprocess, band-local binning/blend, asynchronous all-gather of the image bands (overlaps
-the blend backward), blend-backward on the band, reduce-scatter of the per-Gaussian 2D
-gradients, preprocess-backward on the rank's Gaussian slice (leaf gradients sharded).  The
+the blend backward), blend-backward on the band, sparse all-to-all of the band candidates'
+2D gradients to the ranks owning their Gaussian slice, preprocess-backward on the rank's
+slice (leaf gradients sharded).  The
 whole image is rendered once per step for the job, so value = steps/s of the job
 ("scaling": "strong").  Rank 0 prints ONE JSON line.
 
@@ -123,14 +124,14 @@ def main():
     band = bands.band_rows(gy, world, rank) if world > 1 else None
     if world > 1:
         g0, g1 = bands.gaussian_slice(P, world, rank)
-        g2_padded = torch.zeros((bands.padded_rows(P, world), native.GSR_GRAD2D_STRIDE), device=dev)
 
     def step():
         st = rast.forward(cam, **inputs, sh_degree=D, tile_rows=band)
         if world > 1:
             img = bands.ImageGather(st.color, band, gy, dist)  # overlaps the blend backward
-            rast.backward_blend(st, dpix, out=g2_padded)
-            mine = bands.reduce_scatter_grad2d(g2_padded, dist)
+            g2 = rast.backward_blend(st, dpix)
+            cand = st.view(native.VIEW_GID_BY_RANK, torch.int32, st.buffers.num_ranked)
+            mine = bands.exchange_grad2d(g2, cand, P, dist)  # only the band's candidates travel
             g = rast.backward_preprocess_range(st, g0, g1, mine[: g1 - g0])  # leaf grads of my slice
             img.wait()  # full image on every rank
         else:

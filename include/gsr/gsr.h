@@ -28,7 +28,8 @@
  *     buffers through gsr_alloc_fn (geometry: per Gaussian, binning: per tile instance,
  *     image: per pixel); the caller keeps them alive and passes them back to backward.
  *   - Streams: all work is ordered on `stream` (a hipStream_t; NULL = default stream).
- *     Exactly one device->host read per forward (num_rendered) synchronises that stream.
+ *     One device->host read per forward (num_rendered) synchronises that stream; a banded
+ *     forward (tile_y0/y1 narrower than the image) adds a second (its candidate count).
  *   - Errors: 0 = ok, < 0 = error; message in gsr_last_error() (thread-local).
  *   - Re-entrant; no global state besides the thread-local error string and the optional,
  *     off-by-default stage profiler (gsr_profile_*).
@@ -103,6 +104,8 @@ typedef struct gsr_buffers {
     void* binning;           /* returned by the binning allocation (may be NULL if K == 0) */
     void* image;             /* returned by the image allocation */
     int32_t num_rendered;    /* K = number of (Gaussian, tile) instances */
+    int32_t num_ranked;      /* Gaussians in the depth ranking: P for a full image; for a band,
+                                only those with tiles in the band (pass back unchanged) */
 } gsr_buffers;
 
 int gsr_abi_version(void);
@@ -154,6 +157,8 @@ int gsr_backward_preprocess_range(const gsr_camera* cam, const gsr_gaussians* gs
                                        termination point from T                             */
 #define GSR_VIEW_DEPTH_KEY 6        /* uint32[P]: depth bits, 0xFFFFFFFF when culled       */
 #define GSR_VIEW_TILES_TOUCHED 7    /* uint32[P]                                           */
+#define GSR_VIEW_GID_BY_RANK 9      /* uint32[num_ranked]: Gaussian ids in depth order (a band's
+                                       candidates: exactly the Gaussians it can touch)      */
 #define GSR_VIEW_RECORDS 8          /* float4[3*P]: {x,y,a',b'},{c',o,r,g},{b,ext_x,ext_y,log2 o};
                                        a',b',c' = -log2(e) * (A/2, B, C/2) of the conic */
 const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, int what);

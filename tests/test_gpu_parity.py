@@ -122,6 +122,14 @@ def test_band_sharded_equals_full(rast):
     for y0, y1 in bands:
         st = rast.forward(*args, sh_degree=3, tile_rows=(y0, y1))
         img[:, y0 * 16:y1 * 16] = st.color[:, y0 * 16:y1 * 16]
+        # the band ranks exactly its candidates (Gaussians with tiles in the band), depth-sorted
+        native = pkg("native")
+        nr = st.buffers.num_ranked
+        cand = _np(st.view(native.VIEW_GID_BY_RANK, torch.int32, nr)).astype(np.int64)
+        tt = _np(st.view(native.VIEW_TILES_TOUCHED, torch.int32, s.P))
+        key = _np(st.view(native.VIEW_DEPTH_KEY, torch.int32, s.P)).view(np.uint32)
+        np.testing.assert_array_equal(np.sort(cand), np.nonzero(tt)[0])
+        assert np.all(np.diff(key[cand].astype(np.int64)) >= 0)
         g2 = rast.backward_blend(st, dpix)
         grad2d = g2 if grad2d is None else grad2d + g2
         last = st

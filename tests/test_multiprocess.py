@@ -59,13 +59,17 @@ def _worker(rank, port, outdir):
         img = bands.ImageGather(torch.from_numpy(f.color), band, gy, dist)
         P = g["means2D"].shape[0]
         g2d = np.concatenate([g["means2D"][:, :2], g["conic"], g["opacities"], g["colors"]], axis=1)
-        padded = torch.zeros((bands.padded_rows(P, WORLD), g2d.shape[1]))
-        padded[:P] = torch.from_numpy(g2d)
+        padded = torch.zeros((bands.padded_rows(P, WORLD), 12))  # GSR_GRAD2D_STRIDE rows
+        padded[:P, :9] = torch.from_numpy(g2d)
         g0, g1 = bands.gaussian_slice(P, WORLD, rank)
-        mine = bands.reduce_scatter_grad2d(padded, dist)[: g1 - g0].clone()
+        mine = bands.reduce_scatter_grad2d(padded.clone(), dist)[: g1 - g0].clone()
+        # sparse form: only the band's candidates (Gaussians with tiles in the band) travel
+        cand = torch.from_numpy(np.nonzero(f.state.preprocess()["tiles_touched"])[0].astype(np.int32))
+        sparse = bands.exchange_grad2d(padded[:P].clone(), cand, P, dist)[: g1 - g0]
+        assert torch.equal(sparse[:, :9], mine[:, :9]) or float((sparse[:, :9] - mine[:, :9]).abs().max()) < 1e-6
         slices = [torch.zeros_like(padded[: padded.shape[0] // WORLD]) for _ in range(WORLD)]
         dist.all_gather(slices, torch.nn.functional.pad(mine, (0, 0, 0, slices[0].shape[0] - mine.shape[0])))
-        grad2d = torch.cat(slices)[:P]
+        grad2d = torch.cat(slices)[:P, :9]
         full = img.wait()
         leaf = {k: torch.from_numpy(g[k].copy()) for k in ("means3D", "scales", "rotations", "sh_dc", "sh_rest",
                                                           "opacities")}
