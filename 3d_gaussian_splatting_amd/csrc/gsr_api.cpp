@@ -23,6 +23,42 @@ namespace {
 
 thread_local std::string g_err;
 
+// Low-latency device->host read of one u32: DMA into a per-thread pinned word, then spin on
+// it.  hipStreamSynchronize after a pageable copy measured ~100 us from the end of the scan
+// to the next launch (profiles/r01_kernel_stats + trace); the spin wakes within ~µs.
+struct PinnedWord {
+    volatile uint32_t* p = nullptr;
+    PinnedWord() {
+        void* q = nullptr;
+        if (hipHostMalloc(&q, 64, hipHostMallocDefault) == hipSuccess) p = static_cast<volatile uint32_t*>(q);
+    }
+    ~PinnedWord() {
+        if (p) (void)hipHostFree(const_cast<uint32_t*>(p));
+    }
+};
+thread_local PinnedWord g_pinned;
+
+int read_u32(const uint32_t* dev, uint32_t* out, hipStream_t stream) {
+    constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // never a valid count (< INT32_MAX checked)
+    if (!g_pinned.p) {  // no pinned memory: plain copy + stream sync
+        if (hipError_t e = hipMemcpyAsync(out, dev, sizeof *out, hipMemcpyDeviceToHost, stream)) return (int)e;
+        return (int)hipStreamSynchronize(stream);
+    }
+    *g_pinned.p = kSentinel;
+    if (hipError_t e = hipMemcpyAsync(const_cast<uint32_t*>(g_pinned.p), dev, sizeof(uint32_t),
+                                      hipMemcpyDeviceToHost, stream))
+        return (int)e;
+    for (long spins = 0; *g_pinned.p == kSentinel; ++spins) {
+        if (spins > (1l << 20) && hipStreamQuery(stream) == hipSuccess) {
+            if (*g_pinned.p == kSentinel) return (int)hipErrorUnknown;  // copy done, word never written
+            break;
+        }
+        __builtin_ia32_pause();
+    }
+    *out = *g_pinned.p;
+    return 0;
+}
+
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 int fail(int code, const char* fmt, ...) {
     char buf[512];
@@ -265,9 +301,7 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
                                                                offsets, inst_start, cnt, stream),
                       "band candidates");
             uint32_t n32 = 0;
-            GSR_STAGE(GSR_STAGE_MISC, hipMemcpyAsync(&n32, cnt, sizeof n32, hipMemcpyDeviceToHost, stream),
-                      "read candidate count");
-            GSR_CHECK_HIP(hipStreamSynchronize(stream), "sync candidate count");
+            GSR_STAGE(GSR_STAGE_MISC, read_u32(cnt, &n32, stream), "read candidate count");
             NR = (int)n32;
             sort_keys = offsets;  // free until the scan; inst_start until duplicate
             sort_vals = inst_start;
@@ -277,7 +311,7 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
         GSR_STAGE(GSR_STAGE_DEPTH_SORT, radix_sort(sort_keys, sort_vals, at<uint32_t>(bufs->geom, gl.sB_k),
                                  at<uint32_t>(bufs->geom, gl.sB_v), at<uint32_t>(bufs->geom, gl.sA_k),
                                  at<uint32_t>(bufs->geom, gl.sA_v), NR, 32, at<uint32_t>(bufs->geom, gl.hist),
-                                 &which, stream),
+                                 &which, stream, true),
                       "depth sort");
         if (NR > 0 && which != 1) return fail(-12, "depth sort ended in an unexpected buffer");
         const uint32_t* gid_by_rank = at<uint32_t>(bufs->geom, gl.sA_v);
@@ -286,9 +320,7 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
             GSR_STAGE(GSR_STAGE_SCAN, inclusive_scan_gather(tiles, gid_by_rank, offsets, NR,
                                                 at<uint32_t>(bufs->geom, gl.partials), stream),
                       "scan");
-            GSR_STAGE(GSR_STAGE_MISC, hipMemcpyAsync(&k32, offsets + (NR - 1), sizeof k32, hipMemcpyDeviceToHost, stream),
-                      "read num_rendered");
-            GSR_CHECK_HIP(hipStreamSynchronize(stream), "sync num_rendered");
+            GSR_STAGE(GSR_STAGE_MISC, read_u32(offsets + (NR - 1), &k32, stream), "read num_rendered");
         }
         K = k32;
         if (K > INT32_MAX) return fail(-3, "num_rendered overflow (%lld)", K);
@@ -307,7 +339,7 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
         if (K > 0) {
             int w2 = -1;
             GSR_STAGE(GSR_STAGE_TILE_SORT, radix_sort(kA, inst_gid, kB, vB, kA, vA, K, tile_bits(gx * gy),
-                                     at<uint32_t>(bufs->binning, bl.hist), &w2, stream),
+                                     at<uint32_t>(bufs->binning, bl.hist), &w2, stream, false),
                           "tile sort");
             const bool odd = (tile_passes(gx * gy) & 1) != 0;
             if ((w2 == 0) != odd) return fail(-12, "tile sort ended in an unexpected buffer");

@@ -26,6 +26,13 @@ constexpr int kPart = GSR_GRAD2D_STRIDE;    // floats per partial / grad2d entry
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 inline int div_up(long long a, long long b) { return (int)((a + b - 1) / b); }
 inline int sort_blocks(long long n) { return n > 0 ? div_up(n, kSortTile) : 0; }
+// radix-sort scratch (u32 words): reduce-then-scan needs 256 x (blocks + 1) + 256; onesweep
+// needs 4 x 256 digit totals + 16 tickets + 4 passes x blocks x 256 look-back words.
+inline size_t sort_scratch_words(long long n) {
+    const size_t nb = (size_t)sort_blocks(n) + 1;
+    const size_t a = 256 * nb + 256, b = 4 * 256 + 16 + 4 * nb * 256;
+    return a > b ? a : b;
+}
 
 struct GeomLayout {
     size_t depth_key, tiles, flags, rec, rect, inst_start, offsets, sA_k, sA_v, sB_k, sB_v, hist,
@@ -44,7 +51,7 @@ struct GeomLayout {
         sA_v = take(4 * n);
         sB_k = take(4 * n);
         sB_v = take(4 * n);
-        hist = take(4 * (256 * (size_t)(sort_blocks(n) + 1) + 256));
+        hist = take(4 * sort_scratch_words(n));
         partials = take(4 * ((size_t)sort_blocks(n) + 16));
         counters = take(64);  // [0]: band candidate count
         total = o;
@@ -61,7 +68,7 @@ struct BinLayout {
         kB = take(4 * n);
         vB = take(4 * n);
         inst_gid = take(4 * n);
-        hist = take(4 * (256 * (size_t)(sort_blocks(n) + 1) + 256));
+        hist = take(4 * sort_scratch_words(n));
         total = o;
     }
 };

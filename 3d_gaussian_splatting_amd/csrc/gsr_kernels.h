@@ -29,9 +29,11 @@ int launch_preprocess(const gsr_camera& cam, const GaussIn& in, int ty0, int ty1
 // LSD radix sort of (u32 key, u32 value) by key bits [0, nbits); vals_in == nullptr means the
 // identity permutation.  Ping-pongs between (k0,v0) and (k1,v1); returns in *which (0/1) where
 // the sorted data ended.  hist: 256*(blocks+1)+256 u32.
+// depth_sort: selects the per-pass scheme (onesweep look-back for the P-key depth sort,
+// reduce-then-scan for the K-key tile sort; gsr_sort.hip use_onesweep).
 int radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* k0, uint32_t* v0,
                uint32_t* k1, uint32_t* v1, long long n, int nbits, uint32_t* hist, int* which,
-               hipStream_t s);
+               hipStream_t s, bool depth_sort);
 
 // inclusive scan out[r] = sum_{q<=r} in[idx ? idx[q] : q]; partials: blocks+16 u32
 int inclusive_scan_gather(const uint32_t* in, const uint32_t* idx, uint32_t* out, int n,

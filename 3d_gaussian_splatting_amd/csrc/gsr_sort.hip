@@ -19,6 +19,8 @@
 // scan (per digit over blocks), downsweep (stable wave64 ranking: 8 ballots give each lane
 // its peer mask, popcount below it is its rank in the round; per-wave running counters in
 // LDS; digit base = scanned counts).  All integer work: HBM-bound, no MFMA.
+#include <cstdlib>
+
 #include "gsr_kernels.h"
 
 namespace gsr {
@@ -187,6 +189,170 @@ __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict
 #pragma unroll
         for (int k = 0; k < kWaves; ++k) pre += (k < w) ? wsum[k] : 0u;
         lbase[tid] = pre + x - c;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kI; ++r) {
+        const long long idx = base + r * 64 + lane;
+        if (idx < n) {
+            const uint32_t d = (key[r] >> shift) & mask;
+            const uint32_t lp = lbase[d] + wcnt[w][d] + rank[r];
+            skey[lp] = key[r];
+            sval[lp] = val[r];
+        }
+    }
+    __syncthreads();
+    const int count = (n - bbase) < kSortTile ? (int)(n - bbase) : kSortTile;
+#pragma unroll 4
+    for (int i = tid; i < count; i += kB) {
+        const uint32_t k = skey[i];
+        const uint32_t d = (k >> shift) & mask;
+        const uint32_t pos = gbase[d] + (uint32_t)i - lbase[d];
+        keys_out[pos] = k;
+        vals_out[pos] = sval[i];
+    }
+}
+
+// ---- onesweep LSD radix sort: one kernel per 8-bit pass ----
+// Global digit histograms for every pass come from one read of the keys (radix_hist_all);
+// each pass then needs a single kernel: a block takes the next tile in launch order (atomic
+// ticket, so every tile it waits on is already resident), ranks its 4096 keys exactly as
+// radix_downsweep does, publishes its per-digit counts, and finds the count of each digit
+// in all earlier tiles by decoupled look-back over their published (flag | count) words
+// (relaxed agent-scope atomics, the packed word makes flag and count one atomic).  Each pass
+// reads and writes the keys/values once -- the reduce-then-scan form reads the keys twice
+// and runs three kernels per pass.
+constexpr uint32_t kAgg = 1u << 30, kInc = 2u << 30, kCntMask = kAgg - 1u;
+
+__global__ __launch_bounds__(kB) void radix_hist_all(const uint32_t* __restrict__ keys, long long n,
+                                                     int nbits, uint32_t* __restrict__ ghist) {
+    __shared__ uint32_t h[4][256];
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) h[p][tid] = 0;
+    __syncthreads();
+    const int npass = (nbits + 7) / 8;
+    const long long base = (long long)blockIdx.x * kSortTile;
+#pragma unroll 4
+    for (int r = 0; r < kI; ++r) {
+        const long long idx = base + r * kB + tid;
+        if (idx < n) {
+            const uint32_t k = keys[idx];
+            for (int p = 0; p < npass; ++p) {
+                const int bits = (nbits - 8 * p) < 8 ? (nbits - 8 * p) : 8;
+                atomicAdd(&h[p][(k >> (8 * p)) & ((1u << bits) - 1u)], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    for (int p = 0; p < npass; ++p)
+        if (h[p][tid]) atomicAdd(&ghist[p * 256 + tid], h[p][tid]);
+}
+
+__global__ __launch_bounds__(kB) void radix_onesweep(const uint32_t* __restrict__ keys_in,
+                                                     const uint32_t* __restrict__ vals_in,
+                                                     uint32_t* __restrict__ keys_out,
+                                                     uint32_t* __restrict__ vals_out, long long n,
+                                                     int shift, int nbits,
+                                                     const uint32_t* __restrict__ ghist,
+                                                     uint32_t* __restrict__ status,
+                                                     uint32_t* __restrict__ ticket) {
+    __shared__ uint32_t wcnt[kWaves][256];
+    __shared__ uint32_t gbase[256];
+    __shared__ uint32_t lbase[256];
+    __shared__ uint32_t wsum[kWaves];
+    __shared__ uint32_t skey[kSortTile];
+    __shared__ uint32_t sval[kSortTile];
+    __shared__ int s_tile;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const uint32_t mask = (1u << nbits) - 1u;
+    if (tid == 0) s_tile = (int)atomicAdd(ticket, 1u);
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) wcnt[k][tid] = 0;
+    __syncthreads();
+    const int tile = s_tile;
+    const long long bbase = (long long)tile * kSortTile;
+    const long long base = bbase + (long long)w * kWaveItems;
+    uint32_t key[kI], val[kI], rank[kI];
+    const uint64_t lt = lanemask_lt();
+#pragma unroll
+    for (int r = 0; r < kI; ++r) {
+        const long long idx = base + r * 64 + lane;
+        const bool valid = idx < n;
+        key[r] = valid ? keys_in[idx] : 0xFFFFFFFFu;
+        val[r] = valid ? (vals_in ? vals_in[idx] : (uint32_t)idx) : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < kI; ++r) {
+        const long long idx = base + r * 64 + lane;
+        const bool valid = idx < n;
+        const uint32_t d = (key[r] >> shift) & mask;
+        const uint64_t active = __ballot(valid);
+        const uint64_t peers = match_digit(d, nbits, active);
+        const uint32_t old = wcnt[w][d];
+        rank[r] = old + (uint32_t)__popcll(peers & lt);
+        if (valid && (peers & lt) == 0) wcnt[w][d] = old + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    uint32_t c = 0;  // this tile's count of digit `tid`
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) {
+        const uint32_t t = wcnt[k][tid];
+        wcnt[k][tid] = c;
+        c += t;
+    }
+    // publish, then look back over earlier tiles for digit `tid`
+    uint32_t* my = status + (size_t)tile * 256 + tid;
+    uint32_t excl = 0;
+    if (tile == 0) {
+        __hip_atomic_store(my, kInc | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        __hip_atomic_store(my, kAgg | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int t = tile - 1;
+        uint32_t spins = 0;
+        while (t >= 0) {
+            const uint32_t v = __hip_atomic_load(status + (size_t)t * 256 + tid, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            if ((v & ~kCntMask) == 0u) {
+                if (++spins > (1u << 26)) break;  // never expected: bounded so a bug cannot hang the GPU
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            excl += v & kCntMask;
+            if (v & kInc) break;
+            --t;
+        }
+        __hip_atomic_store(my, kInc | (excl + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    {
+        // global digit base = exclusive scan of the pass histogram + earlier tiles' count
+        const uint32_t v = ghist[tid];
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        uint32_t pre = 0;
+#pragma unroll
+        for (int k = 0; k < kWaves; ++k) pre += (k < w) ? wsum[k] : 0u;
+        gbase[tid] = pre + x - v + excl;
+        __syncthreads();  // wsum reuse
+        // block-local digit starts
+        uint32_t y = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t z = __shfl_up(y, o, 64);
+            if (lane >= o) y += z;
+        }
+        if (lane == 63) wsum[w] = y;
+        __syncthreads();
+        uint32_t pre2 = 0;
+#pragma unroll
+        for (int k = 0; k < kWaves; ++k) pre2 += (k < w) ? wsum[k] : 0u;
+        lbase[tid] = pre2 + y - c;
     }
     __syncthreads();
 #pragma unroll
@@ -425,11 +591,53 @@ __global__ __launch_bounds__(256) void finalize_kernel(const uint32_t* __restric
 
 }  // namespace
 
+// A/B selector (bench/ablation only; read per call like the blend variants):
+// 0 = reduce-then-scan everywhere, 1 = onesweep everywhere, 2 (shipped) = onesweep for the
+// depth sort (P keys: latency-bound, one kernel per pass wins) and reduce-then-scan for the
+// tile sort (K keys: the look-back chain over ~1600 tiles costs more than the extra read).
+static bool use_onesweep(bool depth_sort) {
+    const char* e = std::getenv("GSR_SORT_VARIANT");
+    const int v = e ? std::atoi(e) : 2;
+    return v == 1 || (v == 2 && depth_sort);
+}
+
+// onesweep: ghist (4 x 256) | tickets (16) | status (passes x nb x 256); one memset per sort
+static int radix_sort_onesweep(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* k0, uint32_t* v0,
+                               uint32_t* k1, uint32_t* v1, long long n, int nbits, uint32_t* hist, int* which,
+                               hipStream_t s) {
+    const int nb = sort_blocks(n);
+    const int npass = (nbits + 7) / 8;
+    uint32_t* ghist = hist;
+    uint32_t* tickets = hist + 4 * 256;
+    uint32_t* status = tickets + 16;
+    const size_t words = 4 * 256 + 16 + (size_t)npass * nb * 256;
+    if (hipError_t e = hipMemsetAsync(hist, 0, words * sizeof(uint32_t), s)) return (int)e;
+    hipLaunchKernelGGL(radix_hist_all, dim3(nb), dim3(kB), 0, s, keys_in, n, nbits, ghist);
+    const uint32_t* kin = keys_in;
+    const uint32_t* vin = vals_in;
+    int dst = 0;
+    for (int p = 0; p < npass; ++p) {
+        const int shift = 8 * p;
+        const int bits = (nbits - shift) < 8 ? (nbits - shift) : 8;
+        uint32_t* ko = dst == 0 ? k0 : k1;
+        uint32_t* vo = dst == 0 ? v0 : v1;
+        hipLaunchKernelGGL(radix_onesweep, dim3(nb), dim3(kB), 0, s, kin, vin, ko, vo, n, shift, bits,
+                           ghist + 256 * p, status + (size_t)p * nb * 256, tickets + p);
+        kin = ko;
+        vin = vo;
+        *which = dst;
+        dst ^= 1;
+    }
+    return (int)hipGetLastError();
+}
+
 int radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* k0, uint32_t* v0,
                uint32_t* k1, uint32_t* v1, long long n, int nbits, uint32_t* hist, int* which,
-               hipStream_t s) {
+               hipStream_t s, bool depth_sort) {
     *which = -1;
     if (n <= 0) return 0;
+    if (use_onesweep(depth_sort))
+        return radix_sort_onesweep(keys_in, vals_in, k0, v0, k1, v1, n, nbits, hist, which, s);
     const int nb = sort_blocks(n);
     uint32_t* totals = hist + (size_t)256 * (nb + 1);
     const uint32_t* kin = keys_in;
