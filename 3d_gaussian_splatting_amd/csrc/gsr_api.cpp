@@ -27,10 +27,11 @@ thread_local std::string g_err;
 // it.  hipStreamSynchronize after a pageable copy measured ~100 us from the end of the scan
 // to the next launch (profiles/r01_kernel_stats + trace); the spin wakes within ~µs.
 struct PinnedWord {
+    static constexpr int kWords = 256;
     volatile uint32_t* p = nullptr;
     PinnedWord() {
         void* q = nullptr;
-        if (hipHostMalloc(&q, 64, hipHostMallocDefault) == hipSuccess) p = static_cast<volatile uint32_t*>(q);
+        if (hipHostMalloc(&q, 4 * kWords, hipHostMallocDefault) == hipSuccess) p = static_cast<volatile uint32_t*>(q);
     }
     ~PinnedWord() {
         if (p) (void)hipHostFree(const_cast<uint32_t*>(p));
@@ -38,24 +39,36 @@ struct PinnedWord {
 };
 thread_local PinnedWord g_pinned;
 
-int read_u32(const uint32_t* dev, uint32_t* out, hipStream_t stream) {
-    constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // never a valid count (< INT32_MAX checked)
+// Reads n <= PinnedWord::kWords consecutive u32 counts (each < 2^31) in two steps: begin_read enqueues one DMA
+// into the pinned words (stream-ordered: it lands when the producing kernel is done);
+// end_read spins until every word has changed from the sentinel.  Work enqueued between the
+// two keeps the GPU busy while the host waits.
+int begin_read(const uint32_t* dev, int n, hipStream_t stream) {
+    if (!g_pinned.p) return 0;
+    for (int i = 0; i < n; ++i) g_pinned.p[i] = 0xFFFFFFFFu;
+    return (int)hipMemcpyAsync(const_cast<uint32_t*>(g_pinned.p), dev, sizeof(uint32_t) * n,
+                               hipMemcpyDeviceToHost, stream);
+}
+
+int end_read(const uint32_t* dev, uint32_t* out, int n, hipStream_t stream) {
     if (!g_pinned.p) {  // no pinned memory: plain copy + stream sync
-        if (hipError_t e = hipMemcpyAsync(out, dev, sizeof *out, hipMemcpyDeviceToHost, stream)) return (int)e;
+        if (hipError_t e = hipMemcpyAsync(out, dev, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, stream))
+            return (int)e;
         return (int)hipStreamSynchronize(stream);
     }
-    *g_pinned.p = kSentinel;
-    if (hipError_t e = hipMemcpyAsync(const_cast<uint32_t*>(g_pinned.p), dev, sizeof(uint32_t),
-                                      hipMemcpyDeviceToHost, stream))
-        return (int)e;
-    for (long spins = 0; *g_pinned.p == kSentinel; ++spins) {
+    auto done = [&] {
+        for (int i = 0; i < n; ++i)
+            if (g_pinned.p[i] == 0xFFFFFFFFu) return false;
+        return true;
+    };
+    for (long spins = 0; !done(); ++spins) {
         if (spins > (1l << 20) && hipStreamQuery(stream) == hipSuccess) {
-            if (*g_pinned.p == kSentinel) return (int)hipErrorUnknown;  // copy done, word never written
+            if (!done()) return (int)hipErrorUnknown;  // stream drained, words never written
             break;
         }
         __builtin_ia32_pause();
     }
-    *out = *g_pinned.p;
+    for (int i = 0; i < n; ++i) out[i] = g_pinned.p[i];
     return 0;
 }
 
@@ -283,11 +296,13 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
                            rs->bg[2]);
         GSR_STAGE(GSR_STAGE_MISC, hipGetLastError(), "fill_background");
     }
-    GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(ranges, 0, sizeof(uint2) * (size_t)gx * gy, stream), "memset ranges");
+    uint32_t* counters = at<uint32_t>(bufs->image, il.counters);
+    GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(ranges, 0, il.counters + 4 * 2 * kCountSlots - il.ranges, stream),
+              "memset ranges");
 
     long long K = 0;
     if (P > 0) {
-        PreOut po{radii, depth_key, tiles, flags, rec, at<uint2>(bufs->geom, gl.rect)};
+        PreOut po{radii, depth_key, tiles, flags, rec, at<uint2>(bufs->geom, gl.rect), counters};
         GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess(*cam, gauss_in(gs), ty0, ty1, po, stream), "preprocess");
         // A band ranks only its candidates (Gaussians with tiles in the band): the depth sort,
         // scan, duplicate and gather then scale with the band, not with P.
@@ -295,14 +310,23 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
         int NR = P;
         const uint32_t* sort_keys = depth_key;
         const uint32_t* sort_vals = nullptr;
+        uint32_t cw[2 * kCountSlots];  // preprocess's count partials: candidates, then K
+        uint32_t cnt[2] = {0, 0};
+        auto sum_counts = [&] {
+            uint64_t c = 0, k = 0;
+            for (int i = 0; i < kCountSlots; ++i) c += cw[i], k += cw[kCountSlots + i];
+            cnt[0] = (uint32_t)(c < UINT32_MAX ? c : UINT32_MAX);
+            cnt[1] = (uint32_t)(k < UINT32_MAX ? k : UINT32_MAX);
+            return 0;
+        };
+        GSR_CHECK_HIP(begin_read(counters, 2 * kCountSlots, stream), "read counts");
         if (banded) {
-            uint32_t* cnt = at<uint32_t>(bufs->geom, gl.counters);
             GSR_STAGE(GSR_STAGE_DEPTH_SORT, compact_candidates(tiles, depth_key, P, at<uint32_t>(bufs->geom, gl.partials),
-                                                               offsets, inst_start, cnt, stream),
+                                                               offsets, inst_start, counters + 2 * kCountSlots, stream),
                       "band candidates");
-            uint32_t n32 = 0;
-            GSR_STAGE(GSR_STAGE_MISC, read_u32(cnt, &n32, stream), "read candidate count");
-            NR = (int)n32;
+            GSR_STAGE(GSR_STAGE_MISC, end_read(counters, cw, 2 * kCountSlots, stream), "read counts");
+            sum_counts();
+            NR = (int)cnt[0];
             sort_keys = offsets;  // free until the scan; inst_start until duplicate
             sort_vals = inst_start;
         }
@@ -314,15 +338,19 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
                                  &which, stream, true),
                       "depth sort");
         if (NR > 0 && which != 1) return fail(-12, "depth sort ended in an unexpected buffer");
+        // full image: K is read here, while the depth sort runs, so the host enqueues the rest
+        // of the forward without leaving the GPU idle
+        if (!banded) {
+            GSR_STAGE(GSR_STAGE_MISC, end_read(counters, cw, 2 * kCountSlots, stream), "read counts");
+            sum_counts();
+        }
         const uint32_t* gid_by_rank = at<uint32_t>(bufs->geom, gl.sA_v);
-        uint32_t k32 = 0;
         if (NR > 0) {
             GSR_STAGE(GSR_STAGE_SCAN, inclusive_scan_gather(tiles, gid_by_rank, offsets, NR,
                                                 at<uint32_t>(bufs->geom, gl.partials), stream),
                       "scan");
-            GSR_STAGE(GSR_STAGE_MISC, read_u32(offsets + (NR - 1), &k32, stream), "read num_rendered");
         }
-        K = k32;
+        K = cnt[1];
         if (K > INT32_MAX) return fail(-3, "num_rendered overflow (%lld)", K);
         bufs->num_rendered = (int32_t)K;
         bufs->binning = alloc_binning(ctx, BinLayout(K).total);

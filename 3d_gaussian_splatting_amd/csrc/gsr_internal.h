@@ -6,7 +6,7 @@
 //                                 | radix histogram (256 x blocks) | scan partials
 //   binning  (per instance, K):   tile key/val ping-pong 4 x u32 (values = Gaussian id)
 //                                 | inst_gid u32 (emission order) | radix histogram
-//   image    (per pixel):         ranges uint2[tiles] | final_T f32 | accum 3 x f32
+//   image    (per pixel):         ranges uint2[tiles] | counters | final_T f32 | accum 3 x f32
 //   scratch  (backward, per K):   partial moments float4[2] | partial float  (indexed by emission j)
 #pragma once
 #include <stddef.h>
@@ -22,6 +22,7 @@ constexpr int kSortItems = 16;              // items per thread
 constexpr int kSortTile = kSortBlock * kSortItems;  // 4096 items per block
 constexpr int kRecFloats = 12;              // 3 x float4 per Gaussian record
 constexpr int kPart = GSR_GRAD2D_STRIDE;    // floats per partial / grad2d entry
+constexpr int kCountSlots = 64;             // preprocess count partials (host sums them)
 
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 inline int div_up(long long a, long long b) { return (int)((a + b - 1) / b); }
@@ -36,7 +37,7 @@ inline size_t sort_scratch_words(long long n) {
 
 struct GeomLayout {
     size_t depth_key, tiles, flags, rec, rect, inst_start, offsets, sA_k, sA_v, sB_k, sB_v, hist,
-        partials, counters, total;
+        partials, total;
     GeomLayout(int P) {
         size_t o = 0, n = (size_t)(P > 0 ? P : 1);
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
@@ -53,7 +54,6 @@ struct GeomLayout {
         sB_v = take(4 * n);
         hist = take(4 * sort_scratch_words(n));
         partials = take(4 * ((size_t)sort_blocks(n) + 16));
-        counters = take(64);  // [0]: band candidate count
         total = o;
     }
 };
@@ -74,13 +74,14 @@ struct BinLayout {
 };
 
 struct ImgLayout {
-    size_t ranges, final_T, accum, total;
+    size_t ranges, counters, final_T, accum, total;
     ImgLayout(int W, int H) {
         size_t o = 0;
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
         size_t tiles = (size_t)div_up(W, kTile) * div_up(H, kTile);
         size_t pix = (size_t)W * H;
         ranges = take(8 * (tiles ? tiles : 1));
+        counters = take(4 * (2 * kCountSlots + 16));  // right after ranges: one memset clears both
         final_T = take(4 * (pix ? pix : 1));
         accum = take(12 * (pix ? pix : 1));  // colour sum without background, 3 x H x W
         total = o;

@@ -20,6 +20,8 @@ struct PreOut {
     uint32_t* flags;
     float4* rec;   // blend records: {x, y, a', b'}, {c', o, r, g}, {b, ext_x, ext_y, log2 o}
     uint2* rect;   // tile rect: (minx | miny << 16, maxx | maxy << 16), full image
+    uint32_t* counters;  // nullable, zeroed: [slot] += Gaussians with tiles in the band,
+                         // [kCountSlots + slot] += K (slot = block % kCountSlots)
 };
 
 // F1: projection, EWA cov2D, conic, radius, tile rect, SH->RGB (bit-exact vs the oracle)

@@ -32,20 +32,11 @@ __device__ inline int imax(int a, int b) { return a > b ? a : b; }
 // The block's SH-rest rows (256 Gaussians x M_rest x 3 floats, contiguous in HBM) are staged
 // through LDS with coalesced dword loads: read straight from HBM, each lane's 180-B row at a
 // 180-B lane stride would touch ~90 cache lines per load instruction and thrash L1.
-__global__ __launch_bounds__(256) void preprocess_kernel(const gsr_camera cam, const GaussIn in,
-                                                         int grid_x, int grid_y, int ty0, int ty1,
-                                                         PreOut out) {
-    extern __shared__ __attribute__((aligned(16))) float sh_lds[];
-    const int g = blockIdx.x * 256 + threadIdx.x;
+// One Gaussian; returns its band-clipped tiles_touched.
+__device__ __forceinline__ uint32_t preprocess_one(const gsr_camera& cam, const GaussIn& in, int g, int grid_x,
+                                                   int grid_y, int ty0, int ty1, const PreOut& out,
+                                                   const float* sh_lds) {
     const int M3 = in.M_rest * 3;
-    if (in.sh_rest && !in.colors && in.D > 0) {  // block-uniform
-        const size_t base = (size_t)blockIdx.x * 256 * M3;
-        const int rows = in.P - blockIdx.x * 256 < 256 ? in.P - blockIdx.x * 256 : 256;
-        const int cnt = rows * M3;
-        for (int i = threadIdx.x; i < cnt; i += 256) sh_lds[i] = in.sh_rest[base + i];
-        __syncthreads();
-    }
-    if (g >= in.P) return;
     const float* V = cam.viewmatrix;
     const float* Pm = cam.projmatrix;
     const float p0 = in.means3D[3 * g + 0], p1 = in.means3D[3 * g + 1], p2 = in.means3D[3 * g + 2];
@@ -216,6 +207,47 @@ __global__ __launch_bounds__(256) void preprocess_kernel(const gsr_camera cam, c
     out.radii[g] = radius_out;
     out.depth_key[g] = key_out;
     out.tiles[g] = tiles_out;
+    return tiles_out;
+}
+
+// The block's SH-rest rows are staged through LDS (see above).  The block also adds its
+// candidate count (Gaussians with tiles in the band) and instance count (sum of
+// tiles_touched) into counters[slot] / counters[kCountSlots + slot], so the host can read K
+// right after this kernel -- while the depth sort runs -- instead of after the scan.
+__global__ __launch_bounds__(256) void preprocess_kernel(const gsr_camera cam, const GaussIn in,
+                                                         int grid_x, int grid_y, int ty0, int ty1,
+                                                         PreOut out) {
+    extern __shared__ __attribute__((aligned(16))) float sh_lds[];
+    __shared__ uint32_t wk[4], wc[4];
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    const int M3 = in.M_rest * 3;
+    if (in.sh_rest && !in.colors && in.D > 0) {  // block-uniform
+        const size_t base = (size_t)blockIdx.x * 256 * M3;
+        const int rows = in.P - blockIdx.x * 256 < 256 ? in.P - blockIdx.x * 256 : 256;
+        const int cnt = rows * M3;
+        for (int i = threadIdx.x; i < cnt; i += 256) sh_lds[i] = in.sh_rest[base + i];
+        __syncthreads();
+    }
+    const uint32_t t = g < in.P ? preprocess_one(cam, in, g, grid_x, grid_y, ty0, ty1, out, sh_lds) : 0u;
+    if (out.counters) {
+        uint32_t k = t, c = t ? 1u : 0u;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            k += __shfl_xor(k, o, 64);
+            c += __shfl_xor(c, o, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            wk[threadIdx.x >> 6] = k;
+            wc[threadIdx.x >> 6] = c;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {  // spread over kCountSlots addresses: one hot word serialises
+            const uint32_t K = wk[0] + wk[1] + wk[2] + wk[3], C = wc[0] + wc[1] + wc[2] + wc[3];
+            const int slot = blockIdx.x & (kCountSlots - 1);
+            if (K) atomicAdd(out.counters + kCountSlots + slot, K);
+            if (C) atomicAdd(out.counters + slot, C);
+        }
+    }
 }
 
 }  // namespace
