@@ -90,24 +90,53 @@ __device__ inline float allreduce_rows(float a) {
 struct BlendGeom {
     int W, H, grid_x, ty0, nwg;
     float bg0, bg1, bg2;
+    int ellipse_cull;  // 1: exact ellipse stripe test on top of the box test (shipped)
 };
 
-// Which of the tile's four 16x4 pixel stripes (slot p = rows 4p..4p+3) the record's
-// alpha >= 1/255 footprint box can touch.  Exact culling: a pixel outside the (padded) box
-// fails the alpha test, so skipping it changes no output bit.
-__device__ inline uint32_t stripe_mask(const float4 r0, const float4 r2, float bx0, float by0) {
+// Which of the tile's four 16x4 pixel stripes (slot p = rows 4p..4p+3) can hold a pixel
+// with alpha >= 1/255.  Two conservative tests, both on the record the loading lane holds:
+//  1. the padded footprint box (ext_x, ext_y) must overlap the stripe;
+//  2. the footprint ellipse itself must reach the stripe's pixel-centre rectangle: with the
+//     PD form Q(d) = -(a' dx^2 + b' dx dy + c' dy^2) (the exponent without log2 o), a pixel
+//     passes alpha >= 1/255 iff Q <= log2(255 o), so the stripe is needed iff the minimum of Q
+//     over the rectangle (0 if the mean is inside, else the minimum over its four edges,
+//     each a clamped 1-D quadratic) is within that bound -- padded by 2 % + 0.05 for float
+//     rounding.  Records whose form is not negative definite keep the box test only.
+// Exact culling: a skipped stripe has no pixel that the per-pixel test would accept, so no
+// output bit changes; the ellipse test removes ~22 % of the box test's stripe evaluations
+// and ~17 % of the visited records at 1M/1080p (scripts/cull_stats.py).
+__device__ __forceinline__ float edge_min_q(float a, float b, float c, float u, float v0, float v1) {
+    // min over v in [v0, v1] of a u^2 + b u v + c v^2 (c > 0)
+    const float vs = fminf(fmaxf(-b * u / (2.0f * c), v0), v1);
+    return fmaf(fmaf(c, vs, b * u), vs, a * u * u);
+}
+
+__device__ inline uint32_t stripe_mask(const float4 r0, const float4 r1, const float4 r2, float bx0, float by0,
+                                       bool ellipse) {
     const float ex = r2.y, ey = r2.z;
     if (!(ex >= 0.0f) || r0.x + ex < bx0 || r0.x - ex > bx0 + 15.0f) return 0u;
     const float ylo = r0.y - ey, yhi = r0.y + ey;
+    // PD form coefficients (A dx^2 + B dx dy + C dy^2) and the log2-domain bound
+    const float A = -r0.z, B = -r0.w, C = -r1.x;
+    const bool pd = ellipse && A > 0.0f && C > 0.0f && 4.0f * A * C - B * B > 0.0f;
+    const float bound = fmaf(fmaxf(r2.w + 7.99435343f, 0.0f), 1.02f, 0.05f);  // log2(255 o)
+    const float x0 = bx0 - r0.x, x1 = bx0 + 15.0f - r0.x;  // rect in mean-relative coords
     uint32_t m = 0;
 #pragma unroll
     for (int p = 0; p < kPPL; ++p) {
         const float s0 = by0 + 4.0f * p;
-        m |= (yhi >= s0 && ylo <= s0 + 3.0f) ? (1u << p) : 0u;
+        bool hit = yhi >= s0 && ylo <= s0 + 3.0f;
+        if (hit && pd) {
+            const float y0 = s0 - r0.y, y1 = s0 + 3.0f - r0.y;
+            const bool inside = x0 <= 0.0f && x1 >= 0.0f && y0 <= 0.0f && y1 >= 0.0f;
+            const float q = fminf(fminf(edge_min_q(A, B, C, x0, y0, y1), edge_min_q(A, B, C, x1, y0, y1)),
+                                  fminf(edge_min_q(C, B, A, y0, x0, x1), edge_min_q(C, B, A, y1, x0, x1)));
+            hit = inside || q <= bound;
+        }
+        m |= hit ? (1u << p) : 0u;
     }
     return m;
 }
-
 
 // alpha of one (pixel, record) pair, with the reference's two rejections folded into the
 // select: power > 0 (here: exponent above log2 o) and alpha < 1/255 give 0.
@@ -160,7 +189,7 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
             srec[3 * tid + 0] = r0;
             srec[3 * tid + 1] = r1;
             srec[3 * tid + 2] = r2;
-            smk[tid] = stripe_mask(r0, r2, bx0, by0);
+            smk[tid] = stripe_mask(r0, r1, r2, bx0, by0, geo.ellipse_cull);
         } else {
             smk[tid] = 0u;
         }
@@ -318,7 +347,7 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
                 srec[3 * lane + 0] = q0;
                 srec[3 * lane + 1] = q1;
                 srec[3 * lane + 2] = r2;
-                smask = stripe_mask(q0, r2, bx0, by0);
+                smask = stripe_mask(q0, q1, r2, bx0, by0, geo.ellipse_cull);
             }
         }
 #pragma unroll
@@ -440,6 +469,7 @@ static BlendGeom make_geo(const gsr_camera& cam, const float bg[3], int ty0, int
     g.bg0 = bg[0];
     g.bg1 = bg[1];
     g.bg2 = bg[2];
+    g.ellipse_cull = variant("GSR_CULL_VARIANT", 1);
     return g;
 }
 
