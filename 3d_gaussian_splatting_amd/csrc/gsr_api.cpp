@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -22,6 +23,14 @@ using namespace gsr;
 namespace {
 
 thread_local std::string g_err;
+
+// A/B selector (bench/ablation only): 0 = three-kernel scan then duplicate (shipped),
+// 1 = fused look-back scan + duplicate (one kernel, but the look-back chain over P/256
+// blocks measured slower: 0.102 vs 0.084 ms at 1M).
+int scan_variant() {
+    const char* e = std::getenv("GSR_SCAN_VARIANT");
+    return e ? std::atoi(e) : 0;
+}
 
 // Low-latency device->host read of one u32: DMA into a per-thread pinned word, then spin on
 // it.  hipStreamSynchronize after a pageable copy measured ~100 us from the end of the scan
@@ -199,13 +208,13 @@ void band(const gsr_camera* cam, const gsr_raster_settings* rs, int* y0, int* y1
 }
 
 struct Views {
-    uint32_t *depth_key, *tiles, *flags, *inst_start, *offsets, *gid_by_rank;
+    uint32_t *depth_key, *tiles, *flags, *offsets, *gid_by_rank;
     float4* rec;
     uint2* ranges;
     float* final_T;
     float* accum;
     uint32_t *sorted_tile, *sorted_gid, *inst_gid;
-    uint2* rect;
+    uint4* rect;
 };
 
 Views views(const gsr_camera* cam, int P, const gsr_buffers* b) {
@@ -216,9 +225,8 @@ Views views(const gsr_camera* cam, int P, const gsr_buffers* b) {
     v.tiles = at<uint32_t>(b->geom, gl.tiles);
     v.flags = at<uint32_t>(b->geom, gl.flags);
     v.rec = at<float4>(b->geom, gl.rec);
-    v.inst_start = at<uint32_t>(b->geom, gl.inst_start);
     v.offsets = at<uint32_t>(b->geom, gl.offsets);
-    v.rect = at<uint2>(b->geom, gl.rect);
+    v.rect = at<uint4>(b->geom, gl.rect);
     // 32-bit depth key = 4 passes (even) -> result in the A buffers
     v.gid_by_rank = at<uint32_t>(b->geom, gl.sA_v);
     v.ranges = at<uint2>(b->image, il.ranges);
@@ -285,7 +293,7 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
     uint32_t* flags = at<uint32_t>(bufs->geom, gl.flags);
     float4* rec = at<float4>(bufs->geom, gl.rec);
     uint32_t* offsets = at<uint32_t>(bufs->geom, gl.offsets);
-    uint32_t* inst_start = at<uint32_t>(bufs->geom, gl.inst_start);
+    uint32_t* cand_tmp = at<uint32_t>(bufs->geom, gl.cand_tmp);
     uint2* ranges = at<uint2>(bufs->image, il.ranges);
     float* final_T = at<float>(bufs->image, il.final_T);
 
@@ -302,7 +310,7 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
 
     long long K = 0;
     if (P > 0) {
-        PreOut po{radii, depth_key, tiles, flags, rec, at<uint2>(bufs->geom, gl.rect), counters};
+        PreOut po{radii, depth_key, tiles, flags, rec, at<uint4>(bufs->geom, gl.rect), counters};
         GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess(*cam, gauss_in(gs), ty0, ty1, po, stream), "preprocess");
         // A band ranks only its candidates (Gaussians with tiles in the band): the depth sort,
         // scan, duplicate and gather then scale with the band, not with P.
@@ -322,13 +330,13 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
         GSR_CHECK_HIP(begin_read(counters, 2 * kCountSlots, stream), "read counts");
         if (banded) {
             GSR_STAGE(GSR_STAGE_DEPTH_SORT, compact_candidates(tiles, depth_key, P, at<uint32_t>(bufs->geom, gl.partials),
-                                                               offsets, inst_start, counters + 2 * kCountSlots, stream),
+                                                               offsets, cand_tmp, counters + 2 * kCountSlots, stream),
                       "band candidates");
             GSR_STAGE(GSR_STAGE_MISC, end_read(counters, cw, 2 * kCountSlots, stream), "read counts");
             sum_counts();
             NR = (int)cnt[0];
-            sort_keys = offsets;  // free until the scan; inst_start until duplicate
-            sort_vals = inst_start;
+            sort_keys = offsets;  // free until the scan
+            sort_vals = cand_tmp;
         }
         bufs->num_ranked = NR;
         int which = NR > 0 ? -1 : 1;
@@ -345,7 +353,8 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
             sum_counts();
         }
         const uint32_t* gid_by_rank = at<uint32_t>(bufs->geom, gl.sA_v);
-        if (NR > 0) {
+        const bool fused = scan_variant() == 1;
+        if (NR > 0 && !fused) {
             GSR_STAGE(GSR_STAGE_SCAN, inclusive_scan_gather(tiles, gid_by_rank, offsets, NR,
                                                 at<uint32_t>(bufs->geom, gl.partials), stream),
                       "scan");
@@ -361,9 +370,16 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
         uint32_t* kB = at<uint32_t>(bufs->binning, bl.kB);
         uint32_t* vB = at<uint32_t>(bufs->binning, bl.vB);
         uint32_t* inst_gid = at<uint32_t>(bufs->binning, bl.inst_gid);
-        GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate(gid_by_rank, offsets, tiles, at<uint2>(bufs->geom, gl.rect), NR, gx, ty0, ty1, inst_start, kA,
-                                       inst_gid, stream),
+        if (fused) {
+            GSR_STAGE(GSR_STAGE_DUPLICATE, launch_scan_duplicate(gid_by_rank, tiles, at<uint4>(bufs->geom, gl.rect), NR, gx, ty0,
+                                                offsets, kA, inst_gid,
+                                                at<uint32_t>(bufs->geom, gl.hist), stream),
+                      "scan + duplicate");
+        } else {
+            GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate(gid_by_rank, offsets, tiles, at<uint4>(bufs->geom, gl.rect), NR, gx, ty0, ty1,
+                                               kA, inst_gid, stream),
                       "duplicate");
+        }
         if (K > 0) {
             int w2 = -1;
             GSR_STAGE(GSR_STAGE_TILE_SORT, radix_sort(kA, inst_gid, kB, vB, kA, vA, K, tile_bits(gx * gy),
@@ -413,7 +429,7 @@ static int backward_impl(const gsr_camera* cam, const gsr_gaussians* gs, const g
         if (!alloc_scratch) return fail(-1, "null scratch allocator");
         partial = static_cast<float*>(alloc_scratch(ctx, gsr_scratch_bytes((int32_t)K)));
         if (!partial) return fail(-2, "allocation failed (scratch, K=%lld)", K);
-        GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.inst_start, v.rect, v.rec,
+        GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.rect, v.rec,
                                             v.final_T, v.accum, dL_dpix, partial, K, stream),
                       "blend backward");
     }
@@ -473,7 +489,7 @@ int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raste
     float* grad2d = static_cast<float*>(alloc_scratch(ctx, sizeof(float) * kPart * (size_t)P));
     if (!partial || !grad2d) return fail(-2, "allocation failed (scratch, K=%lld, P=%d)", K, P);
     if (K > 0) {
-        GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.inst_start, v.rect, v.rec,
+        GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.rect, v.rec,
                                             v.final_T, v.accum, dL_dpix, partial, K, stream),
                       "blend backward");
         GSR_STAGE(GSR_STAGE_GATHER, gather_all(v, bufs, partial, K, P, grad2d, stream),

@@ -285,8 +285,7 @@ template <bool DEFER>
 __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
                                                             const uint2* __restrict__ ranges,
                                                             const uint32_t* __restrict__ sorted_gid,
-                                                            const uint32_t* __restrict__ inst_start,
-                                                            const uint2* __restrict__ rect,
+                                                            const uint4* __restrict__ rect,
                                                             const float4* __restrict__ rec,
                                                             const float* __restrict__ final_T,
                                                             const float* __restrict__ accum,
@@ -335,10 +334,10 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
         float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0;
         if (lane < cnt) {
             const uint32_t g = sorted_gid[range.x + e_l];
-            const uint2 rr = rect[g];
+            const uint4 rr = rect[g];  // rect + inst_start in one 16-B load
             const int minx = rr.x & 0xFFFF, miny = rr.x >> 16, maxx = rr.y & 0xFFFF;
             const int y0 = miny > geo.ty0 ? miny : geo.ty0;
-            jl = inst_start[g] + (uint32_t)((ty - y0) * (maxx - minx) + (tx - minx));
+            jl = rr.z + (uint32_t)((ty - y0) * (maxx - minx) + (tx - minx));
             if (live) {
                 const float4* r = rec + 3 * (size_t)g;
                 q0 = r[0];
@@ -492,8 +491,8 @@ int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int 
 }
 
 int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
-                          const uint2* ranges, const uint32_t* sorted_gid, const uint32_t* inst_start,
-                          const uint2* rect, const float4* rec, const float* final_T,
+                          const uint2* ranges, const uint32_t* sorted_gid, const uint4* rect,
+                          const float4* rec, const float* final_T,
                           const float* accum, const float* dL_dpix, float* partial, long long K,
                           hipStream_t s) {
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1);
@@ -503,11 +502,11 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
     // 1: deferred quad/LDS reduction (shipped); 0: full per-record DPP/permlane reduction
     if (variant("GSR_BWD_VARIANT", 1) == 0)
         hipLaunchKernelGGL(blend_backward_kernel<false>, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid,
-                           inst_start, rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(base + pl.p8),
+                           rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(base + pl.p8),
                            reinterpret_cast<float*>(base + pl.p1));
     else
         hipLaunchKernelGGL(blend_backward_kernel<true>, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid,
-                           inst_start, rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(base + pl.p8),
+                           rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(base + pl.p8),
                            reinterpret_cast<float*>(base + pl.p1));
     return (int)hipGetLastError();
 }

@@ -1,8 +1,9 @@
 // gsr_internal.h -- buffer layouts and launch helpers shared by the C-ABI (gsr_api.cpp)
 // and the kernels.  HBM layout (DESIGN.md "Data layout"):
 //
-//   geometry (per Gaussian, P):   depth_key u32 | tiles u32 | flags u32 | rec float4[3] | rect uint2
-//                                 | inst_start u32 | offsets u32 | sort ping-pong 4 x u32
+//   geometry (per Gaussian, P):   depth_key u32 | tiles u32 | flags u32 | rec float4[3]
+//                                 | rect uint4 (rect + inst_start) | cand_tmp u32 | offsets u32
+//                                 | sort ping-pong 4 x u32
 //                                 | radix histogram (256 x blocks) | scan partials
 //   binning  (per instance, K):   tile key/val ping-pong 4 x u32 (values = Gaussian id)
 //                                 | inst_gid u32 (emission order) | radix histogram
@@ -36,7 +37,7 @@ inline size_t sort_scratch_words(long long n) {
 }
 
 struct GeomLayout {
-    size_t depth_key, tiles, flags, rec, rect, inst_start, offsets, sA_k, sA_v, sB_k, sB_v, hist,
+    size_t depth_key, tiles, flags, rec, rect, cand_tmp, offsets, sA_k, sA_v, sB_k, sB_v, hist,
         partials, total;
     GeomLayout(int P) {
         size_t o = 0, n = (size_t)(P > 0 ? P : 1);
@@ -45,8 +46,8 @@ struct GeomLayout {
         tiles = take(4 * n);
         flags = take(4 * n);
         rec = take(16 * 3 * n);
-        rect = take(8 * n);
-        inst_start = take(4 * n);
+        rect = take(16 * n);  // uint4: minx|miny<<16, maxx|maxy<<16, inst_start, 0
+        cand_tmp = take(4 * n);  // band compaction: candidate gids before the depth sort
         offsets = take(4 * n);
         sA_k = take(4 * n);
         sA_v = take(4 * n);

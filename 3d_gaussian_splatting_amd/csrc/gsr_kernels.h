@@ -19,7 +19,7 @@ struct PreOut {
     uint32_t* tiles;
     uint32_t* flags;
     float4* rec;   // blend records: {x, y, a', b'}, {c', o, r, g}, {b, ext_x, ext_y, log2 o}
-    uint2* rect;   // tile rect: (minx | miny << 16, maxx | maxy << 16), full image
+    uint4* rect;   // (minx | miny << 16, maxx | maxy << 16, inst_start (set by F3), 0)
     uint32_t* counters;  // nullable, zeroed: [slot] += Gaussians with tiles in the band,
                          // [kCountSlots + slot] += K (slot = block % kCountSlots)
 };
@@ -48,8 +48,14 @@ int compact_candidates(const uint32_t* tiles, const uint32_t* depth_key, int n, 
 
 // F3: emit (tile key, owner gid) for every (Gaussian, tile in band) in depth-rank order
 int launch_duplicate(const uint32_t* gid_by_rank, const uint32_t* offsets, const uint32_t* tiles,
-                     const uint2* rect, int P, int grid_x, int ty0, int ty1, uint32_t* inst_start,
-                     uint32_t* tkey, uint32_t* inst_gid, hipStream_t s);
+                     uint4* rect, int P, int grid_x, int ty0, int ty1, uint32_t* tkey, uint32_t* inst_gid,
+                     hipStream_t s);
+
+// F2 + F3 fused (decoupled look-back scan): offsets (inclusive), inst_start, emitted
+// (tile key, gid) pairs.  scratch: 16 + ceil(n / 256) u32 (zeroed here).
+int launch_scan_duplicate(const uint32_t* gid_by_rank, const uint32_t* tiles, uint4* rect, int n,
+                          int grid_x, int ty0, uint32_t* offsets, uint32_t* tkey, uint32_t* inst_gid,
+                          uint32_t* scratch, hipStream_t s);
 
 // F5: ranges[tile] = [start, end) of the sorted tile keys
 int launch_finalize(const uint32_t* sorted_tile, long long K, uint2* ranges, hipStream_t s);
@@ -63,8 +69,8 @@ int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int 
 // emission index j = inst_start[g] + row-major index of the tile in g's band-clipped rect.
 // `partial` is the base of a PartLayout(K) block.
 int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
-                          const uint2* ranges, const uint32_t* sorted_gid, const uint32_t* inst_start,
-                          const uint2* rect, const float4* rec, const float* final_T,
+                          const uint2* ranges, const uint32_t* sorted_gid, const uint4* rect,
+                          const float4* rec, const float* final_T,
                           const float* accum, const float* dL_dpix, float* partial, long long K,
                           hipStream_t s);
 

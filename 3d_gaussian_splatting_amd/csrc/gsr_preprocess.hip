@@ -198,8 +198,8 @@ __device__ __forceinline__ uint32_t preprocess_one(const gsr_camera& cam, const 
                 rec[0] = make_float4(xs, ys, -0.5f * kL2E * cA, -kL2E * cB);
                 rec[1] = make_float4(-0.5f * kL2E * cC, opac, rgb[0], rgb[1]);
                 rec[2] = make_float4(rgb[2], ex, ey, log2f(opac));
-                out.rect[g] = make_uint2((uint32_t)minx | ((uint32_t)miny << 16),
-                                         (uint32_t)maxx | ((uint32_t)maxy << 16));
+                out.rect[g] = make_uint4((uint32_t)minx | ((uint32_t)miny << 16),
+                                         (uint32_t)maxx | ((uint32_t)maxy << 16), 0u, 0u);
                 out.flags[g] = clamped;
             }
         }

@@ -466,6 +466,131 @@ __global__ __launch_bounds__(kB) void scan_downsweep(const uint32_t* __restrict_
 
 // ---- F3 duplicate: wave-cooperative expansion (one wave = 64 consecutive ranks, whose
 // instances are contiguous; lanes write consecutive instances -> coalesced stores) ----
+__device__ __forceinline__ uint32_t udiv_small(uint32_t a, uint32_t b) {
+    // a / b for a < 2^20, 1 <= b < 2^12: the float quotient of (a + 0.5) is at least 0.5 / b
+    // away from an integer and rcp is accurate to ~1 ulp, so truncation is exact
+    return (uint32_t)(((float)a + 0.5f) * __builtin_amdgcn_rcpf((float)b));
+}
+
+// ---- fused F2 + F3: scan of tiles_touched in rank order + duplicate, one kernel ----
+// Block b (in launch order, atomic ticket) owns ranks [256 b, 256 b + 256): it scans their
+// tiles_touched, finds the instances of all earlier blocks by a wave-parallel decoupled
+// look-back (64 predecessors per probe; relaxed agent-scope atomics on packed flag|count
+// words), writes offsets / inst_start, and emits its own instances exactly as
+// duplicate_kernel does.  Replaces three scan kernels + a second pass over the ranks.
+
+__global__ __launch_bounds__(256) void scan_duplicate_kernel(const uint32_t* __restrict__ gid_by_rank,
+                                                             const uint32_t* __restrict__ tiles,
+                                                             uint4* __restrict__ rect, int n,
+                                                             int grid_x, int ty0,
+                                                             uint32_t* __restrict__ offsets,
+                                                             uint32_t* __restrict__ tkey,
+                                                             uint32_t* __restrict__ inst_gid,
+                                                             uint32_t* __restrict__ status,
+                                                             uint32_t* __restrict__ ticket) {
+    __shared__ uint32_t s_start[kWaves][64], s_g[kWaves][64], s_w[kWaves][64], s_x0[kWaves][64],
+        s_y0[kWaves][64];
+    __shared__ uint32_t wsum[kWaves];
+    __shared__ uint32_t s_excl;
+    __shared__ int s_b;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    if (tid == 0) s_b = (int)atomicAdd(ticket, 1u);
+    __syncthreads();
+    const int b = s_b;
+    const int r = b * 256 + tid;
+    const bool valid = r < n;
+    uint32_t g = 0, nt = 0, minx = 0, maxx = 0, y0 = 0;
+    if (valid) {
+        g = gid_by_rank[r];
+        nt = tiles[g];
+        if (nt) {
+            const uint4 rr = rect[g];
+            minx = rr.x & 0xFFFF;
+            maxx = rr.y & 0xFFFF;
+            const uint32_t miny = rr.x >> 16;
+            y0 = miny > (uint32_t)ty0 ? miny : (uint32_t)ty0;
+        }
+    }
+    // block scan
+    uint32_t x = nt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t pre = 0, total = 0;
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) {
+        pre += (k < w) ? wsum[k] : 0u;
+        total += wsum[k];
+    }
+    // look-back (wave 0)
+    if (w == 0) {
+        uint32_t excl = 0;
+        if (b == 0) {
+            if (lane == 0) __hip_atomic_store(status, kInc | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (lane == 0) __hip_atomic_store(status + b, kAgg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int pos = b - 1;
+            uint32_t spins = 0;
+            while (true) {
+                const int idx = pos - lane;
+                uint32_t v = kInc;  // before block 0: an inclusive zero
+                if (idx >= 0) v = __hip_atomic_load(status + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                while (__ballot((v & ~kCntMask) == 0u)) {  // some predecessor not published yet
+                    if (++spins > (1u << 24)) break;     // never expected; bounded so a bug cannot hang
+                    __builtin_amdgcn_s_sleep(1);
+                    if (idx >= 0 && (v & ~kCntMask) == 0u)
+                        v = __hip_atomic_load(status + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                const uint64_t inc = __ballot((v & kInc) != 0u);
+                const int k = inc ? __builtin_ctzll(inc) : 64;  // nearest inclusive predecessor
+                uint32_t c = lane <= k ? (v & kCntMask) : 0u;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+                excl += c;
+                if (inc || spins > (1u << 24)) break;
+                pos -= 64;
+            }
+            if (lane == 0)
+                __hip_atomic_store(status + b, kInc | (excl + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) s_excl = excl;
+    }
+    __syncthreads();
+    const uint32_t excl = s_excl;
+    const uint32_t lex = pre + x - nt;  // block-local exclusive offset
+    if (valid) {
+        offsets[r] = excl + lex + nt;
+        if (nt) rect[g].z = excl + lex;  // inst_start
+    }
+    // emission: this wave's instances [excl + pre_w, + wsum[w]) with pre_w = first lane's lex
+    const uint32_t wbase = pre;  // = lex of lane 0 of this wave
+    const uint32_t wtotal = wsum[w];
+    s_start[w][lane] = (valid && nt) ? lex - wbase : 0xFFFFFFFFu;
+    s_g[w][lane] = g;
+    s_w[w][lane] = maxx - minx;
+    s_x0[w][lane] = minx;
+    s_y0[w][lane] = y0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t first = excl + wbase;
+    for (uint32_t i = lane; i < wtotal; i += 64) {
+        int o = 0;  // owner = last lane whose start <= i (lanes without instances never own one)
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1)
+            if (s_start[w][o + step] <= i) o += step;
+        const uint32_t local = i - s_start[w][o];
+        const uint32_t wd = s_w[w][o];
+        const uint32_t dy = udiv_small(local, wd), dx = local - dy * wd;
+        tkey[first + i] = (s_y0[w][o] + dy) * (uint32_t)grid_x + s_x0[w][o] + dx;
+        inst_gid[first + i] = s_g[w][o];
+    }
+}
+
 // ---- band candidates: order-preserving compaction of the Gaussians with tiles in the band ----
 // A block owns kSortTile consecutive gids; wave w handles the contiguous 1024-gid run
 // [w*1024, (w+1)*1024) of it in 16 rounds of 64 lanes, so ballot prefix counts keep gid order.
@@ -526,9 +651,8 @@ __global__ __launch_bounds__(kB) void compact_scatter(const uint32_t* __restrict
 __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restrict__ gid_by_rank,
                                                         const uint32_t* __restrict__ offsets,
                                                         const uint32_t* __restrict__ tiles,
-                                                        const uint2* __restrict__ rect, int P,
+                                                        uint4* __restrict__ rect, int P,
                                                         int grid_x, int ty0, int ty1,
-                                                        uint32_t* __restrict__ inst_start,
                                                         uint32_t* __restrict__ tkey,
                                                         uint32_t* __restrict__ inst_gid) {
     __shared__ uint32_t s_start[kWaves][64], s_g[kWaves][64], s_w[kWaves][64], s_x0[kWaves][64],
@@ -541,11 +665,11 @@ __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restri
         g = gid_by_rank[r];
         nt = tiles[g];
         end = offsets[r];
-        inst_start[g] = end - nt;
     }
     uint32_t minx = 0, maxx = 0, y0 = 0;
     if (nt) {
-        const uint2 rr = rect[g];
+        rect[g].z = end - nt;  // inst_start
+        const uint4 rr = rect[g];
         minx = rr.x & 0xFFFF;
         maxx = rr.y & 0xFFFF;
         const uint32_t miny = rr.x >> 16;
@@ -572,7 +696,7 @@ __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restri
             if (s_start[w][o + step] <= i) o += step;
         const uint32_t local = i - s_start[w][o];
         const uint32_t wd = s_w[w][o];
-        const uint32_t dy = local / wd, dx = local - dy * wd;
+        const uint32_t dy = udiv_small(local, wd), dx = local - dy * wd;
         tkey[first + i] = (s_y0[w][o] + dy) * (uint32_t)grid_x + s_x0[w][o] + dx;
         inst_gid[first + i] = s_g[w][o];
     }
@@ -681,11 +805,24 @@ int compact_candidates(const uint32_t* tiles, const uint32_t* depth_key, int n, 
 }
 
 int launch_duplicate(const uint32_t* gid_by_rank, const uint32_t* offsets, const uint32_t* tiles,
-                     const uint2* rect, int P, int grid_x, int ty0, int ty1, uint32_t* inst_start,
-                     uint32_t* tkey, uint32_t* inst_gid, hipStream_t s) {
+                     uint4* rect, int P, int grid_x, int ty0, int ty1, uint32_t* tkey, uint32_t* inst_gid,
+                     hipStream_t s) {
     if (P <= 0) return 0;
     hipLaunchKernelGGL(duplicate_kernel, dim3(div_up(P, 256)), dim3(256), 0, s, gid_by_rank, offsets,
-                       tiles, rect, P, grid_x, ty0, ty1, inst_start, tkey, inst_gid);
+                       tiles, rect, P, grid_x, ty0, ty1, tkey, inst_gid);
+    return (int)hipGetLastError();
+}
+
+int launch_scan_duplicate(const uint32_t* gid_by_rank, const uint32_t* tiles, uint4* rect, int n,
+                          int grid_x, int ty0, uint32_t* offsets, uint32_t* tkey, uint32_t* inst_gid,
+                          uint32_t* scratch, hipStream_t s) {
+    if (n <= 0) return 0;
+    const int nb = div_up(n, 256);
+    uint32_t* ticket = scratch;
+    uint32_t* status = scratch + 16;
+    if (hipError_t e = hipMemsetAsync(scratch, 0, sizeof(uint32_t) * (16 + (size_t)nb), s)) return (int)e;
+    hipLaunchKernelGGL(scan_duplicate_kernel, dim3(nb), dim3(256), 0, s, gid_by_rank, tiles, rect, n, grid_x, ty0,
+                       offsets, tkey, inst_gid, status, ticket);
     return (int)hipGetLastError();
 }
 
