@@ -28,7 +28,8 @@ HIP_SOURCES = {
     "gsr_sort.hip": [],
     # F6 and B1 must evaluate alpha / T identically; no SLP packing (it splits DPP-fused adds)
     "gsr_blend.hip": ["-ffp-contract=off", "-fno-slp-vectorize"],
-    "gsr_preprocess_bwd.hip": [],
+    # recomputes the forward's SH clamp bits: must round exactly like gsr_preprocess.hip
+    "gsr_preprocess_bwd.hip": ["-ffp-contract=off"],
     "gsr_api.cpp": [],
 }
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fno-fast-math",

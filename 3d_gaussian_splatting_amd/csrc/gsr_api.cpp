@@ -208,7 +208,7 @@ void band(const gsr_camera* cam, const gsr_raster_settings* rs, int* y0, int* y1
 }
 
 struct Views {
-    uint32_t *depth_key, *tiles, *flags, *offsets, *gid_by_rank;
+    uint32_t *depth_key, *tiles, *offsets, *gid_by_rank;
     float4* rec;
     uint2* ranges;
     float* final_T;
@@ -223,7 +223,6 @@ Views views(const gsr_camera* cam, int P, const gsr_buffers* b) {
     ImgLayout il(cam->width, cam->height);
     v.depth_key = at<uint32_t>(b->geom, gl.depth_key);
     v.tiles = at<uint32_t>(b->geom, gl.tiles);
-    v.flags = at<uint32_t>(b->geom, gl.flags);
     v.rec = at<float4>(b->geom, gl.rec);
     v.offsets = at<uint32_t>(b->geom, gl.offsets);
     v.rect = at<uint4>(b->geom, gl.rect);
@@ -290,7 +289,6 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
     ImgLayout il(W, H);
     uint32_t* depth_key = at<uint32_t>(bufs->geom, gl.depth_key);
     uint32_t* tiles = at<uint32_t>(bufs->geom, gl.tiles);
-    uint32_t* flags = at<uint32_t>(bufs->geom, gl.flags);
     float4* rec = at<float4>(bufs->geom, gl.rec);
     uint32_t* offsets = at<uint32_t>(bufs->geom, gl.offsets);
     uint32_t* cand_tmp = at<uint32_t>(bufs->geom, gl.cand_tmp);
@@ -310,7 +308,7 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
 
     long long K = 0;
     if (P > 0) {
-        PreOut po{radii, depth_key, tiles, flags, rec, at<uint4>(bufs->geom, gl.rect), counters};
+        PreOut po{radii, depth_key, tiles, rec, at<uint4>(bufs->geom, gl.rect), counters};
         GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess(*cam, gauss_in(gs), ty0, ty1, po, stream), "preprocess");
         // A band ranks only its candidates (Gaussians with tiles in the band): the depth sort,
         // scan, duplicate and gather then scale with the band, not with P.
@@ -497,7 +495,7 @@ int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raste
     } else {
         GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(grad2d, 0, sizeof(float) * kPart * (size_t)P, stream), "zero grad2d");
     }
-    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), 0, P, v.depth_key, v.flags, grad2d,
+    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), 0, P, v.depth_key, grad2d,
                                              grad_out(grads), stream),
                   "preprocess backward");
     return 0;
@@ -524,7 +522,7 @@ int gsr_backward_preprocess_range(const gsr_camera* cam, const gsr_gaussians* gs
     const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
     GeomLayout gl(gs->P);
     GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), g0, g1, at<uint32_t>(bufs->geom, gl.depth_key),
-                                             at<uint32_t>(bufs->geom, gl.flags), grad2d,
+                                             grad2d,
                                              grad_out(grads), stream),
                   "preprocess backward");
     return 0;

@@ -1,7 +1,7 @@
 // gsr_internal.h -- buffer layouts and launch helpers shared by the C-ABI (gsr_api.cpp)
 // and the kernels.  HBM layout (DESIGN.md "Data layout"):
 //
-//   geometry (per Gaussian, P):   depth_key u32 | tiles u32 | flags u32 | rec float4[3]
+//   geometry (per Gaussian, P):   depth_key u32 | tiles u32 | rec float4[3]
 //                                 | rect uint4 (rect + inst_start) | cand_tmp u32 | offsets u32
 //                                 | sort ping-pong 4 x u32
 //                                 | radix histogram (256 x blocks) | scan partials
@@ -37,14 +37,13 @@ inline size_t sort_scratch_words(long long n) {
 }
 
 struct GeomLayout {
-    size_t depth_key, tiles, flags, rec, rect, cand_tmp, offsets, sA_k, sA_v, sB_k, sB_v, hist,
+    size_t depth_key, tiles, rec, rect, cand_tmp, offsets, sA_k, sA_v, sB_k, sB_v, hist,
         partials, total;
     GeomLayout(int P) {
         size_t o = 0, n = (size_t)(P > 0 ? P : 1);
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
         depth_key = take(4 * n);
         tiles = take(4 * n);
-        flags = take(4 * n);
         rec = take(16 * 3 * n);
         rect = take(16 * n);  // uint4: minx|miny<<16, maxx|maxy<<16, inst_start, 0
         cand_tmp = take(4 * n);  // band compaction: candidate gids before the depth sort

@@ -12,7 +12,8 @@
 // gaussian_model.cpp:270-298; camera matrices src/scene/camera.cpp:66-71.
 //
 // Roofline: HBM-bound.  Algorithmic bytes per Gaussian: 44 B params + 12*M B SH (visible
-// only) in; radius, depth key, tiles, flags (16 B) + 48 B record out.
+// only) in; radius, depth key, tiles (12 B) + 48 B record + 16 B rect out.
+// For a band (multi-GPU) only the band's candidates evaluate SH and write records.
 #include "gsr_kernels.h"
 
 namespace gsr {
@@ -130,9 +131,17 @@ __device__ __forceinline__ uint32_t preprocess_one(const gsr_camera& cam, const 
             const int miny = imin(grid_y, imax(0, (int)((ys - rf) / (float)kTile)));
             const int maxx = imin(grid_x, imax(0, (int)((xs + rf + (float)(kTile - 1)) / (float)kTile)));
             const int maxy = imin(grid_y, imax(0, (int)((ys + rf + (float)(kTile - 1)) / (float)kTile)));
+            const int by0 = imax(miny, ty0), by1 = imin(maxy, ty1);
+            const int band_rows = by1 > by0 ? by1 - by0 : 0;
             if ((maxx - minx) * (maxy - miny) != 0) {
+                radius_out = radius;
+                key_out = __float_as_uint(tz);
+                tiles_out = (uint32_t)((maxx - minx) * band_rows);
+            }
+            // colour and blend record only for Gaussians this band blends (all visible ones
+            // for a full image); B2 recomputes the clamp bits itself
+            if (tiles_out != 0) {
                 float rgb[3];
-                uint32_t clamped = 0;
                 if (in.colors) {
                     rgb[0] = in.colors[3 * g + 0];
                     rgb[1] = in.colors[3 * g + 1];
@@ -167,7 +176,9 @@ __device__ __forceinline__ uint32_t preprocess_one(const gsr_camera& cam, const 
                         }
                     }
                     const int nb = (D + 1) * (D + 1);
-                    const float* rest = sh_lds + threadIdx.x * M3;
+                    // LDS-staged row (full image) or this Gaussian's own row in HBM (band:
+                    // only ~1/N of the rows are needed, so the block does not stage)
+                    const float* rest = sh_lds ? sh_lds + threadIdx.x * M3 : in.sh_rest + (size_t)g * M3;
 #pragma unroll
                     for (int ch = 0; ch < 3; ++ch) {
                         float r = basis[0] * in.sh_dc[3 * g + ch];
@@ -175,15 +186,9 @@ __device__ __forceinline__ uint32_t preprocess_one(const gsr_camera& cam, const 
                         for (int k = 1; k < 16; ++k)
                             if (k < nb) r = r + basis[k] * rest[3 * (k - 1) + ch];
                         r = r + 0.5f;
-                        clamped |= (r < 0.0f ? 1u : 0u) << ch;
                         rgb[ch] = fmaxf(r, 0.0f);
                     }
                 }
-                const int by0 = imax(miny, ty0), by1 = imin(maxy, ty1);
-                const int band_rows = by1 > by0 ? by1 - by0 : 0;
-                radius_out = radius;
-                key_out = __float_as_uint(tz);
-                tiles_out = (uint32_t)((maxx - minx) * band_rows);
                 // Blend record (SURVEY B.3 power with -0.5 and log2(e) folded in, so the blend
                 // evaluates exp2 directly; log2(o) rides along so o * G is one exp2) + the
                 // half-extents of the alpha >= 1/255 footprint:
@@ -200,7 +205,6 @@ __device__ __forceinline__ uint32_t preprocess_one(const gsr_camera& cam, const 
                 rec[2] = make_float4(rgb[2], ex, ey, log2f(opac));
                 out.rect[g] = make_uint4((uint32_t)minx | ((uint32_t)miny << 16),
                                          (uint32_t)maxx | ((uint32_t)maxy << 16), 0u, 0u);
-                out.flags[g] = clamped;
             }
         }
     }
@@ -221,14 +225,17 @@ __global__ __launch_bounds__(256) void preprocess_kernel(const gsr_camera cam, c
     __shared__ uint32_t wk[4], wc[4];
     const int g = blockIdx.x * 256 + threadIdx.x;
     const int M3 = in.M_rest * 3;
-    if (in.sh_rest && !in.colors && in.D > 0) {  // block-uniform
+    const bool band = ty0 > 0 || ty1 < grid_y;
+    const bool stage = in.sh_rest && !in.colors && in.D > 0 && !band;  // grid-uniform
+    if (stage) {
         const size_t base = (size_t)blockIdx.x * 256 * M3;
         const int rows = in.P - blockIdx.x * 256 < 256 ? in.P - blockIdx.x * 256 : 256;
         const int cnt = rows * M3;
         for (int i = threadIdx.x; i < cnt; i += 256) sh_lds[i] = in.sh_rest[base + i];
         __syncthreads();
     }
-    const uint32_t t = g < in.P ? preprocess_one(cam, in, g, grid_x, grid_y, ty0, ty1, out, sh_lds) : 0u;
+    const uint32_t t = g < in.P ? preprocess_one(cam, in, g, grid_x, grid_y, ty0, ty1, out, stage ? sh_lds : nullptr)
+                                : 0u;
     if (out.counters) {
         uint32_t k = t, c = t ? 1u : 0u;
 #pragma unroll
@@ -256,7 +263,8 @@ int launch_preprocess(const gsr_camera& cam, const GaussIn& in, int ty0, int ty1
                       hipStream_t s) {
     if (in.P <= 0) return 0;
     const int gx = div_up(cam.width, kTile), gy = div_up(cam.height, kTile);
-    const size_t lds = (in.sh_rest && !in.colors && in.D > 0) ? sizeof(float) * 256 * 3 * in.M_rest : 0;
+    const bool band = ty0 > 0 || ty1 < gy;  // a band reads SH rows directly (see preprocess_kernel)
+    const size_t lds = (in.sh_rest && !in.colors && in.D > 0 && !band) ? sizeof(float) * 256 * 3 * in.M_rest : 0;
     hipLaunchKernelGGL(preprocess_kernel, dim3(div_up(in.P, 256)), dim3(256), lds, s, cam, in, gx, gy,
                        ty0, ty1, out);
     return (int)hipGetLastError();
