@@ -450,6 +450,203 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
 }
 
 
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// B1 with NW waves per tile: wave w owns stripes [w*PPL, (w+1)*PPL) (PPL = 4 / NW), so a
+// tile's records are swept by NW waves at once -- the multi-GPU bands have only 1/N of the
+// tiles, and at one wave per tile B1 would leave most SIMDs idle.  Each wave reduces its own
+// stripes' terms (quad DPP + parked LDS partials, wave-local syncs) into its own moment row;
+// the NW rows are summed in fixed wave order at batch end, so results stay deterministic.
+// Same arithmetic per (pixel, record) as blend_backward_kernel.
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void blend_backward_nw_kernel(const BlendGeom geo,
+                                                                    const uint2* __restrict__ ranges,
+                                                                    const uint32_t* __restrict__ sorted_gid,
+                                                                    const uint4* __restrict__ rect,
+                                                                    const float4* __restrict__ rec,
+                                                                    const float* __restrict__ final_T,
+                                                                    const float* __restrict__ accum,
+                                                                    const float* __restrict__ dL_dpix,
+                                                                    float4* __restrict__ part8,
+                                                                    float* __restrict__ part1) {
+    constexpr int PPL = kPPL / NW;
+    __shared__ float4 srec[64 * 3];
+    __shared__ uint32_t smk[64];
+    __shared__ float smom[NW][64 * 9];
+    __shared__ float qpark[NW][kPark * 16 * 12];
+    __shared__ int qrec[NW][kPark];
+    const int tile = xcd_tile(blockIdx.x, geo.nwg) + geo.ty0 * geo.grid_x;
+    const int tx = tile % geo.grid_x, ty = tile / geo.grid_x;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int px = tx * kTile + (lane & 15);
+    const float pfx = (float)px;
+    const float bx0 = (float)(tx * kTile), by0 = (float)(ty * kTile);
+    const size_t npix = (size_t)geo.W * geo.H;
+    const float hw = 0.5f * (float)geo.W, hh = 0.5f * (float)geo.H;
+    const int row = lane >> 4;
+    float pfy[PPL], T[PPL], Sp[PPL], cb[PPL], dp0[PPL], dp1[PPL], dp2[PPL];
+#pragma unroll
+    for (int p = 0; p < PPL; ++p) {
+        const int py = ty * kTile + row + 4 * (w * PPL + p);
+        pfy[p] = (float)py;
+        const bool in = px < geo.W && py < geo.H;
+        const size_t pix = in ? (size_t)py * geo.W + px : 0;
+        const float Tfin = in ? final_T[pix] : 1.0f;
+        dp0[p] = in ? dL_dpix[pix] : 0.0f;
+        dp1[p] = in ? dL_dpix[npix + pix] : 0.0f;
+        dp2[p] = in ? dL_dpix[2 * npix + pix] : 0.0f;
+        const float sdp = in ? accum[pix] * dp0[p] + accum[npix + pix] * dp1[p] + accum[2 * npix + pix] * dp2[p]
+                             : 0.0f;
+        cb[p] = sdp + Tfin * (geo.bg0 * dp0[p] + geo.bg1 * dp1[p] + geo.bg2 * dp2[p]);
+        T[p] = in ? 1.0f : -1.0f;
+        Sp[p] = 0.0f;
+    }
+    auto live_mask = [&]() {
+        uint32_t lv = 0;
+#pragma unroll
+        for (int p = 0; p < PPL; ++p) lv |= __any(T[p] > 0.0f) ? (1u << p) : 0u;
+        return lv;
+    };
+    float* qp = qpark[w];
+    int* qr = qrec[w];
+    float* sm = smom[w];
+    auto flush = [&](int parked) {
+        wave_lds_sync();
+        if (lane < parked * 9) {
+            const int slot = lane / 9, c = lane - 9 * slot;
+            const float* q = qp + slot * 16 * 12 + c;
+            float t4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < 16; ++i) t4[i & 3] += q[i * 12];
+            sm[qr[slot] * 9 + c] = (t4[0] + t4[1]) + (t4[2] + t4[3]);
+        }
+        wave_lds_sync();
+    };
+    const uint2 range = ranges[tile];
+    const int n = (int)(range.y - range.x);
+    for (int base = 0; base < n; base += 64) {
+        const int cnt = (n - base) < 64 ? (n - base) : 64;
+        uint32_t live = live_mask();
+        const int any_live = __syncthreads_or(live != 0);
+        uint32_t jl = 0;
+        float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0;
+        if (w == 0 && lane < cnt) {
+            const uint32_t g = sorted_gid[range.x + base + lane];
+            const uint4 rr = rect[g];
+            const int minx = rr.x & 0xFFFF, miny = rr.x >> 16, maxx = rr.y & 0xFFFF;
+            const int y0 = miny > geo.ty0 ? miny : geo.ty0;
+            jl = rr.z + (uint32_t)((ty - y0) * (maxx - minx) + (tx - minx));
+            uint32_t mk = 0;
+            if (any_live) {
+                const float4* r = rec + 3 * (size_t)g;
+                q0 = r[0];
+                q1 = r[1];
+                const float4 r2 = r[2];
+                srec[3 * lane + 0] = q0;
+                srec[3 * lane + 1] = q1;
+                srec[3 * lane + 2] = r2;
+                mk = stripe_mask(q0, q1, r2, bx0, by0, geo.ellipse_cull);
+            }
+            smk[lane] = mk;
+        } else if (w == 0) {
+            smk[lane] = 0u;
+        }
+#pragma unroll
+        for (int c = 0; c < 9; ++c) sm[lane * 9 + c] = 0.0f;
+        __syncthreads();
+        const uint32_t mine = (smk[lane] >> (w * PPL)) & ((1u << PPL) - 1u);
+        uint64_t todo = __ballot((mine & live) != 0u);
+        int visited = 0, parked = 0;
+        while (todo) {
+            const int k = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)mine, k) & live;
+            const float4 r0 = srec[3 * k + 0];
+            const float4 r1 = srec[3 * k + 1];
+            const float4 r2 = srec[3 * k + 2];
+            const float dx = r0.x - pfx;
+            const float bdx = r0.w * dx;
+            const float K = fmaf(r0.z * dx, dx, r2.w);
+            float s0 = 0.f, sy = 0.f, syy = 0.f, g0 = 0.f, g1 = 0.f, g2 = 0.f;
+            bool any = false;
+#pragma unroll
+            for (int p = 0; p < PPL; ++p) {
+                if (!(m & (1u << p))) continue;  // wave-uniform
+                const float dy = r0.y - pfy[p];
+                const float e = fmaf(bdx, dy, fmaf(r1.x * dy, dy, K));
+                float oG;
+                const float a = pair_alpha(e, r2.w, oG);
+                const float one_m = 1.0f - a;
+                const float tT = T[p] * one_m;
+                const bool ok = tT >= 0.0001f;
+                if (ok && a > 0.0f) {
+                    any = true;
+                    const float wt = a * T[p];
+                    const float cdp = fmaf(r1.z, dp0[p], fmaf(r1.w, dp1[p], r2.x * dp2[p]));
+                    Sp[p] = fmaf(wt, cdp, Sp[p]);
+                    const float dLda = fmaf(T[p], cdp, -(cb[p] - Sp[p]) * __builtin_amdgcn_rcpf(one_m));
+                    g0 = fmaf(wt, dp0[p], g0);
+                    g1 = fmaf(wt, dp1[p], g1);
+                    g2 = fmaf(wt, dp2[p], g2);
+                    const float sv = oG * dLda;
+                    s0 += sv;
+                    const float svy = sv * dy;
+                    sy += svy;
+                    syy = fmaf(svy, dy, syy);
+                }
+                T[p] = ok ? tT : -fabsf(T[p]);
+            }
+            if (__any(any)) {
+                const float sx = s0 * dx;
+                float v[9] = {sx, sy, sx * dx, sy * dx, syy, s0, g0, g1, g2};
+#pragma unroll
+                for (int i = 0; i < 9; ++i) v[i] += dpp_f<0xB1>(v[i]);  // quad_perm [1,0,3,2]
+#pragma unroll
+                for (int i = 0; i < 9; ++i) v[i] += dpp_f<0x4E>(v[i]);  // quad_perm [2,3,0,1]
+                if ((lane & 3) == 0) {
+                    float* dst = qp + (parked * 16 + (lane >> 2)) * 12;
+                    *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+                    *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
+                    dst[8] = v[8];
+                }
+                if (lane == 0) qr[parked] = k;
+                if (++parked == kPark) {
+                    flush(parked);
+                    parked = 0;
+                }
+            }
+            if ((++visited & 7) == 0) {
+                live = live_mask();
+                if (live == 0) break;
+            }
+        }
+        if (parked) flush(parked);
+        __syncthreads();
+        if (w == 0 && lane < cnt) {
+            float mo[9];
+#pragma unroll
+            for (int c = 0; c < 9; ++c) {
+                float acc = smom[0][lane * 9 + c];
+#pragma unroll
+                for (int v2 = 1; v2 < NW; ++v2) acc += smom[v2][lane * 9 + c];  // fixed wave order
+                mo[c] = acc;
+            }
+            const float Sx = mo[0], Sy = mo[1], Sxx = mo[2], Sxy = mo[3], Syy = mo[4], S0 = mo[5];
+            const float A = -2.0f * kLn2 * q0.z, B = -kLn2 * q0.w, C = -2.0f * kLn2 * q1.x;
+            const float dop = S0 != 0.0f ? S0 / q1.y : 0.0f;
+            part8[2 * (size_t)jl + 0] = make_float4((-A * Sx - B * Sy) * hw, (-C * Sy - B * Sx) * hh, -0.5f * Sxx, -Sxy);
+            part8[2 * (size_t)jl + 1] = make_float4(-0.5f * Syy, dop, mo[6], mo[7]);
+            part1[jl] = mo[8];
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 // Kernel-variant selector for A/B timing (bench/ablation only; default = shipped variant).
@@ -477,7 +674,9 @@ int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int 
                          float* out_color, float* final_T, float* accum, hipStream_t s) {
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1);
     if (geo.nwg <= 0) return 0;
-    const int v = variant("GSR_FWD_VARIANT", 2);  // waves per tile
+    // waves per tile: 2 for a full image, 4 when the launch has too few tiles to fill the
+    // chip (multi-GPU bands)
+    const int v = variant("GSR_FWD_VARIANT", geo.nwg >= 4096 ? 2 : 4);
     if (v == 1)
         hipLaunchKernelGGL(blend_forward_kernel<1>, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid, rec,
                            out_color, final_T, accum);
@@ -499,15 +698,25 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
     if (geo.nwg <= 0) return 0;
     const PartLayout pl(K);
     char* base = reinterpret_cast<char*>(partial);
-    // 1: deferred quad/LDS reduction (shipped); 0: full per-record DPP/permlane reduction
-    if (variant("GSR_BWD_VARIANT", 1) == 0)
+    // 0: one wave per tile, full per-record DPP/permlane reduction; 1: one wave per tile,
+    // deferred quad/LDS reduction; 2 / 4: that many waves per tile.  Default: 1 for a full
+    // image, 4 waves when the launch has too few tiles to fill the chip (multi-GPU bands).
+    const int dflt = geo.nwg >= 4096 ? 1 : 4;
+    const int v = variant("GSR_BWD_VARIANT", dflt);
+    char* p8 = base + pl.p8;
+    float* p1 = reinterpret_cast<float*>(base + pl.p1);
+    if (v == 0)
         hipLaunchKernelGGL(blend_backward_kernel<false>, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid,
-                           rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(base + pl.p8),
-                           reinterpret_cast<float*>(base + pl.p1));
+                           rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(p8), p1);
+    else if (v == 2)
+        hipLaunchKernelGGL(blend_backward_nw_kernel<2>, dim3(geo.nwg), dim3(128), 0, s, geo, ranges, sorted_gid,
+                           rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(p8), p1);
+    else if (v == 4)
+        hipLaunchKernelGGL(blend_backward_nw_kernel<4>, dim3(geo.nwg), dim3(256), 0, s, geo, ranges, sorted_gid,
+                           rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(p8), p1);
     else
         hipLaunchKernelGGL(blend_backward_kernel<true>, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid,
-                           rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(base + pl.p8),
-                           reinterpret_cast<float*>(base + pl.p1));
+                           rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(p8), p1);
     return (int)hipGetLastError();
 }
 
