@@ -215,12 +215,13 @@ struct Views {
     float* accum;
     uint32_t *sorted_tile, *sorted_gid, *inst_gid;
     uint4* rect;
+    float4* ck;  // B1 chunk checkpoints (nullptr: not chunked)
 };
 
-Views views(const gsr_camera* cam, int P, const gsr_buffers* b) {
+Views views(const gsr_camera* cam, int P, const gsr_buffers* b, int ck_tiles = 0) {
     Views v{};
     GeomLayout gl(P);
-    ImgLayout il(cam->width, cam->height);
+    ImgLayout il(cam->width, cam->height, ck_tiles);
     v.depth_key = at<uint32_t>(b->geom, gl.depth_key);
     v.tiles = at<uint32_t>(b->geom, gl.tiles);
     v.rec = at<float4>(b->geom, gl.rec);
@@ -231,6 +232,7 @@ Views views(const gsr_camera* cam, int P, const gsr_buffers* b) {
     v.ranges = at<uint2>(b->image, il.ranges);
     v.final_T = at<float>(b->image, il.final_T);
     v.accum = at<float>(b->image, il.accum);
+    v.ck = ck_tiles ? at<float4>(b->image, il.ck) : nullptr;
     if (b->binning) {
         BinLayout bl(b->num_rendered);
         const int tiles = div_up(cam->width, kTile) * div_up(cam->height, kTile);
@@ -283,10 +285,11 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
     band(cam, rs, &ty0, &ty1);
     std::memset(bufs, 0, sizeof *bufs);
     bufs->geom = alloc_geom(ctx, GeomLayout(P).total);
-    bufs->image = alloc_image(ctx, ImgLayout(W, H).total);
+    const int ckt = chunked_tiles(W, ty0, ty1);
+    bufs->image = alloc_image(ctx, ImgLayout(W, H, ckt).total);
     if (!bufs->geom || !bufs->image) return fail(-2, "allocation failed (geometry/image)");
     GeomLayout gl(P);
-    ImgLayout il(W, H);
+    ImgLayout il(W, H, ckt);
     uint32_t* depth_key = at<uint32_t>(bufs->geom, gl.depth_key);
     uint32_t* tiles = at<uint32_t>(bufs->geom, gl.tiles);
     float4* rec = at<float4>(bufs->geom, gl.rec);
@@ -391,9 +394,9 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
     } else {
         bufs->binning = alloc_binning(ctx, BinLayout(0).total);
     }
-    const Views v = views(cam, P, bufs);
+    const Views v = views(cam, P, bufs, ckt);
     GSR_STAGE(GSR_STAGE_BLEND_FWD, launch_blend_forward(*cam, rs->bg, ty0, ty1, ranges, v.sorted_gid, rec, out_color, final_T,
-                                       v.accum, stream),
+                                       v.accum, v.ck, stream),
                   "blend forward");
     return 0;
 }
@@ -420,7 +423,7 @@ static int backward_impl(const gsr_camera* cam, const gsr_gaussians* gs, const g
     if (P == 0) return 0;
     int ty0, ty1;
     band(cam, rs, &ty0, &ty1);
-    const Views v = views(cam, P, bufs);
+    const Views v = views(cam, P, bufs, chunked_tiles(cam->width, ty0, ty1));
     const long long K = bufs->num_rendered;
     float* partial = nullptr;
     if (K > 0) {
@@ -428,7 +431,7 @@ static int backward_impl(const gsr_camera* cam, const gsr_gaussians* gs, const g
         partial = static_cast<float*>(alloc_scratch(ctx, gsr_scratch_bytes((int32_t)K)));
         if (!partial) return fail(-2, "allocation failed (scratch, K=%lld)", K);
         GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.rect, v.rec,
-                                            v.final_T, v.accum, dL_dpix, partial, K, stream),
+                                            v.final_T, v.accum, dL_dpix, partial, K, v.ck, stream),
                       "blend backward");
     }
     if (grad2d) {
@@ -480,7 +483,7 @@ int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raste
     int ty0, ty1;
     band(cam, rs, &ty0, &ty1);
     const int P = gs->P;
-    const Views v = views(cam, P, bufs);
+    const Views v = views(cam, P, bufs, chunked_tiles(cam->width, ty0, ty1));
     const long long K = bufs->num_rendered;
     // two scratch blocks: per-instance partials (K x 48 B) and per-Gaussian grad2d (P x 48 B)
     float* partial = static_cast<float*>(alloc_scratch(ctx, gsr_scratch_bytes((int32_t)K)));
@@ -488,7 +491,7 @@ int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raste
     if (!partial || !grad2d) return fail(-2, "allocation failed (scratch, K=%lld, P=%d)", K, P);
     if (K > 0) {
         GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.rect, v.rec,
-                                            v.final_T, v.accum, dL_dpix, partial, K, stream),
+                                            v.final_T, v.accum, dL_dpix, partial, K, v.ck, stream),
                       "blend backward");
         GSR_STAGE(GSR_STAGE_GATHER, gather_all(v, bufs, partial, K, P, grad2d, stream),
                   "gather grad2d");

@@ -149,6 +149,14 @@ __device__ __forceinline__ float pair_alpha(float e, float L, float& oG) {
 // F6.  T > 0: pixel live; T <= 0: done, |T| = final transmittance (the T after the last
 // contributor -- the reference's final_T).  A pair is blended when T (1 - alpha) >= 1e-4,
 // otherwise the pixel terminates with T unchanged (SURVEY B.3 / forward.cu renderCUDA).
+// Chunk length of a tile's list when B1 is chunked: at most kMaxChunks chunks of whole
+// 64-record sub-batches (F6 checkpoints at 64-record boundaries).  Most of a tile's B1 work
+// is in its front records (pixels terminate), so chunks stay short to split that front.
+__device__ __forceinline__ int chunk_len(int n) {
+    const int c = (n + kMaxChunks - 1) / kMaxChunks;
+    return ((c + 63) / 64) * 64;
+}
+
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom geo,
                                                                 const uint2* __restrict__ ranges,
@@ -156,12 +164,14 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
                                                                 const float4* __restrict__ rec,
                                                                 float* __restrict__ out_color,
                                                                 float* __restrict__ final_T,
-                                                                float* __restrict__ accum) {
+                                                                float* __restrict__ accum,
+                                                                float4* __restrict__ ck) {
     constexpr int PPL = kPPL / NW;
     constexpr int BATCH = 64 * NW;
     __shared__ float4 srec[BATCH * 3];
     __shared__ uint32_t smk[BATCH];
-    const int tile = xcd_tile(blockIdx.x, geo.nwg) + geo.ty0 * geo.grid_x;
+    const int tl = xcd_tile(blockIdx.x, geo.nwg);  // band-local tile index
+    const int tile = tl + geo.ty0 * geo.grid_x;
     const int tx = tile % geo.grid_x, ty = tile / geo.grid_x;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int px = tx * kTile + (lane & 15);
@@ -177,6 +187,14 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
     }
     const uint2 range = ranges[tile];
     const int n = (int)(range.y - range.x);
+    // B1 chunk checkpoints: (T, colour sum) of every pixel before records CH, 2 CH, ...
+    const int CH = chunk_len(n);
+    int nck = 0;  // checkpoints written
+    auto checkpoint = [&](int c) {
+        float4* dst = ck + ((size_t)tl * (kMaxChunks - 1) + c) * 256;
+#pragma unroll
+        for (int p = 0; p < PPL; ++p) dst[64 * (w * PPL + p) + lane] = make_float4(T[p], C0[p], C1[p], C2[p]);
+    };
     for (int base = 0; base < n; base += BATCH) {
         uint32_t live = 0;
 #pragma unroll
@@ -197,6 +215,7 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
         const int cnt = (n - base) < BATCH ? (n - base) : BATCH;
         int visited = 0;
         for (int c0 = 0; c0 < cnt && live; c0 += 64) {
+            if (ck && base + c0 > 0 && (base + c0) % CH == 0) checkpoint(nck++);  // state before record base + c0
             const uint32_t mine = (smk[c0 + lane] >> (w * PPL)) & ((1u << PPL) - 1u);
             uint64_t todo = __ballot((mine & live) != 0u && c0 + lane < cnt);
             while (todo) {
@@ -236,6 +255,8 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
         }
         __syncthreads();
     }
+    if (ck)  // the list ended or every pixel finished: later chunks start from the final state
+        for (; nck * CH + CH < n && nck < kMaxChunks - 1; ++nck) checkpoint(nck);
     const size_t npix = (size_t)geo.W * geo.H;
 #pragma unroll
     for (int p = 0; p < PPL; ++p) {
@@ -291,12 +312,29 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
                                                             const float* __restrict__ accum,
                                                             const float* __restrict__ dL_dpix,
                                                             float4* __restrict__ part8,
-                                                            float* __restrict__ part1) {
+                                                            float* __restrict__ part1,
+                                                            const float4* __restrict__ ck) {
     __shared__ float4 srec[64 * 3];
     __shared__ float smom[64 * 12];
     __shared__ float qpark[DEFER ? kPark * 16 * 12 : 1];  // [slot][quad][9 of 12]
     __shared__ int qrec[DEFER ? kPark : 1];
-    const int tile = xcd_tile(blockIdx.x, geo.nwg) + geo.ty0 * geo.grid_x;
+    // chunked (ck != nullptr): block -> (tile, chunk).  Each XCD (blocks b with equal b % 8)
+    // takes a contiguous tile range as in xcd_tile, visited chunk-major, so every tile's
+    // front chunk -- the longest -- is dispatched first.  Grid: 8 x ceil(nwg / 8) x chunks.
+    int tl, chunk;
+    if (ck) {
+        const int q = geo.nwg / 8, r = geo.nwg % 8, xcd = blockIdx.x % 8, local = blockIdx.x / 8;
+        const int t0 = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q, nt = q + (xcd < r ? 1 : 0);
+        const int per = q + 1;  // padded tiles per XCD
+        chunk = local / per;
+        const int i = local - chunk * per;
+        if (i >= nt) return;
+        tl = t0 + i;
+    } else {
+        tl = xcd_tile(blockIdx.x, geo.nwg);
+        chunk = 0;
+    }
+    const int tile = tl + geo.ty0 * geo.grid_x;
     const int tx = tile % geo.grid_x, ty = tile / geo.grid_x;
     const int lane = threadIdx.x;
     const int px = tx * kTile + (lane & 15);
@@ -323,8 +361,24 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
         Sp[p] = 0.0f;
     }
     const uint2 range = ranges[tile];
-    const int n = (int)(range.y - range.x);
-    for (int base = 0; base < n; base += 64) {
+    const int n_all = (int)(range.y - range.x);
+    int start = 0, n = n_all;
+    if (ck) {
+        const int CH = chunk_len(n_all);
+        start = chunk * CH;
+        if (start >= n_all) return;  // no such chunk for this tile
+        n = start + CH < n_all ? start + CH : n_all;
+        if (chunk > 0) {  // resume from F6's checkpoint: T and Sp = dL/dpix . (colour sum so far)
+            const float4* src = ck + ((size_t)tl * (kMaxChunks - 1) + (chunk - 1)) * 256;
+#pragma unroll
+            for (int p = 0; p < kPPL; ++p) {
+                const float4 c4 = src[64 * p + lane];
+                T[p] = c4.x;
+                Sp[p] = fmaf(c4.y, dp0[p], fmaf(c4.z, dp1[p], c4.w * dp2[p]));
+            }
+        }
+    }
+    for (int base = start; base < n; base += 64) {
         const int cnt = (n - base) < 64 ? (n - base) : 64;
         const int e_l = base + lane;
         uint32_t live = 0;
@@ -671,7 +725,7 @@ static BlendGeom make_geo(const gsr_camera& cam, const float bg[3], int ty0, int
 
 int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
                          const uint2* ranges, const uint32_t* sorted_gid, const float4* rec,
-                         float* out_color, float* final_T, float* accum, hipStream_t s) {
+                         float* out_color, float* final_T, float* accum, float4* ck, hipStream_t s) {
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1);
     if (geo.nwg <= 0) return 0;
     // waves per tile: 2 for a full image, 4 when the launch has too few tiles to fill the
@@ -679,13 +733,13 @@ int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int 
     const int v = variant("GSR_FWD_VARIANT", geo.nwg >= 4096 ? 2 : 4);
     if (v == 1)
         hipLaunchKernelGGL(blend_forward_kernel<1>, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid, rec,
-                           out_color, final_T, accum);
+                           out_color, final_T, accum, ck);
     else if (v == 4)
         hipLaunchKernelGGL(blend_forward_kernel<4>, dim3(geo.nwg), dim3(256), 0, s, geo, ranges, sorted_gid, rec,
-                           out_color, final_T, accum);
+                           out_color, final_T, accum, ck);
     else
         hipLaunchKernelGGL(blend_forward_kernel<2>, dim3(geo.nwg), dim3(128), 0, s, geo, ranges, sorted_gid, rec,
-                           out_color, final_T, accum);
+                           out_color, final_T, accum, ck);
     return (int)hipGetLastError();
 }
 
@@ -693,7 +747,7 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
                           const uint2* ranges, const uint32_t* sorted_gid, const uint4* rect,
                           const float4* rec, const float* final_T,
                           const float* accum, const float* dL_dpix, float* partial, long long K,
-                          hipStream_t s) {
+                          const float4* ck, hipStream_t s) {
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1);
     if (geo.nwg <= 0) return 0;
     const PartLayout pl(K);
@@ -701,13 +755,16 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
     // 0: one wave per tile, full per-record DPP/permlane reduction; 1: one wave per tile,
     // deferred quad/LDS reduction; 2 / 4: that many waves per tile.  Default: 1 for a full
     // image, 4 waves when the launch has too few tiles to fill the chip (multi-GPU bands).
-    const int dflt = geo.nwg >= 4096 ? 1 : 4;
-    const int v = variant("GSR_BWD_VARIANT", dflt);
+    // 1 (shipped): one wave per tile (per tile chunk when F6 wrote checkpoints), deferred
+    // quad/LDS reduction; 0: full per-record DPP/permlane reduction; 2 / 4: that many waves
+    // per tile (no chunks).
+    const int v = variant("GSR_BWD_VARIANT", 1);
     char* p8 = base + pl.p8;
     float* p1 = reinterpret_cast<float*>(base + pl.p1);
+    const int blocks = ck ? 8 * (geo.nwg / 8 + 1) * kMaxChunks : geo.nwg;
     if (v == 0)
-        hipLaunchKernelGGL(blend_backward_kernel<false>, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid,
-                           rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(p8), p1);
+        hipLaunchKernelGGL(blend_backward_kernel<false>, dim3(blocks), dim3(64), 0, s, geo, ranges, sorted_gid,
+                           rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(p8), p1, ck);
     else if (v == 2)
         hipLaunchKernelGGL(blend_backward_nw_kernel<2>, dim3(geo.nwg), dim3(128), 0, s, geo, ranges, sorted_gid,
                            rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(p8), p1);
@@ -715,8 +772,8 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
         hipLaunchKernelGGL(blend_backward_nw_kernel<4>, dim3(geo.nwg), dim3(256), 0, s, geo, ranges, sorted_gid,
                            rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(p8), p1);
     else
-        hipLaunchKernelGGL(blend_backward_kernel<true>, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid,
-                           rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(p8), p1);
+        hipLaunchKernelGGL(blend_backward_kernel<true>, dim3(blocks), dim3(64), 0, s, geo, ranges, sorted_gid,
+                           rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(p8), p1, ck);
     return (int)hipGetLastError();
 }
 

@@ -12,6 +12,7 @@
 #pragma once
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/gsr/gsr.h"
 
@@ -73,9 +74,22 @@ struct BinLayout {
     }
 };
 
+// Chunked B1 for launches with few tiles (multi-GPU bands): F6 checkpoints every pixel's
+// (T, colour sum) at kMaxChunks - 1 points of each tile's list, so B1 can sweep the chunks of
+// one tile in parallel blocks.  Full images have enough tiles and skip it.
+constexpr int kMaxChunks = 8;
+constexpr int kChunkTiles = 4096;  // launches with fewer tiles than this are chunked
+inline int chunked_tiles(int W, int ty0, int ty1) {
+    const char* e = std::getenv("GSR_CHUNK");  // A/B switch: 0 never, 2 always (bench/ablation only)
+    const int mode = e ? std::atoi(e) : 1;
+    const int nwg = (ty1 - ty0) * div_up(W, kTile);
+    if (mode == 0 || nwg <= 0) return 0;
+    return mode == 2 || nwg < kChunkTiles ? nwg : 0;
+}
+
 struct ImgLayout {
-    size_t ranges, counters, final_T, accum, total;
-    ImgLayout(int W, int H) {
+    size_t ranges, counters, final_T, accum, ck, total;
+    ImgLayout(int W, int H, int ck_tiles = 0) {
         size_t o = 0;
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
         size_t tiles = (size_t)div_up(W, kTile) * div_up(H, kTile);
@@ -84,6 +98,7 @@ struct ImgLayout {
         counters = take(4 * (2 * kCountSlots + 16));  // right after ranges: one memset clears both
         final_T = take(4 * (pix ? pix : 1));
         accum = take(12 * (pix ? pix : 1));  // colour sum without background, 3 x H x W
+        ck = take((size_t)ck_tiles * (kMaxChunks - 1) * 256 * 16);  // float4 (T, C) checkpoints
         total = o;
     }
 };

@@ -59,10 +59,11 @@ int launch_scan_duplicate(const uint32_t* gid_by_rank, const uint32_t* tiles, ui
 // F5: ranges[tile] = [start, end) of the sorted tile keys
 int launch_finalize(const uint32_t* sorted_tile, long long K, uint2* ranges, hipStream_t s);
 
-// F6: per-tile front-to-back blend -> colour, final T, colour sum without background
+// F6: per-tile front-to-back blend -> colour, final T, colour sum without background; with
+// ck != nullptr also the B1 chunk checkpoints (ImgLayout.ck, chunked_tiles)
 int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
                          const uint2* ranges, const uint32_t* sorted_gid, const float4* rec,
-                         float* out_color, float* final_T, float* accum, hipStream_t s);
+                         float* out_color, float* final_T, float* accum, float4* ck, hipStream_t s);
 
 // B1: per-tile front-to-back gradients -> per-instance partial entry j (PartLayout), where the
 // emission index j = inst_start[g] + row-major index of the tile in g's band-clipped rect.
@@ -71,7 +72,7 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
                           const uint2* ranges, const uint32_t* sorted_gid, const uint4* rect,
                           const float4* rec, const float* final_T,
                           const float* accum, const float* dL_dpix, float* partial, long long K,
-                          hipStream_t s);
+                          const float4* ck, hipStream_t s);
 
 // record layout constants shared by preprocess and the blend kernels
 constexpr float kLn2 = 0.6931471805599453f;  // conic A = -2 ln2 a', B = -ln2 b', C = -2 ln2 c' 
