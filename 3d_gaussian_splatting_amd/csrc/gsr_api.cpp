@@ -266,7 +266,9 @@ const char* gsr_last_error(void) { return g_err.c_str(); }
 
 size_t gsr_geom_bytes(int32_t P) { return GeomLayout(P).total; }
 size_t gsr_binning_bytes(int32_t K) { return BinLayout(K).total; }
-size_t gsr_image_bytes(int32_t w, int32_t h) { return ImgLayout(w, h).total; }
+size_t gsr_image_bytes(int32_t w, int32_t h) {
+    return ImgLayout(w, h, chunked_tiles(w, 0, div_up(h, kTile))).total;
+}
 size_t gsr_scratch_bytes(int32_t K) { return PartLayout(K).total; }
 
 int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,

@@ -74,11 +74,12 @@ struct BinLayout {
     }
 };
 
-// Chunked B1 for launches with few tiles (multi-GPU bands): F6 checkpoints every pixel's
-// (T, colour sum) at kMaxChunks - 1 points of each tile's list, so B1 can sweep the chunks of
-// one tile in parallel blocks.  Full images have enough tiles and skip it.
+// Chunked B1: F6 checkpoints every pixel's (T, colour sum) at kMaxChunks - 1 points of each
+// tile's list, so B1 sweeps the chunks of one tile in parallel blocks.  Essential for the
+// multi-GPU bands (1/N of the tiles: B1 0.27 -> 0.13 ms at N = 8) and still -7 % B1 on a full
+// 1080p image (shorter tail), for 16 B per pixel per checkpoint of extra F6 writes.
 constexpr int kMaxChunks = 8;
-constexpr int kChunkTiles = 4096;  // launches with fewer tiles than this are chunked
+constexpr int kChunkTiles = 1 << 30;  // launches with fewer tiles than this are chunked
 inline int chunked_tiles(int W, int ty0, int ty1) {
     const char* e = std::getenv("GSR_CHUNK");  // A/B switch: 0 never, 2 always (bench/ablation only)
     const int mode = e ? std::atoi(e) : 1;
