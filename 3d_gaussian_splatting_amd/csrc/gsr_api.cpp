@@ -24,12 +24,13 @@ namespace {
 
 thread_local std::string g_err;
 
-// A/B selector (bench/ablation only): 0 = three-kernel scan then duplicate (shipped),
-// 1 = fused look-back scan + duplicate (one kernel, but the look-back chain over P/256
-// blocks measured slower: 0.102 vs 0.084 ms at 1M).
-int scan_variant() {
+// A/B selector (bench/ablation only): 0 = three-kernel scan then duplicate, 1 = fused
+// look-back scan + duplicate.  Shipped: fused for up to 2^19 ranked Gaussians (a band's
+// candidates: 0.030 vs 0.037 ms at 133k), three kernels above (0.084 vs 0.102 ms at 1M: the
+// look-back chain over n / 256 blocks dominates).
+int scan_variant(int n) {
     const char* e = std::getenv("GSR_SCAN_VARIANT");
-    return e ? std::atoi(e) : 0;
+    return e ? std::atoi(e) : (n <= (1 << 19) ? 1 : 0);
 }
 
 // Low-latency device->host read of one u32: DMA into a per-thread pinned word, then spin on
@@ -356,7 +357,7 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
             sum_counts();
         }
         const uint32_t* gid_by_rank = at<uint32_t>(bufs->geom, gl.sA_v);
-        const bool fused = scan_variant() == 1;
+        const bool fused = scan_variant(NR) == 1;
         if (NR > 0 && !fused) {
             GSR_STAGE(GSR_STAGE_SCAN, inclusive_scan_gather(tiles, gid_by_rank, offsets, NR,
                                                 at<uint32_t>(bufs->geom, gl.partials), stream),

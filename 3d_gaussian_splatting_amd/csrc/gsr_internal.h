@@ -30,10 +30,13 @@ inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 inline int div_up(long long a, long long b) { return (int)((a + b - 1) / b); }
 inline int sort_blocks(long long n) { return n > 0 ? div_up(n, kSortTile) : 0; }
 // radix-sort scratch (u32 words): reduce-then-scan needs 256 x (blocks + 1) + 256; onesweep
-// needs 4 x 256 digit totals + 16 tickets + 4 passes x blocks x 256 look-back words.
+// needs 4 x 256 digit totals + 16 tickets + 4 passes x tiles x 256 look-back words, with
+// tiles of 1024 keys (the small-n form) in the worst case.
+constexpr long long kOnesweepSmall = 1 << 19;  // key counts up to this use 1024-key tiles
 inline size_t sort_scratch_words(long long n) {
     const size_t nb = (size_t)sort_blocks(n) + 1;
-    const size_t a = 256 * nb + 256, b = 4 * 256 + 16 + 4 * nb * 256;
+    const size_t nbs = (size_t)(n > 0 ? (n + 1023) / 1024 : 0) + 1;
+    const size_t a = 256 * nb + 256, b = 4 * 256 + 16 + 4 * (nbs > nb ? nbs : nb) * 256;
     return a > b ? a : b;
 }
 

@@ -249,6 +249,7 @@ __global__ __launch_bounds__(kB) void radix_hist_all(const uint32_t* __restrict_
         if (h[p][tid]) atomicAdd(&ghist[p * 256 + tid], h[p][tid]);
 }
 
+template <int KI>
 __global__ __launch_bounds__(kB) void radix_onesweep(const uint32_t* __restrict__ keys_in,
                                                      const uint32_t* __restrict__ vals_in,
                                                      uint32_t* __restrict__ keys_out,
@@ -261,8 +262,9 @@ __global__ __launch_bounds__(kB) void radix_onesweep(const uint32_t* __restrict_
     __shared__ uint32_t gbase[256];
     __shared__ uint32_t lbase[256];
     __shared__ uint32_t wsum[kWaves];
-    __shared__ uint32_t skey[kSortTile];
-    __shared__ uint32_t sval[kSortTile];
+    constexpr int TILE = kB * KI, WITEMS = KI * 64;
+    __shared__ uint32_t skey[TILE];
+    __shared__ uint32_t sval[TILE];
     __shared__ int s_tile;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const uint32_t mask = (1u << nbits) - 1u;
@@ -271,19 +273,19 @@ __global__ __launch_bounds__(kB) void radix_onesweep(const uint32_t* __restrict_
     for (int k = 0; k < kWaves; ++k) wcnt[k][tid] = 0;
     __syncthreads();
     const int tile = s_tile;
-    const long long bbase = (long long)tile * kSortTile;
-    const long long base = bbase + (long long)w * kWaveItems;
-    uint32_t key[kI], val[kI], rank[kI];
+    const long long bbase = (long long)tile * TILE;
+    const long long base = bbase + (long long)w * WITEMS;
+    uint32_t key[KI], val[KI], rank[KI];
     const uint64_t lt = lanemask_lt();
 #pragma unroll
-    for (int r = 0; r < kI; ++r) {
+    for (int r = 0; r < KI; ++r) {
         const long long idx = base + r * 64 + lane;
         const bool valid = idx < n;
         key[r] = valid ? keys_in[idx] : 0xFFFFFFFFu;
         val[r] = valid ? (vals_in ? vals_in[idx] : (uint32_t)idx) : 0u;
     }
 #pragma unroll
-    for (int r = 0; r < kI; ++r) {
+    for (int r = 0; r < KI; ++r) {
         const long long idx = base + r * 64 + lane;
         const bool valid = idx < n;
         const uint32_t d = (key[r] >> shift) & mask;
@@ -356,7 +358,7 @@ __global__ __launch_bounds__(kB) void radix_onesweep(const uint32_t* __restrict_
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kI; ++r) {
+    for (int r = 0; r < KI; ++r) {
         const long long idx = base + r * 64 + lane;
         if (idx < n) {
             const uint32_t d = (key[r] >> shift) & mask;
@@ -366,7 +368,7 @@ __global__ __launch_bounds__(kB) void radix_onesweep(const uint32_t* __restrict_
         }
     }
     __syncthreads();
-    const int count = (n - bbase) < kSortTile ? (int)(n - bbase) : kSortTile;
+    const int count = (n - bbase) < TILE ? (int)(n - bbase) : TILE;
 #pragma unroll 4
     for (int i = tid; i < count; i += kB) {
         const uint32_t k = skey[i];
@@ -726,17 +728,27 @@ static bool use_onesweep(bool depth_sort) {
 }
 
 // onesweep: ghist (4 x 256) | tickets (16) | status (passes x nb x 256); one memset per sort
+// Items per thread of the onesweep tiles: 16 (4096-key tiles) or 4 (1024-key tiles, 4x the
+// blocks -- for the small candidate sets of multi-GPU bands, where a pass is latency-bound).
+static int onesweep_items(long long n) {
+    const char* e = std::getenv("GSR_ONESWEEP_ITEMS");
+    if (e) return std::atoi(e) == 4 ? 4 : 16;
+    return n <= kOnesweepSmall ? 4 : 16;
+}
+
 static int radix_sort_onesweep(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* k0, uint32_t* v0,
                                uint32_t* k1, uint32_t* v1, long long n, int nbits, uint32_t* hist, int* which,
                                hipStream_t s) {
-    const int nb = sort_blocks(n);
+    const int items = onesweep_items(n);
+    const int nb = div_up(n, (long long)kB * items);  // look-back tiles
+    const int nbh = sort_blocks(n);                  // histogram blocks
     const int npass = (nbits + 7) / 8;
     uint32_t* ghist = hist;
     uint32_t* tickets = hist + 4 * 256;
     uint32_t* status = tickets + 16;
     const size_t words = 4 * 256 + 16 + (size_t)npass * nb * 256;
     if (hipError_t e = hipMemsetAsync(hist, 0, words * sizeof(uint32_t), s)) return (int)e;
-    hipLaunchKernelGGL(radix_hist_all, dim3(nb), dim3(kB), 0, s, keys_in, n, nbits, ghist);
+    hipLaunchKernelGGL(radix_hist_all, dim3(nbh), dim3(kB), 0, s, keys_in, n, nbits, ghist);
     const uint32_t* kin = keys_in;
     const uint32_t* vin = vals_in;
     int dst = 0;
@@ -745,8 +757,12 @@ static int radix_sort_onesweep(const uint32_t* keys_in, const uint32_t* vals_in,
         const int bits = (nbits - shift) < 8 ? (nbits - shift) : 8;
         uint32_t* ko = dst == 0 ? k0 : k1;
         uint32_t* vo = dst == 0 ? v0 : v1;
-        hipLaunchKernelGGL(radix_onesweep, dim3(nb), dim3(kB), 0, s, kin, vin, ko, vo, n, shift, bits,
-                           ghist + 256 * p, status + (size_t)p * nb * 256, tickets + p);
+        if (items == 4)
+            hipLaunchKernelGGL(radix_onesweep<4>, dim3(nb), dim3(kB), 0, s, kin, vin, ko, vo, n, shift, bits,
+                               ghist + 256 * p, status + (size_t)p * nb * 256, tickets + p);
+        else
+            hipLaunchKernelGGL(radix_onesweep<16>, dim3(nb), dim3(kB), 0, s, kin, vin, ko, vo, n, shift, bits,
+                               ghist + 256 * p, status + (size_t)p * nb * 256, tickets + p);
         kin = ko;
         vin = vo;
         *which = dst;
