@@ -314,7 +314,9 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
 
     long long K = 0;
     if (P > 0) {
-        PreOut po{radii, depth_key, tiles, rec, at<uint4>(bufs->geom, gl.rect), counters};
+        const bool full_img = ty0 == 0 && ty1 == gy;
+        PreOut po{radii, depth_key, tiles, rec, at<uint4>(bufs->geom, gl.rect),
+                  full_img ? at<uint32_t>(bufs->geom, gl.flags) : nullptr, counters};
         GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess(*cam, gauss_in(gs), ty0, ty1, po, stream), "preprocess");
         // A band ranks only its candidates (Gaussians with tiles in the band): the depth sort,
         // scan, duplicate and gather then scale with the band, not with P.
@@ -402,6 +404,15 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
                                        v.accum, v.ck, stream),
                   "blend forward");
     return 0;
+}
+
+// SH clamp bits stored by the forward (full image), or nullptr: B2 recomputes them (band).
+static const uint32_t* stored_flags(const gsr_camera* cam, const gsr_raster_settings* rs, const gsr_buffers* b,
+                                    int P) {
+    int ty0, ty1;
+    band(cam, rs, &ty0, &ty1);
+    if (ty0 != 0 || ty1 != div_up(cam->height, kTile)) return nullptr;
+    return at<uint32_t>(b->geom, GeomLayout(P).flags);
 }
 
 // Per-Gaussian grad2d for all P: the gather covers the ranked Gaussians (a band's candidates);
@@ -501,7 +512,7 @@ int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raste
     } else {
         GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(grad2d, 0, sizeof(float) * kPart * (size_t)P, stream), "zero grad2d");
     }
-    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), 0, P, v.depth_key, grad2d,
+    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), 0, P, v.depth_key, stored_flags(cam, rs, bufs, P), grad2d,
                                              grad_out(grads), stream),
                   "preprocess backward");
     return 0;
@@ -528,7 +539,7 @@ int gsr_backward_preprocess_range(const gsr_camera* cam, const gsr_gaussians* gs
     const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
     GeomLayout gl(gs->P);
     GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), g0, g1, at<uint32_t>(bufs->geom, gl.depth_key),
-                                             grad2d,
+                                             stored_flags(cam, rs, bufs, gs->P), grad2d,
                                              grad_out(grads), stream),
                   "preprocess backward");
     return 0;

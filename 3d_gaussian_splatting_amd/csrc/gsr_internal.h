@@ -41,13 +41,14 @@ inline size_t sort_scratch_words(long long n) {
 }
 
 struct GeomLayout {
-    size_t depth_key, tiles, rec, rect, cand_tmp, offsets, sA_k, sA_v, sB_k, sB_v, hist,
+    size_t depth_key, tiles, flags, rec, rect, cand_tmp, offsets, sA_k, sA_v, sB_k, sB_v, hist,
         partials, total;
     GeomLayout(int P) {
         size_t o = 0, n = (size_t)(P > 0 ? P : 1);
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
         depth_key = take(4 * n);
         tiles = take(4 * n);
+        flags = take(4 * n);  // SH clamp bits (full-image forwards; bands let B2 recompute)
         rec = take(16 * 3 * n);
         rect = take(16 * n);  // uint4: minx|miny<<16, maxx|maxy<<16, inst_start, 0
         cand_tmp = take(4 * n);  // band compaction: candidate gids before the depth sort

@@ -19,6 +19,7 @@ struct PreOut {
     uint32_t* tiles;
     float4* rec;   // blend records: {x, y, a', b'}, {c', o, r, g}, {b, ext_x, ext_y, log2 o}
     uint4* rect;   // (minx | miny << 16, maxx | maxy << 16, inst_start (set by F3), 0)
+    uint32_t* flags;     // nullable: SH clamp bits per Gaussian (B2 recomputes them when absent)
     uint32_t* counters;  // nullable, zeroed: [slot] += Gaussians with tiles in the band,
                          // [kCountSlots + slot] += K (slot = block % kCountSlots)
 };
@@ -89,7 +90,7 @@ struct GradOut {
 // B2: chain rule to the leaves for Gaussians [g0, g1) from their 2D gradients (grad2d, kPart
 // floats each).  Inputs are indexed by g; grad2d and all outputs by g - g0.
 int launch_preprocess_backward(const gsr_camera& cam, const GaussIn& in, int g0, int g1,
-                               const uint32_t* depth_key, const float* grad2d,
+                               const uint32_t* depth_key, const uint32_t* flags, const float* grad2d,
                                const GradOut& out, hipStream_t s);
 
 }  // namespace gsr

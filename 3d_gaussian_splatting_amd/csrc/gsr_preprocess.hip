@@ -142,6 +142,7 @@ __device__ __forceinline__ uint32_t preprocess_one(const gsr_camera& cam, const 
             // for a full image); B2 recomputes the clamp bits itself
             if (tiles_out != 0) {
                 float rgb[3];
+                uint32_t clamped = 0;
                 if (in.colors) {
                     rgb[0] = in.colors[3 * g + 0];
                     rgb[1] = in.colors[3 * g + 1];
@@ -186,6 +187,7 @@ __device__ __forceinline__ uint32_t preprocess_one(const gsr_camera& cam, const 
                         for (int k = 1; k < 16; ++k)
                             if (k < nb) r = r + basis[k] * rest[3 * (k - 1) + ch];
                         r = r + 0.5f;
+                        clamped |= (r < 0.0f ? 1u : 0u) << ch;
                         rgb[ch] = fmaxf(r, 0.0f);
                     }
                 }
@@ -205,6 +207,7 @@ __device__ __forceinline__ uint32_t preprocess_one(const gsr_camera& cam, const 
                 rec[2] = make_float4(rgb[2], ex, ey, log2f(opac));
                 out.rect[g] = make_uint4((uint32_t)minx | ((uint32_t)miny << 16),
                                          (uint32_t)maxx | ((uint32_t)maxy << 16), 0u, 0u);
+                if (out.flags) out.flags[g] = clamped;
             }
         }
     }

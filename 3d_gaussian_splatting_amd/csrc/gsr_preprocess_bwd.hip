@@ -74,6 +74,7 @@ __global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __re
 // overwritten in place with the row's gradient), or nullptr when there is no SH-rest input.
 __device__ void preprocess_backward_one(const gsr_camera& cam, const GaussIn& in, int g, int o,
                                         const uint32_t* __restrict__ depth_key,
+                                        const uint32_t* __restrict__ flags,
                                         const float* __restrict__ grad2d, const GradOut& out,
                                         float* lrest) {
     const bool visible = depth_key[g] != 0xFFFFFFFFu;
@@ -178,11 +179,14 @@ __device__ void preprocess_backward_one(const gsr_camera& cam, const GaussIn& in
                 dbx[15] = kC3[6] * 3.f * (xx - yy); dby[15] = kC3[6] * -6.f * xy;
             }
         }
-        // Clamp bits of the forward's SH->RGB, recomputed with the forward's exact arithmetic
-        // (same basis expressions and summation order, both files built -ffp-contract=off;
-        // gsr_preprocess.hip), so the forward need not store them and a banded forward may
-        // skip SH for Gaussians outside its band.
+        // Clamp bits of the forward's SH->RGB: stored by a full-image forward, else recomputed
+        // with the forward's exact arithmetic (same basis expressions and summation order, both
+        // files built -ffp-contract=off; gsr_preprocess.hip) -- a banded forward skips SH for
+        // Gaussians outside its band, which B2 on this rank's slice may still need.
         uint32_t cl = 0;
+        if (flags) {
+            cl = flags[g];
+        } else {
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) {
             float r = basis[0] * in.sh_dc[3 * g + ch];
@@ -193,6 +197,7 @@ __device__ void preprocess_backward_one(const gsr_camera& cam, const GaussIn& in
             }
             r = r + 0.5f;
             cl |= (r < 0.0f ? 1u : 0u) << ch;
+        }
         }
         const float dres[3] = {(cl & 1u) ? 0.f : g2[6], (cl & 2u) ? 0.f : g2[7], (cl & 4u) ? 0.f : g2[8]};
 #pragma unroll
@@ -367,7 +372,7 @@ __device__ void preprocess_backward_one(const gsr_camera& cam, const GaussIn& in
 // Gaussians [g0, g0 + n): inputs indexed by g, grad2d and every output by o = g - g0.
 __global__ __launch_bounds__(256) void preprocess_backward_kernel(
     const gsr_camera cam, const GaussIn in, int g0, int n, const uint32_t* __restrict__ depth_key,
-    const float* __restrict__ grad2d, GradOut out) {
+    const uint32_t* __restrict__ flags, const float* __restrict__ grad2d, GradOut out) {
     extern __shared__ __attribute__((aligned(16))) float sh_lds[];
     const int o = blockIdx.x * 256 + threadIdx.x;
     const int M3 = in.M_rest * 3;
@@ -379,7 +384,7 @@ __global__ __launch_bounds__(256) void preprocess_backward_kernel(
         __syncthreads();
     }
     if (o < n)
-        preprocess_backward_one(cam, in, g0 + o, o, depth_key, grad2d, out,
+        preprocess_backward_one(cam, in, g0 + o, o, depth_key, flags, grad2d, out,
                                 stage ? sh_lds + threadIdx.x * M3 : nullptr);
     if (stage) {  // coalesced write-back of the SH-rest gradient rows
         __syncthreads();
@@ -401,13 +406,13 @@ int launch_gather_grad2d(const uint32_t* gid_by_rank, const uint32_t* offsets, c
 }
 
 int launch_preprocess_backward(const gsr_camera& cam, const GaussIn& in, int g0, int g1,
-                               const uint32_t* depth_key, const float* grad2d,
+                               const uint32_t* depth_key, const uint32_t* flags, const float* grad2d,
                                const GradOut& out, hipStream_t s) {
     const int n = g1 - g0;
     if (n <= 0) return 0;
     const size_t lds = (in.sh_rest && !in.colors) ? sizeof(float) * 256 * 3 * in.M_rest : 0;
     hipLaunchKernelGGL(preprocess_backward_kernel, dim3(div_up(n, 256)), dim3(256), lds, s, cam, in, g0, n,
-                       depth_key, grad2d, out);
+                       depth_key, flags, grad2d, out);
     return (int)hipGetLastError();
 }
 

@@ -77,6 +77,30 @@ __global__ __launch_bounds__(kB) void radix_upsweep(const uint32_t* __restrict__
     hist[(size_t)tid * nb + blockIdx.x] = s;
 }
 
+// Same counts with LDS atomics (per-wave sub-histograms): counting needs no stable rank, so
+// the 8-ballot peer match of radix_upsweep is not needed here.
+__global__ __launch_bounds__(kB) void radix_upsweep_atomic(const uint32_t* __restrict__ keys, long long n,
+                                                           int shift, int nbits, int nb,
+                                                           uint32_t* __restrict__ hist) {
+    __shared__ uint32_t cnt[kWaves][256];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) cnt[k][tid] = 0;
+    __syncthreads();
+    const uint32_t mask = (1u << nbits) - 1u;
+    const long long base = (long long)blockIdx.x * kSortTile + (long long)w * kWaveItems;
+#pragma unroll 4
+    for (int r = 0; r < kI; ++r) {
+        const long long idx = base + r * 64 + lane;
+        if (idx < n) atomicAdd(&cnt[w][(keys[idx] >> shift) & mask], 1u);
+    }
+    __syncthreads();
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) s += cnt[k][tid];
+    hist[(size_t)tid * nb + blockIdx.x] = s;
+}
+
 // ---- column scan: block d turns hist[d*nb .. +nb) into an exclusive scan; totals[d] ----
 __global__ __launch_bounds__(kB) void radix_colscan(uint32_t* __restrict__ hist, int nb,
                                                     uint32_t* __restrict__ totals) {
@@ -728,6 +752,12 @@ static bool use_onesweep(bool depth_sort) {
 }
 
 // onesweep: ghist (4 x 256) | tickets (16) | status (passes x nb x 256); one memset per sort
+// reduce-then-scan upsweep: LDS-atomic counts (1, shipped) or ballot peer match (0)
+static bool upsweep_atomic() {
+    const char* e = std::getenv("GSR_UPSWEEP_VARIANT");
+    return e ? std::atoi(e) != 0 : true;
+}
+
 // Items per thread of the onesweep tiles: 16 (4096-key tiles) or 4 (1024-key tiles, 4x the
 // blocks -- for the small candidate sets of multi-GPU bands, where a pass is latency-bound).
 static int onesweep_items(long long n) {
@@ -787,7 +817,10 @@ int radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* k0, u
         const int bits = (nbits - shift) < 8 ? (nbits - shift) : 8;
         uint32_t* ko = dst == 0 ? k0 : k1;
         uint32_t* vo = dst == 0 ? v0 : v1;
-        hipLaunchKernelGGL(radix_upsweep, dim3(nb), dim3(kB), 0, s, kin, n, shift, bits, nb, hist);
+        if (upsweep_atomic())
+            hipLaunchKernelGGL(radix_upsweep_atomic, dim3(nb), dim3(kB), 0, s, kin, n, shift, bits, nb, hist);
+        else
+            hipLaunchKernelGGL(radix_upsweep, dim3(nb), dim3(kB), 0, s, kin, n, shift, bits, nb, hist);
         hipLaunchKernelGGL(radix_colscan, dim3(256), dim3(kB), 0, s, hist, nb, totals);
         hipLaunchKernelGGL(radix_downsweep, dim3(nb), dim3(kB), 0, s, kin, vin, ko, vo, n, shift, bits, nb,
                            hist, totals);
