@@ -21,15 +21,16 @@
 // round-robin dispatch, speed only), so each XCD gets a contiguous band of tile rows and
 // its L2 keeps the records those neighbouring tiles share.
 //
-// B1 reduces each record's 9 gradient terms over the tile's 256 pixels: 4 pixels per lane in
+// B1 reduces each record's 9 raw moments over the tile's 256 pixels: 4 pixels per lane in
 // registers, a 2-step quad DPP reduction, then the 16 quad partials wait in LDS and are summed
-// four records at a time (one (record, value) output per lane) -- ~40% fewer VALU ops than a
-// full 64-lane DPP/permlane reduction per record.  It writes ONE 36-B partial per
-// (tile, instance) with plain stores, indexed by the instance's emission index j.
+// four records at a time (one (record, moment) output per lane, stored straight to HBM) --
+// ~40% fewer VALU ops than a full 64-lane DPP/permlane reduction per record, and no per-batch
+// moment buffer in LDS (more waves per SIMD).  It writes ONE 36-B partial per (tile, instance)
+// with plain stores, indexed by the instance's emission index j.
 //
 // Measured and rejected (scripts/ablate.py): packing two stripes per VGPR pair
-// (v_pk_fma_f32) -- register shuffles and scalar/pair path splits cost more than the packed
-// issue saved (F6 0.31 -> 0.38 ms); 4 waves per tile; record prefetch into registers.  The
+// (v_pk_fma_f32 issues 2 FMAs in 4 cycles -- no gain over v_fma_f32 on gfx950, and the
+// register shuffles cost extra); 4 waves per tile; record prefetch into registers.  The
 // per-Gaussian sum happens later in fixed emission order (gsr_preprocess_bwd.hip), so
 // gradients are deterministic and no float atomics are issued.
 #include <cstdlib>
@@ -53,38 +54,17 @@ __device__ inline float dpp_f(float x) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
 }
 
-// Row-level (16-lane) all-reduce of N independent values, step-interleaved so consecutive
-// DPP reads never hit the VGPR written by the instruction right before (no s_nop hazards).
-template <int N>
-__device__ inline void row_reduce(float (&v)[N]) {
+// Quad (4-lane) all-reduce of 9 values.  The empty asm pins each sum in the block that
+// computes it: without it the compiler sinks the second add into the quad leaders' branch,
+// the DPP move can no longer fuse into it, and each value costs a zero move, a DPP move and
+// an add instead of one v_add_f32_dpp (18 extra VALU ops per record).
+__device__ __forceinline__ void quad_reduce9(float (&v)[9]) {
 #pragma unroll
-    for (int i = 0; i < N; ++i) v[i] += dpp_f<0xB1>(v[i]);   // quad_perm [1,0,3,2]
+    for (int i = 0; i < 9; ++i) v[i] += dpp_f<0xB1>(v[i]);  // quad_perm [1,0,3,2]
 #pragma unroll
-    for (int i = 0; i < N; ++i) v[i] += dpp_f<0x4E>(v[i]);   // quad_perm [2,3,0,1]
+    for (int i = 0; i < 9; ++i) v[i] += dpp_f<0x4E>(v[i]);  // quad_perm [2,3,0,1]
 #pragma unroll
-    for (int i = 0; i < N; ++i) v[i] += dpp_f<0x141>(v[i]);  // row_half_mirror
-#pragma unroll
-    for (int i = 0; i < N; ++i) v[i] += dpp_f<0x140>(v[i]);  // row_mirror
-}
-
-// gfx950 reduce-scatter of four row-reduced values: afterwards lanes of row 0/1/2/3 hold the
-// 64-lane totals of a/b/c/d.  v_permlane16_swap swaps VDST rows 1,3 with VSRC rows 0,2;
-// v_permlane32_swap swaps VDST lanes 32-63 with VSRC lanes 0-31.
-__device__ inline float scatter4(float a, float b, float c, float d) {
-    auto ab = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
-    auto cd = __builtin_amdgcn_permlane16_swap(__float_as_uint(c), __float_as_uint(d), false, false);
-    const float x = __uint_as_float(ab[0]) + __uint_as_float(ab[1]);  // rows: a01 b01 a23 b23
-    const float y = __uint_as_float(cd[0]) + __uint_as_float(cd[1]);  // rows: c01 d01 c23 d23
-    auto xy = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
-    return __uint_as_float(xy[0]) + __uint_as_float(xy[1]);           // rows: a b c d
-}
-
-// full 64-lane all-reduce of a row-reduced value (every lane gets the total)
-__device__ inline float allreduce_rows(float a) {
-    auto s16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(a), false, false);
-    const float x = __uint_as_float(s16[0]) + __uint_as_float(s16[1]);
-    auto s32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-    return __uint_as_float(s32[0]) + __uint_as_float(s32[1]);
+    for (int i = 0; i < 9; ++i) asm volatile("" : "+v"(v[i]));
 }
 
 struct BlendGeom {
@@ -275,11 +255,13 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
     }
 }
 
-// Deferred B1 reduction: 16 quad partials of 9 values for each of `parked` records wait in
-// LDS; lane (slot, c) sums the 16 partials of one (record, value) output in fixed quad order.
+// Deferred B1 reduction.  A record's 9 per-lane moments are quad-reduced by DPP; the 16 quad
+// partials wait in LDS, and every kPark records one (record, moment) output per lane is summed
+// from LDS in fixed quad order and stored straight to the partial arrays at the record's
+// emission index j (8 moments in part8[2j..2j+1], the 9th in part1[j]).
 constexpr int kPark = 4;
-__device__ __forceinline__ void park_flush(const float* qpark, const int* qrec, int parked, float* smom,
-                                           int lane) {
+__device__ __forceinline__ void park_flush(const float* qpark, const uint32_t* qjl, int parked, float* p8f,
+                                           float* p1, int lane) {
     __syncthreads();  // one-wave block: orders the quad leaders' LDS writes before the reads
     if (lane < parked * 9) {
         const int slot = lane / 9, c = lane - 9 * slot;
@@ -287,7 +269,9 @@ __device__ __forceinline__ void park_flush(const float* qpark, const int* qrec, 
         float t[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int i = 0; i < 16; ++i) t[i & 3] += q[i * 12];
-        smom[qrec[slot] * 12 + c] = (t[0] + t[1]) + (t[2] + t[3]);
+        const uint32_t j = qjl[slot];
+        float* dst = c < 8 ? p8f + 8 * (size_t)j + c : p1 + j;
+        *dst = (t[0] + t[1]) + (t[2] + t[3]);
     }
     __syncthreads();
 }
@@ -295,15 +279,24 @@ __device__ __forceinline__ void park_flush(const float* qpark, const int* qrec, 
 // B1 front to back.  With S = the forward's colour sum (no background) and the running
 // Sp = sum over processed contributors of w * (c . dL/dpix), the colour behind entry k is
 // (S . dL/dpix - Sp) / (1 - alpha_k) after T_k, so
-//   dL/dalpha_k = T_k (c_k . dL/dpix) - (S . dL/dpix - Sp + T_final bg . dL/dpix) / (1 - alpha_k)
-// (SURVEY B.4 rewritten; same value as the back-to-front recursion).  T is recomputed with
+//   dL/dalpha_k = T_k (c_k . dL/dpix) - R / (1 - alpha_k),
+//   R = S . dL/dpix + T_final bg . dL/dpix - Sp
+// (SURVEY B.4 rewritten; same value as the back-to-front recursion).  A lane keeps R itself
+// (R -= w (c . dL/dpix) per contributor), one register and one op fewer than Sp and S.  T is recomputed with
 // the forward's own instructions (same alpha, same T (1 - alpha), same sign encoding), so
 // the set of contributing pairs -- and the termination point -- is exactly the forward's.
 // Per record the lane accumulates sv = o G dL/dalpha moments along its column
 // (sum sv, sum sv dy, sum sv dy^2) and applies dx afterwards:
 //   Sx = dx sum sv, Sxx = dx^2 sum sv, Sxy = dx sum sv dy.
-template <bool DEFER>
-__global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
+// B1 stores the raw tile sums (Sx, Sy, Sxx, Sxy, Syy, S0, colour x3); they are linear in the
+// gradients, so gather_grad2d converts them once per Gaussian after summing over tiles.
+//
+// Grid: one 64-lane block per (tile, chunk) when F6 wrote chunk checkpoints (ck), else per
+// tile.  Each XCD (blocks b with equal b % 8) takes a contiguous tile range as in xcd_tile,
+// visited chunk-major, so every tile's front chunk -- the longest -- is dispatched first.
+// 6 waves per SIMD: 80 VGPRs (no spills) and 6.2 KB of LDS per one-wave block.  Measured
+// 0.552 ms vs 0.564 at the compiler's own 85 VGPRs (5 waves); 7 and 8 waves spill.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void blend_backward_kernel(const BlendGeom geo,
                                                             const uint2* __restrict__ ranges,
                                                             const uint32_t* __restrict__ sorted_gid,
                                                             const uint4* __restrict__ rect,
@@ -311,16 +304,14 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
                                                             const float* __restrict__ final_T,
                                                             const float* __restrict__ accum,
                                                             const float* __restrict__ dL_dpix,
-                                                            float4* __restrict__ part8,
-                                                            float* __restrict__ part1,
+                                                            float* __restrict__ p8f,
+                                                            float* __restrict__ p1,
                                                             const float4* __restrict__ ck) {
     __shared__ float4 srec[64 * 3];
-    __shared__ float smom[64 * 12];
-    __shared__ float qpark[DEFER ? kPark * 16 * 12 : 1];  // [slot][quad][9 of 12]
-    __shared__ int qrec[DEFER ? kPark : 1];
-    // chunked (ck != nullptr): block -> (tile, chunk).  Each XCD (blocks b with equal b % 8)
-    // takes a contiguous tile range as in xcd_tile, visited chunk-major, so every tile's
-    // front chunk -- the longest -- is dispatched first.  Grid: 8 x ceil(nwg / 8) x chunks.
+    __shared__ float qpark[kPark * 16 * 12];  // [slot][quad][9 of 12]
+    __shared__ uint32_t qjl[kPark];
+    const int lane = threadIdx.x;
+    float* const qlane = qpark + (lane >> 2) * 12;  // this quad's parking row
     int tl, chunk;
     if (ck) {
         const int q = geo.nwg / 8, r = geo.nwg % 8, xcd = blockIdx.x % 8, local = blockIdx.x / 8;
@@ -336,14 +327,13 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
     }
     const int tile = tl + geo.ty0 * geo.grid_x;
     const int tx = tile % geo.grid_x, ty = tile / geo.grid_x;
-    const int lane = threadIdx.x;
     const int px = tx * kTile + (lane & 15);
     const float pfx = (float)px;
     const float bx0 = (float)(tx * kTile), by0 = (float)(ty * kTile);
     const size_t npix = (size_t)geo.W * geo.H;
-    const float hw = 0.5f * (float)geo.W, hh = 0.5f * (float)geo.H;
     const int row = lane >> 4;
-    float pfy[kPPL], T[kPPL], Sp[kPPL], cb[kPPL], dp0[kPPL], dp1[kPPL], dp2[kPPL];
+    // R = S . dL/dpix - Sp + T_final bg . dL/dpix: the colour term behind the current record
+    float pfy[kPPL], T[kPPL], R[kPPL], dp0[kPPL], dp1[kPPL], dp2[kPPL];
 #pragma unroll
     for (int p = 0; p < kPPL; ++p) {
         const int py = ty * kTile + row + 4 * p;
@@ -356,9 +346,8 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
         dp2[p] = in ? dL_dpix[2 * npix + pix] : 0.0f;
         const float sdp = in ? accum[pix] * dp0[p] + accum[npix + pix] * dp1[p] + accum[2 * npix + pix] * dp2[p]
                              : 0.0f;
-        cb[p] = sdp + Tfin * (geo.bg0 * dp0[p] + geo.bg1 * dp1[p] + geo.bg2 * dp2[p]);
+        R[p] = sdp + Tfin * (geo.bg0 * dp0[p] + geo.bg1 * dp1[p] + geo.bg2 * dp2[p]);
         T[p] = in ? 1.0f : -1.0f;
-        Sp[p] = 0.0f;
     }
     const uint2 range = ranges[tile];
     const int n_all = (int)(range.y - range.x);
@@ -368,45 +357,40 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
         start = chunk * CH;
         if (start >= n_all) return;  // no such chunk for this tile
         n = start + CH < n_all ? start + CH : n_all;
-        if (chunk > 0) {  // resume from F6's checkpoint: T and Sp = dL/dpix . (colour sum so far)
+        if (chunk > 0) {  // resume from F6's checkpoint: T, and R less dL/dpix . (colour sum so far)
             const float4* src = ck + ((size_t)tl * (kMaxChunks - 1) + (chunk - 1)) * 256;
 #pragma unroll
             for (int p = 0; p < kPPL; ++p) {
                 const float4 c4 = src[64 * p + lane];
                 T[p] = c4.x;
-                Sp[p] = fmaf(c4.y, dp0[p], fmaf(c4.z, dp1[p], c4.w * dp2[p]));
+                R[p] -= fmaf(c4.y, dp0[p], fmaf(c4.z, dp1[p], c4.w * dp2[p]));
             }
         }
     }
     for (int base = start; base < n; base += 64) {
         const int cnt = (n - base) < 64 ? (n - base) : 64;
-        const int e_l = base + lane;
         uint32_t live = 0;
 #pragma unroll
         for (int p = 0; p < kPPL; ++p) live |= __any(T[p] > 0.0f) ? (1u << p) : 0u;
         uint32_t jl = 0, smask = 0;
-        float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0;
         if (lane < cnt) {
-            const uint32_t g = sorted_gid[range.x + e_l];
+            const uint32_t g = sorted_gid[range.x + base + lane];
             const uint4 rr = rect[g];  // rect + inst_start in one 16-B load
             const int minx = rr.x & 0xFFFF, miny = rr.x >> 16, maxx = rr.y & 0xFFFF;
             const int y0 = miny > geo.ty0 ? miny : geo.ty0;
             jl = rr.z + (uint32_t)((ty - y0) * (maxx - minx) + (tx - minx));
             if (live) {
                 const float4* r = rec + 3 * (size_t)g;
-                q0 = r[0];
-                q1 = r[1];
-                const float4 r2 = r[2];
-                srec[3 * lane + 0] = q0;
-                srec[3 * lane + 1] = q1;
+                const float4 r0 = r[0], r1 = r[1], r2 = r[2];
+                srec[3 * lane + 0] = r0;
+                srec[3 * lane + 1] = r1;
                 srec[3 * lane + 2] = r2;
-                smask = stripe_mask(q0, q1, r2, bx0, by0, geo.ellipse_cull);
+                smask = stripe_mask(r0, r1, r2, bx0, by0, geo.ellipse_cull);
             }
         }
-#pragma unroll
-        for (int c = 0; c < 12; ++c) smom[lane * 12 + c] = 0.0f;
         __syncthreads();
         uint64_t todo = __ballot((smask & live) != 0u);
+        uint64_t stored = 0;  // records whose moments were flushed
         int visited = 0, parked = 0;
         while (todo) {
             const int k = __builtin_ctzll(todo);
@@ -434,8 +418,8 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
                     any = true;
                     const float w = a * T[p];
                     const float cdp = fmaf(r1.z, dp0[p], fmaf(r1.w, dp1[p], r2.x * dp2[p]));
-                    Sp[p] = fmaf(w, cdp, Sp[p]);
-                    const float dLda = fmaf(T[p], cdp, -(cb[p] - Sp[p]) * __builtin_amdgcn_rcpf(one_m));
+                    R[p] = fmaf(-w, cdp, R[p]);
+                    const float dLda = fmaf(T[p], cdp, -R[p] * __builtin_amdgcn_rcpf(one_m));
                     g0 = fmaf(w, dp0[p], g0);
                     g1 = fmaf(w, dp1[p], g1);
                     g2 = fmaf(w, dp2[p], g2);
@@ -450,33 +434,18 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
             if (__any(any)) {
                 const float sx = s0 * dx;
                 float v[9] = {sx, sy, sx * dx, sy * dx, syy, s0, g0, g1, g2};
-                if (DEFER) {
-                    // quad partials -> LDS; summed kPark records at a time by park_flush
-#pragma unroll
-                    for (int i = 0; i < 9; ++i) v[i] += dpp_f<0xB1>(v[i]);  // quad_perm [1,0,3,2]
-#pragma unroll
-                    for (int i = 0; i < 9; ++i) v[i] += dpp_f<0x4E>(v[i]);  // quad_perm [2,3,0,1]
-                    if ((lane & 3) == 0) {
-                        float* dst = qpark + (parked * 16 + (lane >> 2)) * 12;
-                        *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
-                        *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
-                        dst[8] = v[8];
-                    }
-                    if (lane == 0) qrec[parked] = k;
-                    if (++parked == kPark) {
-                        park_flush(qpark, qrec, parked, smom, lane);
-                        parked = 0;
-                    }
-                } else {
-                    row_reduce(v);
-                    const float t0 = scatter4(v[0], v[1], v[2], v[3]);
-                    const float t1 = scatter4(v[4], v[5], v[6], v[7]);
-                    const float t2 = allreduce_rows(v[8]);
-                    if ((lane & 15) == 0) {
-                        smom[k * 12 + row] = t0;
-                        smom[k * 12 + 4 + row] = t1;
-                        if (row == 0) smom[k * 12 + 8] = t2;
-                    }
+                quad_reduce9(v);
+                if ((lane & 3) == 0) {
+                    float* dst = qlane + parked * (16 * 12);
+                    *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+                    *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
+                    dst[8] = v[8];
+                }
+                if (lane == 0) qjl[parked] = (uint32_t)__builtin_amdgcn_readlane((int)jl, k);
+                stored |= 1ull << k;
+                if (++parked == kPark) {
+                    park_flush(qpark, qjl, parked, p8f, p1, lane);
+                    parked = 0;
                 }
             }
             if ((++visited & 7) == 0) {
@@ -487,220 +456,16 @@ __global__ __launch_bounds__(64) void blend_backward_kernel(const BlendGeom geo,
                 if (live == 0) break;
             }
         }
-        if (DEFER && parked) park_flush(qpark, qrec, parked, smom, lane);
-        __syncthreads();
-        if (lane < cnt) {
-            // moments -> d mean2D (NDC), d conic, d opacity (sum G dL/dalpha = sum sv / o), d colour
-            const float* mo = smom + lane * 12;
-            const float Sx = mo[0], Sy = mo[1], Sxx = mo[2], Sxy = mo[3], Syy = mo[4], S0 = mo[5];
-            const float A = -2.0f * kLn2 * q0.z, B = -kLn2 * q0.w, C = -2.0f * kLn2 * q1.x;
-            const float dop = S0 != 0.0f ? S0 / q1.y : 0.0f;
-            part8[2 * (size_t)jl + 0] = make_float4((-A * Sx - B * Sy) * hw, (-C * Sy - B * Sx) * hh, -0.5f * Sxx, -Sxy);
-            part8[2 * (size_t)jl + 1] = make_float4(-0.5f * Syy, dop, mo[6], mo[7]);
-            part1[jl] = mo[8];
+        if (parked) park_flush(qpark, qjl, parked, p8f, p1, lane);
+        if (lane < cnt && !((stored >> lane) & 1ull)) {  // no pixel took a gradient from it
+            float4* d8 = reinterpret_cast<float4*>(p8f) + 2 * (size_t)jl;
+            d8[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+            d8[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+            p1[jl] = 0.f;
         }
-        __syncthreads();
+        __syncthreads();  // srec / qpark are rewritten by the next batch
     }
 }
-
-
-
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// B1 with NW waves per tile: wave w owns stripes [w*PPL, (w+1)*PPL) (PPL = 4 / NW), so a
-// tile's records are swept by NW waves at once -- the multi-GPU bands have only 1/N of the
-// tiles, and at one wave per tile B1 would leave most SIMDs idle.  Each wave reduces its own
-// stripes' terms (quad DPP + parked LDS partials, wave-local syncs) into its own moment row;
-// the NW rows are summed in fixed wave order at batch end, so results stay deterministic.
-// Same arithmetic per (pixel, record) as blend_backward_kernel.
-template <int NW>
-__global__ __launch_bounds__(64 * NW) void blend_backward_nw_kernel(const BlendGeom geo,
-                                                                    const uint2* __restrict__ ranges,
-                                                                    const uint32_t* __restrict__ sorted_gid,
-                                                                    const uint4* __restrict__ rect,
-                                                                    const float4* __restrict__ rec,
-                                                                    const float* __restrict__ final_T,
-                                                                    const float* __restrict__ accum,
-                                                                    const float* __restrict__ dL_dpix,
-                                                                    float4* __restrict__ part8,
-                                                                    float* __restrict__ part1) {
-    constexpr int PPL = kPPL / NW;
-    __shared__ float4 srec[64 * 3];
-    __shared__ uint32_t smk[64];
-    __shared__ float smom[NW][64 * 9];
-    __shared__ float qpark[NW][kPark * 16 * 12];
-    __shared__ int qrec[NW][kPark];
-    const int tile = xcd_tile(blockIdx.x, geo.nwg) + geo.ty0 * geo.grid_x;
-    const int tx = tile % geo.grid_x, ty = tile / geo.grid_x;
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const int px = tx * kTile + (lane & 15);
-    const float pfx = (float)px;
-    const float bx0 = (float)(tx * kTile), by0 = (float)(ty * kTile);
-    const size_t npix = (size_t)geo.W * geo.H;
-    const float hw = 0.5f * (float)geo.W, hh = 0.5f * (float)geo.H;
-    const int row = lane >> 4;
-    float pfy[PPL], T[PPL], Sp[PPL], cb[PPL], dp0[PPL], dp1[PPL], dp2[PPL];
-#pragma unroll
-    for (int p = 0; p < PPL; ++p) {
-        const int py = ty * kTile + row + 4 * (w * PPL + p);
-        pfy[p] = (float)py;
-        const bool in = px < geo.W && py < geo.H;
-        const size_t pix = in ? (size_t)py * geo.W + px : 0;
-        const float Tfin = in ? final_T[pix] : 1.0f;
-        dp0[p] = in ? dL_dpix[pix] : 0.0f;
-        dp1[p] = in ? dL_dpix[npix + pix] : 0.0f;
-        dp2[p] = in ? dL_dpix[2 * npix + pix] : 0.0f;
-        const float sdp = in ? accum[pix] * dp0[p] + accum[npix + pix] * dp1[p] + accum[2 * npix + pix] * dp2[p]
-                             : 0.0f;
-        cb[p] = sdp + Tfin * (geo.bg0 * dp0[p] + geo.bg1 * dp1[p] + geo.bg2 * dp2[p]);
-        T[p] = in ? 1.0f : -1.0f;
-        Sp[p] = 0.0f;
-    }
-    auto live_mask = [&]() {
-        uint32_t lv = 0;
-#pragma unroll
-        for (int p = 0; p < PPL; ++p) lv |= __any(T[p] > 0.0f) ? (1u << p) : 0u;
-        return lv;
-    };
-    float* qp = qpark[w];
-    int* qr = qrec[w];
-    float* sm = smom[w];
-    auto flush = [&](int parked) {
-        wave_lds_sync();
-        if (lane < parked * 9) {
-            const int slot = lane / 9, c = lane - 9 * slot;
-            const float* q = qp + slot * 16 * 12 + c;
-            float t4[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int i = 0; i < 16; ++i) t4[i & 3] += q[i * 12];
-            sm[qr[slot] * 9 + c] = (t4[0] + t4[1]) + (t4[2] + t4[3]);
-        }
-        wave_lds_sync();
-    };
-    const uint2 range = ranges[tile];
-    const int n = (int)(range.y - range.x);
-    for (int base = 0; base < n; base += 64) {
-        const int cnt = (n - base) < 64 ? (n - base) : 64;
-        uint32_t live = live_mask();
-        const int any_live = __syncthreads_or(live != 0);
-        uint32_t jl = 0;
-        float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0;
-        if (w == 0 && lane < cnt) {
-            const uint32_t g = sorted_gid[range.x + base + lane];
-            const uint4 rr = rect[g];
-            const int minx = rr.x & 0xFFFF, miny = rr.x >> 16, maxx = rr.y & 0xFFFF;
-            const int y0 = miny > geo.ty0 ? miny : geo.ty0;
-            jl = rr.z + (uint32_t)((ty - y0) * (maxx - minx) + (tx - minx));
-            uint32_t mk = 0;
-            if (any_live) {
-                const float4* r = rec + 3 * (size_t)g;
-                q0 = r[0];
-                q1 = r[1];
-                const float4 r2 = r[2];
-                srec[3 * lane + 0] = q0;
-                srec[3 * lane + 1] = q1;
-                srec[3 * lane + 2] = r2;
-                mk = stripe_mask(q0, q1, r2, bx0, by0, geo.ellipse_cull);
-            }
-            smk[lane] = mk;
-        } else if (w == 0) {
-            smk[lane] = 0u;
-        }
-#pragma unroll
-        for (int c = 0; c < 9; ++c) sm[lane * 9 + c] = 0.0f;
-        __syncthreads();
-        const uint32_t mine = (smk[lane] >> (w * PPL)) & ((1u << PPL) - 1u);
-        uint64_t todo = __ballot((mine & live) != 0u);
-        int visited = 0, parked = 0;
-        while (todo) {
-            const int k = __builtin_ctzll(todo);
-            todo &= todo - 1;
-            const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)mine, k) & live;
-            const float4 r0 = srec[3 * k + 0];
-            const float4 r1 = srec[3 * k + 1];
-            const float4 r2 = srec[3 * k + 2];
-            const float dx = r0.x - pfx;
-            const float bdx = r0.w * dx;
-            const float K = fmaf(r0.z * dx, dx, r2.w);
-            float s0 = 0.f, sy = 0.f, syy = 0.f, g0 = 0.f, g1 = 0.f, g2 = 0.f;
-            bool any = false;
-#pragma unroll
-            for (int p = 0; p < PPL; ++p) {
-                if (!(m & (1u << p))) continue;  // wave-uniform
-                const float dy = r0.y - pfy[p];
-                const float e = fmaf(bdx, dy, fmaf(r1.x * dy, dy, K));
-                float oG;
-                const float a = pair_alpha(e, r2.w, oG);
-                const float one_m = 1.0f - a;
-                const float tT = T[p] * one_m;
-                const bool ok = tT >= 0.0001f;
-                if (ok && a > 0.0f) {
-                    any = true;
-                    const float wt = a * T[p];
-                    const float cdp = fmaf(r1.z, dp0[p], fmaf(r1.w, dp1[p], r2.x * dp2[p]));
-                    Sp[p] = fmaf(wt, cdp, Sp[p]);
-                    const float dLda = fmaf(T[p], cdp, -(cb[p] - Sp[p]) * __builtin_amdgcn_rcpf(one_m));
-                    g0 = fmaf(wt, dp0[p], g0);
-                    g1 = fmaf(wt, dp1[p], g1);
-                    g2 = fmaf(wt, dp2[p], g2);
-                    const float sv = oG * dLda;
-                    s0 += sv;
-                    const float svy = sv * dy;
-                    sy += svy;
-                    syy = fmaf(svy, dy, syy);
-                }
-                T[p] = ok ? tT : -fabsf(T[p]);
-            }
-            if (__any(any)) {
-                const float sx = s0 * dx;
-                float v[9] = {sx, sy, sx * dx, sy * dx, syy, s0, g0, g1, g2};
-#pragma unroll
-                for (int i = 0; i < 9; ++i) v[i] += dpp_f<0xB1>(v[i]);  // quad_perm [1,0,3,2]
-#pragma unroll
-                for (int i = 0; i < 9; ++i) v[i] += dpp_f<0x4E>(v[i]);  // quad_perm [2,3,0,1]
-                if ((lane & 3) == 0) {
-                    float* dst = qp + (parked * 16 + (lane >> 2)) * 12;
-                    *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
-                    *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
-                    dst[8] = v[8];
-                }
-                if (lane == 0) qr[parked] = k;
-                if (++parked == kPark) {
-                    flush(parked);
-                    parked = 0;
-                }
-            }
-            if ((++visited & 7) == 0) {
-                live = live_mask();
-                if (live == 0) break;
-            }
-        }
-        if (parked) flush(parked);
-        __syncthreads();
-        if (w == 0 && lane < cnt) {
-            float mo[9];
-#pragma unroll
-            for (int c = 0; c < 9; ++c) {
-                float acc = smom[0][lane * 9 + c];
-#pragma unroll
-                for (int v2 = 1; v2 < NW; ++v2) acc += smom[v2][lane * 9 + c];  // fixed wave order
-                mo[c] = acc;
-            }
-            const float Sx = mo[0], Sy = mo[1], Sxx = mo[2], Sxy = mo[3], Syy = mo[4], S0 = mo[5];
-            const float A = -2.0f * kLn2 * q0.z, B = -kLn2 * q0.w, C = -2.0f * kLn2 * q1.x;
-            const float dop = S0 != 0.0f ? S0 / q1.y : 0.0f;
-            part8[2 * (size_t)jl + 0] = make_float4((-A * Sx - B * Sy) * hw, (-C * Sy - B * Sx) * hh, -0.5f * Sxx, -Sxy);
-            part8[2 * (size_t)jl + 1] = make_float4(-0.5f * Syy, dop, mo[6], mo[7]);
-            part1[jl] = mo[8];
-        }
-        __syncthreads();
-    }
-}
-
 }  // namespace
 
 // Kernel-variant selector for A/B timing (bench/ablation only; default = shipped variant).
@@ -752,28 +517,10 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
     if (geo.nwg <= 0) return 0;
     const PartLayout pl(K);
     char* base = reinterpret_cast<char*>(partial);
-    // 0: one wave per tile, full per-record DPP/permlane reduction; 1: one wave per tile,
-    // deferred quad/LDS reduction; 2 / 4: that many waves per tile.  Default: 1 for a full
-    // image, 4 waves when the launch has too few tiles to fill the chip (multi-GPU bands).
-    // 1 (shipped): one wave per tile (per tile chunk when F6 wrote checkpoints), deferred
-    // quad/LDS reduction; 0: full per-record DPP/permlane reduction; 2 / 4: that many waves
-    // per tile (no chunks).
-    const int v = variant("GSR_BWD_VARIANT", 1);
-    char* p8 = base + pl.p8;
-    float* p1 = reinterpret_cast<float*>(base + pl.p1);
     const int blocks = ck ? 8 * (geo.nwg / 8 + 1) * kMaxChunks : geo.nwg;
-    if (v == 0)
-        hipLaunchKernelGGL(blend_backward_kernel<false>, dim3(blocks), dim3(64), 0, s, geo, ranges, sorted_gid,
-                           rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(p8), p1, ck);
-    else if (v == 2)
-        hipLaunchKernelGGL(blend_backward_nw_kernel<2>, dim3(geo.nwg), dim3(128), 0, s, geo, ranges, sorted_gid,
-                           rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(p8), p1);
-    else if (v == 4)
-        hipLaunchKernelGGL(blend_backward_nw_kernel<4>, dim3(geo.nwg), dim3(256), 0, s, geo, ranges, sorted_gid,
-                           rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(p8), p1);
-    else
-        hipLaunchKernelGGL(blend_backward_kernel<true>, dim3(blocks), dim3(64), 0, s, geo, ranges, sorted_gid,
-                           rect, rec, final_T, accum, dL_dpix, reinterpret_cast<float4*>(p8), p1, ck);
+    hipLaunchKernelGGL(blend_backward_kernel, dim3(blocks), dim3(64), 0, s, geo, ranges, sorted_gid, rect, rec,
+                       final_T, accum, dL_dpix, reinterpret_cast<float*>(base + pl.p8),
+                       reinterpret_cast<float*>(base + pl.p1), ck);
     return (int)hipGetLastError();
 }
 

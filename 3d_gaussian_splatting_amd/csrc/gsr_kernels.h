@@ -81,7 +81,7 @@ constexpr float kLn2 = 0.6931471805599453f;  // conic A = -2 ln2 a', B = -ln2 b'
 // sum partials per Gaussian (emission order) -> grad2d (kPart floats per Gaussian; zeros for
 // culled Gaussians).  gid_by_rank / offsets: depth-sort permutation and inclusive tile scan.
 int launch_gather_grad2d(const uint32_t* gid_by_rank, const uint32_t* offsets, const float* partial,
-                         long long K, int P, float* grad2d, hipStream_t s);
+                         const float4* rec, int W, int H, long long K, int P, float* grad2d, hipStream_t s);
 
 struct GradOut {
     float *means2D, *conic, *opac, *colors, *means3D, *sh_dc, *sh_rest, *scales, *rots, *cov3D;

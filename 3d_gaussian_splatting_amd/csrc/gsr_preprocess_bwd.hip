@@ -31,14 +31,18 @@ constexpr float kC1 = 0.4886025119029199f;
 // consecutive depth ranks; their segments [offsets[r-1], offsets[r]) tile one contiguous
 // stretch of the partial arrays, which the block streams through LDS in coalesced windows of
 // kGatherWin entries.  Each thread then adds the part of its own segment that lies in the
-// window, in order, from LDS.  The 48-B result lands at grad2d[gid].
+// window, in order, from LDS.  The partials are B1's raw tile moments (Sx, Sy, Sxx, Sxy, Syy,
+// S0, colour x3, gsr_blend.hip); they are linear in the 2D gradients, so the conversion
+// runs once on the per-Gaussian sum, with the Gaussian's own conic and opacity from its blend
+// record.  The 48-B result lands at grad2d[gid].
 constexpr int kGatherWin = 512;
 
 __global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __restrict__ gid_by_rank,
                                                             const uint32_t* __restrict__ offsets,
                                                             const float4* __restrict__ p8,
-                                                            const float* __restrict__ p1, int P,
-                                                            float* __restrict__ grad2d) {
+                                                            const float* __restrict__ p1,
+                                                            const float4* __restrict__ rec, float hw, float hh,
+                                                            int P, float* __restrict__ grad2d) {
     __shared__ float4 w8[2 * kGatherWin];
     __shared__ float w1[kGatherWin];
     const int r0 = blockIdx.x * 256, r = r0 + threadIdx.x;
@@ -64,9 +68,14 @@ __global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __re
         __syncthreads();
     }
     if (r >= P) return;
-    float4* dst = reinterpret_cast<float4*>(grad2d + (size_t)kPart * gid_by_rank[r]);
-    dst[0] = make_float4(a[0], a[1], a[2], a[3]);
-    dst[1] = make_float4(a[4], a[5], a[6], a[7]);
+    const uint32_t g = gid_by_rank[r];
+    // moments -> d mean2D (NDC), d conic, d opacity (sum G dL/dalpha = S0 / o), d colour
+    const float4 q0 = rec[3 * (size_t)g], q1 = rec[3 * (size_t)g + 1];
+    const float A = -2.0f * kLn2 * q0.z, B = -kLn2 * q0.w, C = -2.0f * kLn2 * q1.x;
+    const float Sx = a[0], Sy = a[1], S0 = a[5];
+    float4* dst = reinterpret_cast<float4*>(grad2d + (size_t)kPart * g);
+    dst[0] = make_float4((-A * Sx - B * Sy) * hw, (-C * Sy - B * Sx) * hh, -0.5f * a[2], -a[3]);
+    dst[1] = make_float4(-0.5f * a[4], S0 != 0.0f ? S0 / q1.y : 0.0f, a[6], a[7]);
     dst[2] = make_float4(a[8], 0.f, 0.f, 0.f);
 }
 
@@ -395,13 +404,13 @@ __global__ __launch_bounds__(256) void preprocess_backward_kernel(
 }  // namespace
 
 int launch_gather_grad2d(const uint32_t* gid_by_rank, const uint32_t* offsets, const float* partial,
-                         long long K, int P, float* grad2d, hipStream_t s) {
+                         const float4* rec, int W, int H, long long K, int P, float* grad2d, hipStream_t s) {
     if (P <= 0) return 0;
     const PartLayout pl(K);
     const char* base = reinterpret_cast<const char*>(partial);
     hipLaunchKernelGGL(gather_grad2d_kernel, dim3(div_up(P, 256)), dim3(256), 0, s, gid_by_rank, offsets,
                        reinterpret_cast<const float4*>(base + pl.p8), reinterpret_cast<const float*>(base + pl.p1),
-                       P, grad2d);
+                       rec, 0.5f * (float)W, 0.5f * (float)H, P, grad2d);
     return (int)hipGetLastError();
 }
 
