@@ -126,9 +126,6 @@ __device__ __forceinline__ float pair_alpha(float e, float L, float& oG) {
     return (e <= L && oG >= (1.0f / 255.0f)) ? a : 0.0f;
 }
 
-// F6.  T > 0: pixel live; T <= 0: done, |T| = final transmittance (the T after the last
-// contributor -- the reference's final_T).  A pair is blended when T (1 - alpha) >= 1e-4,
-// otherwise the pixel terminates with T unchanged (SURVEY B.3 / forward.cu renderCUDA).
 // Chunk length of a tile's list when B1 is chunked: at most kMaxChunks chunks of whole
 // 64-record sub-batches (F6 checkpoints at 64-record boundaries).  Most of a tile's B1 work
 // is in its front records (pixels terminate), so chunks stay short to split that front.
@@ -137,6 +134,11 @@ __device__ __forceinline__ int chunk_len(int n) {
     return ((c + 63) / 64) * 64;
 }
 
+// F6.  T > 0: pixel live; T <= 0: done, |T| = final transmittance (the T after the last
+// contributor -- the reference's final_T).  A pair is blended when the next transmittance
+// T - alpha T (the reference's T (1 - alpha), one op shorter) is >= 1e-4; otherwise the pixel
+// terminates with T unchanged (SURVEY B.3 / forward.cu renderCUDA).  The exponent is
+// Horner-form: ((c' dy + b' dx) dy) + (a' dx^2 + log2 o), 3 ops per stripe with dy.
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom geo,
                                                                 const uint2* __restrict__ ranges,
@@ -213,12 +215,13 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
                 for (int p = 0; p < PPL; ++p) {
                     if (!(m & (1u << p))) continue;  // wave-uniform
                     const float dy = r0.y - pfy[p];
-                    const float e = fmaf(bdx, dy, fmaf(r1.x * dy, dy, K));
+                    const float e = fmaf(fmaf(r1.x, dy, bdx), dy, K);
                     float oG;
                     const float a = pair_alpha(e, r2.w, oG);
-                    const float tT = T[p] * (1.0f - a);
+                    const float w = a * T[p];
+                    const float tT = T[p] - w;
                     const bool ok = tT >= 0.0001f;
-                    const float wgt = ok ? a * T[p] : 0.0f;
+                    const float wgt = ok ? w : 0.0f;
                     C0[p] = fmaf(r1.z, wgt, C0[p]);
                     C1[p] = fmaf(r1.w, wgt, C1[p]);
                     C2[p] = fmaf(r2.x, wgt, C2[p]);
@@ -282,8 +285,9 @@ __device__ __forceinline__ void park_flush(const float* qpark, const uint32_t* q
 //   dL/dalpha_k = T_k (c_k . dL/dpix) - R / (1 - alpha_k),
 //   R = S . dL/dpix + T_final bg . dL/dpix - Sp
 // (SURVEY B.4 rewritten; same value as the back-to-front recursion).  A lane keeps R itself
-// (R -= w (c . dL/dpix) per contributor), one register and one op fewer than Sp and S.  T is recomputed with
-// the forward's own instructions (same alpha, same T (1 - alpha), same sign encoding), so
+// (R -= w (c . dL/dpix) per contributor), one register and one op fewer than Sp and S.  T is
+// recomputed with the forward's own instructions (same exponent, alpha, T - alpha T and sign
+// encoding), so
 // the set of contributing pairs -- and the termination point -- is exactly the forward's.
 // Per record the lane accumulates sv = o G dL/dalpha moments along its column
 // (sum sv, sum sv dy, sum sv dy^2) and applies dx afterwards:
@@ -408,15 +412,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
             for (int p = 0; p < kPPL; ++p) {
                 if (!(m & (1u << p))) continue;  // wave-uniform
                 const float dy = r0.y - pfy[p];
-                const float e = fmaf(bdx, dy, fmaf(r1.x * dy, dy, K));
+                const float e = fmaf(fmaf(r1.x, dy, bdx), dy, K);
                 float oG;
                 const float a = pair_alpha(e, r2.w, oG);
-                const float one_m = 1.0f - a;
-                const float tT = T[p] * one_m;
+                const float w = a * T[p];
+                const float tT = T[p] - w;
                 const bool ok = tT >= 0.0001f;
                 if (ok && a > 0.0f) {
                     any = true;
-                    const float w = a * T[p];
+                    const float one_m = 1.0f - a;
                     const float cdp = fmaf(r1.z, dp0[p], fmaf(r1.w, dp1[p], r2.x * dp2[p]));
                     R[p] = fmaf(-w, cdp, R[p]);
                     const float dLda = fmaf(T[p], cdp, -R[p] * __builtin_amdgcn_rcpf(one_m));
