@@ -14,6 +14,8 @@
 // Roofline: HBM-bound.  Algorithmic bytes per Gaussian: 44 B params + 12*M B SH (visible
 // only) in; radius, depth key, tiles (12 B) + 48 B record + 16 B rect out.
 // For a band (multi-GPU) only the band's candidates evaluate SH and write records.
+#include <cstdlib>
+
 #include "gsr_kernels.h"
 
 namespace gsr {
@@ -30,19 +32,56 @@ constexpr float kSH_C1 = 0.4886025119029199f;
 __device__ inline int imin(int a, int b) { return a < b ? a : b; }
 __device__ inline int imax(int a, int b) { return a > b ? a : b; }
 
-// The block's SH-rest rows (256 Gaussians x M_rest x 3 floats, contiguous in HBM) are staged
-// through LDS with coalesced dword loads: read straight from HBM, each lane's 180-B row at a
-// 180-B lane stride would touch ~90 cache lines per load instruction and thrash L1.
-// One Gaussian; returns its band-clipped tiles_touched.
-__device__ __forceinline__ uint32_t preprocess_one(const gsr_camera& cam, const GaussIn& in, int g, int grid_x,
-                                                   int grid_y, int ty0, int ty1, const PreOut& out,
-                                                   const float* sh_lds) {
-    const int M3 = in.M_rest * 3;
+// Geometry of one Gaussian (everything but its colour): radius, depth key, band-clipped
+// tiles_touched and what the blend record needs.
+struct Geo {
+    float xs, ys, cA, cB, cC, a, c;
+    int minx, miny, maxx, maxy;
+    int32_t radius;
+    uint32_t key, tiles;
+};
+
+// Per-Gaussian inputs, all loaded up front so their HBM latencies overlap (a load issued
+// only after tz > 0.2 is known would add a second round trip per wave).
+struct Params {
+    float p0, p1, p2;
+    float4 q;          // rotation (w, x, y, z), or cov3D[0..3]
+    float s0, s1, s2;  // scales, or cov3D[4..5]
+    float opac;
+    float c0, c1, c2;  // sh_dc, or precomputed colours
+};
+
+__device__ __forceinline__ Params load_params(const GaussIn& in, int g) {
+    Params P;
+    P.p0 = in.means3D[3 * g + 0];
+    P.p1 = in.means3D[3 * g + 1];
+    P.p2 = in.means3D[3 * g + 2];
+    if (in.cov3D) {
+        P.q = make_float4(in.cov3D[6 * g + 0], in.cov3D[6 * g + 1], in.cov3D[6 * g + 2], in.cov3D[6 * g + 3]);
+        P.s0 = in.cov3D[6 * g + 4];
+        P.s1 = in.cov3D[6 * g + 5];
+        P.s2 = 0.0f;
+    } else {
+        P.q = *reinterpret_cast<const float4*>(in.rots + 4 * g);
+        P.s0 = in.scales[3 * g + 0];
+        P.s1 = in.scales[3 * g + 1];
+        P.s2 = in.scales[3 * g + 2];
+    }
+    P.opac = in.opac[g];
+    const float* c = in.colors ? in.colors : in.sh_dc;
+    P.c0 = c[3 * g + 0];
+    P.c1 = c[3 * g + 1];
+    P.c2 = c[3 * g + 2];
+    return P;
+}
+
+__device__ __forceinline__ Geo preprocess_geom(const gsr_camera& cam, const GaussIn& in, const Params& I, int grid_x,
+                                               int grid_y, int ty0, int ty1) {
     const float* V = cam.viewmatrix;
     const float* Pm = cam.projmatrix;
-    const float p0 = in.means3D[3 * g + 0], p1 = in.means3D[3 * g + 1], p2 = in.means3D[3 * g + 2];
-    int32_t radius_out = 0;
-    uint32_t key_out = 0xFFFFFFFFu, tiles_out = 0;
+    const float p0 = I.p0, p1 = I.p1, p2 = I.p2;
+    Geo G{};
+    G.key = 0xFFFFFFFFu;
 
     const float tx = V[0] * p0 + V[4] * p1 + V[8] * p2 + V[12];
     const float ty = V[1] * p0 + V[5] * p1 + V[9] * p2 + V[13];
@@ -55,11 +94,14 @@ __device__ __forceinline__ uint32_t preprocess_one(const gsr_camera& cam, const 
         const float px = hx * pw, py = hy * pw;
         float c3[6];
         if (in.cov3D) {
-#pragma unroll
-            for (int k = 0; k < 6; ++k) c3[k] = in.cov3D[6 * g + k];
+            c3[0] = I.q.x;
+            c3[1] = I.q.y;
+            c3[2] = I.q.z;
+            c3[3] = I.q.w;
+            c3[4] = I.s0;
+            c3[5] = I.s1;
         } else {
-            const float4 q = *reinterpret_cast<const float4*>(in.rots + 4 * g);
-            const float r = q.x, x = q.y, y = q.z, z = q.w;
+            const float r = I.q.x, x = I.q.y, y = I.q.z, z = I.q.w;
             float R[9];
             R[0] = 1.f - 2.f * (y * y + z * z);
             R[1] = 2.f * (x * y - r * z);
@@ -70,9 +112,9 @@ __device__ __forceinline__ uint32_t preprocess_one(const gsr_camera& cam, const 
             R[6] = 2.f * (x * z - r * y);
             R[7] = 2.f * (y * z + r * x);
             R[8] = 1.f - 2.f * (x * x + y * y);
-            const float sx = in.smod * in.scales[3 * g + 0];
-            const float sy = in.smod * in.scales[3 * g + 1];
-            const float sz = in.smod * in.scales[3 * g + 2];
+            const float sx = in.smod * I.s0;
+            const float sy = in.smod * I.s1;
+            const float sz = in.smod * I.s2;
             float L[9];
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
@@ -134,111 +176,192 @@ __device__ __forceinline__ uint32_t preprocess_one(const gsr_camera& cam, const 
             const int by0 = imax(miny, ty0), by1 = imin(maxy, ty1);
             const int band_rows = by1 > by0 ? by1 - by0 : 0;
             if ((maxx - minx) * (maxy - miny) != 0) {
-                radius_out = radius;
-                key_out = __float_as_uint(tz);
-                tiles_out = (uint32_t)((maxx - minx) * band_rows);
+                G.radius = radius;
+                G.key = __float_as_uint(tz);
+                G.tiles = (uint32_t)((maxx - minx) * band_rows);
             }
-            // colour and blend record only for Gaussians this band blends (all visible ones
-            // for a full image); B2 recomputes the clamp bits itself
-            if (tiles_out != 0) {
-                float rgb[3];
-                uint32_t clamped = 0;
-                if (in.colors) {
-                    rgb[0] = in.colors[3 * g + 0];
-                    rgb[1] = in.colors[3 * g + 1];
-                    rgb[2] = in.colors[3 * g + 2];
-                } else {
-                    const float dx = p0 - cam.campos[0], dy = p1 - cam.campos[1], dz = p2 - cam.campos[2];
-                    const float len = sqrtf(dx * dx + dy * dy + dz * dz);
-                    const float x = dx / len, y = dy / len, z = dz / len;
-                    float basis[16];
-                    const int D = in.D;
-                    basis[0] = kSH_C0;
-                    if (D >= 1) {
-                        basis[1] = -kSH_C1 * y;
-                        basis[2] = kSH_C1 * z;
-                        basis[3] = -kSH_C1 * x;
-                    }
-                    if (D >= 2) {
-                        const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-                        basis[4] = kSH_C2[0] * xy;
-                        basis[5] = kSH_C2[1] * yz;
-                        basis[6] = kSH_C2[2] * (2.0f * zz - xx - yy);
-                        basis[7] = kSH_C2[3] * xz;
-                        basis[8] = kSH_C2[4] * (xx - yy);
-                        if (D >= 3) {
-                            basis[9] = kSH_C3[0] * y * (3.0f * xx - yy);
-                            basis[10] = kSH_C3[1] * xy * z;
-                            basis[11] = kSH_C3[2] * y * (4.0f * zz - xx - yy);
-                            basis[12] = kSH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy);
-                            basis[13] = kSH_C3[4] * x * (4.0f * zz - xx - yy);
-                            basis[14] = kSH_C3[5] * z * (xx - yy);
-                            basis[15] = kSH_C3[6] * x * (xx - 3.0f * yy);
-                        }
-                    }
-                    const int nb = (D + 1) * (D + 1);
-                    // LDS-staged row (full image) or this Gaussian's own row in HBM (band:
-                    // only ~1/N of the rows are needed, so the block does not stage)
-                    const float* rest = sh_lds ? sh_lds + threadIdx.x * M3 : in.sh_rest + (size_t)g * M3;
-#pragma unroll
-                    for (int ch = 0; ch < 3; ++ch) {
-                        float r = basis[0] * in.sh_dc[3 * g + ch];
-#pragma unroll
-                        for (int k = 1; k < 16; ++k)
-                            if (k < nb) r = r + basis[k] * rest[3 * (k - 1) + ch];
-                        r = r + 0.5f;
-                        clamped |= (r < 0.0f ? 1u : 0u) << ch;
-                        rgb[ch] = fmaxf(r, 0.0f);
-                    }
-                }
-                // Blend record (SURVEY B.3 power with -0.5 and log2(e) folded in, so the blend
-                // evaluates exp2 directly; log2(o) rides along so o * G is one exp2) + the
-                // half-extents of the alpha >= 1/255 footprint:
-                // d^T Q d <= t, t = 2 ln(255 o)  =>  |dx| <= sqrt(t a), |dy| <= sqrt(t c),
-                // padded (x1.02 + 0.5 px) so the per-stripe cull never drops a contributing pixel.
-                const float opac = in.opac[g];
-                const float kL2E = 1.4426950408889634f;
-                const float tthr = 2.0f * logf(255.0f * opac);
-                const float ex = tthr > 0.0f ? sqrtf(tthr * a) * 1.02f + 0.5f : -1.0f;
-                const float ey = tthr > 0.0f ? sqrtf(tthr * c) * 1.02f + 0.5f : -1.0f;
-                float4* rec = out.rec + 3 * (size_t)g;
-                rec[0] = make_float4(xs, ys, -0.5f * kL2E * cA, -kL2E * cB);
-                rec[1] = make_float4(-0.5f * kL2E * cC, opac, rgb[0], rgb[1]);
-                rec[2] = make_float4(rgb[2], ex, ey, log2f(opac));
-                out.rect[g] = make_uint4((uint32_t)minx | ((uint32_t)miny << 16),
-                                         (uint32_t)maxx | ((uint32_t)maxy << 16), 0u, 0u);
-                if (out.flags) out.flags[g] = clamped;
-            }
+            G.xs = xs;
+            G.ys = ys;
+            G.cA = cA;
+            G.cB = cB;
+            G.cC = cC;
+            G.a = a;
+            G.c = c;
+            G.minx = minx;
+            G.miny = miny;
+            G.maxx = maxx;
+            G.maxy = maxy;
         }
     }
-    out.radii[g] = radius_out;
-    out.depth_key[g] = key_out;
-    out.tiles[g] = tiles_out;
-    return tiles_out;
+    return G;
 }
 
-// The block's SH-rest rows are staged through LDS (see above).  The block also adds its
-// candidate count (Gaussians with tiles in the band) and instance count (sum of
-// tiles_touched) into counters[slot] / counters[kCountSlots + slot], so the host can read K
-// right after this kernel -- while the depth sort runs -- instead of after the scan.
-__global__ __launch_bounds__(256) void preprocess_kernel(const gsr_camera cam, const GaussIn in,
+// Real SH basis (degree <= 3) of the unit view direction of Gaussian g.
+__device__ __forceinline__ void sh_basis(const gsr_camera& cam, const GaussIn& in, const Params& I,
+                                         float (&basis)[16]) {
+    const float dx = I.p0 - cam.campos[0], dy = I.p1 - cam.campos[1], dz = I.p2 - cam.campos[2];
+    const float len = sqrtf(dx * dx + dy * dy + dz * dz);
+    const float x = dx / len, y = dy / len, z = dz / len;
+    const int D = in.D;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) basis[k] = 0.0f;
+    basis[0] = kSH_C0;
+    if (D >= 1) {
+        basis[1] = -kSH_C1 * y;
+        basis[2] = kSH_C1 * z;
+        basis[3] = -kSH_C1 * x;
+    }
+    if (D >= 2) {
+        const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+        basis[4] = kSH_C2[0] * xy;
+        basis[5] = kSH_C2[1] * yz;
+        basis[6] = kSH_C2[2] * (2.0f * zz - xx - yy);
+        basis[7] = kSH_C2[3] * xz;
+        basis[8] = kSH_C2[4] * (xx - yy);
+        if (D >= 3) {
+            basis[9] = kSH_C3[0] * y * (3.0f * xx - yy);
+            basis[10] = kSH_C3[1] * xy * z;
+            basis[11] = kSH_C3[2] * y * (4.0f * zz - xx - yy);
+            basis[12] = kSH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy);
+            basis[13] = kSH_C3[4] * x * (4.0f * zz - xx - yy);
+            basis[14] = kSH_C3[5] * z * (xx - yy);
+            basis[15] = kSH_C3[6] * x * (xx - 3.0f * yy);
+        }
+    }
+}
+
+// Blend record (SURVEY B.3 power with -0.5 and log2(e) folded in, so the blend evaluates exp2
+// directly; log2(o) rides along so o * G is one exp2) + the half-extents of the alpha >= 1/255
+// footprint: d^T Q d <= t, t = 2 ln(255 o)  =>  |dx| <= sqrt(t a), |dy| <= sqrt(t c), padded
+// (x1.02 + 0.5 px) so the per-stripe cull never drops a contributing pixel.
+__device__ __forceinline__ void write_record(int g, float opac, const Geo& G, const float (&rgb)[3],
+                                             uint32_t clamped, const PreOut& out) {
+    const float kL2E = 1.4426950408889634f;
+    const float tthr = 2.0f * logf(255.0f * opac);
+    const float ex = tthr > 0.0f ? sqrtf(tthr * G.a) * 1.02f + 0.5f : -1.0f;
+    const float ey = tthr > 0.0f ? sqrtf(tthr * G.c) * 1.02f + 0.5f : -1.0f;
+    float4* rec = out.rec + 3 * (size_t)g;
+    rec[0] = make_float4(G.xs, G.ys, -0.5f * kL2E * G.cA, -kL2E * G.cB);
+    rec[1] = make_float4(-0.5f * kL2E * G.cC, opac, rgb[0], rgb[1]);
+    rec[2] = make_float4(rgb[2], ex, ey, log2f(opac));
+    out.rect[g] = make_uint4((uint32_t)G.minx | ((uint32_t)G.miny << 16), (uint32_t)G.maxx | ((uint32_t)G.maxy << 16),
+                             0u, 0u);
+    if (out.flags) out.flags[g] = clamped;
+}
+
+// SH rows (M_rest x 3 floats per Gaussian, contiguous) reach the lanes in one of three ways:
+//  kShDirect : each lane reads its own row from HBM (bands: only ~1/N of the rows are needed);
+//  kShChunks : the block stages 5-coefficient column chunks (15 floats per row, 15 KB of LDS)
+//              and accumulates the colour chunk by chunk in the same k order (bit-identical
+//              to one pass), with 8 waves per SIMD.
+// Measured at 1M/SH3 (scripts/ablate.py GSR_PRE_VARIANT): direct 0.53 ms -- each lane's
+// 180-B row at a 180-B lane stride touches ~90 cache lines per load instruction; whole rows
+// staged in LDS (46 KB, 3 waves per SIMD) 0.106 ms; chunks 0.082 ms.
+enum { kShDirect = 0, kShChunks = 2 };
+constexpr int kChunkK = 5;               // SH coefficients per staged chunk
+constexpr int kChunkF = 3 * kChunkK;     // floats per row per chunk
+
+// The block also adds its candidate count (Gaussians with tiles in the band) and instance
+// count (sum of tiles_touched) into counters[slot] / counters[kCountSlots + slot], so the host
+// can read K right after this kernel -- while the depth sort runs -- instead of after the scan.
+template <int SH>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void preprocess_kernel(const gsr_camera cam, const GaussIn in,
                                                          int grid_x, int grid_y, int ty0, int ty1,
                                                          PreOut out) {
     extern __shared__ __attribute__((aligned(16))) float sh_lds[];
     __shared__ uint32_t wk[4], wc[4];
     const int g = blockIdx.x * 256 + threadIdx.x;
     const int M3 = in.M_rest * 3;
-    const bool band = ty0 > 0 || ty1 < grid_y;
-    const bool stage = in.sh_rest && !in.colors && in.D > 0 && !band;  // grid-uniform
-    if (stage) {
-        const size_t base = (size_t)blockIdx.x * 256 * M3;
-        const int rows = in.P - blockIdx.x * 256 < 256 ? in.P - blockIdx.x * 256 : 256;
-        const int cnt = rows * M3;
-        for (int i = threadIdx.x; i < cnt; i += 256) sh_lds[i] = in.sh_rest[base + i];
-        __syncthreads();
+    const int rows = in.P - blockIdx.x * 256 < 256 ? in.P - blockIdx.x * 256 : 256;
+    const bool sh = in.sh_rest && !in.colors && in.D > 0;  // grid-uniform
+    // kShChunks: lane (r0, col) moves column f0 + col of rows r0, r0 + 16, ...; chunk c + 1 is
+    // loaded into registers while chunk c is consumed, and chunk 0 while the geometry runs.
+    const int col = threadIdx.x & 15, r0 = threadIdx.x >> 4;
+    const size_t base = (size_t)blockIdx.x * 256 * M3;
+    const int nb = (in.D + 1) * (in.D + 1);
+    // Buffer loads over the block's rows: one 32-bit lane offset, the row step in the scalar
+    // offset, and the descriptor's range check zero-fills rows past the end of the array.
+    float pre[16];
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in.sh_rest + base), 0,
+                                                        rows * M3 * (int)sizeof(float), 0x00020000);
+    auto load_chunk = [&](int c) {
+        const int voff = (r0 * M3 + kChunkF * c + col) * (int)sizeof(float);
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            pre[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                   rsrc, voff, j * 16 * M3 * (int)sizeof(float), 0));
+    };
+    Params I{};
+    if (g < in.P) I = load_params(in, g);
+    if (SH == kShChunks && sh) load_chunk(0);
+    Geo G{};
+    G.key = 0xFFFFFFFFu;
+    if (g < in.P) {
+        G = preprocess_geom(cam, in, I, grid_x, grid_y, ty0, ty1);
+        out.radii[g] = G.radius;
+        out.depth_key[g] = G.key;
+        out.tiles[g] = G.tiles;
     }
-    const uint32_t t = g < in.P ? preprocess_one(cam, in, g, grid_x, grid_y, ty0, ty1, out, stage ? sh_lds : nullptr)
-                                : 0u;
+    const bool need = G.tiles != 0;  // colour and record only for Gaussians this band blends
+    float rgb[3] = {0.f, 0.f, 0.f}, basis[16];
+    if (need) {
+        rgb[0] = I.c0;
+        rgb[1] = I.c1;
+        rgb[2] = I.c2;
+        if (!in.colors) {
+            sh_basis(cam, in, I, basis);
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) rgb[ch] = basis[0] * rgb[ch];
+        }
+    }
+    if (sh) {
+        if (SH == kShChunks) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {  // k = 1 + 5c .. 5 + 5c; SH degree <= 3 => k < 16
+                const int k0 = 1 + kChunkK * c;
+                if (k0 >= nb) break;  // grid-uniform
+                if (c > 0) __syncthreads();  // the previous chunk has been consumed
+                if (col < kChunkF)
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) sh_lds[(r0 + 16 * j) * kChunkF + col] = pre[j];
+                if (c < 2 && k0 + kChunkK < nb) load_chunk(c + 1);
+                __syncthreads();
+                if (need) {
+                    const float* rest = sh_lds + threadIdx.x * kChunkF;
+#pragma unroll
+                    for (int kk = 0; kk < kChunkK; ++kk) {
+                        const int k = k0 + kk;
+                        if (k < nb)
+#pragma unroll
+                            for (int ch = 0; ch < 3; ++ch) rgb[ch] = rgb[ch] + basis[k] * rest[3 * kk + ch];
+                    }
+                }
+            }
+        } else if (need) {
+            const float* rest = in.sh_rest + (size_t)g * M3;
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) {
+                float r = rgb[ch];
+#pragma unroll
+                for (int k = 1; k < 16; ++k)
+                    if (k < nb) r = r + basis[k] * rest[3 * (k - 1) + ch];
+                rgb[ch] = r;
+            }
+        }
+    }
+    if (need) {
+        uint32_t clamped = 0;
+        if (!in.colors) {
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) {
+                const float r = rgb[ch] + 0.5f;
+                clamped |= (r < 0.0f ? 1u : 0u) << ch;
+                rgb[ch] = fmaxf(r, 0.0f);
+            }
+        }
+        write_record(g, I.opac, G, rgb, clamped, out);
+    }
+    const uint32_t t = G.tiles;
     if (out.counters) {
         uint32_t k = t, c = t ? 1u : 0u;
 #pragma unroll
@@ -266,10 +389,16 @@ int launch_preprocess(const gsr_camera& cam, const GaussIn& in, int ty0, int ty1
                       hipStream_t s) {
     if (in.P <= 0) return 0;
     const int gx = div_up(cam.width, kTile), gy = div_up(cam.height, kTile);
-    const bool band = ty0 > 0 || ty1 < gy;  // a band reads SH rows directly (see preprocess_kernel)
-    const size_t lds = (in.sh_rest && !in.colors && in.D > 0 && !band) ? sizeof(float) * 256 * 3 * in.M_rest : 0;
-    hipLaunchKernelGGL(preprocess_kernel, dim3(div_up(in.P, 256)), dim3(256), lds, s, cam, in, gx, gy,
-                       ty0, ty1, out);
+    const bool band = ty0 > 0 || ty1 < gy;  // a band reads SH rows directly
+    const bool sh = in.sh_rest && !in.colors && in.D > 0;
+    const char* v = std::getenv("GSR_PRE_VARIANT");
+    const int mode = !sh || band ? kShDirect : v ? std::atoi(v) : kShChunks;
+    const dim3 grid(div_up(in.P, 256)), block(256);
+    if (mode == kShChunks)
+        hipLaunchKernelGGL(preprocess_kernel<kShChunks>, grid, block, sizeof(float) * 256 * kChunkF, s, cam, in, gx,
+                           gy, ty0, ty1, out);
+    else
+        hipLaunchKernelGGL(preprocess_kernel<kShDirect>, grid, block, 0, s, cam, in, gx, gy, ty0, ty1, out);
     return (int)hipGetLastError();
 }
 
