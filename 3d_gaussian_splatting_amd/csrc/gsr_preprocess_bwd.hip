@@ -50,6 +50,13 @@ __global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __re
     const uint32_t J0 = r0 ? offsets[r0 - 1] : 0u, J1 = offsets[rl - 1];
     const uint32_t s = r < P ? (r ? offsets[r - 1] : 0u) : 0u;
     const uint32_t e = r < P ? offsets[r] : 0u;
+    // the Gaussian's conic and opacity, loaded before the window loop (latency overlaps it)
+    const uint32_t g = r < P ? gid_by_rank[r] : 0u;
+    float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0;
+    if (r < P) {
+        q0 = rec[3 * (size_t)g];
+        q1 = rec[3 * (size_t)g + 1];
+    }
     float a[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) a[k] = 0.f;
@@ -68,9 +75,7 @@ __global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __re
         __syncthreads();
     }
     if (r >= P) return;
-    const uint32_t g = gid_by_rank[r];
     // moments -> d mean2D (NDC), d conic, d opacity (sum G dL/dalpha = S0 / o), d colour
-    const float4 q0 = rec[3 * (size_t)g], q1 = rec[3 * (size_t)g + 1];
     const float A = -2.0f * kLn2 * q0.z, B = -kLn2 * q0.w, C = -2.0f * kLn2 * q1.x;
     const float Sx = a[0], Sy = a[1], S0 = a[5];
     float4* dst = reinterpret_cast<float4*>(grad2d + (size_t)kPart * g);
@@ -79,27 +84,55 @@ __global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __re
     dst[2] = make_float4(a[8], 0.f, 0.f, 0.f);
 }
 
+// Per-Gaussian inputs of B2, loaded before the SH rows are staged so that their HBM
+// latency overlaps the staging instead of following it.
+struct BwdIn {
+    bool visible;
+    float g2[9];
+    float p0, p1, p2;
+    float c3[6];  // cov3D, or (rotation w, x, y, z, unused x2)
+    float s[3];   // raw scales
+    uint32_t cl;  // stored SH clamp bits (flags != nullptr)
+};
+
+__device__ __forceinline__ BwdIn load_bwd_in(const GaussIn& in, int g, int o, const uint32_t* __restrict__ depth_key,
+                                             const uint32_t* __restrict__ flags,
+                                             const float* __restrict__ grad2d) {
+    BwdIn b;
+    b.visible = depth_key[g] != 0xFFFFFFFFu;
+    const float4* src = reinterpret_cast<const float4*>(grad2d + (size_t)kPart * o);
+    const float4 v0 = src[0], v1 = src[1], v2 = src[2];
+    b.g2[0] = v0.x; b.g2[1] = v0.y; b.g2[2] = v0.z; b.g2[3] = v0.w;
+    b.g2[4] = v1.x; b.g2[5] = v1.y; b.g2[6] = v1.z; b.g2[7] = v1.w;
+    b.g2[8] = v2.x;
+    b.p0 = in.means3D[3 * g + 0];
+    b.p1 = in.means3D[3 * g + 1];
+    b.p2 = in.means3D[3 * g + 2];
+    if (in.cov3D) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) b.c3[k] = in.cov3D[6 * g + k];
+        b.s[0] = b.s[1] = b.s[2] = 0.f;
+    } else {
+        const float4 q = *reinterpret_cast<const float4*>(in.rots + 4 * g);
+        b.c3[0] = q.x; b.c3[1] = q.y; b.c3[2] = q.z; b.c3[3] = q.w; b.c3[4] = b.c3[5] = 0.f;
+        b.s[0] = in.scales[3 * g + 0];
+        b.s[1] = in.scales[3 * g + 1];
+        b.s[2] = in.scales[3 * g + 2];
+    }
+    b.cl = flags ? flags[g] : 0u;
+    return b;
+}
+
 // One Gaussian's chain rule.  `lrest`: this thread's SH-rest row staged in LDS (read, then
 // overwritten in place with the row's gradient), or nullptr when there is no SH-rest input.
-__device__ void preprocess_backward_one(const gsr_camera& cam, const GaussIn& in, int g, int o,
-                                        const uint32_t* __restrict__ depth_key,
-                                        const uint32_t* __restrict__ flags,
-                                        const float* __restrict__ grad2d, const GradOut& out,
-                                        float* lrest) {
-    const bool visible = depth_key[g] != 0xFFFFFFFFu;
+__device__ __forceinline__ void preprocess_backward_one(const gsr_camera& cam, const GaussIn& in, int g, int o,
+                                                        const BwdIn& bi, const uint32_t* __restrict__ flags,
+                                                        const GradOut& out, float* lrest) {
+    const bool visible = bi.visible;
     // ---- 2D gradients ----
     float g2[9];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) g2[k] = 0.f;
-    if (visible) {
-        {
-            const float4* src = reinterpret_cast<const float4*>(grad2d + (size_t)kPart * o);
-            const float4 v0 = src[0], v1 = src[1], v2 = src[2];
-            g2[0] = v0.x; g2[1] = v0.y; g2[2] = v0.z; g2[3] = v0.w;
-            g2[4] = v1.x; g2[5] = v1.y; g2[6] = v1.z; g2[7] = v1.w;
-            g2[8] = v2.x;
-        }
-    }
+    for (int k = 0; k < 9; ++k) g2[k] = visible ? bi.g2[k] : 0.f;
     out.means2D[3 * o + 0] = g2[0];
     out.means2D[3 * o + 1] = g2[1];
     out.means2D[3 * o + 2] = 0.f;
@@ -112,7 +145,7 @@ __device__ void preprocess_backward_one(const gsr_camera& cam, const GaussIn& in
 
     const float* V = cam.viewmatrix;
     const float* Pm = cam.projmatrix;
-    const float p0 = in.means3D[3 * g + 0], p1 = in.means3D[3 * g + 1], p2 = in.means3D[3 * g + 2];
+    const float p0 = bi.p0, p1 = bi.p1, p2 = bi.p2;
     const float p[3] = {p0, p1, p2};
     float dm[3] = {0.f, 0.f, 0.f};
     const int D = in.D;
@@ -194,7 +227,7 @@ __device__ void preprocess_backward_one(const gsr_camera& cam, const GaussIn& in
         // Gaussians outside its band, which B2 on this rank's slice may still need.
         uint32_t cl = 0;
         if (flags) {
-            cl = flags[g];
+            cl = bi.cl;
         } else {
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) {
@@ -256,9 +289,9 @@ __device__ void preprocess_backward_one(const gsr_camera& cam, const GaussIn& in
     float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
     if (in.cov3D) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) c3[k] = in.cov3D[6 * g + k];
+        for (int k = 0; k < 6; ++k) c3[k] = bi.c3[k];
     } else {
-        q = *reinterpret_cast<const float4*>(in.rots + 4 * g);
+        q = make_float4(bi.c3[0], bi.c3[1], bi.c3[2], bi.c3[3]);
         const float r = q.x, x = q.y, y = q.z, z = q.w;
         R[0] = 1.f - 2.f * (y * y + z * z);
         R[1] = 2.f * (x * y - r * z);
@@ -269,9 +302,9 @@ __device__ void preprocess_backward_one(const gsr_camera& cam, const GaussIn& in
         R[6] = 2.f * (x * z - r * y);
         R[7] = 2.f * (y * z + r * x);
         R[8] = 1.f - 2.f * (x * x + y * y);
-        se[0] = in.smod * in.scales[3 * g + 0];
-        se[1] = in.smod * in.scales[3 * g + 1];
-        se[2] = in.smod * in.scales[3 * g + 2];
+        se[0] = in.smod * bi.s[0];
+        se[1] = in.smod * bi.s[1];
+        se[2] = in.smod * bi.s[2];
         float L[9];
 #pragma unroll
         for (int i = 0; i < 3; ++i)
@@ -388,13 +421,13 @@ __global__ __launch_bounds__(256) void preprocess_backward_kernel(
     const bool stage = in.sh_rest != nullptr && !in.colors;  // block-uniform
     const int rows = n - blockIdx.x * 256 < 256 ? n - blockIdx.x * 256 : 256;
     const size_t obase = (size_t)blockIdx.x * 256 * M3, ibase = (size_t)g0 * M3 + obase;
+    BwdIn bi{};
+    if (o < n) bi = load_bwd_in(in, g0 + o, o, depth_key, flags, grad2d);
     if (stage) {  // coalesced staging of the block's SH-rest rows (see preprocess_kernel)
         for (int i = threadIdx.x; i < rows * M3; i += 256) sh_lds[i] = in.sh_rest[ibase + i];
         __syncthreads();
     }
-    if (o < n)
-        preprocess_backward_one(cam, in, g0 + o, o, depth_key, flags, grad2d, out,
-                                stage ? sh_lds + threadIdx.x * M3 : nullptr);
+    if (o < n) preprocess_backward_one(cam, in, g0 + o, o, bi, flags, out, stage ? sh_lds + threadIdx.x * M3 : nullptr);
     if (stage) {  // coalesced write-back of the SH-rest gradient rows
         __syncthreads();
         for (int i = threadIdx.x; i < rows * M3; i += 256) out.sh_rest[obase + i] = sh_lds[i];
