@@ -343,6 +343,9 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
             NR = (int)cnt[0];
             sort_keys = offsets;  // free until the scan
             sort_vals = cand_tmp;
+            if (colour_pass_needed(*cam, gauss_in(gs), ty0, ty1))
+                GSR_STAGE(GSR_STAGE_PREPROCESS, launch_colour(*cam, gauss_in(gs), cand_tmp, NR, rec, stream),
+                          "band colours");
         }
         bufs->num_ranked = NR;
         int which = NR > 0 ? -1 : 1;

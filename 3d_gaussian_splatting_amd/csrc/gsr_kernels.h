@@ -27,6 +27,11 @@ struct PreOut {
 // F1: projection, EWA cov2D, conic, radius, tile rect, SH->RGB (bit-exact vs the oracle)
 int launch_preprocess(const gsr_camera& cam, const GaussIn& in, int ty0, int ty1, const PreOut& out,
                       hipStream_t s);
+// A band's F1 leaves the record colours zero when they come from SH (only ~1/N of the rows
+// are needed); launch_colour fills them for the band's compacted candidates `cand`.
+bool colour_pass_needed(const gsr_camera& cam, const GaussIn& in, int ty0, int ty1);
+int launch_colour(const gsr_camera& cam, const GaussIn& in, const uint32_t* cand, int n, float4* rec,
+                  hipStream_t s);
 
 // LSD radix sort of (u32 key, u32 value) by key bits [0, nbits); vals_in == nullptr means the
 // identity permutation.  Ping-pongs between (k0,v0) and (k1,v1); returns in *which (0/1) where
