@@ -301,7 +301,7 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
     uint2* ranges = at<uint2>(bufs->image, il.ranges);
     float* final_T = at<float>(bufs->image, il.final_T);
 
-    if (ty0 > 0 || ty1 < gy) {
+    if ((ty0 > 0 || ty1 < gy) && !(rs->flags & GSR_FLAG_BAND_ONLY)) {
         const int npix = W * H;
         hipLaunchKernelGGL(fill_background, dim3(div_up(npix, 256)), dim3(256), 0, stream, out_color,
                            final_T, at<float>(bufs->image, il.accum), npix, rs->bg[0], rs->bg[1],
@@ -420,10 +420,10 @@ static const uint32_t* stored_flags(const gsr_camera* cam, const gsr_raster_sett
 
 // Per-Gaussian grad2d for all P: the gather covers the ranked Gaussians (a band's candidates);
 // the rest touched no tile of the band and get zeros.
-static int gather_all(const gsr_camera* cam, const Views& v, const gsr_buffers* bufs, const float* partial,
-                      long long K, int P, float* grad2d, hipStream_t stream) {
+static int gather_all(const gsr_camera* cam, const gsr_raster_settings* rs, const Views& v, const gsr_buffers* bufs,
+                      const float* partial, long long K, int P, float* grad2d, hipStream_t stream) {
     const int NR = bufs->num_ranked > 0 ? bufs->num_ranked : P;
-    if (NR < P) {
+    if (NR < P && !(rs->flags & GSR_FLAG_BAND_ONLY)) {
         if (hipError_t e = hipMemsetAsync(grad2d, 0, sizeof(float) * kPart * (size_t)P, stream)) return (int)e;
     }
     return launch_gather_grad2d(v.gid_by_rank, v.offsets, partial, v.rec, cam->width, cam->height, K, NR, grad2d,
@@ -454,7 +454,7 @@ static int backward_impl(const gsr_camera* cam, const gsr_gaussians* gs, const g
     }
     if (grad2d) {
         if (K > 0) {
-            GSR_STAGE(GSR_STAGE_GATHER, gather_all(cam, v, bufs, partial, K, P, grad2d, stream), "gather grad2d");
+            GSR_STAGE(GSR_STAGE_GATHER, gather_all(cam, rs, v, bufs, partial, K, P, grad2d, stream), "gather grad2d");
         } else {
             GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(grad2d, 0, sizeof(float) * kPart * (size_t)P, stream), "zero grad2d");
         }
@@ -511,7 +511,7 @@ int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raste
         GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.rect, v.rec,
                                             v.final_T, v.accum, dL_dpix, partial, K, v.ck, stream),
                       "blend backward");
-        GSR_STAGE(GSR_STAGE_GATHER, gather_all(cam, v, bufs, partial, K, P, grad2d, stream),
+        GSR_STAGE(GSR_STAGE_GATHER, gather_all(cam, rs, v, bufs, partial, K, P, grad2d, stream),
                   "gather grad2d");
     } else {
         GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(grad2d, 0, sizeof(float) * kPart * (size_t)P, stream), "zero grad2d");

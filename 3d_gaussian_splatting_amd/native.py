@@ -19,6 +19,7 @@ LIB_DIR = os.path.join(PKG, "lib")
 HIP_LIB = os.path.join(LIB_DIR, "libgsr_hip.so")
 
 GSR_FLAG_DEBUG = 1
+GSR_FLAG_BAND_ONLY = 2
 GSR_GRAD2D_STRIDE = 12
 VIEW_SORTED_GID, VIEW_SORTED_TILE, VIEW_RANGES, VIEW_FINAL_T, VIEW_N_CONTRIB, VIEW_DEPTH_KEY, \
     VIEW_TILES_TOUCHED, VIEW_RECORDS, VIEW_GID_BY_RANK = range(1, 10)

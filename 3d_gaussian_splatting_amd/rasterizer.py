@@ -100,7 +100,7 @@ class CAbiRasterizer:
 
     def forward(self, cam: RasterCamera, means3D, opacities, scales=None, rotations=None, sh_dc=None,
                 sh_rest=None, sh_degree=0, colors_precomp=None, cov3D_precomp=None, scale_modifier=1.0,
-                bg=(0.0, 0.0, 0.0), tile_rows=None, debug=False) -> ForwardState:
+                bg=(0.0, 0.0, 0.0), tile_rows=None, band_only=False, debug=False) -> ForwardState:
         dev = self.device
         means3D = _f32(means3D, device=dev)
         P = int(means3D.shape[0])
@@ -124,7 +124,7 @@ class CAbiRasterizer:
         s = native.Settings()
         s.bg[:] = [float(v) for v in bg]
         s.tile_y0, s.tile_y1 = (0, INT32_MAX) if tile_rows is None else (int(tile_rows[0]), int(tile_rows[1]))
-        s.flags = native.GSR_FLAG_DEBUG if debug else 0
+        s.flags = (native.GSR_FLAG_DEBUG if debug else 0) | (native.GSR_FLAG_BAND_ONLY if band_only else 0)
         color = torch.empty((3, cam.height, cam.width), dtype=torch.float32, device=dev)
         radii = torch.empty((P,), dtype=torch.int32, device=dev)
         ag, ab, ai = _Allocator(dev), _Allocator(dev), _Allocator(dev)

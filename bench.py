@@ -130,7 +130,7 @@ def main():
         g0, g1 = bands.gaussian_slice(P, world, rank)
 
     def step():
-        st = rast.forward(cam, **inputs, sh_degree=D, tile_rows=band)
+        st = rast.forward(cam, **inputs, sh_degree=D, tile_rows=band, band_only=world > 1)
         if world > 1:
             img = bands.ImageGather(st.color, band, gy, dist)  # overlaps the blend backward
             g2 = rast.backward_blend(st, dpix)

@@ -50,6 +50,9 @@ extern "C" {
 
 /* flags */
 #define GSR_FLAG_DEBUG 1u /* synchronise + check after every stage */
+#define GSR_FLAG_BAND_ONLY 2u /* band forward/backward_blend for multi-GPU: leave pixels outside
+                                 the band and grad2d rows of Gaussians outside the band's
+                                 ranking unwritten (only those rows are exchanged) */
 
 typedef struct gsr_camera {
     int32_t width, height;
@@ -112,7 +115,8 @@ int gsr_abi_version(void);
 const char* gsr_last_error(void);
 
 /* Forward: out_color (3 x H x W, channel-major) and radii (P, int32; 0 = culled).
- * Pixels outside the tile band are set to the background.  Fills *bufs. */
+ * Pixels outside the tile band are set to the background (left unwritten under
+ * GSR_FLAG_BAND_ONLY).  Fills *bufs. */
 int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
                 float* out_color, int32_t* radii, gsr_alloc_fn alloc_geom,
                 gsr_alloc_fn alloc_binning, gsr_alloc_fn alloc_image, void* alloc_ctx,
@@ -127,7 +131,8 @@ int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raste
 
 /* B1 only: per-Gaussian 2D gradients into grad2d (P x GSR_GRAD2D_STRIDE floats:
  * mean2D.x, mean2D.y, conic A, B, C, opacity, r, g, b, 0, 0, 0). Summable across
- * tile bands (all-reduce) before gsr_backward_preprocess. */
+ * tile bands (all-reduce) before gsr_backward_preprocess.  A band writes zeros for the
+ * Gaussians outside its ranking (GSR_VIEW_GID_BY_RANK), or nothing under GSR_FLAG_BAND_ONLY. */
 int gsr_backward_blend(const gsr_camera* cam, const gsr_gaussians* gs,
                        const gsr_raster_settings* rs, const gsr_buffers* bufs,
                        const float* dL_dout_color, gsr_alloc_fn alloc_scratch, void* alloc_ctx,

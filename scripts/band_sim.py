@@ -46,7 +46,7 @@ def main():
     g0, g1 = bands.gaussian_slice(P, args.world, args.rank)
 
     def step():
-        st = rast.forward(cam, **inputs, sh_degree=D, tile_rows=band)
+        st = rast.forward(cam, **inputs, sh_degree=D, tile_rows=band, band_only=True)
         g2 = rast.backward_blend(st, dpix)
         return st, rast.backward_preprocess_range(st, g0, g1, g2[g0:g1])
 

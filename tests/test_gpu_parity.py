@@ -139,6 +139,29 @@ def test_band_sharded_equals_full(rast):
         assert rel_l2(_np(g[k]), _np(g_full[k])) <= 1e-5, k
 
 
+def test_band_only_flag(rast):
+    """GSR_FLAG_BAND_ONLY (the multi-GPU path) leaves out-of-band pixels and non-candidate
+    grad2d rows unwritten; the band rows and candidate rows equal the default run's."""
+    gr, sc, native = pkg("graphics"), pkg("scene"), pkg("native")
+    cam = gr.synthetic_camera(320, 240)
+    s = sc.make_scene(cam, 8000, max_sh_degree=3, seed=6)
+    dpix = sc.make_dL_dpix(cam, seed=7)
+    args = (cam, s.means3D, s.opacities, s.scales, s.rotations, s.sh_dc, s.sh_rest)
+    y0, y1 = 5, 10
+    ref = rast.forward(*args, sh_degree=3, tile_rows=(y0, y1))
+    g_ref = rast.backward_blend(ref, dpix)
+    st = rast.forward(*args, sh_degree=3, tile_rows=(y0, y1), band_only=True)
+    assert torch.equal(st.color[:, y0 * 16:y1 * 16], ref.color[:, y0 * 16:y1 * 16])
+    out = torch.full_like(g_ref, float("nan"))
+    g2 = rast.backward_blend(st, dpix, out=out)
+    cand = st.view(native.VIEW_GID_BY_RANK, torch.int32, st.buffers.num_ranked).long()
+    assert torch.equal(g2[cand], g_ref[cand])
+    rest = torch.ones(s.P, dtype=torch.bool, device=g2.device)
+    rest[cand] = False
+    assert bool(torch.isnan(g2[rest]).all())  # untouched
+    assert float(g_ref[rest].abs().max()) == 0.0
+
+
 def test_empty_and_culled(rast):
     gr, sc = pkg("graphics"), pkg("scene")
     cam = gr.synthetic_camera(64, 48)
