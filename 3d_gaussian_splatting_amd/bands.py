@@ -13,8 +13,8 @@ bit-identical to the same rows of a single-GPU render.  The exchange is two coll
   (``gaussian_slice``) and runs B2 on that slice only (``gsr_backward_preprocess_range``),
   so the leaf gradients -- and an optimizer step after them -- are sharded by Gaussian.
 
-``exchange_grad2d`` is the sparse form of the reduce-scatter: only a band's candidate
-Gaussians carry gradient, so only their rows travel.  ``ImageGather`` starts the image
+``GradExchange`` / ``exchange_grad2d`` is the sparse form of the reduce-scatter: only a
+band's candidate Gaussians carry gradient, so only their rows travel.  ``ImageGather`` starts the image
 all-gather asynchronously so it overlaps the blend backward.
 
 Both work on any torch.distributed backend (RCCL on the GPU box, gloo in the CPU tests).
@@ -65,44 +65,93 @@ def reduce_scatter_grad2d(grad2d_padded: torch.Tensor, dist, group=None) -> torc
     return out
 
 
-def exchange_grad2d(grad2d: torch.Tensor, cand: torch.Tensor, P: int, dist, group=None) -> torch.Tensor:
+_SIDE_STREAMS: dict = {}
+
+
+def _side_stream(dev: torch.device) -> torch.cuda.Stream:
+    if dev not in _SIDE_STREAMS:
+        _SIDE_STREAMS[dev] = torch.cuda.Stream(dev)
+    return _SIDE_STREAMS[dev]
+
+
+class GradExchange:
     """Sparse reduce-scatter of the 2D gradients: a band only produced rows for its candidate
     Gaussians (``cand``: their ids, e.g. ``GSR_VIEW_GID_BY_RANK``), so each rank sends just
-    those rows, bucketed by owning rank (``gaussian_slice``), in one all_to_all.  The owner
-    places every received row in a per-source dense slab and sums the slabs, so the result
-    is the same fixed-order sum whatever the arrival order.  Returns this rank's slice
-    (ceil(P / world) rows x 12).  The gid rides in padding column 9 of each row."""
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    S = -(-P // world)
-    width = grad2d.shape[1]
-    if width < 10:
-        raise ValueError("exchange_grad2d: rows need a padding column 9 (GSR_GRAD2D_STRIDE = 12)")
-    dev = grad2d.device
-    cand = cand.to(torch.int64)
-    owner = torch.div(cand, S, rounding_mode="floor")
-    order = torch.argsort(owner, stable=True)
-    cs = cand[order]
-    rows = grad2d.index_select(0, cs)
-    rows[:, 9] = cs.to(torch.int32).view(torch.float32)
-    send = torch.bincount(owner, minlength=world)
-    # gloo has no device all-to-all: stage through host memory there
-    host = dist.get_backend(group) == "gloo" and dev.type != "cpu"
-    xdev = torch.device("cpu") if host else dev
-    send_x = send.to(xdev)
-    recv_x = torch.empty_like(send_x)
-    dist.all_to_all_single(recv_x, send_x, group=group)
-    sc, rc = send_x.tolist(), recv_x.tolist()
-    got = torch.empty((sum(rc), width), dtype=rows.dtype, device=xdev)
-    dist.all_to_all_single(got, rows.to(xdev), rc, sc, group=group)
-    got = got.to(dev)
-    gid = got[:, 9].contiguous().view(torch.int32).to(torch.int64) - rank * S
-    src = torch.repeat_interleave(torch.arange(world, device=dev), torch.tensor(rc, device=dev))
-    dense = grad2d.new_zeros((world, S, width))
-    dense[src, gid] = got
-    out = dense.sum(0)
-    out[:, 9] = 0.0
-    return out
+    those rows, bucketed by owning rank (``gaussian_slice``), in one all_to_all.  The gid
+    rides in padding column 9 of each row.
+
+    Two phases so the host never stalls the GPU: the constructor (right after the forward --
+    the candidates are known then) starts the all_to_all of the per-owner row counts and
+    copies the received counts to pinned host memory on a side stream that waits only for
+    that collective; ``run(grad2d)`` (after the blend backward has been enqueued) reads the
+    counts -- long since arrived -- and moves the rows.  The owner sums the rows it receives
+    source by source in rank order (each source sends a Gaussian at most once, so every
+    ``index_add_`` has unique indices): a fixed-order, deterministic sum.  ``run`` returns
+    this rank's slice (ceil(P / world) rows x 12)."""
+
+    def __init__(self, cand: torch.Tensor, P: int, dist, group=None):
+        self.dist, self.group = dist, group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.S = -(-P // self.world)
+        cand = cand.to(torch.int64)
+        self.dev = cand.device
+        owner = torch.div(cand, self.S, rounding_mode="floor")
+        order = torch.argsort(owner, stable=True)
+        self.cs = cand[order]
+        send = torch.bincount(owner, minlength=self.world)
+        # gloo has no device all-to-all: stage through host memory there
+        self.host = dist.get_backend(group) == "gloo" and self.dev.type != "cpu"
+        if self.host or self.dev.type == "cpu":
+            xdev = torch.device("cpu")
+            send_x = send.to(xdev)
+            recv_x = torch.empty_like(send_x)
+            dist.all_to_all_single(recv_x, send_x, group=group)
+            self.sc, self.rc = send_x.tolist(), recv_x.tolist()
+            self.event = None
+            return
+        recv = torch.empty_like(send)
+        work = dist.all_to_all_single(recv, send, group=group, async_op=True)
+        side = _side_stream(self.dev)
+        side.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(side):
+            work.wait()  # the side stream waits for the collective, the compute stream does not
+            self.send_h = torch.empty(self.world, dtype=torch.int64, pin_memory=True)
+            self.recv_h = torch.empty(self.world, dtype=torch.int64, pin_memory=True)
+            self.send_h.copy_(send, non_blocking=True)
+            self.recv_h.copy_(recv, non_blocking=True)
+            self.event = torch.cuda.Event()
+            self.event.record(side)
+        self._keep = (send, recv)
+
+    def run(self, grad2d: torch.Tensor) -> torch.Tensor:
+        width = grad2d.shape[1]
+        if width < 10:
+            raise ValueError("GradExchange: rows need a padding column 9 (GSR_GRAD2D_STRIDE = 12)")
+        if self.event is not None:
+            self.event.synchronize()
+            self.sc, self.rc = self.send_h.tolist(), self.recv_h.tolist()
+        dev = grad2d.device
+        rows = grad2d.index_select(0, self.cs)
+        rows[:, 9] = self.cs.to(torch.int32).view(torch.float32)
+        xdev = torch.device("cpu") if self.host else dev
+        got = torch.empty((sum(self.rc), width), dtype=rows.dtype, device=xdev)
+        self.dist.all_to_all_single(got, rows.to(xdev), self.rc, self.sc, group=self.group)
+        got = got.to(dev)
+        gid = got[:, 9].contiguous().view(torch.int32).to(torch.int64) - self.rank * self.S
+        out = grad2d.new_zeros((self.S, width))
+        off = 0
+        for n in self.rc:  # source ranks in order
+            if n:
+                out.index_add_(0, gid[off:off + n], got[off:off + n])
+            off += n
+        out[:, 9] = 0.0
+        return out
+
+
+def exchange_grad2d(grad2d: torch.Tensor, cand: torch.Tensor, P: int, dist, group=None) -> torch.Tensor:
+    """One-call form of ``GradExchange``: count exchange and row exchange back to back."""
+    return GradExchange(cand, P, dist, group).run(grad2d)
 
 
 class ImageGather:

@@ -133,9 +133,10 @@ def main():
         st = rast.forward(cam, **inputs, sh_degree=D, tile_rows=band, band_only=world > 1)
         if world > 1:
             img = bands.ImageGather(st.color, band, gy, dist)  # overlaps the blend backward
-            g2 = rast.backward_blend(st, dpix)
             cand = st.view(native.VIEW_GID_BY_RANK, torch.int32, st.buffers.num_ranked)
-            mine = bands.exchange_grad2d(g2, cand, P, dist)  # only the band's candidates travel
+            xg = bands.GradExchange(cand, P, dist)  # row counts travel while B1 runs
+            g2 = rast.backward_blend(st, dpix)
+            mine = xg.run(g2)  # only the band's candidates' rows travel
             g = rast.backward_preprocess_range(st, g0, g1, mine[: g1 - g0])  # leaf grads of my slice
             img.wait()  # full image on every rank
         else:
