@@ -217,7 +217,8 @@ def main():
         pmc = pmc_record(kernel_name)
         result["roofline"] = {"bound": "hbm", "kernel": kernel_name, "achieved": round(achieved, 2),
                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                              "traffic": pmc.get("hbm_bytes_per_launch"), "mean_launch_ms": round(mean_ms, 4),
+                              # PMC passes are of the N = 1 launch; a band launch has no committed counts
+                              "traffic": pmc.get("hbm_bytes_per_launch") if world == 1 else None, "mean_launch_ms": round(mean_ms, 4),
                               "algorithmic_bytes_per_launch": int(bytes_launch)}
         if "valu_insts_per_launch" in pmc and world == 1:  # PMC counts are of the N = 1 launch
             # F6/B1 are VALU-issue-bound, not HBM-bound (DESIGN.md "Rooflines"): share of the
