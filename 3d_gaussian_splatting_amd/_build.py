@@ -30,6 +30,8 @@ HIP_SOURCES = {
     "gsr_blend.hip": ["-ffp-contract=off", "-fno-slp-vectorize"],
     # recomputes the forward's SH clamp bits: must round exactly like gsr_preprocess.hip
     "gsr_preprocess_bwd.hip": ["-ffp-contract=off"],
+    # training-step kernels (loss, fused Adam, densification): tolerance-compared, default flags
+    "gsr_train.hip": [],
     "gsr_api.cpp": [],
 }
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fno-fast-math",

@@ -260,6 +260,14 @@ __global__ void fill_background(float* out_color, float* final_T, float* accum,
 
 }  // namespace
 
+namespace gsr {
+// error hook for the other translation units of the library (gsr_train.hip)
+int set_error(int code, const char* msg) {
+    g_err = msg;
+    return code;
+}
+}  // namespace gsr
+
 extern "C" {
 
 int gsr_abi_version(void) { return GSR_ABI_VERSION; }

@@ -27,6 +27,12 @@ EXPORTS = ["gsr_abi_version", "gsr_last_error", "gsr_forward", "gsr_backward", "
            "gsr_backward_preprocess", "gsr_backward_preprocess_range", "gsr_view", "gsr_geom_bytes", "gsr_binning_bytes",
            "gsr_image_bytes", "gsr_scratch_bytes", "gsr_profile_enable", "gsr_profile_read",
            "gsr_stage_name"]
+# include/gsr/gsr_train.h (training-step kernels)
+TRAIN_EXPORTS = ["gsr_activate", "gsr_loss_scratch_bytes", "gsr_loss_forward", "gsr_loss_backward", "gsr_adam_step",
+                 "gsr_densify_stats", "gsr_compact_scratch_bytes", "gsr_compact_index", "gsr_gather_rows"]
+ACT_NONE, ACT_EXP, ACT_SIGMOID, ACT_NORMALIZE4 = range(4)
+ADAM_MAX_GROUPS = 8
+GATHER_MAX = 24
 STAGES = ["preprocess", "depth_sort", "scan", "duplicate", "tile_sort", "finalize", "blend_fwd", "blend_bwd",
           "preprocess_bwd", "gather_grad2d", "misc"]
 
@@ -59,6 +65,16 @@ class Grads(ctypes.Structure):
 class Buffers(ctypes.Structure):
     _fields_ = [("geom", ctypes.c_void_p), ("binning", ctypes.c_void_p), ("image", ctypes.c_void_p),
                 ("num_rendered", ctypes.c_int32), ("num_ranked", ctypes.c_int32)]
+
+
+class AdamGroup(ctypes.Structure):
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("n", ctypes.c_int64), ("act", ctypes.c_int32),
+                ("step", ctypes.c_int32), ("lr", ctypes.c_float)]
+
+
+class RowCopy(ctypes.Structure):
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("width", ctypes.c_int32)]
 
 
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
@@ -113,6 +129,26 @@ def load_hip() -> ctypes.CDLL:
         L.gsr_stage_name.argtypes = [ctypes.c_int]
         L.gsr_image_bytes.restype = ctypes.c_size_t
         L.gsr_image_bytes.argtypes = [i32, i32]
+        # gsr_train.h
+        f32 = ctypes.c_float
+        L.gsr_activate.restype = ctypes.c_int
+        L.gsr_activate.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp]
+        L.gsr_loss_scratch_bytes.restype = ctypes.c_size_t
+        L.gsr_loss_scratch_bytes.argtypes = [i32, i32, i32]
+        L.gsr_loss_forward.restype = ctypes.c_int
+        L.gsr_loss_forward.argtypes = [vp, vp, i32, i32, i32, f32, vp, vp, vp]
+        L.gsr_loss_backward.restype = ctypes.c_int
+        L.gsr_loss_backward.argtypes = [vp, vp, i32, i32, i32, f32, vp, vp, vp]
+        L.gsr_adam_step.restype = ctypes.c_int
+        L.gsr_adam_step.argtypes = [ctypes.POINTER(AdamGroup), i32, f32, f32, f32, vp]
+        L.gsr_densify_stats.restype = ctypes.c_int
+        L.gsr_densify_stats.argtypes = [vp, vp, i32, vp, vp, vp, vp]
+        L.gsr_compact_scratch_bytes.restype = ctypes.c_size_t
+        L.gsr_compact_scratch_bytes.argtypes = [i32]
+        L.gsr_compact_index.restype = ctypes.c_int
+        L.gsr_compact_index.argtypes = [vp, i32, vp, vp, vp, vp]
+        L.gsr_gather_rows.restype = ctypes.c_int
+        L.gsr_gather_rows.argtypes = [ctypes.POINTER(RowCopy), i32, vp, i32, vp]
         _hip = L
     return _hip
 

@@ -96,9 +96,15 @@ def main():
     ap.add_argument("--config", default="1m_1080p", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stage-events", action="store_true")
+    ap.add_argument("--mode", default="render", choices=("render", "train"),
+                    help="render: the BASELINE metric (rasterizer forward+backward); train: one full "
+                         "training iteration (activations, render, L1+D-SSIM loss, backward, "
+                         "densification statistics, fused Adam), SURVEY §8f")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank) or gloo (rehearsal: ranks may share a GPU)")
     args = ap.parse_args()
+    if args.mode == "train":
+        return train_main(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -261,6 +267,88 @@ def main():
         print(json.dumps(result))
     if dist:
         dist.destroy_process_group()
+
+
+def train_main(args):
+    """One training iteration per step (trainer.GaussianTrainer.step, densification off so the
+    Gaussian count stays fixed): N = 1 only.  Stage times from torch events on the launch
+    stream (the C-ABI calls run on torch's current stream); roofline for the fused Adam, the
+    only new HBM-bound stream whose bytes scale with P x 59 floats."""
+    Tr = importlib.import_module(f"{PKG}.trainer")
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit("--mode train runs on one GPU")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    cfg = CONFIGS[args.config]
+    P, W, H, D = cfg["P"], cfg["W"], cfg["H"], cfg["D"]
+    cam = gr.synthetic_camera(W, H)
+    scene = sc.make_scene(cam, P, max_sh_degree=max(D, 0), seed=0)
+    tr = Tr.GaussianTrainer(scene.means3D, scene.sh_dc, scene.sh_rest, scene.raw_opacities, scene.raw_scales,
+                            scene.raw_rotations, max_sh_degree=D, device=dev)
+    tr.active_sh_degree = D
+    gt = torch.tensor(sc.make_dL_dpix(cam, seed=2), device=dev) * 0.5 + 0.5  # synthetic target in [0, 1]
+    it = [1]
+
+    def step():
+        out = tr.step(it[0], cam, gt, densify=False)
+        it[0] += 1
+        return out
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # stage split (separate pass): events between the phases of one iteration
+    ev = lambda: torch.cuda.Event(enable_timing=True)
+    names = ("activate+render", "loss", "backward", "stats+adam")
+    acc = dict.fromkeys(names, 0.0)
+    adam_ms = 0.0
+    for _ in range(args.steps):
+        e = [ev() for _ in range(6)]
+        e[0].record()
+        st = tr.render(cam)
+        e[1].record()
+        stats, maps = tr.k.loss_forward(st.color, gt, tr.opt.lambda_dssim)
+        dimg = tr.k.loss_backward(st.color, gt, tr.opt.lambda_dssim, maps)
+        e[2].record()
+        g = tr.rast.backward(st, dimg)
+        e[3].record()
+        tr.k.densify_stats(st.radii, g["means2D"], tr.max_radii2D, tr.xyz_gradient_accum, tr.denom)
+        grads = {"xyz": g["means3D"], "f_dc": g["sh_dc"], "f_rest": g["sh_rest"], "opacity": g["opacities"],
+                 "scaling": g["scales"], "rotation": g["rotations"]}
+        e[4].record()
+        tr.optimizer_step(grads)
+        e[5].record()
+        torch.cuda.synchronize()
+        for i, n in enumerate(names[:3]):
+            acc[n] += e[i].elapsed_time(e[i + 1])
+        acc["stats+adam"] += e[3].elapsed_time(e[5])
+        adam_ms += e[4].elapsed_time(e[5])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ms = 1e3 * elapsed / args.steps
+    floats = sum(v.numel() for v in tr.params.values())
+    adam_bytes = floats * 28  # p, m, v read + written, grad read (f32)
+    adam_mean = adam_ms / args.steps
+    stats = out["stats"].cpu().tolist()
+    res = {"metric": "training iterations/s at 1080p, 1M Gaussians (activations + render + L1/D-SSIM loss + "
+                     "backward + densification statistics + fused Adam)",
+           "value": round(args.steps / elapsed, 3), "unit": "iters/s", "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "strong",
+           "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+           "config": {"workload": f"{args.config} training step: {P} Gaussians, {W}x{H}, SH degree {D}, "
+                                  f"densification off", "gaussians": P, "width": W, "height": H, "sh_degree": D},
+           "stage_ms": {k: round(v / args.steps, 4) for k, v in acc.items()},
+           "roofline": {"bound": "hbm", "kernel": "adam_kernel", "achieved": round(adam_bytes / (adam_mean * 1e-3) / 1e9, 2),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(adam_bytes / (adam_mean * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "mean_launch_ms": round(adam_mean, 4), "algorithmic_bytes_per_launch": adam_bytes,
+                        "note": "activation backward fused; the event pair brackets the single adam launch"},
+           "loss": {"loss": stats[0], "l1": stats[1], "ssim": stats[2]}}
+    print(json.dumps(res))
 
 
 if __name__ == "__main__":

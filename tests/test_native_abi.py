@@ -10,17 +10,43 @@ import pytest
 from conftest import ROOT, pkg
 
 HEADER = os.path.join(ROOT, "include", "gsr", "gsr.h")
+TRAIN_HEADER = os.path.join(ROOT, "include", "gsr", "gsr_train.h")
 
 
-def declared_functions():
-    text = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w\*\s]+?\b(gsr_\w+)\s*\(", text, re.M)) - {"gsr_alloc_fn"})
+def declared_functions(header=None):
+    headers = [header] if header else [HEADER, TRAIN_HEADER]
+    out = set()
+    for h in headers:
+        text = open(h).read()
+        out |= set(re.findall(r"^\s*(?:const\s+)?[\w\*\s]+?\b(gsr_\w+)\s*\(", text, re.M))
+    return sorted(out - {"gsr_alloc_fn"})
 
 
 def test_header_declares_expected_entry_points():
-    fns = declared_functions()
     native = pkg("native")
-    assert set(native.EXPORTS) == set(fns), fns
+    assert set(native.EXPORTS) == set(declared_functions(HEADER)), declared_functions(HEADER)
+    assert set(native.TRAIN_EXPORTS) == set(declared_functions(TRAIN_HEADER)), declared_functions(TRAIN_HEADER)
+
+
+def test_train_abi_validation_without_gpu():
+    """gsr_train.h entry points load, size their scratch and reject bad arguments (no launch)."""
+    native = pkg("native")
+    L = native.load_hip()
+    assert L.gsr_loss_scratch_bytes(3, 1080, 1920) >= 3 * 3 * 1080 * 1920 * 4
+    assert L.gsr_compact_scratch_bytes(1 << 20) >= 1024 * 4
+    assert L.gsr_loss_forward(None, None, 3, 8, 8, 0.2, None, None, None) < 0
+    assert "loss" in native.last_error()
+    g = (native.AdamGroup * 1)()
+    g[0].n, g[0].step, g[0].act = 8, 0, native.ACT_NONE
+    g[0].param = g[0].grad = g[0].exp_avg = g[0].exp_avg_sq = 256
+    assert L.gsr_adam_step(g, 1, 0.9, 0.999, 1e-8, None) < 0 and "step" in native.last_error()
+    g[0].step, g[0].act, g[0].n = 1, native.ACT_NORMALIZE4, 6
+    assert L.gsr_adam_step(g, 1, 0.9, 0.999, 1e-8, None) < 0 and "rows of 4" in native.last_error()
+    assert L.gsr_adam_step(g, 9, 0.9, 0.999, 1e-8, None) < 0
+    c = (native.RowCopy * 1)()
+    c[0].src, c[0].dst, c[0].width = 256, 256, 3
+    assert L.gsr_gather_rows(c, 1, ctypes.c_void_p(512), 4, None) < 0 and "alias" in native.last_error()
+    assert L.gsr_densify_stats(None, None, 4, None, None, None, None) < 0
 
 
 def test_library_exports_every_symbol():
