@@ -1,9 +1,10 @@
 // gsr_api.cpp -- the C ABI (include/gsr/gsr.h) over the CDNA4 kernels.
 //
-// Stage order (forward): F1 preprocess -> depth sort (P keys) -> scan of tiles_touched in
-// depth-rank order -> ONE device->host read of K -> F3 duplicate -> tile-key sort (K keys)
-// -> F5 finalize (sorted gid + tile ranges) -> F6 blend.  Backward: B1 blend backward ->
-// B2 preprocess backward (or B1 -> per-Gaussian grad2d for the multi-GPU all-reduce).
+// Stage order (forward, shipped binning): F1 preprocess -> scan of tiles_touched in gid order
+// (a band: compaction of its candidates first) -> ONE device->host read of K -> F3 duplicate
+// -> tile-key sort (K keys) -> F5 finalize (tile ranges) -> per-tile depth sort -> F6 blend.
+// Backward: B1 blend backward -> gather -> B2 preprocess backward (or B1 -> per-Gaussian grad2d
+// for the multi-GPU exchange).
 // No persistent allocations; every scratch buffer comes from the caller's callbacks.
 #include <hip/hip_runtime.h>
 
@@ -31,6 +32,34 @@ thread_local std::string g_err;
 int scan_variant(int n) {
     const char* e = std::getenv("GSR_SCAN_VARIANT");
     return e ? std::atoi(e) : (n <= (1 << 19) ? 1 : 0);
+}
+
+// Binning scheme (A/B, bench/ablation only); all three give the same canonical order.
+// Stage sums at 1M/1080p (scripts/ablate.py), whole forward + backward step:
+//   1 (shipped, 1.406 ms) = no global depth sort: the instances are emitted in gid order (the
+//       scan and F3 read tiles / rects coalesced), a stable LSD sort of the tile keys groups
+//       them by tile in gid order, and each tile's slice is sorted by depth alone with a stable
+//       LDS radix sort (launch_tile_depth_sort); the gather of B1's partials then also walks
+//       the Gaussians in gid order (0.079 vs 0.108 ms);
+//   0 (1.464 ms) = global LSD depth sort of the P (or band-candidate) keys before the scan,
+//       then the tile-key LSD sort (round-1's first design);
+//   2 (1.537 ms) = count binning: F3 counts instances per tile with atomics, one scan gives the
+//       ranges, a scatter with returning atomics groups them by tile (unordered), then a
+//       bitonic (depth, gid) sort per tile.  The 6.5 M atomics on 8160 hot words cost
+//       0.088 ms in F3 and 0.16 ms in the scatter -- more than the two LSD passes they replace.
+int bin_variant() {
+    const char* e = std::getenv("GSR_BIN_VARIANT");
+    return e ? std::atoi(e) : 1;
+}
+
+// A/B (bench/ablation only): 1 = binning variant 1 carries each instance's depth key through
+// the tile sort so the per-tile sort reads its keys contiguously; 0 (shipped) = the per-tile
+// sort gathers depth_key[gid].  Measured at 1M/1080p: carrying costs the tile sort +0.048 ms
+// (a third array per pass) and saves the per-tile sort only 0.005 ms -- the random 4-B gathers
+// hit L2 / MALL, and that sort is VALU-bound, not gather-bound.
+bool carry_depth() {
+    const char* e = std::getenv("GSR_CARRY_DEPTH");
+    return e ? std::atoi(e) != 0 : false;
 }
 
 // Low-latency device->host read of one u32: DMA into a per-thread pinned word, then spin on
@@ -317,11 +346,106 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
         GSR_STAGE(GSR_STAGE_MISC, hipGetLastError(), "fill_background");
     }
     uint32_t* counters = at<uint32_t>(bufs->image, il.counters);
-    GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(ranges, 0, il.counters + 4 * 2 * kCountSlots - il.ranges, stream),
-              "memset ranges");
+    GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(ranges, 0, il.ovf - il.ranges, stream), "memset ranges");
 
     long long K = 0;
-    if (P > 0) {
+    const int bv = bin_variant();
+    if (P > 0 && bv != 0) {
+        // F1 -> [band: candidate compaction] -> F2 scan (gid order) -> F3 (+ per-tile counts)
+        // -> group by tile (count binning, or tile-key sort + F5) -> per-tile (depth, gid)
+        // order.  gid_by_rank = the identity (full image, written by the scan) or the band's
+        // candidates in gid order (written by the compaction).
+        const bool full_img = ty0 == 0 && ty1 == gy;
+        uint32_t* tcount = bv == 2 ? at<uint32_t>(bufs->image, il.tcount) : nullptr;
+        PreOut po{radii, depth_key, tiles, rec, at<uint4>(bufs->geom, gl.rect),
+                  full_img ? at<uint32_t>(bufs->geom, gl.flags) : nullptr, counters};
+        GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess(*cam, gauss_in(gs), ty0, ty1, po, stream), "preprocess");
+        uint32_t* gid_by_rank = at<uint32_t>(bufs->geom, gl.sA_v);
+        uint32_t cw[2 * kCountSlots];
+        uint64_t csum = 0, ksum = 0;
+        GSR_CHECK_HIP(begin_read(counters, 2 * kCountSlots, stream), "read counts");
+        int NR = P;
+        bool scanned = false;
+        if (!full_img) {
+            GSR_STAGE(GSR_STAGE_DEPTH_SORT, compact_candidates(tiles, depth_key, P, at<uint32_t>(bufs->geom, gl.partials),
+                                                               offsets, gid_by_rank, counters + kCandCountSlot, stream),
+                      "band candidates");
+        } else {
+            // the scan needs no count: enqueue it before the host waits for K
+            GSR_STAGE(GSR_STAGE_SCAN, inclusive_scan_gather(tiles, nullptr, offsets, P,
+                                                            at<uint32_t>(bufs->geom, gl.partials), stream, gid_by_rank),
+                      "scan");
+            scanned = true;
+        }
+        GSR_STAGE(GSR_STAGE_MISC, end_read(counters, cw, 2 * kCountSlots, stream), "read counts");
+        for (int i = 0; i < kCountSlots; ++i) csum += cw[i], ksum += cw[kCountSlots + i];
+        if (!full_img) {
+            NR = (int)(csum < (uint64_t)P ? csum : (uint64_t)P);
+            if (colour_pass_needed(*cam, gauss_in(gs), ty0, ty1))
+                GSR_STAGE(GSR_STAGE_PREPROCESS, launch_colour(*cam, gauss_in(gs), gid_by_rank, NR, rec, stream),
+                          "band colours");
+        }
+        bufs->num_ranked = NR;
+        K = (long long)ksum;
+        if (K > INT32_MAX) return fail(-3, "num_rendered overflow (%lld)", K);
+        bufs->num_rendered = (int32_t)K;
+        bufs->binning = alloc_binning(ctx, BinLayout(K).total);
+        if (!bufs->binning) return fail(-2, "allocation failed (binning, K=%lld)", K);
+        BinLayout bl(K);
+        uint32_t* kA = at<uint32_t>(bufs->binning, bl.kA);
+        uint32_t* vA = at<uint32_t>(bufs->binning, bl.vA);
+        uint32_t* kB = at<uint32_t>(bufs->binning, bl.kB);
+        uint32_t* vB = at<uint32_t>(bufs->binning, bl.vB);
+        uint32_t* inst_gid = at<uint32_t>(bufs->binning, bl.inst_gid);
+        // final (tile, gid) arrays where views() expects them, and the free pair beside them
+        const bool odd = (tile_passes(gx * gy) & 1) != 0;
+        uint32_t* fk = odd ? kB : kA;
+        uint32_t* fv = odd ? vB : vA;
+        uint32_t* sk = odd ? kA : kB;
+        uint32_t* sv = odd ? vA : vB;
+        uint32_t* dup_key = bv == 2 ? sk : kA;  // F3's tile keys (emission order)
+        // variant 1: F3 also writes each instance's depth key, the tile sort carries it, and
+        // the per-tile sort reads it contiguously instead of gathering depth_key[gid]
+        const bool carry = bv == 1 && carry_depth();
+        uint32_t* dA = at<uint32_t>(bufs->binning, bl.dA);
+        uint32_t* dB = at<uint32_t>(bufs->binning, bl.dB);
+        if (NR > 0 && !scanned && scan_variant(NR) == 1) {
+            GSR_STAGE(GSR_STAGE_DUPLICATE, launch_scan_duplicate(gid_by_rank, tiles, at<uint4>(bufs->geom, gl.rect), NR, gx,
+                                                                 ty0, offsets, dup_key, inst_gid,
+                                                                 at<uint32_t>(bufs->geom, gl.hist), stream, tcount,
+                                                                 depth_key, carry ? dA : nullptr),
+                      "scan + duplicate");
+        } else if (NR > 0) {
+            if (!scanned)
+                GSR_STAGE(GSR_STAGE_SCAN, inclusive_scan_gather(tiles, gid_by_rank, offsets, NR,
+                                                                at<uint32_t>(bufs->geom, gl.partials), stream),
+                          "scan");
+            GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate(gid_by_rank, offsets, tiles, at<uint4>(bufs->geom, gl.rect), NR,
+                                                            gx, ty0, ty1, dup_key, inst_gid, stream, tcount,
+                                                            depth_key, carry ? dA : nullptr),
+                      "duplicate");
+        }
+        if (K > 0) {
+            if (bv == 2) {
+                GSR_STAGE(GSR_STAGE_TILE_SORT, launch_tile_bins(sk, inst_gid, K, ty0 * gx, (ty1 - ty0) * gx, tcount, ranges,
+                                                                fk, fv, stream),
+                          "tile bins");
+            } else {
+                int w2 = -1;
+                GSR_STAGE(GSR_STAGE_TILE_SORT, radix_sort(kA, inst_gid, kB, vB, kA, vA, K, tile_bits(gx * gy),
+                                                          at<uint32_t>(bufs->binning, bl.hist), &w2, stream, false,
+                                                          carry ? dA : nullptr, dB, dA),
+                          "tile sort");
+                if ((w2 == 0) != odd) return fail(-12, "tile sort ended in an unexpected buffer");
+                GSR_STAGE(GSR_STAGE_FINALIZE, launch_finalize(fk, K, ranges, stream), "finalize");
+            }
+            GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_tile_depth_sort(ranges, ty0 * gx, (ty1 - ty0) * gx, K, depth_key, fv,
+                                                                   at<uint32_t>(bufs->image, il.ovf),
+                                                                   counters + kOvfCountSlot, sk, sv, stream, bv == 1,
+                                                                   carry ? (odd ? dB : dA) : nullptr),
+                      "per-tile depth order");
+        }
+    } else if (P > 0) {
         const bool full_img = ty0 == 0 && ty1 == gy;
         PreOut po{radii, depth_key, tiles, rec, at<uint4>(bufs->geom, gl.rect),
                   full_img ? at<uint32_t>(bufs->geom, gl.flags) : nullptr, counters};
@@ -344,7 +468,7 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
         GSR_CHECK_HIP(begin_read(counters, 2 * kCountSlots, stream), "read counts");
         if (banded) {
             GSR_STAGE(GSR_STAGE_DEPTH_SORT, compact_candidates(tiles, depth_key, P, at<uint32_t>(bufs->geom, gl.partials),
-                                                               offsets, cand_tmp, counters + 2 * kCountSlots, stream),
+                                                               offsets, cand_tmp, counters + kCandCountSlot, stream),
                       "band candidates");
             GSR_STAGE(GSR_STAGE_MISC, end_read(counters, cw, 2 * kCountSlots, stream), "read counts");
             sum_counts();

@@ -126,6 +126,14 @@ __device__ __forceinline__ float pair_alpha(float e, float L, float& oG) {
     return (e <= L && oG >= (1.0f / 255.0f)) ? a : 0.0f;
 }
 
+// Same alpha, plus the keep predicate itself: keep implies alpha >= 1/255 > 0 and !keep gives
+// alpha = 0, so B1 tests `keep` (an SGPR mask it already has) instead of re-comparing alpha > 0.
+__device__ __forceinline__ float pair_alpha_keep(float e, float L, float& oG, bool& keep) {
+    oG = __builtin_amdgcn_exp2f(e);
+    keep = e <= L && oG >= (1.0f / 255.0f);
+    return keep ? __builtin_amdgcn_fmed3f(oG, 0.0f, 0.99f) : 0.0f;
+}
+
 // Chunk length of a tile's list when B1 is chunked: at most kMaxChunks chunks of whole
 // 64-record sub-batches (F6 checkpoints at 64-record boundaries).  Most of a tile's B1 work
 // is in its front records (pixels terminate), so chunks stay short to split that front.
@@ -414,11 +422,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                 const float dy = r0.y - pfy[p];
                 const float e = fmaf(fmaf(r1.x, dy, bdx), dy, K);
                 float oG;
-                const float a = pair_alpha(e, r2.w, oG);
+                bool keep;
+                const float a = pair_alpha_keep(e, r2.w, oG, keep);
                 const float w = a * T[p];
                 const float tT = T[p] - w;
                 const bool ok = tT >= 0.0001f;
-                if (ok && a > 0.0f) {
+                if (ok && keep) {
                     any = true;
                     const float one_m = 1.0f - a;
                     const float cdp = fmaf(r1.z, dp0[p], fmaf(r1.w, dp1[p], r2.x * dp2[p]));

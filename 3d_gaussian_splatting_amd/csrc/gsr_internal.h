@@ -6,7 +6,8 @@
 //                                 | sort ping-pong 4 x u32
 //                                 | radix histogram (256 x blocks) | scan partials
 //   binning  (per instance, K):   tile key/val ping-pong 4 x u32 (values = Gaussian id)
-//                                 | inst_gid u32 (emission order) | radix histogram
+//                                 | inst_gid u32 (emission order) | depth key ping-pong 2 x u32
+//                                 | radix histogram
 //   image    (per pixel):         ranges uint2[tiles] | counters | final_T f32 | accum 3 x f32
 //   scratch  (backward, per K):   partial moments float4[2] | partial float  (indexed by emission j)
 #pragma once
@@ -64,7 +65,7 @@ struct GeomLayout {
 };
 
 struct BinLayout {
-    size_t kA, vA, kB, vB, inst_gid, hist, total;
+    size_t kA, vA, kB, vB, inst_gid, dA, dB, hist, total;
     BinLayout(long long K) {
         size_t o = 0, n = (size_t)(K > 0 ? K : 1);
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
@@ -73,6 +74,8 @@ struct BinLayout {
         kB = take(4 * n);
         vB = take(4 * n);
         inst_gid = take(4 * n);
+        dA = take(4 * n);  // per-instance depth keys carried through the tile sort (ping-pong)
+        dB = take(4 * n);
         hist = take(4 * sort_scratch_words(n));
         total = o;
     }
@@ -93,14 +96,17 @@ inline int chunked_tiles(int W, int ty0, int ty1) {
 }
 
 struct ImgLayout {
-    size_t ranges, counters, final_T, accum, ck, total;
+    size_t ranges, counters, tcount, ovf, final_T, accum, ck, total;
     ImgLayout(int W, int H, int ck_tiles = 0) {
         size_t o = 0;
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
         size_t tiles = (size_t)div_up(W, kTile) * div_up(H, kTile);
         size_t pix = (size_t)W * H;
         ranges = take(8 * (tiles ? tiles : 1));
-        counters = take(4 * (2 * kCountSlots + 16));  // right after ranges: one memset clears both
+        counters = take(4 * (2 * kCountSlots + 16));  // ranges, counters and tcount are
+        tcount = take(4 * (tiles ? tiles : 1));       // contiguous: one memset clears all three
+        // (tcount: per-tile instance counts from F3, then the count binning's scatter cursors)
+        ovf = take(4 * (tiles ? tiles : 1));  // tiles the per-tile depth sort hands to its large form
         final_T = take(4 * (pix ? pix : 1));
         accum = take(12 * (pix ? pix : 1));  // colour sum without background, 3 x H x W
         ck = take((size_t)ck_tiles * (kMaxChunks - 1) * 256 * 16);  // float4 (T, C) checkpoints
@@ -120,6 +126,10 @@ struct PartLayout {
         total = p1 + align_up(4 * n);
     }
 };
+
+// counters[] slots past the preprocess partials (2 x kCountSlots)
+constexpr int kCandCountSlot = 2 * kCountSlots;      // band candidate count (compaction)
+constexpr int kOvfCountSlot = 2 * kCountSlots + 8;   // tiles queued for the large per-tile depth sort
 
 // number of 8-bit LSD passes to sort tile ids of a grid with `tiles` tiles
 inline int tile_bits(int tiles) {

@@ -1,24 +1,26 @@
-// gsr_sort.hip -- binning on gfx950: scan, duplicateWithKeys, LSD radix sort, tile ranges.
+// gsr_sort.hip -- binning on gfx950: scan, duplicateWithKeys, LSD radix sort, tile ranges,
+// per-tile depth order.
 //
 // Canonical instance order is (tile, depth bits, gid) (SURVEY §8a notes).  It is reached
-// with far fewer sorted bytes than one 45-bit key sort over K instances:
-//   1. depth sort of the P Gaussians: stable LSD over the 32-bit depth key, values = gid
-//      (identity input, so ties keep gid order)            -> gid_by_rank
-//   2. inclusive scan of tiles_touched in rank order        -> offsets (K = last)
-//   3. duplicate: rank r emits its band-clipped rect row-major at offsets[r-1]: the instance
-//      array is then already in (depth bits, gid, rect order) order
-//   4. stable LSD over the ceil(log2 tiles)-bit tile key only (2 passes at 1080p),
-//      values = the instance's Gaussian id                   -> sorted_gid
-//   5. finalize: tile ranges from key boundaries
+// with far fewer sorted bytes than one 45-bit key sort over K instances (shipped binning,
+// GSR_BIN_VARIANT 1, gsr_api.cpp):
+//   1. inclusive scan of tiles_touched in gid order           -> offsets (K = last)
+//   2. duplicate: Gaussian g emits its band-clipped rect row-major at offsets[g-1] (coalesced
+//      reads of tiles / rects, wave-cooperative expansion)
+//   3. stable LSD over the ceil(log2 tiles)-bit tile key only (2 passes at 1080p), values =
+//      the instance's Gaussian id -> grouped by tile, gid order inside a tile
+//   4. finalize: tile ranges from key boundaries
+//   5. per tile, a stable LDS radix sort of the slice by the 32-bit depth key alone (ties keep
+//      gid order) -> (tile, depth, gid)
 // (B1 recovers an instance's emission index j from its Gaussian's rect, so no permutation
-// array is carried through the sort.)
-// Sorted bytes at 1M/1080p: 4 passes x 1M x 8 B + 2 passes x 6.5M x 8 B, vs 6 passes x 6.5M
-// x 12 B for a 45-bit (tile|depth) key sort.
+// array is carried through the sort.)  The older order -- a global depth sort of the P keys
+// first, then emission in depth order (variant 0) -- and a count binning (variant 2) are kept
+// for A/B.
 //
 // Radix sort = reduce-then-scan per 8-bit digit: upsweep (per-block digit counts), column
 // scan (per digit over blocks), downsweep (stable wave64 ranking: 8 ballots give each lane
 // its peer mask, popcount below it is its rank in the round; per-wave running counters in
-// LDS; digit base = scanned counts).  All integer work: HBM-bound, no MFMA.
+// LDS; digit base = scanned counts).  All integer work: HBM / issue-bound, no MFMA.
 #include <cstdlib>
 
 #include "gsr_kernels.h"
@@ -134,19 +136,23 @@ __global__ __launch_bounds__(kB) void radix_colscan(uint32_t* __restrict__ hist,
 }
 
 // ---- downsweep: stable scatter, reordered through LDS so global writes are coalesced ----
+template <bool V2>
 __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict__ keys_in,
                                                       const uint32_t* __restrict__ vals_in,
                                                       uint32_t* __restrict__ keys_out,
                                                       uint32_t* __restrict__ vals_out, long long n,
                                                       int shift, int nbits, int nb,
                                                       const uint32_t* __restrict__ hist,
-                                                      const uint32_t* __restrict__ totals) {
+                                                      const uint32_t* __restrict__ totals,
+                                                      const uint32_t* __restrict__ v2_in,
+                                                      uint32_t* __restrict__ v2_out) {
     __shared__ uint32_t wcnt[kWaves][256];
     __shared__ uint32_t gbase[256];   // global position of this block's first item of digit d
     __shared__ uint32_t lbase[256];   // block-local position of the first item of digit d
     __shared__ uint32_t wsum[kWaves];
     __shared__ uint32_t skey[kSortTile];
     __shared__ uint32_t sval[kSortTile];
+    __shared__ uint32_t sv2[V2 ? kSortTile : 1];  // second value array (V2)
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const uint32_t mask = (1u << nbits) - 1u;
 #pragma unroll
@@ -170,7 +176,7 @@ __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict
     __syncthreads();
     const long long bbase = (long long)blockIdx.x * kSortTile;
     const long long base = bbase + (long long)w * kWaveItems;
-    uint32_t key[kI], val[kI], rank[kI];
+    uint32_t key[kI], val[kI], rank[kI], v2[kI];
     const uint64_t lt = lanemask_lt();
 #pragma unroll
     for (int r = 0; r < kI; ++r) {
@@ -178,6 +184,7 @@ __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict
         const bool valid = idx < n;
         key[r] = valid ? keys_in[idx] : 0xFFFFFFFFu;
         val[r] = valid ? (vals_in ? vals_in[idx] : (uint32_t)idx) : 0u;
+        v2[r] = (V2 && valid) ? v2_in[idx] : 0u;
     }
 #pragma unroll
     for (int r = 0; r < kI; ++r) {
@@ -223,6 +230,7 @@ __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict
             const uint32_t lp = lbase[d] + wcnt[w][d] + rank[r];
             skey[lp] = key[r];
             sval[lp] = val[r];
+            if (V2) sv2[lp] = v2[r];
         }
     }
     __syncthreads();
@@ -234,6 +242,7 @@ __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict
         const uint32_t pos = gbase[d] + (uint32_t)i - lbase[d];
         keys_out[pos] = k;
         vals_out[pos] = sval[i];
+        if (V2) v2_out[pos] = sv2[i];
     }
 }
 
@@ -273,7 +282,7 @@ __global__ __launch_bounds__(kB) void radix_hist_all(const uint32_t* __restrict_
         if (h[p][tid]) atomicAdd(&ghist[p * 256 + tid], h[p][tid]);
 }
 
-template <int KI>
+template <int KI, int LB>
 __global__ __launch_bounds__(kB) void radix_onesweep(const uint32_t* __restrict__ keys_in,
                                                      const uint32_t* __restrict__ vals_in,
                                                      uint32_t* __restrict__ keys_out,
@@ -336,17 +345,48 @@ __global__ __launch_bounds__(kB) void radix_onesweep(const uint32_t* __restrict_
         __hip_atomic_store(my, kAgg | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         int t = tile - 1;
         uint32_t spins = 0;
-        while (t >= 0) {
-            const uint32_t v = __hip_atomic_load(status + (size_t)t * 256 + tid, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-            if ((v & ~kCntMask) == 0u) {
-                if (++spins > (1u << 26)) break;  // never expected: bounded so a bug cannot hang the GPU
-                __builtin_amdgcn_s_sleep(1);
-                continue;
+        if (LB == 1) {
+            while (t >= 0) {
+                const uint32_t v = __hip_atomic_load(status + (size_t)t * 256 + tid, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                if ((v & ~kCntMask) == 0u) {
+                    if (++spins > (1u << 26)) break;  // never expected: bounded so a bug cannot hang the GPU
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                excl += v & kCntMask;
+                if (v & kInc) break;
+                --t;
             }
-            excl += v & kCntMask;
-            if (v & kInc) break;
-            --t;
+        } else {
+            // windowed look-back: LB predecessors' words per probe, all loads in flight at
+            // once; consume them nearest-first up to the first inclusive prefix (done) or the
+            // first unpublished word (re-probe from there).  Before tile 0: an inclusive zero.
+            while (t >= 0) {
+                uint32_t v[LB];
+#pragma unroll
+                for (int j = 0; j < LB; ++j)
+                    v[j] = (t - j >= 0) ? __hip_atomic_load(status + (size_t)(t - j) * 256 + tid, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT)
+                                        : kInc;
+                int used = 0;
+                bool done = false;
+                for (; used < LB; ++used) {
+                    const uint32_t x = v[used];
+                    if ((x & ~kCntMask) == 0u) break;
+                    excl += x & kCntMask;
+                    if (x & kInc) {
+                        done = true;
+                        break;
+                    }
+                }
+                if (done) break;
+                if (used == 0) {
+                    if (++spins > (1u << 26)) break;  // never expected: bounded so a bug cannot hang the GPU
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                t -= used;
+            }
         }
         __hip_atomic_store(my, kInc | (excl + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -457,7 +497,8 @@ __global__ __launch_bounds__(1024) void scan_partials(uint32_t* __restrict__ par
 __global__ __launch_bounds__(kB) void scan_downsweep(const uint32_t* __restrict__ in,
                                                      const uint32_t* __restrict__ idx, int n,
                                                      const uint32_t* __restrict__ partials,
-                                                     uint32_t* __restrict__ out) {
+                                                     uint32_t* __restrict__ out,
+                                                     uint32_t* __restrict__ iota_out) {
     __shared__ uint32_t buf[kSortTile + kSortTile / 32];
     __shared__ uint32_t wsum[kWaves];
     const int base = blockIdx.x * kSortTile;
@@ -486,7 +527,10 @@ __global__ __launch_bounds__(kB) void scan_downsweep(const uint32_t* __restrict_
 #pragma unroll
     for (int r = 0; r < kI; ++r) {
         const int i = r * kB + tid;
-        if (base + i < n) out[base + i] = buf[pad(i)];
+        if (base + i < n) {
+            out[base + i] = buf[pad(i)];
+            if (iota_out) iota_out[base + i] = (uint32_t)(base + i);
+        }
     }
 }
 
@@ -513,9 +557,12 @@ __global__ __launch_bounds__(256) void scan_duplicate_kernel(const uint32_t* __r
                                                              uint32_t* __restrict__ tkey,
                                                              uint32_t* __restrict__ inst_gid,
                                                              uint32_t* __restrict__ status,
-                                                             uint32_t* __restrict__ ticket) {
+                                                             uint32_t* __restrict__ ticket,
+                                                             uint32_t* __restrict__ tcount,
+                                                             const uint32_t* __restrict__ depth_key,
+                                                             uint32_t* __restrict__ inst_depth) {
     __shared__ uint32_t s_start[kWaves][64], s_g[kWaves][64], s_w[kWaves][64], s_x0[kWaves][64],
-        s_y0[kWaves][64];
+        s_y0[kWaves][64], s_dk[kWaves][64];
     __shared__ uint32_t wsum[kWaves];
     __shared__ uint32_t s_excl;
     __shared__ int s_b;
@@ -600,6 +647,7 @@ __global__ __launch_bounds__(256) void scan_duplicate_kernel(const uint32_t* __r
     s_w[w][lane] = maxx - minx;
     s_x0[w][lane] = minx;
     s_y0[w][lane] = y0;
+    s_dk[w][lane] = (inst_depth && nt) ? depth_key[g] : 0u;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -612,8 +660,11 @@ __global__ __launch_bounds__(256) void scan_duplicate_kernel(const uint32_t* __r
         const uint32_t local = i - s_start[w][o];
         const uint32_t wd = s_w[w][o];
         const uint32_t dy = udiv_small(local, wd), dx = local - dy * wd;
-        tkey[first + i] = (s_y0[w][o] + dy) * (uint32_t)grid_x + s_x0[w][o] + dx;
+        const uint32_t tk = (s_y0[w][o] + dy) * (uint32_t)grid_x + s_x0[w][o] + dx;
+        tkey[first + i] = tk;
         inst_gid[first + i] = s_g[w][o];
+        if (tcount) atomicAdd(tcount + tk, 1u);  // count binning: no-return atomic
+        if (inst_depth) inst_depth[first + i] = s_dk[w][o];  // per-tile depth sort keys
     }
 }
 
@@ -680,9 +731,12 @@ __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restri
                                                         uint4* __restrict__ rect, int P,
                                                         int grid_x, int ty0, int ty1,
                                                         uint32_t* __restrict__ tkey,
-                                                        uint32_t* __restrict__ inst_gid) {
+                                                        uint32_t* __restrict__ inst_gid,
+                                                        uint32_t* __restrict__ tcount,
+                                                        const uint32_t* __restrict__ depth_key,
+                                                        uint32_t* __restrict__ inst_depth) {
     __shared__ uint32_t s_start[kWaves][64], s_g[kWaves][64], s_w[kWaves][64], s_x0[kWaves][64],
-        s_y0[kWaves][64];
+        s_y0[kWaves][64], s_dk[kWaves][64];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int r = blockIdx.x * 256 + tid;
     const bool valid = r < P;
@@ -711,6 +765,7 @@ __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restri
     s_w[w][lane] = maxx - minx;
     s_x0[w][lane] = minx;
     s_y0[w][lane] = y0;
+    s_dk[w][lane] = (inst_depth && nt) ? depth_key[g] : 0u;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -723,8 +778,11 @@ __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restri
         const uint32_t local = i - s_start[w][o];
         const uint32_t wd = s_w[w][o];
         const uint32_t dy = udiv_small(local, wd), dx = local - dy * wd;
-        tkey[first + i] = (s_y0[w][o] + dy) * (uint32_t)grid_x + s_x0[w][o] + dx;
+        const uint32_t tk = (s_y0[w][o] + dy) * (uint32_t)grid_x + s_x0[w][o] + dx;
+        tkey[first + i] = tk;
         inst_gid[first + i] = s_g[w][o];
+        if (tcount) atomicAdd(tcount + tk, 1u);  // count binning: no-return atomic
+        if (inst_depth) inst_depth[first + i] = s_dk[w][o];  // per-tile depth sort keys
     }
     (void)ty1;
 }
@@ -739,6 +797,330 @@ __global__ __launch_bounds__(256) void finalize_kernel(const uint32_t* __restric
     if (i == K - 1 || stile[i + 1] != t) ranges[t].y = (uint32_t)(i + 1);
 }
 
+
+// ---- count binning (GSR_BIN_VARIANT 2, shipped): the instance list grouped by tile without a
+// key sort.  F3 adds every instance into its tile's counter (no-return atomics); one block
+// scans the counts into the tile ranges and turns each count into a cursor; the scatter claims
+// a slot per instance with a returning atomic on its tile's cursor.  Order inside a tile is
+// arbitrary here -- the per-tile (depth, gid) sort below makes it canonical -- so no stability
+// is needed, and the K (tile, gid) pairs are read and written once instead of two LSD passes
+// (each a read, a histogram pass and a write) plus the finalize pass.
+__global__ __launch_bounds__(1024) void tile_offsets_kernel(uint32_t* __restrict__ tcount, int t0, int nt,
+                                                            uint2* __restrict__ ranges) {
+    __shared__ uint32_t wsum[16];
+    uint32_t carry = 0;
+    for (int base = 0; base < nt; base += 1024) {
+        const int i = base + threadIdx.x;
+        const uint32_t v = i < nt ? tcount[t0 + i] : 0u;
+        uint32_t tot;
+        const uint32_t ex = carry + block_exclusive_scan(v, wsum, &tot);
+        if (i < nt) {
+            ranges[t0 + i] = make_uint2(ex, ex + v);
+            tcount[t0 + i] = ex;  // the tile's scatter cursor
+        }
+        carry += tot;
+    }
+}
+
+__global__ __launch_bounds__(256) void tile_scatter_kernel(const uint32_t* __restrict__ tkey,
+                                                           const uint32_t* __restrict__ gid, long long K,
+                                                           uint32_t* __restrict__ cursor,
+                                                           uint32_t* __restrict__ stile,
+                                                           uint32_t* __restrict__ sgid) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= K) return;
+    const uint32_t t = tkey[i];
+    const uint32_t pos = atomicAdd(cursor + t, 1u);
+    stile[pos] = t;
+    sgid[pos] = gid[i];
+}
+
+// ---- per-tile depth order (canonical (tile, depth bits, gid) without a global depth sort) ----
+// After the stable tile-bits sort of instances emitted in gid order, each tile's slice holds
+// its Gaussians in gid order; sorting the slice by the unique 64-bit key (depth bits << 32 |
+// gid) gives exactly the canonical order.  Bitonic network in the all-ascending ("flip")
+// form, so padding keys (all ones) stay at the top and a virtually padded global slice needs
+// no storage beyond its n entries.  Integer work: LDS-latency-bound, no MFMA.
+// key of slice entry i: the depth key carried through the tile sort (sdepth, contiguous) or,
+// without it, gathered per instance from the Gaussian's depth key (random 4-B reads)
+__device__ __forceinline__ uint64_t depth_gid_key(const uint32_t* __restrict__ depth_key,
+                                                  const uint32_t* __restrict__ sdepth, uint32_t pos, uint32_t g) {
+    return ((uint64_t)(sdepth ? sdepth[pos] : depth_key[g]) << 32) | g;
+}
+
+template <int NT>
+__device__ __forceinline__ void bitonic_lds(uint64_t* k, int m) {
+    for (int size = 2; size <= m; size <<= 1) {
+        const int half = size >> 1;
+        for (int t = threadIdx.x; t < (m >> 1); t += NT) {
+            const int i = ((t & ~(half - 1)) << 1) | (t & (half - 1));
+            const int j = i ^ (size - 1);  // mirror partner within the size block
+            const uint64_t a = k[i], b = k[j];
+            if (a > b) {
+                k[i] = b;
+                k[j] = a;
+            }
+        }
+        __syncthreads();
+        for (int d = half >> 1; d >= 1; d >>= 1) {
+            for (int t = threadIdx.x; t < (m >> 1); t += NT) {
+                const int i = ((t & ~(d - 1)) << 1) | (t & (d - 1));
+                const int j = i + d;
+                const uint64_t a = k[i], b = k[j];
+                if (a > b) {
+                    k[i] = b;
+                    k[j] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__device__ __forceinline__ int pow2_at_least(int n) {
+    int m = 1;
+    while (m < n) m <<= 1;
+    return m;
+}
+
+// Small form: one block of NT threads per tile, slices of up to CAP instances in LDS; longer
+// slices are queued for tile_depth_sort_large.  The host picks CAP from the mean instances per
+// tile (launch_tile_depth_sort), so the queue stays empty on ordinary scenes.
+template <int CAP, int NT>
+__global__ __launch_bounds__(NT) void tile_depth_sort_small(const uint2* __restrict__ ranges, int tile0,
+                                                            const uint32_t* __restrict__ depth_key,
+                                                            const uint32_t* __restrict__ sdepth,
+                                                            uint32_t* __restrict__ gid, uint32_t* __restrict__ ovf,
+                                                            uint32_t* __restrict__ ovf_count) {
+    __shared__ uint64_t k[CAP];
+    const int tile = tile0 + blockIdx.x;
+    const uint2 r = ranges[tile];
+    const int n = (int)(r.y - r.x);
+    if (n <= 1) return;
+    if (n > CAP) {
+        if (threadIdx.x == 0) ovf[atomicAdd(ovf_count, 1u)] = (uint32_t)tile;
+        return;
+    }
+    const int m = pow2_at_least(n);
+    for (int i = threadIdx.x; i < m; i += NT)
+        k[i] = i < n ? depth_gid_key(depth_key, sdepth, r.x + i, gid[r.x + i]) : ~0ull;
+    __syncthreads();
+    bitonic_lds<NT>(k, m);
+    for (int i = threadIdx.x; i < n; i += NT) gid[r.x + i] = (uint32_t)k[i];
+}
+
+// Radix form (shipped for stable input): when the tile's slice is already in gid order (the
+// stable tile-key sort of gid-order emissions, GSR_BIN_VARIANT 1), a stable LSD sort of the
+// 32-bit depth keys alone gives (depth, gid) order.  Four 8-bit passes in LDS, each ranked
+// exactly as radix_downsweep ranks (wave64 ballot peer match, per-wave digit counters, a
+// digit-major block scan): ~20 B of LDS traffic per key per pass, against ~log2(n)^2 / 2 x 12 B
+// for the bitonic network, which is LDS-bandwidth-bound.  Measured at 1M/1080p: radix 0.102 ms,
+// bitonic 0.130 ms; rocprofv3 shows the radix form VALU-issue-bound (the 8-ballot peer match
+// per 64 keys per pass).  Passes whose digit is equal for every key of the slice are skipped.
+// NT threads, I items per thread: CAP = NT * I keys; wave w owns the contiguous run
+// [w * 64 I, (w + 1) * 64 I) of the slice, ranked round by round in index order (stable).
+template <int NT, int I>
+__global__ __launch_bounds__(NT) void tile_depth_radix(const uint2* __restrict__ ranges, int tile0,
+                                                      const uint32_t* __restrict__ depth_key,
+                                                      const uint32_t* __restrict__ sdepth,
+                                                      uint32_t* __restrict__ gid, uint32_t* __restrict__ ovf,
+                                                      uint32_t* __restrict__ ovf_count) {
+    constexpr int NWV = NT / 64, CAP = NT * I;
+    __shared__ uint32_t wcnt[NWV][256];
+    __shared__ uint32_t lbase[256];
+    __shared__ uint32_t wsum[NWV];
+    __shared__ uint32_t red[2][NWV];
+    __shared__ uint32_t skey[CAP];
+    __shared__ uint32_t sval[CAP];
+    const int tile = tile0 + blockIdx.x;
+    const uint2 rg = ranges[tile];
+    const int n = (int)(rg.y - rg.x);
+    if (n <= 1) return;
+    if (n > CAP) {
+        if (threadIdx.x == 0) ovf[atomicAdd(ovf_count, 1u)] = (uint32_t)tile;
+        return;
+    }
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    // wave w owns [w * per, (w + 1) * per): per = the slice split evenly over the waves in whole
+    // 64-lane rounds (<= 64 I since n <= CAP)
+    const int per = (n + NWV * 64 - 1) / (NWV * 64) * 64;
+    const int base = w * per;
+    const int end = base + per < n ? base + per : n;
+    uint32_t key[I], val[I], rank[I];
+    uint32_t kor = 0u, kand = 0xFFFFFFFFu;
+#pragma unroll
+    for (int r = 0; r < I; ++r) {
+        const int idx = base + r * 64 + lane;
+        const bool valid = idx < end;
+        val[r] = valid ? gid[rg.x + idx] : 0u;
+        key[r] = valid ? (sdepth ? sdepth[rg.x + idx] : depth_key[val[r]]) : 0xFFFFFFFFu;
+        if (valid) {
+            kor |= key[r];
+            kand &= key[r];
+        }
+    }
+    // bits where the slice's keys differ: passes over constant digits are no-ops (stable)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        kor |= __shfl_xor(kor, o, 64);
+        kand &= __shfl_xor(kand, o, 64);
+    }
+    if (lane == 0) {
+        red[0][w] = kor;
+        red[1][w] = kand;
+    }
+    __syncthreads();
+    uint32_t diff = 0u;
+    {
+        uint32_t o_ = 0u, a_ = 0xFFFFFFFFu;
+#pragma unroll
+        for (int k = 0; k < NWV; ++k) {
+            o_ |= red[0][k];
+            a_ &= red[1][k];
+        }
+        diff = o_ ^ a_;
+    }
+    const uint64_t lt = lanemask_lt();
+    for (int shift = 0; shift < 32; shift += 8) {
+        if (((diff >> shift) & 0xFFu) == 0u) continue;  // block-uniform
+        for (int d = tid; d < NWV * 256; d += NT) (&wcnt[0][0])[d] = 0u;
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < I; ++r) {
+            if (base + r * 64 >= end) break;  // wave-uniform: only the rounds holding keys
+            const int idx = base + r * 64 + lane;
+            const bool valid = idx < end;
+            const uint32_t d = (key[r] >> shift) & 0xFFu;
+            const uint64_t peers = match_digit(d, 8, __ballot(valid));
+            const uint32_t old = wcnt[w][d];
+            rank[r] = old + (uint32_t)__popcll(peers & lt);
+            if (valid && (peers & lt) == 0) wcnt[w][d] = old + (uint32_t)__popcll(peers);
+        }
+        __syncthreads();
+        // per digit: wave prefixes in place, then the digit-major block scan -> lbase
+        for (int d = tid; d < 256; d += NT) {
+            uint32_t c = 0;
+#pragma unroll
+            for (int k = 0; k < NWV; ++k) {
+                const uint32_t t = wcnt[k][d];
+                wcnt[k][d] = c;
+                c += t;
+            }
+            lbase[d] = c;
+        }
+        __syncthreads();
+        if (tid < 64) {  // exclusive scan of the 256 digit totals, 4 per lane
+            uint32_t c4[4], s4 = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                c4[q] = lbase[4 * tid + q];
+                s4 += c4[q];
+            }
+            uint32_t x = s4;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o, 64);
+                if (lane >= o) x += y;
+            }
+            uint32_t run = x - s4;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                lbase[4 * tid + q] = run;
+                run += c4[q];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < I; ++r) {
+            const int idx = base + r * 64 + lane;
+            if (idx < end) {
+                const uint32_t d = (key[r] >> shift) & 0xFFu;
+                const uint32_t lp = lbase[d] + wcnt[w][d] + rank[r];
+                skey[lp] = key[r];
+                sval[lp] = val[r];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < I; ++r) {
+            const int idx = base + r * 64 + lane;
+            if (idx < end) {
+                key[r] = skey[idx];
+                val[r] = sval[idx];
+            }
+        }
+        __syncthreads();  // skey / sval / wcnt are rewritten by the next pass
+    }
+#pragma unroll
+    for (int r = 0; r < I; ++r) {
+        const int idx = base + r * 64 + lane;
+        if (idx < end) gid[rg.x + idx] = val[r];
+    }
+}
+
+// Large form: the queued tiles, 1024 threads per block.  Up to kLargeLds instances in LDS;
+// beyond that (dense real scenes) the same network runs on the slice in global memory, with
+// the key split into two u32 arrays (the tile sort's free ping-pong pair), virtually padded.
+constexpr int kLargeLds = 8192;
+__global__ __launch_bounds__(1024) void tile_depth_sort_large(const uint2* __restrict__ ranges,
+                                                              const uint32_t* __restrict__ depth_key,
+                                                              const uint32_t* __restrict__ sdepth,
+                                                              uint32_t* __restrict__ gid,
+                                                              const uint32_t* __restrict__ ovf,
+                                                              const uint32_t* __restrict__ ovf_count,
+                                                              uint32_t* __restrict__ hi, uint32_t* __restrict__ lo) {
+    extern __shared__ uint64_t kl[];
+    const uint32_t cnt = *ovf_count;
+    for (uint32_t q = blockIdx.x; q < cnt; q += gridDim.x) {
+        const uint2 r = ranges[ovf[q]];
+        const int n = (int)(r.y - r.x);
+        const int m = pow2_at_least(n);
+        if (m <= kLargeLds) {
+            for (int i = threadIdx.x; i < m; i += 1024)
+                kl[i] = i < n ? depth_gid_key(depth_key, sdepth, r.x + i, gid[r.x + i]) : ~0ull;
+            __syncthreads();
+            bitonic_lds<1024>(kl, m);
+            for (int i = threadIdx.x; i < n; i += 1024) gid[r.x + i] = (uint32_t)kl[i];
+            __syncthreads();
+            continue;
+        }
+        uint32_t* H = hi + r.x;
+        uint32_t* L = lo + r.x;
+        for (int i = threadIdx.x; i < n; i += 1024) {
+            const uint32_t g = gid[r.x + i];
+            H[i] = sdepth ? sdepth[r.x + i] : depth_key[g];
+            L[i] = g;
+        }
+        __syncthreads();
+        auto cex = [&](int i, int j) {  // i < j; indices >= n are +inf padding
+            if (j >= n) return;
+            const uint64_t a = ((uint64_t)H[i] << 32) | L[i], b = ((uint64_t)H[j] << 32) | L[j];
+            if (a > b) {
+                H[i] = (uint32_t)(b >> 32), L[i] = (uint32_t)b;
+                H[j] = (uint32_t)(a >> 32), L[j] = (uint32_t)a;
+            }
+        };
+        for (int size = 2; size <= m; size <<= 1) {
+            const int half = size >> 1;
+            for (int t = threadIdx.x; t < (m >> 1); t += 1024) {
+                const int i = ((t & ~(half - 1)) << 1) | (t & (half - 1));
+                cex(i, i ^ (size - 1));
+            }
+            __threadfence_block();
+            __syncthreads();
+            for (int d = half >> 1; d >= 1; d >>= 1) {
+                for (int t = threadIdx.x; t < (m >> 1); t += 1024) {
+                    const int i = ((t & ~(d - 1)) << 1) | (t & (d - 1));
+                    cex(i, i + d);
+                }
+                __threadfence_block();
+                __syncthreads();
+            }
+        }
+        for (int i = threadIdx.x; i < n; i += 1024) gid[r.x + i] = L[i];
+        __syncthreads();
+    }
+}
 }  // namespace
 
 // A/B selector (bench/ablation only; read per call like the blend variants):
@@ -762,14 +1144,25 @@ static bool upsweep_atomic() {
 // blocks -- for the small candidate sets of multi-GPU bands, where a pass is latency-bound).
 static int onesweep_items(long long n) {
     const char* e = std::getenv("GSR_ONESWEEP_ITEMS");
-    if (e) return std::atoi(e) == 4 ? 4 : 16;
+    if (e) {
+        const int v = std::atoi(e);
+        return v == 4 || v == 8 ? v : 16;
+    }
     return n <= kOnesweepSmall ? 4 : 16;
+}
+
+// Look-back window of the onesweep passes: 8 predecessor words per probe (shipped) or 1.
+static int lookback_window() {
+    const char* e = std::getenv("GSR_LOOKBACK");
+    const int v = e ? std::atoi(e) : 8;
+    return v == 1 || v == 32 ? v : 8;
 }
 
 static int radix_sort_onesweep(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* k0, uint32_t* v0,
                                uint32_t* k1, uint32_t* v1, long long n, int nbits, uint32_t* hist, int* which,
                                hipStream_t s) {
     const int items = onesweep_items(n);
+    const int lb = lookback_window();
     const int nb = div_up(n, (long long)kB * items);  // look-back tiles
     const int nbh = sort_blocks(n);                  // histogram blocks
     const int npass = (nbits + 7) / 8;
@@ -787,12 +1180,18 @@ static int radix_sort_onesweep(const uint32_t* keys_in, const uint32_t* vals_in,
         const int bits = (nbits - shift) < 8 ? (nbits - shift) : 8;
         uint32_t* ko = dst == 0 ? k0 : k1;
         uint32_t* vo = dst == 0 ? v0 : v1;
-        if (items == 4)
-            hipLaunchKernelGGL(radix_onesweep<4>, dim3(nb), dim3(kB), 0, s, kin, vin, ko, vo, n, shift, bits,
-                               ghist + 256 * p, status + (size_t)p * nb * 256, tickets + p);
-        else
-            hipLaunchKernelGGL(radix_onesweep<16>, dim3(nb), dim3(kB), 0, s, kin, vin, ko, vo, n, shift, bits,
-                               ghist + 256 * p, status + (size_t)p * nb * 256, tickets + p);
+        uint32_t* st = status + (size_t)p * nb * 256;
+#define GSR_ONESWEEP(KI_, LB_)                                                                          \
+    hipLaunchKernelGGL((radix_onesweep<KI_, LB_>), dim3(nb), dim3(kB), 0, s, kin, vin, ko, vo, n, shift, bits, \
+                       ghist + 256 * p, st, tickets + p)
+        if (items == 4) {
+            if (lb == 1) GSR_ONESWEEP(4, 1); else if (lb == 32) GSR_ONESWEEP(4, 32); else GSR_ONESWEEP(4, 8);
+        } else if (items == 8) {
+            if (lb == 1) GSR_ONESWEEP(8, 1); else if (lb == 32) GSR_ONESWEEP(8, 32); else GSR_ONESWEEP(8, 8);
+        } else {
+            if (lb == 1) GSR_ONESWEEP(16, 1); else if (lb == 32) GSR_ONESWEEP(16, 32); else GSR_ONESWEEP(16, 8);
+        }
+#undef GSR_ONESWEEP
         kin = ko;
         vin = vo;
         *which = dst;
@@ -803,29 +1202,36 @@ static int radix_sort_onesweep(const uint32_t* keys_in, const uint32_t* vals_in,
 
 int radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* k0, uint32_t* v0,
                uint32_t* k1, uint32_t* v1, long long n, int nbits, uint32_t* hist, int* which,
-               hipStream_t s, bool depth_sort) {
+               hipStream_t s, bool depth_sort, const uint32_t* v2_in, uint32_t* v2_0, uint32_t* v2_1) {
     *which = -1;
     if (n <= 0) return 0;
-    if (use_onesweep(depth_sort))
+    if (use_onesweep(depth_sort) && !v2_in)
         return radix_sort_onesweep(keys_in, vals_in, k0, v0, k1, v1, n, nbits, hist, which, s);
     const int nb = sort_blocks(n);
     uint32_t* totals = hist + (size_t)256 * (nb + 1);
     const uint32_t* kin = keys_in;
     const uint32_t* vin = vals_in;
+    const uint32_t* v2in = v2_in;
     int dst = 0;
     for (int shift = 0; shift < nbits; shift += 8) {
         const int bits = (nbits - shift) < 8 ? (nbits - shift) : 8;
         uint32_t* ko = dst == 0 ? k0 : k1;
         uint32_t* vo = dst == 0 ? v0 : v1;
+        uint32_t* v2o = dst == 0 ? v2_0 : v2_1;
         if (upsweep_atomic())
             hipLaunchKernelGGL(radix_upsweep_atomic, dim3(nb), dim3(kB), 0, s, kin, n, shift, bits, nb, hist);
         else
             hipLaunchKernelGGL(radix_upsweep, dim3(nb), dim3(kB), 0, s, kin, n, shift, bits, nb, hist);
         hipLaunchKernelGGL(radix_colscan, dim3(256), dim3(kB), 0, s, hist, nb, totals);
-        hipLaunchKernelGGL(radix_downsweep, dim3(nb), dim3(kB), 0, s, kin, vin, ko, vo, n, shift, bits, nb,
-                           hist, totals);
+        if (v2in)
+            hipLaunchKernelGGL(radix_downsweep<true>, dim3(nb), dim3(kB), 0, s, kin, vin, ko, vo, n, shift, bits, nb,
+                               hist, totals, v2in, v2o);
+        else
+            hipLaunchKernelGGL(radix_downsweep<false>, dim3(nb), dim3(kB), 0, s, kin, vin, ko, vo, n, shift, bits, nb,
+                               hist, totals, nullptr, nullptr);
         kin = ko;
         vin = vo;
+        v2in = v2in ? v2o : nullptr;
         *which = dst;
         dst ^= 1;
     }
@@ -833,12 +1239,12 @@ int radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* k0, u
 }
 
 int inclusive_scan_gather(const uint32_t* in, const uint32_t* idx, uint32_t* out, int n,
-                          uint32_t* partials, hipStream_t s) {
+                          uint32_t* partials, hipStream_t s, uint32_t* iota_out) {
     if (n <= 0) return 0;
     const int nb = sort_blocks(n);
     hipLaunchKernelGGL(scan_reduce, dim3(nb), dim3(kB), 0, s, in, idx, n, partials);
     hipLaunchKernelGGL(scan_partials, dim3(1), dim3(1024), 0, s, partials, nb);
-    hipLaunchKernelGGL(scan_downsweep, dim3(nb), dim3(kB), 0, s, in, idx, n, partials, out);
+    hipLaunchKernelGGL(scan_downsweep, dim3(nb), dim3(kB), 0, s, in, idx, n, partials, out, iota_out);
     return (int)hipGetLastError();
 }
 
@@ -855,23 +1261,81 @@ int compact_candidates(const uint32_t* tiles, const uint32_t* depth_key, int n, 
 
 int launch_duplicate(const uint32_t* gid_by_rank, const uint32_t* offsets, const uint32_t* tiles,
                      uint4* rect, int P, int grid_x, int ty0, int ty1, uint32_t* tkey, uint32_t* inst_gid,
-                     hipStream_t s) {
+                     hipStream_t s, uint32_t* tcount, const uint32_t* depth_key, uint32_t* inst_depth) {
     if (P <= 0) return 0;
     hipLaunchKernelGGL(duplicate_kernel, dim3(div_up(P, 256)), dim3(256), 0, s, gid_by_rank, offsets,
-                       tiles, rect, P, grid_x, ty0, ty1, tkey, inst_gid);
+                       tiles, rect, P, grid_x, ty0, ty1, tkey, inst_gid, tcount, depth_key, inst_depth);
     return (int)hipGetLastError();
 }
 
 int launch_scan_duplicate(const uint32_t* gid_by_rank, const uint32_t* tiles, uint4* rect, int n,
                           int grid_x, int ty0, uint32_t* offsets, uint32_t* tkey, uint32_t* inst_gid,
-                          uint32_t* scratch, hipStream_t s) {
+                          uint32_t* scratch, hipStream_t s, uint32_t* tcount, const uint32_t* depth_key,
+                          uint32_t* inst_depth) {
     if (n <= 0) return 0;
     const int nb = div_up(n, 256);
     uint32_t* ticket = scratch;
     uint32_t* status = scratch + 16;
     if (hipError_t e = hipMemsetAsync(scratch, 0, sizeof(uint32_t) * (16 + (size_t)nb), s)) return (int)e;
     hipLaunchKernelGGL(scan_duplicate_kernel, dim3(nb), dim3(256), 0, s, gid_by_rank, tiles, rect, n, grid_x, ty0,
-                       offsets, tkey, inst_gid, status, ticket);
+                       offsets, tkey, inst_gid, status, ticket, tcount, depth_key, inst_depth);
+    return (int)hipGetLastError();
+}
+
+// Per-tile sort form (A/B, bench/ablation only): 1 (shipped) = LDS radix when the slices are
+// in gid order, 0 = bitonic network (always used for unordered slices).
+static int tile_sort_variant() {
+    const char* e = std::getenv("GSR_TILESORT_VARIANT");
+    return e ? std::atoi(e) : 1;
+}
+
+int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long K, const uint32_t* depth_key,
+                           uint32_t* gid, uint32_t* ovf, uint32_t* ovf_count, uint32_t* scratch_hi,
+                           uint32_t* scratch_lo, hipStream_t s, bool gid_ordered, const uint32_t* sdepth) {
+    if (ntiles <= 0 || K <= 0) return 0;
+    // capacity of the LDS form: a power of two >= 1.5x the mean slice, 1024 .. 8192
+    const long long mean = K / ntiles;
+    int cap = 1024;
+    while (cap < 8192 && cap < mean + mean / 2) cap <<= 1;
+    if (gid_ordered && tile_sort_variant() == 1) {
+        if (cap == 1024)
+            hipLaunchKernelGGL((tile_depth_radix<256, 4>), dim3(ntiles), dim3(256), 0, s, ranges, tile0, depth_key, sdepth, gid,
+                               ovf, ovf_count);
+        else if (cap == 2048)
+            hipLaunchKernelGGL((tile_depth_radix<256, 8>), dim3(ntiles), dim3(256), 0, s, ranges, tile0, depth_key, sdepth, gid,
+                               ovf, ovf_count);
+        else if (cap == 4096)
+            hipLaunchKernelGGL((tile_depth_radix<256, 16>), dim3(ntiles), dim3(256), 0, s, ranges, tile0, depth_key, sdepth, gid,
+                               ovf, ovf_count);
+        else
+            hipLaunchKernelGGL((tile_depth_radix<512, 16>), dim3(ntiles), dim3(512), 0, s, ranges, tile0, depth_key, sdepth, gid,
+                               ovf, ovf_count);
+    } else if (cap == 1024)
+        hipLaunchKernelGGL((tile_depth_sort_small<1024, 256>), dim3(ntiles), dim3(256), 0, s, ranges, tile0, depth_key,
+                           sdepth, gid, ovf, ovf_count);
+    else if (cap == 2048)
+        hipLaunchKernelGGL((tile_depth_sort_small<2048, 256>), dim3(ntiles), dim3(256), 0, s, ranges, tile0, depth_key,
+                           sdepth, gid, ovf, ovf_count);
+    else if (cap == 4096)
+        hipLaunchKernelGGL((tile_depth_sort_small<4096, 512>), dim3(ntiles), dim3(512), 0, s, ranges, tile0, depth_key,
+                           sdepth, gid, ovf, ovf_count);
+    else
+        hipLaunchKernelGGL((tile_depth_sort_small<8192, 1024>), dim3(ntiles), dim3(1024), 0, s, ranges, tile0,
+                           depth_key, sdepth, gid, ovf, ovf_count);
+    // the rare longer slices: the queue length is on the device; 64 blocks drain it (blocks
+    // past the count exit at once)
+    const int grid = ntiles < 64 ? ntiles : 64;
+    hipLaunchKernelGGL(tile_depth_sort_large, dim3(grid), dim3(1024), sizeof(uint64_t) * kLargeLds, s, ranges,
+                       depth_key, sdepth, gid, ovf, ovf_count, scratch_hi, scratch_lo);
+    return (int)hipGetLastError();
+}
+
+int launch_tile_bins(const uint32_t* tkey, const uint32_t* gid, long long K, int tile0, int ntiles,
+                     uint32_t* tcount, uint2* ranges, uint32_t* stile, uint32_t* sgid, hipStream_t s) {
+    if (K <= 0 || ntiles <= 0) return 0;
+    if (!tcount) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(tile_offsets_kernel, dim3(1), dim3(1024), 0, s, tcount, tile0, ntiles, ranges);
+    hipLaunchKernelGGL(tile_scatter_kernel, dim3(div_up(K, 256)), dim3(256), 0, s, tkey, gid, K, tcount, stile, sgid);
     return (int)hipGetLastError();
 }
 

@@ -162,8 +162,9 @@ int gsr_backward_preprocess_range(const gsr_camera* cam, const gsr_gaussians* gs
                                        termination point from T                             */
 #define GSR_VIEW_DEPTH_KEY 6        /* uint32[P]: depth bits, 0xFFFFFFFF when culled       */
 #define GSR_VIEW_TILES_TOUCHED 7    /* uint32[P]                                           */
-#define GSR_VIEW_GID_BY_RANK 9      /* uint32[num_ranked]: Gaussian ids in depth order (a band's
-                                       candidates: exactly the Gaussians it can touch)      */
+#define GSR_VIEW_GID_BY_RANK 9      /* uint32[num_ranked]: the ranked Gaussian ids -- ascending
+                                       (shipped binning; depth order under GSR_BIN_VARIANT=0);
+                                       a band's candidates: exactly the Gaussians it can touch */
 #define GSR_VIEW_RECORDS 8          /* float4[3*P]: {x,y,a',b'},{c',o,r,g},{b,ext_x,ext_y,log2 o};
                                        a',b',c' = -log2(e) * (A/2, B, C/2) of the conic */
 const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, int what);
@@ -173,7 +174,8 @@ const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, 
  * call's stream; gsr_profile_read synchronises those events and returns the accumulated
  * milliseconds and launch counts per stage (arrays of GSR_NUM_STAGES), then resets. */
 #define GSR_STAGE_PREPROCESS 0     /* F1 */
-#define GSR_STAGE_DEPTH_SORT 1     /* depth-key LSD sort of the P Gaussians */
+#define GSR_STAGE_DEPTH_SORT 1     /* depth order: per-tile depth sort (shipped) or the global
+                                      depth-key LSD sort of the P Gaussians; band compaction */
 #define GSR_STAGE_SCAN 2           /* F2 scan of tiles_touched (rank order) */
 #define GSR_STAGE_DUPLICATE 3      /* F3 */
 #define GSR_STAGE_TILE_SORT 4      /* F4 tile-key LSD sort of the K instances */

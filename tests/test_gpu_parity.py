@@ -122,14 +122,18 @@ def test_band_sharded_equals_full(rast):
     for y0, y1 in bands:
         st = rast.forward(*args, sh_degree=3, tile_rows=(y0, y1))
         img[:, y0 * 16:y1 * 16] = st.color[:, y0 * 16:y1 * 16]
-        # the band ranks exactly its candidates (Gaussians with tiles in the band), depth-sorted
+        # the band ranks exactly its candidates (Gaussians with tiles in the band): in gid
+        # order (shipped binning, per-tile depth order) or depth-sorted (GSR_BIN_VARIANT=0)
         native = pkg("native")
         nr = st.buffers.num_ranked
         cand = _np(st.view(native.VIEW_GID_BY_RANK, torch.int32, nr)).astype(np.int64)
         tt = _np(st.view(native.VIEW_TILES_TOUCHED, torch.int32, s.P))
         key = _np(st.view(native.VIEW_DEPTH_KEY, torch.int32, s.P)).view(np.uint32)
         np.testing.assert_array_equal(np.sort(cand), np.nonzero(tt)[0])
-        assert np.all(np.diff(key[cand].astype(np.int64)) >= 0)
+        if os.environ.get("GSR_BIN_VARIANT", "2") == "0":
+            assert np.all(np.diff(key[cand].astype(np.int64)) >= 0)
+        else:
+            assert np.all(np.diff(cand) > 0)
         g2 = rast.backward_blend(st, dpix)
         grad2d = g2 if grad2d is None else grad2d + g2
         last = st
@@ -160,6 +164,36 @@ def test_band_only_flag(rast):
     rest[cand] = False
     assert bool(torch.isnan(g2[rest]).all())  # untouched
     assert float(g_ref[rest].abs().max()) == 0.0
+
+
+def test_dense_tiles_sort_paths(rast, oracle):
+    """Tiles holding more instances than the per-tile depth sort's shared-memory form takes:
+    (a) 60k Gaussians on a 64x48 image (12 tiles, ~10^4 instances each) exercise the
+    global-memory form beyond 8192; (b) a cluster of 6000 Gaussians in the middle of a
+    sparse 256x256 scene overflows a 1024-slot tile into the 8192-slot LDS form.  Canonical
+    order, ranges and outputs must still match the oracle."""
+    gr, sc = pkg("graphics"), pkg("scene")
+    cam = gr.synthetic_camera(64, 48)
+    s = sc.make_scene(cam, 60000, max_sh_degree=1, seed=11)
+    args = (cam, s.means3D, s.opacities, s.scales, s.rotations, s.sh_dc, s.sh_rest)
+    st = rast.forward(*args, sh_degree=1)
+    f = oracle.forward(*args, sh_degree=1)
+    tiles = cam.grid[0] * cam.grid[1]
+    rng = _np(st.view(pkg("native").VIEW_RANGES, torch.int32, 2 * tiles)).view(np.uint32).reshape(-1, 2)
+    assert int((rng[:, 1] - rng[:, 0]).max()) > 8192
+    _compare(st, f, sc.make_dL_dpix(cam, seed=12), rast)
+
+    cam = gr.synthetic_camera(256, 256)
+    s = sc.make_scene(cam, 20000, max_sh_degree=1, seed=13)
+    s.means3D[:6000, :2] *= 0.02  # pile 6000 Gaussians onto the centre tiles
+    args = (cam, s.means3D, s.opacities, s.scales, s.rotations, s.sh_dc, s.sh_rest)
+    st = rast.forward(*args, sh_degree=1)
+    f = oracle.forward(*args, sh_degree=1)
+    tiles = cam.grid[0] * cam.grid[1]
+    rng = _np(st.view(pkg("native").VIEW_RANGES, torch.int32, 2 * tiles)).view(np.uint32).reshape(-1, 2)
+    n = rng[:, 1] - rng[:, 0]
+    assert 1024 < int(n.max()) <= 8192 and float(n.mean()) < 1024
+    _compare(st, f, sc.make_dL_dpix(cam, seed=14), rast)
 
 
 def test_empty_and_culled(rast):
