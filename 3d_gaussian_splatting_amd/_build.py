@@ -32,6 +32,8 @@ HIP_SOURCES = {
     "gsr_preprocess_bwd.hip": ["-ffp-contract=off"],
     # training-step kernels (loss, fused Adam, densification): tolerance-compared, default flags
     "gsr_train.hip": [],
+    # point-cloud initialisation (exact k-NN): box and point distances must round alike
+    "gsr_init.hip": ["-ffp-contract=off"],
     "gsr_api.cpp": [],
 }
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fno-fast-math",
@@ -54,7 +56,7 @@ def _stamp(paths, extra=""):
 
 
 def _headers():
-    out = [os.path.join(ROOT, "include", "gsr", "gsr.h")]
+    out = [os.path.join(ROOT, "include", "gsr", h) for h in ("gsr.h", "gsr_train.h")]
     out += [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     return out
 

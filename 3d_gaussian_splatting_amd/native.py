@@ -29,7 +29,8 @@ EXPORTS = ["gsr_abi_version", "gsr_last_error", "gsr_forward", "gsr_backward", "
            "gsr_stage_name"]
 # include/gsr/gsr_train.h (training-step kernels)
 TRAIN_EXPORTS = ["gsr_activate", "gsr_loss_scratch_bytes", "gsr_loss_forward", "gsr_loss_backward", "gsr_adam_step",
-                 "gsr_densify_stats", "gsr_compact_scratch_bytes", "gsr_compact_index", "gsr_gather_rows"]
+                 "gsr_densify_stats", "gsr_compact_scratch_bytes", "gsr_compact_index", "gsr_gather_rows",
+                 "gsr_knn_scratch_bytes", "gsr_knn_mean_dist2"]
 ACT_NONE, ACT_EXP, ACT_SIGMOID, ACT_NORMALIZE4 = range(4)
 ADAM_MAX_GROUPS = 8
 GATHER_MAX = 24
@@ -149,6 +150,10 @@ def load_hip() -> ctypes.CDLL:
         L.gsr_compact_index.argtypes = [vp, i32, vp, vp, vp, vp]
         L.gsr_gather_rows.restype = ctypes.c_int
         L.gsr_gather_rows.argtypes = [ctypes.POINTER(RowCopy), i32, vp, i32, vp]
+        L.gsr_knn_scratch_bytes.restype = ctypes.c_size_t
+        L.gsr_knn_scratch_bytes.argtypes = [i32]
+        L.gsr_knn_mean_dist2.restype = ctypes.c_int
+        L.gsr_knn_mean_dist2.argtypes = [vp, i32, vp, vp, vp]
         _hip = L
     return _hip
 

@@ -19,6 +19,9 @@ What it mirrors in the reference (seiya-kumada/3d_gaussian_splatting):
 * densify_and_clone / densify_and_split / prune_points / reset_opacity: the upstream 3DGS
   semantics the reference's stats tensors exist for (the reference has no densification
   code).
+* ``capture`` / ``restore``: GaussianModel::capture / restore (gaussian_model.cpp:76-267);
+  ``from_point_cloud`` / ``save_ply`` / ``from_ply``: the upstream create_from_pcd / save_ply /
+  load_ply, the k-NN scale initialisation on the GPU.
 
 Device work per iteration, all through the C ABI: gsr_activate -> gsr_forward -> loss
 forward/backward -> gsr_backward -> gsr_densify_stats -> gsr_adam_step (one launch for the
@@ -32,9 +35,10 @@ import ctypes
 import math
 from dataclasses import dataclass
 
+import numpy as np
 import torch
 
-from . import native
+from . import native, scene_io
 from .general import build_rotation, get_expon_lr_func
 from .rasterizer import CAbiRasterizer
 
@@ -153,6 +157,19 @@ class TrainKernels:
                     "gsr_compact_index")
         return idx[: int(cnt.item())]
 
+    def knn_mean_dist2(self, points: torch.Tensor) -> torch.Tensor:
+        """Mean squared distance of each point to its 3 nearest others (exact; gsr_knn_mean_dist2)."""
+        if not (points.is_contiguous() and points.dtype == torch.float32 and points.device == self.device):
+            raise ValueError(f"knn: points must be a contiguous f32 (N, 3) tensor on {self.device}")
+        n = int(points.shape[0])
+        out = torch.empty(n, dtype=torch.float32, device=self.device)
+        if n == 0:
+            return out
+        scratch = torch.empty(int(self.L.gsr_knn_scratch_bytes(n)), dtype=torch.uint8, device=self.device)
+        self._check(self.L.gsr_knn_mean_dist2(_p(points), n, _p(out), _p(scratch), _stream(self.device)),
+                    "gsr_knn_mean_dist2")
+        return out
+
     def gather_rows(self, tensors, idx: torch.Tensor):
         """[t[idx] for t in tensors] (rows) in one launch; tensors are (N, ...) f32."""
         n_out = int(idx.numel())
@@ -198,6 +215,66 @@ class GaussianTrainer:
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(seed)
         self.setup(opt or OptimizationParams())
+
+    @classmethod
+    def from_point_cloud(cls, points, colors, max_sh_degree: int, spatial_lr_scale: float,
+                         opt: OptimizationParams | None = None, device="cuda", seed: int = 0) -> "GaussianTrainer":
+        """Upstream create_from_pcd (the reference has none: its point-cloud branch is commented
+        out, src/scene/dataset_readers.cpp:198-219): means = the points, f_dc = RGB2SH(colour),
+        f_rest = 0, every scale axis = log(sqrt(max(d, 1e-7))) with d the mean squared distance to
+        the 3 nearest other points (gsr_knn_mean_dist2 on the GPU), rotation = (1, 0, 0, 0),
+        opacity = inverse_sigmoid(0.1); spatial_lr_scale = the cameras' extent."""
+        dev = _device(device)
+        pts = torch.as_tensor(np.asarray(points, np.float32), device=dev).reshape(-1, 3).contiguous()
+        n = int(pts.shape[0])
+        d2 = TrainKernels(dev).knn_mean_dist2(pts)
+        scales = torch.log(torch.sqrt(torch.clamp_min(d2, 1e-7)))[:, None].repeat(1, 3)
+        rots = torch.zeros((n, 4), dtype=torch.float32, device=dev)
+        rots[:, 0] = 1.0
+        o = torch.full((n, 1), 0.1, dtype=torch.float32, device=dev)
+        opac = torch.log(o / (1 - o))
+        rgb = torch.as_tensor(np.asarray(colors, np.float32), device=dev).reshape(-1, 3)
+        f_dc = ((rgb - 0.5) / scene_io.SH_C0)[:, None, :]
+        f_rest = torch.zeros((n, (max_sh_degree + 1) ** 2 - 1, 3), dtype=torch.float32, device=dev)
+        return cls(pts, f_dc, f_rest, opac, scales, rots, max_sh_degree, opt, spatial_lr_scale, dev, seed)
+
+    # ---------------------------------------------------------------- checkpoints / PLY
+    def capture(self, path: str) -> None:
+        """GaussianModel::capture (src/scene/gaussian_model.cpp:76-131, 228-246): parameters,
+        statistics, SH degree, spatial LR scale and every group's Adam state, one file."""
+        scene_io.save_checkpoint(path, {
+            "active_sh_degree": self.active_sh_degree, "spatial_lr_scale": self.spatial_lr_scale,
+            "params": self.params, "max_radii2D": self.max_radii2D, "xyz_gradient_accum": self.xyz_gradient_accum,
+            "denom": self.denom, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq, "steps": self.steps})
+
+    def restore(self, path: str, opt: OptimizationParams | None = None) -> None:
+        """GaussianModel::restore (gaussian_model.cpp:248-267): setup(opt), then the captured
+        tensors and Adam states replace the fresh ones."""
+        st = scene_io.load_checkpoint(path, self.device)
+        self.params = {k: v.contiguous() for k, v in st["params"].items()}
+        self.spatial_lr_scale = st["spatial_lr_scale"]
+        self.setup(opt or self.opt)
+        self.active_sh_degree = st["active_sh_degree"]
+        self.max_radii2D, self.xyz_gradient_accum, self.denom = st["max_radii2D"], st["xyz_gradient_accum"], st["denom"]
+        for k in self.params:
+            if k in st["exp_avg"]:
+                self.exp_avg[k] = st["exp_avg"][k].contiguous()
+                self.exp_avg_sq[k] = st["exp_avg_sq"][k].contiguous()
+                self.steps[k] = st["steps"][k]
+
+    def save_ply(self, path: str) -> None:
+        """The raw leaves in the upstream point-cloud PLY layout (scene_io.save_gaussians_ply)."""
+        scene_io.save_gaussians_ply(path, **self.params)
+
+    @classmethod
+    def from_ply(cls, path: str, max_sh_degree: int, opt: OptimizationParams | None = None,
+                 spatial_lr_scale: float = 1.0, device="cuda", seed: int = 0) -> "GaussianTrainer":
+        """Upstream load_ply: the leaves of a Gaussian PLY, active SH degree = max_sh_degree."""
+        g = scene_io.load_gaussians_ply(path, max_sh_degree)
+        tr = cls(g["xyz"], g["f_dc"], g["f_rest"], g["opacity"], g["scaling"], g["rotation"], max_sh_degree, opt,
+                 spatial_lr_scale, device, seed)
+        tr.active_sh_degree = max_sh_degree
+        return tr
 
     # ---------------------------------------------------------------- GaussianModel surface
     @property

@@ -98,6 +98,15 @@ typedef struct gsr_row_copy {
 int gsr_gather_rows(const gsr_row_copy* copies, int32_t ncopies, const int32_t* idx, int32_t n_out,
                     void* stream);
 
+/* Point-cloud initialisation (upstream create_from_pcd, whose distCUDA2 this
+ * replaces -- the reference's point-cloud branch is commented out,
+ * src/scene/dataset_readers.cpp:198-219): dist2[i] = mean of the squared distances from point i
+ * to its 3 nearest OTHER points (exact; with fewer than 3 other points the missing ones count as
+ * FLT_MAX, as in upstream's kernel, so the mean is FLT_MAX / 3 or overflows to +inf).
+ * points: N x 3 f32 device; scratch: gsr_knn_scratch_bytes(N) bytes. */
+size_t gsr_knn_scratch_bytes(int32_t N);
+int gsr_knn_mean_dist2(const float* points, int32_t N, float* dist2, void* scratch, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
