@@ -309,13 +309,10 @@ size_t gsr_image_bytes(int32_t w, int32_t h) {
 }
 size_t gsr_scratch_bytes(int32_t K) { return PartLayout(K).total; }
 
-int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
-                float* out_color, int32_t* radii, gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_binning,
-                gsr_alloc_fn alloc_image, void* ctx, gsr_buffers* bufs, void* stream_) {
-    g_err.clear();
-    if (int e = validate(cam, gs, rs)) return e;
-    if (!out_color || (gs->P > 0 && !radii) || !bufs || !alloc_geom || !alloc_binning || !alloc_image)
-        return fail(-1, "null output / allocator");
+// GSR_BIN_VARIANT=0 (A/B only): global depth sort of the P (or band-candidate) keys first.
+static int forward_global_depth(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
+                                float* out_color, int32_t* radii, gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_binning,
+                                gsr_alloc_fn alloc_image, void* ctx, gsr_buffers* bufs, void* stream_) {
     hipStream_t stream = (hipStream_t)stream_;
     const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
     const int P = gs->P;
@@ -349,103 +346,7 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
     GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(ranges, 0, il.ovf - il.ranges, stream), "memset ranges");
 
     long long K = 0;
-    const int bv = bin_variant();
-    if (P > 0 && bv != 0) {
-        // F1 -> [band: candidate compaction] -> F2 scan (gid order) -> F3 (+ per-tile counts)
-        // -> group by tile (count binning, or tile-key sort + F5) -> per-tile (depth, gid)
-        // order.  gid_by_rank = the identity (full image, written by the scan) or the band's
-        // candidates in gid order (written by the compaction).
-        const bool full_img = ty0 == 0 && ty1 == gy;
-        uint32_t* tcount = bv == 2 ? at<uint32_t>(bufs->image, il.tcount) : nullptr;
-        PreOut po{radii, depth_key, tiles, rec, at<uint4>(bufs->geom, gl.rect),
-                  full_img ? at<uint32_t>(bufs->geom, gl.flags) : nullptr, counters};
-        GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess(*cam, gauss_in(gs), ty0, ty1, po, stream), "preprocess");
-        uint32_t* gid_by_rank = at<uint32_t>(bufs->geom, gl.sA_v);
-        uint32_t cw[2 * kCountSlots];
-        uint64_t csum = 0, ksum = 0;
-        GSR_CHECK_HIP(begin_read(counters, 2 * kCountSlots, stream), "read counts");
-        int NR = P;
-        bool scanned = false;
-        if (!full_img) {
-            GSR_STAGE(GSR_STAGE_DEPTH_SORT, compact_candidates(tiles, depth_key, P, at<uint32_t>(bufs->geom, gl.partials),
-                                                               offsets, gid_by_rank, counters + kCandCountSlot, stream),
-                      "band candidates");
-        } else {
-            // the scan needs no count: enqueue it before the host waits for K
-            GSR_STAGE(GSR_STAGE_SCAN, inclusive_scan_gather(tiles, nullptr, offsets, P,
-                                                            at<uint32_t>(bufs->geom, gl.partials), stream, gid_by_rank),
-                      "scan");
-            scanned = true;
-        }
-        GSR_STAGE(GSR_STAGE_MISC, end_read(counters, cw, 2 * kCountSlots, stream), "read counts");
-        for (int i = 0; i < kCountSlots; ++i) csum += cw[i], ksum += cw[kCountSlots + i];
-        if (!full_img) {
-            NR = (int)(csum < (uint64_t)P ? csum : (uint64_t)P);
-            if (colour_pass_needed(*cam, gauss_in(gs), ty0, ty1))
-                GSR_STAGE(GSR_STAGE_PREPROCESS, launch_colour(*cam, gauss_in(gs), gid_by_rank, NR, rec, stream),
-                          "band colours");
-        }
-        bufs->num_ranked = NR;
-        K = (long long)ksum;
-        if (K > INT32_MAX) return fail(-3, "num_rendered overflow (%lld)", K);
-        bufs->num_rendered = (int32_t)K;
-        bufs->binning = alloc_binning(ctx, BinLayout(K).total);
-        if (!bufs->binning) return fail(-2, "allocation failed (binning, K=%lld)", K);
-        BinLayout bl(K);
-        uint32_t* kA = at<uint32_t>(bufs->binning, bl.kA);
-        uint32_t* vA = at<uint32_t>(bufs->binning, bl.vA);
-        uint32_t* kB = at<uint32_t>(bufs->binning, bl.kB);
-        uint32_t* vB = at<uint32_t>(bufs->binning, bl.vB);
-        uint32_t* inst_gid = at<uint32_t>(bufs->binning, bl.inst_gid);
-        // final (tile, gid) arrays where views() expects them, and the free pair beside them
-        const bool odd = (tile_passes(gx * gy) & 1) != 0;
-        uint32_t* fk = odd ? kB : kA;
-        uint32_t* fv = odd ? vB : vA;
-        uint32_t* sk = odd ? kA : kB;
-        uint32_t* sv = odd ? vA : vB;
-        uint32_t* dup_key = bv == 2 ? sk : kA;  // F3's tile keys (emission order)
-        // variant 1: F3 also writes each instance's depth key, the tile sort carries it, and
-        // the per-tile sort reads it contiguously instead of gathering depth_key[gid]
-        const bool carry = bv == 1 && carry_depth();
-        uint32_t* dA = at<uint32_t>(bufs->binning, bl.dA);
-        uint32_t* dB = at<uint32_t>(bufs->binning, bl.dB);
-        if (NR > 0 && !scanned && scan_variant(NR) == 1) {
-            GSR_STAGE(GSR_STAGE_DUPLICATE, launch_scan_duplicate(gid_by_rank, tiles, at<uint4>(bufs->geom, gl.rect), NR, gx,
-                                                                 ty0, offsets, dup_key, inst_gid,
-                                                                 at<uint32_t>(bufs->geom, gl.hist), stream, tcount,
-                                                                 depth_key, carry ? dA : nullptr),
-                      "scan + duplicate");
-        } else if (NR > 0) {
-            if (!scanned)
-                GSR_STAGE(GSR_STAGE_SCAN, inclusive_scan_gather(tiles, gid_by_rank, offsets, NR,
-                                                                at<uint32_t>(bufs->geom, gl.partials), stream),
-                          "scan");
-            GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate(gid_by_rank, offsets, tiles, at<uint4>(bufs->geom, gl.rect), NR,
-                                                            gx, ty0, ty1, dup_key, inst_gid, stream, tcount,
-                                                            depth_key, carry ? dA : nullptr),
-                      "duplicate");
-        }
-        if (K > 0) {
-            if (bv == 2) {
-                GSR_STAGE(GSR_STAGE_TILE_SORT, launch_tile_bins(sk, inst_gid, K, ty0 * gx, (ty1 - ty0) * gx, tcount, ranges,
-                                                                fk, fv, stream),
-                          "tile bins");
-            } else {
-                int w2 = -1;
-                GSR_STAGE(GSR_STAGE_TILE_SORT, radix_sort(kA, inst_gid, kB, vB, kA, vA, K, tile_bits(gx * gy),
-                                                          at<uint32_t>(bufs->binning, bl.hist), &w2, stream, false,
-                                                          carry ? dA : nullptr, dB, dA),
-                          "tile sort");
-                if ((w2 == 0) != odd) return fail(-12, "tile sort ended in an unexpected buffer");
-                GSR_STAGE(GSR_STAGE_FINALIZE, launch_finalize(fk, K, ranges, stream), "finalize");
-            }
-            GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_tile_depth_sort(ranges, ty0 * gx, (ty1 - ty0) * gx, K, depth_key, fv,
-                                                                   at<uint32_t>(bufs->image, il.ovf),
-                                                                   counters + kOvfCountSlot, sk, sv, stream, bv == 1,
-                                                                   carry ? (odd ? dB : dA) : nullptr),
-                      "per-tile depth order");
-        }
-    } else if (P > 0) {
+    if (P > 0) {
         const bool full_img = ty0 == 0 && ty1 == gy;
         PreOut po{radii, depth_key, tiles, rec, at<uint4>(bufs->geom, gl.rect),
                   full_img ? at<uint32_t>(bufs->geom, gl.flags) : nullptr, counters};
@@ -540,6 +441,269 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
                   "blend forward");
     return 0;
 }
+
+}  // extern "C"
+
+namespace {
+
+// One view's forward (binning variants 1 / 2), split at the host read of its instance count:
+// a batch enqueues phase 1 of every view before it waits once (gsr_forward_batch).
+struct FwdJob {
+    const gsr_camera* cam;
+    const gsr_gaussians* gs;
+    const gsr_raster_settings* rs;
+    float* out_color;
+    int32_t* radii;
+    gsr_buffers* bufs;
+    int ty0 = 0, ty1 = 0, gx = 0, gy = 0, ckt = 0;
+    bool full_img = true;
+};
+
+// Allocations, background / range clears, F1, then the scan (full image) or the band's
+// candidate compaction.  read_counts: enqueue the D2H of F1's count partials right after F1,
+// so the scan / compaction run while the host waits for them.
+int fwd_phase1(FwdJob& j, gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_image, void* ctx, hipStream_t stream,
+               bool debug, bool read_counts) {
+    const gsr_camera* cam = j.cam;
+    const gsr_gaussians* gs = j.gs;
+    const gsr_raster_settings* rs = j.rs;
+    gsr_buffers* bufs = j.bufs;
+    const int P = gs->P, W = cam->width, H = cam->height;
+    j.gx = div_up(W, kTile);
+    j.gy = div_up(H, kTile);
+    band(cam, rs, &j.ty0, &j.ty1);
+    j.full_img = j.ty0 == 0 && j.ty1 == j.gy;
+    std::memset(bufs, 0, sizeof *bufs);
+    bufs->geom = alloc_geom(ctx, GeomLayout(P).total);
+    j.ckt = chunked_tiles(W, j.ty0, j.ty1);
+    bufs->image = alloc_image(ctx, ImgLayout(W, H, j.ckt).total);
+    if (!bufs->geom || !bufs->image) return fail(-2, "allocation failed (geometry/image)");
+    GeomLayout gl(P);
+    ImgLayout il(W, H, j.ckt);
+    uint2* ranges = at<uint2>(bufs->image, il.ranges);
+    if (!j.full_img && !(rs->flags & GSR_FLAG_BAND_ONLY)) {
+        const int npix = W * H;
+        hipLaunchKernelGGL(fill_background, dim3(div_up(npix, 256)), dim3(256), 0, stream, j.out_color,
+                           at<float>(bufs->image, il.final_T), at<float>(bufs->image, il.accum), npix, rs->bg[0],
+                           rs->bg[1], rs->bg[2]);
+        GSR_STAGE(GSR_STAGE_MISC, hipGetLastError(), "fill_background");
+    }
+    GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(ranges, 0, il.ovf - il.ranges, stream), "memset ranges");
+    if (P == 0) return 0;
+    uint32_t* depth_key = at<uint32_t>(bufs->geom, gl.depth_key);
+    uint32_t* tiles = at<uint32_t>(bufs->geom, gl.tiles);
+    uint32_t* counters = at<uint32_t>(bufs->image, il.counters);
+    uint32_t* gid_by_rank = at<uint32_t>(bufs->geom, gl.sA_v);
+    PreOut po{j.radii, depth_key, tiles, at<float4>(bufs->geom, gl.rec), at<uint4>(bufs->geom, gl.rect),
+              j.full_img ? at<uint32_t>(bufs->geom, gl.flags) : nullptr, counters};
+    GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess(*cam, gauss_in(gs), j.ty0, j.ty1, po, stream), "preprocess");
+    if (read_counts) GSR_CHECK_HIP(begin_read(counters, 2 * kCountSlots, stream), "read counts");
+    if (!j.full_img) {
+        GSR_STAGE(GSR_STAGE_DEPTH_SORT, compact_candidates(tiles, depth_key, P, at<uint32_t>(bufs->geom, gl.partials),
+                                                           at<uint32_t>(bufs->geom, gl.offsets), gid_by_rank,
+                                                           counters + kCandCountSlot, stream),
+                  "band candidates");
+    } else {
+        // the scan needs no count; gid_by_rank = the identity ranking
+        GSR_STAGE(GSR_STAGE_SCAN, inclusive_scan_gather(tiles, nullptr, at<uint32_t>(bufs->geom, gl.offsets), P,
+                                                        at<uint32_t>(bufs->geom, gl.partials), stream, gid_by_rank),
+                  "scan");
+    }
+    return 0;
+}
+
+// The rest, given F1's counts: band colours, binning, per-tile depth order, F6.
+int fwd_phase2(FwdJob& j, uint64_t csum, uint64_t ksum, gsr_alloc_fn alloc_binning, void* ctx, hipStream_t stream,
+               bool debug) {
+    const gsr_camera* cam = j.cam;
+    const gsr_gaussians* gs = j.gs;
+    const gsr_raster_settings* rs = j.rs;
+    gsr_buffers* bufs = j.bufs;
+    const int P = gs->P, gx = j.gx, gy = j.gy, ty0 = j.ty0, ty1 = j.ty1;
+    const bool full_img = j.full_img, scanned = j.full_img;
+    const int bv = bin_variant();
+    GeomLayout gl(P);
+    ImgLayout il(cam->width, cam->height, j.ckt);
+    uint32_t* depth_key = at<uint32_t>(bufs->geom, gl.depth_key);
+    uint32_t* tiles = at<uint32_t>(bufs->geom, gl.tiles);
+    float4* rec = at<float4>(bufs->geom, gl.rec);
+    uint32_t* offsets = at<uint32_t>(bufs->geom, gl.offsets);
+    uint32_t* counters = at<uint32_t>(bufs->image, il.counters);
+    uint2* ranges = at<uint2>(bufs->image, il.ranges);
+    uint32_t* gid_by_rank = at<uint32_t>(bufs->geom, gl.sA_v);
+    uint32_t* tcount = bv == 2 ? at<uint32_t>(bufs->image, il.tcount) : nullptr;
+    long long K = 0;
+    if (P > 0) {
+        int NR = P;
+        if (!full_img) {
+            NR = (int)(csum < (uint64_t)P ? csum : (uint64_t)P);
+            if (colour_pass_needed(*cam, gauss_in(gs), ty0, ty1))
+                GSR_STAGE(GSR_STAGE_PREPROCESS, launch_colour(*cam, gauss_in(gs), gid_by_rank, NR, rec, stream),
+                          "band colours");
+        }
+        bufs->num_ranked = NR;
+        K = (long long)ksum;
+        if (K > INT32_MAX) return fail(-3, "num_rendered overflow (%lld)", K);
+        bufs->num_rendered = (int32_t)K;
+        bufs->binning = alloc_binning(ctx, BinLayout(K).total);
+        if (!bufs->binning) return fail(-2, "allocation failed (binning, K=%lld)", K);
+        BinLayout bl(K);
+        uint32_t* kA = at<uint32_t>(bufs->binning, bl.kA);
+        uint32_t* vA = at<uint32_t>(bufs->binning, bl.vA);
+        uint32_t* kB = at<uint32_t>(bufs->binning, bl.kB);
+        uint32_t* vB = at<uint32_t>(bufs->binning, bl.vB);
+        uint32_t* inst_gid = at<uint32_t>(bufs->binning, bl.inst_gid);
+        // final (tile, gid) arrays where views() expects them, and the free pair beside them
+        const bool odd = (tile_passes(gx * gy) & 1) != 0;
+        uint32_t* fk = odd ? kB : kA;
+        uint32_t* fv = odd ? vB : vA;
+        uint32_t* sk = odd ? kA : kB;
+        uint32_t* sv = odd ? vA : vB;
+        uint32_t* dup_key = bv == 2 ? sk : kA;  // F3's tile keys (emission order)
+        // variant 1: F3 also writes each instance's depth key, the tile sort carries it, and
+        // the per-tile sort reads it contiguously instead of gathering depth_key[gid]
+        const bool carry = bv == 1 && carry_depth();
+        uint32_t* dA = at<uint32_t>(bufs->binning, bl.dA);
+        uint32_t* dB = at<uint32_t>(bufs->binning, bl.dB);
+        if (NR > 0 && !scanned && scan_variant(NR) == 1) {
+            GSR_STAGE(GSR_STAGE_DUPLICATE, launch_scan_duplicate(gid_by_rank, tiles, at<uint4>(bufs->geom, gl.rect), NR, gx,
+                                                                 ty0, offsets, dup_key, inst_gid,
+                                                                 at<uint32_t>(bufs->geom, gl.hist), stream, tcount,
+                                                                 depth_key, carry ? dA : nullptr),
+                      "scan + duplicate");
+        } else if (NR > 0) {
+            if (!scanned)
+                GSR_STAGE(GSR_STAGE_SCAN, inclusive_scan_gather(tiles, gid_by_rank, offsets, NR,
+                                                                at<uint32_t>(bufs->geom, gl.partials), stream),
+                          "scan");
+            GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate(gid_by_rank, offsets, tiles, at<uint4>(bufs->geom, gl.rect), NR,
+                                                            gx, ty0, ty1, dup_key, inst_gid, stream, tcount,
+                                                            depth_key, carry ? dA : nullptr),
+                      "duplicate");
+        }
+        if (K > 0) {
+            if (bv == 2) {
+                GSR_STAGE(GSR_STAGE_TILE_SORT, launch_tile_bins(sk, inst_gid, K, ty0 * gx, (ty1 - ty0) * gx, tcount, ranges,
+                                                                fk, fv, stream),
+                          "tile bins");
+            } else {
+                int w2 = -1;
+                GSR_STAGE(GSR_STAGE_TILE_SORT, radix_sort(kA, inst_gid, kB, vB, kA, vA, K, tile_bits(gx * gy),
+                                                          at<uint32_t>(bufs->binning, bl.hist), &w2, stream, false,
+                                                          carry ? dA : nullptr, dB, dA),
+                          "tile sort");
+                if ((w2 == 0) != odd) return fail(-12, "tile sort ended in an unexpected buffer");
+                GSR_STAGE(GSR_STAGE_FINALIZE, launch_finalize(fk, K, ranges, stream), "finalize");
+            }
+            GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_tile_depth_sort(ranges, ty0 * gx, (ty1 - ty0) * gx, K, depth_key, fv,
+                                                                   at<uint32_t>(bufs->image, il.ovf),
+                                                                   counters + kOvfCountSlot, sk, sv, stream, bv == 1,
+                                                                   carry ? (odd ? dB : dA) : nullptr),
+                      "per-tile depth order");
+        }
+    } else {
+        bufs->binning = alloc_binning(ctx, BinLayout(0).total);
+    }
+    const Views v = views(cam, P, bufs, j.ckt);
+    GSR_STAGE(GSR_STAGE_BLEND_FWD, launch_blend_forward(*cam, rs->bg, ty0, ty1, ranges, v.sorted_gid, rec, j.out_color,
+                                                        at<float>(bufs->image, il.final_T), v.accum, v.ck, stream),
+              "blend forward");
+    return 0;
+}
+
+// Per view of a batch: the sum of F1's 64 instance-count partials, as a u64 in two words.
+struct CountPtrs {
+    const uint32_t* c[GSR_MAX_BATCH];
+};
+__global__ __launch_bounds__(64) void batch_counts_kernel(CountPtrs p, uint32_t* __restrict__ out) {
+    const uint32_t* c = p.c[blockIdx.x];
+    uint32_t lo = c[kCountSlots + threadIdx.x], hi = 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {  // 64-bit sum from two 32-bit shuffles
+        const uint32_t l2 = __shfl_xor(lo, o, 64), h2 = __shfl_xor(hi, o, 64);
+        const uint32_t s = lo + l2;
+        hi = hi + h2 + (s < lo ? 1u : 0u);
+        lo = s;
+    }
+    if (threadIdx.x == 0) {
+        out[2 * blockIdx.x] = lo;
+        out[2 * blockIdx.x + 1] = hi;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
+                float* out_color, int32_t* radii, gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_binning,
+                gsr_alloc_fn alloc_image, void* ctx, gsr_buffers* bufs, void* stream_) {
+    g_err.clear();
+    if (int e = validate(cam, gs, rs)) return e;
+    if (!out_color || (gs->P > 0 && !radii) || !bufs || !alloc_geom || !alloc_binning || !alloc_image)
+        return fail(-1, "null output / allocator");
+    if (bin_variant() == 0)
+        return forward_global_depth(cam, gs, rs, out_color, radii, alloc_geom, alloc_binning, alloc_image, ctx, bufs,
+                                    stream_);
+    hipStream_t stream = (hipStream_t)stream_;
+    const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
+    FwdJob j{cam, gs, rs, out_color, radii, bufs};
+    if (int e = fwd_phase1(j, alloc_geom, alloc_image, ctx, stream, debug, true)) return e;
+    uint64_t csum = 0, ksum = 0;
+    if (gs->P > 0) {
+        uint32_t cw[2 * kCountSlots];
+        const uint32_t* counters = at<uint32_t>(bufs->image, ImgLayout(cam->width, cam->height, j.ckt).counters);
+        GSR_STAGE(GSR_STAGE_MISC, end_read(counters, cw, 2 * kCountSlots, stream), "read counts");
+        for (int i = 0; i < kCountSlots; ++i) csum += cw[i], ksum += cw[kCountSlots + i];
+    }
+    return fwd_phase2(j, csum, ksum, alloc_binning, ctx, stream, debug);
+}
+
+int gsr_forward_batch(int32_t V, const gsr_camera* cams, const gsr_gaussians* gs, const gsr_raster_settings* rs,
+                      float* const* out_colors, int32_t* const* radii, gsr_alloc_fn alloc_geom,
+                      gsr_alloc_fn alloc_binning, gsr_alloc_fn alloc_image, void* ctx, gsr_buffers* bufs,
+                      void* stream_) {
+    g_err.clear();
+    if (V < 0 || V > GSR_MAX_BATCH) return fail(-1, "batch: 0..%d views, got %d", GSR_MAX_BATCH, V);
+    if (V == 0) return 0;
+    if (!cams || !gs || !rs || !out_colors || !bufs || !alloc_geom || !alloc_binning || !alloc_image ||
+        (gs->P > 0 && !radii))
+        return fail(-1, "batch: null argument");
+    if (bin_variant() == 0) return fail(-1, "batch: needs the per-tile binning (GSR_BIN_VARIANT != 0)");
+    hipStream_t stream = (hipStream_t)stream_;
+    const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
+    std::vector<FwdJob> jobs;
+    jobs.reserve(V);
+    for (int v = 0; v < V; ++v) {
+        if (int e = validate(&cams[v], gs, rs)) return e;
+        if (rs->tile_y0 > 0 || rs->tile_y1 < div_up(cams[v].height, kTile))
+            return fail(-1, "batch: full-image views only (view %d)", v);
+        if (!out_colors[v] || (gs->P > 0 && !radii[v])) return fail(-1, "batch: null output of view %d", v);
+        jobs.push_back(FwdJob{&cams[v], gs, rs, out_colors[v], gs->P > 0 ? radii[v] : nullptr, &bufs[v]});
+        if (int e = fwd_phase1(jobs[v], alloc_geom, alloc_image, ctx, stream, debug, false)) return e;
+    }
+    std::vector<uint64_t> K(V, 0);
+    if (gs->P > 0) {
+        uint32_t* words = static_cast<uint32_t*>(alloc_image(ctx, 8 * (size_t)V));
+        if (!words) return fail(-2, "allocation failed (batch counts)");
+        CountPtrs cp{};
+        for (int v = 0; v < V; ++v)
+            cp.c[v] = at<uint32_t>(bufs[v].image, ImgLayout(cams[v].width, cams[v].height, jobs[v].ckt).counters);
+        hipLaunchKernelGGL(batch_counts_kernel, dim3(V), dim3(64), 0, stream, cp, words);
+        GSR_STAGE(GSR_STAGE_MISC, hipGetLastError(), "batch counts");
+        uint32_t host[2 * GSR_MAX_BATCH];
+        GSR_CHECK_HIP(begin_read(words, 2 * V, stream), "read counts");
+        GSR_STAGE(GSR_STAGE_MISC, end_read(words, host, 2 * V, stream), "read counts");
+        for (int v = 0; v < V; ++v) K[v] = (uint64_t)host[2 * v] | ((uint64_t)host[2 * v + 1] << 32);
+    }
+    for (int v = 0; v < V; ++v)
+        if (int e = fwd_phase2(jobs[v], (uint64_t)gs->P, K[v], alloc_binning, ctx, stream, debug)) return e;
+    return 0;
+}
+
+}  // extern "C"
+
+extern "C" {
 
 // SH clamp bits stored by the forward (full image), or nullptr: B2 recomputes them (band).
 static const uint32_t* stored_flags(const gsr_camera* cam, const gsr_raster_settings* rs, const gsr_buffers* b,

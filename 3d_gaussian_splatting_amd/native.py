@@ -21,9 +21,11 @@ HIP_LIB = os.path.join(LIB_DIR, "libgsr_hip.so")
 GSR_FLAG_DEBUG = 1
 GSR_FLAG_BAND_ONLY = 2
 GSR_GRAD2D_STRIDE = 12
+GSR_MAX_BATCH = 64
 VIEW_SORTED_GID, VIEW_SORTED_TILE, VIEW_RANGES, VIEW_FINAL_T, VIEW_N_CONTRIB, VIEW_DEPTH_KEY, \
     VIEW_TILES_TOUCHED, VIEW_RECORDS, VIEW_GID_BY_RANK = range(1, 10)
-EXPORTS = ["gsr_abi_version", "gsr_last_error", "gsr_forward", "gsr_backward", "gsr_backward_blend",
+EXPORTS = ["gsr_abi_version", "gsr_last_error", "gsr_forward", "gsr_forward_batch", "gsr_backward",
+           "gsr_backward_blend",
            "gsr_backward_preprocess", "gsr_backward_preprocess_range", "gsr_view", "gsr_geom_bytes", "gsr_binning_bytes",
            "gsr_image_bytes", "gsr_scratch_bytes", "gsr_profile_enable", "gsr_profile_read",
            "gsr_stage_name"]
@@ -102,6 +104,10 @@ def load_hip() -> ctypes.CDLL:
         L.gsr_forward.restype = ctypes.c_int
         L.gsr_forward.argtypes = [ctypes.POINTER(Camera), ctypes.POINTER(Gaussians), ctypes.POINTER(Settings),
                                   vp, vp, ALLOC_FN, ALLOC_FN, ALLOC_FN, vp, ctypes.POINTER(Buffers), vp]
+        L.gsr_forward_batch.restype = ctypes.c_int
+        L.gsr_forward_batch.argtypes = [i32, ctypes.POINTER(Camera), ctypes.POINTER(Gaussians),
+                                        ctypes.POINTER(Settings), ctypes.POINTER(vp), ctypes.POINTER(vp), ALLOC_FN,
+                                        ALLOC_FN, ALLOC_FN, vp, ctypes.POINTER(Buffers), vp]
         L.gsr_backward.restype = ctypes.c_int
         L.gsr_backward.argtypes = [ctypes.POINTER(Camera), ctypes.POINTER(Gaussians), ctypes.POINTER(Settings),
                                    ctypes.POINTER(Buffers), vp, ALLOC_FN, vp, ctypes.POINTER(Grads), vp]

@@ -98,9 +98,8 @@ class CAbiRasterizer:
         if rc != 0:
             raise RuntimeError(f"{what} failed ({rc}): {native.last_error()}")
 
-    def forward(self, cam: RasterCamera, means3D, opacities, scales=None, rotations=None, sh_dc=None,
-                sh_rest=None, sh_degree=0, colors_precomp=None, cov3D_precomp=None, scale_modifier=1.0,
-                bg=(0.0, 0.0, 0.0), tile_rows=None, band_only=False, debug=False) -> ForwardState:
+    def _prepare(self, means3D, opacities, scales, rotations, sh_dc, sh_rest, sh_degree, colors_precomp,
+                 cov3D_precomp, scale_modifier, bg, tile_rows, band_only, debug):
         dev = self.device
         means3D = _f32(means3D, device=dev)
         P = int(means3D.shape[0])
@@ -125,6 +124,15 @@ class CAbiRasterizer:
         s.bg[:] = [float(v) for v in bg]
         s.tile_y0, s.tile_y1 = (0, INT32_MAX) if tile_rows is None else (int(tile_rows[0]), int(tile_rows[1]))
         s.flags = (native.GSR_FLAG_DEBUG if debug else 0) | (native.GSR_FLAG_BAND_ONLY if band_only else 0)
+        return inputs, g, s
+
+    def forward(self, cam: RasterCamera, means3D, opacities, scales=None, rotations=None, sh_dc=None,
+                sh_rest=None, sh_degree=0, colors_precomp=None, cov3D_precomp=None, scale_modifier=1.0,
+                bg=(0.0, 0.0, 0.0), tile_rows=None, band_only=False, debug=False) -> ForwardState:
+        dev = self.device
+        inputs, g, s = self._prepare(means3D, opacities, scales, rotations, sh_dc, sh_rest, sh_degree,
+                                     colors_precomp, cov3D_precomp, scale_modifier, bg, tile_rows, band_only, debug)
+        P = g.P
         color = torch.empty((3, cam.height, cam.width), dtype=torch.float32, device=dev)
         radii = torch.empty((P,), dtype=torch.int32, device=dev)
         ag, ab, ai = _Allocator(dev), _Allocator(dev), _Allocator(dev)
@@ -136,6 +144,32 @@ class CAbiRasterizer:
         self._check(rc, "gsr_forward")
         return ForwardState(cam=cam, inputs=inputs, settings=s, gauss=g, buffers=bufs, color=color,
                             radii=radii, allocs=[ag, ab, ai])
+
+    def forward_batch(self, cams, means3D, opacities, scales=None, rotations=None, sh_dc=None, sh_rest=None,
+                      sh_degree=0, colors_precomp=None, cov3D_precomp=None, scale_modifier=1.0,
+                      bg=(0.0, 0.0, 0.0), debug=False) -> list:
+        """gsr_forward_batch: one ForwardState per camera (full images), one host wait in total."""
+        dev = self.device
+        inputs, g, s = self._prepare(means3D, opacities, scales, rotations, sh_dc, sh_rest, sh_degree,
+                                     colors_precomp, cov3D_precomp, scale_modifier, bg, None, False, debug)
+        V, P = len(cams), g.P
+        colors = [torch.empty((3, c.height, c.width), dtype=torch.float32, device=dev) for c in cams]
+        radii = [torch.empty((P,), dtype=torch.int32, device=dev) for _ in cams]
+        ag, ab, ai = _Allocator(dev), _Allocator(dev), _Allocator(dev)
+        bufs = (native.Buffers * V)()
+        cs = (native.Camera * V)(*[native.camera_struct(c) for c in cams])
+        col_p = (ctypes.c_void_p * V)(*[t.data_ptr() for t in colors])
+        rad_p = (ctypes.c_void_p * V)(*[t.data_ptr() for t in radii])
+        rc = self.L.gsr_forward_batch(V, cs, ctypes.byref(g), ctypes.byref(s), col_p, rad_p if P else None, ag.cb,
+                                      ab.cb, ai.cb, None, bufs, self._stream())
+        self._check(rc, "gsr_forward_batch")
+        out = []
+        for v, cam in enumerate(cams):
+            b = native.Buffers()
+            ctypes.memmove(ctypes.byref(b), ctypes.byref(bufs[v]), ctypes.sizeof(b))
+            out.append(ForwardState(cam=cam, inputs=inputs, settings=s, gauss=g, buffers=b, color=colors[v],
+                                    radii=radii[v], allocs=[ag, ab, ai]))
+        return out
 
     def _grad_tensors(self, st: ForwardState, P: int | None = None):
         P = st.gauss.P if P is None else P

@@ -96,7 +96,8 @@ def main():
     ap.add_argument("--config", default="1m_1080p", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stage-events", action="store_true")
-    ap.add_argument("--mode", default="render", choices=("render", "train"),
+    ap.add_argument("--views", type=int, default=8, help="--mode views: cameras per batch")
+    ap.add_argument("--mode", default="render", choices=("render", "train", "views"),
                     help="render: the BASELINE metric (rasterizer forward+backward); train: one full "
                          "training iteration (activations, render, L1+D-SSIM loss, backward, "
                          "densification statistics, fused Adam), SURVEY §8f")
@@ -105,6 +106,8 @@ def main():
     args = ap.parse_args()
     if args.mode == "train":
         return train_main(args)
+    if args.mode == "views":
+        return views_main(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -349,6 +352,60 @@ def train_main(args):
                         "note": "activation backward fused; the event pair brackets the single adam launch"},
            "loss": {"loss": stats[0], "l1": stats[1], "ssim": stats[2]}}
     print(json.dumps(res))
+
+
+def views_main(args):
+    """V cameras around the scene per step, forward + backward of each view.
+    Batched (gsr_forward_batch: one host wait per batch) against the same views one
+    gsr_forward at a time; value = batched views/s.  N = 1 only."""
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit("--mode views runs on one GPU")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    cfg = CONFIGS[args.config]
+    P, W, H, D = cfg["P"], cfg["W"], cfg["H"], cfg["D"]
+    cam0 = gr.synthetic_camera(W, H)
+    scene = sc.make_scene(cam0, P, max_sh_degree=max(D, 0), seed=0)
+    fx = math.radians(60.0)
+    fy = 2 * math.atan(math.tan(fx / 2) * H / W)
+    cams = []
+    for v in range(args.views):  # small yaw sweep around the synthetic camera
+        a = math.radians(-10.0 + 20.0 * v / max(args.views - 1, 1))
+        Rm = np.array([[math.cos(a), 0, math.sin(a)], [0, 1, 0], [-math.sin(a), 0, math.cos(a)]])
+        cams.append(gr.make_camera(Rm, np.zeros(3), fx, fy, W, H))
+    rast = R.CAbiRasterizer(dev)
+    t = lambda a: torch.tensor(a, device=dev)
+    inputs = dict(means3D=t(scene.means3D), opacities=t(scene.opacities), scales=t(scene.scales),
+                  rotations=t(scene.rotations), sh_dc=t(scene.sh_dc), sh_rest=t(scene.sh_rest))
+    dpix = t(sc.make_dL_dpix(cam0, seed=1))
+
+    def batched():
+        for st in rast.forward_batch(cams, **inputs, sh_degree=D):
+            rast.backward(st, dpix)
+
+    def single():
+        for c in cams:
+            rast.backward(rast.forward(c, **inputs, sh_degree=D), dpix)
+
+    res = {}
+    for name, fn in (("single", single), ("batched", batched), ("single", single), ("batched", batched)):
+        for _ in range(args.warmup):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            fn()
+        torch.cuda.synchronize()
+        res.setdefault(name, []).append(args.steps * args.views / (time.perf_counter() - t0))
+    b, s1 = max(res["batched"]), max(res["single"])
+    print(json.dumps({
+        "metric": f"forward+backward views/s, {args.views} cameras per batch", "value": round(b, 2),
+        "unit": "views/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(1e3 * args.views / b, 4), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"{args.config} x {args.views} views (yaw -10..10 deg), gsr_forward_batch + "
+                               f"per-view gsr_backward", "gaussians": P, "width": W, "height": H, "sh_degree": D},
+        "single_view_calls_views_per_s": round(s1, 2), "batch_speedup": round(b / s1, 4)}))
 
 
 if __name__ == "__main__":

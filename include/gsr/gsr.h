@@ -122,6 +122,20 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
                 gsr_alloc_fn alloc_binning, gsr_alloc_fn alloc_image, void* alloc_ctx,
                 gsr_buffers* bufs, void* stream);
 
+/* Batched forward over V views of the same Gaussians (the reference's loop
+ * renders one camera per iteration, src/utils/train_utils.cpp:128-145).  Per view the work of
+ * gsr_forward, but the V first phases (preprocess + scan) are enqueued back to back and ONE
+ * device->host read returns all V instance counts, so the host waits once per batch instead of
+ * once per view and the GPU is not left idle between views.  cams[v], out_colors[v]
+ * (3 x H_v x W_v), radii[v] (P), bufs[v]: as for gsr_forward; each view's backward is
+ * gsr_backward with bufs[v].  Full-image views only (rs->tile_y0/y1 must cover every view);
+ * one extra 8*V-byte allocation through alloc_image holds the counts.  0 < V <= GSR_MAX_BATCH. */
+#define GSR_MAX_BATCH 64
+int gsr_forward_batch(int32_t V, const gsr_camera* cams, const gsr_gaussians* gs,
+                      const gsr_raster_settings* rs, float* const* out_colors, int32_t* const* radii,
+                      gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_binning, gsr_alloc_fn alloc_image,
+                      void* alloc_ctx, gsr_buffers* bufs, void* stream);
+
 /* Full backward (B1 + gather + B2).  dL_dout_color: 3 x H x W.  scratch: asked for twice
  * through alloc_scratch (gsr_scratch_bytes(K) for per-instance partial gradients, then
  * 48 * P bytes for the per-Gaussian screen-space gradient), valid for the duration of the call. */
