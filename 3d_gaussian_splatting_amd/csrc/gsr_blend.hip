@@ -414,7 +414,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
             const float dx = r0.x - pfx;
             const float bdx = r0.w * dx;
             const float K = fmaf(r0.z * dx, dx, r2.w);
-            float s0 = 0.f, sy = 0.f, syy = 0.f, g0 = 0.f, g1 = 0.f, g2 = 0.f;
+            // -0 is the exact identity of IEEE addition (x + -0 = x for every x, +0 included), so
+            // the first stripe's adds / FMAs into these fold into plain moves / multiplies
+            // without fast-math; +0 would keep them (0 + -0 = +0)
+            float s0 = -0.f, sy = -0.f, syy = -0.f, g0 = -0.f, g1 = -0.f, g2 = -0.f;
             bool any = false;
 #pragma unroll
             for (int p = 0; p < kPPL; ++p) {

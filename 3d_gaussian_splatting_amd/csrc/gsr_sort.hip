@@ -38,11 +38,12 @@ __device__ inline uint64_t lanemask_lt() {
     return (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 }
 
-// lanes (among `active`) holding the same digit as this lane
+// lanes (among `active`) holding the same digit as this lane (digits of up to MAXB bits)
+template <int MAXB = 8>
 __device__ inline uint64_t match_digit(uint32_t d, int nbits, uint64_t active) {
     uint64_t peers = active;
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < MAXB; ++b) {
         if (b < nbits) {
             const bool bit = (d >> b) & 1u;
             const uint64_t m = __ballot(bit);
@@ -914,20 +915,23 @@ __global__ __launch_bounds__(NT) void tile_depth_sort_small(const uint2* __restr
 // 32-bit depth keys alone gives (depth, gid) order.  Four 8-bit passes in LDS, each ranked
 // exactly as radix_downsweep ranks (wave64 ballot peer match, per-wave digit counters, a
 // digit-major block scan): ~20 B of LDS traffic per key per pass, against ~log2(n)^2 / 2 x 12 B
-// for the bitonic network, which is LDS-bandwidth-bound.  Measured at 1M/1080p: radix 0.102 ms,
-// bitonic 0.130 ms; rocprofv3 shows the radix form VALU-issue-bound (the 8-ballot peer match
-// per 64 keys per pass).  Passes whose digit is equal for every key of the slice are skipped.
+// for the bitonic network, which is LDS-bandwidth-bound.  Passes whose digit is equal for every
+// key of the slice are skipped, so 9-bit digits need 3 passes for the <= 27 differing bits of
+// a 0.2 .. 100 depth range.  Measured at 1M/1080p: 9-bit radix 0.098 ms, 8-bit 0.102 ms,
+// bitonic 0.130 ms; the radix form is latency-bound per block (dependent LDS counter updates
+// per 64-key round, ~6 syncs per pass), not by LDS bandwidth.
 // NT threads, I items per thread: CAP = NT * I keys; wave w owns the contiguous run
 // [w * 64 I, (w + 1) * 64 I) of the slice, ranked round by round in index order (stable).
-template <int NT, int I>
+template <int NT, int I, int DB>
 __global__ __launch_bounds__(NT) void tile_depth_radix(const uint2* __restrict__ ranges, int tile0,
                                                       const uint32_t* __restrict__ depth_key,
                                                       const uint32_t* __restrict__ sdepth,
                                                       uint32_t* __restrict__ gid, uint32_t* __restrict__ ovf,
                                                       uint32_t* __restrict__ ovf_count) {
-    constexpr int NWV = NT / 64, CAP = NT * I;
-    __shared__ uint32_t wcnt[NWV][256];
-    __shared__ uint32_t lbase[256];
+    constexpr int NWV = NT / 64, CAP = NT * I, BINS = 1 << DB;
+    constexpr uint32_t DMASK = BINS - 1u;
+    __shared__ uint32_t wcnt[NWV][BINS];
+    __shared__ uint32_t lbase[BINS];
     __shared__ uint32_t wsum[NWV];
     __shared__ uint32_t red[2][NWV];
     __shared__ uint32_t skey[CAP];
@@ -981,24 +985,24 @@ __global__ __launch_bounds__(NT) void tile_depth_radix(const uint2* __restrict__
         diff = o_ ^ a_;
     }
     const uint64_t lt = lanemask_lt();
-    for (int shift = 0; shift < 32; shift += 8) {
-        if (((diff >> shift) & 0xFFu) == 0u) continue;  // block-uniform
-        for (int d = tid; d < NWV * 256; d += NT) (&wcnt[0][0])[d] = 0u;
+    for (int shift = 0; shift < 32; shift += DB) {
+        if (((diff >> shift) & DMASK) == 0u) continue;  // block-uniform
+        for (int d = tid; d < NWV * BINS; d += NT) (&wcnt[0][0])[d] = 0u;
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < I; ++r) {
             if (base + r * 64 >= end) break;  // wave-uniform: only the rounds holding keys
             const int idx = base + r * 64 + lane;
             const bool valid = idx < end;
-            const uint32_t d = (key[r] >> shift) & 0xFFu;
-            const uint64_t peers = match_digit(d, 8, __ballot(valid));
+            const uint32_t d = (key[r] >> shift) & DMASK;
+            const uint64_t peers = match_digit<DB>(d, DB, __ballot(valid));
             const uint32_t old = wcnt[w][d];
             rank[r] = old + (uint32_t)__popcll(peers & lt);
             if (valid && (peers & lt) == 0) wcnt[w][d] = old + (uint32_t)__popcll(peers);
         }
         __syncthreads();
         // per digit: wave prefixes in place, then the digit-major block scan -> lbase
-        for (int d = tid; d < 256; d += NT) {
+        for (int d = tid; d < BINS; d += NT) {
             uint32_t c = 0;
 #pragma unroll
             for (int k = 0; k < NWV; ++k) {
@@ -1009,11 +1013,12 @@ __global__ __launch_bounds__(NT) void tile_depth_radix(const uint2* __restrict__
             lbase[d] = c;
         }
         __syncthreads();
-        if (tid < 64) {  // exclusive scan of the 256 digit totals, 4 per lane
-            uint32_t c4[4], s4 = 0;
+        if (tid < 64) {  // exclusive scan of the BINS digit totals, BINS / 64 per lane
+            constexpr int Q = BINS / 64;
+            uint32_t c4[Q], s4 = 0;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                c4[q] = lbase[4 * tid + q];
+            for (int q = 0; q < Q; ++q) {
+                c4[q] = lbase[Q * tid + q];
                 s4 += c4[q];
             }
             uint32_t x = s4;
@@ -1024,8 +1029,8 @@ __global__ __launch_bounds__(NT) void tile_depth_radix(const uint2* __restrict__
             }
             uint32_t run = x - s4;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                lbase[4 * tid + q] = run;
+            for (int q = 0; q < Q; ++q) {
+                lbase[Q * tid + q] = run;
                 run += c4[q];
             }
         }
@@ -1034,7 +1039,7 @@ __global__ __launch_bounds__(NT) void tile_depth_radix(const uint2* __restrict__
         for (int r = 0; r < I; ++r) {
             const int idx = base + r * 64 + lane;
             if (idx < end) {
-                const uint32_t d = (key[r] >> shift) & 0xFFu;
+                const uint32_t d = (key[r] >> shift) & DMASK;
                 const uint32_t lp = lbase[d] + wcnt[w][d] + rank[r];
                 skey[lp] = key[r];
                 sval[lp] = val[r];
@@ -1289,6 +1294,14 @@ static int tile_sort_variant() {
     return e ? std::atoi(e) : 1;
 }
 
+// Digit width of the per-tile radix form (A/B): 9 (shipped) sorts the <= 27 bits in which a
+// tile's depth keys differ (depths 0.2 .. 100 differ in the low 27 bits; constant high digits
+// are skipped) in 3 passes, 8 needs 4.
+static int tile_sort_digit_bits() {
+    const char* e = std::getenv("GSR_TILESORT_BITS");
+    return e && std::atoi(e) == 8 ? 8 : 9;
+}
+
 int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long K, const uint32_t* depth_key,
                            uint32_t* gid, uint32_t* ovf, uint32_t* ovf_count, uint32_t* scratch_hi,
                            uint32_t* scratch_lo, hipStream_t s, bool gid_ordered, const uint32_t* sdepth) {
@@ -1298,18 +1311,21 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
     int cap = 1024;
     while (cap < 8192 && cap < mean + mean / 2) cap <<= 1;
     if (gid_ordered && tile_sort_variant() == 1) {
-        if (cap == 1024)
-            hipLaunchKernelGGL((tile_depth_radix<256, 4>), dim3(ntiles), dim3(256), 0, s, ranges, tile0, depth_key, sdepth, gid,
-                               ovf, ovf_count);
-        else if (cap == 2048)
-            hipLaunchKernelGGL((tile_depth_radix<256, 8>), dim3(ntiles), dim3(256), 0, s, ranges, tile0, depth_key, sdepth, gid,
-                               ovf, ovf_count);
-        else if (cap == 4096)
-            hipLaunchKernelGGL((tile_depth_radix<256, 16>), dim3(ntiles), dim3(256), 0, s, ranges, tile0, depth_key, sdepth, gid,
-                               ovf, ovf_count);
-        else
-            hipLaunchKernelGGL((tile_depth_radix<512, 16>), dim3(ntiles), dim3(512), 0, s, ranges, tile0, depth_key, sdepth, gid,
-                               ovf, ovf_count);
+#define GSR_TILE_RADIX(NT_, I_, DB_)                                                                          \
+    hipLaunchKernelGGL((tile_depth_radix<NT_, I_, DB_>), dim3(ntiles), dim3(NT_), 0, s, ranges, tile0, depth_key, \
+                       sdepth, gid, ovf, ovf_count)
+        if (tile_sort_digit_bits() == 8) {
+            if (cap == 1024) GSR_TILE_RADIX(256, 4, 8);
+            else if (cap == 2048) GSR_TILE_RADIX(256, 8, 8);
+            else if (cap == 4096) GSR_TILE_RADIX(256, 16, 8);
+            else GSR_TILE_RADIX(512, 16, 8);
+        } else {
+            if (cap == 1024) GSR_TILE_RADIX(256, 4, 9);
+            else if (cap == 2048) GSR_TILE_RADIX(256, 8, 9);
+            else if (cap == 4096) GSR_TILE_RADIX(256, 16, 9);
+            else GSR_TILE_RADIX(512, 16, 9);
+        }
+#undef GSR_TILE_RADIX
     } else if (cap == 1024)
         hipLaunchKernelGGL((tile_depth_sort_small<1024, 256>), dim3(ntiles), dim3(256), 0, s, ranges, tile0, depth_key,
                            sdepth, gid, ovf, ovf_count);
