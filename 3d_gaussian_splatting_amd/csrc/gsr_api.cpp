@@ -62,6 +62,16 @@ bool carry_depth() {
     return e ? std::atoi(e) != 0 : false;
 }
 
+// A/B (bench/ablation only): 1 = gsr_backward runs the gather and B2 as one kernel when the
+// ranking is the identity; 0 (shipped) = two kernels through the grad2d buffer.  Measured at
+// 1M/1080p: fused 0.215 ms vs 0.078 + 0.118 ms -- the fused block holds B2's 46 KB of SH
+// staging through the latency-bound gather phase (3 blocks per CU instead of 8), which costs
+// more than the 96 MB grad2d round trip it saves.
+bool fuse_gather() {
+    const char* e = std::getenv("GSR_FUSE_GATHER");
+    return e ? std::atoi(e) != 0 : false;
+}
+
 // Low-latency device->host read of one u32: DMA into a per-thread pinned word, then spin on
 // it.  hipStreamSynchronize after a pageable copy measured ~100 us from the end of the scan
 // to the next launch (profiles/r01_kernel_stats + trace); the spin wakes within ~µs.
@@ -803,10 +813,20 @@ int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raste
     float* partial = static_cast<float*>(alloc_scratch(ctx, gsr_scratch_bytes((int32_t)K)));
     float* grad2d = static_cast<float*>(alloc_scratch(ctx, sizeof(float) * kPart * (size_t)P));
     if (!partial || !grad2d) return fail(-2, "allocation failed (scratch, K=%lld, P=%d)", K, P);
+    // full image ranked in gid order (shipped binning): gather + B2 fused, grad2d unused
+    const bool fuse = K > 0 && bin_variant() != 0 && ty0 == 0 && ty1 == div_up(cam->height, kTile) &&
+                      bufs->num_ranked == P && fuse_gather();
     if (K > 0) {
         GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.rect, v.rec,
                                             v.final_T, v.accum, dL_dpix, partial, K, v.ck, stream),
                       "blend backward");
+        if (fuse) {
+            GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_gather_backward(*cam, gauss_in(gs), v.depth_key,
+                                                                       stored_flags(cam, rs, bufs, P), v.offsets,
+                                                                       partial, v.rec, K, grad_out(grads), stream),
+                      "gather + preprocess backward");
+            return 0;
+        }
         GSR_STAGE(GSR_STAGE_GATHER, gather_all(cam, rs, v, bufs, partial, K, P, grad2d, stream),
                   "gather grad2d");
     } else {

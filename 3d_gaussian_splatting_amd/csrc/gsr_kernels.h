@@ -122,6 +122,13 @@ struct GradOut {
     float *means2D, *conic, *opac, *colors, *means3D, *sh_dc, *sh_rest, *scales, *rots, *cov3D;
 };
 
+// gather + B2 in one kernel for a full image whose ranking is the identity (gid order): the
+// per-Gaussian 2D gradient never leaves registers.  Same results as launch_gather_grad2d
+// followed by launch_preprocess_backward over [0, P).
+int launch_gather_backward(const gsr_camera& cam, const GaussIn& in, const uint32_t* depth_key, const uint32_t* flags,
+                           const uint32_t* offsets, const float* partial, const float4* rec, long long K,
+                           const GradOut& out, hipStream_t s);
+
 // B2: chain rule to the leaves for Gaussians [g0, g1) from their 2D gradients (grad2d, kPart
 // floats each).  Inputs are indexed by g; grad2d and all outputs by g - g0.
 int launch_preprocess_backward(const gsr_camera& cam, const GaussIn& in, int g0, int g1,

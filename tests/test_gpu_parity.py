@@ -273,3 +273,22 @@ def test_backward_preprocess_range_matches_full():
         part = rast.backward_preprocess_range(st, g0, g1, g2[g0:g1])
         for k, v in part.items():
             assert torch.equal(v, full[k][g0:g1]), (k, g0, g1)
+
+
+@pytest.mark.gpu
+def test_fused_gather_backward_matches_two_kernels(monkeypatch):
+    """gsr_backward's fused gather + B2 (GSR_FUSE_GATHER=1; full image, gid-order ranking)
+    equals B1 -> grad2d -> B2 through gsr_backward_blend / gsr_backward_preprocess, bit for bit."""
+    monkeypatch.setenv("GSR_FUSE_GATHER", "1")
+    R, gr, sc = pkg("rasterizer"), pkg("graphics"), pkg("scene")
+    dev = torch.device("cuda", 0)
+    for D, P, (W, H) in ((3, 20000, (320, 240)), (0, 3000, (200, 120))):
+        cam = gr.synthetic_camera(W, H)
+        s = sc.make_scene(cam, P, max_sh_degree=3, seed=17)
+        dpix = torch.tensor(sc.make_dL_dpix(cam, seed=18), device=dev)
+        rast = R.CAbiRasterizer(dev)
+        st = rast.forward(cam, s.means3D, s.opacities, s.scales, s.rotations, s.sh_dc, s.sh_rest, sh_degree=D)
+        fused = rast.backward(st, dpix)
+        two = rast.backward_preprocess(st, rast.backward_blend(st, dpix))
+        for k, v in fused.items():
+            assert torch.equal(v, two[k]), (D, k)
