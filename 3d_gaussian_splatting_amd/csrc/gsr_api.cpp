@@ -607,7 +607,9 @@ int fwd_phase2(FwdJob& j, uint64_t csum, uint64_t ksum, gsr_alloc_fn alloc_binni
             }
             GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_tile_depth_sort(ranges, ty0 * gx, (ty1 - ty0) * gx, K, depth_key, fv,
                                                                    at<uint32_t>(bufs->image, il.ovf),
-                                                                   counters + kOvfCountSlot, sk, sv, stream, bv == 1,
+                                                                   counters + kOvfCountSlot,
+                                                                   at<uint32_t>(bufs->image, il.ovf2),
+                                                                   counters + kOvf2CountSlot, sk, sv, stream, bv == 1,
                                                                    carry ? (odd ? dB : dA) : nullptr),
                       "per-tile depth order");
         }

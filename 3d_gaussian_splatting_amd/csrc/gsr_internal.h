@@ -96,7 +96,7 @@ inline int chunked_tiles(int W, int ty0, int ty1) {
 }
 
 struct ImgLayout {
-    size_t ranges, counters, tcount, ovf, final_T, accum, ck, total;
+    size_t ranges, counters, tcount, ovf, ovf2, final_T, accum, ck, total;
     ImgLayout(int W, int H, int ck_tiles = 0) {
         size_t o = 0;
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
@@ -106,7 +106,8 @@ struct ImgLayout {
         counters = take(4 * (2 * kCountSlots + 16));  // ranges, counters and tcount are
         tcount = take(4 * (tiles ? tiles : 1));       // contiguous: one memset clears all three
         // (tcount: per-tile instance counts from F3, then the count binning's scatter cursors)
-        ovf = take(4 * (tiles ? tiles : 1));  // tiles the per-tile depth sort hands to its large form
+        ovf = take(4 * (tiles ? tiles : 1));   // tiles the per-tile depth sort hands to its larger
+        ovf2 = take(4 * (tiles ? tiles : 1));  // forms (two queues: LDS, then global memory)
         final_T = take(4 * (pix ? pix : 1));
         accum = take(12 * (pix ? pix : 1));  // colour sum without background, 3 x H x W
         ck = take((size_t)ck_tiles * (kMaxChunks - 1) * 256 * 16);  // float4 (T, C) checkpoints
@@ -130,6 +131,7 @@ struct PartLayout {
 // counters[] slots past the preprocess partials (2 x kCountSlots)
 constexpr int kCandCountSlot = 2 * kCountSlots;      // band candidate count (compaction)
 constexpr int kOvfCountSlot = 2 * kCountSlots + 8;   // tiles queued for the large per-tile depth sort
+constexpr int kOvf2CountSlot = 2 * kCountSlots + 9;  // ... and for its global-memory form
 
 // number of 8-bit LSD passes to sort tile ids of a grid with `tiles` tiles
 inline int tile_bits(int tiles) {

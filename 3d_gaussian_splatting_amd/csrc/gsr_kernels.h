@@ -54,14 +54,14 @@ int inclusive_scan_gather(const uint32_t* in, const uint32_t* idx, uint32_t* out
 // sorted in place by (depth_key[gid], gid) -- the canonical (tile, depth, gid) order.  Tiles
 // of up to 1.5x the mean slice (pow2, 1024..8192) sort in LDS; larger ones are queued in `ovf`
 // (count at *ovf_count, zeroed) and sorted by a second launch (LDS up to 8192, global
-// scratch lo/hi beyond).  scratch_hi / scratch_lo: K u32 each, free after the tile sort.
+// scratch lo/hi beyond; the radix form queues those once more in ovf2 / *ovf2_count).  scratch_hi / scratch_lo: K u32 each, free after the tile sort.
 // gid_ordered: each slice is in ascending gid order (stable tile sort of gid-order emissions),
 // so a stable sort of the depth keys alone suffices (LDS radix form).  sdepth (nullable): the
 // depth key of every sorted instance (carried through the tile sort); without it the keys are
 // gathered per instance from depth_key[gid].
 int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long K, const uint32_t* depth_key,
-                           uint32_t* gid, uint32_t* ovf, uint32_t* ovf_count, uint32_t* scratch_hi,
-                           uint32_t* scratch_lo, hipStream_t s, bool gid_ordered,
+                           uint32_t* gid, uint32_t* ovf, uint32_t* ovf_count, uint32_t* ovf2, uint32_t* ovf2_count,
+                           uint32_t* scratch_hi, uint32_t* scratch_lo, hipStream_t s, bool gid_ordered,
                            const uint32_t* sdepth = nullptr);
 
 // Band candidates: the Gaussians with tiles[g] != 0, in gid order -> (depth key, gid) pairs

@@ -922,28 +922,19 @@ __global__ __launch_bounds__(NT) void tile_depth_sort_small(const uint2* __restr
 // per 64-key round, ~6 syncs per pass), not by LDS bandwidth.
 // NT threads, I items per thread: CAP = NT * I keys; wave w owns the contiguous run
 // [w * 64 I, (w + 1) * 64 I) of the slice, ranked round by round in index order (stable).
+// One slice [rg.x, rg.y) of n <= NT * I entries, sorted by the whole block.  Ends with every
+// LDS access behind a barrier, so a block may call it again for another slice.
 template <int NT, int I, int DB>
-__global__ __launch_bounds__(NT) void tile_depth_radix(const uint2* __restrict__ ranges, int tile0,
-                                                      const uint32_t* __restrict__ depth_key,
-                                                      const uint32_t* __restrict__ sdepth,
-                                                      uint32_t* __restrict__ gid, uint32_t* __restrict__ ovf,
-                                                      uint32_t* __restrict__ ovf_count) {
+__device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t* __restrict__ depth_key,
+                                                 const uint32_t* __restrict__ sdepth, uint32_t* __restrict__ gid) {
     constexpr int NWV = NT / 64, CAP = NT * I, BINS = 1 << DB;
     constexpr uint32_t DMASK = BINS - 1u;
     __shared__ uint32_t wcnt[NWV][BINS];
     __shared__ uint32_t lbase[BINS];
-    __shared__ uint32_t wsum[NWV];
     __shared__ uint32_t red[2][NWV];
     __shared__ uint32_t skey[CAP];
     __shared__ uint32_t sval[CAP];
-    const int tile = tile0 + blockIdx.x;
-    const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
-    if (n <= 1) return;
-    if (n > CAP) {
-        if (threadIdx.x == 0) ovf[atomicAdd(ovf_count, 1u)] = (uint32_t)tile;
-        return;
-    }
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     // wave w owns [w * per, (w + 1) * per): per = the slice split evenly over the waves in whole
     // 64-lane rounds (<= 64 I since n <= CAP)
@@ -1061,7 +1052,50 @@ __global__ __launch_bounds__(NT) void tile_depth_radix(const uint2* __restrict__
         const int idx = base + r * 64 + lane;
         if (idx < end) gid[rg.x + idx] = val[r];
     }
+    __syncthreads();  // red[] is rewritten by the next slice
 }
+
+// One block per tile of the launch; slices longer than NT * I go to the queue `ovf`.
+template <int NT, int I, int DB>
+__global__ __launch_bounds__(NT) void tile_depth_radix(const uint2* __restrict__ ranges, int tile0,
+                                                      const uint32_t* __restrict__ depth_key,
+                                                      const uint32_t* __restrict__ sdepth,
+                                                      uint32_t* __restrict__ gid, uint32_t* __restrict__ ovf,
+                                                      uint32_t* __restrict__ ovf_count) {
+    const int tile = tile0 + blockIdx.x;
+    const uint2 rg = ranges[tile];
+    const int n = (int)(rg.y - rg.x);
+    if (n <= 1) return;
+    if (n > NT * I) {
+        if (threadIdx.x == 0) ovf[atomicAdd(ovf_count, 1u)] = (uint32_t)tile;
+        return;
+    }
+    radix_sort_slice<NT, I, DB>(rg, depth_key, sdepth, gid);
+}
+
+// The queued (longer) slices: blocks walk the queue; slices longer than NT * I go on to the
+// second queue (ovf2), which the global-memory form drains.  The queue length is on the device,
+// so blocks past it exit at once.
+template <int NT, int I, int DB>
+__global__ __launch_bounds__(NT) void tile_depth_radix_queue(const uint2* __restrict__ ranges,
+                                                            const uint32_t* __restrict__ depth_key,
+                                                            const uint32_t* __restrict__ sdepth,
+                                                            uint32_t* __restrict__ gid,
+                                                            const uint32_t* __restrict__ ovf,
+                                                            const uint32_t* __restrict__ ovf_count,
+                                                            uint32_t* __restrict__ ovf2, uint32_t* __restrict__ ovf2_count) {
+    const uint32_t cnt = *ovf_count;
+    for (uint32_t q = blockIdx.x; q < cnt; q += gridDim.x) {
+        const uint32_t tile = ovf[q];
+        const uint2 rg = ranges[tile];
+        if ((int)(rg.y - rg.x) > NT * I) {
+            if (threadIdx.x == 0) ovf2[atomicAdd(ovf2_count, 1u)] = tile;
+            continue;  // block-uniform
+        }
+        radix_sort_slice<NT, I, DB>(rg, depth_key, sdepth, gid);
+    }
+}
+
 
 // Large form: the queued tiles, 1024 threads per block.  Up to kLargeLds instances in LDS;
 // beyond that (dense real scenes) the same network runs on the slice in global memory, with
@@ -1303,8 +1337,9 @@ static int tile_sort_digit_bits() {
 }
 
 int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long K, const uint32_t* depth_key,
-                           uint32_t* gid, uint32_t* ovf, uint32_t* ovf_count, uint32_t* scratch_hi,
-                           uint32_t* scratch_lo, hipStream_t s, bool gid_ordered, const uint32_t* sdepth) {
+                           uint32_t* gid, uint32_t* ovf, uint32_t* ovf_count, uint32_t* ovf2, uint32_t* ovf2_count,
+                           uint32_t* scratch_hi, uint32_t* scratch_lo, hipStream_t s, bool gid_ordered,
+                           const uint32_t* sdepth) {
     if (ntiles <= 0 || K <= 0) return 0;
     // capacity of the LDS form: a power of two >= 1.5x the mean slice, 1024 .. 8192
     const long long mean = K / ntiles;
@@ -1314,18 +1349,26 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
 #define GSR_TILE_RADIX(NT_, I_, DB_)                                                                          \
     hipLaunchKernelGGL((tile_depth_radix<NT_, I_, DB_>), dim3(ntiles), dim3(NT_), 0, s, ranges, tile0, depth_key, \
                        sdepth, gid, ovf, ovf_count)
+        // one block per tile up to 4096 entries (<= 43 KB of LDS: 3 blocks per CU); longer slices
+        // queue for 512-thread blocks of up to 8192 (73 KB: 2 per CU) walking the queue, and
+        // beyond that for the global-memory bitonic form
         if (tile_sort_digit_bits() == 8) {
             if (cap == 1024) GSR_TILE_RADIX(256, 4, 8);
             else if (cap == 2048) GSR_TILE_RADIX(256, 8, 8);
-            else if (cap == 4096) GSR_TILE_RADIX(256, 16, 8);
-            else GSR_TILE_RADIX(512, 16, 8);
+            else GSR_TILE_RADIX(256, 16, 8);
         } else {
             if (cap == 1024) GSR_TILE_RADIX(256, 4, 9);
             else if (cap == 2048) GSR_TILE_RADIX(256, 8, 9);
-            else if (cap == 4096) GSR_TILE_RADIX(256, 16, 9);
-            else GSR_TILE_RADIX(512, 16, 9);
+            else GSR_TILE_RADIX(256, 16, 9);
         }
 #undef GSR_TILE_RADIX
+        const int qgrid = ntiles < 512 ? ntiles : 512;
+        hipLaunchKernelGGL((tile_depth_radix_queue<512, 16, 8>), dim3(qgrid), dim3(512), 0, s, ranges, depth_key,
+                           sdepth, gid, ovf, ovf_count, ovf2, ovf2_count);
+        const int grid = ntiles < 64 ? ntiles : 64;
+        hipLaunchKernelGGL(tile_depth_sort_large, dim3(grid), dim3(1024), sizeof(uint64_t) * kLargeLds, s, ranges,
+                           depth_key, sdepth, gid, ovf2, ovf2_count, scratch_hi, scratch_lo);
+        return (int)hipGetLastError();
     } else if (cap == 1024)
         hipLaunchKernelGGL((tile_depth_sort_small<1024, 256>), dim3(ntiles), dim3(256), 0, s, ranges, tile0, depth_key,
                            sdepth, gid, ovf, ovf_count);
