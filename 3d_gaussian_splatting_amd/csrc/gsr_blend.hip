@@ -25,8 +25,10 @@
 // registers, a 2-step quad DPP reduction, then the 16 quad partials wait in LDS and are summed
 // four records at a time (one (record, moment) output per lane, stored straight to HBM) --
 // ~40% fewer VALU ops than a full 64-lane DPP/permlane reduction per record, and no per-batch
-// moment buffer in LDS (more waves per SIMD).  It writes ONE 36-B partial per (tile, instance)
-// with plain stores, indexed by the instance's emission index j.
+// moment buffer in LDS (more waves per SIMD).  It writes ONE 36-B partial per contributing
+// (tile, instance) with plain stores, indexed by the instance's emission index j; the rest stay
+// at the zeros the launcher clears the partial block to, and a tile stops at the first batch
+// whose pixels have all terminated.
 //
 // Measured and rejected (scripts/ablate.py): packing two stripes per VGPR pair
 // (v_pk_fma_f32 issues 2 FMAs in 4 cycles -- no gain over v_fma_f32 on gfx950, and the
@@ -384,6 +386,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
         uint32_t live = 0;
 #pragma unroll
         for (int p = 0; p < kPPL; ++p) live |= __any(T[p] > 0.0f) ? (1u << p) : 0u;
+        // Every pixel of the tile has terminated: the rest of this chunk (and every later chunk,
+        // which starts from a dead checkpoint) contributes nothing, and its partials keep the
+        // zeros the launcher cleared them to.
+        if (live == 0) break;
         uint32_t jl = 0, smask = 0;
         if (lane < cnt) {
             const uint32_t g = sorted_gid[range.x + base + lane];
@@ -402,7 +408,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
         }
         __syncthreads();
         uint64_t todo = __ballot((smask & live) != 0u);
-        uint64_t stored = 0;  // records whose moments were flushed
         int visited = 0, parked = 0;
         while (todo) {
             const int k = __builtin_ctzll(todo);
@@ -458,7 +463,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                     dst[8] = v[8];
                 }
                 if (lane == 0) qjl[parked] = (uint32_t)__builtin_amdgcn_readlane((int)jl, k);
-                stored |= 1ull << k;
                 if (++parked == kPark) {
                     park_flush(qpark, qjl, parked, p8f, p1, lane);
                     parked = 0;
@@ -473,12 +477,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
             }
         }
         if (parked) park_flush(qpark, qjl, parked, p8f, p1, lane);
-        if (lane < cnt && !((stored >> lane) & 1ull)) {  // no pixel took a gradient from it
-            float4* d8 = reinterpret_cast<float4*>(p8f) + 2 * (size_t)jl;
-            d8[0] = make_float4(0.f, 0.f, 0.f, 0.f);
-            d8[1] = make_float4(0.f, 0.f, 0.f, 0.f);
-            p1[jl] = 0.f;
-        }
         __syncthreads();  // srec / qpark are rewritten by the next batch
     }
 }
@@ -533,6 +531,11 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
     if (geo.nwg <= 0) return 0;
     const PartLayout pl(K);
     char* base = reinterpret_cast<char*>(partial);
+    // Partials of records no pixel takes a gradient from -- including every record after a
+    // tile's pixels have all terminated -- are never written by the kernel: one streaming clear
+    // (K x 36 B at the fill rate) replaces their scattered 36-B zero stores and the gid / rect
+    // reads that located them (at 5M Gaussians most of a tile list lies past termination).
+    if (hipError_t e = hipMemsetAsync(partial, 0, pl.total, s)) return (int)e;
     const int blocks = ck ? 8 * (geo.nwg / 8 + 1) * kMaxChunks : geo.nwg;
     hipLaunchKernelGGL(blend_backward_kernel, dim3(blocks), dim3(64), 0, s, geo, ranges, sorted_gid, rect, rec,
                        final_T, accum, dL_dpix, reinterpret_cast<float*>(base + pl.p8),
