@@ -273,12 +273,16 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
 // from LDS in fixed quad order and stored straight to the partial arrays at the record's
 // emission index j (8 moments in part8[2j..2j+1], the 9th in part1[j]).
 constexpr int kPark = 4;
+// Parking slot stride: 16 quads x 12 floats, padded by 12 so that the flush's 36 lanes (4 slots
+// x 9 moments) read 36 distinct banks -- at 192 the 4 slots alias (4-way LDS bank conflicts,
+// ~1 conflict cycle per LDS instruction of B1 in the PMC pass).
+constexpr int kParkSlot = 16 * 12 + 12;
 __device__ __forceinline__ void park_flush(const float* qpark, const uint32_t* qjl, int parked, float* p8f,
                                            float* p1, int lane) {
     __syncthreads();  // one-wave block: orders the quad leaders' LDS writes before the reads
     if (lane < parked * 9) {
         const int slot = lane / 9, c = lane - 9 * slot;
-        const float* q = qpark + slot * 16 * 12 + c;
+        const float* q = qpark + slot * kParkSlot + c;
         float t[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int i = 0; i < 16; ++i) t[i & 3] += q[i * 12];
@@ -322,7 +326,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                                                             float* __restrict__ p1,
                                                             const float4* __restrict__ ck) {
     __shared__ float4 srec[64 * 3];
-    __shared__ float qpark[kPark * 16 * 12];  // [slot][quad][9 of 12]
+    __shared__ float qpark[kPark * kParkSlot];  // [slot][quad][9 of 12]
     __shared__ uint32_t qjl[kPark];
     const int lane = threadIdx.x;
     float* const qlane = qpark + (lane >> 2) * 12;  // this quad's parking row
@@ -457,7 +461,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                 float v[9] = {sx, sy, sx * dx, sy * dx, syy, s0, g0, g1, g2};
                 quad_reduce9(v);
                 if ((lane & 3) == 0) {
-                    float* dst = qlane + parked * (16 * 12);
+                    float* dst = qlane + parked * kParkSlot;
                     *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
                     *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
                     dst[8] = v[8];

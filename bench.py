@@ -50,9 +50,12 @@ CONFIGS = {
     "5m_1080p": dict(P=5_000_000, W=1920, H=1080, D=3),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
-# wave64 VALU issue: 256 CUs x 4 SIMDs, one instruction per 4 cycles per SIMD, 2.4 GHz peak
-# clock (MI355X_MICROARCH 'vector-instruction ISSUE cost'; scripts/ubench/pk_rate.hip)
-VALU_ISSUE_PER_S = 256 * 4 * 2.4e9 / 4
+# wave64 VALU issue peak: 256 CUs x 4 SIMD-32 units, one wave64 op per 2 cycles per SIMD at
+# 2.4 GHz (MI355X_MICROARCH constants table, `v_fma_f32 (wave64) 2 cyc (SIMD-32)`).  The
+# sustained rate of an FMA-only stream, 8 waves per SIMD, ILP 8, measured here
+# (scripts/ubench/pk_rate.hip): 1.9 ns per wave-instruction per SIMD.
+VALU_ISSUE_PER_S = 256 * 4 * 2.4e9 / 2
+VALU_FMA_SUSTAINED_PER_S = 256 * 4 / 1.9e-9
 
 
 ALG_STAGES = ("preprocess", "scan", "duplicate", "tile_sort", "finalize", "blend_fwd", "blend_bwd",
@@ -230,14 +233,16 @@ def main():
                               "traffic": pmc.get("hbm_bytes_per_launch") if world == 1 else None, "mean_launch_ms": round(mean_ms, 4),
                               "algorithmic_bytes_per_launch": int(bytes_launch)}
         if "valu_insts_per_launch" in pmc and world == 1:  # PMC counts are of the N = 1 launch
-            # F6/B1 are VALU-issue-bound, not HBM-bound (DESIGN.md "Rooflines"): share of the
-            # chip's VALU issue slots (1024 SIMDs x one wave64 op per 4 cycles at 2.4 GHz) that
-            # the kernel's measured instruction count fills over its measured duration.
+            # F6/B1 are bound by VALU issue, not HBM: the kernel's measured
+            # instruction count over its measured duration, against the spec issue peak (1024
+            # SIMDs x one wave64 op per 2 cycles at 2.4 GHz) and the measured FMA stream rate.
             slots = VALU_ISSUE_PER_S * mean_ms * 1e-3
             result["roofline"]["valu_issue"] = {
                 "insts_per_launch": pmc["valu_insts_per_launch"],
                 "frac": round(pmc["valu_insts_per_launch"] / slots, 4),
-                "peak_insts_per_s": VALU_ISSUE_PER_S}
+                "peak_insts_per_s": VALU_ISSUE_PER_S,
+                "frac_of_sustained_fma_rate": round(
+                    pmc["valu_insts_per_launch"] / (VALU_FMA_SUSTAINED_PER_S * mean_ms * 1e-3), 4)}
         total_alg = sum(alg.values())
         result["pipeline_roofline"] = {
             "algorithmic_bytes_per_step": int(total_alg),
