@@ -756,6 +756,7 @@ static int backward_impl(const gsr_camera* cam, const gsr_gaussians* gs, const g
         if (!alloc_scratch) return fail(-1, "null scratch allocator");
         partial = static_cast<float*>(alloc_scratch(ctx, gsr_scratch_bytes((int32_t)K)));
         if (!partial) return fail(-2, "allocation failed (scratch, K=%lld)", K);
+        GSR_STAGE(GSR_STAGE_MISC, launch_clear_partial(partial, K, stream), "clear partials");
         GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.rect, v.rec,
                                             v.final_T, v.accum, dL_dpix, partial, K, v.ck, stream),
                       "blend backward");
@@ -819,6 +820,7 @@ int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raste
     const bool fuse = K > 0 && bin_variant() != 0 && ty0 == 0 && ty1 == div_up(cam->height, kTile) &&
                       bufs->num_ranked == P && fuse_gather();
     if (K > 0) {
+        GSR_STAGE(GSR_STAGE_MISC, launch_clear_partial(partial, K, stream), "clear partials");
         GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.rect, v.rec,
                                             v.final_T, v.accum, dL_dpix, partial, K, v.ck, stream),
                       "blend backward");

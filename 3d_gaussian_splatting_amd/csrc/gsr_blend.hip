@@ -87,9 +87,13 @@ struct BlendGeom {
 // Exact culling: a skipped stripe has no pixel that the per-pixel test would accept, so no
 // output bit changes; the ellipse test removes ~22 % of the box test's stripe evaluations
 // and ~17 % of the visited records at 1M/1080p (scripts/cull_stats.py).
-__device__ __forceinline__ float edge_min_q(float a, float b, float c, float u, float v0, float v1) {
-    // min over v in [v0, v1] of a u^2 + b u v + c v^2 (c > 0)
-    const float vs = fminf(fmaxf(-b * u / (2.0f * c), v0), v1);
+// min over v in [v0, v1] of a u^2 + b u v + c v^2 (c > 0), given k = -b / (2c): the minimiser
+// k u clamped to the edge.  k comes from a hardware reciprocal (1 ulp), not an IEEE division
+// (~11 instructions each, 16 per record): a minimiser off by a few ulp raises q by c d^2, far
+// inside the 2 % + 0.05 pad, and any point of the edge bounds the minimum from above only by
+// that amount, so the test stays conservative.
+__device__ __forceinline__ float edge_min_q(float a, float b, float c, float k, float u, float v0, float v1) {
+    const float vs = fminf(fmaxf(k * u, v0), v1);
     return fmaf(fmaf(c, vs, b * u), vs, a * u * u);
 }
 
@@ -103,6 +107,7 @@ __device__ inline uint32_t stripe_mask(const float4 r0, const float4 r1, const f
     const bool pd = ellipse && A > 0.0f && C > 0.0f && 4.0f * A * C - B * B > 0.0f;
     const float bound = fmaf(fmaxf(r2.w + 7.99435343f, 0.0f), 1.02f, 0.05f);  // log2(255 o)
     const float x0 = bx0 - r0.x, x1 = bx0 + 15.0f - r0.x;  // rect in mean-relative coords
+    const float kc = -B * __builtin_amdgcn_rcpf(2.0f * C), ka = -B * __builtin_amdgcn_rcpf(2.0f * A);
     uint32_t m = 0;
 #pragma unroll
     for (int p = 0; p < kPPL; ++p) {
@@ -111,8 +116,8 @@ __device__ inline uint32_t stripe_mask(const float4 r0, const float4 r1, const f
         if (hit && pd) {
             const float y0 = s0 - r0.y, y1 = s0 + 3.0f - r0.y;
             const bool inside = x0 <= 0.0f && x1 >= 0.0f && y0 <= 0.0f && y1 >= 0.0f;
-            const float q = fminf(fminf(edge_min_q(A, B, C, x0, y0, y1), edge_min_q(A, B, C, x1, y0, y1)),
-                                  fminf(edge_min_q(C, B, A, y0, x0, x1), edge_min_q(C, B, A, y1, x0, x1)));
+            const float q = fminf(fminf(edge_min_q(A, B, C, kc, x0, y0, y1), edge_min_q(A, B, C, kc, x1, y0, y1)),
+                                  fminf(edge_min_q(C, B, A, ka, y0, x0, x1), edge_min_q(C, B, A, ka, y1, x0, x1)));
             hit = inside || q <= bound;
         }
         m |= hit ? (1u << p) : 0u;
@@ -526,6 +531,15 @@ int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int 
     return (int)hipGetLastError();
 }
 
+// Partials of records no pixel takes a gradient from -- including every record after a tile's
+// pixels have all terminated -- are never written by blend_backward_kernel: one streaming clear
+// (K x 36 B at the fill rate) before it replaces their scattered 36-B zero stores and the gid /
+// rect reads that located them (at 5M Gaussians most of a tile list lies past termination).
+// A launch of its own so that stage timing separates it from the kernel.
+int launch_clear_partial(float* partial, long long K, hipStream_t s) {
+    return (int)hipMemsetAsync(partial, 0, PartLayout(K).total, s);
+}
+
 int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
                           const uint2* ranges, const uint32_t* sorted_gid, const uint4* rect,
                           const float4* rec, const float* final_T,
@@ -535,11 +549,6 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
     if (geo.nwg <= 0) return 0;
     const PartLayout pl(K);
     char* base = reinterpret_cast<char*>(partial);
-    // Partials of records no pixel takes a gradient from -- including every record after a
-    // tile's pixels have all terminated -- are never written by the kernel: one streaming clear
-    // (K x 36 B at the fill rate) replaces their scattered 36-B zero stores and the gid / rect
-    // reads that located them (at 5M Gaussians most of a tile list lies past termination).
-    if (hipError_t e = hipMemsetAsync(partial, 0, pl.total, s)) return (int)e;
     const int blocks = ck ? 8 * (geo.nwg / 8 + 1) * kMaxChunks : geo.nwg;
     hipLaunchKernelGGL(blend_backward_kernel, dim3(blocks), dim3(64), 0, s, geo, ranges, sorted_gid, rect, rec,
                        final_T, accum, dL_dpix, reinterpret_cast<float*>(base + pl.p8),

@@ -104,6 +104,8 @@ int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int 
 // B1: per-tile front-to-back gradients -> per-instance partial entry j (PartLayout), where the
 // emission index j = inst_start[g] + row-major index of the tile in g's band-clipped rect.
 // `partial` is the base of a PartLayout(K) block.
+// Zeroes the partial block launch_blend_backward fills (must precede it on the stream).
+int launch_clear_partial(float* partial, long long K, hipStream_t s);
 int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
                           const uint2* ranges, const uint32_t* sorted_gid, const uint4* rect,
                           const float4* rec, const float* final_T,
