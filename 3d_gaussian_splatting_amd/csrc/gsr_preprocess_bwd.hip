@@ -14,8 +14,6 @@
 // the normalised view direction, NDC mean through the homogeneous divide.
 //
 // Roofline: HBM-bound (V*(80+12M) + N*(60+12M) bytes).
-#include <cstdlib>
-
 #include "gsr_kernels.h"
 
 namespace gsr {
@@ -154,68 +152,11 @@ __device__ __forceinline__ BwdIn load_bwd_in(const GaussIn& in, int g, int o, co
     return load_bwd_in_g2(in, g, depth_key, flags, G2{src[0], src[1], src[2]});
 }
 
-// Unit view direction (x, y, z), its length, the SH basis of degree D at it and the basis
-// derivatives -- one expression set shared by both B2 forms (bit-identical results).
-struct ShDir {
-    float x, y, z, len;
-    float basis[16], dbx[16], dby[16], dbz[16];
-};
-__device__ __forceinline__ void sh_dir(const gsr_camera& cam, float p0, float p1, float p2, int D, ShDir& d) {
-    const float vx = p0 - cam.campos[0], vy = p1 - cam.campos[1], vz = p2 - cam.campos[2];
-    const float len = sqrtf(vx * vx + vy * vy + vz * vz);
-    const float x = vx / len, y = vy / len, z = vz / len;
-    d.x = x; d.y = y; d.z = z; d.len = len;
-    float* basis = d.basis;
-    float* dbx = d.dbx;
-    float* dby = d.dby;
-    float* dbz = d.dbz;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) basis[k] = dbx[k] = dby[k] = dbz[k] = 0.f;
-    basis[0] = kC0;
-    if (D >= 1) {
-        basis[1] = -kC1 * y; basis[2] = kC1 * z; basis[3] = -kC1 * x;
-        dby[1] = -kC1; dbz[2] = kC1; dbx[3] = -kC1;
-    }
-    if (D >= 2) {
-        const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-        basis[4] = kC2[0] * xy;
-        basis[5] = kC2[1] * yz;
-        basis[6] = kC2[2] * (2.0f * zz - xx - yy);
-        basis[7] = kC2[3] * xz;
-        basis[8] = kC2[4] * (xx - yy);
-        dbx[4] = kC2[0] * y; dby[4] = kC2[0] * x;
-        dby[5] = kC2[1] * z; dbz[5] = kC2[1] * y;
-        dbx[6] = kC2[2] * -2.f * x; dby[6] = kC2[2] * -2.f * y; dbz[6] = kC2[2] * 4.f * z;
-        dbx[7] = kC2[3] * z; dbz[7] = kC2[3] * x;
-        dbx[8] = kC2[4] * 2.f * x; dby[8] = kC2[4] * -2.f * y;
-        if (D >= 3) {
-            basis[9] = kC3[0] * y * (3.0f * xx - yy);
-            basis[10] = kC3[1] * xy * z;
-            basis[11] = kC3[2] * y * (4.0f * zz - xx - yy);
-            basis[12] = kC3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy);
-            basis[13] = kC3[4] * x * (4.0f * zz - xx - yy);
-            basis[14] = kC3[5] * z * (xx - yy);
-            basis[15] = kC3[6] * x * (xx - 3.0f * yy);
-            dbx[9] = kC3[0] * 6.f * xy; dby[9] = kC3[0] * 3.f * (xx - yy);
-            dbx[10] = kC3[1] * yz; dby[10] = kC3[1] * xz; dbz[10] = kC3[1] * xy;
-            dbx[11] = kC3[2] * -2.f * xy; dby[11] = kC3[2] * (4.f * zz - xx - 3.f * yy); dbz[11] = kC3[2] * 8.f * yz;
-            dbx[12] = kC3[3] * -6.f * xz; dby[12] = kC3[3] * -6.f * yz; dbz[12] = kC3[3] * (6.f * zz - 3.f * xx - 3.f * yy);
-            dbx[13] = kC3[4] * (4.f * zz - 3.f * xx - yy); dby[13] = kC3[4] * -2.f * xy; dbz[13] = kC3[4] * 8.f * xz;
-            dbx[14] = kC3[5] * 2.f * xz; dby[14] = kC3[5] * -2.f * yz; dbz[14] = kC3[5] * (xx - yy);
-            dbx[15] = kC3[6] * 3.f * (xx - yy); dby[15] = kC3[6] * -6.f * xy;
-        }
-    }
-}
-
 // One Gaussian's chain rule.  `lrest`: this thread's SH-rest row staged in LDS (read, then
 // overwritten in place with the row's gradient), or nullptr when there is no SH-rest input.
-// `dd_rest`: the SH-rest rows' share of the view-direction gradient (sum over k of
-// d basis_k / d dir (rest_k . dres)), when the caller has already accumulated it chunk by chunk
-// (preprocess_backward_kernel's chunked form) -- lrest is then nullptr.
 __device__ __forceinline__ void preprocess_backward_one(const gsr_camera& cam, const GaussIn& in, int g, int o,
                                                         const BwdIn& bi, const uint32_t* __restrict__ flags,
-                                                        const GradOut& out, float* lrest,
-                                                        const float* dd_rest = nullptr) {
+                                                        const GradOut& out, float* lrest) {
     const bool visible = bi.visible;
     // ---- 2D gradients ----
     float g2[9];
@@ -269,13 +210,46 @@ __device__ __forceinline__ void preprocess_backward_one(const gsr_camera& cam, c
         out.colors[3 * o + 1] = g2[7];
         out.colors[3 * o + 2] = g2[8];
     } else {
-        ShDir sd;
-        sh_dir(cam, p0, p1, p2, D, sd);
-        const float x = sd.x, y = sd.y, z = sd.z, len = sd.len;
-        const float* basis = sd.basis;
-        const float* dbx = sd.dbx;
-        const float* dby = sd.dby;
-        const float* dbz = sd.dbz;
+        const float vx = p0 - cam.campos[0], vy = p1 - cam.campos[1], vz = p2 - cam.campos[2];
+        const float len = sqrtf(vx * vx + vy * vy + vz * vz);
+        const float x = vx / len, y = vy / len, z = vz / len;
+        float basis[16], dbx[16], dby[16], dbz[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) basis[k] = dbx[k] = dby[k] = dbz[k] = 0.f;
+        basis[0] = kC0;
+        if (D >= 1) {
+            basis[1] = -kC1 * y; basis[2] = kC1 * z; basis[3] = -kC1 * x;
+            dby[1] = -kC1; dbz[2] = kC1; dbx[3] = -kC1;
+        }
+        if (D >= 2) {
+            const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+            basis[4] = kC2[0] * xy;
+            basis[5] = kC2[1] * yz;
+            basis[6] = kC2[2] * (2.0f * zz - xx - yy);
+            basis[7] = kC2[3] * xz;
+            basis[8] = kC2[4] * (xx - yy);
+            dbx[4] = kC2[0] * y; dby[4] = kC2[0] * x;
+            dby[5] = kC2[1] * z; dbz[5] = kC2[1] * y;
+            dbx[6] = kC2[2] * -2.f * x; dby[6] = kC2[2] * -2.f * y; dbz[6] = kC2[2] * 4.f * z;
+            dbx[7] = kC2[3] * z; dbz[7] = kC2[3] * x;
+            dbx[8] = kC2[4] * 2.f * x; dby[8] = kC2[4] * -2.f * y;
+            if (D >= 3) {
+                basis[9] = kC3[0] * y * (3.0f * xx - yy);
+                basis[10] = kC3[1] * xy * z;
+                basis[11] = kC3[2] * y * (4.0f * zz - xx - yy);
+                basis[12] = kC3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy);
+                basis[13] = kC3[4] * x * (4.0f * zz - xx - yy);
+                basis[14] = kC3[5] * z * (xx - yy);
+                basis[15] = kC3[6] * x * (xx - 3.0f * yy);
+                dbx[9] = kC3[0] * 6.f * xy; dby[9] = kC3[0] * 3.f * (xx - yy);
+                dbx[10] = kC3[1] * yz; dby[10] = kC3[1] * xz; dbz[10] = kC3[1] * xy;
+                dbx[11] = kC3[2] * -2.f * xy; dby[11] = kC3[2] * (4.f * zz - xx - 3.f * yy); dbz[11] = kC3[2] * 8.f * yz;
+                dbx[12] = kC3[3] * -6.f * xz; dby[12] = kC3[3] * -6.f * yz; dbz[12] = kC3[3] * (6.f * zz - 3.f * xx - 3.f * yy);
+                dbx[13] = kC3[4] * (4.f * zz - 3.f * xx - yy); dby[13] = kC3[4] * -2.f * xy; dbz[13] = kC3[4] * 8.f * xz;
+                dbx[14] = kC3[5] * 2.f * xz; dby[14] = kC3[5] * -2.f * yz; dbz[14] = kC3[5] * (xx - yy);
+                dbx[15] = kC3[6] * 3.f * (xx - yy); dby[15] = kC3[6] * -6.f * xy;
+            }
+        }
         // Clamp bits of the forward's SH->RGB: stored by a full-image forward, else recomputed
         // with the forward's exact arithmetic (same basis expressions and summation order, both
         // files built -ffp-contract=off; gsr_preprocess.hip) -- a banded forward skips SH for
@@ -300,11 +274,7 @@ __device__ __forceinline__ void preprocess_backward_one(const gsr_camera& cam, c
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) out.sh_dc[3 * o + ch] = basis[0] * dres[ch];
         float ddx = 0.f, ddy = 0.f, ddz = 0.f;
-        if (dd_rest) {
-            ddx = dd_rest[0];
-            ddy = dd_rest[1];
-            ddz = dd_rest[2];
-        } else if (lrest) {
+        if (lrest) {
             const float* rest = lrest;
             float* drest = lrest;
 #pragma unroll
@@ -471,11 +441,9 @@ __device__ __forceinline__ void preprocess_backward_one(const gsr_camera& cam, c
 }
 
 // Gaussians [g0, g0 + n): inputs indexed by g, grad2d and every output by o = g - g0.
-constexpr int kChunkK = 5;            // SH coefficients per staged chunk (as preprocess_kernel)
-constexpr int kChunkF = 3 * kChunkK;  // floats per row per chunk
 __global__ __launch_bounds__(256) void preprocess_backward_kernel(
     const gsr_camera cam, const GaussIn in, int g0, int n, const uint32_t* __restrict__ depth_key,
-    const uint32_t* __restrict__ flags, const float* __restrict__ grad2d, GradOut out, int b2_chunks) {
+    const uint32_t* __restrict__ flags, const float* __restrict__ grad2d, GradOut out) {
     extern __shared__ __attribute__((aligned(16))) float sh_lds[];
     const int o = blockIdx.x * 256 + threadIdx.x;
     const int M3 = in.M_rest * 3;
@@ -484,60 +452,6 @@ __global__ __launch_bounds__(256) void preprocess_backward_kernel(
     const size_t obase = (size_t)blockIdx.x * 256 * M3, ibase = (size_t)g0 * M3 + obase;
     BwdIn bi{};
     if (o < n) bi = load_bwd_in(in, g0 + o, o, depth_key, flags, grad2d);
-    if (stage && flags && b2_chunks) {
-        // Chunked form (stored clamp bits: the rows are needed only for the direction
-        // gradient): 5-coefficient column chunks of the block's rows pass through 15 KB of LDS
-        // -- staged, consumed and overwritten with their gradient, written back -- instead of
-        // the whole 46-KB rows.  Same k order, so bit-identical to the whole-row form.
-        const int col = threadIdx.x & 15, r0 = threadIdx.x >> 4;
-        const bool mine = o < n && bi.visible;
-        ShDir sd;
-        float dres[3] = {0.f, 0.f, 0.f};
-        if (mine) {
-            sh_dir(cam, bi.p0, bi.p1, bi.p2, in.D, sd);
-            dres[0] = (bi.cl & 1u) ? 0.f : bi.g2[6];
-            dres[1] = (bi.cl & 2u) ? 0.f : bi.g2[7];
-            dres[2] = (bi.cl & 4u) ? 0.f : bi.g2[8];
-        }
-        const int nb = (in.D + 1) * (in.D + 1);
-        float dd[3] = {0.f, 0.f, 0.f};
-        for (int c = 0; c < 3; ++c) {  // k = 1 + 5c .. 5 + 5c <= M_rest (block-uniform)
-            const int k0 = 1 + kChunkK * c;
-            if (k0 > in.M_rest) break;
-            const int f0 = kChunkF * c, nf = (in.M_rest - k0 + 1) * 3 < kChunkF ? (in.M_rest - k0 + 1) * 3 : kChunkF;
-            if (col < nf)
-                for (int r = r0; r < rows; r += 16) sh_lds[r * kChunkF + col] = in.sh_rest[ibase + (size_t)r * M3 + f0 + col];
-            __syncthreads();
-            if (o < n) {
-                float* row = sh_lds + threadIdx.x * kChunkF;
-#pragma unroll
-                for (int kk = 0; kk < kChunkK; ++kk) {
-                    const int k = k0 + kk;
-                    if (k > in.M_rest) break;
-                    if (mine && k < nb) {
-                        const float c0 = row[3 * kk + 0], c1 = row[3 * kk + 1], c2 = row[3 * kk + 2];
-                        row[3 * kk + 0] = sd.basis[k] * dres[0];
-                        row[3 * kk + 1] = sd.basis[k] * dres[1];
-                        row[3 * kk + 2] = sd.basis[k] * dres[2];
-                        const float sdot = c0 * dres[0] + c1 * dres[1] + c2 * dres[2];
-                        dd[0] += sd.dbx[k] * sdot;
-                        dd[1] += sd.dby[k] * sdot;
-                        dd[2] += sd.dbz[k] * sdot;
-                    } else {
-                        row[3 * kk + 0] = 0.f;
-                        row[3 * kk + 1] = 0.f;
-                        row[3 * kk + 2] = 0.f;
-                    }
-                }
-            }
-            __syncthreads();
-            if (col < nf)
-                for (int r = r0; r < rows; r += 16) out.sh_rest[obase + (size_t)r * M3 + f0 + col] = sh_lds[r * kChunkF + col];
-            __syncthreads();  // the next chunk reuses the LDS
-        }
-        if (o < n) preprocess_backward_one(cam, in, g0 + o, o, bi, flags, out, nullptr, dd);
-        return;
-    }
     if (stage) {  // coalesced staging of the block's SH-rest rows (see preprocess_kernel)
         for (int i = threadIdx.x; i < rows * M3; i += 256) sh_lds[i] = in.sh_rest[ibase + i];
         __syncthreads();
@@ -617,16 +531,9 @@ int launch_preprocess_backward(const gsr_camera& cam, const GaussIn& in, int g0,
                                const GradOut& out, hipStream_t s) {
     const int n = g1 - g0;
     if (n <= 0) return 0;
-    // A/B (bench/ablation only): GSR_B2_VARIANT=0 stages whole SH-rest rows (46 KB of LDS per
-    // block at SH3), 1 (shipped) streams them in 15-KB column chunks when the clamp bits are stored.
-    const char* e = std::getenv("GSR_B2_VARIANT");
-    const int chunks = e ? std::atoi(e) : 1;
-    const bool chunked = chunks != 0 && flags != nullptr && in.sh_rest && !in.colors;
-    const size_t lds = (in.sh_rest && !in.colors)
-                           ? (chunked ? sizeof(float) * 256 * kChunkF : sizeof(float) * 256 * 3 * in.M_rest)
-                           : 0;
+    const size_t lds = (in.sh_rest && !in.colors) ? sizeof(float) * 256 * 3 * in.M_rest : 0;
     hipLaunchKernelGGL(preprocess_backward_kernel, dim3(div_up(n, 256)), dim3(256), lds, s, cam, in, g0, n,
-                       depth_key, flags, grad2d, out, chunked ? 1 : 0);
+                       depth_key, flags, grad2d, out);
     return (int)hipGetLastError();
 }
 
