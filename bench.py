@@ -76,15 +76,17 @@ def algorithmic_bytes(P, V, K, pix, tiles, M):
     }
 
 
-def pmc_record(kernel_prefix):
+def pmc_record(kernel_prefix, workload):
     """Per-launch PMC figures of `kernel_prefix` (HBM bytes, VALU instructions) from the
     committed rocprofv3 passes (profiles/pmc_traffic.json, written by
-    scripts/pmc_summary.py --traffic), or {}."""
+    scripts/pmc_summary.py --traffic), or {} when those passes were of another workload."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return {}
     with open(path) as fh:
         data = json.load(fh)
+    if data.get("workload") != workload:
+        return {}
     for name, rec in data.get("kernels", {}).items():
         if name.startswith(kernel_prefix):
             return rec
@@ -226,7 +228,7 @@ def main():
         achieved = bytes_launch / (mean_ms * 1e-3) / 1e9
         kernel_name = {"blend_fwd": "blend_forward_kernel", "blend_bwd": "blend_backward_kernel",
                        "preprocess": "preprocess_kernel", "preprocess_bwd": "preprocess_backward_kernel"}.get(dom, dom)
-        pmc = pmc_record(kernel_name)
+        pmc = pmc_record(kernel_name, args.config)
         result["roofline"] = {"bound": "hbm", "kernel": kernel_name, "achieved": round(achieved, 2),
                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                               # PMC passes are of the N = 1 launch; a band launch has no committed counts

@@ -41,6 +41,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("--traffic", default=None)
+    ap.add_argument("--workload", default="1m_1080p", help="bench.py --config the passes ran")
     args = ap.parse_args()
     vals = load(args.dirs)
     kernels = sorted({k for k, _ in vals})
@@ -56,6 +57,7 @@ def main():
             (f"{table[k][c]:18.4g}" if c in table[k] else " " * 18) for c in counters))
     if args.traffic:
         out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU, separate passes",
+               "workload": args.workload,
                "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving)",
                "kernels": {}}
         for k in kernels:
