@@ -154,7 +154,7 @@ __device__ __forceinline__ int chunk_len(int n) {
 // T - alpha T (the reference's T (1 - alpha), one op shorter) is >= 1e-4; otherwise the pixel
 // terminates with T unchanged (SURVEY B.3 / forward.cu renderCUDA).  The exponent is
 // Horner-form: ((c' dy + b' dx) dy) + (a' dx^2 + log2 o), 3 ops per stripe with dy.
-template <int NW>
+template <int NW, bool BRANCHLESS = false>
 __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom geo,
                                                                 const uint2* __restrict__ ranges,
                                                                 const uint32_t* __restrict__ sorted_gid,
@@ -228,7 +228,12 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
                 const float K = fmaf(r0.z * dx, dx, r2.w);  // column part of the exponent + log2 o
 #pragma unroll
                 for (int p = 0; p < PPL; ++p) {
-                    if (!(m & (1u << p))) continue;  // wave-uniform
+                    // A culled stripe's pixels all get alpha 0 (exact test), which leaves C and T
+                    // bit-for-bit unchanged, so the skip is only a saving.  With two waves per
+                    // tile (shipped) both stripes of a visited record run in one basic block:
+                    // the two chains interleave, 0.257 vs 0.263 ms.  B1 keeps the branch (its
+                    // culled stripes skip 28 ops, branchless 0.518 vs 0.465 ms).
+                    if (!BRANCHLESS && !(m & (1u << p))) continue;  // wave-uniform
                     const float dy = r0.y - pfy[p];
                     const float e = fmaf(fmaf(r1.x, dy, bdx), dy, K);
                     float oG;
@@ -525,6 +530,9 @@ int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int 
     else if (v == 4)
         hipLaunchKernelGGL(blend_forward_kernel<4>, dim3(geo.nwg), dim3(256), 0, s, geo, ranges, sorted_gid, rec,
                            out_color, final_T, accum, ck);
+    else if (variant("GSR_F6_BRANCHLESS", 1))
+        hipLaunchKernelGGL((blend_forward_kernel<2, true>), dim3(geo.nwg), dim3(128), 0, s, geo, ranges, sorted_gid,
+                           rec, out_color, final_T, accum, ck);
     else
         hipLaunchKernelGGL(blend_forward_kernel<2>, dim3(geo.nwg), dim3(128), 0, s, geo, ranges, sorted_gid, rec,
                            out_color, final_T, accum, ck);
