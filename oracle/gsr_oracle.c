@@ -456,7 +456,7 @@ int gsro_forward(const gsro_camera* cam, int P, int D, int M_rest, const float* 
 static void blend_tile_backward(gsro_state* st, int tile, const float* dL_dpix, float* partial) {
     int W = st->cam.width, H = st->cam.height;
     int tx = tile % st->grid_x, ty = tile / st->grid_x;
-    uint32_t beg = st->ranges[2 * tile], end = st->ranges[2 * tile + 1];
+    uint32_t beg = st->ranges[2 * tile]; /* back to front from beg + n_contrib */
     const float ddelx_dx = 0.5f * (float)W, ddely_dy = 0.5f * (float)H;
     size_t npix = (size_t)W * H;
     for (int ly = 0; ly < TILE; ++ly)
