@@ -292,3 +292,24 @@ def test_fused_gather_backward_matches_two_kernels(monkeypatch):
         two = rast.backward_preprocess(st, rast.backward_blend(st, dpix))
         for k, v in fused.items():
             assert torch.equal(v, two[k]), (D, k)
+
+
+@pytest.mark.gpu
+def test_f6_stripe_variants_bit_identical(monkeypatch):
+    """F6's shipped branchless stripe pair (GSR_F6_BRANCHLESS=1) and the per-stripe branch
+    (=0) give the same image and, through F6's chunk checkpoints, the same gradients, bit for
+    bit: a culled stripe's pixels get alpha 0, which leaves C and T unchanged."""
+    R, gr, sc = pkg("rasterizer"), pkg("graphics"), pkg("scene")
+    dev = torch.device("cuda", 0)
+    cam = gr.synthetic_camera(640, 480)
+    s = sc.make_scene(cam, 60000, max_sh_degree=3, seed=23)
+    dpix = torch.tensor(sc.make_dL_dpix(cam, seed=24), device=dev)
+    out = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("GSR_F6_BRANCHLESS", v)
+        rast = R.CAbiRasterizer(dev)
+        st = rast.forward(cam, s.means3D, s.opacities, s.scales, s.rotations, s.sh_dc, s.sh_rest, sh_degree=3)
+        out[v] = (st.color.clone(), rast.backward(st, dpix))
+    assert torch.equal(out["0"][0], out["1"][0])
+    for k, g in out["0"][1].items():
+        assert torch.equal(g, out["1"][1][k]), k
