@@ -4,8 +4,9 @@
   lib/_gsr_torch*.so     libtorch render() + autograd Function (C++), links libgsr_hip.so
 
 Per-file flags: gsr_preprocess.hip is compiled with -ffp-contract=off so its key-feeding
-arithmetic is bit-identical to the CPU oracle; the blend / backward files keep hipcc's
-default FMA contraction (their outputs are compared within tolerance, not bitwise).
+arithmetic is bit-identical to the CPU oracle; the blend and preprocess-backward files too
+(B1 replays the forward's alpha / T bit for bit; B2 recomputes clamp bits like F1); the
+training kernels keep hipcc's default FMA contraction (compared within tolerance).
 """
 from __future__ import annotations
 
@@ -34,6 +35,8 @@ HIP_SOURCES = {
     "gsr_train.hip": [],
     # point-cloud initialisation (exact k-NN): box and point distances must round alike
     "gsr_init.hip": ["-ffp-contract=off"],
+    # multi-GPU splat pack / unpack / gradient sum (copies and integer work)
+    "gsr_shard.hip": [],
     "gsr_api.cpp": [],
 }
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fno-fast-math",

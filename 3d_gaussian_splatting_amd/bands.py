@@ -1,34 +1,69 @@
-"""Screen-space tile-row bands: the multi-GPU partition of the rasterizer (DESIGN.md §7,
-SURVEY §8e).
+"""Multi-GPU partition of the rasterizer (SURVEY §8e "scaling version").
 
-Rank r of N owns tile rows [rows[r], rows[r+1]) with rows[i] = floor(i * grid_y / N).  It
-bins and blends only those rows (``gsr_raster_settings.tile_y0/y1``), so its image band is
-bit-identical to the same rows of a single-GPU render.  The exchange is two collectives:
+Rank r of N owns
 
-* ``gather_image``: all-gather of the bands (padded to the tallest band) into the full
-  (3, H, W) image;
-* ``reduce_grad2d``: sum over ranks of the per-Gaussian 2D gradients (grad2d, P x 12
-  floats) that ``gsr_backward_blend`` leaves for each band; B2 then runs on the sum; or
-  ``reduce_scatter_grad2d``: each rank receives the sum for its own Gaussian slice
-  (``gaussian_slice``) and runs B2 on that slice only (``gsr_backward_preprocess_range``),
-  so the leaf gradients -- and an optimizer step after them -- are sharded by Gaussian.
+* the Gaussian shard [g0, g1) = ``gaussian_shard(P, N, r)`` (contiguous, in rank order): it
+  runs F1 (preprocess) and B2 (preprocess backward) for those Gaussians only, and its leaf
+  gradients -- and an optimizer step after them -- stay sharded;
+* the band of tile rows [rows[r], rows[r+1]): it bins, blends (F2..F6) and runs the blend
+  backward (B1) for those rows only.  ``balance_bands`` places the cuts so each band holds about
+  the same number of (Gaussian, tile) instances, from the per-tile-row instance histogram the
+  shard forward accumulates (``row_hist``, summed over ranks).
 
-``GradExchange`` / ``exchange_grad2d`` is the sparse form of the reduce-scatter: only a
-band's candidate Gaussians carry gradient, so only their rows travel.  ``ImageGather`` starts the image
-all-gather asynchronously so it overlaps the blend backward.
+One step (``ShardStep.step``) moves data three times, all over torch.distributed (RCCL on the
+GPU box, gloo in the CPU tests):
 
-Both work on any torch.distributed backend (RCCL on the GPU box, gloo in the CPU tests).
+1. all-to-all of the projected Gaussians ("splats", 64 B): shard -> every band its tile rect
+   overlaps.  Fixed-capacity blocks (``pair_cap`` splats per (source, band) pair, sized once
+   from a probe step) so the sizes never have to reach the host: one ``all_to_all_single``
+   with equal splits, the true counts ride in each block's header;
+2. all-gather of the band images, padded to the tallest band, asynchronous: it overlaps B1;
+3. all-to-all back of each splat's 48-B 2D gradient to its shard, which sums them per
+   Gaussian in band order (deterministic) before B2.
+
+Splats reach a band in (source rank, shard index) order, i.e. ascending global Gaussian id, so
+the band's canonical (tile, depth, gid) order and every pixel equal the single-GPU render.
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 TILE = 16
 
 
-def band_rows(grid_y: int, world: int, rank: int) -> tuple[int, int]:
-    """Tile-row range [y0, y1) of `rank` among `world` contiguous bands."""
-    return (rank * grid_y) // world, ((rank + 1) * grid_y) // world
+def gaussian_shard(P: int, world: int, rank: int) -> tuple[int, int]:
+    """Gaussians [g0, g1) rank `rank` owns (slices of ceil(P / world), the last one short)."""
+    S = -(-P // world)
+    return min(rank * S, P), min((rank + 1) * S, P)
+
+
+def equal_bands(grid_y: int, world: int) -> list[int]:
+    """Tile-row cuts of `world` bands of (nearly) equal height: rows[0] = 0 .. rows[world] = grid_y."""
+    return [(r * grid_y) // world for r in range(world + 1)]
+
+
+def balance_bands(row_counts, world: int) -> list[int]:
+    """Tile-row cuts so each band holds about total / world instances (row_counts[y] = the
+    instances in tile row y).  Each cut is the row boundary whose prefix sum is nearest the
+    target k * total / world, kept strictly increasing so no band is empty (world <= rows)."""
+    c = np.asarray(row_counts, dtype=np.float64)
+    gy = len(c)
+    if world > gy:
+        raise ValueError(f"{world} bands need at least as many tile rows (got {gy})")
+    pre = np.concatenate([[0.0], np.cumsum(c)])
+    total = pre[-1]
+    if total <= 0:
+        return equal_bands(gy, world)
+    rows = [0]
+    for k in range(1, world):
+        t = k * total / world
+        y = int(np.argmin(np.abs(pre - t)))
+        y = max(y, rows[-1] + 1)            # at least one row per band ...
+        y = min(y, gy - (world - k))        # ... and room for the bands after it
+        rows.append(y)
+    rows.append(gy)
+    return rows
 
 
 def band_pixel_rows(band: tuple[int, int], height: int) -> tuple[int, int]:
@@ -36,138 +71,27 @@ def band_pixel_rows(band: tuple[int, int], height: int) -> tuple[int, int]:
     return min(band[0] * TILE, height), min(band[1] * TILE, height)
 
 
-def max_band_pixel_rows(grid_y: int, world: int) -> int:
-    return max(b - a for a, b in (band_rows(grid_y, world, r) for r in range(world))) * TILE
-
-
-def gaussian_slice(P: int, world: int, rank: int) -> tuple[int, int]:
-    """Gaussians [g0, g1) whose leaf gradients rank `rank` owns (equal slices of
-    ceil(P / world), the last one short)."""
-    S = -(-P // world)
-    return min(rank * S, P), min((rank + 1) * S, P)
-
-
-def padded_rows(P: int, world: int) -> int:
-    return -(-P // world) * world
-
-
-def reduce_scatter_grad2d(grad2d_padded: torch.Tensor, dist, group=None) -> torch.Tensor:
-    """Sum grad2d (padded_rows(P, world) x 12) over ranks; return this rank's slice
-    (ceil(P / world) rows, the tail beyond P is padding)."""
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    S = grad2d_padded.shape[0] // world
-    if dist.get_backend(group) == "gloo":  # no reduce_scatter in gloo: all-reduce, keep the slice
-        dist.all_reduce(grad2d_padded, group=group)
-        return grad2d_padded[rank * S:(rank + 1) * S]
-    out = grad2d_padded.new_empty((S,) + tuple(grad2d_padded.shape[1:]))
-    dist.reduce_scatter_tensor(out, grad2d_padded, group=group)
-    return out
-
-
-_SIDE_STREAMS: dict = {}
-
-
-def _side_stream(dev: torch.device) -> torch.cuda.Stream:
-    if dev not in _SIDE_STREAMS:
-        _SIDE_STREAMS[dev] = torch.cuda.Stream(dev)
-    return _SIDE_STREAMS[dev]
-
-
-class GradExchange:
-    """Sparse reduce-scatter of the 2D gradients: a band only produced rows for its candidate
-    Gaussians (``cand``: their ids, e.g. ``GSR_VIEW_GID_BY_RANK``), so each rank sends just
-    those rows, bucketed by owning rank (``gaussian_slice``), in one all_to_all.  The gid
-    rides in padding column 9 of each row.
-
-    Two phases so the host never stalls the GPU: the constructor (right after the forward --
-    the candidates are known then) starts the all_to_all of the per-owner row counts and
-    copies the received counts to pinned host memory on a side stream that waits only for
-    that collective; ``run(grad2d)`` (after the blend backward has been enqueued) reads the
-    counts -- long since arrived -- and moves the rows.  The owner sums the rows it receives
-    source by source in rank order (each source sends a Gaussian at most once, so every
-    ``index_add_`` has unique indices): a fixed-order, deterministic sum.  ``run`` returns
-    this rank's slice (ceil(P / world) rows x 12)."""
-
-    def __init__(self, cand: torch.Tensor, P: int, dist, group=None):
-        self.dist, self.group = dist, group
-        self.world = dist.get_world_size(group)
-        self.rank = dist.get_rank(group)
-        self.S = -(-P // self.world)
-        cand = cand.to(torch.int64)
-        self.dev = cand.device
-        owner = torch.div(cand, self.S, rounding_mode="floor")
-        order = torch.argsort(owner, stable=True)
-        self.cs = cand[order]
-        send = torch.bincount(owner, minlength=self.world)
-        # gloo has no device all-to-all: stage through host memory there
-        self.host = dist.get_backend(group) == "gloo" and self.dev.type != "cpu"
-        if self.host or self.dev.type == "cpu":
-            xdev = torch.device("cpu")
-            send_x = send.to(xdev)
-            recv_x = torch.empty_like(send_x)
-            dist.all_to_all_single(recv_x, send_x, group=group)
-            self.sc, self.rc = send_x.tolist(), recv_x.tolist()
-            self.event = None
-            return
-        recv = torch.empty_like(send)
-        work = dist.all_to_all_single(recv, send, group=group, async_op=True)
-        side = _side_stream(self.dev)
-        side.wait_stream(torch.cuda.current_stream(self.dev))
-        with torch.cuda.stream(side):
-            work.wait()  # the side stream waits for the collective, the compute stream does not
-            self.send_h = torch.empty(self.world, dtype=torch.int64, pin_memory=True)
-            self.recv_h = torch.empty(self.world, dtype=torch.int64, pin_memory=True)
-            self.send_h.copy_(send, non_blocking=True)
-            self.recv_h.copy_(recv, non_blocking=True)
-            self.event = torch.cuda.Event()
-            self.event.record(side)
-        self._keep = (send, recv)
-
-    def run(self, grad2d: torch.Tensor) -> torch.Tensor:
-        width = grad2d.shape[1]
-        if width < 10:
-            raise ValueError("GradExchange: rows need a padding column 9 (GSR_GRAD2D_STRIDE = 12)")
-        if self.event is not None:
-            self.event.synchronize()
-            self.sc, self.rc = self.send_h.tolist(), self.recv_h.tolist()
-        dev = grad2d.device
-        rows = grad2d.index_select(0, self.cs)
-        rows[:, 9] = self.cs.to(torch.int32).view(torch.float32)
-        xdev = torch.device("cpu") if self.host else dev
-        got = torch.empty((sum(self.rc), width), dtype=rows.dtype, device=xdev)
-        self.dist.all_to_all_single(got, rows.to(xdev), self.rc, self.sc, group=self.group)
-        got = got.to(dev)
-        gid = got[:, 9].contiguous().view(torch.int32).to(torch.int64) - self.rank * self.S
-        out = grad2d.new_zeros((self.S, width))
-        off = 0
-        for n in self.rc:  # source ranks in order
-            if n:
-                out.index_add_(0, gid[off:off + n], got[off:off + n])
-            off += n
-        out[:, 9] = 0.0
-        return out
-
-
-def exchange_grad2d(grad2d: torch.Tensor, cand: torch.Tensor, P: int, dist, group=None) -> torch.Tensor:
-    """One-call form of ``GradExchange``: count exchange and row exchange back to back."""
-    return GradExchange(cand, P, dist, group).run(grad2d)
+def round_up(x: int, m: int = 256) -> int:
+    return -(-int(x) // m) * m
 
 
 class ImageGather:
-    """Asynchronous all-gather of the band images: start it after the forward, wait() for the
-    full (3, H, W) image after the backward -- the collective runs on the communicator's own
-    stream while the blend backward runs on the compute stream."""
+    """Asynchronous all-gather of the band images: start it after the band forward, wait() for
+    the full (3, H, W) image after the backward -- the collective runs on the communicator's
+    own stream while the blend backward runs on the compute stream.  Bands are padded to the
+    tallest one so a single all_gather_into_tensor (one RCCL call) moves them."""
 
-    def __init__(self, color: torch.Tensor, band: tuple[int, int], grid_y: int, dist, group=None):
-        self.world = dist.get_world_size(group)
+    def __init__(self, color: torch.Tensor, rows: list, rank: int, dist, group=None):
+        self.world = len(rows) - 1
         _, self.H, W = color.shape
-        self.grid_y = grid_y
-        rows = max_band_pixel_rows(grid_y, self.world)
-        py0, py1 = band_pixel_rows(band, self.H)
-        self.mine = color.new_zeros((3, rows, W))
+        self.rows = rows
+        tall = max(band_pixel_rows((rows[r], rows[r + 1]), self.H)[1] - band_pixel_rows((rows[r], rows[r + 1]),
+                                                                                     self.H)[0]
+                   for r in range(self.world))
+        py0, py1 = band_pixel_rows((rows[rank], rows[rank + 1]), self.H)
+        self.mine = color.new_zeros((3, max(tall, 1), W))
         self.mine[:, : py1 - py0] = color[:, py0:py1]
-        self.buf = color.new_empty((self.world, 3, rows, W))
+        self.buf = color.new_empty((self.world, 3, max(tall, 1), W))
         if dist.get_backend(group) != "gloo":
             self.work = dist.all_gather_into_tensor(self.buf.view(-1), self.mine.view(-1), group=group,
                                                     async_op=True)
@@ -179,18 +103,132 @@ class ImageGather:
         self.work.wait()
         out = self.color.new_empty((3, self.H, self.color.shape[2]))
         for r in range(self.world):
-            a0, a1 = band_pixel_rows(band_rows(self.grid_y, self.world, r), self.H)
+            a0, a1 = band_pixel_rows((self.rows[r], self.rows[r + 1]), self.H)
             out[:, a0:a1] = self.buf[r, :, : a1 - a0]
         return out
 
 
-def gather_image(color: torch.Tensor, band: tuple[int, int], grid_y: int, dist, group=None) -> torch.Tensor:
-    """All-gather the band rows of `color` (3, H, W; only this rank's band is valid) into the
-    full image (synchronous form of ImageGather).  Bands are padded to the tallest one so a
-    single all_gather_into_tensor (one RCCL call) moves them."""
-    return ImageGather(color, band, grid_y, dist, group).wait()
+def all_to_all_blocks(send: torch.Tensor, world: int, dist, group=None) -> torch.Tensor:
+    """Equal-split all-to-all of `world` contiguous blocks (block b -> rank b).  gloo has no
+    device all-to-all: staged through host memory there."""
+    recv = torch.empty_like(send)
+    if dist.get_backend(group) == "gloo" and send.device.type != "cpu":
+        h = send.cpu()
+        hr = torch.empty_like(h)
+        dist.all_to_all_single(hr, h, group=group)
+        recv.copy_(hr)
+    else:
+        dist.all_to_all_single(recv, send, group=group)
+    return recv
 
 
-def reduce_grad2d(grad2d: torch.Tensor, dist, group=None, async_op: bool = False):
-    """Sum the per-band 2D gradients over ranks in place (every rank gets the total)."""
-    return dist.all_reduce(grad2d, group=group, async_op=async_op)
+class ShardStep:
+    """Forward + backward of one rank of the multi-GPU path (rasterizer.ShardRasterizer calls,
+    the exchanges above in between).  `inputs`: the full Gaussian arrays (device tensors) --
+    each rank reads only its shard's rows.  ``plan`` sizes the exchange once from a probe:
+    the band cuts from the summed row histogram, ``pair_cap`` and the band's instance capacity
+    from the true counts, each with ``headroom``."""
+
+    def __init__(self, rast, cam, inputs: dict, sh_degree: int, dist, group=None, headroom: float = 1.25):
+        self.rast, self.cam, self.dist, self.group = rast, cam, dist, group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.D = sh_degree
+        self.headroom = headroom
+        P = int(inputs["means3D"].shape[0])
+        self.P = P
+        self.g0, self.g1 = gaussian_shard(P, self.world, self.rank)
+        self.shard = {k: (v[self.g0:self.g1] if v is not None else None) for k, v in inputs.items()}
+        self.gy = (cam.height + TILE - 1) // TILE
+        self.rows = equal_bands(self.gy, self.world)
+        self.pair_cap = 0
+        self.capacity = 0
+
+    def _shard_forward(self, pair_cap, row_hist=None):
+        return self.rast.shard_forward(self.cam, self.rows, pair_cap, **self.shard, sh_degree=self.D,
+                                       row_hist=row_hist)
+
+    def plan(self):
+        """Probe (synchronous, setup only): balanced band cuts, then the pair capacity and the
+        band's instance capacity."""
+        dev = self.shard["means3D"].device
+        hist = torch.zeros(self.gy, dtype=torch.int32, device=dev)
+        self._shard_forward(0, hist)  # pair_cap 0: headers only
+        self.dist.all_reduce(hist, group=self.group)
+        counts = hist.cpu().numpy().astype(np.int64)
+        self.rows = balance_bands(counts, self.world)
+        sh = self._shard_forward(0)
+        pc = sh.counts.to(torch.int64)
+        self.dist.all_reduce(pc, op=self.dist.ReduceOp.MAX, group=self.group)
+        self.pair_cap = round_up(max(int(pc.max()), 1) * self.headroom)
+        band_k = [int(counts[self.rows[b]:self.rows[b + 1]].sum()) for b in range(self.world)]
+        self.capacity = round_up(max(max(band_k), 1) * self.headroom)
+        self.band_instances = band_k
+        return self
+
+    @property
+    def band(self) -> tuple[int, int]:
+        return self.rows[self.rank], self.rows[self.rank + 1]
+
+    def forward(self):
+        sh = self._shard_forward(self.pair_cap)
+        recv = all_to_all_blocks(sh.send, self.world, self.dist, self.group)
+        st = self.rast.band_forward(self.cam, self.band, self.world, self.pair_cap, recv, self.capacity)
+        return sh, st
+
+    def step(self, dL_dpix: torch.Tensor):
+        """-> (full image, this shard's leaf gradients, shard state, band state)."""
+        sh, st = self.forward()
+        img = ImageGather(st.color, self.rows, self.rank, self.dist, self.group)  # overlaps B1
+        g2 = self.rast.band_backward(st, self.world, self.pair_cap, dL_dpix)
+        back = all_to_all_blocks(g2, self.world, self.dist, self.group)
+        grads = self.rast.shard_backward(sh, back)
+        return img.wait(), grads, sh, st
+
+
+def simulate_ranks(rast, cam, inputs: dict, sh_degree: int, world: int, dL_dpix: torch.Tensor,
+                   headroom: float = 1.25, rows=None, timer=None):
+    """Every rank's compute of one multi-GPU step, in one process on one GPU, with the
+    collectives replaced by block copies (same layouts as the RCCL exchange): the rehearsal of
+    scripts/band_sim.py and the GPU parity tests.  `timer(name, rank, fn)` (optional) wraps each
+    per-rank call.  Returns (image, leaf gradients of all P, plan dict)."""
+    run = timer or (lambda name, r, fn: fn())
+    P = int(inputs["means3D"].shape[0])
+    gy = (cam.height + TILE - 1) // TILE
+    shards = [gaussian_shard(P, world, r) for r in range(world)]
+    sub = lambda r: {k: (v[shards[r][0]:shards[r][1]] if v is not None else None) for k, v in inputs.items()}
+    dev = inputs["means3D"].device
+    if rows is None:  # probe 1: row histogram over all shards -> balanced cuts
+        hist = torch.zeros(gy, dtype=torch.int32, device=dev)
+        for r in range(world):
+            rast.shard_forward(cam, equal_bands(gy, world), 0, **sub(r), sh_degree=sh_degree, row_hist=hist)
+        counts = hist.cpu().numpy().astype(np.int64)
+        rows = balance_bands(counts, world)
+    else:
+        hist = torch.zeros(gy, dtype=torch.int32, device=dev)
+        for r in range(world):
+            rast.shard_forward(cam, rows, 0, **sub(r), sh_degree=sh_degree, row_hist=hist)
+        counts = hist.cpu().numpy().astype(np.int64)
+    pc = max(int(rast.shard_forward(cam, rows, 0, **sub(r), sh_degree=sh_degree).counts.max()) for r in range(world))
+    pair_cap = round_up(max(pc, 1) * headroom)
+    capacity = round_up(max(max(int(counts[rows[b]:rows[b + 1]].sum()) for b in range(world)), 1) * headroom)
+    shs = [run("shard_forward", r, lambda r=r: rast.shard_forward(cam, rows, pair_cap, **sub(r), sh_degree=sh_degree))
+           for r in range(world)]
+    blk = shs[0].send.numel() // world
+    image = torch.zeros((3, cam.height, cam.width), dtype=torch.float32, device=dev)
+    back_parts = [[None] * world for _ in range(world)]  # [src][band]
+    bsts = []
+    for b in range(world):
+        recv = torch.cat([shs[r].send[b * blk:(b + 1) * blk] for r in range(world)])
+        st = run("band_forward", b, lambda b=b, recv=recv: rast.band_forward(cam, (rows[b], rows[b + 1]), world,
+                                                                                pair_cap, recv, capacity,
+                                                                                out_color=image))
+        g2 = run("band_backward", b, lambda st=st: rast.band_backward(st, world, pair_cap, dL_dpix))
+        for r in range(world):
+            back_parts[r][b] = g2[r * pair_cap:(r + 1) * pair_cap]
+        bsts.append(st)
+    grads = [run("shard_backward", r, lambda r=r: rast.shard_backward(shs[r], torch.cat(back_parts[r])))
+             for r in range(world)]
+    full = {k: torch.cat([g[k] for g in grads]) for k in grads[0]}
+    return image, full, dict(rows=rows, pair_cap=pair_cap, capacity=capacity, shards=shs, bands=bsts,
+                             band_instances=[int(counts[rows[b]:rows[b + 1]].sum()) for b in range(world)])

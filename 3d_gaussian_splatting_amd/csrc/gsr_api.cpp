@@ -25,53 +25,6 @@ namespace {
 
 thread_local std::string g_err;
 
-// A/B selector (bench/ablation only): 0 = three-kernel scan then duplicate, 1 = fused
-// look-back scan + duplicate.  Shipped: fused for up to 2^19 ranked Gaussians (a band's
-// candidates: 0.030 vs 0.037 ms at 133k), three kernels above (0.084 vs 0.102 ms at 1M: the
-// look-back chain over n / 256 blocks dominates).
-int scan_variant(int n) {
-    const char* e = std::getenv("GSR_SCAN_VARIANT");
-    return e ? std::atoi(e) : (n <= (1 << 19) ? 1 : 0);
-}
-
-// Binning scheme (A/B, bench/ablation only); all three give the same canonical order.
-// Stage sums at 1M/1080p (scripts/ablate.py), whole forward + backward step:
-//   1 (shipped, 1.406 ms) = no global depth sort: the instances are emitted in gid order (the
-//       scan and F3 read tiles / rects coalesced), a stable LSD sort of the tile keys groups
-//       them by tile in gid order, and each tile's slice is sorted by depth alone with a stable
-//       LDS radix sort (launch_tile_depth_sort); the gather of B1's partials then also walks
-//       the Gaussians in gid order (0.079 vs 0.108 ms);
-//   0 (1.464 ms) = global LSD depth sort of the P (or band-candidate) keys before the scan,
-//       then the tile-key LSD sort (round-1's first design);
-//   2 (1.537 ms) = count binning: F3 counts instances per tile with atomics, one scan gives the
-//       ranges, a scatter with returning atomics groups them by tile (unordered), then a
-//       bitonic (depth, gid) sort per tile.  The 6.5 M atomics on 8160 hot words cost
-//       0.088 ms in F3 and 0.16 ms in the scatter -- more than the two LSD passes they replace.
-int bin_variant() {
-    const char* e = std::getenv("GSR_BIN_VARIANT");
-    return e ? std::atoi(e) : 1;
-}
-
-// A/B (bench/ablation only): 1 = binning variant 1 carries each instance's depth key through
-// the tile sort so the per-tile sort reads its keys contiguously; 0 (shipped) = the per-tile
-// sort gathers depth_key[gid].  Measured at 1M/1080p: carrying costs the tile sort +0.048 ms
-// (a third array per pass) and saves the per-tile sort only 0.005 ms -- the random 4-B gathers
-// hit L2 / MALL, and that sort is VALU-bound, not gather-bound.
-bool carry_depth() {
-    const char* e = std::getenv("GSR_CARRY_DEPTH");
-    return e ? std::atoi(e) != 0 : false;
-}
-
-// A/B (bench/ablation only): 1 = gsr_backward runs the gather and B2 as one kernel when the
-// ranking is the identity; 0 (shipped) = two kernels through the grad2d buffer.  Measured at
-// 1M/1080p: fused 0.215 ms vs 0.078 + 0.118 ms -- the fused block holds B2's 46 KB of SH
-// staging through the latency-bound gather phase (3 blocks per CU instead of 8), which costs
-// more than the 96 MB grad2d round trip it saves.
-bool fuse_gather() {
-    const char* e = std::getenv("GSR_FUSE_GATHER");
-    return e ? std::atoi(e) != 0 : false;
-}
-
 // Low-latency device->host read of one u32: DMA into a per-thread pinned word, then spin on
 // it.  hipStreamSynchronize after a pageable copy measured ~100 us from the end of the scan
 // to the next launch (profiles/r01_kernel_stats + trace); the spin wakes within ~µs.
@@ -181,11 +134,11 @@ struct StageTimer {
         std::lock_guard<std::mutex> lk(p.mu);
         a = p.get();
         b = p.get();
-        if (a && b) hipEventRecord(a, stream);
+        if (a && b) (void)hipEventRecord(a, stream);
     }
     ~StageTimer() {
         if (!a || !b) return;
-        hipEventRecord(b, stream);
+        (void)hipEventRecord(b, stream);
         Profiler& p = prof();
         std::lock_guard<std::mutex> lk(p.mu);
         p.pending.push_back({stage, a, b});
@@ -247,39 +200,55 @@ void band(const gsr_camera* cam, const gsr_raster_settings* rs, int* y0, int* y1
     if (*y1 < *y0) *y1 = *y0;
 }
 
+// Device pointers into the caller's buffers (layouts in gsr_internal.h).  n: Gaussians (or
+// received splat slots) indexed; cap: the binning's instance capacity.
 struct Views {
-    uint32_t *depth_key, *tiles, *offsets, *gid_by_rank;
+    uint32_t *depth_key, *tiles, *flags, *offsets, *partials, *lookback;
     float4* rec;
-    uint2* ranges;
-    float* final_T;
-    float* accum;
-    uint32_t *sorted_tile, *sorted_gid, *inst_gid;
     uint4* rect;
-    float4* ck;  // B1 chunk checkpoints (nullptr: not chunked)
+    uint2* ranges;
+    uint32_t *counters, *K_dev, *ovf, *ovf2, *term;
+    float *final_T, *accum;
+    float4* ck;
+    uint32_t *kA, *vA, *kB, *vB, *hist;
+    uint32_t *sorted_tile, *sorted_gid;  // where the tile sort's result lands
+    uint32_t *free_k, *free_v;           // the other ping-pong pair (scratch after the sort)
 };
 
-Views views(const gsr_camera* cam, int P, const gsr_buffers* b, int ck_tiles = 0) {
+Views views(const gsr_camera* cam, long long n, const gsr_buffers* b) {
     Views v{};
-    GeomLayout gl(P);
-    ImgLayout il(cam->width, cam->height, ck_tiles);
+    const GeomLayout gl(n);
+    const ImgLayout il(cam->width, cam->height);
     v.depth_key = at<uint32_t>(b->geom, gl.depth_key);
     v.tiles = at<uint32_t>(b->geom, gl.tiles);
+    v.flags = at<uint32_t>(b->geom, gl.flags);
     v.rec = at<float4>(b->geom, gl.rec);
-    v.offsets = at<uint32_t>(b->geom, gl.offsets);
     v.rect = at<uint4>(b->geom, gl.rect);
-    // 32-bit depth key = 4 passes (even) -> result in the A buffers
-    v.gid_by_rank = at<uint32_t>(b->geom, gl.sA_v);
+    v.offsets = at<uint32_t>(b->geom, gl.offsets);
+    v.partials = at<uint32_t>(b->geom, gl.partials);
+    v.lookback = at<uint32_t>(b->geom, gl.lookback);
     v.ranges = at<uint2>(b->image, il.ranges);
+    v.counters = at<uint32_t>(b->image, il.counters);
+    v.K_dev = v.counters + kTotalSlot;
+    v.ovf = at<uint32_t>(b->image, il.ovf);
+    v.ovf2 = at<uint32_t>(b->image, il.ovf2);
+    v.term = at<uint32_t>(b->image, il.term);
     v.final_T = at<float>(b->image, il.final_T);
     v.accum = at<float>(b->image, il.accum);
-    v.ck = ck_tiles ? at<float4>(b->image, il.ck) : nullptr;
+    v.ck = at<float4>(b->image, il.ck);
     if (b->binning) {
-        BinLayout bl(b->num_rendered);
+        const BinLayout bl(b->capacity);
+        v.kA = at<uint32_t>(b->binning, bl.kA);
+        v.vA = at<uint32_t>(b->binning, bl.vA);
+        v.kB = at<uint32_t>(b->binning, bl.kB);
+        v.vB = at<uint32_t>(b->binning, bl.vB);
+        v.hist = at<uint32_t>(b->binning, bl.hist);
         const int tiles = div_up(cam->width, kTile) * div_up(cam->height, kTile);
-        const bool odd = (tile_passes(tiles) & 1) != 0;
-        v.sorted_tile = at<uint32_t>(b->binning, odd ? bl.kB : bl.kA);
-        v.sorted_gid = at<uint32_t>(b->binning, odd ? bl.vB : bl.vA);
-        v.inst_gid = at<uint32_t>(b->binning, bl.inst_gid);
+        const bool odd = (tile_passes(tiles) & 1) != 0;  // the sort ends in (kB, vB) after odd passes
+        v.sorted_tile = odd ? v.kB : v.kA;
+        v.sorted_gid = odd ? v.vB : v.vA;
+        v.free_k = odd ? v.kA : v.kB;
+        v.free_v = odd ? v.vA : v.vB;
     }
     return v;
 }
@@ -297,328 +266,77 @@ __global__ void fill_background(float* out_color, float* final_T, float* accum,
     final_T[i] = 1.0f;
 }
 
-}  // namespace
-
-namespace gsr {
-// error hook for the other translation units of the library (gsr_train.hip)
-int set_error(int code, const char* msg) {
-    g_err = msg;
-    return code;
-}
-}  // namespace gsr
-
-extern "C" {
-
-int gsr_abi_version(void) { return GSR_ABI_VERSION; }
-const char* gsr_last_error(void) { return g_err.c_str(); }
-
-size_t gsr_geom_bytes(int32_t P) { return GeomLayout(P).total; }
-size_t gsr_binning_bytes(int32_t K) { return BinLayout(K).total; }
-size_t gsr_image_bytes(int32_t w, int32_t h) {
-    return ImgLayout(w, h, chunked_tiles(w, 0, div_up(h, kTile))).total;
-}
-size_t gsr_scratch_bytes(int32_t K) { return PartLayout(K).total; }
-
-// GSR_BIN_VARIANT=0 (A/B only): global depth sort of the P (or band-candidate) keys first.
-static int forward_global_depth(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
-                                float* out_color, int32_t* radii, gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_binning,
-                                gsr_alloc_fn alloc_image, void* ctx, gsr_buffers* bufs, void* stream_) {
-    hipStream_t stream = (hipStream_t)stream_;
-    const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
-    const int P = gs->P;
-    const int W = cam->width, H = cam->height;
-    const int gx = div_up(W, kTile), gy = div_up(H, kTile);
-    int ty0, ty1;
-    band(cam, rs, &ty0, &ty1);
-    std::memset(bufs, 0, sizeof *bufs);
-    bufs->geom = alloc_geom(ctx, GeomLayout(P).total);
-    const int ckt = chunked_tiles(W, ty0, ty1);
-    bufs->image = alloc_image(ctx, ImgLayout(W, H, ckt).total);
-    if (!bufs->geom || !bufs->image) return fail(-2, "allocation failed (geometry/image)");
-    GeomLayout gl(P);
-    ImgLayout il(W, H, ckt);
-    uint32_t* depth_key = at<uint32_t>(bufs->geom, gl.depth_key);
-    uint32_t* tiles = at<uint32_t>(bufs->geom, gl.tiles);
-    float4* rec = at<float4>(bufs->geom, gl.rec);
-    uint32_t* offsets = at<uint32_t>(bufs->geom, gl.offsets);
-    uint32_t* cand_tmp = at<uint32_t>(bufs->geom, gl.cand_tmp);
-    uint2* ranges = at<uint2>(bufs->image, il.ranges);
-    float* final_T = at<float>(bufs->image, il.final_T);
-
-    if ((ty0 > 0 || ty1 < gy) && !(rs->flags & GSR_FLAG_BAND_ONLY)) {
-        const int npix = W * H;
-        hipLaunchKernelGGL(fill_background, dim3(div_up(npix, 256)), dim3(256), 0, stream, out_color,
-                           final_T, at<float>(bufs->image, il.accum), npix, rs->bg[0], rs->bg[1],
-                           rs->bg[2]);
-        GSR_STAGE(GSR_STAGE_MISC, hipGetLastError(), "fill_background");
-    }
-    uint32_t* counters = at<uint32_t>(bufs->image, il.counters);
-    GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(ranges, 0, il.ovf - il.ranges, stream), "memset ranges");
-
-    long long K = 0;
-    if (P > 0) {
-        const bool full_img = ty0 == 0 && ty1 == gy;
-        PreOut po{radii, depth_key, tiles, rec, at<uint4>(bufs->geom, gl.rect),
-                  full_img ? at<uint32_t>(bufs->geom, gl.flags) : nullptr, counters};
-        GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess(*cam, gauss_in(gs), ty0, ty1, po, stream), "preprocess");
-        // A band ranks only its candidates (Gaussians with tiles in the band): the depth sort,
-        // scan, duplicate and gather then scale with the band, not with P.
-        const bool banded = ty0 > 0 || ty1 < gy;
-        int NR = P;
-        const uint32_t* sort_keys = depth_key;
-        const uint32_t* sort_vals = nullptr;
-        uint32_t cw[2 * kCountSlots];  // preprocess's count partials: candidates, then K
-        uint32_t cnt[2] = {0, 0};
-        auto sum_counts = [&] {
-            uint64_t c = 0, k = 0;
-            for (int i = 0; i < kCountSlots; ++i) c += cw[i], k += cw[kCountSlots + i];
-            cnt[0] = (uint32_t)(c < UINT32_MAX ? c : UINT32_MAX);
-            cnt[1] = (uint32_t)(k < UINT32_MAX ? k : UINT32_MAX);
-            return 0;
-        };
-        GSR_CHECK_HIP(begin_read(counters, 2 * kCountSlots, stream), "read counts");
-        if (banded) {
-            GSR_STAGE(GSR_STAGE_DEPTH_SORT, compact_candidates(tiles, depth_key, P, at<uint32_t>(bufs->geom, gl.partials),
-                                                               offsets, cand_tmp, counters + kCandCountSlot, stream),
-                      "band candidates");
-            GSR_STAGE(GSR_STAGE_MISC, end_read(counters, cw, 2 * kCountSlots, stream), "read counts");
-            sum_counts();
-            NR = (int)cnt[0];
-            sort_keys = offsets;  // free until the scan
-            sort_vals = cand_tmp;
-            if (colour_pass_needed(*cam, gauss_in(gs), ty0, ty1))
-                GSR_STAGE(GSR_STAGE_PREPROCESS, launch_colour(*cam, gauss_in(gs), cand_tmp, NR, rec, stream),
-                          "band colours");
-        }
-        bufs->num_ranked = NR;
-        int which = NR > 0 ? -1 : 1;
-        GSR_STAGE(GSR_STAGE_DEPTH_SORT, radix_sort(sort_keys, sort_vals, at<uint32_t>(bufs->geom, gl.sB_k),
-                                 at<uint32_t>(bufs->geom, gl.sB_v), at<uint32_t>(bufs->geom, gl.sA_k),
-                                 at<uint32_t>(bufs->geom, gl.sA_v), NR, 32, at<uint32_t>(bufs->geom, gl.hist),
-                                 &which, stream, true),
-                      "depth sort");
-        if (NR > 0 && which != 1) return fail(-12, "depth sort ended in an unexpected buffer");
-        // full image: K is read here, while the depth sort runs, so the host enqueues the rest
-        // of the forward without leaving the GPU idle
-        if (!banded) {
-            GSR_STAGE(GSR_STAGE_MISC, end_read(counters, cw, 2 * kCountSlots, stream), "read counts");
-            sum_counts();
-        }
-        const uint32_t* gid_by_rank = at<uint32_t>(bufs->geom, gl.sA_v);
-        const bool fused = scan_variant(NR) == 1;
-        if (NR > 0 && !fused) {
-            GSR_STAGE(GSR_STAGE_SCAN, inclusive_scan_gather(tiles, gid_by_rank, offsets, NR,
-                                                at<uint32_t>(bufs->geom, gl.partials), stream),
-                      "scan");
-        }
-        K = cnt[1];
-        if (K > INT32_MAX) return fail(-3, "num_rendered overflow (%lld)", K);
-        bufs->num_rendered = (int32_t)K;
-        bufs->binning = alloc_binning(ctx, BinLayout(K).total);
-        if (!bufs->binning) return fail(-2, "allocation failed (binning, K=%lld)", K);
-        BinLayout bl(K);
-        uint32_t* kA = at<uint32_t>(bufs->binning, bl.kA);
-        uint32_t* vA = at<uint32_t>(bufs->binning, bl.vA);
-        uint32_t* kB = at<uint32_t>(bufs->binning, bl.kB);
-        uint32_t* vB = at<uint32_t>(bufs->binning, bl.vB);
-        uint32_t* inst_gid = at<uint32_t>(bufs->binning, bl.inst_gid);
-        if (fused) {
-            GSR_STAGE(GSR_STAGE_DUPLICATE, launch_scan_duplicate(gid_by_rank, tiles, at<uint4>(bufs->geom, gl.rect), NR, gx, ty0,
-                                                offsets, kA, inst_gid,
-                                                at<uint32_t>(bufs->geom, gl.hist), stream),
-                      "scan + duplicate");
-        } else {
-            GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate(gid_by_rank, offsets, tiles, at<uint4>(bufs->geom, gl.rect), NR, gx, ty0, ty1,
-                                               kA, inst_gid, stream),
-                      "duplicate");
-        }
-        if (K > 0) {
-            int w2 = -1;
-            GSR_STAGE(GSR_STAGE_TILE_SORT, radix_sort(kA, inst_gid, kB, vB, kA, vA, K, tile_bits(gx * gy),
-                                     at<uint32_t>(bufs->binning, bl.hist), &w2, stream, false),
-                          "tile sort");
-            const bool odd = (tile_passes(gx * gy) & 1) != 0;
-            if ((w2 == 0) != odd) return fail(-12, "tile sort ended in an unexpected buffer");
-            GSR_STAGE(GSR_STAGE_FINALIZE, launch_finalize(odd ? kB : kA, K, ranges, stream),
-                          "finalize");
-        }
-    } else {
-        bufs->binning = alloc_binning(ctx, BinLayout(0).total);
-    }
-    const Views v = views(cam, P, bufs, ckt);
-    GSR_STAGE(GSR_STAGE_BLEND_FWD, launch_blend_forward(*cam, rs->bg, ty0, ty1, ranges, v.sorted_gid, rec, out_color, final_T,
-                                       v.accum, v.ck, stream),
-                  "blend forward");
-    return 0;
-}
-
-}  // extern "C"
-
-namespace {
-
-// One view's forward (binning variants 1 / 2), split at the host read of its instance count:
-// a batch enqueues phase 1 of every view before it waits once (gsr_forward_batch).
+// One forward, split at the (optional) host read of K so a batch can wait once for all views.
 struct FwdJob {
     const gsr_camera* cam;
-    const gsr_gaussians* gs;
     const gsr_raster_settings* rs;
     float* out_color;
-    int32_t* radii;
     gsr_buffers* bufs;
-    int ty0 = 0, ty1 = 0, gx = 0, gy = 0, ckt = 0;
-    bool full_img = true;
+    long long n = 0;  // Gaussians (or splat slots) indexed
+    int ty0 = 0, ty1 = 0, gx = 0, gy = 0;
 };
 
-// Allocations, background / range clears, F1, then the scan (full image) or the band's
-// candidate compaction.  read_counts: enqueue the D2H of F1's count partials right after F1,
-// so the scan / compaction run while the host waits for them.
-int fwd_phase1(FwdJob& j, gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_image, void* ctx, hipStream_t stream,
-               bool debug, bool read_counts) {
+// Allocations (geometry from the caller when geom_ready), range / counter clears, background
+// outside the band (unless band_pixels_only), then F1 via `pre` (may be empty: splats unpacked
+// by the caller) and the three-kernel scan when n is large.
+template <class Pre>
+int fwd_phase1(FwdJob& j, gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_image, void* ctx, hipStream_t stream, bool debug,
+               bool band_pixels_only, Pre&& pre) {
     const gsr_camera* cam = j.cam;
-    const gsr_gaussians* gs = j.gs;
     const gsr_raster_settings* rs = j.rs;
     gsr_buffers* bufs = j.bufs;
-    const int P = gs->P, W = cam->width, H = cam->height;
+    const int W = cam->width, H = cam->height;
     j.gx = div_up(W, kTile);
     j.gy = div_up(H, kTile);
     band(cam, rs, &j.ty0, &j.ty1);
-    j.full_img = j.ty0 == 0 && j.ty1 == j.gy;
     std::memset(bufs, 0, sizeof *bufs);
-    bufs->geom = alloc_geom(ctx, GeomLayout(P).total);
-    j.ckt = chunked_tiles(W, j.ty0, j.ty1);
-    bufs->image = alloc_image(ctx, ImgLayout(W, H, j.ckt).total);
+    bufs->num_rendered = -1;
+    bufs->n_local = (int32_t)j.n;
+    bufs->geom = alloc_geom(ctx, GeomLayout(j.n).total);
+    bufs->image = alloc_image(ctx, ImgLayout(W, H).total);
     if (!bufs->geom || !bufs->image) return fail(-2, "allocation failed (geometry/image)");
-    GeomLayout gl(P);
-    ImgLayout il(W, H, j.ckt);
-    uint2* ranges = at<uint2>(bufs->image, il.ranges);
-    if (!j.full_img && !(rs->flags & GSR_FLAG_BAND_ONLY)) {
+    const ImgLayout il(W, H);
+    const Views v = views(cam, j.n, bufs);
+    if ((j.ty0 > 0 || j.ty1 < j.gy) && !band_pixels_only) {
         const int npix = W * H;
-        hipLaunchKernelGGL(fill_background, dim3(div_up(npix, 256)), dim3(256), 0, stream, j.out_color,
-                           at<float>(bufs->image, il.final_T), at<float>(bufs->image, il.accum), npix, rs->bg[0],
-                           rs->bg[1], rs->bg[2]);
+        hipLaunchKernelGGL(fill_background, dim3(div_up(npix, 256)), dim3(256), 0, stream, j.out_color, v.final_T,
+                           v.accum, npix, rs->bg[0], rs->bg[1], rs->bg[2]);
         GSR_STAGE(GSR_STAGE_MISC, hipGetLastError(), "fill_background");
     }
-    GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(ranges, 0, il.ovf - il.ranges, stream), "memset ranges");
-    if (P == 0) return 0;
-    uint32_t* depth_key = at<uint32_t>(bufs->geom, gl.depth_key);
-    uint32_t* tiles = at<uint32_t>(bufs->geom, gl.tiles);
-    uint32_t* counters = at<uint32_t>(bufs->image, il.counters);
-    uint32_t* gid_by_rank = at<uint32_t>(bufs->geom, gl.sA_v);
-    PreOut po{j.radii, depth_key, tiles, at<float4>(bufs->geom, gl.rec), at<uint4>(bufs->geom, gl.rect),
-              j.full_img ? at<uint32_t>(bufs->geom, gl.flags) : nullptr, counters};
-    GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess(*cam, gauss_in(gs), j.ty0, j.ty1, po, stream), "preprocess");
-    if (read_counts) GSR_CHECK_HIP(begin_read(counters, 2 * kCountSlots, stream), "read counts");
-    if (!j.full_img) {
-        GSR_STAGE(GSR_STAGE_DEPTH_SORT, compact_candidates(tiles, depth_key, P, at<uint32_t>(bufs->geom, gl.partials),
-                                                           at<uint32_t>(bufs->geom, gl.offsets), gid_by_rank,
-                                                           counters + kCandCountSlot, stream),
-                  "band candidates");
-    } else {
-        // the scan needs no count; gid_by_rank = the identity ranking
-        GSR_STAGE(GSR_STAGE_SCAN, inclusive_scan_gather(tiles, nullptr, at<uint32_t>(bufs->geom, gl.offsets), P,
-                                                        at<uint32_t>(bufs->geom, gl.partials), stream, gid_by_rank),
-                  "scan");
-    }
+    GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(v.ranges, 0, il.ovf - il.ranges, stream), "clear ranges");
+    if (int e = pre(v)) return e;
+    GSR_STAGE(GSR_STAGE_SCAN, launch_scan(v.tiles, (int)j.n, v.offsets, v.partials, v.K_dev, stream), "scan");
     return 0;
 }
 
-// The rest, given F1's counts: band colours, binning, per-tile depth order, F6.
-int fwd_phase2(FwdJob& j, uint64_t csum, uint64_t ksum, gsr_alloc_fn alloc_binning, void* ctx, hipStream_t stream,
-               bool debug) {
+// The rest, given the binning capacity: F3 (with F2 when fused), tile sort, ranges, per-tile
+// depth order, F6.
+int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, hipStream_t stream, bool debug) {
     const gsr_camera* cam = j.cam;
-    const gsr_gaussians* gs = j.gs;
-    const gsr_raster_settings* rs = j.rs;
     gsr_buffers* bufs = j.bufs;
-    const int P = gs->P, gx = j.gx, gy = j.gy, ty0 = j.ty0, ty1 = j.ty1;
-    const bool full_img = j.full_img, scanned = j.full_img;
-    const int bv = bin_variant();
-    GeomLayout gl(P);
-    ImgLayout il(cam->width, cam->height, j.ckt);
-    uint32_t* depth_key = at<uint32_t>(bufs->geom, gl.depth_key);
-    uint32_t* tiles = at<uint32_t>(bufs->geom, gl.tiles);
-    float4* rec = at<float4>(bufs->geom, gl.rec);
-    uint32_t* offsets = at<uint32_t>(bufs->geom, gl.offsets);
-    uint32_t* counters = at<uint32_t>(bufs->image, il.counters);
-    uint2* ranges = at<uint2>(bufs->image, il.ranges);
-    uint32_t* gid_by_rank = at<uint32_t>(bufs->geom, gl.sA_v);
-    uint32_t* tcount = bv == 2 ? at<uint32_t>(bufs->image, il.tcount) : nullptr;
-    long long K = 0;
-    if (P > 0) {
-        int NR = P;
-        if (!full_img) {
-            NR = (int)(csum < (uint64_t)P ? csum : (uint64_t)P);
-            if (colour_pass_needed(*cam, gauss_in(gs), ty0, ty1))
-                GSR_STAGE(GSR_STAGE_PREPROCESS, launch_colour(*cam, gauss_in(gs), gid_by_rank, NR, rec, stream),
-                          "band colours");
-        }
-        bufs->num_ranked = NR;
-        K = (long long)ksum;
-        if (K > INT32_MAX) return fail(-3, "num_rendered overflow (%lld)", K);
-        bufs->num_rendered = (int32_t)K;
-        bufs->binning = alloc_binning(ctx, BinLayout(K).total);
-        if (!bufs->binning) return fail(-2, "allocation failed (binning, K=%lld)", K);
-        BinLayout bl(K);
-        uint32_t* kA = at<uint32_t>(bufs->binning, bl.kA);
-        uint32_t* vA = at<uint32_t>(bufs->binning, bl.vA);
-        uint32_t* kB = at<uint32_t>(bufs->binning, bl.kB);
-        uint32_t* vB = at<uint32_t>(bufs->binning, bl.vB);
-        uint32_t* inst_gid = at<uint32_t>(bufs->binning, bl.inst_gid);
-        // final (tile, gid) arrays where views() expects them, and the free pair beside them
-        const bool odd = (tile_passes(gx * gy) & 1) != 0;
-        uint32_t* fk = odd ? kB : kA;
-        uint32_t* fv = odd ? vB : vA;
-        uint32_t* sk = odd ? kA : kB;
-        uint32_t* sv = odd ? vA : vB;
-        uint32_t* dup_key = bv == 2 ? sk : kA;  // F3's tile keys (emission order)
-        // variant 1: F3 also writes each instance's depth key, the tile sort carries it, and
-        // the per-tile sort reads it contiguously instead of gathering depth_key[gid]
-        const bool carry = bv == 1 && carry_depth();
-        uint32_t* dA = at<uint32_t>(bufs->binning, bl.dA);
-        uint32_t* dB = at<uint32_t>(bufs->binning, bl.dB);
-        if (NR > 0 && !scanned && scan_variant(NR) == 1) {
-            GSR_STAGE(GSR_STAGE_DUPLICATE, launch_scan_duplicate(gid_by_rank, tiles, at<uint4>(bufs->geom, gl.rect), NR, gx,
-                                                                 ty0, offsets, dup_key, inst_gid,
-                                                                 at<uint32_t>(bufs->geom, gl.hist), stream, tcount,
-                                                                 depth_key, carry ? dA : nullptr),
-                      "scan + duplicate");
-        } else if (NR > 0) {
-            if (!scanned)
-                GSR_STAGE(GSR_STAGE_SCAN, inclusive_scan_gather(tiles, gid_by_rank, offsets, NR,
-                                                                at<uint32_t>(bufs->geom, gl.partials), stream),
-                          "scan");
-            GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate(gid_by_rank, offsets, tiles, at<uint4>(bufs->geom, gl.rect), NR,
-                                                            gx, ty0, ty1, dup_key, inst_gid, stream, tcount,
-                                                            depth_key, carry ? dA : nullptr),
-                      "duplicate");
-        }
-        if (K > 0) {
-            if (bv == 2) {
-                GSR_STAGE(GSR_STAGE_TILE_SORT, launch_tile_bins(sk, inst_gid, K, ty0 * gx, (ty1 - ty0) * gx, tcount, ranges,
-                                                                fk, fv, stream),
-                          "tile bins");
-            } else {
-                int w2 = -1;
-                GSR_STAGE(GSR_STAGE_TILE_SORT, radix_sort(kA, inst_gid, kB, vB, kA, vA, K, tile_bits(gx * gy),
-                                                          at<uint32_t>(bufs->binning, bl.hist), &w2, stream, false,
-                                                          carry ? dA : nullptr, dB, dA),
-                          "tile sort");
-                if ((w2 == 0) != odd) return fail(-12, "tile sort ended in an unexpected buffer");
-                GSR_STAGE(GSR_STAGE_FINALIZE, launch_finalize(fk, K, ranges, stream), "finalize");
-            }
-            GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_tile_depth_sort(ranges, ty0 * gx, (ty1 - ty0) * gx, K, depth_key, fv,
-                                                                   at<uint32_t>(bufs->image, il.ovf),
-                                                                   counters + kOvfCountSlot,
-                                                                   at<uint32_t>(bufs->image, il.ovf2),
-                                                                   counters + kOvf2CountSlot, sk, sv, stream, bv == 1,
-                                                                   carry ? (odd ? dB : dA) : nullptr),
-                      "per-tile depth order");
-        }
-    } else {
-        bufs->binning = alloc_binning(ctx, BinLayout(0).total);
+    if (cap > INT32_MAX) return fail(-3, "num_rendered overflow (%lld)", cap);
+    bufs->capacity = (int32_t)cap;
+    bufs->binning = alloc_binning(ctx, BinLayout(cap).total);
+    if (!bufs->binning) return fail(-2, "allocation failed (binning, %lld instances)", cap);
+    const Views v = views(cam, j.n, bufs);
+    const int tiles = j.gx * j.gy, ntiles = (j.ty1 - j.ty0) * j.gx;
+    GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate(v.tiles, v.rect, (int)j.n, j.gx, j.ty0, v.offsets, v.lookback, v.kA,
+                                                    v.vA, cap, v.K_dev, stream),
+              "duplicate");
+    if (cap > 0) {
+        int which = -1;
+        GSR_STAGE(GSR_STAGE_TILE_SORT, radix_sort(v.kA, v.vA, v.kB, v.vB, v.kA, v.vA, cap, v.K_dev, tile_bits(tiles),
+                                                  v.hist, &which, stream),
+                  "tile sort");
+        if ((which == 1) != (v.sorted_tile == v.kB)) return fail(-12, "tile sort ended in an unexpected buffer");
+        GSR_STAGE(GSR_STAGE_FINALIZE, launch_finalize(v.sorted_tile, cap, v.K_dev, v.ranges, stream), "finalize");
+        GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_tile_depth_sort(v.ranges, j.ty0 * j.gx, ntiles, cap, v.depth_key,
+                                                               v.sorted_gid, v.ovf, v.counters + kOvfCountSlot, v.ovf2,
+                                                               v.counters + kOvf2CountSlot, v.free_k, v.free_v, stream),
+                  "per-tile depth order");
     }
-    const Views v = views(cam, P, bufs, j.ckt);
-    GSR_STAGE(GSR_STAGE_BLEND_FWD, launch_blend_forward(*cam, rs->bg, ty0, ty1, ranges, v.sorted_gid, rec, j.out_color,
-                                                        at<float>(bufs->image, il.final_T), v.accum, v.ck, stream),
+    GSR_STAGE(GSR_STAGE_BLEND_FWD, launch_blend_forward(*cam, j.rs->bg, j.ty0, j.ty1, v.ranges, v.sorted_gid, v.rec,
+                                                        j.out_color, v.final_T, v.accum, v.term, v.ck, stream),
               "blend forward");
     return 0;
 }
@@ -643,136 +361,39 @@ __global__ __launch_bounds__(64) void batch_counts_kernel(CountPtrs p, uint32_t*
     }
 }
 
-}  // namespace
-
-extern "C" {
-
-int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
-                float* out_color, int32_t* radii, gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_binning,
-                gsr_alloc_fn alloc_image, void* ctx, gsr_buffers* bufs, void* stream_) {
-    g_err.clear();
-    if (int e = validate(cam, gs, rs)) return e;
-    if (!out_color || (gs->P > 0 && !radii) || !bufs || !alloc_geom || !alloc_binning || !alloc_image)
-        return fail(-1, "null output / allocator");
-    if (bin_variant() == 0)
-        return forward_global_depth(cam, gs, rs, out_color, radii, alloc_geom, alloc_binning, alloc_image, ctx, bufs,
-                                    stream_);
-    hipStream_t stream = (hipStream_t)stream_;
-    const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
-    FwdJob j{cam, gs, rs, out_color, radii, bufs};
-    if (int e = fwd_phase1(j, alloc_geom, alloc_image, ctx, stream, debug, true)) return e;
-    uint64_t csum = 0, ksum = 0;
-    if (gs->P > 0) {
-        uint32_t cw[2 * kCountSlots];
-        const uint32_t* counters = at<uint32_t>(bufs->image, ImgLayout(cam->width, cam->height, j.ckt).counters);
-        GSR_STAGE(GSR_STAGE_MISC, end_read(counters, cw, 2 * kCountSlots, stream), "read counts");
-        for (int i = 0; i < kCountSlots; ++i) csum += cw[i], ksum += cw[kCountSlots + i];
-    }
-    return fwd_phase2(j, csum, ksum, alloc_binning, ctx, stream, debug);
-}
-
-int gsr_forward_batch(int32_t V, const gsr_camera* cams, const gsr_gaussians* gs, const gsr_raster_settings* rs,
-                      float* const* out_colors, int32_t* const* radii, gsr_alloc_fn alloc_geom,
-                      gsr_alloc_fn alloc_binning, gsr_alloc_fn alloc_image, void* ctx, gsr_buffers* bufs,
-                      void* stream_) {
-    g_err.clear();
-    if (V < 0 || V > GSR_MAX_BATCH) return fail(-1, "batch: 0..%d views, got %d", GSR_MAX_BATCH, V);
-    if (V == 0) return 0;
-    if (!cams || !gs || !rs || !out_colors || !bufs || !alloc_geom || !alloc_binning || !alloc_image ||
-        (gs->P > 0 && !radii))
-        return fail(-1, "batch: null argument");
-    if (bin_variant() == 0) return fail(-1, "batch: needs the per-tile binning (GSR_BIN_VARIANT != 0)");
-    hipStream_t stream = (hipStream_t)stream_;
-    const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
-    std::vector<FwdJob> jobs;
-    jobs.reserve(V);
-    for (int v = 0; v < V; ++v) {
-        if (int e = validate(&cams[v], gs, rs)) return e;
-        if (rs->tile_y0 > 0 || rs->tile_y1 < div_up(cams[v].height, kTile))
-            return fail(-1, "batch: full-image views only (view %d)", v);
-        if (!out_colors[v] || (gs->P > 0 && !radii[v])) return fail(-1, "batch: null output of view %d", v);
-        jobs.push_back(FwdJob{&cams[v], gs, rs, out_colors[v], gs->P > 0 ? radii[v] : nullptr, &bufs[v]});
-        if (int e = fwd_phase1(jobs[v], alloc_geom, alloc_image, ctx, stream, debug, false)) return e;
-    }
-    std::vector<uint64_t> K(V, 0);
-    if (gs->P > 0) {
-        uint32_t* words = static_cast<uint32_t*>(alloc_image(ctx, 8 * (size_t)V));
-        if (!words) return fail(-2, "allocation failed (batch counts)");
-        CountPtrs cp{};
-        for (int v = 0; v < V; ++v)
-            cp.c[v] = at<uint32_t>(bufs[v].image, ImgLayout(cams[v].width, cams[v].height, jobs[v].ckt).counters);
-        hipLaunchKernelGGL(batch_counts_kernel, dim3(V), dim3(64), 0, stream, cp, words);
-        GSR_STAGE(GSR_STAGE_MISC, hipGetLastError(), "batch counts");
-        uint32_t host[2 * GSR_MAX_BATCH];
-        GSR_CHECK_HIP(begin_read(words, 2 * V, stream), "read counts");
-        GSR_STAGE(GSR_STAGE_MISC, end_read(words, host, 2 * V, stream), "read counts");
-        for (int v = 0; v < V; ++v) K[v] = (uint64_t)host[2 * v] | ((uint64_t)host[2 * v + 1] << 32);
-    }
-    for (int v = 0; v < V; ++v)
-        if (int e = fwd_phase2(jobs[v], (uint64_t)gs->P, K[v], alloc_binning, ctx, stream, debug)) return e;
+// F1 over Gaussians [0, P) with the count partials K is read from
+int run_preprocess(const gsr_camera* cam, const gsr_gaussians* gs, int ty0, int ty1, int32_t* radii, const Views& v,
+                   hipStream_t stream, bool debug) {
+    if (gs->P <= 0) return 0;
+    PreOut po{radii, v.depth_key, v.tiles, v.rec, v.rect, v.flags, v.counters};
+    GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess(*cam, gauss_in(gs), ty0, ty1, po, stream), "preprocess");
     return 0;
 }
 
-}  // extern "C"
-
-extern "C" {
-
-// SH clamp bits stored by the forward (full image), or nullptr: B2 recomputes them (band).
-static const uint32_t* stored_flags(const gsr_camera* cam, const gsr_raster_settings* rs, const gsr_buffers* b,
-                                    int P) {
+// B1 (+ the per-Gaussian gather into grad2d): shared by every backward entry point.
+int blend_backward(const gsr_camera* cam, const gsr_raster_settings* rs, const gsr_buffers* bufs, const float* dL_dpix,
+                   gsr_alloc_fn alloc_scratch, void* ctx, float* grad2d, hipStream_t stream, bool debug) {
+    if (!bufs || !bufs->geom || !bufs->image || !bufs->binning || !dL_dpix) return fail(-1, "missing forward buffers / dL_dpix");
+    if (!grad2d) return fail(-1, "null grad2d");
+    const long long n = bufs->n_local, cap = bufs->capacity;
+    if (n <= 0) return 0;
     int ty0, ty1;
     band(cam, rs, &ty0, &ty1);
-    if (ty0 != 0 || ty1 != div_up(cam->height, kTile)) return nullptr;
-    return at<uint32_t>(b->geom, GeomLayout(P).flags);
-}
-
-// Per-Gaussian grad2d for all P: the gather covers the ranked Gaussians (a band's candidates);
-// the rest touched no tile of the band and get zeros.
-static int gather_all(const gsr_camera* cam, const gsr_raster_settings* rs, const Views& v, const gsr_buffers* bufs,
-                      const float* partial, long long K, int P, float* grad2d, hipStream_t stream) {
-    const int NR = bufs->num_ranked > 0 ? bufs->num_ranked : P;
-    if (NR < P && !(rs->flags & GSR_FLAG_BAND_ONLY)) {
-        if (hipError_t e = hipMemsetAsync(grad2d, 0, sizeof(float) * kPart * (size_t)P, stream)) return (int)e;
-    }
-    return launch_gather_grad2d(v.gid_by_rank, v.offsets, partial, v.rec, cam->width, cam->height, K, NR, grad2d,
-                                stream);
-}
-
-static int backward_impl(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
-                         const gsr_buffers* bufs, const float* dL_dpix, gsr_alloc_fn alloc_scratch,
-                         void* ctx, const gsr_grads* grads, float* grad2d, void* stream_) {
-    if (int e = validate(cam, gs, rs)) return e;
-    if (!bufs || !bufs->geom || !bufs->image || !dL_dpix) return fail(-1, "missing forward buffers / dL_dpix");
-    hipStream_t stream = (hipStream_t)stream_;
-    const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
-    const int P = gs->P;
-    if (P == 0) return 0;
-    int ty0, ty1;
-    band(cam, rs, &ty0, &ty1);
-    const Views v = views(cam, P, bufs, chunked_tiles(cam->width, ty0, ty1));
-    const long long K = bufs->num_rendered;
-    float* partial = nullptr;
-    if (K > 0) {
-        if (!alloc_scratch) return fail(-1, "null scratch allocator");
-        partial = static_cast<float*>(alloc_scratch(ctx, gsr_scratch_bytes((int32_t)K)));
-        if (!partial) return fail(-2, "allocation failed (scratch, K=%lld)", K);
-        GSR_STAGE(GSR_STAGE_MISC, launch_clear_partial(partial, K, stream), "clear partials");
-        GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.rect, v.rec,
-                                            v.final_T, v.accum, dL_dpix, partial, K, v.ck, stream),
-                      "blend backward");
-    }
-    if (grad2d) {
-        if (K > 0) {
-            GSR_STAGE(GSR_STAGE_GATHER, gather_all(cam, rs, v, bufs, partial, K, P, grad2d, stream), "gather grad2d");
-        } else {
-            GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(grad2d, 0, sizeof(float) * kPart * (size_t)P, stream), "zero grad2d");
-        }
-        return 0;
-    }
+    const Views v = views(cam, n, bufs);
+    if (!alloc_scratch) return fail(-1, "null scratch allocator");
+    float* partial = static_cast<float*>(alloc_scratch(ctx, PartLayout(cap).total));
+    if (!partial) return fail(-2, "allocation failed (scratch, %lld instances)", cap);
+    GSR_STAGE(GSR_STAGE_MISC, launch_clear_partial(partial, cap, v.K_dev, stream), "clear partials");
+    GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.rect, v.rec,
+                                                         v.final_T, v.accum, dL_dpix, partial, cap, v.term, v.ck, stream),
+              "blend backward");
+    GSR_STAGE(GSR_STAGE_GATHER, launch_gather_grad2d(v.offsets, partial, v.rec, cam->width, cam->height, cap, (int)n,
+                                                     grad2d, stream),
+              "gather grad2d");
     return 0;
 }
 
-static int check_grads(const gsr_gaussians* gs, const gsr_grads* g) {
+int check_grads(const gsr_gaussians* gs, const gsr_grads* g) {
     if (!g || !g->dL_dmeans2D || !g->dL_dopacity || !g->dL_dmeans3D) return fail(-1, "missing gradient outputs");
     if (gs->colors_precomp ? !g->dL_dcolors : !g->dL_dsh_dc) return fail(-1, "missing colour/SH gradient output");
     if (!gs->colors_precomp && gs->sh_rest && !g->dL_dsh_rest) return fail(-1, "missing sh_rest gradient output");
@@ -781,7 +402,7 @@ static int check_grads(const gsr_gaussians* gs, const gsr_grads* g) {
     return 0;
 }
 
-static GradOut grad_out(const gsr_grads* g) {
+GradOut grad_out(const gsr_grads* g) {
     GradOut o;
     o.means2D = g->dL_dmeans2D;
     o.conic = g->dL_dconic;
@@ -796,6 +417,152 @@ static GradOut grad_out(const gsr_grads* g) {
     return o;
 }
 
+int band_rows_of(int32_t nbands, const int32_t* band_rows, int gy, BandRows& br) {
+    if (nbands < 1 || nbands > kMaxBands) return fail(-1, "nbands must be 1..%d (got %d)", kMaxBands, nbands);
+    if (!band_rows) return fail(-1, "null band_rows");
+    br.n = nbands;
+    for (int b = 0; b <= nbands; ++b) {
+        br.row[b] = band_rows[b];
+        if (band_rows[b] < 0 || band_rows[b] > gy || (b > 0 && band_rows[b] < band_rows[b - 1]))
+            return fail(-1, "band_rows must be non-decreasing within [0, %d]", gy);
+    }
+    if (band_rows[0] != 0 || band_rows[nbands] != gy) return fail(-1, "band_rows must cover tile rows [0, %d)", gy);
+    return 0;
+}
+
+GaussIn shard_in(const gsr_gaussians* gs) { return gauss_in(gs); }
+
+}  // namespace
+
+namespace gsr {
+// error hook for the other translation units of the library (gsr_train.hip)
+int set_error(int code, const char* msg) {
+    g_err = msg;
+    return code;
+}
+}  // namespace gsr
+
+extern "C" {
+
+int gsr_abi_version(void) { return GSR_ABI_VERSION; }
+const char* gsr_last_error(void) { return g_err.c_str(); }
+
+size_t gsr_geom_bytes(int32_t P) { return GeomLayout(P).total; }
+size_t gsr_binning_bytes(int32_t capacity) { return BinLayout(capacity).total; }
+size_t gsr_image_bytes(int32_t w, int32_t h) { return ImgLayout(w, h).total; }
+size_t gsr_scratch_bytes(int32_t capacity) { return PartLayout(capacity).total; }
+size_t gsr_exchange_block_bytes(int32_t pair_cap) { return exchange_block_bytes(pair_cap > 0 ? pair_cap : 0); }
+size_t gsr_shard_state_bytes(int32_t P, int32_t nbands, int32_t pair_cap) {
+    (void)pair_cap;
+    return ShardLayout(P, nbands > 0 ? nbands : 1).total;
+}
+
+int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
+                float* out_color, int32_t* radii, gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_binning,
+                gsr_alloc_fn alloc_image, void* ctx, gsr_buffers* bufs, void* stream_) {
+    g_err.clear();
+    if (int e = validate(cam, gs, rs)) return e;
+    if (!out_color || (gs->P > 0 && !radii) || !bufs || !alloc_geom || !alloc_binning || !alloc_image)
+        return fail(-1, "null output / allocator");
+    if (rs->max_rendered < 0) return fail(-1, "negative max_rendered");
+    hipStream_t stream = (hipStream_t)stream_;
+    const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
+    FwdJob j{cam, rs, out_color, bufs};
+    j.n = gs->P;
+    const bool exact = rs->max_rendered == 0;
+    if (int e = fwd_phase1(j, alloc_geom, alloc_image, ctx, stream, debug, false, [&](const Views& v) {
+            if (int e2 = run_preprocess(cam, gs, j.ty0, j.ty1, radii, v, stream, debug)) return e2;
+            // exact sizing: F1's count partials go to the host while the scan runs
+            if (exact && gs->P > 0) GSR_CHECK_HIP(begin_read(v.counters, 2 * kCountSlots, stream), "read counts");
+            return 0;
+        }))
+        return e;
+    long long cap = rs->max_rendered;
+    if (exact) {
+        uint64_t ksum = 0;
+        if (gs->P > 0) {
+            uint32_t cw[2 * kCountSlots];
+            const Views v = views(cam, j.n, bufs);
+            GSR_STAGE(GSR_STAGE_MISC, end_read(v.counters, cw, 2 * kCountSlots, stream), "read counts");
+            for (int i = 0; i < kCountSlots; ++i) ksum += cw[kCountSlots + i];
+        }
+        if (ksum > (uint64_t)INT32_MAX) return fail(-3, "num_rendered overflow (%llu)", (unsigned long long)ksum);
+        cap = (long long)ksum;
+        bufs->num_rendered = (int32_t)ksum;
+    }
+    return fwd_phase2(j, cap, alloc_binning, ctx, stream, debug);
+}
+
+int gsr_read_num_rendered(const gsr_camera* cam, const gsr_buffers* bufs, int32_t* num_rendered, void* stream_) {
+    g_err.clear();
+    if (!cam || !bufs || !bufs->image) return fail(-1, "null camera / buffers");
+    hipStream_t stream = (hipStream_t)stream_;
+    const Views v = views(cam, bufs->n_local, bufs);
+    uint32_t K = 0;
+    if (bufs->n_local > 0) {
+        if (int e = begin_read(v.K_dev, 1, stream)) return fail(-10, "read K: %s", hipGetErrorString((hipError_t)e));
+        if (int e = end_read(v.K_dev, &K, 1, stream)) return fail(-10, "read K: %s", hipGetErrorString((hipError_t)e));
+    }
+    if (num_rendered) *num_rendered = (int32_t)(K > (uint32_t)INT32_MAX ? INT32_MAX : K);
+    if ((long long)K > (long long)bufs->capacity)
+        return fail(GSR_ERR_OVERFLOW, "binning overflow: K = %u instances, capacity %d", K, bufs->capacity);
+    return 0;
+}
+
+int gsr_forward_batch(int32_t V, const gsr_camera* cams, const gsr_gaussians* gs, const gsr_raster_settings* rs,
+                      float* const* out_colors, int32_t* const* radii, gsr_alloc_fn alloc_geom,
+                      gsr_alloc_fn alloc_binning, gsr_alloc_fn alloc_image, void* ctx, gsr_buffers* bufs,
+                      void* stream_) {
+    g_err.clear();
+    if (V < 0 || V > GSR_MAX_BATCH) return fail(-1, "batch: 0..%d views, got %d", GSR_MAX_BATCH, V);
+    if (V == 0) return 0;
+    if (!cams || !gs || !rs || !out_colors || !bufs || !alloc_geom || !alloc_binning || !alloc_image ||
+        (gs->P > 0 && !radii))
+        return fail(-1, "batch: null argument");
+    if (rs->max_rendered < 0) return fail(-1, "negative max_rendered");
+    hipStream_t stream = (hipStream_t)stream_;
+    const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
+    const bool exact = rs->max_rendered == 0;
+    std::vector<FwdJob> jobs;
+    jobs.reserve(V);
+    for (int v = 0; v < V; ++v) {
+        if (int e = validate(&cams[v], gs, rs)) return e;
+        if (rs->tile_y0 > 0 || rs->tile_y1 < div_up(cams[v].height, kTile))
+            return fail(-1, "batch: full-image views only (view %d)", v);
+        if (!out_colors[v] || (gs->P > 0 && !radii[v])) return fail(-1, "batch: null output of view %d", v);
+        jobs.push_back(FwdJob{&cams[v], rs, out_colors[v], &bufs[v]});
+        jobs[v].n = gs->P;
+        int32_t* rad = gs->P > 0 ? radii[v] : nullptr;
+        if (int e = fwd_phase1(jobs[v], alloc_geom, alloc_image, ctx, stream, debug, false, [&](const Views& vw) {
+                return run_preprocess(&cams[v], gs, jobs[v].ty0, jobs[v].ty1, rad, vw, stream, debug);
+            }))
+            return e;
+    }
+    std::vector<long long> cap(V, rs->max_rendered);
+    if (exact && gs->P > 0) {
+        uint32_t* words = static_cast<uint32_t*>(alloc_image(ctx, 8 * (size_t)V));
+        if (!words) return fail(-2, "allocation failed (batch counts)");
+        CountPtrs cp{};
+        for (int v = 0; v < V; ++v) cp.c[v] = views(&cams[v], gs->P, &bufs[v]).counters;
+        hipLaunchKernelGGL(batch_counts_kernel, dim3(V), dim3(64), 0, stream, cp, words);
+        GSR_STAGE(GSR_STAGE_MISC, hipGetLastError(), "batch counts");
+        uint32_t host[2 * GSR_MAX_BATCH];
+        GSR_CHECK_HIP(begin_read(words, 2 * V, stream), "read counts");
+        GSR_STAGE(GSR_STAGE_MISC, end_read(words, host, 2 * V, stream), "read counts");
+        for (int v = 0; v < V; ++v) {
+            const uint64_t K = (uint64_t)host[2 * v] | ((uint64_t)host[2 * v + 1] << 32);
+            if (K > (uint64_t)INT32_MAX) return fail(-3, "num_rendered overflow (view %d)", v);
+            cap[v] = (long long)K;
+            bufs[v].num_rendered = (int32_t)K;
+        }
+    } else if (exact) {
+        for (int v = 0; v < V; ++v) cap[v] = 0, bufs[v].num_rendered = 0;
+    }
+    for (int v = 0; v < V; ++v)
+        if (int e = fwd_phase2(jobs[v], cap[v], alloc_binning, ctx, stream, debug)) return e;
+    return 0;
+}
+
 int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
                  const gsr_buffers* bufs, const float* dL_dpix, gsr_alloc_fn alloc_scratch, void* ctx,
                  const gsr_grads* grads, void* stream_) {
@@ -803,84 +570,151 @@ int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raste
     if (int e = validate(cam, gs, rs)) return e;
     if (gs->P == 0) return 0;
     if (int e = check_grads(gs, grads)) return e;
+    if (!bufs || bufs->n_local != gs->P) return fail(-1, "forward buffers do not match the Gaussians");
     hipStream_t stream = (hipStream_t)stream_;
     const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
-    if (!bufs || !bufs->geom || !bufs->image || !dL_dpix) return fail(-1, "missing forward buffers / dL_dpix");
     if (!alloc_scratch) return fail(-1, "null scratch allocator");
-    int ty0, ty1;
-    band(cam, rs, &ty0, &ty1);
-    const int P = gs->P;
-    const Views v = views(cam, P, bufs, chunked_tiles(cam->width, ty0, ty1));
-    const long long K = bufs->num_rendered;
-    // two scratch blocks: per-instance partials (K x 48 B) and per-Gaussian grad2d (P x 48 B)
-    float* partial = static_cast<float*>(alloc_scratch(ctx, gsr_scratch_bytes((int32_t)K)));
-    float* grad2d = static_cast<float*>(alloc_scratch(ctx, sizeof(float) * kPart * (size_t)P));
-    if (!partial || !grad2d) return fail(-2, "allocation failed (scratch, K=%lld, P=%d)", K, P);
-    // full image ranked in gid order (shipped binning): gather + B2 fused, grad2d unused
-    const bool fuse = K > 0 && bin_variant() != 0 && ty0 == 0 && ty1 == div_up(cam->height, kTile) &&
-                      bufs->num_ranked == P && fuse_gather();
-    if (K > 0) {
-        GSR_STAGE(GSR_STAGE_MISC, launch_clear_partial(partial, K, stream), "clear partials");
-        GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.rect, v.rec,
-                                            v.final_T, v.accum, dL_dpix, partial, K, v.ck, stream),
-                      "blend backward");
-        if (fuse) {
-            GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_gather_backward(*cam, gauss_in(gs), v.depth_key,
-                                                                       stored_flags(cam, rs, bufs, P), v.offsets,
-                                                                       partial, v.rec, K, grad_out(grads), stream),
-                      "gather + preprocess backward");
-            return 0;
-        }
-        GSR_STAGE(GSR_STAGE_GATHER, gather_all(cam, rs, v, bufs, partial, K, P, grad2d, stream),
-                  "gather grad2d");
-    } else {
-        GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(grad2d, 0, sizeof(float) * kPart * (size_t)P, stream), "zero grad2d");
-    }
-    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), 0, P, v.depth_key, stored_flags(cam, rs, bufs, P), grad2d,
-                                             grad_out(grads), stream),
-                  "preprocess backward");
+    float* grad2d = static_cast<float*>(alloc_scratch(ctx, sizeof(float) * kPart * (size_t)gs->P));
+    if (!grad2d) return fail(-2, "allocation failed (grad2d, P=%d)", gs->P);
+    if (int e = blend_backward(cam, rs, bufs, dL_dpix, alloc_scratch, ctx, grad2d, stream, debug)) return e;
+    const Views v = views(cam, gs->P, bufs);
+    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), 0, gs->P, v.depth_key, v.flags,
+                                                                   grad2d, grad_out(grads), stream),
+              "preprocess backward");
     return 0;
 }
 
 int gsr_backward_blend(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
                        const gsr_buffers* bufs, const float* dL_dpix, gsr_alloc_fn alloc_scratch, void* ctx,
-                       float* grad2d, void* stream) {
-    g_err.clear();
-    if (!grad2d && gs && gs->P > 0) return fail(-1, "null grad2d");
-    return backward_impl(cam, gs, rs, bufs, dL_dpix, alloc_scratch, ctx, nullptr, grad2d, stream);
-}
-
-int gsr_backward_preprocess_range(const gsr_camera* cam, const gsr_gaussians* gs,
-                                  const gsr_raster_settings* rs, const gsr_buffers* bufs, int32_t g0,
-                                  int32_t g1, const float* grad2d, const gsr_grads* grads, void* stream_) {
+                       float* grad2d, void* stream_) {
     g_err.clear();
     if (int e = validate(cam, gs, rs)) return e;
-    if (g0 < 0 || g1 > gs->P || g0 > g1) return fail(-1, "bad Gaussian range [%d, %d) for P=%d", g0, g1, gs->P);
-    if (g0 == g1) return 0;
+    if (gs->P == 0) return 0;
+    if (!bufs || bufs->n_local != gs->P) return fail(-1, "forward buffers do not match the Gaussians");
+    const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
+    return blend_backward(cam, rs, bufs, dL_dpix, alloc_scratch, ctx, grad2d, (hipStream_t)stream_, debug);
+}
+
+int gsr_backward_preprocess(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
+                            const gsr_buffers* bufs, const float* grad2d, const gsr_grads* grads, void* stream_) {
+    g_err.clear();
+    if (int e = validate(cam, gs, rs)) return e;
+    if (gs->P == 0) return 0;
     if (int e = check_grads(gs, grads)) return e;
     if (!bufs || !bufs->geom || !grad2d) return fail(-1, "missing forward buffers / grad2d");
     hipStream_t stream = (hipStream_t)stream_;
     const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
-    GeomLayout gl(gs->P);
-    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), g0, g1, at<uint32_t>(bufs->geom, gl.depth_key),
-                                             stored_flags(cam, rs, bufs, gs->P), grad2d,
-                                             grad_out(grads), stream),
-                  "preprocess backward");
+    const GeomLayout gl(gs->P);
+    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), 0, gs->P,
+                                                                   at<uint32_t>(bufs->geom, gl.depth_key),
+                                                                   at<uint32_t>(bufs->geom, gl.flags), grad2d,
+                                                                   grad_out(grads), stream),
+              "preprocess backward");
     return 0;
 }
 
-int gsr_backward_preprocess(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
-                            const gsr_buffers* bufs, const float* grad2d, const gsr_grads* grads,
-                            void* stream) {
-    if (!gs) return fail(-1, "null gaussians");
-    return gsr_backward_preprocess_range(cam, gs, rs, bufs, 0, gs->P, grad2d, grads, stream);
+// ---- multi-GPU: Gaussian shards x tile-row bands ----
+int gsr_shard_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs, int32_t nbands,
+                      const int32_t* band_rows, int32_t pair_cap, void* send, int32_t* radii, void* shard_state,
+                      uint32_t* row_hist, void* stream_) {
+    g_err.clear();
+    if (int e = validate(cam, gs, rs)) return e;
+    if (pair_cap < 0 || !send || !shard_state || (gs->P > 0 && !radii)) return fail(-1, "shard: null buffer / bad pair_cap");
+    const int gy = div_up(cam->height, kTile);
+    if (row_hist && gy > kMaxHistRows) return fail(-1, "shard: row histogram holds at most %d tile rows", kMaxHistRows);
+    BandRows br;
+    if (int e = band_rows_of(nbands, band_rows, gy, br)) return e;
+    hipStream_t stream = (hipStream_t)stream_;
+    const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
+    const int P = gs->P;
+    const ShardLayout sl(P, nbands);
+    const GeomLayout& gl = sl.geo;
+    uint32_t* depth_key = at<uint32_t>(shard_state, gl.depth_key);
+    uint32_t* tiles = at<uint32_t>(shard_state, gl.tiles);
+    float4* rec = at<float4>(shard_state, gl.rec);
+    uint4* rect = at<uint4>(shard_state, gl.rect);
+    if (P > 0) {
+        PreOut po{radii, depth_key, tiles, rec, rect, at<uint32_t>(shard_state, gl.flags), nullptr};
+        GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess(*cam, shard_in(gs), 0, gy, po, stream), "preprocess");
+    }
+    GSR_STAGE(GSR_STAGE_EXCHANGE, launch_pack_splats(tiles, rect, depth_key, rec, P, br,
+                                                     at<uint32_t>(shard_state, sl.partials), static_cast<char*>(send),
+                                                     pair_cap, at<uint32_t>(shard_state, sl.slot_of), row_hist, gy,
+                                                     stream),
+              "pack splats");
+    return 0;
+}
+
+int gsr_band_forward(const gsr_camera* cam, const gsr_raster_settings* rs, int32_t nsrc, int32_t pair_cap,
+                     const void* recv, float* out_color, gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_binning,
+                     gsr_alloc_fn alloc_image, void* ctx, gsr_buffers* bufs, void* stream_) {
+    g_err.clear();
+    if (!cam || !rs) return fail(-1, "null camera / settings");
+    if (nsrc < 1 || nsrc > kMaxBands || pair_cap < 0) return fail(-1, "band: bad nsrc / pair_cap");
+    if (!recv || !out_color || !bufs || !alloc_geom || !alloc_binning || !alloc_image)
+        return fail(-1, "band: null buffer / allocator");
+    if (rs->max_rendered <= 0) return fail(-1, "band: max_rendered (the band's instance capacity) is required");
+    const long long n = (long long)nsrc * pair_cap;
+    if (n > INT32_MAX) return fail(-1, "band: nsrc * pair_cap too large");
+    hipStream_t stream = (hipStream_t)stream_;
+    const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
+    FwdJob j{cam, rs, out_color, bufs};
+    j.n = n;
+    if (int e = fwd_phase1(j, alloc_geom, alloc_image, ctx, stream, debug, true, [&](const Views& v) {
+            GSR_STAGE(GSR_STAGE_EXCHANGE, launch_unpack_splats(static_cast<const char*>(recv), nsrc, pair_cap, j.ty0,
+                                                               j.ty1, v.rec, v.depth_key, v.tiles, v.rect, stream),
+                      "unpack splats");
+            return 0;
+        }))
+        return e;
+    return fwd_phase2(j, rs->max_rendered, alloc_binning, ctx, stream, debug);
+}
+
+int gsr_band_backward(const gsr_camera* cam, const gsr_raster_settings* rs, int32_t nsrc, int32_t pair_cap,
+                      const gsr_buffers* bufs, const float* dL_dpix, gsr_alloc_fn alloc_scratch, void* ctx,
+                      void* grad_send, void* stream_) {
+    g_err.clear();
+    if (!cam || !rs || !bufs || !grad_send) return fail(-1, "band backward: null argument");
+    if ((long long)nsrc * pair_cap != bufs->n_local) return fail(-1, "band backward: nsrc * pair_cap != the forward's");
+    const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
+    return blend_backward(cam, rs, bufs, dL_dpix, alloc_scratch, ctx, static_cast<float*>(grad_send),
+                          (hipStream_t)stream_, debug);
+}
+
+int gsr_shard_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs, int32_t nbands,
+                       const int32_t* band_rows, int32_t pair_cap, const void* shard_state, const void* grad_recv,
+                       const gsr_grads* grads, void* stream_) {
+    g_err.clear();
+    if (int e = validate(cam, gs, rs)) return e;
+    if (gs->P == 0) return 0;
+    if (int e = check_grads(gs, grads)) return e;
+    if (!shard_state || !grad_recv || pair_cap < 0) return fail(-1, "shard backward: null buffer / bad pair_cap");
+    BandRows br;
+    if (int e = band_rows_of(nbands, band_rows, div_up(cam->height, kTile), br)) return e;
+    hipStream_t stream = (hipStream_t)stream_;
+    const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
+    const int P = gs->P;
+    const ShardLayout sl(P, nbands);
+    const GeomLayout& gl = sl.geo;
+    const uint32_t* tiles = at<uint32_t>(shard_state, gl.tiles);
+    const uint4* rect = at<uint4>(shard_state, gl.rect);
+    float* grad2d = const_cast<float*>(at<float>(shard_state, sl.grad2d));
+    GSR_STAGE(GSR_STAGE_EXCHANGE, launch_grad_sum(tiles, rect, P, br, at<uint32_t>(shard_state, sl.slot_of),
+                                                  static_cast<const float*>(grad_recv), pair_cap, grad2d, stream),
+              "gradient sum");
+    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, shard_in(gs), 0, P,
+                                                                   at<uint32_t>(shard_state, gl.depth_key),
+                                                                   at<uint32_t>(shard_state, gl.flags), grad2d,
+                                                                   grad_out(grads), stream),
+              "preprocess backward");
+    return 0;
 }
 
 int gsr_profile_enable(uint32_t stage_mask) {
     Profiler& p = prof();
     std::lock_guard<std::mutex> lk(p.mu);
     for (auto& r : p.pending) {
-        hipEventSynchronize(r.b);
+        (void)hipEventSynchronize(r.b);
         p.pool.push_back(r.a);
         p.pool.push_back(r.b);
     }
@@ -915,15 +749,15 @@ int gsr_profile_read(double* ms, uint32_t* counts) {
 const char* gsr_stage_name(int stage) {
     static const char* names[GSR_NUM_STAGES] = {"preprocess", "depth_sort", "scan", "duplicate", "tile_sort",
                                                "finalize", "blend_fwd", "blend_bwd", "preprocess_bwd",
-                                               "gather_grad2d", "misc"};
+                                               "gather_grad2d", "misc", "exchange"};
     return (stage >= 0 && stage < GSR_NUM_STAGES) ? names[stage] : "?";
 }
 
 const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, int what) {
     if (!cam || !bufs || !bufs->geom || !bufs->image) return nullptr;
-    const Views v = views(cam, P, bufs);
+    const Views v = views(cam, bufs->n_local > 0 ? bufs->n_local : P, bufs);
     switch (what) {
-        case GSR_VIEW_RADII_SORTED_GID: return v.sorted_gid;
+        case GSR_VIEW_SORTED_GID: return v.sorted_gid;
         case GSR_VIEW_SORTED_TILE: return v.sorted_tile;
         case GSR_VIEW_RANGES: return v.ranges;
         case GSR_VIEW_FINAL_T: return v.final_T;
@@ -931,7 +765,8 @@ const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, 
         case GSR_VIEW_DEPTH_KEY: return v.depth_key;
         case GSR_VIEW_TILES_TOUCHED: return v.tiles;
         case GSR_VIEW_RECORDS: return v.rec;
-        case GSR_VIEW_GID_BY_RANK: return v.gid_by_rank;
+        case GSR_VIEW_COUNTS: return v.K_dev;
+        case GSR_VIEW_TERM: return v.term;
         default: return nullptr;
     }
 }

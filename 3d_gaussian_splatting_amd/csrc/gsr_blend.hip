@@ -35,8 +35,6 @@
 // register shuffles cost extra); 4 waves per tile; record prefetch into registers.  The
 // per-Gaussian sum happens later in fixed emission order (gsr_preprocess_bwd.hip), so
 // gradients are deterministic and no float atomics are issued.
-#include <cstdlib>
-
 #include "gsr_kernels.h"
 
 namespace gsr {
@@ -72,7 +70,6 @@ __device__ __forceinline__ void quad_reduce9(float (&v)[9]) {
 struct BlendGeom {
     int W, H, grid_x, ty0, nwg;
     float bg0, bg1, bg2;
-    int ellipse_cull;  // 1: exact ellipse stripe test on top of the box test (shipped)
 };
 
 // Which of the tile's four 16x4 pixel stripes (slot p = rows 4p..4p+3) can hold a pixel
@@ -97,14 +94,13 @@ __device__ __forceinline__ float edge_min_q(float a, float b, float c, float k, 
     return fmaf(fmaf(c, vs, b * u), vs, a * u * u);
 }
 
-__device__ inline uint32_t stripe_mask(const float4 r0, const float4 r1, const float4 r2, float bx0, float by0,
-                                       bool ellipse) {
+__device__ inline uint32_t stripe_mask(const float4 r0, const float4 r1, const float4 r2, float bx0, float by0) {
     const float ex = r2.y, ey = r2.z;
     if (!(ex >= 0.0f) || r0.x + ex < bx0 || r0.x - ex > bx0 + 15.0f) return 0u;
     const float ylo = r0.y - ey, yhi = r0.y + ey;
     // PD form coefficients (A dx^2 + B dx dy + C dy^2) and the log2-domain bound
     const float A = -r0.z, B = -r0.w, C = -r1.x;
-    const bool pd = ellipse && A > 0.0f && C > 0.0f && 4.0f * A * C - B * B > 0.0f;
+    const bool pd = A > 0.0f && C > 0.0f && 4.0f * A * C - B * B > 0.0f;
     const float bound = fmaf(fmaxf(r2.w + 7.99435343f, 0.0f), 1.02f, 0.05f);  // log2(255 o)
     const float x0 = bx0 - r0.x, x1 = bx0 + 15.0f - r0.x;  // rect in mean-relative coords
     const float kc = -B * __builtin_amdgcn_rcpf(2.0f * C), ka = -B * __builtin_amdgcn_rcpf(2.0f * A);
@@ -154,7 +150,7 @@ __device__ __forceinline__ int chunk_len(int n) {
 // T - alpha T (the reference's T (1 - alpha), one op shorter) is >= 1e-4; otherwise the pixel
 // terminates with T unchanged (SURVEY B.3 / forward.cu renderCUDA).  The exponent is
 // Horner-form: ((c' dy + b' dx) dy) + (a' dx^2 + log2 o), 3 ops per stripe with dy.
-template <int NW, bool BRANCHLESS = false>
+template <int NW>
 __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom geo,
                                                                 const uint2* __restrict__ ranges,
                                                                 const uint32_t* __restrict__ sorted_gid,
@@ -162,6 +158,7 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
                                                                 float* __restrict__ out_color,
                                                                 float* __restrict__ final_T,
                                                                 float* __restrict__ accum,
+                                                                uint32_t* __restrict__ term,
                                                                 float4* __restrict__ ck) {
     constexpr int PPL = kPPL / NW;
     constexpr int BATCH = 64 * NW;
@@ -187,6 +184,7 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
     // B1 chunk checkpoints: (T, colour sum) of every pixel before records CH, 2 CH, ...
     const int CH = chunk_len(n);
     int nck = 0;  // checkpoints written
+    int tend = n;  // termination index: every pixel of the tile has finished before record tend
     auto checkpoint = [&](int c) {
         float4* dst = ck + ((size_t)tl * (kMaxChunks - 1) + c) * 256;
 #pragma unroll
@@ -196,7 +194,10 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
         uint32_t live = 0;
 #pragma unroll
         for (int p = 0; p < PPL; ++p) live |= __any(T[p] > 0.0f) ? (1u << p) : 0u;
-        if (__syncthreads_or(live != 0) == 0) break;
+        if (__syncthreads_or(live != 0) == 0) {
+            tend = base;
+            break;
+        }
         if (base + tid < n) {
             const uint32_t g = sorted_gid[range.x + base + tid];
             const float4* r = rec + 3 * (size_t)g;
@@ -204,7 +205,7 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
             srec[3 * tid + 0] = r0;
             srec[3 * tid + 1] = r1;
             srec[3 * tid + 2] = r2;
-            smk[tid] = stripe_mask(r0, r1, r2, bx0, by0, geo.ellipse_cull);
+            smk[tid] = stripe_mask(r0, r1, r2, bx0, by0);
         } else {
             smk[tid] = 0u;
         }
@@ -212,14 +213,13 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
         const int cnt = (n - base) < BATCH ? (n - base) : BATCH;
         int visited = 0;
         for (int c0 = 0; c0 < cnt && live; c0 += 64) {
-            if (ck && base + c0 > 0 && (base + c0) % CH == 0) checkpoint(nck++);  // state before record base + c0
+            if (base + c0 > 0 && (base + c0) % CH == 0) checkpoint(nck++);  // state before record base + c0
             const uint32_t mine = (smk[c0 + lane] >> (w * PPL)) & ((1u << PPL) - 1u);
             uint64_t todo = __ballot((mine & live) != 0u && c0 + lane < cnt);
             while (todo) {
                 const int kk = __builtin_ctzll(todo);
                 todo &= todo - 1;
                 const int k = c0 + kk;
-                const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)mine, kk) & live;
                 const float4 r0 = srec[3 * k + 0];
                 const float4 r1 = srec[3 * k + 1];
                 const float4 r2 = srec[3 * k + 2];
@@ -228,12 +228,12 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
                 const float K = fmaf(r0.z * dx, dx, r2.w);  // column part of the exponent + log2 o
 #pragma unroll
                 for (int p = 0; p < PPL; ++p) {
-                    // A culled stripe's pixels all get alpha 0 (exact test), which leaves C and T
-                    // bit-for-bit unchanged, so the skip is only a saving.  With two waves per
-                    // tile (shipped) both stripes of a visited record run in one basic block:
-                    // the two chains interleave, 0.257 vs 0.263 ms.  B1 keeps the branch (its
+                    // No per-stripe branch: a culled stripe's pixels all get alpha 0 (exact test),
+                    // which leaves C and T bit-for-bit unchanged, and with two waves per tile both
+                    // stripes of a visited record run in one basic block -- the two chains
+                    // interleave (0.257 vs 0.263 ms with the branch; with four waves a visited
+                    // record always covers the wave's one stripe).  B1 keeps the branch (its
                     // culled stripes skip 28 ops, branchless 0.518 vs 0.465 ms).
-                    if (!BRANCHLESS && !(m & (1u << p))) continue;  // wave-uniform
                     const float dy = r0.y - pfy[p];
                     const float e = fmaf(fmaf(r1.x, dy, bdx), dy, K);
                     float oG;
@@ -258,8 +258,11 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
         }
         __syncthreads();
     }
-    if (ck)  // the list ended or every pixel finished: later chunks start from the final state
-        for (; nck * CH + CH < n && nck < kMaxChunks - 1; ++nck) checkpoint(nck);
+    // The list ended or every pixel finished: the remaining chunks that start before the
+    // termination index begin from the final state (a wave whose own pixels finished early stops
+    // writing checkpoints in the loop); chunks from tend on are skipped by B1 (term[]).
+    for (; nck * CH + CH < tend && nck < kMaxChunks - 1; ++nck) checkpoint(nck);
+    if (threadIdx.x == 0) term[tile] = (uint32_t)tend;
     const size_t npix = (size_t)geo.W * geo.H;
 #pragma unroll
     for (int p = 0; p < PPL; ++p) {
@@ -319,8 +322,8 @@ __device__ __forceinline__ void park_flush(const float* qpark, const uint32_t* q
 // B1 stores the raw tile sums (Sx, Sy, Sxx, Sxy, Syy, S0, colour x3); they are linear in the
 // gradients, so gather_grad2d converts them once per Gaussian after summing over tiles.
 //
-// Grid: one 64-lane block per (tile, chunk) when F6 wrote chunk checkpoints (ck), else per
-// tile.  Each XCD (blocks b with equal b % 8) takes a contiguous tile range as in xcd_tile,
+// Grid: one 64-lane block per (tile, chunk); a chunk resumes from F6's checkpoint, and chunks
+// from the tile's termination index on exit at once.  Each XCD (blocks b with equal b % 8) takes a contiguous tile range as in xcd_tile,
 // visited chunk-major, so every tile's front chunk -- the longest -- is dispatched first.
 // 6 waves per SIMD: 80 VGPRs (no spills) and 6.2 KB of LDS per one-wave block.  Measured
 // 0.552 ms vs 0.564 at the compiler's own 85 VGPRs (5 waves); 7 and 8 waves spill.
@@ -334,6 +337,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                                                             const float* __restrict__ dL_dpix,
                                                             float* __restrict__ p8f,
                                                             float* __restrict__ p1,
+                                                            const uint32_t* __restrict__ term,
                                                             const float4* __restrict__ ck) {
     __shared__ float4 srec[64 * 3];
     __shared__ float qpark[kPark * kParkSlot];  // [slot][quad][9 of 12]
@@ -341,7 +345,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
     const int lane = threadIdx.x;
     float* const qlane = qpark + (lane >> 2) * 12;  // this quad's parking row
     int tl, chunk;
-    if (ck) {
+    {
         const int q = geo.nwg / 8, r = geo.nwg % 8, xcd = blockIdx.x % 8, local = blockIdx.x / 8;
         const int t0 = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q, nt = q + (xcd < r ? 1 : 0);
         const int per = q + 1;  // padded tiles per XCD
@@ -349,11 +353,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
         const int i = local - chunk * per;
         if (i >= nt) return;
         tl = t0 + i;
-    } else {
-        tl = xcd_tile(blockIdx.x, geo.nwg);
-        chunk = 0;
     }
     const int tile = tl + geo.ty0 * geo.grid_x;
+    const uint2 range = ranges[tile];
+    const int n_all = (int)(range.y - range.x);
+    const int CH = chunk_len(n_all);
+    const int start = chunk * CH;
+    // no such chunk for this tile, or every pixel had finished before it (F6's term[])
+    if (start >= n_all || start >= (int)term[tile]) return;
+    const int n = start + CH < n_all ? start + CH : n_all;
     const int tx = tile % geo.grid_x, ty = tile / geo.grid_x;
     const int px = tx * kTile + (lane & 15);
     const float pfx = (float)px;
@@ -377,22 +385,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
         R[p] = sdp + Tfin * (geo.bg0 * dp0[p] + geo.bg1 * dp1[p] + geo.bg2 * dp2[p]);
         T[p] = in ? 1.0f : -1.0f;
     }
-    const uint2 range = ranges[tile];
-    const int n_all = (int)(range.y - range.x);
-    int start = 0, n = n_all;
-    if (ck) {
-        const int CH = chunk_len(n_all);
-        start = chunk * CH;
-        if (start >= n_all) return;  // no such chunk for this tile
-        n = start + CH < n_all ? start + CH : n_all;
-        if (chunk > 0) {  // resume from F6's checkpoint: T, and R less dL/dpix . (colour sum so far)
-            const float4* src = ck + ((size_t)tl * (kMaxChunks - 1) + (chunk - 1)) * 256;
+    if (chunk > 0) {  // resume from F6's checkpoint: T, and R less dL/dpix . (colour sum so far)
+        const float4* src = ck + ((size_t)tl * (kMaxChunks - 1) + (chunk - 1)) * 256;
 #pragma unroll
-            for (int p = 0; p < kPPL; ++p) {
-                const float4 c4 = src[64 * p + lane];
-                T[p] = c4.x;
-                R[p] -= fmaf(c4.y, dp0[p], fmaf(c4.z, dp1[p], c4.w * dp2[p]));
-            }
+        for (int p = 0; p < kPPL; ++p) {
+            const float4 c4 = src[64 * p + lane];
+            T[p] = c4.x;
+            R[p] -= fmaf(c4.y, dp0[p], fmaf(c4.z, dp1[p], c4.w * dp2[p]));
         }
     }
     for (int base = start; base < n; base += 64) {
@@ -417,7 +416,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                 srec[3 * lane + 0] = r0;
                 srec[3 * lane + 1] = r1;
                 srec[3 * lane + 2] = r2;
-                smask = stripe_mask(r0, r1, r2, bx0, by0, geo.ellipse_cull);
+                smask = stripe_mask(r0, r1, r2, bx0, by0);
             }
         }
         __syncthreads();
@@ -496,11 +495,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
 }
 }  // namespace
 
-// Kernel-variant selector for A/B timing (bench/ablation only; default = shipped variant).
-static int variant(const char* name, int dflt) {
-    const char* v = std::getenv(name);
-    return v ? std::atoi(v) : dflt;
-}
+// Waves per F6 tile: 2 for a full image (wave w owns stripes 2w, 2w + 1), 4 when the launch
+// has too few tiles to fill the chip (multi-GPU bands).  Measured at 1M/1080p with the
+// branchless stripe pair: 2 waves 0.258 ms, 1 wave 0.269 (with branches) / 0.343 (branchless,
+// 4 stripes), 4 waves 0.299.
+constexpr int kF6FullWaves = 2, kF6BandWaves = 4, kF6BandTiles = 4096;
 
 static BlendGeom make_geo(const gsr_camera& cam, const float bg[3], int ty0, int ty1) {
     BlendGeom g;
@@ -512,55 +511,60 @@ static BlendGeom make_geo(const gsr_camera& cam, const float bg[3], int ty0, int
     g.bg0 = bg[0];
     g.bg1 = bg[1];
     g.bg2 = bg[2];
-    g.ellipse_cull = variant("GSR_CULL_VARIANT", 1);
     return g;
 }
 
 int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
                          const uint2* ranges, const uint32_t* sorted_gid, const float4* rec,
-                         float* out_color, float* final_T, float* accum, float4* ck, hipStream_t s) {
+                         float* out_color, float* final_T, float* accum, uint32_t* term, float4* ck,
+                         hipStream_t s) {
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1);
     if (geo.nwg <= 0) return 0;
-    // waves per tile: 2 for a full image, 4 when the launch has too few tiles to fill the
-    // chip (multi-GPU bands)
-    const int v = variant("GSR_FWD_VARIANT", geo.nwg >= 4096 ? 2 : 4);
-    if (v == 1)
-        hipLaunchKernelGGL(blend_forward_kernel<1>, dim3(geo.nwg), dim3(64), 0, s, geo, ranges, sorted_gid, rec,
-                           out_color, final_T, accum, ck);
-    else if (v == 4)
-        hipLaunchKernelGGL(blend_forward_kernel<4>, dim3(geo.nwg), dim3(256), 0, s, geo, ranges, sorted_gid, rec,
-                           out_color, final_T, accum, ck);
-    else if (variant("GSR_F6_BRANCHLESS", 1))
-        hipLaunchKernelGGL((blend_forward_kernel<2, true>), dim3(geo.nwg), dim3(128), 0, s, geo, ranges, sorted_gid,
-                           rec, out_color, final_T, accum, ck);
+    if (geo.nwg >= kF6BandTiles)
+        hipLaunchKernelGGL(blend_forward_kernel<kF6FullWaves>, dim3(geo.nwg), dim3(64 * kF6FullWaves), 0, s, geo,
+                           ranges, sorted_gid, rec, out_color, final_T, accum, term, ck);
     else
-        hipLaunchKernelGGL(blend_forward_kernel<2>, dim3(geo.nwg), dim3(128), 0, s, geo, ranges, sorted_gid, rec,
-                           out_color, final_T, accum, ck);
+        hipLaunchKernelGGL(blend_forward_kernel<kF6BandWaves>, dim3(geo.nwg), dim3(64 * kF6BandWaves), 0, s, geo,
+                           ranges, sorted_gid, rec, out_color, final_T, accum, term, ck);
     return (int)hipGetLastError();
 }
 
 // Partials of records no pixel takes a gradient from -- including every record after a tile's
 // pixels have all terminated -- are never written by blend_backward_kernel: one streaming clear
-// (K x 36 B at the fill rate) before it replaces their scattered 36-B zero stores and the gid /
-// rect reads that located them (at 5M Gaussians most of a tile list lies past termination).
-// A launch of its own so that stage timing separates it from the kernel.
-int launch_clear_partial(float* partial, long long K, hipStream_t s) {
-    return (int)hipMemsetAsync(partial, 0, PartLayout(K).total, s);
+// of the K live entries (36 B each at the fill rate) before it replaces their scattered 36-B
+// zero stores and the gid / rect reads that located them (at 5M Gaussians most of a tile list
+// lies past termination).  K is read on the device (the binning may be sized by a bound).
+__global__ __launch_bounds__(256) void clear_partial_kernel(float4* __restrict__ p8, float* __restrict__ p1,
+                                                            long long cap, const uint32_t* __restrict__ K_dev) {
+    const long long K = (long long)*K_dev < cap ? (long long)*K_dev : cap;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < 2 * K; i += (long long)gridDim.x * 256) p8[i] = z;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < K; i += (long long)gridDim.x * 256) p1[i] = 0.f;
+}
+
+int launch_clear_partial(float* partial, long long cap, const uint32_t* K_dev, hipStream_t s) {
+    if (cap <= 0) return 0;
+    const PartLayout pl(cap);
+    char* base = reinterpret_cast<char*>(partial);
+    const long long blocks = (2 * cap + 255) / 256;
+    hipLaunchKernelGGL(clear_partial_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s,
+                       reinterpret_cast<float4*>(base + pl.p8), reinterpret_cast<float*>(base + pl.p1), cap, K_dev);
+    return (int)hipGetLastError();
 }
 
 int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
                           const uint2* ranges, const uint32_t* sorted_gid, const uint4* rect,
                           const float4* rec, const float* final_T,
-                          const float* accum, const float* dL_dpix, float* partial, long long K,
-                          const float4* ck, hipStream_t s) {
+                          const float* accum, const float* dL_dpix, float* partial, long long cap,
+                          const uint32_t* term, const float4* ck, hipStream_t s) {
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1);
     if (geo.nwg <= 0) return 0;
-    const PartLayout pl(K);
+    const PartLayout pl(cap);
     char* base = reinterpret_cast<char*>(partial);
-    const int blocks = ck ? 8 * (geo.nwg / 8 + 1) * kMaxChunks : geo.nwg;
+    const int blocks = 8 * (geo.nwg / 8 + 1) * kMaxChunks;
     hipLaunchKernelGGL(blend_backward_kernel, dim3(blocks), dim3(64), 0, s, geo, ranges, sorted_gid, rect, rec,
                        final_T, accum, dL_dpix, reinterpret_cast<float*>(base + pl.p8),
-                       reinterpret_cast<float*>(base + pl.p1), ck);
+                       reinterpret_cast<float*>(base + pl.p1), term, ck);
     return (int)hipGetLastError();
 }
 

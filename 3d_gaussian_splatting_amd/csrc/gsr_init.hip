@@ -235,8 +235,8 @@ int gsr_knn_mean_dist2(const float* points, int32_t N, float* dist2, void* scrat
     hipLaunchKernelGGL(knn_morton_kernel, dim3(nb), dim3(256), 0, s, points, N, bb, code);
     // 30-bit codes, identity values: 4 passes ping-pong (k0, v0) -> (code, v1)
     int which = -1;
-    if (int e = radix_sort(code, nullptr, k0, v0, code, v1, N, 30,
-                           reinterpret_cast<uint32_t*>(base + L.hist), &which, s, true))
+    if (int e = radix_sort(code, nullptr, k0, v0, code, v1, N, nullptr, 30,
+                           reinterpret_cast<uint32_t*>(base + L.hist), &which, s))
         return e;
     const uint32_t* order = which == 0 ? v0 : v1;
     const int nbox = (N + kBox - 1) / kBox;

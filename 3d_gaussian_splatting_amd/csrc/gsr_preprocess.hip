@@ -249,17 +249,15 @@ __device__ __forceinline__ void write_record(int g, float opac, const Geo& G, co
     if (out.flags) out.flags[g] = clamped;
 }
 
-// SH rows (M_rest x 3 floats per Gaussian, contiguous) reach the lanes in one of three ways:
-//  kShDirect : each lane reads its own row from HBM (no SH rows, or an A/B reference);
-//  kShLater  : no colour here (bands): record colours are filled by colour_kernel over the
-//              band's compacted candidates, which stages only their rows;
+// SH rows (M_rest x 3 floats per Gaussian, contiguous) reach the lanes in one of two ways:
+//  kShDirect : each lane reads its own row from HBM (used only when there are no SH rows);
 //  kShChunks : the block stages 5-coefficient column chunks (15 floats per row, 15 KB of LDS)
 //              and accumulates the colour chunk by chunk in the same k order (bit-identical
 //              to one pass), with 8 waves per SIMD.
-// Measured at 1M/SH3 (scripts/ablate.py GSR_PRE_VARIANT): direct 0.53 ms -- each lane's
-// 180-B row at a 180-B lane stride touches ~90 cache lines per load instruction; whole rows
-// staged in LDS (46 KB, 3 waves per SIMD) 0.106 ms; chunks 0.082 ms.
-enum { kShDirect = 0, kShLater = 1, kShChunks = 2 };
+// Measured at 1M/SH3: direct 0.53 ms -- each lane's 180-B row at a 180-B lane stride touches
+// ~90 cache lines per load instruction; whole rows staged in LDS (46 KB, 3 waves per SIMD)
+// 0.106 ms; chunks 0.082 ms.
+enum { kShDirect = 0, kShChunks = 2 };
 constexpr int kChunkK = 5;               // SH coefficients per staged chunk
 constexpr int kChunkF = 3 * kChunkK;     // floats per row per chunk
 
@@ -306,7 +304,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void p
     }
     const bool need = G.tiles != 0;  // colour and record only for Gaussians this band blends
     float rgb[3] = {0.f, 0.f, 0.f}, basis[16];
-    if (need && SH != kShLater) {
+    if (need) {
         rgb[0] = I.c0;
         rgb[1] = I.c1;
         rgb[2] = I.c2;
@@ -316,7 +314,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void p
             for (int ch = 0; ch < 3; ++ch) rgb[ch] = basis[0] * rgb[ch];
         }
     }
-    if (sh && SH != kShLater) {
+    if (sh) {
         if (SH == kShChunks) {
 #pragma unroll
             for (int c = 0; c < 3; ++c) {  // k = 1 + 5c .. 5 + 5c; SH degree <= 3 => k < 16
@@ -353,7 +351,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void p
     }
     if (need) {
         uint32_t clamped = 0;
-        if (!in.colors && SH != kShLater) {
+        if (!in.colors) {
 #pragma unroll
             for (int ch = 0; ch < 3; ++ch) {
                 const float r = rgb[ch] + 0.5f;
@@ -385,100 +383,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void p
     }
 }
 
-// Band colour pass (kShLater): SH -> RGB for the band's candidates only (gids in
-// `cand`, ascending), into the records F1 wrote with zero colour.  The candidates' rows are
-// scattered, so each 16-lane group gathers one 60-B row chunk per load -- still full 60-B
-// runs -- and the colour is summed chunk by chunk in the same k order as preprocess_kernel
-// (bit-identical to the full image's colour).
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void colour_kernel(
-    const gsr_camera cam, const GaussIn in, const uint32_t* __restrict__ cand, int n, float4* __restrict__ rec) {
-    extern __shared__ __attribute__((aligned(16))) float sh_lds[];
-    __shared__ uint32_t sg[256];
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    const int rows = n - blockIdx.x * 256 < 256 ? n - blockIdx.x * 256 : 256;
-    const int M3 = in.M_rest * 3, nb = (in.D + 1) * (in.D + 1);
-    const uint32_t g = threadIdx.x < rows ? cand[i] : 0u;
-    sg[threadIdx.x] = g;
-    Params I{};
-    if (threadIdx.x < rows) I = load_params(in, (int)g);
-    __syncthreads();
-    const int col = threadIdx.x & 15, r0 = threadIdx.x >> 4;
-    // byte offsets are unsigned 32-bit: rows beyond 4 GB of SH data are not addressable here
-    const unsigned long long bytes = (unsigned long long)in.P * M3 * sizeof(float);
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in.sh_rest), 0,
-                                                        (int)(uint32_t)(bytes < 0xFFFFFFFFull ? bytes : 0xFFFFFFFFull),
-                                                        0x00020000);
-    float pre[16];
-    auto load_chunk = [&](int c) {
-        const int f = kChunkF * c + col;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int r = r0 + 16 * j;
-            const uint32_t voff = r < rows && col < kChunkF && f < M3 ? (sg[r] * (uint32_t)M3 + f) * 4u : 0xFFFFFFFFu;
-            pre[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)voff, 0, 0));
-        }
-    };
-    load_chunk(0);
-    float rgb[3] = {I.c0, I.c1, I.c2}, basis[16];
-    sh_basis(cam, in, I, basis);
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) rgb[ch] = basis[0] * rgb[ch];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {  // k = 1 + 5c .. 5 + 5c; SH degree <= 3 => k < 16
-        const int k0 = 1 + kChunkK * c;
-        if (k0 >= nb) break;  // grid-uniform
-        if (c > 0) __syncthreads();
-        if (col < kChunkF)
-#pragma unroll
-            for (int j = 0; j < 16; ++j) sh_lds[(r0 + 16 * j) * kChunkF + col] = pre[j];
-        if (c < 2 && k0 + kChunkK < nb) load_chunk(c + 1);
-        __syncthreads();
-        const float* rest = sh_lds + threadIdx.x * kChunkF;
-#pragma unroll
-        for (int kk = 0; kk < kChunkK; ++kk) {
-            const int k = k0 + kk;
-            if (k < nb)
-#pragma unroll
-                for (int ch = 0; ch < 3; ++ch) rgb[ch] = rgb[ch] + basis[k] * rest[3 * kk + ch];
-        }
-    }
-    if (threadIdx.x >= rows) return;
-    float* r = reinterpret_cast<float*>(rec + 3 * (size_t)g);
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) r[6 + ch] = fmaxf(rgb[ch] + 0.5f, 0.0f);  // rec[1].zw, rec[2].x
-}
-
 }  // namespace
 
 int launch_preprocess(const gsr_camera& cam, const GaussIn& in, int ty0, int ty1, const PreOut& out,
                       hipStream_t s) {
     if (in.P <= 0) return 0;
     const int gx = div_up(cam.width, kTile), gy = div_up(cam.height, kTile);
-    const bool band = ty0 > 0 || ty1 < gy;  // a band reads SH rows directly
     const bool sh = in.sh_rest && !in.colors && in.D > 0;
-    const char* v = std::getenv("GSR_PRE_VARIANT");
-    const int mode = !sh ? kShDirect : band ? kShLater : v ? std::atoi(v) : kShChunks;
     const dim3 grid(div_up(in.P, 256)), block(256);
-    if (mode == kShLater)
-        hipLaunchKernelGGL(preprocess_kernel<kShLater>, grid, block, 0, s, cam, in, gx, gy, ty0, ty1, out);
-    else if (mode == kShChunks)
+    if (sh)
         hipLaunchKernelGGL(preprocess_kernel<kShChunks>, grid, block, sizeof(float) * 256 * kChunkF, s, cam, in, gx,
                            gy, ty0, ty1, out);
     else
         hipLaunchKernelGGL(preprocess_kernel<kShDirect>, grid, block, 0, s, cam, in, gx, gy, ty0, ty1, out);
-    return (int)hipGetLastError();
-}
-
-bool colour_pass_needed(const gsr_camera& cam, const GaussIn& in, int ty0, int ty1) {
-    const int gy = div_up(cam.height, kTile);
-    return in.sh_rest && !in.colors && in.D > 0 && (ty0 > 0 || ty1 < gy);
-}
-
-int launch_colour(const gsr_camera& cam, const GaussIn& in, const uint32_t* cand, int n, float4* rec,
-                  hipStream_t s) {
-    if (n <= 0) return 0;
-    hipLaunchKernelGGL(colour_kernel, dim3(div_up(n, 256)), dim3(256), sizeof(float) * 256 * kChunkF, s, cam, in,
-                       cand, n, rec);
     return (int)hipGetLastError();
 }
 

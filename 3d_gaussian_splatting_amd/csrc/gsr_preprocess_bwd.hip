@@ -28,7 +28,7 @@ constexpr float kC0 = 0.28209479177387814f;
 constexpr float kC1 = 0.4886025119029199f;
 
 // Per-Gaussian sum of its per-(tile, instance) partials in emission order.  A block owns 256
-// consecutive depth ranks; their segments [offsets[r-1], offsets[r]) tile one contiguous
+// consecutive Gaussians; their segments [offsets[g-1], offsets[g]) tile one contiguous
 // stretch of the partial arrays, which the block streams through LDS in coalesced windows of
 // kGatherWin entries.  Each thread then adds the part of its own segment that lies in the
 // window, in order, from LDS.  The partials are B1's raw tile moments (Sx, Sy, Sxx, Sxy, Syy,
@@ -37,31 +37,23 @@ constexpr float kC1 = 0.4886025119029199f;
 // record.  The 48-B result lands at grad2d[gid].
 constexpr int kGatherWin = 512;
 
-// A Gaussian's 2D gradient as it sits in a grad2d row: mean2D x/y, conic A/B/C, opacity,
-// colour r/g/b, then 3 unused floats.
-struct G2 {
-    float4 a, b, c;
-};
-
-// One block's gather: thread r of the block (rank r0 + r) sums its Gaussian's partials and
-// converts them to its 2D gradient `res` (12 floats: mean2D x/y, conic A/B/C, opacity, colour
-// r/g/b, 0 x 3) for Gaussian *g_out.  gid_by_rank == nullptr: the ranks are the gids.
-// w8 / w1: the block's LDS windows (2 kGatherWin float4 + kGatherWin floats).  Every thread of
-// the block must call it (it synchronises).
-__device__ __forceinline__ void gather_block(const uint32_t* __restrict__ gid_by_rank,
-                                             const uint32_t* __restrict__ offsets, const float4* __restrict__ p8,
-                                             const float* __restrict__ p1, const float4* __restrict__ rec, float hw,
-                                             float hh, int P, float4* w8, float* w1, G2& res,
-                                             uint32_t& g_out) {
-    const int r0 = blockIdx.x * 256, r = r0 + threadIdx.x;
-    const int rl = (P - r0 < 256 ? P - r0 : 256) + r0;  // one past the block's last rank
-    const uint32_t J0 = r0 ? offsets[r0 - 1] : 0u, J1 = offsets[rl - 1];
-    const uint32_t s = r < P ? (r ? offsets[r - 1] : 0u) : 0u;
-    const uint32_t e = r < P ? offsets[r] : 0u;
+__global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __restrict__ offsets,
+                                                            const float4* __restrict__ p8,
+                                                            const float* __restrict__ p1,
+                                                            const float4* __restrict__ rec, float hw, float hh,
+                                                            int P, uint32_t cap, float* __restrict__ grad2d) {
+    __shared__ float4 w8[2 * kGatherWin];
+    __shared__ float w1[kGatherWin];
+    const int g0 = blockIdx.x * 256, g = g0 + threadIdx.x;
+    const int gl = (P - g0 < 256 ? P - g0 : 256) + g0;  // one past the block's last Gaussian
+    // emission indices past the binning's capacity were never emitted (overflow): clamped
+    auto off = [&](int i) { const uint32_t o = offsets[i]; return o < cap ? o : cap; };
+    const uint32_t J0 = g0 ? off(g0 - 1) : 0u, J1 = off(gl - 1);
+    const uint32_t s = g < P ? (g ? off(g - 1) : 0u) : 0u;
+    const uint32_t e = g < P ? off(g) : 0u;
     // the Gaussian's conic and opacity, loaded before the window loop (latency overlaps it)
-    const uint32_t g = r < P ? (gid_by_rank ? gid_by_rank[r] : (uint32_t)r) : 0u;
     float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0;
-    if (r < P) {
+    if (g < P && e > s) {
         q0 = rec[3 * (size_t)g];
         q1 = rec[3 * (size_t)g + 1];
     }
@@ -82,31 +74,14 @@ __device__ __forceinline__ void gather_block(const uint32_t* __restrict__ gid_by
         }
         __syncthreads();
     }
+    if (g >= P) return;
     // moments -> d mean2D (NDC), d conic, d opacity (sum G dL/dalpha = S0 / o), d colour
     const float A = -2.0f * kLn2 * q0.z, B = -kLn2 * q0.w, C = -2.0f * kLn2 * q1.x;
     const float Sx = a[0], Sy = a[1], S0 = a[5];
-    res.a = make_float4((-A * Sx - B * Sy) * hw, (-C * Sy - B * Sx) * hh, -0.5f * a[2], -a[3]);
-    res.b = make_float4(-0.5f * a[4], S0 != 0.0f ? S0 / q1.y : 0.0f, a[6], a[7]);
-    res.c = make_float4(a[8], 0.f, 0.f, 0.f);
-    g_out = g;
-}
-
-__global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __restrict__ gid_by_rank,
-                                                            const uint32_t* __restrict__ offsets,
-                                                            const float4* __restrict__ p8,
-                                                            const float* __restrict__ p1,
-                                                            const float4* __restrict__ rec, float hw, float hh,
-                                                            int P, float* __restrict__ grad2d) {
-    __shared__ float4 w8[2 * kGatherWin];
-    __shared__ float w1[kGatherWin];
-    G2 res;
-    uint32_t g;
-    gather_block(gid_by_rank, offsets, p8, p1, rec, hw, hh, P, w8, w1, res, g);
-    if (blockIdx.x * 256 + threadIdx.x >= P) return;
     float4* dst = reinterpret_cast<float4*>(grad2d + (size_t)kPart * g);
-    dst[0] = res.a;
-    dst[1] = res.b;
-    dst[2] = res.c;
+    dst[0] = make_float4((-A * Sx - B * Sy) * hw, (-C * Sy - B * Sx) * hh, -0.5f * a[2], -a[3]);
+    dst[1] = make_float4(-0.5f * a[4], S0 != 0.0f ? S0 / q1.y : 0.0f, a[6], a[7]);
+    dst[2] = make_float4(a[8], 0.f, 0.f, 0.f);
 }
 
 // Per-Gaussian inputs of B2, loaded before the SH rows are staged so that their HBM
@@ -120,11 +95,12 @@ struct BwdIn {
     uint32_t cl;  // stored SH clamp bits (flags != nullptr)
 };
 
-__device__ __forceinline__ BwdIn load_bwd_in_g2(const GaussIn& in, int g, const uint32_t* __restrict__ depth_key,
-                                                const uint32_t* __restrict__ flags, const G2 v) {
+__device__ __forceinline__ BwdIn load_bwd_in(const GaussIn& in, int g, int o, const uint32_t* __restrict__ depth_key,
+                                             const uint32_t* __restrict__ flags, const float* __restrict__ grad2d) {
     BwdIn b;
     b.visible = depth_key[g] != 0xFFFFFFFFu;
-    const float4 v0 = v.a, v1 = v.b, v2 = v.c;
+    const float4* src = reinterpret_cast<const float4*>(grad2d + (size_t)kPart * o);
+    const float4 v0 = src[0], v1 = src[1], v2 = src[2];
     b.g2[0] = v0.x; b.g2[1] = v0.y; b.g2[2] = v0.z; b.g2[3] = v0.w;
     b.g2[4] = v1.x; b.g2[5] = v1.y; b.g2[6] = v1.z; b.g2[7] = v1.w;
     b.g2[8] = v2.x;
@@ -144,12 +120,6 @@ __device__ __forceinline__ BwdIn load_bwd_in_g2(const GaussIn& in, int g, const 
     }
     b.cl = flags ? flags[g] : 0u;
     return b;
-}
-
-__device__ __forceinline__ BwdIn load_bwd_in(const GaussIn& in, int g, int o, const uint32_t* __restrict__ depth_key,
-                                             const uint32_t* __restrict__ flags, const float* __restrict__ grad2d) {
-    const float4* src = reinterpret_cast<const float4*>(grad2d + (size_t)kPart * o);
-    return load_bwd_in_g2(in, g, depth_key, flags, G2{src[0], src[1], src[2]});
 }
 
 // One Gaussian's chain rule.  `lrest`: this thread's SH-rest row staged in LDS (read, then
@@ -463,66 +433,16 @@ __global__ __launch_bounds__(256) void preprocess_backward_kernel(
     }
 }
 
-// Full image, gid-order ranking (the shipped binning): the gather and B2 share their block of
-// 256 Gaussians, so one kernel does both -- the 2D gradient stays in registers instead of a
-// 48-B-per-Gaussian round trip through HBM, and one launch goes.  The gather's LDS windows and
-// the SH-row staging reuse the same dynamic LDS.  Arithmetic and order are those of the two
-// kernels (bit-identical results).
-__global__ __launch_bounds__(256) void gather_backward_kernel(const gsr_camera cam, const GaussIn in, int n,
-                                                              const uint32_t* __restrict__ depth_key,
-                                                              const uint32_t* __restrict__ flags,
-                                                              const uint32_t* __restrict__ offsets,
-                                                              const float4* __restrict__ p8, const float* __restrict__ p1,
-                                                              const float4* __restrict__ rec, float hw, float hh,
-                                                              GradOut out) {
-    extern __shared__ __attribute__((aligned(16))) float sh_lds[];
-    G2 res;
-    uint32_t g;
-    gather_block(nullptr, offsets, p8, p1, rec, hw, hh, n, reinterpret_cast<float4*>(sh_lds),
-                 sh_lds + 8 * kGatherWin, res, g);  // ends with a block barrier: the LDS is free again
-    const int o = blockIdx.x * 256 + threadIdx.x;
-    const int M3 = in.M_rest * 3;
-    const bool stage = in.sh_rest != nullptr && !in.colors;  // block-uniform
-    const int rows = n - blockIdx.x * 256 < 256 ? n - blockIdx.x * 256 : 256;
-    const size_t base = (size_t)blockIdx.x * 256 * M3;
-    BwdIn bi{};
-    if (o < n) bi = load_bwd_in_g2(in, o, depth_key, flags, res);
-    if (stage) {
-        for (int i = threadIdx.x; i < rows * M3; i += 256) sh_lds[i] = in.sh_rest[base + i];
-        __syncthreads();
-    }
-    if (o < n) preprocess_backward_one(cam, in, o, o, bi, flags, out, stage ? sh_lds + threadIdx.x * M3 : nullptr);
-    if (stage) {
-        __syncthreads();
-        for (int i = threadIdx.x; i < rows * M3; i += 256) out.sh_rest[base + i] = sh_lds[i];
-    }
-}
-
 }  // namespace
 
-int launch_gather_backward(const gsr_camera& cam, const GaussIn& in, const uint32_t* depth_key, const uint32_t* flags,
-                           const uint32_t* offsets, const float* partial, const float4* rec, long long K,
-                           const GradOut& out, hipStream_t s) {
-    if (in.P <= 0) return 0;
-    const PartLayout pl(K);
-    const char* base = reinterpret_cast<const char*>(partial);
-    const size_t sh = (in.sh_rest && !in.colors) ? sizeof(float) * 256 * 3 * in.M_rest : 0;
-    const size_t win = (2 * sizeof(float4) + sizeof(float)) * kGatherWin;
-    hipLaunchKernelGGL(gather_backward_kernel, dim3(div_up(in.P, 256)), dim3(256), sh > win ? sh : win, s, cam, in,
-                       in.P, depth_key, flags, offsets, reinterpret_cast<const float4*>(base + pl.p8),
-                       reinterpret_cast<const float*>(base + pl.p1), rec, 0.5f * (float)cam.width,
-                       0.5f * (float)cam.height, out);
-    return (int)hipGetLastError();
-}
-
-int launch_gather_grad2d(const uint32_t* gid_by_rank, const uint32_t* offsets, const float* partial,
-                         const float4* rec, int W, int H, long long K, int P, float* grad2d, hipStream_t s) {
+int launch_gather_grad2d(const uint32_t* offsets, const float* partial, const float4* rec, int W, int H,
+                         long long cap, int P, float* grad2d, hipStream_t s) {
     if (P <= 0) return 0;
-    const PartLayout pl(K);
+    const PartLayout pl(cap);
     const char* base = reinterpret_cast<const char*>(partial);
-    hipLaunchKernelGGL(gather_grad2d_kernel, dim3(div_up(P, 256)), dim3(256), 0, s, gid_by_rank, offsets,
+    hipLaunchKernelGGL(gather_grad2d_kernel, dim3(div_up(P, 256)), dim3(256), 0, s, offsets,
                        reinterpret_cast<const float4*>(base + pl.p8), reinterpret_cast<const float*>(base + pl.p1),
-                       rec, 0.5f * (float)W, 0.5f * (float)H, P, grad2d);
+                       rec, 0.5f * (float)W, 0.5f * (float)H, P, (uint32_t)cap, grad2d);
     return (int)hipGetLastError();
 }
 

@@ -1,0 +1,298 @@
+// gsr_shard.hip -- the multi-GPU split of the path (the scaling version): pack the
+// projected Gaussians ("splats") of a Gaussian shard into per-band send blocks, unpack the
+// blocks a band owner receives into its local geometry arrays, and sum the 2D gradients the
+// bands send back, per Gaussian in band order.
+//
+// Splat (64 B, GSR_SPLAT_BYTES): the F1 blend record (3 float4) and {depth key, rect lo,
+// rect hi, 0}.  A band owner needs nothing else: its binning (F2..F5), blend (F6) and blend
+// backward (B1 + gather) read only these.  Splats of one (source, band) pair are packed in
+// shard order by an order-preserving compaction (wave64 ballot prefix per band), and sources
+// are laid out in rank order, so a band's local index order is ascending global Gaussian id:
+// the canonical (tile, depth, gid) order -- and every pixel -- equal the single-GPU forward's.
+//
+// All integer / copy work: HBM-bound, no MFMA.
+#include "gsr_kernels.h"
+
+namespace gsr {
+namespace {
+
+constexpr int kB = kSortBlock;   // 256 threads
+constexpr int kI = kSortItems;   // 16 rounds of 64 per wave: 4096 Gaussians per block
+constexpr int kWaves = kB / 64;
+
+__device__ inline uint64_t lanemask_lt() {
+    const int lane = threadIdx.x & 63;
+    return (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+}
+
+// the bands [b_lo, b_hi] a rect's tile rows [miny, maxy) overlap (b_lo > b_hi: none)
+__device__ __forceinline__ void band_span(const BandRows& br, uint32_t miny, uint32_t maxy, int& b_lo, int& b_hi) {
+    b_lo = br.n;
+    b_hi = -1;
+    for (int b = 0; b < br.n; ++b) {
+        if ((int)miny < br.row[b + 1] && (int)maxy > br.row[b]) {
+            b_lo = b < b_lo ? b : b_lo;
+            b_hi = b;
+        }
+    }
+}
+
+// Per block: splats per band (partials[b * nblk + blk]); optionally the per-tile-row instance
+// histogram (LDS, then one global add per row).
+__global__ __launch_bounds__(kB) void pack_count_kernel(const uint32_t* __restrict__ tiles,
+                                                        const uint4* __restrict__ rect, int P, BandRows br,
+                                                        uint32_t* __restrict__ partials, int nblk,
+                                                        uint32_t* __restrict__ row_hist, int grid_y) {
+    __shared__ uint32_t cnt[kWaves][kMaxBands];
+    __shared__ uint32_t hist[kMaxHistRows];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const bool do_hist = row_hist != nullptr;
+    if (do_hist)
+        for (int y = threadIdx.x; y < grid_y; y += kB) hist[y] = 0u;
+    __syncthreads();
+    uint32_t c[kMaxBands];
+#pragma unroll
+    for (int b = 0; b < kMaxBands; ++b) c[b] = 0u;
+    const int base = blockIdx.x * kSortTile + w * (kI * 64);
+    for (int r = 0; r < kI; ++r) {
+        const int g = base + r * 64 + lane;
+        int b_lo = kMaxBands, b_hi = -1;
+        if (g < P && tiles[g] != 0u) {
+            const uint4 rr = rect[g];
+            const uint32_t miny = rr.x >> 16, maxy = rr.y >> 16;
+            band_span(br, miny, maxy, b_lo, b_hi);
+            if (do_hist) {
+                const uint32_t wd = (rr.y & 0xFFFF) - (rr.x & 0xFFFF);
+                for (uint32_t y = miny; y < maxy; ++y) atomicAdd(&hist[y], wd);
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < kMaxBands; ++b)
+            if (b < br.n) c[b] += (uint32_t)__popcll(__ballot(b >= b_lo && b <= b_hi));
+    }
+    if (lane == 0)
+        for (int b = 0; b < br.n; ++b) cnt[w][b] = c[b];
+    __syncthreads();
+    if (threadIdx.x < br.n) {
+        uint32_t t = 0;
+        for (int k = 0; k < kWaves; ++k) t += cnt[k][threadIdx.x];
+        partials[threadIdx.x * nblk + blockIdx.x] = t;
+    }
+    if (do_hist)
+        for (int y = threadIdx.x; y < grid_y; y += kB)
+            if (hist[y]) atomicAdd(row_hist + y, hist[y]);
+}
+
+// Block b: exclusive scan of band b's per-block counts in place; the band's total into its send
+// block's header (the true count, which may exceed pair_cap).
+__global__ __launch_bounds__(1024) void pack_scan_kernel(uint32_t* __restrict__ partials, int nblk,
+                                                         char* __restrict__ send, size_t block_bytes) {
+    __shared__ uint32_t wsum[16];
+    uint32_t* col = partials + (size_t)blockIdx.x * nblk;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    uint32_t carry = 0;
+    for (int base = 0; base < nblk; base += 1024) {
+        const int i = base + tid;
+        const uint32_t v = i < nblk ? col[i] : 0u;
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        uint32_t pre = 0, tot = 0;
+        for (int k = 0; k < 16; ++k) {
+            pre += k < w ? wsum[k] : 0u;
+            tot += wsum[k];
+        }
+        if (i < nblk) col[i] = carry + pre + x - v;
+        carry += tot;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        uint32_t* hdr = reinterpret_cast<uint32_t*>(send + (size_t)blockIdx.x * block_bytes);
+        hdr[0] = carry;
+        hdr[1] = 0u;
+        hdr[2] = 0u;
+        hdr[3] = 0u;
+    }
+}
+
+// Scatter: every splat of band b goes to slot partials[b][blk] + (earlier waves' and lanes'
+// splats of the band), in shard order; slot_of[b * P + g] remembers it for the gradient sum.
+__global__ __launch_bounds__(kB) void pack_scatter_kernel(const uint32_t* __restrict__ tiles,
+                                                          const uint4* __restrict__ rect,
+                                                          const uint32_t* __restrict__ depth_key,
+                                                          const float4* __restrict__ rec, int P, BandRows br,
+                                                          const uint32_t* __restrict__ partials, int nblk,
+                                                          char* __restrict__ send, size_t block_bytes, int pair_cap,
+                                                          uint32_t* __restrict__ slot_of) {
+    __shared__ uint32_t cnt[kWaves][kMaxBands];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int base = blockIdx.x * kSortTile + w * (kI * 64);
+    // pass 1: this wave's count per band (for the wave offsets)
+    uint32_t c[kMaxBands];
+#pragma unroll
+    for (int b = 0; b < kMaxBands; ++b) c[b] = 0u;
+    for (int r = 0; r < kI; ++r) {
+        const int g = base + r * 64 + lane;
+        int b_lo = kMaxBands, b_hi = -1;
+        if (g < P && tiles[g] != 0u) {
+            const uint4 rr = rect[g];
+            band_span(br, rr.x >> 16, rr.y >> 16, b_lo, b_hi);
+        }
+#pragma unroll
+        for (int b = 0; b < kMaxBands; ++b)
+            if (b < br.n) c[b] += (uint32_t)__popcll(__ballot(b >= b_lo && b <= b_hi));
+    }
+    if (lane == 0)
+        for (int b = 0; b < br.n; ++b) cnt[w][b] = c[b];
+    __syncthreads();
+    uint32_t pos[kMaxBands];
+#pragma unroll
+    for (int b = 0; b < kMaxBands; ++b) {
+        pos[b] = 0u;
+        if (b < br.n) {
+            pos[b] = partials[b * nblk + blockIdx.x];
+            for (int k = 0; k < w; ++k) pos[b] += cnt[k][b];
+        }
+    }
+    const uint64_t lt = lanemask_lt();
+    for (int r = 0; r < kI; ++r) {
+        const int g = base + r * 64 + lane;
+        int b_lo = kMaxBands, b_hi = -1;
+        uint4 rr = make_uint4(0u, 0u, 0u, 0u);
+        if (g < P && tiles[g] != 0u) {
+            rr = rect[g];
+            band_span(br, rr.x >> 16, rr.y >> 16, b_lo, b_hi);
+        }
+        float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
+        uint32_t dk = 0u;
+        if (b_lo <= b_hi) {
+            r0 = rec[3 * (size_t)g];
+            r1 = rec[3 * (size_t)g + 1];
+            r2 = rec[3 * (size_t)g + 2];
+            dk = depth_key[g];
+        }
+#pragma unroll
+        for (int b = 0; b < kMaxBands; ++b) {
+            if (b >= br.n) continue;  // grid-uniform
+            const bool in = b >= b_lo && b <= b_hi;
+            const uint64_t m = __ballot(in);
+            if (in) {
+                const uint32_t slot = pos[b] + (uint32_t)__popcll(m & lt);
+                slot_of[(size_t)b * P + g] = slot;
+                if (slot < (uint32_t)pair_cap) {
+                    float4* dst = reinterpret_cast<float4*>(send + (size_t)b * block_bytes + kSplatBytes +
+                                                            (size_t)slot * kSplatBytes);
+                    dst[0] = r0;
+                    dst[1] = r1;
+                    dst[2] = r2;
+                    dst[3] = make_float4(__uint_as_float(dk), __uint_as_float(rr.x), __uint_as_float(rr.y), 0.f);
+                }
+            }
+            pos[b] += (uint32_t)__popcll(m);
+        }
+    }
+}
+
+// Band owner: local index i = src * pair_cap + slot.  Live slots get their record, depth key,
+// rect and the tile count of the rect clipped to the band's rows; empty slots get no tiles.
+__global__ __launch_bounds__(256) void unpack_kernel(const char* __restrict__ recv, size_t block_bytes, int nsrc,
+                                                     int pair_cap, int ty0, int ty1, float4* __restrict__ rec,
+                                                     uint32_t* __restrict__ depth_key, uint32_t* __restrict__ tiles,
+                                                     uint4* __restrict__ rect) {
+    const long long n = (long long)nsrc * pair_cap;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+        const int src = (int)(i / pair_cap), slot = (int)(i - (long long)src * pair_cap);
+        const char* blk = recv + (size_t)src * block_bytes;
+        const uint32_t count = *reinterpret_cast<const uint32_t*>(blk);
+        if ((uint32_t)slot < count) {
+            const float4* sp = reinterpret_cast<const float4*>(blk + kSplatBytes + (size_t)slot * kSplatBytes);
+            const float4 a = sp[3];
+            rec[3 * i] = sp[0];
+            rec[3 * i + 1] = sp[1];
+            rec[3 * i + 2] = sp[2];
+            const uint32_t lo = __float_as_uint(a.y), hi = __float_as_uint(a.z);
+            depth_key[i] = __float_as_uint(a.x);
+            rect[i] = make_uint4(lo, hi, 0u, 0u);
+            const int miny = (int)(lo >> 16), maxy = (int)(hi >> 16);
+            const int y0 = miny > ty0 ? miny : ty0, y1 = maxy < ty1 ? maxy : ty1;
+            tiles[i] = y1 > y0 ? ((hi & 0xFFFF) - (lo & 0xFFFF)) * (uint32_t)(y1 - y0) : 0u;
+        } else {
+            depth_key[i] = 0xFFFFFFFFu;
+            tiles[i] = 0u;
+        }
+    }
+}
+
+// Source: grad2d[g] = sum over the bands g was sent to, in band order, of the 2D gradient the
+// band sent back for g's slot (fixed order: deterministic).
+__global__ __launch_bounds__(256) void grad_sum_kernel(const uint32_t* __restrict__ tiles,
+                                                       const uint4* __restrict__ rect, int P, BandRows br,
+                                                       const uint32_t* __restrict__ slot_of,
+                                                       const float4* __restrict__ back, int pair_cap,
+                                                       float4* __restrict__ grad2d) {
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= P) return;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b4 = a, c4 = a;
+    if (tiles[g] != 0u) {
+        const uint4 rr = rect[g];
+        int b_lo, b_hi;
+        band_span(br, rr.x >> 16, rr.y >> 16, b_lo, b_hi);
+        for (int b = b_lo; b <= b_hi; ++b) {
+            const uint32_t slot = slot_of[(size_t)b * P + g];
+            if (slot >= (uint32_t)pair_cap) continue;  // overflowed: never sent
+            const float4* src = back + ((size_t)b * pair_cap + slot) * 3;
+            const float4 u = src[0], v = src[1], w = src[2];
+            a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+            b4.x += v.x; b4.y += v.y; b4.z += v.z; b4.w += v.w;
+            c4.x += w.x;
+        }
+    }
+    grad2d[3 * (size_t)g] = a;
+    grad2d[3 * (size_t)g + 1] = b4;
+    grad2d[3 * (size_t)g + 2] = c4;
+}
+
+}  // namespace
+
+int launch_pack_splats(const uint32_t* tiles, const uint4* rect, const uint32_t* depth_key, const float4* rec, int P,
+                       const BandRows& br, uint32_t* partials, char* send, int pair_cap, uint32_t* slot_of,
+                       uint32_t* row_hist, int grid_y, hipStream_t s) {
+    const size_t bb = exchange_block_bytes(pair_cap);
+    if (P <= 0) {  // empty shard: zero headers
+        for (int b = 0; b < br.n; ++b)
+            if (hipError_t e = hipMemsetAsync(send + (size_t)b * bb, 0, kSplatBytes, s)) return (int)e;
+        return 0;
+    }
+    const int nblk = sort_blocks(P);
+    hipLaunchKernelGGL(pack_count_kernel, dim3(nblk), dim3(kB), 0, s, tiles, rect, P, br, partials, nblk, row_hist,
+                       grid_y);
+    hipLaunchKernelGGL(pack_scan_kernel, dim3(br.n), dim3(1024), 0, s, partials, nblk, send, bb);
+    hipLaunchKernelGGL(pack_scatter_kernel, dim3(nblk), dim3(kB), 0, s, tiles, rect, depth_key, rec, P, br, partials,
+                       nblk, send, bb, pair_cap, slot_of);
+    return (int)hipGetLastError();
+}
+
+int launch_unpack_splats(const char* recv, int nsrc, int pair_cap, int ty0, int ty1, float4* rec, uint32_t* depth_key,
+                         uint32_t* tiles, uint4* rect, hipStream_t s) {
+    const long long n = (long long)nsrc * pair_cap;
+    if (n <= 0) return 0;
+    const long long blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0, s, recv,
+                       exchange_block_bytes(pair_cap), nsrc, pair_cap, ty0, ty1, rec, depth_key, tiles, rect);
+    return (int)hipGetLastError();
+}
+
+int launch_grad_sum(const uint32_t* tiles, const uint4* rect, int P, const BandRows& br, const uint32_t* slot_of,
+                    const float* back, int pair_cap, float* grad2d, hipStream_t s) {
+    if (P <= 0) return 0;
+    hipLaunchKernelGGL(grad_sum_kernel, dim3(div_up(P, 256)), dim3(256), 0, s, tiles, rect, P, br, slot_of,
+                       reinterpret_cast<const float4*>(back), pair_cap, reinterpret_cast<float4*>(grad2d));
+    return (int)hipGetLastError();
+}
+
+}  // namespace gsr

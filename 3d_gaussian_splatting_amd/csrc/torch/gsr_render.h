@@ -17,6 +17,7 @@
 #include <torch/torch.h>
 
 #include <array>
+#include <cmath>
 #include <optional>
 
 #include "gsr/gsr.h"
@@ -46,8 +47,9 @@ struct RasterSettings {
     std::array<float, 3> bg{0.f, 0.f, 0.f};
     float scale_modifier = 1.f;
     int sh_degree = 0;
-    int tile_y0 = 0, tile_y1 = INT32_MAX;  // tile-row band (multi-GPU sharding)
+    int tile_y0 = 0, tile_y1 = INT32_MAX;  // tile-row band
     bool debug = false;
+    int max_rendered = 0;  // > 0: binning sized for this many instances, no host read (gsr.h)
 };
 
 struct RenderOutput {
@@ -83,8 +85,12 @@ RenderOutput render(const RasterCamera& cam, Model& pc, const Pipe& pipe, const 
     rs.sh_degree = core.active_sh_degree_;
     rs.debug = pipe.debug_;
     torch::Tensor scales, rotations, cov3D, sh_dc, sh_rest, colors;
-    if (pipe.compute_cov3D_python_) {
-        cov3D = pc.get_covariance(scaling_modifier);
+    // The reference's GaussianModel::get_covariance takes an int modifier
+    // (gaussian_model.h:89), so it is called only with an integral one; any other modifier is
+    // applied in-kernel to get_scaling() (F1 builds the same R S S^T R^T covariance,
+    // general_utils.cpp:88-99) instead of being truncated to an int.
+    if (pipe.compute_cov3D_python_ && scaling_modifier == std::nearbyint(scaling_modifier)) {
+        cov3D = pc.get_covariance(static_cast<int>(scaling_modifier));
     } else {
         scales = pc.get_scaling();
         rotations = pc.get_rotation();

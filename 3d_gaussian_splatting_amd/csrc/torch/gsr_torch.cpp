@@ -89,6 +89,7 @@ gsr_raster_settings make_settings(const RasterSettings& rs) {
     s.tile_y0 = rs.tile_y0;
     s.tile_y1 = rs.tile_y1;
     s.flags = rs.debug ? GSR_FLAG_DEBUG : 0u;
+    s.max_rendered = rs.max_rendered;
     return s;
 }
 
@@ -96,8 +97,7 @@ void* cur_stream() { return (void*)c10::hip::getCurrentHIPStream().stream(); }
 
 struct FwdResult {
     torch::Tensor color, radii, geom, binning, image;
-    int32_t K;
-    int32_t NR;  // num_ranked
+    gsr_buffers bufs;
 };
 
 FwdResult forward_impl(const RasterCamera& cam, const RasterSettings& rs, const torch::Tensor& means3D,
@@ -127,19 +127,19 @@ FwdResult forward_impl(const RasterCamera& cam, const RasterSettings& rs, const 
     r.geom = geom.keep.at(0);
     r.binning = bin.keep.empty() ? torch::Tensor() : bin.keep.at(0);
     r.image = img.keep.at(0);
-    r.K = b.num_rendered;
-    r.NR = b.num_ranked;
+    r.bufs = b;
     return r;
 }
 
 gsr_buffers buffers_of(const torch::Tensor& geom, const torch::Tensor& binning, const torch::Tensor& image,
-                       int32_t K, int32_t NR) {
+                       int32_t K, int32_t cap, int32_t n_local) {
     gsr_buffers b{};
     b.geom = geom.data_ptr();
     b.binning = binning.defined() ? binning.data_ptr() : nullptr;
     b.image = image.data_ptr();
     b.num_rendered = K;
-    b.num_ranked = NR;
+    b.capacity = cap;
+    b.n_local = n_local;
     return b;
 }
 
@@ -156,8 +156,9 @@ class RasterizeGaussians : public torch::autograd::Function<RasterizeGaussians> 
         auto r = forward_impl(cam, rs, means3D, sh_dc, sh_rest, colors, opac, scales, rots, cov3D);
         ctx->save_for_backward({means3D, sh_dc, sh_rest, colors, opac, scales, rots, cov3D, r.geom, r.binning,
                                 r.image});
-        ctx->saved_data["K"] = (int64_t)r.K;
-        ctx->saved_data["NR"] = (int64_t)r.NR;
+        ctx->saved_data["K"] = (int64_t)r.bufs.num_rendered;
+        ctx->saved_data["cap"] = (int64_t)r.bufs.capacity;
+        ctx->saved_data["n_local"] = (int64_t)r.bufs.n_local;
         ctx->saved_data["cam_w"] = (int64_t)cam.width;
         ctx->saved_data["cam_h"] = (int64_t)cam.height;
         ctx->saved_data["cam_tx"] = (double)cam.tanfovx;
@@ -171,6 +172,7 @@ class RasterizeGaussians : public torch::autograd::Function<RasterizeGaussians> 
         ctx->saved_data["ty0"] = (int64_t)rs.tile_y0;
         ctx->saved_data["ty1"] = (int64_t)rs.tile_y1;
         ctx->saved_data["debug"] = rs.debug;
+        ctx->saved_data["max_rendered"] = (int64_t)rs.max_rendered;
         ctx->mark_non_differentiable({r.radii});
         return {r.color, r.radii};
     }
@@ -197,8 +199,10 @@ class RasterizeGaussians : public torch::autograd::Function<RasterizeGaussians> 
         rs.tile_y0 = (int)ctx->saved_data["ty0"].toInt();
         rs.tile_y1 = (int)ctx->saved_data["ty1"].toInt();
         rs.debug = ctx->saved_data["debug"].toBool();
+        rs.max_rendered = (int)ctx->saved_data["max_rendered"].toInt();
         const int32_t K = (int32_t)ctx->saved_data["K"].toInt();
-        const int32_t NR = (int32_t)ctx->saved_data["NR"].toInt();
+        const int32_t cap = (int32_t)ctx->saved_data["cap"].toInt();
+        const int32_t n_local = (int32_t)ctx->saved_data["n_local"].toInt();
         auto dL_dcolor = grad_out[0].contiguous();
         const int64_t P = means3D.size(0);
         auto fo = means3D.options();
@@ -233,7 +237,7 @@ class RasterizeGaussians : public torch::autograd::Function<RasterizeGaussians> 
         const gsr_camera c = cam.to_c();
         const gsr_gaussians g = make_gaussians(rs, means3D, sh_dc, sh_rest, colors, opac, scales, rots, cov3D);
         const gsr_raster_settings s = make_settings(rs);
-        const gsr_buffers b = buffers_of(geom, binning, image, K, NR);
+        const gsr_buffers b = buffers_of(geom, binning, image, K, cap, n_local);
         AllocCtx scratch{means3D.device(), {}};
         check(gsr_backward(&c, &g, &s, &b, dL_dcolor.data_ptr<float>(), alloc_cb, &scratch, &gg, cur_stream()),
               "gsr_backward");
@@ -336,8 +340,9 @@ static gsr::RasterCamera cam_from_py(int w, int h, float tx, float ty, const std
 }
 
 static gsr::RasterSettings settings_from_py(const std::vector<float>& bg, float smod, int D, int ty0, int ty1,
-                                            bool debug) {
+                                            bool debug, int max_rendered) {
     gsr::RasterSettings rs;
+    rs.max_rendered = max_rendered;
     for (int i = 0; i < 3; ++i) rs.bg[i] = bg.at(i);
     rs.scale_modifier = smod;
     rs.sh_degree = D;
@@ -355,11 +360,16 @@ PYBIND11_MODULE(_gsr_torch, m) {
         .def(py::init(&cam_from_py), py::arg("width"), py::arg("height"), py::arg("tanfovx"),
              py::arg("tanfovy"), py::arg("viewmatrix"), py::arg("projmatrix"), py::arg("campos"))
         .def_readonly("width", &gsr::RasterCamera::width)
-        .def_readonly("height", &gsr::RasterCamera::height);
+        .def_readonly("height", &gsr::RasterCamera::height)
+        .def_readonly("tanfovx", &gsr::RasterCamera::tanfovx)
+        .def_readonly("tanfovy", &gsr::RasterCamera::tanfovy)
+        .def_readonly("viewmatrix", &gsr::RasterCamera::viewmatrix)
+        .def_readonly("projmatrix", &gsr::RasterCamera::projmatrix)
+        .def_readonly("campos", &gsr::RasterCamera::campos);
     py::class_<gsr::RasterSettings>(m, "RasterSettings")
         .def(py::init(&settings_from_py), py::arg("bg"), py::arg("scale_modifier") = 1.0f,
              py::arg("sh_degree") = 0, py::arg("tile_y0") = 0, py::arg("tile_y1") = INT32_MAX,
-             py::arg("debug") = false);
+             py::arg("debug") = false, py::arg("max_rendered") = 0);
     m.def(
         "rasterize_gaussians",
         [](const gsr::RasterCamera& cam, const gsr::RasterSettings& rs, torch::Tensor means3D,
@@ -374,6 +384,13 @@ PYBIND11_MODULE(_gsr_torch, m) {
         py::arg("sh_rest"), py::arg("colors_precomp"), py::arg("opacities"), py::arg("scales"),
         py::arg("rotations"), py::arg("cov3D_precomp"));
     m.def("eval_sh_colors", &gsr::eval_sh_colors);
+    m.def(
+        "camera_from_tensors",
+        [](int w, int h, double fovx, double fovy, torch::Tensor wv, torch::Tensor fp, torch::Tensor cc) {
+            return gsr::RasterCamera::from_tensors(w, h, fovx, fovy, wv, fp, cc);
+        },
+        py::arg("width"), py::arg("height"), py::arg("FoVx"), py::arg("FoVy"), py::arg("world_view_transform"),
+        py::arg("full_proj_transform"), py::arg("camera_center"));
     m.def("abi_version", []() { return gsr_abi_version(); });
 }
 #endif  // GSR_NO_PYBIND

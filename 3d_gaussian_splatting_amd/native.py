@@ -3,9 +3,10 @@
 Product path, no fallback: if lib/libgsr_hip.so or the libtorch extension is missing this
 module raises -- it never substitutes a CPU implementation.
 
-``CAbi`` is the ctypes stub a Python (or any FFI) caller binds: the parity tests drive the
-HIP kernels through it directly (gsr_forward / gsr_backward / gsr_backward_blend /
-gsr_backward_preprocess / gsr_view), with device memory owned by torch tensors.
+The ctypes structures and argtypes below are the stub a Python (or any FFI) caller binds: the
+parity tests drive the HIP kernels through them directly (gsr_forward / gsr_backward /
+gsr_backward_blend / gsr_backward_preprocess / the multi-GPU gsr_shard_* / gsr_band_* split /
+gsr_view), with device memory owned by torch tensors.
 """
 from __future__ import annotations
 
@@ -18,15 +19,20 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(PKG, "lib")
 HIP_LIB = os.path.join(LIB_DIR, "libgsr_hip.so")
 
+ABI_VERSION = 2
 GSR_FLAG_DEBUG = 1
-GSR_FLAG_BAND_ONLY = 2
+GSR_ERR_OVERFLOW = -4
 GSR_GRAD2D_STRIDE = 12
 GSR_MAX_BATCH = 64
+GSR_SPLAT_BYTES = 64
+GSR_SPLAT_GRAD_BYTES = 48
+MAX_BANDS = 16
 VIEW_SORTED_GID, VIEW_SORTED_TILE, VIEW_RANGES, VIEW_FINAL_T, VIEW_N_CONTRIB, VIEW_DEPTH_KEY, \
-    VIEW_TILES_TOUCHED, VIEW_RECORDS, VIEW_GID_BY_RANK = range(1, 10)
-EXPORTS = ["gsr_abi_version", "gsr_last_error", "gsr_forward", "gsr_forward_batch", "gsr_backward",
-           "gsr_backward_blend",
-           "gsr_backward_preprocess", "gsr_backward_preprocess_range", "gsr_view", "gsr_geom_bytes", "gsr_binning_bytes",
+    VIEW_TILES_TOUCHED, VIEW_RECORDS, VIEW_COUNTS, VIEW_TERM = range(1, 11)
+EXPORTS = ["gsr_abi_version", "gsr_last_error", "gsr_forward", "gsr_read_num_rendered", "gsr_forward_batch",
+           "gsr_backward", "gsr_backward_blend", "gsr_backward_preprocess", "gsr_shard_forward",
+           "gsr_band_forward", "gsr_band_backward", "gsr_shard_backward", "gsr_exchange_block_bytes",
+           "gsr_shard_state_bytes", "gsr_view", "gsr_geom_bytes", "gsr_binning_bytes",
            "gsr_image_bytes", "gsr_scratch_bytes", "gsr_profile_enable", "gsr_profile_read",
            "gsr_stage_name"]
 # include/gsr/gsr_train.h (training-step kernels)
@@ -37,7 +43,7 @@ ACT_NONE, ACT_EXP, ACT_SIGMOID, ACT_NORMALIZE4 = range(4)
 ADAM_MAX_GROUPS = 8
 GATHER_MAX = 24
 STAGES = ["preprocess", "depth_sort", "scan", "duplicate", "tile_sort", "finalize", "blend_fwd", "blend_bwd",
-          "preprocess_bwd", "gather_grad2d", "misc"]
+          "preprocess_bwd", "gather_grad2d", "misc", "exchange"]
 
 
 class Camera(ctypes.Structure):
@@ -56,7 +62,7 @@ class Gaussians(ctypes.Structure):
 
 class Settings(ctypes.Structure):
     _fields_ = [("bg", ctypes.c_float * 3), ("tile_y0", ctypes.c_int32), ("tile_y1", ctypes.c_int32),
-                ("flags", ctypes.c_uint32)]
+                ("flags", ctypes.c_uint32), ("max_rendered", ctypes.c_int32)]
 
 
 class Grads(ctypes.Structure):
@@ -67,7 +73,8 @@ class Grads(ctypes.Structure):
 
 class Buffers(ctypes.Structure):
     _fields_ = [("geom", ctypes.c_void_p), ("binning", ctypes.c_void_p), ("image", ctypes.c_void_p),
-                ("num_rendered", ctypes.c_int32), ("num_ranked", ctypes.c_int32)]
+                ("num_rendered", ctypes.c_int32), ("capacity", ctypes.c_int32), ("n_local", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
 
 
 class AdamGroup(ctypes.Structure):
@@ -104,6 +111,8 @@ def load_hip() -> ctypes.CDLL:
         L.gsr_forward.restype = ctypes.c_int
         L.gsr_forward.argtypes = [ctypes.POINTER(Camera), ctypes.POINTER(Gaussians), ctypes.POINTER(Settings),
                                   vp, vp, ALLOC_FN, ALLOC_FN, ALLOC_FN, vp, ctypes.POINTER(Buffers), vp]
+        L.gsr_read_num_rendered.restype = ctypes.c_int
+        L.gsr_read_num_rendered.argtypes = [ctypes.POINTER(Camera), ctypes.POINTER(Buffers), ctypes.POINTER(i32), vp]
         L.gsr_forward_batch.restype = ctypes.c_int
         L.gsr_forward_batch.argtypes = [i32, ctypes.POINTER(Camera), ctypes.POINTER(Gaussians),
                                         ctypes.POINTER(Settings), ctypes.POINTER(vp), ctypes.POINTER(vp), ALLOC_FN,
@@ -119,10 +128,24 @@ def load_hip() -> ctypes.CDLL:
         L.gsr_backward_preprocess.argtypes = [ctypes.POINTER(Camera), ctypes.POINTER(Gaussians),
                                               ctypes.POINTER(Settings), ctypes.POINTER(Buffers), vp,
                                               ctypes.POINTER(Grads), vp]
-        L.gsr_backward_preprocess_range.restype = ctypes.c_int
-        L.gsr_backward_preprocess_range.argtypes = [ctypes.POINTER(Camera), ctypes.POINTER(Gaussians),
-                                                    ctypes.POINTER(Settings), ctypes.POINTER(Buffers), i32, i32,
-                                                    vp, ctypes.POINTER(Grads), vp]
+        # multi-GPU split: shard F1 + pack, band F2..F6, band B1, shard sum + B2
+        pi32 = ctypes.POINTER(i32)
+        L.gsr_exchange_block_bytes.restype = ctypes.c_size_t
+        L.gsr_exchange_block_bytes.argtypes = [i32]
+        L.gsr_shard_state_bytes.restype = ctypes.c_size_t
+        L.gsr_shard_state_bytes.argtypes = [i32, i32, i32]
+        L.gsr_shard_forward.restype = ctypes.c_int
+        L.gsr_shard_forward.argtypes = [ctypes.POINTER(Camera), ctypes.POINTER(Gaussians), ctypes.POINTER(Settings),
+                                        i32, pi32, i32, vp, vp, vp, vp, vp]
+        L.gsr_band_forward.restype = ctypes.c_int
+        L.gsr_band_forward.argtypes = [ctypes.POINTER(Camera), ctypes.POINTER(Settings), i32, i32, vp, vp,
+                                       ALLOC_FN, ALLOC_FN, ALLOC_FN, vp, ctypes.POINTER(Buffers), vp]
+        L.gsr_band_backward.restype = ctypes.c_int
+        L.gsr_band_backward.argtypes = [ctypes.POINTER(Camera), ctypes.POINTER(Settings), i32, i32,
+                                        ctypes.POINTER(Buffers), vp, ALLOC_FN, vp, vp, vp]
+        L.gsr_shard_backward.restype = ctypes.c_int
+        L.gsr_shard_backward.argtypes = [ctypes.POINTER(Camera), ctypes.POINTER(Gaussians), ctypes.POINTER(Settings),
+                                         i32, pi32, i32, vp, vp, ctypes.POINTER(Grads), vp]
         L.gsr_view.restype = vp
         L.gsr_view.argtypes = [ctypes.POINTER(Camera), i32, ctypes.POINTER(Buffers), ctypes.c_int]
         for n in ("gsr_geom_bytes", "gsr_binning_bytes", "gsr_scratch_bytes"):

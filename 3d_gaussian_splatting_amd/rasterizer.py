@@ -62,6 +62,19 @@ class ForwardState:
 
     @property
     def num_rendered(self) -> int:
+        """K.  Under a binning bound (max_rendered > 0) K stays on the device until asked for:
+        the first access reads it back (synchronising the stream) and raises on an overflow."""
+        if self.buffers.num_rendered < 0:
+            L = native.load_hip()
+            c = native.camera_struct(self.cam)
+            k = ctypes.c_int32(0)
+            rc = L.gsr_read_num_rendered(ctypes.byref(c), ctypes.byref(self.buffers), ctypes.byref(k),
+                                         ctypes.c_void_p(torch.cuda.current_stream(self.color.device).cuda_stream))
+            if rc == native.GSR_ERR_OVERFLOW:
+                raise OverflowError(native.last_error())
+            if rc != 0:
+                raise RuntimeError(f"gsr_read_num_rendered failed ({rc}): {native.last_error()}")
+            self.buffers.num_rendered = k.value
         return int(self.buffers.num_rendered)
 
     def _owner(self, ptr: int):
@@ -99,7 +112,7 @@ class CAbiRasterizer:
             raise RuntimeError(f"{what} failed ({rc}): {native.last_error()}")
 
     def _prepare(self, means3D, opacities, scales, rotations, sh_dc, sh_rest, sh_degree, colors_precomp,
-                 cov3D_precomp, scale_modifier, bg, tile_rows, band_only, debug):
+                 cov3D_precomp, scale_modifier, bg, tile_rows, max_rendered, debug):
         dev = self.device
         means3D = _f32(means3D, device=dev)
         P = int(means3D.shape[0])
@@ -123,15 +136,19 @@ class CAbiRasterizer:
         s = native.Settings()
         s.bg[:] = [float(v) for v in bg]
         s.tile_y0, s.tile_y1 = (0, INT32_MAX) if tile_rows is None else (int(tile_rows[0]), int(tile_rows[1]))
-        s.flags = (native.GSR_FLAG_DEBUG if debug else 0) | (native.GSR_FLAG_BAND_ONLY if band_only else 0)
+        s.flags = native.GSR_FLAG_DEBUG if debug else 0
+        s.max_rendered = int(max_rendered)
         return inputs, g, s
 
     def forward(self, cam: RasterCamera, means3D, opacities, scales=None, rotations=None, sh_dc=None,
                 sh_rest=None, sh_degree=0, colors_precomp=None, cov3D_precomp=None, scale_modifier=1.0,
-                bg=(0.0, 0.0, 0.0), tile_rows=None, band_only=False, debug=False) -> ForwardState:
+                bg=(0.0, 0.0, 0.0), tile_rows=None, max_rendered=0, debug=False) -> ForwardState:
+        """gsr_forward.  max_rendered > 0 sizes the binning for that many instances and skips the
+        host read of K (see ForwardState.num_rendered)."""
         dev = self.device
         inputs, g, s = self._prepare(means3D, opacities, scales, rotations, sh_dc, sh_rest, sh_degree,
-                                     colors_precomp, cov3D_precomp, scale_modifier, bg, tile_rows, band_only, debug)
+                                     colors_precomp, cov3D_precomp, scale_modifier, bg, tile_rows, max_rendered,
+                                     debug)
         P = g.P
         color = torch.empty((3, cam.height, cam.width), dtype=torch.float32, device=dev)
         radii = torch.empty((P,), dtype=torch.int32, device=dev)
@@ -147,11 +164,12 @@ class CAbiRasterizer:
 
     def forward_batch(self, cams, means3D, opacities, scales=None, rotations=None, sh_dc=None, sh_rest=None,
                       sh_degree=0, colors_precomp=None, cov3D_precomp=None, scale_modifier=1.0,
-                      bg=(0.0, 0.0, 0.0), debug=False) -> list:
-        """gsr_forward_batch: one ForwardState per camera (full images), one host wait in total."""
+                      bg=(0.0, 0.0, 0.0), max_rendered=0, debug=False) -> list:
+        """gsr_forward_batch: one ForwardState per camera (full images), one host wait in total
+        (none with max_rendered > 0)."""
         dev = self.device
         inputs, g, s = self._prepare(means3D, opacities, scales, rotations, sh_dc, sh_rest, sh_degree,
-                                     colors_precomp, cov3D_precomp, scale_modifier, bg, None, False, debug)
+                                     colors_precomp, cov3D_precomp, scale_modifier, bg, None, max_rendered, debug)
         V, P = len(cams), g.P
         colors = [torch.empty((3, c.height, c.width), dtype=torch.float32, device=dev) for c in cams]
         radii = [torch.empty((P,), dtype=torch.int32, device=dev) for _ in cams]
@@ -208,7 +226,7 @@ class CAbiRasterizer:
 
     def backward_blend(self, st: ForwardState, dL_dpix, out: torch.Tensor | None = None) -> torch.Tensor:
         """B1 + per-Gaussian sum -> grad2d (P x 12).  `out`: optional contiguous (>= P) x 12
-        tensor to write into (e.g. a buffer padded for a reduce-scatter)."""
+        tensor to write into."""
         dpix = _f32(dL_dpix, (3, st.cam.height, st.cam.width), self.device)
         if out is None:
             grad2d = torch.empty((st.gauss.P, native.GSR_GRAD2D_STRIDE), dtype=torch.float32, device=self.device)
@@ -235,16 +253,107 @@ class CAbiRasterizer:
         self._check(rc, "gsr_backward_preprocess")
         return out
 
-    def backward_preprocess_range(self, st: ForwardState, g0: int, g1: int, grad2d: torch.Tensor) -> dict:
-        """B2 on Gaussians [g0, g1): `grad2d` holds that slice's rows; the returned gradients
-        are the slice's (g1 - g0 rows)."""
-        out, gg = self._grad_tensors(st, g1 - g0)
-        grad2d = grad2d.contiguous()
+
+# ------------------------------------------------------------------------------------------
+# multi-GPU split (gsr_shard_* / gsr_band_*): the compute of one rank
+# ------------------------------------------------------------------------------------------
+@dataclass
+class ShardState:
+    """gsr_shard_forward's outputs a rank keeps until gsr_shard_backward."""
+    cam: RasterCamera
+    inputs: dict
+    settings: native.Settings
+    gauss: native.Gaussians
+    band_rows: list
+    pair_cap: int
+    send: torch.Tensor        # nbands exchange blocks (uint8)
+    state: torch.Tensor       # gsr_shard_state_bytes (uint8)
+    radii: torch.Tensor
+
+    @property
+    def counts(self) -> torch.Tensor:
+        """Splats packed per band (device u32 headers; > pair_cap = overflow)."""
+        nb = len(self.band_rows) - 1
+        blk = self.send.numel() // nb
+        return self.send.view(nb, blk)[:, :4].contiguous().view(torch.int32)[:, 0]
+
+
+class ShardRasterizer(CAbiRasterizer):
+    """The per-rank calls of the multi-GPU path; the caller moves the exchange blocks."""
+
+    def block_bytes(self, pair_cap: int) -> int:
+        return int(self.L.gsr_exchange_block_bytes(int(pair_cap)))
+
+    def shard_forward(self, cam: RasterCamera, band_rows, pair_cap: int, means3D, opacities, scales=None,
+                      rotations=None, sh_dc=None, sh_rest=None, sh_degree=0, colors_precomp=None,
+                      cov3D_precomp=None, scale_modifier=1.0, row_hist: torch.Tensor | None = None,
+                      debug=False) -> ShardState:
+        dev = self.device
+        inputs, g, s = self._prepare(means3D, opacities, scales, rotations, sh_dc, sh_rest, sh_degree,
+                                     colors_precomp, cov3D_precomp, scale_modifier, (0.0, 0.0, 0.0), None, 0, debug)
+        nb = len(band_rows) - 1
+        rows = (ctypes.c_int32 * (nb + 1))(*[int(r) for r in band_rows])
+        send = torch.empty(nb * self.block_bytes(pair_cap), dtype=torch.uint8, device=dev)
+        state = torch.empty(int(self.L.gsr_shard_state_bytes(g.P, nb, int(pair_cap))), dtype=torch.uint8,
+                            device=dev)
+        radii = torch.empty((g.P,), dtype=torch.int32, device=dev)
+        c = native.camera_struct(cam)
+        rc = self.L.gsr_shard_forward(ctypes.byref(c), ctypes.byref(g), ctypes.byref(s), nb, rows, int(pair_cap),
+                                      _ptr(send), _ptr(radii) if g.P else None, _ptr(state), _ptr(row_hist),
+                                      self._stream())
+        self._check(rc, "gsr_shard_forward")
+        return ShardState(cam=cam, inputs=inputs, settings=s, gauss=g, band_rows=list(band_rows),
+                          pair_cap=int(pair_cap), send=send, state=state, radii=radii)
+
+    def band_forward(self, cam: RasterCamera, tile_rows, nsrc: int, pair_cap: int, recv: torch.Tensor,
+                     max_rendered: int, out_color: torch.Tensor | None = None, bg=(0.0, 0.0, 0.0),
+                     debug=False) -> ForwardState:
+        """F2..F6 over the splats received from nsrc shards; only the band's pixels of
+        out_color are written."""
+        dev = self.device
+        s = native.Settings()
+        s.bg[:] = [float(v) for v in bg]
+        s.tile_y0, s.tile_y1 = int(tile_rows[0]), int(tile_rows[1])
+        s.flags = native.GSR_FLAG_DEBUG if debug else 0
+        s.max_rendered = int(max_rendered)
+        color = out_color if out_color is not None else torch.zeros((3, cam.height, cam.width),
+                                                                     dtype=torch.float32, device=dev)
+        ag, ab, ai = _Allocator(dev), _Allocator(dev), _Allocator(dev)
+        bufs = native.Buffers()
+        c = native.camera_struct(cam)
+        rc = self.L.gsr_band_forward(ctypes.byref(c), ctypes.byref(s), int(nsrc), int(pair_cap), _ptr(recv),
+                                     _ptr(color), ag.cb, ab.cb, ai.cb, None, ctypes.byref(bufs), self._stream())
+        self._check(rc, "gsr_band_forward")
+        g = native.Gaussians()
+        g.P = int(nsrc) * int(pair_cap)
+        return ForwardState(cam=cam, inputs={"recv": recv}, settings=s, gauss=g, buffers=bufs, color=color,
+                            radii=torch.empty(0, dtype=torch.int32, device=dev), allocs=[ag, ab, ai])
+
+    def band_backward(self, st: ForwardState, nsrc: int, pair_cap: int, dL_dpix) -> torch.Tensor:
+        """B1 + per-splat 2D gradients in the received slot layout: (nsrc * pair_cap, 12) f32."""
+        dpix = _f32(dL_dpix, (3, st.cam.height, st.cam.width), self.device)
+        out = torch.empty((int(nsrc) * int(pair_cap), native.GSR_GRAD2D_STRIDE), dtype=torch.float32,
+                          device=self.device)
+        scratch = _Allocator(self.device)
         c = native.camera_struct(st.cam)
-        rc = self.L.gsr_backward_preprocess_range(ctypes.byref(c), ctypes.byref(st.gauss), ctypes.byref(st.settings),
-                                                  ctypes.byref(st.buffers), int(g0), int(g1), _ptr(grad2d),
-                                                  ctypes.byref(gg), self._stream())
-        self._check(rc, "gsr_backward_preprocess_range")
+        rc = self.L.gsr_band_backward(ctypes.byref(c), ctypes.byref(st.settings), int(nsrc), int(pair_cap),
+                                      ctypes.byref(st.buffers), _ptr(dpix), scratch.cb, None, _ptr(out),
+                                      self._stream())
+        self._check(rc, "gsr_band_backward")
+        return out
+
+    def shard_backward(self, sh: ShardState, grad_recv: torch.Tensor) -> dict:
+        """Sum of the bands' 2D gradients per Gaussian (band order), then B2 on the shard."""
+        st = ForwardState(cam=sh.cam, inputs=sh.inputs, settings=sh.settings, gauss=sh.gauss,
+                          buffers=native.Buffers(), color=sh.radii, radii=sh.radii)
+        out, gg = self._grad_tensors(st)
+        nb = len(sh.band_rows) - 1
+        rows = (ctypes.c_int32 * (nb + 1))(*[int(r) for r in sh.band_rows])
+        c = native.camera_struct(sh.cam)
+        rc = self.L.gsr_shard_backward(ctypes.byref(c), ctypes.byref(sh.gauss), ctypes.byref(sh.settings), nb, rows,
+                                       sh.pair_cap, _ptr(sh.state), _ptr(grad_recv.contiguous()), ctypes.byref(gg),
+                                       self._stream())
+        self._check(rc, "gsr_shard_backward")
         return out
 
 
@@ -260,13 +369,14 @@ def ext_camera(cam: RasterCamera):
 
 def rasterize_gaussians(cam: RasterCamera, means3D, means2D, opacities, sh_dc=None, sh_rest=None,
                         colors_precomp=None, scales=None, rotations=None, cov3D_precomp=None,
-                        sh_degree=0, scale_modifier=1.0, bg=(0.0, 0.0, 0.0), tile_rows=None, debug=False):
+                        sh_degree=0, scale_modifier=1.0, bg=(0.0, 0.0, 0.0), tile_rows=None, debug=False,
+                        max_rendered=0):
     """RasterizeGaussians.apply: returns (color (3,H,W), radii (P,) int32); differentiable in
     every tensor input (means2D receives the screen-space gradient)."""
     ext = native.load_torch_ext()
     y0, y1 = (0, INT32_MAX) if tile_rows is None else tile_rows
     rs = ext.RasterSettings([float(v) for v in bg], float(scale_modifier), int(sh_degree), int(y0), int(y1),
-                            bool(debug))
+                            bool(debug), int(max_rendered))
     return ext.rasterize_gaussians(ext_camera(cam), rs, means3D, means2D, sh_dc, sh_rest, colors_precomp,
                                    opacities, scales, rotations, cov3D_precomp)
 

@@ -199,7 +199,7 @@ class GaussianTrainer:
 
     def __init__(self, xyz, f_dc, f_rest, opacity, scaling, rotation, max_sh_degree: int,
                  opt: OptimizationParams | None = None, spatial_lr_scale: float = 1.0, device="cuda",
-                 seed: int = 0):
+                 seed: int = 0, cameras_extent: float | None = None):
         self.device = _device(device)
         dev = self.device
         f = lambda a, shape: torch.as_tensor(a, dtype=torch.float32).reshape(shape).to(dev).contiguous()
@@ -210,6 +210,9 @@ class GaussianTrainer:
         self.max_sh_degree = int(max_sh_degree)
         self.active_sh_degree = 0
         self.spatial_lr_scale = float(spatial_lr_scale)
+        # scene extent for the clone / split threshold and the world-size prune; upstream sets
+        # spatial_lr_scale to this same value (the nerf++ radius of the training cameras)
+        self.cameras_extent = float(spatial_lr_scale if cameras_extent is None else cameras_extent)
         self.k = TrainKernels(dev)
         self.rast = CAbiRasterizer(dev)
         self.gen = torch.Generator(device=dev)
@@ -244,7 +247,7 @@ class GaussianTrainer:
         statistics, SH degree, spatial LR scale and every group's Adam state, one file."""
         scene_io.save_checkpoint(path, {
             "active_sh_degree": self.active_sh_degree, "spatial_lr_scale": self.spatial_lr_scale,
-            "params": self.params, "max_radii2D": self.max_radii2D, "xyz_gradient_accum": self.xyz_gradient_accum,
+            "cameras_extent": self.cameras_extent, "params": self.params, "max_radii2D": self.max_radii2D, "xyz_gradient_accum": self.xyz_gradient_accum,
             "denom": self.denom, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq, "steps": self.steps})
 
     def restore(self, path: str, opt: OptimizationParams | None = None) -> None:
@@ -253,6 +256,7 @@ class GaussianTrainer:
         st = scene_io.load_checkpoint(path, self.device)
         self.params = {k: v.contiguous() for k, v in st["params"].items()}
         self.spatial_lr_scale = st["spatial_lr_scale"]
+        self.cameras_extent = st.get("cameras_extent", self.spatial_lr_scale)
         self.setup(opt or self.opt)
         self.active_sh_degree = st["active_sh_degree"]
         self.max_radii2D, self.xyz_gradient_accum, self.denom = st["max_radii2D"], st["xyz_gradient_accum"], st["denom"]
@@ -318,9 +322,14 @@ class GaussianTrainer:
         return st
 
     def step(self, iteration: int, cam, gt_image: torch.Tensor, bg=(0.0, 0.0, 0.0), densify: bool = True) -> dict:
-        """One training iteration (train_utils.cpp:128-145 order).  Returns device tensors
-        (loss stats [loss, l1, ssim], radii); no host synchronisation unless a densification
-        or opacity reset is due."""
+        """One training iteration in the upstream order (train_utils.cpp:128-145 plus the body
+        its stub omits): LR update, SH degree, render, loss, backward, densification statistics,
+        densify / prune and opacity reset, then the optimizer step.  As upstream, a group whose
+        tensor densification or the opacity reset has just replaced takes no Adam update in
+        that iteration (torch Adam skips a fresh parameter, whose .grad is None): a densify
+        iteration updates no group, an opacity reset alone skips the opacity group.  Returns
+        device tensors (loss stats [loss, l1, ssim], radii); no host synchronisation unless a
+        densification is due."""
         opt = self.opt
         self.update_learning_rate(iteration)
         if iteration % 1000 == 0:
@@ -329,22 +338,25 @@ class GaussianTrainer:
         stats, maps = self.k.loss_forward(st.color, gt_image, opt.lambda_dssim)
         dimg = self.k.loss_backward(st.color, gt_image, opt.lambda_dssim, maps)
         g = self.rast.backward(st, dimg)
-        if iteration < opt.densify_until_iter:
-            self.k.densify_stats(st.radii, g["means2D"], self.max_radii2D, self.xyz_gradient_accum, self.denom)
         grads = {"xyz": g["means3D"], "f_dc": g["sh_dc"], "opacity": g["opacities"], "scaling": g["scales"],
                  "rotation": g["rotations"]}
         if self.params["f_rest"].shape[1]:
             grads["f_rest"] = g["sh_rest"]
-        self.optimizer_step(grads)
-        if densify and iteration < opt.densify_until_iter:
-            if iteration > opt.densify_from_iter and iteration % opt.densification_interval == 0:
-                size_threshold = 20 if iteration > opt.opacity_reset_interval else None
-                self.densify_and_prune(opt.densify_grad_threshold, 0.005, self.cameras_extent, size_threshold)
-            if iteration % opt.opacity_reset_interval == 0:
-                self.reset_opacity()
-        return {"stats": stats, "radii": st.radii, "num_rendered": st.num_rendered, "image": st.color}
-
-    cameras_extent = 1.0
+        replaced = set()
+        if iteration < opt.densify_until_iter:
+            self.k.densify_stats(st.radii, g["means2D"], self.max_radii2D, self.xyz_gradient_accum, self.denom)
+            if densify:
+                if iteration > opt.densify_from_iter and iteration % opt.densification_interval == 0:
+                    size_threshold = 20 if iteration > opt.opacity_reset_interval else None
+                    self.densify_and_prune(opt.densify_grad_threshold, 0.005, self.cameras_extent, size_threshold)
+                    replaced.update(GROUPS)
+                if iteration % opt.opacity_reset_interval == 0:
+                    self.reset_opacity()
+                    replaced.add("opacity")
+        if iteration < opt.iterations:
+            self.optimizer_step({k: v for k, v in grads.items() if k not in replaced})
+        return {"stats": stats, "radii": st.radii, "num_rendered": st.num_rendered, "image": st.color,
+                "num_points": self.num_points}
 
     def optimizer_step(self, grads: dict):
         groups = []
@@ -355,7 +367,8 @@ class GaussianTrainer:
             groups.append(dict(param=self.params[k], grad=grads[k].reshape(self.params[k].shape).contiguous(),
                                exp_avg=self.exp_avg[k], exp_avg_sq=self.exp_avg_sq[k], act=ACTS[k],
                                step=self.steps[k], lr=self.lr[k]))
-        self.k.adam_step(groups)
+        if groups:
+            self.k.adam_step(groups)
 
     # ---------------------------------------------------------------- densification (upstream)
     def _append(self, new: dict):

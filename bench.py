@@ -7,19 +7,22 @@
 
 One step = gsr_forward + gsr_backward (through the C ABI) of the whole synthetic scene:
 1M Gaussians, 1920x1080, SH degree 3 (BASELINE configs[2], the roofline run; inputs already
-resident in HBM).  N > 1: screen-space tile-row bands, one per rank (RCCL): replicated
-preprocess, band-local binning/blend, asynchronous all-gather of the image bands (overlaps
-the blend backward), blend-backward on the band, sparse all-to-all of the band candidates'
-2D gradients to the ranks owning their Gaussian slice, preprocess-backward on the rank's
-slice (leaf gradients sharded).  The
-whole image is rendered once per step for the job, so value = steps/s of the job
-("scaling": "strong").  Rank 0 prints ONE JSON line.
+resident in HBM).  The binning is sized from the first (untimed) forward's K with 10 %
+headroom (gsr_raster_settings.max_rendered), so no step waits on a host read.  N > 1 (one
+process per GPU, RCCL): the Gaussian-sharded x tile-row-band split of bands.ShardStep -- F1 on
+the rank's Gaussian shard, all-to-all of the projected splats to the bands, band binning +
+blend, asynchronous all-gather of the band images (overlaps B1), B1 on the band, all-to-all of
+the splats' 2D gradients back, B2 on the shard.  The whole image is rendered once per step for
+the job, so value = steps/s of the job ("scaling": "strong").  Rank 0 prints ONE JSON line.
 
 roofline: the dominant kernel's algorithmic HBM bytes (SURVEY §8d formulas) per
 launch / its mean launch time from HIP events recorded on the launch stream over the timed
-region (gsr_profile_*), against 8.0 TB/s.  cpu_baseline: the CPU oracle (oracle/, a C port
-of the same algorithm) timed on this host's cores for ONE forward+backward of the same
-workload (rank 0, N = 1), which also gives the PSNR / gradient error of the GPU result.
+region (gsr_profile_*), against 8.0 TB/s.  `traffic` / `valu_issue` come from the committed
+rocprofv3 PMC passes (profiles/pmc_traffic.json) and are dropped unless those passes were of
+this workload AND of this build of libgsr_hip.so (source stamp).  cpu_baseline: the CPU oracle
+(oracle/, a C port of the same algorithm) timed on this host's cores, median of 3
+forward+backward iterations of the same workload after one warm-up (rank 0, N = 1), which also
+gives the PSNR / gradient error of the GPU result.
 """
 from __future__ import annotations
 
@@ -76,21 +79,39 @@ def algorithmic_bytes(P, V, K, pix, tiles, M):
     }
 
 
+def lib_stamp() -> str | None:
+    """Source stamp of the loaded libgsr_hip.so (sha256 of its sources + flags, _build.py)."""
+    path = native.hip_library_path() + ".stamp"
+    return open(path).read().strip() if os.path.exists(path) else None
+
+
 def pmc_record(kernel_prefix, workload):
     """Per-launch PMC figures of `kernel_prefix` (HBM bytes, VALU instructions) from the
     committed rocprofv3 passes (profiles/pmc_traffic.json, written by
-    scripts/pmc_summary.py --traffic), or {} when those passes were of another workload."""
+    scripts/pmc_summary.py --traffic), or {} when those passes were of another workload or of
+    another build of the library (their lib_stamp differs from the loaded one)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return {}
     with open(path) as fh:
         data = json.load(fh)
-    if data.get("workload") != workload:
+    if data.get("workload") != workload or data.get("lib_stamp") != lib_stamp():
         return {}
     for name, rec in data.get("kernels", {}).items():
         if name.startswith(kernel_prefix):
             return rec
     return {}
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def main():
@@ -133,29 +154,27 @@ def main():
     cam = gr.synthetic_camera(W, H)
     scene = sc.make_scene(cam, P, max_sh_degree=max(D, 0), seed=0)
     dpix_np = sc.make_dL_dpix(cam, seed=1)
-    rast = R.CAbiRasterizer(dev)
     t = lambda a: torch.tensor(a, device=dev)
     inputs = dict(means3D=t(scene.means3D), opacities=t(scene.opacities), scales=t(scene.scales),
                   rotations=t(scene.rotations), sh_dc=t(scene.sh_dc), sh_rest=t(scene.sh_rest))
     dpix = t(dpix_np)
     gx, gy = cam.grid
-    band = bands.band_rows(gy, world, rank) if world > 1 else None
     if world > 1:
-        g0, g1 = bands.gaussian_slice(P, world, rank)
+        rast = R.ShardRasterizer(dev)
+        plan = bands.ShardStep(rast, cam, inputs, D, dist).plan()
+        band = plan.band
 
-    def step():
-        st = rast.forward(cam, **inputs, sh_degree=D, tile_rows=band, band_only=world > 1)
-        if world > 1:
-            img = bands.ImageGather(st.color, band, gy, dist)  # overlaps the blend backward
-            cand = st.view(native.VIEW_GID_BY_RANK, torch.int32, st.buffers.num_ranked)
-            xg = bands.GradExchange(cand, P, dist)  # row counts travel while B1 runs
-            g2 = rast.backward_blend(st, dpix)
-            mine = xg.run(g2)  # only the band's candidates' rows travel
-            g = rast.backward_preprocess_range(st, g0, g1, mine[: g1 - g0])  # leaf grads of my slice
-            img.wait()  # full image on every rank
-        else:
-            g = rast.backward(st, dpix)
-        return st, g
+        def step():
+            img, g, sh, st = plan.step(dpix)
+            return st, g, sh
+    else:
+        rast = R.CAbiRasterizer(dev)
+        K0 = rast.forward(cam, **inputs, sh_degree=D).num_rendered  # sizes the binning once
+        cap = bands.round_up(int(K0 * 1.1) + 1)
+
+        def step():
+            st = rast.forward(cam, **inputs, sh_degree=D, max_rendered=cap)
+            return st, rast.backward(st, dpix), None
 
     for _ in range(args.warmup):
         step()
@@ -184,7 +203,7 @@ def main():
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        st, g = step()
+        st, g, sh = step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -198,16 +217,18 @@ def main():
     ms_per_step = 1e3 * elapsed / args.steps
     value = args.steps / elapsed  # whole-image forward+backward iterations per second (job)
 
-    K = st.num_rendered
-    V = int((st.radii > 0).sum())
+    K = st.num_rendered  # raises on a binning overflow
     tiles = gx * gy
     M = (D + 1) ** 2
-    if world > 1:  # K is band-local; count the band's pixels and tiles
+    if world > 1:  # K, pixels and tiles of the band; P and V of the shard
+        V = int((sh.radii > 0).sum())
+        P_local = plan.g1 - plan.g0
         pix_local = (min(band[1] * 16, H) - band[0] * 16) * W
         tiles_local = (band[1] - band[0]) * gx
     else:
-        pix_local, tiles_local = W * H, tiles
-    alg = algorithmic_bytes(P, V, K, pix_local, tiles_local, M)
+        V = int((st.radii > 0).sum())
+        P_local, pix_local, tiles_local = P, W * H, tiles
+    alg = algorithmic_bytes(P_local, V, K, pix_local, tiles_local, M)
     result = {
         "metric": "forward+backward iters/s at 1080p, 1M Gaussians; PSNR vs CPU ref",
         "value": round(value, 3), "unit": "iters/s", "n_gpus": world, "steps": args.steps,
@@ -215,10 +236,14 @@ def main():
         "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": f"{args.config}: {P} Gaussians, {W}x{H}, SH degree {D}, fwd+bwd",
                    "gaussians": P, "width": W, "height": H, "sh_degree": D,
-                   "parallelism": f"tile-row bands x{world}" if world > 1 else "single GPU"},
+                   "parallelism": (f"Gaussian shards x instance-balanced tile-row bands x{world}" if world > 1
+                                   else "single GPU")},
         "mpixel_per_s": round(W * H * value / 1e6, 2),
         "counts": {"visible": V, "num_rendered": K, "tiles": tiles},
     }
+    if world > 1:
+        result["exchange"] = {"band_rows": plan.rows, "pair_cap": plan.pair_cap, "band_capacity": plan.capacity,
+                              "band_instances": plan.band_instances, "counts_are": "rank 0's shard / band"}
     if stages and rank == 0 and dom_stage in live and live[dom_stage][1]:
         result["stage_ms"] = {k: round(ms / args.steps, 4) for k, (ms, n) in stages.items() if n}
         dom = dom_stage
@@ -230,6 +255,7 @@ def main():
                        "preprocess": "preprocess_kernel", "preprocess_bwd": "preprocess_backward_kernel"}.get(dom, dom)
         pmc = pmc_record(kernel_name, args.config)
         result["roofline"] = {"bound": "hbm", "kernel": kernel_name, "achieved": round(achieved, 2),
+                              "lib_stamp": (lib_stamp() or "")[:16],
                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                               # PMC passes are of the N = 1 launch; a band launch has no committed counts
                               "traffic": pmc.get("hbm_bytes_per_launch") if world == 1 else None, "mean_launch_ms": round(mean_ms, 4),
@@ -255,11 +281,15 @@ def main():
         import gsr_oracle  # cpu_baseline leg only: the checker / reported baseline
         cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
         os.environ.setdefault("OMP_NUM_THREADS", str(cores))
-        c0 = time.perf_counter()
-        f = gsr_oracle.forward(cam, scene.means3D, scene.opacities, scene.scales, scene.rotations, scene.sh_dc,
-                               scene.sh_rest, sh_degree=D)
-        gc = f.state.backward(dpix_np)
-        cpu_s = time.perf_counter() - c0
+        times, f, gc = [], None, None
+        for it in range(4):  # one warm-up, then the median of three
+            c0 = time.perf_counter()
+            f = gsr_oracle.forward(cam, scene.means3D, scene.opacities, scene.scales, scene.rotations,
+                                   scene.sh_dc, scene.sh_rest, sh_degree=D)
+            gc = f.state.backward(dpix_np)
+            if it:
+                times.append(time.perf_counter() - c0)
+        cpu_s = float(np.median(times))
         col = st.color.cpu().numpy().astype(np.float64)
         mse = float(np.mean((col - f.color) ** 2))
         rel = {}
@@ -267,8 +297,11 @@ def main():
             a = g[k].cpu().numpy().reshape(gc[k].shape).astype(np.float64)
             rel[k] = float(np.linalg.norm(a - gc[k]) / max(np.linalg.norm(gc[k]), 1e-30))
         result["cpu_baseline"] = {"value": round(1.0 / cpu_s, 5), "unit": "iters/s", "cores": cores,
-                                  "kind": "port", "sample": f"1 forward+backward of the full {args.config} "
-                                  f"workload on the CPU oracle ({cpu_s:.2f} s, OpenMP {cores} threads)"}
+                                  "kind": "port", "sample": f"full {args.config} forward+backward on the CPU "
+                                  f"oracle, median of 3 after 1 warm-up ({', '.join(f'{x:.2f}' for x in times)} s; "
+                                  f"OpenMP {cores} threads)",
+                                  "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+                                  "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
         result["parity"] = {"psnr_db_vs_cpu": round(10 * math.log10(1.0 / mse), 2) if mse > 0 else float("inf"),
                             "rgb_rel_l2": float(np.linalg.norm(col - f.color) / np.linalg.norm(f.color)),
                             "grad_rel_l2_max": max(rel.values()),

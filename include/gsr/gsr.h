@@ -15,9 +15,11 @@
  *
  *   gsr_forward            <- render() forward         (F1..F6)
  *   gsr_backward           <- loss.backward() into it  (B1+B2, a17-a18)
- *   gsr_backward_blend     <- B1 + per-Gaussian sum only (multi-GPU: all-reduce between)
+ *   gsr_backward_blend     <- B1 + per-Gaussian sum only (2D gradients)
  *   gsr_backward_preprocess<- B2 only, from per-Gaussian 2D gradients
- *   gsr_backward_preprocess_range <- B2 on one Gaussian slice (multi-GPU, after reduce-scatter)
+ *   gsr_shard_* / gsr_band_* <- the multi-GPU split of the same path: F1/B2 on a
+ *                             Gaussian shard, F2..F6/B1 on a band of tile rows, with two
+ *                             all-to-all exchanges in between (done by the caller over RCCL)
  *
  * Conventions
  *   - Every pointer in gsr_gaussians / gsr_grads / outputs is caller-owned DEVICE memory
@@ -28,8 +30,11 @@
  *     buffers through gsr_alloc_fn (geometry: per Gaussian, binning: per tile instance,
  *     image: per pixel); the caller keeps them alive and passes them back to backward.
  *   - Streams: all work is ordered on `stream` (a hipStream_t; NULL = default stream).
- *     One device->host read per forward (num_rendered) synchronises that stream; a banded
- *     forward (tile_y0/y1 narrower than the image) adds a second (its candidate count).
+ *   - Host waits: with rs->max_rendered == 0 the forward reads K (num_rendered) back once to
+ *     size the binning exactly (the read overlaps the scan); with rs->max_rendered > 0 the
+ *     binning is sized for that many instances and nothing is read back: K stays on the
+ *     device (gsr_read_num_rendered), and K > max_rendered is an overflow the caller detects
+ *     there (instances past the bound are dropped, every kernel stays inside its buffers).
  *   - Errors: 0 = ok, < 0 = error; message in gsr_last_error() (thread-local).
  *   - Re-entrant; no global state besides the thread-local error string and the optional,
  *     off-by-default stage profiler (gsr_profile_*).
@@ -44,15 +49,13 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 1
+#define GSR_ABI_VERSION 2
 #define GSR_TILE 16 /* screen tiles are GSR_TILE x GSR_TILE pixels */
 #define GSR_GRAD2D_STRIDE 12 /* floats per Gaussian in a grad2d buffer (9 used) */
 
 /* flags */
 #define GSR_FLAG_DEBUG 1u /* synchronise + check after every stage */
-#define GSR_FLAG_BAND_ONLY 2u /* band forward/backward_blend for multi-GPU: leave pixels outside
-                                 the band and grad2d rows of Gaussians outside the band's
-                                 ranking unwritten (only those rows are exchanged) */
+#define GSR_ERR_OVERFLOW (-4) /* gsr_read_num_rendered: K exceeded the binning's capacity */
 
 typedef struct gsr_camera {
     int32_t width, height;
@@ -83,6 +86,8 @@ typedef struct gsr_raster_settings {
     int32_t tile_y0;         /* band of tile rows to bin/blend: [tile_y0, tile_y1); */
     int32_t tile_y1;         /* 0 and INT32_MAX = whole image (multi-GPU sharding)   */
     uint32_t flags;          /* GSR_FLAG_* */
+    int32_t max_rendered;    /* 0: binning sized from K (one host read per forward);
+                                > 0: binning for this many instances, no host read */
 } gsr_raster_settings;
 
 typedef struct gsr_grads {
@@ -104,31 +109,37 @@ typedef void* (*gsr_alloc_fn)(void* ctx, size_t bytes);
 
 typedef struct gsr_buffers {
     void* geom;              /* returned by the geometry allocation */
-    void* binning;           /* returned by the binning allocation (may be NULL if K == 0) */
+    void* binning;           /* returned by the binning allocation */
     void* image;             /* returned by the image allocation */
-    int32_t num_rendered;    /* K = number of (Gaussian, tile) instances */
-    int32_t num_ranked;      /* Gaussians in the depth ranking: P for a full image; for a band,
-                                only those with tiles in the band (pass back unchanged) */
+    int32_t num_rendered;    /* K = number of (Gaussian, tile) instances; -1 while it is only on
+                                the device (max_rendered > 0; see gsr_read_num_rendered) */
+    int32_t capacity;        /* instances the binning (and the backward's scratch) hold */
+    int32_t n_local;         /* Gaussians (or received splat slots, gsr_band_forward) indexed */
+    int32_t reserved;
 } gsr_buffers;
 
 int gsr_abi_version(void);
 const char* gsr_last_error(void);
 
 /* Forward: out_color (3 x H x W, channel-major) and radii (P, int32; 0 = culled).
- * Pixels outside the tile band are set to the background (left unwritten under
- * GSR_FLAG_BAND_ONLY).  Fills *bufs. */
+ * Pixels outside the tile band are set to the background.  Fills *bufs. */
 int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
                 float* out_color, int32_t* radii, gsr_alloc_fn alloc_geom,
                 gsr_alloc_fn alloc_binning, gsr_alloc_fn alloc_image, void* alloc_ctx,
                 gsr_buffers* bufs, void* stream);
 
+/* K of a forward, read back synchronously (waits for the forward on `stream`): sets
+ * bufs->num_rendered and returns 0, or GSR_ERR_OVERFLOW when K > bufs->capacity (the
+ * forward's outputs are then incomplete: re-run it with a larger max_rendered). */
+int gsr_read_num_rendered(const gsr_camera* cam, const gsr_buffers* bufs, int32_t* num_rendered,
+                          void* stream);
+
 /* Batched forward over V views of the same Gaussians (the reference's loop
  * renders one camera per iteration, src/utils/train_utils.cpp:128-145).  Per view the work of
- * gsr_forward, but the V first phases (preprocess + scan) are enqueued back to back and ONE
- * device->host read returns all V instance counts, so the host waits once per batch instead of
- * once per view and the GPU is not left idle between views.  cams[v], out_colors[v]
- * (3 x H_v x W_v), radii[v] (P), bufs[v]: as for gsr_forward; each view's backward is
- * gsr_backward with bufs[v].  Full-image views only (rs->tile_y0/y1 must cover every view);
+ * gsr_forward; with rs->max_rendered == 0 the V preprocess passes are enqueued back to back and
+ * ONE device->host read returns all V instance counts, so the host waits once per batch
+ * instead of once per view.  cams[v], out_colors[v] (3 x H_v x W_v), radii[v] (P), bufs[v]: as
+ * for gsr_forward; each view's backward is gsr_backward with bufs[v].  Full-image views only;
  * one extra 8*V-byte allocation through alloc_image holds the counts.  0 < V <= GSR_MAX_BATCH. */
 #define GSR_MAX_BATCH 64
 int gsr_forward_batch(int32_t V, const gsr_camera* cams, const gsr_gaussians* gs,
@@ -137,16 +148,15 @@ int gsr_forward_batch(int32_t V, const gsr_camera* cams, const gsr_gaussians* gs
                       void* alloc_ctx, gsr_buffers* bufs, void* stream);
 
 /* Full backward (B1 + gather + B2).  dL_dout_color: 3 x H x W.  scratch: asked for twice
- * through alloc_scratch (gsr_scratch_bytes(K) for per-instance partial gradients, then
+ * through alloc_scratch (gsr_scratch_bytes(capacity) for per-instance partial gradients, then
  * 48 * P bytes for the per-Gaussian screen-space gradient), valid for the duration of the call. */
 int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
                  const gsr_buffers* bufs, const float* dL_dout_color, gsr_alloc_fn alloc_scratch,
                  void* alloc_ctx, const gsr_grads* grads, void* stream);
 
 /* B1 only: per-Gaussian 2D gradients into grad2d (P x GSR_GRAD2D_STRIDE floats:
- * mean2D.x, mean2D.y, conic A, B, C, opacity, r, g, b, 0, 0, 0). Summable across
- * tile bands (all-reduce) before gsr_backward_preprocess.  A band writes zeros for the
- * Gaussians outside its ranking (GSR_VIEW_GID_BY_RANK), or nothing under GSR_FLAG_BAND_ONLY. */
+ * mean2D.x, mean2D.y, conic A, B, C, opacity, r, g, b, 0, 0, 0).  Summable across tile bands
+ * before gsr_backward_preprocess (zeros for Gaussians outside the band). */
 int gsr_backward_blend(const gsr_camera* cam, const gsr_gaussians* gs,
                        const gsr_raster_settings* rs, const gsr_buffers* bufs,
                        const float* dL_dout_color, gsr_alloc_fn alloc_scratch, void* alloc_ctx,
@@ -157,17 +167,57 @@ int gsr_backward_preprocess(const gsr_camera* cam, const gsr_gaussians* gs,
                             const gsr_raster_settings* rs, const gsr_buffers* bufs,
                             const float* grad2d, const gsr_grads* grads, void* stream);
 
-/* B2 on the Gaussian slice [g0, g1) only (multi-GPU: each rank owns a slice after a
- * reduce-scatter of grad2d).  grad2d holds the slice's (g1 - g0) rows, and every output in
- * `grads` is the slice's own array (row g - g0); the inputs in `gs` stay full-size. */
-int gsr_backward_preprocess_range(const gsr_camera* cam, const gsr_gaussians* gs,
-                                  const gsr_raster_settings* rs, const gsr_buffers* bufs,
-                                  int32_t g0, int32_t g1, const float* grad2d,
-                                  const gsr_grads* grads, void* stream);
+/* ---- Multi-GPU: Gaussian shards x tile-row bands (the scaling version) ----
+ * Rank r of N owns the Gaussian shard [g0_r, g1_r) (contiguous, in rank order) and the band
+ * of tile rows [band_rows[r], band_rows[r+1]).  One step:
+ *   1. gsr_shard_forward   F1 on the shard, then every projected Gaussian ("splat", 64 B) is
+ *                          packed into the send block of each band its tile rect overlaps
+ *   2. caller              all-to-all of the send blocks (block b -> rank b)
+ *   3. gsr_band_forward    F2..F6 on the band over the splats received from every shard
+ *   4. caller              all-gather of the band images
+ *   5. gsr_band_backward   B1 + per-splat 2D gradient, written in the received slot layout
+ *   6. caller              all-to-all back (block s -> rank s)
+ *   7. gsr_shard_backward  per Gaussian, the sum of its bands' 2D gradients in band order,
+ *                          then B2 on the shard
+ * Exchange block layout (nblocks blocks of gsr_exchange_block_bytes(pair_cap) each): a 64-B
+ * header whose first u32 is the number of splats the sender packed for that pair (it may
+ * exceed pair_cap: an overflow -- the splats past pair_cap are not sent), then pair_cap
+ * 64-B splats.  The gradient blocks going back are pair_cap x 48 B (no header).  Splats
+ * reach the band in (source rank, shard index) order = ascending global Gaussian id, so the
+ * canonical order and every rendered pixel are those of the single-GPU forward. */
+#define GSR_SPLAT_BYTES 64
+#define GSR_SPLAT_GRAD_BYTES 48
+size_t gsr_exchange_block_bytes(int32_t pair_cap);
+size_t gsr_shard_state_bytes(int32_t P, int32_t nbands, int32_t pair_cap);
+
+/* radii: P (shard rows).  shard_state: gsr_shard_state_bytes, kept until gsr_shard_backward.
+ * send: nbands exchange blocks.  row_hist (nullable, device, zeroed by the caller): += the
+ * instances per tile row of this shard (grid_y u32) -- band balancing for the next step. */
+int gsr_shard_forward(const gsr_camera* cam, const gsr_gaussians* shard, const gsr_raster_settings* rs,
+                      int32_t nbands, const int32_t* band_rows, int32_t pair_cap, void* send,
+                      int32_t* radii, void* shard_state, uint32_t* row_hist, void* stream);
+
+/* recv: nsrc exchange blocks.  rs->tile_y0/y1 = this rank's band; rs->max_rendered > 0 is the
+ * band's instance capacity (no host read).  Writes out_color's band pixels only. */
+int gsr_band_forward(const gsr_camera* cam, const gsr_raster_settings* rs, int32_t nsrc, int32_t pair_cap,
+                     const void* recv, float* out_color, gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_binning,
+                     gsr_alloc_fn alloc_image, void* alloc_ctx, gsr_buffers* bufs, void* stream);
+
+/* grad_send: nsrc x pair_cap x GSR_SPLAT_GRAD_BYTES (the received slot layout; zeros for empty
+ * slots).  dL_dout_color: full image, only the band's pixels are read. */
+int gsr_band_backward(const gsr_camera* cam, const gsr_raster_settings* rs, int32_t nsrc, int32_t pair_cap,
+                      const gsr_buffers* bufs, const float* dL_dout_color, gsr_alloc_fn alloc_scratch,
+                      void* alloc_ctx, void* grad_send, void* stream);
+
+/* grad_recv: nbands x pair_cap x GSR_SPLAT_GRAD_BYTES (what gsr_band_backward wrote for this
+ * shard, one block per band).  band_rows: the forward's.  grads: the shard's rows. */
+int gsr_shard_backward(const gsr_camera* cam, const gsr_gaussians* shard, const gsr_raster_settings* rs,
+                       int32_t nbands, const int32_t* band_rows, int32_t pair_cap, const void* shard_state,
+                       const void* grad_recv, const gsr_grads* grads, void* stream);
 
 /* Introspection for tests / the benchmark (all device pointers into the caller's buffers,
  * or NULL when not applicable).  `what`: see gsr_view_* below. */
-#define GSR_VIEW_RADII_SORTED_GID 1 /* uint32[K]: Gaussian id of sorted instance i       */
+#define GSR_VIEW_SORTED_GID 1       /* uint32[K]: Gaussian id of sorted instance i       */
 #define GSR_VIEW_SORTED_TILE 2      /* uint32[K]: tile id of sorted instance i             */
 #define GSR_VIEW_RANGES 3           /* uint32[2*tiles]: [start,end) per tile               */
 #define GSR_VIEW_FINAL_T 4          /* float[H*W]                                          */
@@ -176,9 +226,8 @@ int gsr_backward_preprocess_range(const gsr_camera* cam, const gsr_gaussians* gs
                                        termination point from T                             */
 #define GSR_VIEW_DEPTH_KEY 6        /* uint32[P]: depth bits, 0xFFFFFFFF when culled       */
 #define GSR_VIEW_TILES_TOUCHED 7    /* uint32[P]                                           */
-#define GSR_VIEW_GID_BY_RANK 9      /* uint32[num_ranked]: the ranked Gaussian ids -- ascending
-                                       (shipped binning; depth order under GSR_BIN_VARIANT=0);
-                                       a band's candidates: exactly the Gaussians it can touch */
+#define GSR_VIEW_COUNTS 9           /* uint32[1]: K, written by the scan (device)          */
+#define GSR_VIEW_TERM 10            /* uint32[tiles]: per-tile termination index (F6)      */
 #define GSR_VIEW_RECORDS 8          /* float4[3*P]: {x,y,a',b'},{c',o,r,g},{b,ext_x,ext_y,log2 o};
                                        a',b',c' = -log2(e) * (A/2, B, C/2) of the conic */
 const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, int what);
@@ -188,10 +237,9 @@ const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, 
  * call's stream; gsr_profile_read synchronises those events and returns the accumulated
  * milliseconds and launch counts per stage (arrays of GSR_NUM_STAGES), then resets. */
 #define GSR_STAGE_PREPROCESS 0     /* F1 */
-#define GSR_STAGE_DEPTH_SORT 1     /* depth order: per-tile depth sort (shipped) or the global
-                                      depth-key LSD sort of the P Gaussians; band compaction */
-#define GSR_STAGE_SCAN 2           /* F2 scan of tiles_touched (rank order) */
-#define GSR_STAGE_DUPLICATE 3      /* F3 */
+#define GSR_STAGE_DEPTH_SORT 1     /* per-tile depth order */
+#define GSR_STAGE_SCAN 2           /* F2 scan of tiles_touched (gid order) */
+#define GSR_STAGE_DUPLICATE 3      /* F3 (with the F2 scan when the two run as one kernel) */
 #define GSR_STAGE_TILE_SORT 4      /* F4 tile-key LSD sort of the K instances */
 #define GSR_STAGE_FINALIZE 5       /* F5 sorted gid + tile ranges */
 #define GSR_STAGE_BLEND_FWD 6      /* F6 */
@@ -199,16 +247,17 @@ const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, 
 #define GSR_STAGE_PREPROCESS_BWD 8 /* B2 */
 #define GSR_STAGE_GATHER 9         /* per-Gaussian grad2d sum of the B1 partials */
 #define GSR_STAGE_MISC 10          /* memsets, background fill, num_rendered read */
-#define GSR_NUM_STAGES 11
+#define GSR_STAGE_EXCHANGE 11      /* multi-GPU splat pack / unpack / gradient sum */
+#define GSR_NUM_STAGES 12
 int gsr_profile_enable(uint32_t stage_mask);
 int gsr_profile_read(double* ms, uint32_t* counts);
 const char* gsr_stage_name(int stage);
 
 /* Byte sizes the allocation callbacks will be asked for (for pre-sizing pools). */
 size_t gsr_geom_bytes(int32_t P);
-size_t gsr_binning_bytes(int32_t K);
+size_t gsr_binning_bytes(int32_t capacity);
 size_t gsr_image_bytes(int32_t width, int32_t height);
-size_t gsr_scratch_bytes(int32_t K);
+size_t gsr_scratch_bytes(int32_t capacity);
 
 #ifdef __cplusplus
 }

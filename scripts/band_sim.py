@@ -1,15 +1,19 @@
 #!/usr/bin/env python3
-"""Single-GPU rehearsal of one rank of the N-GPU band pipeline (no collectives): forward on
-the band, blend-backward, B2 on the rank's Gaussian slice.  Prints per-stage ms and the
-step time, i.e. the per-rank compute an N-GPU run adds to its communication.
-usage: band_sim.py [--world 8] [--rank 3] [--steps 20] [--config 1m_1080p]"""
+"""Single-GPU rehearsal of the N-GPU path (bands.simulate_ranks: every rank's calls in one
+process, collectives replaced by block copies).  For each N it times every rank's compute --
+gsr_shard_forward (F1 + splat pack), gsr_band_forward (unpack + F2..F6), gsr_band_backward
+(B1 + per-splat gather), gsr_shard_backward (gradient sum + B2) -- with HIP events on the
+launch stream, median over --steps runs, and reports the slowest rank's total: the per-step
+compute an N-GPU run adds to its communication.  Also the bytes each rank moves per step
+(splat blocks out, gradient blocks back, its image band), for the xGMI estimate in DESIGN §7.
+usage: band_sim.py [--worlds 1,2,4,8] [--steps 5] [--config 5m_1080p]"""
 import argparse
 import importlib
 import json
 import os
 import sys
-import time
 
+import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -18,56 +22,80 @@ PKG = "3d_gaussian_splatting_amd"
 gr = importlib.import_module(f"{PKG}.graphics")
 sc = importlib.import_module(f"{PKG}.scene")
 R = importlib.import_module(f"{PKG}.rasterizer")
-native = importlib.import_module(f"{PKG}.native")
 bands = importlib.import_module(f"{PKG}.bands")
 bench = importlib.import_module("bench")
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--world", type=int, default=8)
-    ap.add_argument("--rank", type=int, default=3)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="1m_1080p")
+    ap.add_argument("--worlds", default="1,2,4,8")
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--config", default="5m_1080p", choices=sorted(bench.CONFIGS))
     args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
     cfg = bench.CONFIGS[args.config]
     P, W, H, D = cfg["P"], cfg["W"], cfg["H"], cfg["D"]
-    dev = torch.device("cuda", 0)
     cam = gr.synthetic_camera(W, H)
-    scene = sc.make_scene(cam, P, max_sh_degree=max(D, 0), seed=0)
+    s = sc.make_scene(cam, P, max_sh_degree=D, seed=0)
     t = lambda a: torch.tensor(a, device=dev)
-    inputs = dict(means3D=t(scene.means3D), opacities=t(scene.opacities), scales=t(scene.scales),
-                  rotations=t(scene.rotations), sh_dc=t(scene.sh_dc), sh_rest=t(scene.sh_rest))
+    inputs = dict(means3D=t(s.means3D), opacities=t(s.opacities), scales=t(s.scales), rotations=t(s.rotations),
+                  sh_dc=t(s.sh_dc), sh_rest=t(s.sh_rest))
+    del s
     dpix = t(sc.make_dL_dpix(cam, seed=1))
-    rast = R.CAbiRasterizer(dev)
-    gy = cam.grid[1]
-    band = bands.band_rows(gy, args.world, args.rank)
-    g0, g1 = bands.gaussian_slice(P, args.world, args.rank)
+    rast = R.ShardRasterizer(dev)
+    single = R.CAbiRasterizer(dev)
+    # the single-GPU step for reference (same timing method)
+    K0 = single.forward(cam, **inputs, sh_degree=D).num_rendered
+    cap = bands.round_up(int(K0 * 1.1) + 1)
+    ref = []
+    for i in range(args.steps + 2):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        st = single.forward(cam, **inputs, sh_degree=D, max_rendered=cap)
+        single.backward(st, dpix)
+        e1.record()
+        torch.cuda.synchronize()
+        if i >= 2:
+            ref.append(e0.elapsed_time(e1))
+    one_gpu = float(np.median(ref))
+    print(json.dumps({"config": args.config, "world": 1, "path": "single-GPU gsr_forward + gsr_backward",
+                      "ms_per_step": round(one_gpu, 4)}), flush=True)
+    for world in [int(w) for w in args.worlds.split(",")]:
+        plan = None
+        runs = []
+        for i in range(args.steps + 1):
+            times = {}
 
-    def step():
-        st = rast.forward(cam, **inputs, sh_degree=D, tile_rows=band, band_only=True)
-        g2 = rast.backward_blend(st, dpix)
-        return st, rast.backward_preprocess_range(st, g0, g1, g2[g0:g1])
+            def timer(name, r, fn):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                out = fn()
+                e1.record()
+                times.setdefault(r, []).append((name, e0, e1))
+                return out
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    native.profile_enable()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    stages = native.profile_read()
-    native.profile_enable(0)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        st, _ = step()
-    torch.cuda.synchronize()
-    ms = 1e3 * (time.perf_counter() - t0) / args.steps
-    print(json.dumps({"world": args.world, "rank": args.rank, "band_tile_rows": band, "ms_per_step": round(ms, 4),
-                      "candidates": st.buffers.num_ranked, "num_rendered": st.num_rendered,
-                      "stage_ms": {k: round(v / args.steps, 4) for k, (v, n) in stages.items() if n}}))
+            img, g, plan = bands.simulate_ranks(rast, cam, inputs, D, world, dpix, timer=timer,
+                                                rows=None if plan is None else plan["rows"])
+            torch.cuda.synchronize()
+            if i >= 1:
+                runs.append({r: {n: a.elapsed_time(b) for n, a, b in v} for r, v in times.items()})
+        per_rank = {r: {n: float(np.median([run[r][n] for run in runs])) for n in runs[0][r]} for r in runs[0]}
+        totals = {r: sum(v.values()) for r, v in per_rank.items()}
+        slow = max(totals, key=totals.get)
+        pc = plan["pair_cap"]
+        band_px = [(min(plan["rows"][b + 1] * 16, H) - plan["rows"][b] * 16) * W for b in range(world)]
+        print(json.dumps({
+            "config": args.config, "world": world, "rows": plan["rows"], "pair_cap": pc,
+            "band_capacity": plan["capacity"], "band_instances": plan["band_instances"],
+            "splats_per_pair_max": max(int(sh.counts.max()) for sh in plan["shards"]),
+            "rank_ms": {r: round(v, 4) for r, v in totals.items()},
+            "slowest_rank": slow, "slowest_rank_stages_ms": {n: round(v, 4) for n, v in per_rank[slow].items()},
+            "slowest_rank_ms": round(totals[slow], 4), "single_gpu_ms": round(one_gpu, 4),
+            "compute_speedup": round(one_gpu / totals[slow], 3),
+            "bytes_per_rank": {"splats_out": world * (pc + 1) * 64, "grads_back": world * pc * 48,
+                               "image_band": 12 * max(band_px)},
+        }), flush=True)
 
 
 if __name__ == "__main__":

@@ -1,21 +1,28 @@
-"""Multi-rank band sharding on CPU (gloo, world size 2): the exchange code of
-3d_gaussian_splatting_amd/bands.py with the CPU oracle standing in for each rank's renderer
-(test infrastructure; the GPU path runs the same exchange over RCCL in bench.py).
+"""Multi-rank exchange on CPU (gloo, world size 2): the protocol of the multi-GPU path
+(3d_gaussian_splatting_amd/bands.py, DESIGN.md §7, SURVEY §8e scaling version) with the CPU
+oracle standing in for each rank's renderer (test infrastructure; on the GPU box the same
+exchange moves the HIP path's 64-B splats over RCCL in bench.py).
 
-Checks (SURVEY §8e parity rules):
-* the all-gathered band images equal the single-process full render bit for bit;
-* the reduce-scatter of the band-local 2D gradients (mean2D, conic, opacity, colour -- what
-  gsr_backward_blend returns as grad2d) gives each rank its Gaussian slice of the full-image
-  2D gradients (slices re-assembled here to compare), and the leaf gradients after the chain
-  rule (B2 is linear in grad2d) sum to the full-image ones, within 1e-5 relative L2;
-* bands partition the tile rows for every world size up to 8 and uneven heights.
+Each rank owns a Gaussian shard and an instance-balanced band of tile rows:
+* row histogram of its shard's instances -> all_reduce -> ``balance_bands`` (same cuts on every rank);
+* for each band, the shard's Gaussians whose tile rect overlaps it, in shard order, go into
+  that band's fixed-capacity block (header = count) -- the GPU path's block layout, here with
+  the Gaussian's parameters as payload instead of its F1 record -- through
+  ``bands.all_to_all_blocks``;
+* the band owner renders its rows from the received Gaussians (ascending global id), the band
+  images are all-gathered (``ImageGather``, bands padded to the tallest);
+* each received Gaussian's band gradient goes back through ``all_to_all_blocks`` in the received
+  slot layout, and the shard sums them per Gaussian in band order.
+
+Checks (SURVEY §8e parity rules): the gathered image equals the single-process full render bit
+for bit; the summed shard gradients equal the full render's leaf gradients within 1e-5
+relative L2.
 """
 import os
 import socket
 import tempfile
 
 import numpy as np
-import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -23,7 +30,9 @@ import torch.multiprocessing as mp
 from conftest import pkg, rel_l2
 
 WORLD = 2
-W, H = 96, 72  # 6 x 5 tiles: uneven band split for 2 ranks (2 + 3 tile rows)
+W, H = 96, 72  # 6 x 5 tiles
+D = 2
+LEAVES = ("means3D", "opacities", "scales", "rotations", "sh_dc", "sh_rest")
 
 
 def _free_port():
@@ -35,16 +44,34 @@ def _free_port():
 def _scene():
     gr, sc = pkg("graphics"), pkg("scene")
     cam = gr.synthetic_camera(W, H)
-    scene = sc.make_scene(cam, 400, max_sh_degree=2, seed=3)
+    scene = sc.make_scene(cam, 400, max_sh_degree=D, seed=3)
     dpix = sc.make_dL_dpix(cam, seed=4)
     return cam, scene, dpix
 
 
-def _render(cam, scene, dpix, tile_rows=None):
+def _params(scene, idx):
+    """(n, F) f32 rows: the Gaussians' parameters (the stand-in splat payload)."""
+    n = len(idx)
+    return np.concatenate([scene.means3D[idx], scene.opacities[idx].reshape(n, 1), scene.scales[idx],
+                           scene.rotations[idx], scene.sh_dc[idx].reshape(n, -1), scene.sh_rest[idx].reshape(n, -1)],
+                          axis=1).astype(np.float32)
+
+
+def _unparams(rows, M):
+    n = rows.shape[0]
+    return dict(means3D=rows[:, 0:3], opacities=rows[:, 3], scales=rows[:, 4:7], rotations=rows[:, 7:11],
+                sh_dc=rows[:, 11:14].reshape(n, 1, 3), sh_rest=rows[:, 14:].reshape(n, M, 3))
+
+
+def _oracle(cam, p, tile_rows=None):
     import gsr_oracle  # test infrastructure: the per-rank stand-in renderer
-    f = gsr_oracle.forward(cam, scene.means3D, scene.opacities, scene.scales, scene.rotations, scene.sh_dc,
-                           scene.sh_rest, sh_degree=2, tile_rows=tile_rows)
-    return f, f.state.backward(dpix)
+    return gsr_oracle.forward(cam, p["means3D"], p["opacities"], p["scales"], p["rotations"], p["sh_dc"],
+                              p["sh_rest"], sh_degree=D, tile_rows=tile_rows)
+
+
+def _grad_rows(g, n):
+    return np.concatenate([g["means3D"], g["opacities"].reshape(n, 1), g["scales"], g["rotations"],
+                           g["sh_dc"].reshape(n, -1), g["sh_rest"].reshape(n, -1)], axis=1).astype(np.float32)
 
 
 def _worker(rank, port, outdir):
@@ -53,43 +80,76 @@ def _worker(rank, port, outdir):
     try:
         bands = pkg("bands")
         cam, scene, dpix = _scene()
-        gy = (H + 15) // 16
-        band = bands.band_rows(gy, WORLD, rank)
-        f, g = _render(cam, scene, dpix, tile_rows=band)
-        img = bands.ImageGather(torch.from_numpy(f.color), band, gy, dist)
-        P = g["means2D"].shape[0]
-        g2d = np.concatenate([g["means2D"][:, :2], g["conic"], g["opacities"], g["colors"]], axis=1)
-        padded = torch.zeros((bands.padded_rows(P, WORLD), 12))  # GSR_GRAD2D_STRIDE rows
-        padded[:P, :9] = torch.from_numpy(g2d)
-        g0, g1 = bands.gaussian_slice(P, WORLD, rank)
-        mine = bands.reduce_scatter_grad2d(padded.clone(), dist)[: g1 - g0].clone()
-        # sparse form: only the band's candidates (Gaussians with tiles in the band) travel
-        cand = torch.from_numpy(np.nonzero(f.state.preprocess()["tiles_touched"])[0].astype(np.int32))
-        sparse = bands.exchange_grad2d(padded[:P].clone(), cand, P, dist)[: g1 - g0]
-        assert torch.equal(sparse[:, :9], mine[:, :9]) or float((sparse[:, :9] - mine[:, :9]).abs().max()) < 1e-6
-        slices = [torch.zeros_like(padded[: padded.shape[0] // WORLD]) for _ in range(WORLD)]
-        dist.all_gather(slices, torch.nn.functional.pad(mine, (0, 0, 0, slices[0].shape[0] - mine.shape[0])))
-        grad2d = torch.cat(slices)[:P, :9]
+        P, gy = scene.P, cam.grid[1]
+        M = scene.sh_rest.shape[1]
+        g0, g1 = bands.gaussian_shard(P, WORLD, rank)
+        mine = _params(scene, np.arange(g0, g1))
+        shard = _unparams(mine, M)
+        # per-tile-row instance histogram of this shard, summed over ranks -> balanced cuts
+        hist = torch.tensor([int(_oracle(cam, shard, (y, y + 1)).num_rendered) for y in range(gy)], dtype=torch.int64)
+        dist.all_reduce(hist)
+        rows = bands.balance_bands(hist.numpy(), WORLD)
+        band = (rows[rank], rows[rank + 1])
+        # pack: per band the overlapping Gaussians in shard order, fixed-capacity blocks
+        cap = g1 - g0
+        F = mine.shape[1] + 1
+        send = np.zeros((WORLD, 1 + cap, F), np.float32)
+        sent = []
+        for b in range(WORLD):
+            tt = _oracle(cam, shard, (rows[b], rows[b + 1])).state.preprocess()["tiles_touched"]
+            idx = np.nonzero(tt)[0]
+            sent.append(idx)
+            send[b, 0, 0] = len(idx)
+            send[b, 1:1 + len(idx), 0] = (g0 + idx).astype(np.float32)  # global id (exact below 2^24)
+            send[b, 1:1 + len(idx), 1:] = mine[idx]
+        recv = bands.all_to_all_blocks(torch.from_numpy(send).reshape(-1), WORLD, dist).reshape(WORLD, 1 + cap, F)
+        recv = recv.numpy()
+        counts = [int(recv[s, 0, 0]) for s in range(WORLD)]
+        got = np.concatenate([recv[s, 1:1 + counts[s]] for s in range(WORLD)])
+        gid = got[:, 0].astype(np.int64)
+        assert np.all(np.diff(gid) > 0), "splats must reach the band in ascending global id"
+        f = _oracle(cam, _unparams(np.ascontiguousarray(got[:, 1:]), M), band)
+        img = bands.ImageGather(torch.from_numpy(f.color), rows, rank, dist)
+        # backward: the band's gradient of every received Gaussian, back in the received slot layout
+        gb = _grad_rows(f.state.backward(dpix), len(gid))
+        G = gb.shape[1]
+        back = np.zeros((WORLD, cap, G), np.float32)
+        off = 0
+        for s in range(WORLD):
+            back[s, :counts[s]] = gb[off:off + counts[s]]
+            off += counts[s]
+        ret = bands.all_to_all_blocks(torch.from_numpy(back).reshape(-1), WORLD, dist).reshape(WORLD, cap, G).numpy()
+        acc = np.zeros((g1 - g0, G), np.float32)
+        for b in range(WORLD):  # band order: deterministic
+            acc[sent[b]] += ret[b, :len(sent[b])]
         full = img.wait()
-        leaf = {k: torch.from_numpy(g[k].copy()) for k in ("means3D", "scales", "rotations", "sh_dc", "sh_rest",
-                                                          "opacities")}
-        for v in leaf.values():
-            dist.all_reduce(v)
+        parts = [torch.zeros((-(-P // WORLD), G)) for _ in range(WORLD)]
+        pad = torch.zeros((-(-P // WORLD), G))
+        pad[: g1 - g0] = torch.from_numpy(acc)
+        dist.all_gather(parts, pad)
         if rank == 0:
-            np.savez(os.path.join(outdir, "r0.npz"), image=full.numpy(), grad2d=grad2d.numpy(),
-                     **{f"leaf_{k}": v.numpy() for k, v in leaf.items()})
+            grads = torch.cat(parts)[:P].numpy()
+            np.savez(os.path.join(outdir, "r0.npz"), image=full.numpy(), grads=grads, rows=np.array(rows))
     finally:
         dist.destroy_process_group()
 
 
-def test_band_rows_partition():
+def test_band_cuts():
     bands = pkg("bands")
     for gy in (1, 5, 68, 135):
-        for world in range(1, 9):
-            rows = [bands.band_rows(gy, world, r) for r in range(world)]
-            assert rows[0][0] == 0 and rows[-1][1] == gy
-            assert all(rows[i][1] == rows[i + 1][0] for i in range(world - 1))
-            assert bands.max_band_pixel_rows(gy, world) == max(b - a for a, b in rows) * 16
+        for world in range(1, min(gy, 8) + 1):
+            rows = bands.equal_bands(gy, world)
+            assert rows[0] == 0 and rows[-1] == gy and all(b > a for a, b in zip(rows, rows[1:]))
+            rng = np.random.default_rng(gy * 10 + world)
+            for counts in (rng.integers(0, 1000, gy), np.zeros(gy, np.int64), np.r_[np.zeros(gy - 1), [5]]):
+                rows = bands.balance_bands(counts, world)
+                assert rows[0] == 0 and rows[-1] == gy and all(b > a for a, b in zip(rows, rows[1:]))
+    # a skewed histogram: the dense rows end up split across more bands
+    counts = np.r_[np.full(10, 1000), np.full(58, 10)]
+    rows = bands.balance_bands(counts, 4)
+    loads = [counts[a:b].sum() for a, b in zip(rows, rows[1:])]
+    assert max(loads) < 0.5 * counts.sum() and rows[1] < 10
+    assert bands.gaussian_shard(10, 4, 3) == (9, 10) and bands.gaussian_shard(10, 4, 0) == (0, 3)
 
 
 def test_gloo_two_ranks_match_single_process(oracle):
@@ -98,9 +158,11 @@ def test_gloo_two_ranks_match_single_process(oracle):
         mp.start_processes(_worker, args=(port, outdir), nprocs=WORLD, join=True, start_method="spawn")
         got = np.load(os.path.join(outdir, "r0.npz"))
         cam, scene, dpix = _scene()
-        f, g = _render(cam, scene, dpix)
+        full = {k: v for k, v in zip(LEAVES, [scene.means3D, scene.opacities, scene.scales, scene.rotations,
+                                               scene.sh_dc, scene.sh_rest])}
+        f = _oracle(cam, full)
+        g = f.state.backward(dpix)
         np.testing.assert_array_equal(got["image"], f.color)
-        want2d = np.concatenate([g["means2D"][:, :2], g["conic"], g["opacities"], g["colors"]], axis=1)
-        assert rel_l2(got["grad2d"], want2d) < 1e-5
-        for k in ("means3D", "scales", "rotations", "sh_dc", "sh_rest", "opacities"):
-            assert rel_l2(got[f"leaf_{k}"], g[k]) < 1e-5, k
+        want = _grad_rows(g, scene.P)
+        assert rel_l2(got["grads"], want) < 1e-5
+        assert got["rows"][1] not in (0, cam.grid[1])

@@ -62,12 +62,55 @@ def test_library_exports_every_symbol():
 def test_library_loads_and_reports_sizes():
     native = pkg("native")
     L = native.load_hip()
-    assert L.gsr_abi_version() == 1
+    assert L.gsr_abi_version() == native.ABI_VERSION == 2
     assert L.gsr_geom_bytes(1000) > 1000 * 64
     assert L.gsr_binning_bytes(10) >= 10 * 24
     assert L.gsr_image_bytes(1920, 1080) >= 1920 * 1080 * 8
     assert L.gsr_scratch_bytes(100) >= 100 * 9 * 4  # 36-B partial per instance (two arrays, 256-B aligned)
     assert L.gsr_scratch_bytes(1 << 20) == (32 << 20) + (4 << 20)
+    assert L.gsr_exchange_block_bytes(100) == 64 * 101
+    assert L.gsr_shard_state_bytes(1000, 8, 100) > L.gsr_geom_bytes(1000) + 8 * 1000 * 4 + 1000 * 48
+
+
+def _c_sizes():
+    """sizeof / offsetof of the gsr.h structs as the C compiler lays them out."""
+    import tempfile
+    src = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "gsr/gsr.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(gsr_camera), sizeof(gsr_gaussians), sizeof(gsr_raster_settings),
+         sizeof(gsr_grads), sizeof(gsr_buffers), offsetof(gsr_buffers, capacity));
+  printf("%zu %zu\n", offsetof(gsr_raster_settings, max_rendered), offsetof(gsr_buffers, n_local));
+  return 0;
+}
+"""
+    with tempfile.TemporaryDirectory() as d:
+        c, exe = os.path.join(d, "s.c"), os.path.join(d, "s")
+        open(c, "w").write(src)
+        subprocess.run(["gcc", "-std=c99", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
+        return [int(v) for v in subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()]
+
+
+def test_ctypes_structs_match_the_c_layout():
+    """The ctypes mirror (native.py) and the stub INTEGRATION.md hands to FFI callers have the
+    exact sizes and field offsets of include/gsr/gsr.h."""
+    native = pkg("native")
+    sz = _c_sizes()
+    assert [ctypes.sizeof(t) for t in (native.Camera, native.Gaussians, native.Settings, native.Grads,
+                                       native.Buffers)] == sz[:5]
+    assert native.Buffers.capacity.offset == sz[5]
+    assert native.Settings.max_rendered.offset == sz[6] and native.Buffers.n_local.offset == sz[7]
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    stub = re.search(r"```python\n(# ctypes binding stub.*?)```", text, re.S)
+    assert stub, "INTEGRATION.md must carry the ctypes binding stub"
+    ns = {}
+    exec(stub.group(1), ns)
+    for name, mine in (("Camera", native.Camera), ("Gaussians", native.Gaussians), ("Settings", native.Settings),
+                       ("Grads", native.Grads), ("Buffers", native.Buffers)):
+        assert ctypes.sizeof(ns[name]) == ctypes.sizeof(mine), name
+        assert [f[0] for f in ns[name]._fields_] == [f[0] for f in mine._fields_], name
 
 
 def test_validation_rejects_bad_arguments_without_gpu():
@@ -89,12 +132,28 @@ def test_validation_rejects_bad_arguments_without_gpu():
                        native.ALLOC_FN(lambda *_: 0), native.ALLOC_FN(lambda *_: 0), native.ALLOC_FN(lambda *_: 0),
                        None, ctypes.byref(b), None)
     assert rc < 0
+    # multi-GPU entry points validate before touching the device
+    c.width, c.height = 64, 48
+    g.P, g.sh_degree = 0, 0
+    rows = (ctypes.c_int32 * 3)(0, 2, 2)
+    rc = L.gsr_shard_forward(ctypes.byref(c), ctypes.byref(g), ctypes.byref(s), 2, rows, 16, ctypes.c_void_p(256),
+                             None, ctypes.c_void_p(256), None, None)
+    assert rc < 0 and "band_rows" in native.last_error()
+    rc = L.gsr_band_forward(ctypes.byref(c), ctypes.byref(s), 2, 16, ctypes.c_void_p(256), ctypes.c_void_p(256),
+                            native.ALLOC_FN(lambda *_: 0), native.ALLOC_FN(lambda *_: 0), native.ALLOC_FN(lambda *_: 0),
+                            None, ctypes.byref(b), None)
+    assert rc < 0 and "max_rendered" in native.last_error()
+    s.max_rendered = -1
+    rc = L.gsr_forward(ctypes.byref(c), ctypes.byref(g), ctypes.byref(s), ctypes.c_void_p(16), None,
+                       native.ALLOC_FN(lambda *_: 0), native.ALLOC_FN(lambda *_: 0), native.ALLOC_FN(lambda *_: 0),
+                       None, ctypes.byref(b), None)
+    assert rc < 0 and "max_rendered" in native.last_error()
 
 
 def test_torch_extension_loads():
     native = pkg("native")
     ext = native.load_torch_ext()
-    assert ext.abi_version() == 1
+    assert ext.abi_version() == 2
     cam = ext.RasterCamera(16, 16, 0.5, 0.5, [0.0] * 16, [0.0] * 16, [0.0] * 3)
     assert cam.width == 16
 
