@@ -136,6 +136,32 @@ def build_torch_ext(verbose: bool = False, force: bool = False) -> str:
     return out
 
 
+def build_variant(name: str, defines: list, verbose: bool = False) -> str:
+    """An experimental build of libgsr_hip.so with extra -D flags into lib/variants/<name>/ (for
+    A/B timing with `bench.py --lib`; the product library is build_hip's)."""
+    out_dir = os.path.join(LIB, "variants", name)
+    os.makedirs(out_dir, exist_ok=True)
+    so = os.path.join(out_dir, "libgsr_hip.so")
+    hipcc = _hipcc()
+    objs = []
+    for src_name, flags in HIP_SOURCES.items():
+        obj = os.path.join(out_dir, src_name + ".o")
+        lang = ["-x", "hip"] if src_name.endswith(".cpp") else []
+        cmd = [hipcc] + COMMON + flags + ["-D" + d for d in defines] + lang + ["-c", os.path.join(CSRC, src_name),
+                                                                              "-o", obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src_name}:\n{r.stderr}")
+        objs.append(obj)
+    r = subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", so] + objs,
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr}")
+    for o in objs:
+        os.remove(o)
+    return so
+
+
 def build_all(verbose: bool = False, force: bool = False):
     so = build_hip(verbose, force)
     ext = build_torch_ext(verbose, force)

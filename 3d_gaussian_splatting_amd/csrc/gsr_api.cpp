@@ -328,7 +328,8 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
         GSR_STAGE(GSR_STAGE_TILE_SORT, radix_sort(v.kA, v.vA, v.kB, v.vB, v.kA, v.vA, cap, v.K_dev, tile_bits(tiles),
                                                   v.hist, &which, stream),
                   "tile sort");
-        if ((which == 1) != (v.sorted_tile == v.kB)) return fail(-12, "tile sort ended in an unexpected buffer");
+        // pass 1 writes (kB, vB), the next (kA, vA): which == 0 means the result is in (kB, vB)
+        if ((which == 0) != (v.sorted_tile == v.kB)) return fail(-12, "tile sort ended in an unexpected buffer");
         GSR_STAGE(GSR_STAGE_FINALIZE, launch_finalize(v.sorted_tile, cap, v.K_dev, v.ranges, stream), "finalize");
         GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_tile_depth_sort(v.ranges, j.ty0 * j.gx, ntiles, cap, v.depth_key,
                                                                v.sorted_gid, v.ovf, v.counters + kOvfCountSlot, v.ovf2,
@@ -365,7 +366,10 @@ __global__ __launch_bounds__(64) void batch_counts_kernel(CountPtrs p, uint32_t*
 int run_preprocess(const gsr_camera* cam, const gsr_gaussians* gs, int ty0, int ty1, int32_t* radii, const Views& v,
                    hipStream_t stream, bool debug) {
     if (gs->P <= 0) return 0;
-    PreOut po{radii, v.depth_key, v.tiles, v.rec, v.rect, v.flags, v.counters};
+    // SH clamp bits are stored by a full-image F1 only: a band's F1 evaluates the colour of its
+    // own Gaussians alone, and B2 recomputes the bits (stored_flags)
+    const bool full = ty0 == 0 && ty1 == div_up(cam->height, kTile);
+    PreOut po{radii, v.depth_key, v.tiles, v.rec, v.rect, full ? v.flags : nullptr, v.counters};
     GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess(*cam, gauss_in(gs), ty0, ty1, po, stream), "preprocess");
     return 0;
 }
@@ -391,6 +395,13 @@ int blend_backward(const gsr_camera* cam, const gsr_raster_settings* rs, const g
                                                      grad2d, stream),
               "gather grad2d");
     return 0;
+}
+
+// SH clamp bits for B2: stored by a full-image forward, else nullptr (B2 recomputes them)
+const uint32_t* stored_flags(const gsr_camera* cam, const gsr_raster_settings* rs, const uint32_t* flags) {
+    int ty0, ty1;
+    band(cam, rs, &ty0, &ty1);
+    return (ty0 == 0 && ty1 == div_up(cam->height, kTile)) ? flags : nullptr;
 }
 
 int check_grads(const gsr_gaussians* gs, const gsr_grads* g) {
@@ -578,8 +589,9 @@ int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raste
     if (!grad2d) return fail(-2, "allocation failed (grad2d, P=%d)", gs->P);
     if (int e = blend_backward(cam, rs, bufs, dL_dpix, alloc_scratch, ctx, grad2d, stream, debug)) return e;
     const Views v = views(cam, gs->P, bufs);
-    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), 0, gs->P, v.depth_key, v.flags,
-                                                                   grad2d, grad_out(grads), stream),
+    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), 0, gs->P, v.depth_key,
+                                                                   stored_flags(cam, rs, v.flags), grad2d,
+                                                                   grad_out(grads), stream),
               "preprocess backward");
     return 0;
 }
@@ -607,8 +619,8 @@ int gsr_backward_preprocess(const gsr_camera* cam, const gsr_gaussians* gs, cons
     const GeomLayout gl(gs->P);
     GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), 0, gs->P,
                                                                    at<uint32_t>(bufs->geom, gl.depth_key),
-                                                                   at<uint32_t>(bufs->geom, gl.flags), grad2d,
-                                                                   grad_out(grads), stream),
+                                                                   stored_flags(cam, rs, at<uint32_t>(bufs->geom, gl.flags)),
+                                                                   grad2d, grad_out(grads), stream),
               "preprocess backward");
     return 0;
 }

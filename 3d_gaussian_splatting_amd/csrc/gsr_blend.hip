@@ -67,6 +67,34 @@ __device__ __forceinline__ void quad_reduce9(float (&v)[9]) {
     for (int i = 0; i < 9; ++i) asm volatile("" : "+v"(v[i]));
 }
 
+#ifndef GSR_B1_REDUCE
+#define GSR_B1_REDUCE 0
+#endif
+// Wave64 sums of two values folded into one register: lanes 0-31 of the result hold a's pairwise
+// sums (lanes i, i + 32), lanes 32-63 b's (gfx950 v_permlane32_swap).
+__device__ __forceinline__ float fold32(float a, float b) {
+    const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(s[0]) + __uint_as_float(s[1]);
+}
+// The same across 16-lane rows (v_permlane16_swap): rows 0 / 2 of the result sum a's row pairs
+// (0, 1) / (2, 3), rows 1 / 3 b's.
+__device__ __forceinline__ float fold16(float a, float b) {
+    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(s[0]) + __uint_as_float(s[1]);
+}
+// Sum over each 16-lane row, left in every lane of the row (DPP butterflies).
+__device__ __forceinline__ float row_sum16(float x) {
+    x += dpp_f<0xB1>(x);
+    asm volatile("" : "+v"(x));
+    x += dpp_f<0x4E>(x);
+    asm volatile("" : "+v"(x));
+    x += dpp_f<0x141>(x);
+    asm volatile("" : "+v"(x));
+    x += dpp_f<0x140>(x);
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
 struct BlendGeom {
     int W, H, grid_x, ty0, nwg;
     float bg0, bg1, bg2;
@@ -368,6 +396,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
     const float bx0 = (float)(tx * kTile), by0 = (float)(ty * kTile);
     const size_t npix = (size_t)geo.W * geo.H;
     const int row = lane >> 4;
+#if GSR_B1_REDUCE == 1
+    const int slot1 = row == 0 ? 5 : row == 1 ? 4 : row == 2 ? 1 : 6;
+    const int slot2 = row == 0 ? 7 : row == 1 ? 0 : 3;
+#endif
     // R = S . dL/dpix - Sp + T_final bg . dL/dpix: the colour term behind the current record
     float pfy[kPPL], T[kPPL], R[kPPL], dp0[kPPL], dp1[kPPL], dp2[kPPL];
 #pragma unroll
@@ -465,6 +497,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                 }
                 T[p] = ok ? tT : -fabsf(T[p]);
             }
+#if GSR_B1_REDUCE == 1
+            if (__any(any)) {  // EXPERIMENT: full 64-lane sums by permlane folds + DPP, no parking
+                const float A1 = fold32(s0, sy), A2 = fold32(syy, g0), A3 = fold32(g1, g2);
+                const float X1 = A1 * dx, Y1 = X1 * dx;
+                const float Q1 = row_sum16(fold16(A1, A2));    // rows: S0, Syy, Sy, g0
+                const float Q2 = row_sum16(fold16(A3, X1));    // rows: g1, Sx, g2, Sxy
+                const float Q3 = row_sum16(fold16(Y1, 0.0f));  // row 0: Sxx
+                const uint32_t j = (uint32_t)__builtin_amdgcn_readlane((int)jl, k);
+                float* pj = p8f + 8 * (size_t)j;
+                if ((lane & 15) == 0) {
+                    pj[slot1] = Q1;
+                    if (row != 2) pj[slot2] = Q2; else p1[j] = Q2;
+                    if (lane == 0) pj[2] = Q3;
+                }
+            }
+#else
             if (__any(any)) {
                 const float sx = s0 * dx;
                 float v[9] = {sx, sy, sx * dx, sy * dx, syy, s0, g0, g1, g2};
@@ -481,6 +529,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                     parked = 0;
                 }
             }
+#endif
             if ((++visited & 7) == 0) {
                 uint32_t lv = 0;
 #pragma unroll

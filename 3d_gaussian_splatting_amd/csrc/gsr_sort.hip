@@ -443,7 +443,9 @@ __global__ __launch_bounds__(256) void scan_duplicate_kernel(const uint32_t* __r
     if (total_out && tid == 0 && (b + 1) * 256 >= n) *total_out = excl + total;  // the last block: K
     // emission: this wave's instances [excl + pre_w, + wsum[w]) with pre_w = first lane's lex
     const uint32_t wbase = pre;  // = lex of lane 0 of this wave
-    s_start[w][lane] = (valid && nt) ? lex - wbase : 0xFFFFFFFFu;
+    // the owner search needs starts non-decreasing across the wave: a Gaussian without tiles
+    // keeps its (shared) start and never owns an instance; lanes past n sort last
+    s_start[w][lane] = valid ? lex - wbase : 0xFFFFFFFFu;
     s_g[w][lane] = (uint32_t)g;
     s_w[w][lane] = maxx - minx;
     s_x0[w][lane] = minx;

@@ -129,7 +129,13 @@ def main():
                          "densification statistics, fused Adam), SURVEY §8f")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank) or gloo (rehearsal: ranks may share a GPU)")
+    ap.add_argument("--exact-k", action="store_true",
+                    help="size the binning from K every step (one host read per forward) instead of a bound")
+    ap.add_argument("--lib", default=None, help="load this libgsr_hip.so instead of the in-tree one "
+                                                  "(experimental builds: _build.build_variant)")
     args = ap.parse_args()
+    if args.lib:
+        native.HIP_LIB = os.path.abspath(args.lib)
     if args.mode == "train":
         return train_main(args)
     if args.mode == "views":
@@ -170,7 +176,7 @@ def main():
     else:
         rast = R.CAbiRasterizer(dev)
         K0 = rast.forward(cam, **inputs, sh_degree=D).num_rendered  # sizes the binning once
-        cap = bands.round_up(int(K0 * 1.1) + 1)
+        cap = 0 if args.exact_k else bands.round_up(int(K0 * 1.1) + 1)
 
         def step():
             st = rast.forward(cam, **inputs, sh_degree=D, max_rendered=cap)
