@@ -162,9 +162,41 @@ def build_variant(name: str, defines: list, verbose: bool = False) -> str:
     return so
 
 
+def build_dropin(verbose: bool = False, force: bool = False) -> str:
+    """tests/cpp/dropin_main.cpp + csrc/torch/gsr_torch.cpp (-DGSR_NO_PYBIND) into the C++
+    executable lib/gsr_dropin: gsr::render() compiled against the reference's call surface
+    (tests/test_gpu_dropin.py runs it)."""
+    import torch
+    from torch.utils import cpp_extension
+
+    os.makedirs(LIB, exist_ok=True)
+    out = os.path.join(LIB, "gsr_dropin")
+    srcs = [os.path.join(ROOT, "tests", "cpp", "dropin_main.cpp"), os.path.join(CSRC, "torch", "gsr_torch.cpp")]
+    tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    flags = ["-O2", "-std=c++17", "-DGSR_NO_PYBIND", "-D__HIP_PLATFORM_AMD__=1",
+             f"-D_GLIBCXX_USE_CXX11_ABI={int(torch._C._GLIBCXX_USE_CXX11_ABI)}",
+             "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(CSRC, "torch"), "-I/opt/rocm/include"]
+    flags += ["-I" + p for p in cpp_extension.include_paths()]
+    libs = ["-L" + LIB, "-lgsr_hip", "-Wl,-rpath,$ORIGIN", "-L" + tlib, "-Wl,--no-as-needed", "-ltorch_hip",
+            "-lc10_hip", "-Wl,--as-needed", "-ltorch", "-ltorch_cpu", "-lc10", "-Wl,-rpath," + tlib]
+    stamp = _stamp(srcs + _headers() + [os.path.join(CSRC, "torch", "gsr_render.h")], " ".join(flags + libs))
+    stamp_file = out + ".stamp"
+    if not force and os.path.exists(out) and os.path.exists(stamp_file) and open(stamp_file).read() == stamp:
+        return out
+    cxx = shutil.which("g++") or "c++"
+    cmd = [cxx] + flags + srcs + ["-o", out] + libs
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"drop-in executable build failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    with open(stamp_file, "w") as fh:
+        fh.write(stamp)
+    return out
+
+
 def build_all(verbose: bool = False, force: bool = False):
     so = build_hip(verbose, force)
     ext = build_torch_ext(verbose, force)
+    build_dropin(verbose, force)
     return so, ext
 
 

@@ -123,7 +123,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stage-events", action="store_true")
     ap.add_argument("--views", type=int, default=8, help="--mode views: cameras per batch")
-    ap.add_argument("--mode", default="render", choices=("render", "train", "views"),
+    ap.add_argument("--iters", type=int, default=30000, help="--mode loop: training iterations")
+    ap.add_argument("--loop-gt", type=int, default=2_000_000, help="--mode loop: ground-truth Gaussians")
+    ap.add_argument("--loop-init", type=int, default=100_000, help="--mode loop: initial points")
+    ap.add_argument("--loop-size", default="1280x832", help="--mode loop: image size WxH")
+    ap.add_argument("--mode", default="render", choices=("render", "train", "views", "loop"),
                     help="render: the BASELINE metric (rasterizer forward+backward); train: one full "
                          "training iteration (activations, render, L1+D-SSIM loss, backward, "
                          "densification statistics, fused Adam), SURVEY §8f")
@@ -140,6 +144,8 @@ def main():
         return train_main(args)
     if args.mode == "views":
         return views_main(args)
+    if args.mode == "loop":
+        return loop_main(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -452,6 +458,37 @@ def views_main(args):
         "config": {"workload": f"{args.config} x {args.views} views (yaw -10..10 deg), gsr_forward_batch + "
                                f"per-view gsr_backward", "gaussians": P, "width": W, "height": H, "sh_degree": D},
         "single_view_calls_views_per_s": round(s1, 2), "batch_speedup": round(b / s1, 4)}))
+
+
+def loop_main(args):
+    """BASELINE configs[4]: the full training loop (train_loop.train, train_utils.cpp:128-145 order,
+    params.h:50-91 defaults) on a synthetic Mip-NeRF360-scale scene: --views cameras on an orbit,
+    ground truth rendered from a --loop-gt Gaussian cloud, training from a --loop-init point
+    cloud.  value = training iterations/s over the whole run (densification included)."""
+    L = importlib.import_module(f"{PKG}.train_loop")
+    T = importlib.import_module(f"{PKG}.trainer")
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit("--mode loop runs on one GPU")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    W, H = (int(v) for v in args.loop_size.split("x"))
+    t0 = time.perf_counter()
+    scene = L.synthetic_scene(args.loop_gt, args.loop_init, args.views, W, H, seed=0, device=dev)
+    setup_s = time.perf_counter() - t0
+    opt = T.OptimizationParams(iterations=args.iters)
+    res = L.train(scene, opt=opt, max_sh_degree=3, log_every=500, device=dev)
+    print(json.dumps({
+        "metric": "training iterations/s, full train.cpp loop (render + L1/D-SSIM + backward + densification + Adam)",
+        "value": round(res.iters_per_s, 3), "unit": "iters/s", "n_gpus": 1, "steps": res.iterations, "warmup": 0,
+        "ms_per_step": round(1e3 * res.seconds / res.iterations, 4), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"configs[4]: {args.iters} iterations, {args.views} views {W}x{H}, ground truth "
+                               f"{args.loop_gt} Gaussians, init {args.loop_init} points, SH 3",
+                   "width": W, "height": H, "views": args.views},
+        "seconds": round(res.seconds, 2), "setup_seconds": round(setup_s, 2),
+        "final_gaussians": res.final_points, "peak_gaussians": res.peak_points,
+        "gaussians_after_densify": res.num_points[::10] + res.num_points[-1:],
+        "loss_curve": [(i, round(l, 5)) for i, l, _, _ in res.loss][::4] + [(res.loss[-1][0], round(res.loss[-1][1], 5))]}))
 
 
 if __name__ == "__main__":

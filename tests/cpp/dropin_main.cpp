@@ -1,0 +1,244 @@
+// dropin_main.cpp -- gsr::render() compiled against the reference's own call surface and run
+// for one training step: render -> L1 -> backward -> one Adam step per parameter group, the loop
+// body src/utils/train_utils.cpp:128-145 leaves out.  Built by __graft_entry__.build() (g++,
+// libtorch, -DGSR_NO_PYBIND, libgsr_hip.so) into 3d_gaussian_splatting_amd/lib/gsr_dropin and run
+// by tests/test_gpu_dropin.py, which compares every output with the C-ABI path.
+//
+// GaussianModel, PipelineParams and Camera below are stand-ins that reproduce the reference's
+// declarations exactly where render() touches them:
+//   * GaussianModel: CoreParams fields and the public getters of src/scene/gaussian_model.h:9-90,
+//     including get_covariance(int scaling_modifier = 1) and get_xyz() returning a const
+//     reference; activations exp / sigmoid / normalize(dim 1) (gaussian_model.cpp:54-59,
+//     270-304), the covariance from general_utils.cpp:88-99;
+//   * PipelineParams: src/arguments/params.h:93-97;
+//   * Camera: the private members of src/scene/camera.h:7-27 with plain double arrays in place
+//     of cv::Matx33d / cv::Vec3d (OpenCV is absent from this image), the tensors built as
+//     camera.cpp:66-71 builds them, and the one accessor INTEGRATION.md §2 adds.
+// The Adam groups and learning rates are GaussianModel::setup's (gaussian_model.cpp:316-345).
+//
+// usage: gsr_dropin IN.bin OUT.bin   (layouts: tests/test_gpu_dropin.py)
+#include <torch/torch.h>
+
+#include <cmath>
+#include <cstdio>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <vector>
+
+#include "gsr_render.h"
+
+class GaussianModel {
+   public:
+    struct CoreParams {
+        int active_sh_degree_;
+        torch::Tensor xyz_;
+        torch::Tensor features_dc_;
+        torch::Tensor features_rest_;
+        torch::Tensor scaling_;
+        torch::Tensor rotation_;
+        torch::Tensor opacity_;
+        torch::Tensor max_radii2D_;
+        torch::Tensor xyz_gradient_accum_;
+        torch::Tensor denom_;
+        std::map<std::string, std::unique_ptr<torch::optim::Adam>> optimizers_;
+        float spatial_lr_scale_;
+    };
+
+   private:
+    int max_sh_degree_;
+    CoreParams core_params_;
+
+   public:
+    explicit GaussianModel(int sh_degree) : max_sh_degree_(sh_degree) { core_params_.active_sh_degree_ = 0; }
+
+    auto get_core_params() -> CoreParams& { return core_params_; }
+    auto get_core_params() const -> const CoreParams& { return core_params_; }
+
+    auto get_scaling() const -> torch::Tensor { return torch::exp(core_params_.scaling_); }
+    auto get_rotation() const -> torch::Tensor {
+        namespace F = torch::nn::functional;
+        return F::normalize(core_params_.rotation_, F::NormalizeFuncOptions().dim(1).p(2));
+    }
+    auto get_xyz() const -> const torch::Tensor& { return core_params_.xyz_; }
+    auto get_features() const -> torch::Tensor {
+        return torch::cat({core_params_.features_dc_, core_params_.features_rest_}, 1);
+    }
+    auto get_opacity() const -> torch::Tensor { return torch::sigmoid(core_params_.opacity_); }
+    auto get_covariance(int scaling_modifier = 1) const -> torch::Tensor {
+        // R S S^T R^T of the normalised rotation and the modified scales, upper triangle
+        // [xx, xy, xz, yy, yz, zz] (general_utils.cpp:49-62, 73-76, 88-99)
+        auto q = get_rotation();
+        auto r = q.select(1, 0), x = q.select(1, 1), y = q.select(1, 2), z = q.select(1, 3);
+        auto R = torch::stack({1 - 2 * (y * y + z * z), 2 * (x * y - r * z), 2 * (x * z + r * y),
+                               2 * (x * y + r * z), 1 - 2 * (x * x + z * z), 2 * (y * z - r * x),
+                               2 * (x * z - r * y), 2 * (y * z + r * x), 1 - 2 * (x * x + y * y)},
+                              1)
+                     .view({-1, 3, 3});
+        auto L = R * (scaling_modifier * get_scaling()).unsqueeze(1);
+        auto S = torch::bmm(L, L.transpose(1, 2));
+        return torch::stack({S.select(1, 0).select(1, 0), S.select(1, 0).select(1, 1), S.select(1, 0).select(1, 2),
+                             S.select(1, 1).select(1, 1), S.select(1, 1).select(1, 2), S.select(1, 2).select(1, 2)},
+                            1);
+    }
+    auto get_max_sh_degree() const -> int { return max_sh_degree_; }
+};
+
+struct PipelineParams {
+    bool convert_SHs_python_{false};
+    bool compute_cov3D_python_{false};
+    bool debug_{false};
+};
+
+class Camera : public torch::nn::Module {
+   private:
+    int uid_;
+    int colmap_id_;
+    double R_[9];  // cv::Matx33d R_ in the reference
+    double T_[3];  // cv::Vec3d T_
+    double FoVx_;
+    double FoVy_;
+    int image_width_;
+    int image_height_;
+    double zfar_;
+    double znear_;
+    torch::Tensor world_view_transform_;
+    torch::Tensor projection_matrix_;
+    torch::Tensor full_proj_transform_;
+    torch::Tensor camera_center_;
+
+   public:
+    Camera(int uid, int colmap_id, const double* R, const double* T, double FoVx, double FoVy, int width, int height)
+        : uid_(uid), colmap_id_(colmap_id), FoVx_(FoVx), FoVy_(FoVy), image_width_(width), image_height_(height),
+          zfar_(100.0), znear_(0.01) {
+        for (int i = 0; i < 9; ++i) R_[i] = R[i];
+        for (int i = 0; i < 3; ++i) T_[i] = T[i];
+        // get_world2view_2 (graphics_utils.cpp:10-43, translate 0, scale 1): [R^T | t]
+        auto opt = torch::TensorOptions().dtype(torch::kFloat64);
+        auto Rt = torch::zeros({4, 4}, opt);
+        for (int i = 0; i < 3; ++i) {
+            for (int j = 0; j < 3; ++j) Rt[i][j] = R_[3 * j + i];
+            Rt[i][3] = T_[i];
+        }
+        Rt[3][3] = 1.0;
+        auto C2W = torch::inverse(Rt);
+        auto W2C = torch::inverse(C2W);
+        // get_projection_matrix (graphics_utils.cpp:46-72)
+        const double ty = std::tan(FoVy_ / 2), tx = std::tan(FoVx_ / 2);
+        const double top = ty * znear_, bottom = -top, right = tx * znear_, left = -right;
+        auto Pm = torch::zeros({4, 4}, opt);
+        Pm[0][0] = 2.0 * znear_ / (right - left);
+        Pm[1][1] = 2.0 * znear_ / (top - bottom);
+        Pm[0][2] = (right + left) / (right - left);
+        Pm[1][2] = (top + bottom) / (top - bottom);
+        Pm[3][2] = 1.0;
+        Pm[2][2] = zfar_ / (zfar_ - znear_);
+        Pm[2][3] = -(zfar_ * znear_) / (zfar_ - znear_);
+        // camera.cpp:66-71
+        world_view_transform_ = W2C.transpose(0, 1).cuda();
+        projection_matrix_ = Pm.transpose(0, 1).cuda();
+        full_proj_transform_ =
+            world_view_transform_.unsqueeze(0).bmm(projection_matrix_.unsqueeze(0)).squeeze(0);
+        camera_center_ = world_view_transform_.inverse().index({3, torch::indexing::Slice(0, 3)});
+    }
+    // the one accessor the reference's Camera needs
+    gsr::RasterCamera raster_camera() const {
+        return gsr::RasterCamera::from_tensors(image_width_, image_height_, FoVx_, FoVy_, world_view_transform_,
+                                               full_proj_transform_, camera_center_);
+    }
+};
+
+namespace {
+template <class T>
+std::vector<T> read_n(std::ifstream& f, size_t n) {
+    std::vector<T> v(n);
+    f.read(reinterpret_cast<char*>(v.data()), sizeof(T) * n);
+    if (!f) throw std::runtime_error("short input file");
+    return v;
+}
+torch::Tensor to_dev(const std::vector<float>& v, std::vector<int64_t> shape) {
+    return torch::from_blob(const_cast<float*>(v.data()), shape, torch::kFloat32).clone().cuda();
+}
+void write_t(std::ofstream& f, const torch::Tensor& t) {
+    auto c = t.detach().to(torch::kCPU).contiguous();
+    f.write(reinterpret_cast<const char*>(c.data_ptr()), c.numel() * c.element_size());
+}
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc != 3) {
+        std::fprintf(stderr, "usage: %s IN.bin OUT.bin\n", argv[0]);
+        return 2;
+    }
+    try {
+        std::ifstream in(argv[1], std::ios::binary);
+        auto hdr = read_n<int32_t>(in, 8);  // P, W, H, D, M_rest, convert_SHs, compute_cov3D, debug
+        const int P = hdr[0], W = hdr[1], H = hdr[2], D = hdr[3], M = hdr[4];
+        auto cam_d = read_n<double>(in, 14);  // R (9, row-major), T (3), FoVx, FoVy
+        const float smod = read_n<float>(in, 1)[0];
+        auto xyz = read_n<float>(in, (size_t)P * 3), fdc = read_n<float>(in, (size_t)P * 3),
+             frest = read_n<float>(in, (size_t)P * M * 3), opac = read_n<float>(in, (size_t)P),
+             scal = read_n<float>(in, (size_t)P * 3), rot = read_n<float>(in, (size_t)P * 4),
+             target = read_n<float>(in, (size_t)3 * H * W);
+
+        GaussianModel gaussians(3);
+        auto& core = gaussians.get_core_params();
+        core.active_sh_degree_ = D;
+        core.spatial_lr_scale_ = 1.0f;
+        core.xyz_ = to_dev(xyz, {P, 3}).requires_grad_(true);
+        core.features_dc_ = to_dev(fdc, {P, 1, 3}).requires_grad_(true);
+        core.features_rest_ = to_dev(frest, {P, M, 3}).requires_grad_(true);
+        core.opacity_ = to_dev(opac, {P, 1}).requires_grad_(true);
+        core.scaling_ = to_dev(scal, {P, 3}).requires_grad_(true);
+        core.rotation_ = to_dev(rot, {P, 4}).requires_grad_(true);
+        // GaussianModel::setup (gaussian_model.cpp:316-345), OptimizationParams defaults
+        core.optimizers_["xyz"] = std::make_unique<torch::optim::Adam>(
+            std::vector<torch::Tensor>{core.xyz_}, torch::optim::AdamOptions{0.00016 * core.spatial_lr_scale_});
+        core.optimizers_["f_dc"] = std::make_unique<torch::optim::Adam>(std::vector<torch::Tensor>{core.features_dc_},
+                                                                        torch::optim::AdamOptions{0.0025});
+        core.optimizers_["f_rest"] = std::make_unique<torch::optim::Adam>(
+            std::vector<torch::Tensor>{core.features_rest_}, torch::optim::AdamOptions{0.0025 / 20.0});
+        core.optimizers_["opacity"] = std::make_unique<torch::optim::Adam>(std::vector<torch::Tensor>{core.opacity_},
+                                                                           torch::optim::AdamOptions{0.05});
+        core.optimizers_["scaling"] = std::make_unique<torch::optim::Adam>(std::vector<torch::Tensor>{core.scaling_},
+                                                                           torch::optim::AdamOptions{0.005});
+        core.optimizers_["rotation"] = std::make_unique<torch::optim::Adam>(
+            std::vector<torch::Tensor>{core.rotation_}, torch::optim::AdamOptions{0.001});
+
+        PipelineParams pipe;
+        pipe.convert_SHs_python_ = hdr[5] != 0;
+        pipe.compute_cov3D_python_ = hdr[6] != 0;
+        pipe.debug_ = hdr[7] != 0;
+        Camera camera(0, 1, cam_d.data(), cam_d.data() + 9, cam_d[12], cam_d[13], W, H);
+        const gsr::RasterCamera rcam = camera.raster_camera();
+        auto background = torch::zeros({3}, torch::TensorOptions().dtype(torch::kFloat32).device(torch::kCUDA));
+        auto gt = to_dev(target, {3, H, W});
+
+        // the loop body train_utils.cpp:137-144 would hold
+        auto out = gsr::render(rcam, gaussians, pipe, background, smod);
+        auto loss = torch::abs(out.render - gt).mean();
+        loss.backward();
+        std::ofstream o(argv[2], std::ios::binary);
+        write_t(o, out.render);
+        write_t(o, out.radii);
+        write_t(o, out.viewspace_points.grad());
+        for (auto* t : {&core.xyz_, &core.features_dc_, &core.features_rest_, &core.opacity_, &core.scaling_,
+                        &core.rotation_})
+            write_t(o, t->grad());
+        for (auto& kv : core.optimizers_) {
+            kv.second->step();
+            kv.second->zero_grad();
+        }
+        for (auto* t : {&core.xyz_, &core.features_dc_, &core.features_rest_, &core.opacity_, &core.scaling_,
+                        &core.rotation_})
+            write_t(o, *t);
+        write_t(o, loss.reshape({1}));
+        torch::cuda::synchronize();
+        std::printf("gsr_dropin ok: P=%d %dx%d loss=%.6f\n", P, W, H, loss.item<float>());
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "gsr_dropin failed: %s\n", e.what());
+        return 1;
+    }
+    return 0;
+}

@@ -1,0 +1,122 @@
+"""GPU: the C++ drop-in (lib/gsr_dropin, built from tests/cpp/dropin_main.cpp + gsr_torch.cpp with
+-DGSR_NO_PYBIND) -- gsr::render<GaussianModel, PipelineParams>() compiled against the
+reference's exact getter / PipelineParams / Camera surface -- runs one render -> L1 -> backward
+-> Adam step, and every output equals the same step through the C ABI (CAbiRasterizer) with
+torch autograd for the activations and torch.optim.Adam for the update.
+
+Cases: the default pipeline; compute_cov3D_python with an integral modifier (the reference's
+get_covariance(int) path); compute_cov3D_python with modifier 0.8 (must NOT be truncated to 0
+by get_covariance(int): render() applies it in-kernel instead); convert_SHs_python."""
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT, pkg
+
+pytestmark = pytest.mark.gpu
+EXE = os.path.join(ROOT, "3d_gaussian_splatting_amd", "lib", "gsr_dropin")
+LRS = {"xyz": 0.00016, "f_dc": 0.0025, "f_rest": 0.0025 / 20.0, "opacity": 0.05, "scaling": 0.005, "rotation": 0.001}
+
+
+def _inputs(P=3000, W=160, H=120, D=3, seed=5):
+    gr, sc = pkg("graphics"), pkg("scene")
+    cam = gr.synthetic_camera(W, H)
+    s = sc.make_scene(cam, P, max_sh_degree=3, seed=seed)
+    target = (sc.make_dL_dpix(cam, seed=seed + 1) * 0.5 + 0.5).astype(np.float32)
+    return cam, s, target
+
+
+def _run_exe(cam, s, target, D, flags, smod):
+    import math
+    P, M = s.P, s.sh_rest.shape[1]
+    fovx = 2 * math.atan(cam.tanfovx)
+    fovy = 2 * math.atan(cam.tanfovy)
+    with tempfile.TemporaryDirectory() as d:
+        fin, fout = os.path.join(d, "in.bin"), os.path.join(d, "out.bin")
+        with open(fin, "wb") as fh:
+            fh.write(np.array([P, cam.width, cam.height, D, M, *flags], np.int32).tobytes())
+            fh.write(np.concatenate([np.eye(3).ravel(), np.zeros(3), [fovx, fovy]]).astype(np.float64).tobytes())
+            fh.write(np.array([smod], np.float32).tobytes())
+            for a in (s.means3D, s.sh_dc, s.sh_rest, s.raw_opacities, s.raw_scales, s.raw_rotations, target):
+                fh.write(np.ascontiguousarray(a, np.float32).tobytes())
+        r = subprocess.run([EXE, fin, fout], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stdout + r.stderr
+        raw = open(fout, "rb").read()
+    H, W = cam.height, cam.width
+    sizes = [("render", 3 * H * W, np.float32), ("radii", P, np.int32), ("means2D", 3 * P, np.float32),
+             ("g_xyz", 3 * P, np.float32), ("g_f_dc", 3 * P, np.float32), ("g_f_rest", 3 * M * P, np.float32),
+             ("g_opacity", P, np.float32), ("g_scaling", 3 * P, np.float32), ("g_rotation", 4 * P, np.float32),
+             ("xyz", 3 * P, np.float32), ("f_dc", 3 * P, np.float32), ("f_rest", 3 * M * P, np.float32),
+             ("opacity", P, np.float32), ("scaling", 3 * P, np.float32), ("rotation", 4 * P, np.float32),
+             ("loss", 1, np.float32)]
+    out, off = {}, 0
+    for name, n, dt in sizes:
+        out[name] = np.frombuffer(raw, dt, n, off)
+        off += n * np.dtype(dt).itemsize
+    assert off == len(raw)
+    return out
+
+
+def _reference_step(cam, s, target, D, flags, smod):
+    """The same step through the C ABI + torch autograd + torch.optim.Adam (reference path)."""
+    R, general = pkg("rasterizer"), pkg("general")
+    dev = torch.device("cuda", 0)
+    leaf = lambda a, shape: torch.tensor(np.asarray(a, np.float32).reshape(shape), device=dev, requires_grad=True)
+    P, M = s.P, s.sh_rest.shape[1]
+    p = {"xyz": leaf(s.means3D, (P, 3)), "f_dc": leaf(s.sh_dc, (P, 1, 3)), "f_rest": leaf(s.sh_rest, (P, M, 3)),
+         "opacity": leaf(s.raw_opacities, (P, 1)), "scaling": leaf(s.raw_scales, (P, 3)),
+         "rotation": leaf(s.raw_rotations, (P, 4))}
+    sc = torch.exp(p["scaling"])
+    q = torch.nn.functional.normalize(p["rotation"], dim=1)
+    o = torch.sigmoid(p["opacity"])
+    convert, cov_py = flags[0], flags[1]
+    kw = dict(sh_degree=D)
+    if cov_py and smod == round(smod):
+        kw["cov3D_precomp"] = general.build_covariance_from_scaling_rotation(sc, smod, q)
+    else:
+        kw.update(scales=sc, rotations=q, scale_modifier=smod)
+    if convert:
+        dirs = p["xyz"] - torch.tensor(cam.campos, device=dev)
+        dirs = dirs / dirs.norm(dim=1, keepdim=True)
+        feats = torch.cat([p["f_dc"], p["f_rest"]], 1)
+        kw["colors_precomp"] = torch.clamp_min(general.eval_sh(D, feats, dirs) + 0.5, 0.0)
+        kw["sh_degree"] = 0
+    else:
+        kw.update(sh_dc=p["f_dc"], sh_rest=p["f_rest"])
+    means2D = torch.zeros_like(p["xyz"], requires_grad=True)
+    color, radii = R.rasterize_gaussians(cam, p["xyz"], means2D, o, **kw)
+    gt = torch.tensor(target, device=dev)
+    loss = torch.abs(color - gt).mean()
+    loss.backward()
+    grads = {k: v.grad.clone() for k, v in p.items()}
+    opts = [torch.optim.Adam([p[k]], lr=LRS[k]) for k in p]
+    for opt in opts:
+        opt.step()
+    return color.detach(), radii, means2D.grad, grads, {k: v.detach() for k, v in p.items()}, float(loss)
+
+
+@pytest.mark.parametrize("flags,smod", [((0, 0, 0), 1.0), ((0, 1, 0), 1.0), ((0, 1, 0), 0.8), ((1, 0, 0), 1.0)],
+                         ids=["default", "cov3D_python", "cov3D_python_mod0.8", "convert_SHs_python"])
+def test_cpp_dropin_step_matches_cabi(flags, smod):
+    assert os.path.exists(EXE), "run __graft_entry__.build()"
+    cam, s, target = _inputs()
+    D = 3
+    out = _run_exe(cam, s, target, D, flags, smod)
+    color, radii, m2d, grads, params, loss = _reference_step(cam, s, target, D, flags, smod)
+    n = lambda t: t.detach().cpu().numpy().ravel()
+    np.testing.assert_allclose(out["render"], n(color), rtol=0, atol=1e-6)
+    np.testing.assert_array_equal(out["radii"], n(radii))
+    assert abs(out["loss"][0] - loss) <= 1e-6 * max(abs(loss), 1.0)
+    rel = lambda a, b: float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+    assert rel(out["means2D"], n(m2d)) <= 1e-5
+    for k in grads:
+        assert rel(out["g_" + k], n(grads[k])) <= 1e-5, k
+        assert rel(out[k], n(params[k])) <= 1e-6, k
+    if flags[1] and smod != round(smod):
+        # a truncated modifier (get_covariance(int(0.8)) = zero covariances) would have culled
+        # every Gaussian: the render must show them
+        assert int((out["radii"] > 0).sum()) > 0.5 * s.P
