@@ -177,8 +177,16 @@ def build_dropin(verbose: bool = False, force: bool = False) -> str:
              f"-D_GLIBCXX_USE_CXX11_ABI={int(torch._C._GLIBCXX_USE_CXX11_ABI)}",
              "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(CSRC, "torch"), "-I/opt/rocm/include"]
     flags += ["-I" + p for p in cpp_extension.include_paths()]
-    libs = ["-L" + LIB, "-lgsr_hip", "-Wl,-rpath,$ORIGIN", "-L" + tlib, "-Wl,--no-as-needed", "-ltorch_hip",
-            "-lc10_hip", "-Wl,--as-needed", "-ltorch", "-ltorch_cpu", "-lc10", "-Wl,-rpath," + tlib]
+    # One HIP runtime per process: the torch wheel bundles its own libamdhip64 (soname
+    # libamdhip64.so.7, file libamdhip64.so) and libtorch_hip names it by file name, while
+    # libgsr_hip.so asks for libamdhip64.so.7.  The loader resolves dependencies breadth-first
+    # in NEEDED order, so libtorch_hip goes ahead of libgsr_hip: the wheel's runtime is loaded
+    # first and libgsr_hip's request is then satisfied by soname with that same copy.  With
+    # libgsr_hip first, /opt/rocm's runtime is loaded as a second one (two HIP and HSA runtimes,
+    # torch's streams handed to the other, a double free at exit).
+    libs = ["-L" + tlib, "-Wl,--no-as-needed", "-ltorch_hip", "-lc10_hip",
+            "-Wl,--as-needed", "-ltorch", "-ltorch_cpu", "-lc10", "-L" + LIB, "-lgsr_hip",
+            "-Wl,-rpath," + tlib, "-Wl,-rpath,$ORIGIN"]
     stamp = _stamp(srcs + _headers() + [os.path.join(CSRC, "torch", "gsr_render.h")], " ".join(flags + libs))
     stamp_file = out + ".stamp"
     if not force and os.path.exists(out) and os.path.exists(stamp_file) and open(stamp_file).read() == stamp:

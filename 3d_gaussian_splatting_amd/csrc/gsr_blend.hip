@@ -67,34 +67,6 @@ __device__ __forceinline__ void quad_reduce9(float (&v)[9]) {
     for (int i = 0; i < 9; ++i) asm volatile("" : "+v"(v[i]));
 }
 
-#ifndef GSR_B1_REDUCE
-#define GSR_B1_REDUCE 0
-#endif
-// Wave64 sums of two values folded into one register: lanes 0-31 of the result hold a's pairwise
-// sums (lanes i, i + 32), lanes 32-63 b's (gfx950 v_permlane32_swap).
-__device__ __forceinline__ float fold32(float a, float b) {
-    const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
-    return __uint_as_float(s[0]) + __uint_as_float(s[1]);
-}
-// The same across 16-lane rows (v_permlane16_swap): rows 0 / 2 of the result sum a's row pairs
-// (0, 1) / (2, 3), rows 1 / 3 b's.
-__device__ __forceinline__ float fold16(float a, float b) {
-    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
-    return __uint_as_float(s[0]) + __uint_as_float(s[1]);
-}
-// Sum over each 16-lane row, left in every lane of the row (DPP butterflies).
-__device__ __forceinline__ float row_sum16(float x) {
-    x += dpp_f<0xB1>(x);
-    asm volatile("" : "+v"(x));
-    x += dpp_f<0x4E>(x);
-    asm volatile("" : "+v"(x));
-    x += dpp_f<0x141>(x);
-    asm volatile("" : "+v"(x));
-    x += dpp_f<0x140>(x);
-    asm volatile("" : "+v"(x));
-    return x;
-}
-
 struct BlendGeom {
     int W, H, grid_x, ty0, nwg;
     float bg0, bg1, bg2;
@@ -165,13 +137,16 @@ __device__ __forceinline__ float pair_alpha_keep(float e, float L, float& oG, bo
     return keep ? __builtin_amdgcn_fmed3f(oG, 0.0f, 0.99f) : 0.0f;
 }
 
-// Chunk length of a tile's list when B1 is chunked: at most kMaxChunks chunks of whole
-// 64-record sub-batches (F6 checkpoints at 64-record boundaries).  Most of a tile's B1 work
-// is in its front records (pixels terminate), so chunks stay short to split that front.
-__device__ __forceinline__ int chunk_len(int n) {
-    const int c = (n + kMaxChunks - 1) / kMaxChunks;
-    return ((c + 63) / 64) * 64;
-}
+// B1 chunk size in (record, stripe) pairs it will visit (see kMaxChunks).  One pair is one
+// 64-lane evaluation in B1; a tile's front 48 records with four live stripes are 192.  Measured
+// at 1M / 1080p (B1 ms, F6 WRITE_SIZE MB incl. 58 MB of image): 128: 0.467, 187; 192: 0.466,
+// 175; 256: 0.473, 141; 384: 0.481, ~115; 512: 0.501, 100; 768: 0.526, 87.  F6's time does not
+// move with its checkpoint writes (0.253-0.259 ms across the range: they overlap the blend),
+// B1's does, so the bound is set for B1.  At 5M / 1080p: 128: 0.488, 256: 0.492, 512: 0.524.
+#ifndef GSR_CHUNK_WORK
+#define GSR_CHUNK_WORK 192
+#endif
+constexpr int kChunkWork = GSR_CHUNK_WORK;
 
 // F6.  T > 0: pixel live; T <= 0: done, |T| = final transmittance (the T after the last
 // contributor -- the reference's final_T).  A pair is blended when the next transmittance
@@ -192,6 +167,7 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
     constexpr int BATCH = 64 * NW;
     __shared__ float4 srec[BATCH * 3];
     __shared__ uint32_t smk[BATCH];
+    __shared__ uint32_t slive[NW];
     const int tl = xcd_tile(blockIdx.x, geo.nwg);  // band-local tile index
     const int tile = tl + geo.ty0 * geo.grid_x;
     const int tx = tile % geo.grid_x, ty = tile / geo.grid_x;
@@ -209,9 +185,14 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
     }
     const uint2 range = ranges[tile];
     const int n = (int)(range.y - range.x);
-    // B1 chunk checkpoints: (T, colour sum) of every pixel before records CH, 2 CH, ...
-    const int CH = chunk_len(n);
-    int nck = 0;  // checkpoints written
+    // B1 chunk checkpoints: (T, colour sum) of every pixel where a chunk starts.  `work` counts
+    // the (record, stripe) pairs of the current chunk: a record's stripe mask against the stripes
+    // live (anywhere in the tile) at the start of its batch -- block-uniform, so every wave takes
+    // the same chunk decisions, including a wave whose own pixels have all finished (it keeps
+    // writing its final state at the later checkpoints).
+    uint32_t* const table = term + (size_t)tl * kMaxChunks;  // [term, chunk 1..7 starts]
+    int nck = 0;   // checkpoints written
+    int work = 0;  // pairs in the current chunk
     int tend = n;  // termination index: every pixel of the tile has finished before record tend
     auto checkpoint = [&](int c) {
         float4* dst = ck + ((size_t)tl * (kMaxChunks - 1) + c) * 256;
@@ -222,6 +203,7 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
         uint32_t live = 0;
 #pragma unroll
         for (int p = 0; p < PPL; ++p) live |= __any(T[p] > 0.0f) ? (1u << p) : 0u;
+        if (lane == 0) slive[w] = live << (w * PPL);
         if (__syncthreads_or(live != 0) == 0) {
             tend = base;
             break;
@@ -238,11 +220,24 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
             smk[tid] = 0u;
         }
         __syncthreads();
+        uint32_t tile_live = 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) tile_live |= slive[i];
         const int cnt = (n - base) < BATCH ? (n - base) : BATCH;
         int visited = 0;
-        for (int c0 = 0; c0 < cnt && live; c0 += 64) {
-            if (base + c0 > 0 && (base + c0) % CH == 0) checkpoint(nck++);  // state before record base + c0
-            const uint32_t mine = (smk[c0 + lane] >> (w * PPL)) & ((1u << PPL) - 1u);
+        for (int c0 = 0; c0 < cnt; c0 += 64) {
+            const uint32_t sm = smk[c0 + lane];  // 0 past cnt
+            if (work >= kChunkWork && nck < kMaxChunks - 1) {  // chunk nck + 1 starts at base + c0
+                checkpoint(nck);
+                ++nck;
+                if (tid == 0) table[nck] = (uint32_t)(base + c0);
+                work = 0;
+            }
+            const uint32_t tm = sm & tile_live;
+            work += __popcll(__ballot(tm & 1u)) + __popcll(__ballot(tm & 2u)) + __popcll(__ballot(tm & 4u)) +
+                    __popcll(__ballot(tm & 8u));
+            if (!live) continue;
+            const uint32_t mine = (sm >> (w * PPL)) & ((1u << PPL) - 1u);
             uint64_t todo = __ballot((mine & live) != 0u && c0 + lane < cnt);
             while (todo) {
                 const int kk = __builtin_ctzll(todo);
@@ -286,11 +281,10 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
         }
         __syncthreads();
     }
-    // The list ended or every pixel finished: the remaining chunks that start before the
-    // termination index begin from the final state (a wave whose own pixels finished early stops
-    // writing checkpoints in the loop); chunks from tend on are skipped by B1 (term[]).
-    for (; nck * CH + CH < tend && nck < kMaxChunks - 1; ++nck) checkpoint(nck);
-    if (threadIdx.x == 0) term[tile] = (uint32_t)tend;
+    if (tid == 0) {
+        table[0] = (uint32_t)tend;
+        for (int c = nck + 1; c < kMaxChunks; ++c) table[c] = 0xFFFFFFFFu;
+    }
     const size_t npix = (size_t)geo.W * geo.H;
 #pragma unroll
     for (int p = 0; p < PPL; ++p) {
@@ -350,9 +344,10 @@ __device__ __forceinline__ void park_flush(const float* qpark, const uint32_t* q
 // B1 stores the raw tile sums (Sx, Sy, Sxx, Sxy, Syy, S0, colour x3); they are linear in the
 // gradients, so gather_grad2d converts them once per Gaussian after summing over tiles.
 //
-// Grid: one 64-lane block per (tile, chunk); a chunk resumes from F6's checkpoint, and chunks
-// from the tile's termination index on exit at once.  Each XCD (blocks b with equal b % 8) takes a contiguous tile range as in xcd_tile,
-// visited chunk-major, so every tile's front chunk -- the longest -- is dispatched first.
+// Grid: one 64-lane block per (tile, chunk slot); chunk c > 0 starts where F6's chunk table
+// says and resumes from F6's checkpoint, and slots the tile has no chunk for exit at once.  Each
+// XCD (blocks b with equal b % 8) takes a contiguous tile range as in xcd_tile, visited
+// chunk-major, so every tile's first chunk is dispatched first.
 // 6 waves per SIMD: 80 VGPRs (no spills) and 6.2 KB of LDS per one-wave block.  Measured
 // 0.552 ms vs 0.564 at the compiler's own 85 VGPRs (5 waves); 7 and 8 waves spill.
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void blend_backward_kernel(const BlendGeom geo,
@@ -385,21 +380,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
     const int tile = tl + geo.ty0 * geo.grid_x;
     const uint2 range = ranges[tile];
     const int n_all = (int)(range.y - range.x);
-    const int CH = chunk_len(n_all);
-    const int start = chunk * CH;
-    // no such chunk for this tile, or every pixel had finished before it (F6's term[])
-    if (start >= n_all || start >= (int)term[tile]) return;
-    const int n = start + CH < n_all ? start + CH : n_all;
+    // F6's chunk table: [termination index, chunk 1..7 starts (UINT32_MAX: none)]
+    const uint32_t* table = term + (size_t)tl * kMaxChunks;
+    const uint32_t tend = table[0];
+    const uint32_t start_u = chunk == 0 ? 0u : table[chunk];
+    // no such chunk for this tile, or every pixel had finished before it
+    if (start_u >= (uint32_t)n_all || start_u >= tend) return;
+    const int start = (int)start_u;
+    const uint32_t next = chunk + 1 < kMaxChunks ? table[chunk + 1] : 0xFFFFFFFFu;
+    const int n = next < (uint32_t)n_all ? (int)next : n_all;
     const int tx = tile % geo.grid_x, ty = tile / geo.grid_x;
     const int px = tx * kTile + (lane & 15);
     const float pfx = (float)px;
     const float bx0 = (float)(tx * kTile), by0 = (float)(ty * kTile);
     const size_t npix = (size_t)geo.W * geo.H;
     const int row = lane >> 4;
-#if GSR_B1_REDUCE == 1
-    const int slot1 = row == 0 ? 5 : row == 1 ? 4 : row == 2 ? 1 : 6;
-    const int slot2 = row == 0 ? 7 : row == 1 ? 0 : 3;
-#endif
     // R = S . dL/dpix - Sp + T_final bg . dL/dpix: the colour term behind the current record
     float pfy[kPPL], T[kPPL], R[kPPL], dp0[kPPL], dp1[kPPL], dp2[kPPL];
 #pragma unroll
@@ -497,22 +492,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                 }
                 T[p] = ok ? tT : -fabsf(T[p]);
             }
-#if GSR_B1_REDUCE == 1
-            if (__any(any)) {  // EXPERIMENT: full 64-lane sums by permlane folds + DPP, no parking
-                const float A1 = fold32(s0, sy), A2 = fold32(syy, g0), A3 = fold32(g1, g2);
-                const float X1 = A1 * dx, Y1 = X1 * dx;
-                const float Q1 = row_sum16(fold16(A1, A2));    // rows: S0, Syy, Sy, g0
-                const float Q2 = row_sum16(fold16(A3, X1));    // rows: g1, Sx, g2, Sxy
-                const float Q3 = row_sum16(fold16(Y1, 0.0f));  // row 0: Sxx
-                const uint32_t j = (uint32_t)__builtin_amdgcn_readlane((int)jl, k);
-                float* pj = p8f + 8 * (size_t)j;
-                if ((lane & 15) == 0) {
-                    pj[slot1] = Q1;
-                    if (row != 2) pj[slot2] = Q2; else p1[j] = Q2;
-                    if (lane == 0) pj[2] = Q3;
-                }
-            }
-#else
             if (__any(any)) {
                 const float sx = s0 * dx;
                 float v[9] = {sx, sy, sx * dx, sy * dx, syy, s0, g0, g1, g2};
@@ -529,7 +508,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                     parked = 0;
                 }
             }
-#endif
             if ((++visited & 7) == 0) {
                 uint32_t lv = 0;
 #pragma unroll

@@ -69,9 +69,12 @@ struct BinLayout {
 
 // Chunked B1: F6 checkpoints every pixel's (T, colour sum) at up to kMaxChunks - 1 points of each
 // tile's list, so B1 sweeps the chunks of one tile in parallel blocks (a shorter tail; essential
-// for multi-GPU bands, which hold 1/N of the tiles).  A checkpoint is written only for a chunk
-// that starts before the tile's termination index (the first 64-record boundary at which every
-// pixel of the tile has finished, term[]); B1 skips the chunks past it without reading anything.
+// for multi-GPU bands, which hold 1/N of the tiles).  The points are chosen by B1's own cost:
+// F6 counts the (record, stripe) pairs B1 will visit -- a record's stripe mask against the
+// stripes still live -- and starts a new chunk at the first 64-record boundary where the
+// current chunk holds kChunkWork of them.  Chunks are therefore balanced in work whatever the
+// list length, no checkpoint is written past the tile's termination (every pixel finished),
+// and the per-tile chunk table (term[]) tells B1 where each chunk starts.
 constexpr int kMaxChunks = 8;
 
 struct ImgLayout {
@@ -87,7 +90,7 @@ struct ImgLayout {
                                                       // memset clears both
         ovf = take(4 * tiles);   // tiles the per-tile depth sort hands to its larger
         ovf2 = take(4 * tiles);  // forms (two queues: LDS, then global memory)
-        term = take(4 * tiles);  // F6: per-tile termination index (see kMaxChunks)
+        term = take(4 * tiles * kMaxChunks);  // F6: per tile [termination index, chunk 1..7 starts]
         final_T = take(4 * (pix ? pix : 1));
         accum = take(12 * (pix ? pix : 1));  // colour sum without background, 3 x H x W
         ck = take(tiles * (kMaxChunks - 1) * 256 * 16);  // float4 (T, C) checkpoints

@@ -85,6 +85,16 @@ class ForwardState:
                     return t, ptr - base
         raise KeyError("pointer not inside a forward buffer")
 
+    def k_device(self) -> torch.Tensor:
+        """K as a 1-element int32 device tensor aliasing the scan's counter (no copy, no sync)."""
+        L = native.load_hip()
+        c = native.camera_struct(self.cam)
+        p = L.gsr_view(ctypes.byref(c), self.gauss.P, ctypes.byref(self.buffers), native.VIEW_COUNTS)
+        if not p:
+            raise RuntimeError("gsr_view(COUNTS) returned NULL")
+        t, off = self._owner(p)
+        return t[off:off + 4].view(torch.int32)
+
     def view(self, what: int, dtype: torch.dtype, count: int) -> torch.Tensor:
         """Copy of an internal array (gsr_view) as a torch tensor."""
         L = native.load_hip()

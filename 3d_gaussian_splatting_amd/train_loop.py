@@ -20,6 +20,7 @@ noisy sample of the ground-truth centres and colours (the upstream create_from_p
 from __future__ import annotations
 
 import math
+import sys
 import time
 from dataclasses import dataclass, field
 
@@ -137,12 +138,16 @@ class LoopResult:
     loss: list = field(default_factory=list)        # (iteration, loss, l1, ssim) at the log points
     final_points: int = 0
     peak_points: int = 0
+    binning_overflows: int = 0   # bounded renders whose K exceeded the bound (must stay 0)
+    exact_k_reads: int = 0       # renders sized by a host read of K (after each point-set change)
 
 
 def train(scene: LoopScene, iterations: int | None = None, opt: OptimizationParams | None = None,
-          max_sh_degree: int = 3, seed: int = 0, log_every: int = 100, device="cuda") -> LoopResult:
+          max_sh_degree: int = 3, seed: int = 0, log_every: int = 100, device="cuda",
+          progress_every: int = 0) -> LoopResult:
     """train_utils.cpp:128-145 over `scene` (GaussianTrainer.from_point_cloud = create_from_pcd,
-    spatial_lr_scale = the camera extent)."""
+    spatial_lr_scale = the camera extent).  progress_every > 0 prints a line to stderr every
+    that many iterations (no device sync)."""
     opt = opt or OptimizationParams()
     iterations = iterations or opt.iterations
     tr = GaussianTrainer.from_point_cloud(scene.points, scene.colors, max_sh_degree, spatial_lr_scale=scene.extent,
@@ -163,10 +168,16 @@ def train(scene: LoopScene, iterations: int | None = None, opt: OptimizationPara
         if it < opt.densify_until_iter and it > opt.densify_from_iter and it % opt.densification_interval == 0:
             res.num_points.append((it, tr.num_points))
         res.peak_points = max(res.peak_points, tr.num_points)
+        if progress_every and it % progress_every == 0:
+            print(f"[loop] iteration {it} points {tr.num_points} {time.perf_counter() - t0:.1f} s", file=sys.stderr,
+                  flush=True)
     torch.cuda.synchronize()
     res.seconds = time.perf_counter() - t0
     res.iters_per_s = iterations / res.seconds
     res.final_points = tr.num_points
+    tr.binning.poll()
+    res.binning_overflows = tr.binning.overflows
+    res.exact_k_reads = tr.binning.exact_reads
     res.loss = [(it, *[float(x) for x in s.cpu().tolist()]) for it, s in logged]
     res.trainer = tr
     return res

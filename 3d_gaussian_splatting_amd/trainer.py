@@ -27,7 +27,10 @@ Device work per iteration, all through the C ABI: gsr_activate -> gsr_forward ->
 forward/backward -> gsr_backward -> gsr_densify_stats -> gsr_adam_step (one launch for the
 six groups, activation backward fused).  No host synchronisation inside ``step`` (the loss
 stays on the device); densification (every ``densification_interval`` iterations) reads
-counts back.  No CPU fallback: the HIP library is required.
+counts back.  The forward's binning runs under a capacity bound (``BinningCapacity``), so K is
+not read back either: the first render after a change in the point set is sized exactly (one
+read of K), later ones by 1.5x the largest K seen, checked one iteration late from a pinned
+copy.  No CPU fallback: the HIP library is required.
 """
 from __future__ import annotations
 
@@ -193,6 +196,70 @@ class TrainKernels:
         return outs
 
 
+class BinningCapacity:
+    """max_rendered for the trainer's renders without a per-iteration host read of K.
+
+    0 (exact sizing, the forward reads K back) right after the point set changes; afterwards
+    ``headroom`` x the largest K seen, rounded up.  Each bounded render's K (the scan's device
+    counter) is copied to a pinned slot and checked once its event has completed -- one or two
+    iterations later, never waiting.  K above the bound at that check means that render was
+    truncated (its kernels clamp to the bound; GSR_ERR_OVERFLOW semantics): it is counted in
+    ``overflows`` and the bound grows.  The next exact sizing happens at the next
+    densification or opacity reset."""
+
+    def __init__(self, device, headroom: float = 1.5, ring: int = 8):
+        self.headroom = float(headroom)
+        self.cap = 0
+        self.k_max = 0
+        self.overflows = 0
+        self.exact_reads = 0
+        pin = torch.cuda.is_available()
+        self.slots = [torch.zeros(1, dtype=torch.int32, pin_memory=pin) for _ in range(ring)]
+        self.pending: list = []  # (slot, event, cap)
+        self.next_slot = 0
+
+    def bound(self) -> int:
+        self.poll()
+        return self.cap
+
+    def _grow(self):
+        self.cap = (int(self.k_max * self.headroom) + 65536 + 4095) // 4096 * 4096
+
+    def reset(self):
+        """The point set changed: the next render is sized exactly."""
+        self.pending.clear()
+        self.cap = 0
+        self.k_max = 0
+
+    def observe(self, st):
+        """After a forward: record its K (exact read, or an async copy under a bound)."""
+        if self.cap == 0:
+            self.exact_reads += 1
+            self.k_max = max(self.k_max, st.num_rendered)
+            self._grow()
+            return
+        if len(self.pending) == len(self.slots):
+            self.pending[0][1].synchronize()
+            self.poll()
+        slot = self.slots[self.next_slot]
+        self.next_slot = (self.next_slot + 1) % len(self.slots)
+        slot.copy_(st.k_device(), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(st.color.device))
+        self.pending.append((slot, ev, self.cap))
+
+    def poll(self):
+        while self.pending and self.pending[0][1].query():
+            slot, _, cap = self.pending.pop(0)
+            k = int(slot.item())
+            if k > cap:
+                self.overflows += 1
+            if k > self.k_max:
+                self.k_max = k
+                if k * 1.2 > self.cap:
+                    self._grow()
+
+
 class GaussianTrainer:
     """The reference GaussianModel's training state (raw leaves, Adam moments, statistics)
     with the per-iteration step on the HIP kernels."""
@@ -217,6 +284,7 @@ class GaussianTrainer:
         self.rast = CAbiRasterizer(dev)
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(seed)
+        self.binning = BinningCapacity(dev)
         self.setup(opt or OptimizationParams())
 
     @classmethod
@@ -318,7 +386,8 @@ class GaussianTrainer:
         p = self.params
         st = self.rast.forward(cam, p["xyz"], o.reshape(-1), scales=s, rotations=q, sh_dc=p["f_dc"],
                                sh_rest=p["f_rest"] if p["f_rest"].shape[1] else None,
-                               sh_degree=self.active_sh_degree, bg=bg)
+                               sh_degree=self.active_sh_degree, bg=bg, max_rendered=self.binning.bound())
+        self.binning.observe(st)
         return st
 
     def step(self, iteration: int, cam, gt_image: torch.Tensor, bg=(0.0, 0.0, 0.0), densify: bool = True) -> dict:
@@ -349,14 +418,15 @@ class GaussianTrainer:
                 if iteration > opt.densify_from_iter and iteration % opt.densification_interval == 0:
                     size_threshold = 20 if iteration > opt.opacity_reset_interval else None
                     self.densify_and_prune(opt.densify_grad_threshold, 0.005, self.cameras_extent, size_threshold)
+                    self.binning.reset()
                     replaced.update(GROUPS)
                 if iteration % opt.opacity_reset_interval == 0:
                     self.reset_opacity()
+                    self.binning.reset()
                     replaced.add("opacity")
         if iteration < opt.iterations:
             self.optimizer_step({k: v for k, v in grads.items() if k not in replaced})
-        return {"stats": stats, "radii": st.radii, "num_rendered": st.num_rendered, "image": st.color,
-                "num_points": self.num_points}
+        return {"stats": stats, "radii": st.radii, "state": st, "image": st.color, "num_points": self.num_points}
 
     def optimizer_step(self, grads: dict):
         groups = []

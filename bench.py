@@ -476,7 +476,7 @@ def loop_main(args):
     scene = L.synthetic_scene(args.loop_gt, args.loop_init, args.views, W, H, seed=0, device=dev)
     setup_s = time.perf_counter() - t0
     opt = T.OptimizationParams(iterations=args.iters)
-    res = L.train(scene, opt=opt, max_sh_degree=3, log_every=500, device=dev)
+    res = L.train(scene, opt=opt, max_sh_degree=3, log_every=500, device=dev, progress_every=1000)
     print(json.dumps({
         "metric": "training iterations/s, full train.cpp loop (render + L1/D-SSIM + backward + densification + Adam)",
         "value": round(res.iters_per_s, 3), "unit": "iters/s", "n_gpus": 1, "steps": res.iterations, "warmup": 0,
@@ -487,6 +487,7 @@ def loop_main(args):
                    "width": W, "height": H, "views": args.views},
         "seconds": round(res.seconds, 2), "setup_seconds": round(setup_s, 2),
         "final_gaussians": res.final_points, "peak_gaussians": res.peak_points,
+        "binning_overflows": res.binning_overflows, "exact_k_reads": res.exact_k_reads,
         "gaussians_after_densify": res.num_points[::10] + res.num_points[-1:],
         "loss_curve": [(i, round(l, 5)) for i, l, _, _ in res.loss][::4] + [(res.loss[-1][0], round(res.loss[-1][1], 5))]}))
 

@@ -19,8 +19,10 @@
 // usage: gsr_dropin IN.bin OUT.bin   (layouts: tests/test_gpu_dropin.py)
 #include <torch/torch.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <fstream>
 #include <map>
 #include <memory>
@@ -150,6 +152,13 @@ class Camera : public torch::nn::Module {
 };
 
 namespace {
+// progress on stderr (the test prints it when the run fails or times out)
+void mark(const char* what) {
+    static const auto t0 = std::chrono::steady_clock::now();
+    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::fprintf(stderr, "[gsr_dropin %.3f s] %s\n", s, what);
+    std::fflush(stderr);
+}
 template <class T>
 std::vector<T> read_n(std::ifstream& f, size_t n) {
     std::vector<T> v(n);
@@ -171,7 +180,9 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "usage: %s IN.bin OUT.bin\n", argv[0]);
         return 2;
     }
+    std::setvbuf(stdout, nullptr, _IONBF, 0);
     try {
+        mark("start");
         std::ifstream in(argv[1], std::ios::binary);
         auto hdr = read_n<int32_t>(in, 8);  // P, W, H, D, M_rest, convert_SHs, compute_cov3D, debug
         const int P = hdr[0], W = hdr[1], H = hdr[2], D = hdr[3], M = hdr[4];
@@ -182,11 +193,13 @@ int main(int argc, char** argv) {
              scal = read_n<float>(in, (size_t)P * 3), rot = read_n<float>(in, (size_t)P * 4),
              target = read_n<float>(in, (size_t)3 * H * W);
 
+        mark("input read");
         GaussianModel gaussians(3);
         auto& core = gaussians.get_core_params();
         core.active_sh_degree_ = D;
         core.spatial_lr_scale_ = 1.0f;
         core.xyz_ = to_dev(xyz, {P, 3}).requires_grad_(true);
+        mark("first device tensor");
         core.features_dc_ = to_dev(fdc, {P, 1, 3}).requires_grad_(true);
         core.features_rest_ = to_dev(frest, {P, M, 3}).requires_grad_(true);
         core.opacity_ = to_dev(opac, {P, 1}).requires_grad_(true);
@@ -211,14 +224,17 @@ int main(int argc, char** argv) {
         pipe.compute_cov3D_python_ = hdr[6] != 0;
         pipe.debug_ = hdr[7] != 0;
         Camera camera(0, 1, cam_d.data(), cam_d.data() + 9, cam_d[12], cam_d[13], W, H);
+        mark("camera tensors");
         const gsr::RasterCamera rcam = camera.raster_camera();
         auto background = torch::zeros({3}, torch::TensorOptions().dtype(torch::kFloat32).device(torch::kCUDA));
         auto gt = to_dev(target, {3, H, W});
 
         // the loop body train_utils.cpp:137-144 would hold
         auto out = gsr::render(rcam, gaussians, pipe, background, smod);
+        mark("render");
         auto loss = torch::abs(out.render - gt).mean();
         loss.backward();
+        mark("backward");
         std::ofstream o(argv[2], std::ios::binary);
         write_t(o, out.render);
         write_t(o, out.radii);
@@ -234,11 +250,16 @@ int main(int argc, char** argv) {
                         &core.rotation_})
             write_t(o, *t);
         write_t(o, loss.reshape({1}));
+        mark("adam + outputs");
         torch::cuda::synchronize();
+        mark("synchronized");
         std::printf("gsr_dropin ok: P=%d %dx%d loss=%.6f\n", P, W, H, loss.item<float>());
+        core.optimizers_.clear();
+        mark("optimizers released");
     } catch (const std::exception& e) {
         std::fprintf(stderr, "gsr_dropin failed: %s\n", e.what());
         return 1;
     }
+    mark("scope left");
     return 0;
 }

@@ -43,7 +43,11 @@ def _run_exe(cam, s, target, D, flags, smod):
             fh.write(np.array([smod], np.float32).tobytes())
             for a in (s.means3D, s.sh_dc, s.sh_rest, s.raw_opacities, s.raw_scales, s.raw_rotations, target):
                 fh.write(np.ascontiguousarray(a, np.float32).tobytes())
-        r = subprocess.run([EXE, fin, fout], capture_output=True, text=True, timeout=120)
+        try:
+            r = subprocess.run([EXE, fin, fout], capture_output=True, text=True, timeout=150)
+        except subprocess.TimeoutExpired as e:
+            pytest.fail(f"gsr_dropin timed out; its progress:\n{e.stderr}")
+        print(r.stderr)
         assert r.returncode == 0, r.stdout + r.stderr
         raw = open(fout, "rb").read()
     H, W = cam.height, cam.width

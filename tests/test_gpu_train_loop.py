@@ -27,3 +27,7 @@ def test_training_loop_densifies_and_converges():
     for k, v in tr.params.items():
         assert bool(torch.isfinite(v).all()), k
     assert tr.active_sh_degree == 1  # SH degree +1 at iteration 1000
+    # renders ran under the lagged binning bound: no truncated render, and K was read back only
+    # after point-set changes (densify / opacity reset), not per iteration
+    assert res.binning_overflows == 0
+    assert 1 <= res.exact_k_reads <= 2 + len(res.num_points)

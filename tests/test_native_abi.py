@@ -167,3 +167,18 @@ def test_product_does_not_reference_oracle():
                 text = open(os.path.join(dirpath, f)).read()
                 assert not re.search(r"^\s*(import|from)\s+gsr_oracle|#include[^\n]*oracle|libgsr_oracle|"
                                      r"sys\.path[^\n]*oracle", text, re.M), f
+
+
+def test_dropin_executable_has_one_hip_runtime():
+    """The C++ drop-in (lib/gsr_dropin) must resolve libgsr_hip.so's libamdhip64.so.7 to the
+    torch wheel's bundled runtime, not load /opt/rocm's as a second one (_build.build_dropin:
+    libtorch_hip ahead of libgsr_hip in NEEDED order)."""
+    import shutil
+    import subprocess
+    exe = os.path.join(ROOT, "3d_gaussian_splatting_amd", "lib", "gsr_dropin")
+    if not os.path.exists(exe) or not shutil.which("ldd"):
+        pytest.skip("drop-in executable not built")
+    out = subprocess.run(["ldd", exe], capture_output=True, text=True).stdout
+    hip = [l.split("=>")[1].split("(")[0].strip() for l in out.splitlines() if "libamdhip64" in l and "=>" in l]
+    hsa = [l for l in out.splitlines() if "libhsa-runtime64" in l]
+    assert len(hip) == 1 and len(hsa) == 1, out
