@@ -227,8 +227,10 @@ def simulate_ranks(rast, cam, inputs: dict, sh_degree: int, world: int, dL_dpix:
         for r in range(world):
             back_parts[r][b] = g2[r * pair_cap:(r + 1) * pair_cap]
         bsts.append(st)
-    grads = [run("shard_backward", r, lambda r=r: rast.shard_backward(shs[r], torch.cat(back_parts[r])))
-             for r in range(world)]
+    # the gradient all-to-all: rank r receives band b's rows for its splats (a contiguous receive
+    # buffer, as the collective writes it -- the copy is the exchange, outside the compute timer)
+    grad_recv = [torch.cat(back_parts[r]) for r in range(world)]
+    grads = [run("shard_backward", r, lambda r=r: rast.shard_backward(shs[r], grad_recv[r])) for r in range(world)]
     full = {k: torch.cat([g[k] for g in grads]) for k in grads[0]}
     return image, full, dict(rows=rows, pair_cap=pair_cap, capacity=capacity, shards=shs, bands=bsts,
                              band_instances=[int(counts[rows[b]:rows[b + 1]].sum()) for b in range(world)])

@@ -28,6 +28,12 @@ constexpr int kFusedScanMax = 1 << 19;      // Gaussian counts up to this scan +
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 inline int div_up(long long a, long long b) { return (int)((a + b - 1) / b); }
 inline int sort_blocks(long long n) { return n > 0 ? div_up(n, kSortTile) : 0; }
+// multi-GPU splat packing: 256 threads x 4 rounds = 1024 Gaussians per block, so a 1/8 shard
+// (~600k at 5M) still launches ~600 blocks (at the sort's 4096 per block it left 3/4 of the
+// SIMDs idle)
+constexpr int kPackItems = 4;
+constexpr int kPackTile = kSortBlock * kPackItems;
+inline int pack_blocks(long long n) { return n > 0 ? div_up(n, kPackTile) : 0; }
 // reduce-then-scan radix-sort scratch (u32 words): 256 digit columns of (blocks + 1) counts
 // plus 256 digit totals
 inline size_t sort_scratch_words(long long n) { return 256 * ((size_t)sort_blocks(n) + 1) + 256; }
@@ -136,7 +142,7 @@ struct ShardLayout {
         const size_t n = (size_t)(P > 0 ? P : 1);
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
         slot_of = take(4 * n * (size_t)nbands);
-        partials = take(4 * ((size_t)sort_blocks(n) + 1) * (size_t)nbands);
+        partials = take(4 * ((size_t)pack_blocks(n) + 1) * (size_t)nbands);
         grad2d = take(4 * (size_t)kPart * n);
         total = o;
     }

@@ -17,7 +17,7 @@ namespace gsr {
 namespace {
 
 constexpr int kB = kSortBlock;   // 256 threads
-constexpr int kI = kSortItems;   // 16 rounds of 64 per wave: 4096 Gaussians per block
+constexpr int kI = kPackItems;   // rounds of 64 per wave: kPackTile Gaussians per block
 constexpr int kWaves = kB / 64;
 
 __device__ inline uint64_t lanemask_lt() {
@@ -53,7 +53,7 @@ __global__ __launch_bounds__(kB) void pack_count_kernel(const uint32_t* __restri
     uint32_t c[kMaxBands];
 #pragma unroll
     for (int b = 0; b < kMaxBands; ++b) c[b] = 0u;
-    const int base = blockIdx.x * kSortTile + w * (kI * 64);
+    const int base = blockIdx.x * kPackTile + w * (kI * 64);
     for (int r = 0; r < kI; ++r) {
         const int g = base + r * 64 + lane;
         int b_lo = kMaxBands, b_hi = -1;
@@ -131,7 +131,7 @@ __global__ __launch_bounds__(kB) void pack_scatter_kernel(const uint32_t* __rest
                                                           uint32_t* __restrict__ slot_of) {
     __shared__ uint32_t cnt[kWaves][kMaxBands];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int base = blockIdx.x * kSortTile + w * (kI * 64);
+    const int base = blockIdx.x * kPackTile + w * (kI * 64);
     // pass 1: this wave's count per band (for the wave offsets)
     uint32_t c[kMaxBands];
 #pragma unroll
@@ -268,7 +268,7 @@ int launch_pack_splats(const uint32_t* tiles, const uint4* rect, const uint32_t*
             if (hipError_t e = hipMemsetAsync(send + (size_t)b * bb, 0, kSplatBytes, s)) return (int)e;
         return 0;
     }
-    const int nblk = sort_blocks(P);
+    const int nblk = pack_blocks(P);
     hipLaunchKernelGGL(pack_count_kernel, dim3(nblk), dim3(kB), 0, s, tiles, rect, P, br, partials, nblk, row_hist,
                        grid_y);
     hipLaunchKernelGGL(pack_scan_kernel, dim3(br.n), dim3(1024), 0, s, partials, nblk, send, bb);

@@ -124,9 +124,11 @@ def main():
     ap.add_argument("--no-stage-events", action="store_true")
     ap.add_argument("--views", type=int, default=8, help="--mode views: cameras per batch")
     ap.add_argument("--iters", type=int, default=30000, help="--mode loop: training iterations")
-    ap.add_argument("--loop-gt", type=int, default=2_000_000, help="--mode loop: ground-truth Gaussians")
-    ap.add_argument("--loop-init", type=int, default=100_000, help="--mode loop: initial points")
+    ap.add_argument("--loop-gt", type=int, default=4_000_000, help="--mode loop: ground-truth Gaussians")
+    ap.add_argument("--loop-init", type=int, default=1_000_000, help="--mode loop: initial points")
     ap.add_argument("--loop-size", default="1280x832", help="--mode loop: image size WxH")
+    ap.add_argument("--loop-views", type=int, default=128, help="--mode loop: training cameras")
+    ap.add_argument("--loop-texture", type=float, default=1.0, help="--mode loop: ground-truth colour noise")
     ap.add_argument("--mode", default="render", choices=("render", "train", "views", "loop"),
                     help="render: the BASELINE metric (rasterizer forward+backward); train: one full "
                          "training iteration (activations, render, L1+D-SSIM loss, backward, "
@@ -473,7 +475,8 @@ def loop_main(args):
     torch.cuda.set_device(dev)
     W, H = (int(v) for v in args.loop_size.split("x"))
     t0 = time.perf_counter()
-    scene = L.synthetic_scene(args.loop_gt, args.loop_init, args.views, W, H, seed=0, device=dev)
+    scene = L.synthetic_scene(args.loop_gt, args.loop_init, args.loop_views, W, H, seed=0, device=dev,
+                              texture=args.loop_texture)
     setup_s = time.perf_counter() - t0
     opt = T.OptimizationParams(iterations=args.iters)
     res = L.train(scene, opt=opt, max_sh_degree=3, log_every=500, device=dev, progress_every=1000)
@@ -482,9 +485,9 @@ def loop_main(args):
         "value": round(res.iters_per_s, 3), "unit": "iters/s", "n_gpus": 1, "steps": res.iterations, "warmup": 0,
         "ms_per_step": round(1e3 * res.seconds / res.iterations, 4), "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": f"configs[4]: {args.iters} iterations, {args.views} views {W}x{H}, ground truth "
-                               f"{args.loop_gt} Gaussians, init {args.loop_init} points, SH 3",
-                   "width": W, "height": H, "views": args.views},
+        "config": {"workload": f"configs[4]: {args.iters} iterations, {args.loop_views} views {W}x{H}, ground truth "
+                               f"{args.loop_gt} Gaussians (texture {args.loop_texture}), init {args.loop_init} points, "
+                               f"SH 3", "width": W, "height": H, "views": args.loop_views},
         "seconds": round(res.seconds, 2), "setup_seconds": round(setup_s, 2),
         "final_gaussians": res.final_points, "peak_gaussians": res.peak_points,
         "binning_overflows": res.binning_overflows, "exact_k_reads": res.exact_k_reads,

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--config", default="5m_1080p", choices=sorted(bench.CONFIGS))
+    ap.add_argument("--no-single", action="store_true", help="skip the single-GPU reference step (kernel traces)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -46,10 +47,10 @@ def main():
     rast = R.ShardRasterizer(dev)
     single = R.CAbiRasterizer(dev)
     # the single-GPU step for reference (same timing method)
-    K0 = single.forward(cam, **inputs, sh_degree=D).num_rendered
+    K0 = 0 if args.no_single else single.forward(cam, **inputs, sh_degree=D).num_rendered
     cap = bands.round_up(int(K0 * 1.1) + 1)
     ref = []
-    for i in range(args.steps + 2):
+    for i in range(0 if args.no_single else args.steps + 2):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         st = single.forward(cam, **inputs, sh_degree=D, max_rendered=cap)
@@ -58,7 +59,7 @@ def main():
         torch.cuda.synchronize()
         if i >= 2:
             ref.append(e0.elapsed_time(e1))
-    one_gpu = float(np.median(ref))
+    one_gpu = float(np.median(ref)) if ref else float("nan")
     print(json.dumps({"config": args.config, "world": 1, "path": "single-GPU gsr_forward + gsr_backward",
                       "ms_per_step": round(one_gpu, 4)}), flush=True)
     for world in [int(w) for w in args.worlds.split(",")]:

@@ -250,6 +250,13 @@ int main(int argc, char** argv) {
                         &core.rotation_})
             write_t(o, *t);
         write_t(o, loss.reshape({1}));
+        {  // the RasterCamera from_tensors built (tanfovx, tanfovy, viewmatrix, projmatrix, campos)
+            std::vector<float> c = {rcam.tanfovx, rcam.tanfovy};
+            c.insert(c.end(), rcam.viewmatrix.begin(), rcam.viewmatrix.end());
+            c.insert(c.end(), rcam.projmatrix.begin(), rcam.projmatrix.end());
+            c.insert(c.end(), rcam.campos.begin(), rcam.campos.end());
+            o.write(reinterpret_cast<const char*>(c.data()), c.size() * sizeof(float));
+        }
         mark("adam + outputs");
         torch::cuda::synchronize();
         mark("synchronized");
