@@ -59,6 +59,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 # (scripts/ubench/pk_rate.hip): 1.9 ns per wave-instruction per SIMD.
 VALU_ISSUE_PER_S = 256 * 4 * 2.4e9 / 2
 VALU_FMA_SUSTAINED_PER_S = 256 * 4 / 1.9e-9
+# SURVEY §8d secondary bound for F6 + B1: exact (pixel, list-entry) pairs from the CPU oracle x
+# VALU lane-ops per pair (the per-stripe loop bodies in the ISA, DESIGN §5.1: F6 ~20, B1 ~30
+# wave64 instructions per 64-pixel stripe evaluation; per-record overhead left out, so a floor)
+# over 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
+VALU_LANE_OPS_PER_S = 256 * 4 * 32 * 2.4e9
+C_F6_PER_PAIR, C_B1_PER_PAIR = 20, 30
 
 
 ALG_STAGES = ("preprocess", "scan", "duplicate", "tile_sort", "finalize", "blend_fwd", "blend_bwd",
@@ -316,6 +322,14 @@ def main():
                                   f"OpenMP {cores} threads)",
                                   "cpu_model": cpu_model(), "nproc": os.cpu_count(),
                                   "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+        if "roofline" in result:
+            pairs = f.state.forward_pairs()
+            floor_ms = pairs * (C_F6_PER_PAIR + C_B1_PER_PAIR) / VALU_LANE_OPS_PER_S * 1e3
+            meas = sum(result.get("stage_ms", {}).get(k, 0.0) for k in ("blend_fwd", "blend_bwd"))
+            result["roofline"]["valu_pair_bound"] = {
+                "pairs": pairs, "lane_ops_per_pair": {"f6": C_F6_PER_PAIR, "b1": C_B1_PER_PAIR},
+                "peak_lane_ops_per_s": VALU_LANE_OPS_PER_S, "floor_ms_f6_b1": round(floor_ms, 4),
+                "measured_ms_f6_b1": round(meas, 4), "frac": round(floor_ms / meas, 4) if meas else None}
         result["parity"] = {"psnr_db_vs_cpu": round(10 * math.log10(1.0 / mse), 2) if mse > 0 else float("inf"),
                             "rgb_rel_l2": float(np.linalg.norm(col - f.color) / np.linalg.norm(f.color)),
                             "grad_rel_l2_max": max(rel.values()),
