@@ -54,18 +54,21 @@ __device__ inline float dpp_f(float x) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
 }
 
-// Quad (4-lane) all-reduce of 9 values.  The empty asm pins each sum in the block that
+// Quad (4-lane) all-reduce of N values.  The empty asm pins each sum in the block that
 // computes it: without it the compiler sinks the second add into the quad leaders' branch,
 // the DPP move can no longer fuse into it, and each value costs a zero move, a DPP move and
-// an add instead of one v_add_f32_dpp (18 extra VALU ops per record).
-__device__ __forceinline__ void quad_reduce9(float (&v)[9]) {
+// an add instead of one v_add_f32_dpp (2N extra VALU ops per record).
+template <int N>
+__device__ __forceinline__ void quad_reduce(float (&v)[N]) {
 #pragma unroll
-    for (int i = 0; i < 9; ++i) v[i] += dpp_f<0xB1>(v[i]);  // quad_perm [1,0,3,2]
+    for (int i = 0; i < N; ++i) v[i] += dpp_f<0xB1>(v[i]);  // quad_perm [1,0,3,2]
 #pragma unroll
-    for (int i = 0; i < 9; ++i) v[i] += dpp_f<0x4E>(v[i]);  // quad_perm [2,3,0,1]
+    for (int i = 0; i < N; ++i) v[i] += dpp_f<0x4E>(v[i]);  // quad_perm [2,3,0,1]
 #pragma unroll
-    for (int i = 0; i < 9; ++i) asm volatile("" : "+v"(v[i]));
+    for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i]));
 }
+
+
 
 struct BlendGeom {
     int W, H, grid_x, ty0, nwg;
@@ -390,11 +393,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
     const uint32_t next = chunk + 1 < kMaxChunks ? table[chunk + 1] : 0xFFFFFFFFu;
     const int n = next < (uint32_t)n_all ? (int)next : n_all;
     const int tx = tile % geo.grid_x, ty = tile / geo.grid_x;
-    const int px = tx * kTile + (lane & 15);
+    // lane = 4 col + row: a quad holds one column's 4 rows of a stripe, so it shares dx and
+    // the record's moments reduce over the quad before dx is applied (F6 lays a stripe out
+    // row-major, lane = col + 16 row; B1 reads F6's checkpoints through that map)
+    const int col = lane >> 2, row = lane & 3;
+    const int px = tx * kTile + col;
     const float pfx = (float)px;
     const float bx0 = (float)(tx * kTile), by0 = (float)(ty * kTile);
     const size_t npix = (size_t)geo.W * geo.H;
-    const int row = lane >> 4;
     // R = S . dL/dpix - Sp + T_final bg . dL/dpix: the colour term behind the current record
     float pfy[kPPL], T[kPPL], R[kPPL], dp0[kPPL], dp1[kPPL], dp2[kPPL];
 #pragma unroll
@@ -416,7 +422,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
         const float4* src = ck + ((size_t)tl * (kMaxChunks - 1) + (chunk - 1)) * 256;
 #pragma unroll
         for (int p = 0; p < kPPL; ++p) {
-            const float4 c4 = src[64 * p + lane];
+            const float4 c4 = src[64 * p + col + 16 * row];  // F6's lane of this pixel
             T[p] = c4.x;
             R[p] -= fmaf(c4.y, dp0[p], fmaf(c4.z, dp1[p], c4.w * dp2[p]));
         }
@@ -493,9 +499,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                 T[p] = ok ? tT : -fabsf(T[p]);
             }
             if (__any(any)) {
-                const float sx = s0 * dx;
-                float v[9] = {sx, sy, sx * dx, sy * dx, syy, s0, g0, g1, g2};
-                quad_reduce9(v);
+                // the quad shares dx: reduce the six column sums (12 DPP adds, not 18 for the
+                // nine dx-weighted moments of a row-major quad), then apply dx once
+                float u[6] = {s0, sy, syy, g0, g1, g2};
+                quad_reduce(u);
+                const float sx = u[0] * dx;
+                float v[9] = {sx, u[1], sx * dx, u[1] * dx, u[2], u[0], u[3], u[4], u[5]};
                 if ((lane & 3) == 0) {
                     float* dst = qlane + parked * kParkSlot;
                     *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
