@@ -364,8 +364,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                                                             float* __restrict__ p8f,
                                                             float* __restrict__ p1,
                                                             const uint32_t* __restrict__ term,
-                                                            const float4* __restrict__ ck) {
+                                                            const float4* __restrict__ ck,
+                                                            uint32_t* __restrict__ part_clean) {
     __shared__ float4 srec[64 * 3];
+    // this backward dirties the partial block: a later backward of the same forward re-clears
+    if (blockIdx.x == 0 && threadIdx.x == 0) *part_clean = 0u;
     __shared__ float qpark[kPark * kParkSlot];  // [slot][quad][9 of 12]
     __shared__ uint32_t qjl[kPark];
     const int lane = threadIdx.x;
@@ -571,20 +574,24 @@ int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int 
 // zero stores and the gid / rect reads that located them (at 5M Gaussians most of a tile list
 // lies past termination).  K is read on the device (the binning may be sized by a bound).
 __global__ __launch_bounds__(256) void clear_partial_kernel(float4* __restrict__ p8, float* __restrict__ p1,
-                                                            long long cap, const uint32_t* __restrict__ K_dev) {
+                                                            long long cap, const uint32_t* __restrict__ K_dev,
+                                                            const uint32_t* __restrict__ part_clean) {
+    if (*part_clean == 1u) return;  // zeroed by the forward's per-tile depth sort
     const long long K = (long long)*K_dev < cap ? (long long)*K_dev : cap;
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
     for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < 2 * K; i += (long long)gridDim.x * 256) p8[i] = z;
     for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < K; i += (long long)gridDim.x * 256) p1[i] = 0.f;
 }
 
-int launch_clear_partial(float* partial, long long cap, const uint32_t* K_dev, hipStream_t s) {
+int launch_clear_partial(float* partial, long long cap, const uint32_t* K_dev, const uint32_t* part_clean,
+                         hipStream_t s) {
     if (cap <= 0) return 0;
     const PartLayout pl(cap);
     char* base = reinterpret_cast<char*>(partial);
     const long long blocks = (2 * cap + 255) / 256;
     hipLaunchKernelGGL(clear_partial_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s,
-                       reinterpret_cast<float4*>(base + pl.p8), reinterpret_cast<float*>(base + pl.p1), cap, K_dev);
+                       reinterpret_cast<float4*>(base + pl.p8), reinterpret_cast<float*>(base + pl.p1), cap, K_dev,
+                       part_clean);
     return (int)hipGetLastError();
 }
 
@@ -592,7 +599,7 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
                           const uint2* ranges, const uint32_t* sorted_gid, const uint4* rect,
                           const float4* rec, const float* final_T,
                           const float* accum, const float* dL_dpix, float* partial, long long cap,
-                          const uint32_t* term, const float4* ck, hipStream_t s) {
+                          const uint32_t* term, const float4* ck, uint32_t* part_clean, hipStream_t s) {
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1);
     if (geo.nwg <= 0) return 0;
     const PartLayout pl(cap);
@@ -600,7 +607,7 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
     const int blocks = 8 * (geo.nwg / 8 + 1) * kMaxChunks;
     hipLaunchKernelGGL(blend_backward_kernel, dim3(blocks), dim3(64), 0, s, geo, ranges, sorted_gid, rect, rec,
                        final_T, accum, dL_dpix, reinterpret_cast<float*>(base + pl.p8),
-                       reinterpret_cast<float*>(base + pl.p1), term, ck);
+                       reinterpret_cast<float*>(base + pl.p1), term, ck, part_clean);
     return (int)hipGetLastError();
 }
 

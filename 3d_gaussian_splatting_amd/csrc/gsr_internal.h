@@ -58,9 +58,14 @@ struct GeomLayout {
 };
 
 // Binning for up to `cap` instances (the exact K, or a caller-given bound).  The tile-key sort
-// ping-pongs (kA, vA) <-> (kB, vB); F3 emits into (kA, vA).
+// ping-pongs (kA, vA) <-> (kB, vB); F3 emits into (kA, vA).  `part` is B1's partial block
+// (PartLayout, declared below), owned by the forward so that the per-tile depth sort -- a
+// latency-bound LDS kernel -- zeroes it in its memory shadow instead of a separate clear pass
+// in the backward.
+struct PartLayout;
+inline size_t part_bytes(long long K);
 struct BinLayout {
-    size_t kA, vA, kB, vB, hist, total;
+    size_t kA, vA, kB, vB, hist, part, total;
     BinLayout(long long cap) {
         size_t o = 0, n = (size_t)(cap > 0 ? cap : 1);
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
@@ -69,6 +74,7 @@ struct BinLayout {
         kB = take(4 * n);
         vB = take(4 * n);
         hist = take(4 * sort_scratch_words(n));
+        part = take(part_bytes((long long)n));
         total = o;
     }
 };
@@ -116,6 +122,7 @@ struct PartLayout {
         total = p1 + align_up(4 * n);
     }
 };
+inline size_t part_bytes(long long K) { return PartLayout(K).total; }
 
 // ---- multi-GPU exchange (gsr_shard.hip) ----
 constexpr int kMaxBands = 16;       // tile-row bands (ranks) of one exchange
@@ -152,6 +159,9 @@ struct ShardLayout {
 constexpr int kTotalSlot = 2 * kCountSlots;          // K = sum of tiles_touched, written by the scan
 constexpr int kOvfCountSlot = 2 * kCountSlots + 8;   // tiles queued for the large per-tile depth sort
 constexpr int kOvf2CountSlot = 2 * kCountSlots + 9;  // ... and for its global-memory form
+// 1: the binning's B1 partial block holds zeros for the live K entries (set by the per-tile
+// depth sort that zeroed it); 0 (the forward's memset, or B1 having written it): not known
+constexpr int kPartCleanSlot = 2 * kCountSlots + 10;
 
 // number of 8-bit LSD passes to sort tile ids of a grid with `tiles` tiles
 inline int tile_bits(int tiles) {
