@@ -211,8 +211,6 @@ struct Views {
     float *final_T, *accum;
     float4* ck;
     uint32_t *kA, *vA, *kB, *vB, *hist;
-    float* part;                         // B1's partial block (zeroed by the per-tile depth sort)
-    uint32_t* part_clean;
     uint32_t *sorted_tile, *sorted_gid;  // where the tile sort's result lands
     uint32_t *free_k, *free_v;           // the other ping-pong pair (scratch after the sort)
 };
@@ -232,7 +230,6 @@ Views views(const gsr_camera* cam, long long n, const gsr_buffers* b) {
     v.ranges = at<uint2>(b->image, il.ranges);
     v.counters = at<uint32_t>(b->image, il.counters);
     v.K_dev = v.counters + kTotalSlot;
-    v.part_clean = v.counters + kPartCleanSlot;
     v.ovf = at<uint32_t>(b->image, il.ovf);
     v.ovf2 = at<uint32_t>(b->image, il.ovf2);
     v.term = at<uint32_t>(b->image, il.term);
@@ -246,7 +243,6 @@ Views views(const gsr_camera* cam, long long n, const gsr_buffers* b) {
         v.kB = at<uint32_t>(b->binning, bl.kB);
         v.vB = at<uint32_t>(b->binning, bl.vB);
         v.hist = at<uint32_t>(b->binning, bl.hist);
-        v.part = at<float>(b->binning, bl.part);
         const int tiles = div_up(cam->width, kTile) * div_up(cam->height, kTile);
         const bool odd = (tile_passes(tiles) & 1) != 0;  // the sort ends in (kB, vB) after odd passes
         v.sorted_tile = odd ? v.kB : v.kA;
@@ -337,8 +333,7 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
         GSR_STAGE(GSR_STAGE_FINALIZE, launch_finalize(v.sorted_tile, cap, v.K_dev, v.ranges, stream), "finalize");
         GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_tile_depth_sort(v.ranges, j.ty0 * j.gx, ntiles, cap, v.depth_key,
                                                                v.sorted_gid, v.ovf, v.counters + kOvfCountSlot, v.ovf2,
-                                                               v.counters + kOvf2CountSlot, v.free_k, v.free_v,
-                                                               v.part, v.K_dev, v.part_clean, stream),
+                                                               v.counters + kOvf2CountSlot, v.free_k, v.free_v, stream),
                   "per-tile depth order");
     }
     GSR_STAGE(GSR_STAGE_BLEND_FWD, launch_blend_forward(*cam, j.rs->bg, j.ty0, j.ty1, v.ranges, v.sorted_gid, v.rec,
@@ -389,15 +384,13 @@ int blend_backward(const gsr_camera* cam, const gsr_raster_settings* rs, const g
     int ty0, ty1;
     band(cam, rs, &ty0, &ty1);
     const Views v = views(cam, n, bufs);
-    (void)alloc_scratch;  // the partial block lives in the forward's binning (BinLayout.part)
-    (void)ctx;
-    float* partial = v.part;
-    // a no-op when the forward's per-tile depth sort zeroed the block and no backward has run
-    // since; otherwise (a second backward of one forward) the clear runs
-    GSR_STAGE(GSR_STAGE_MISC, launch_clear_partial(partial, cap, v.K_dev, v.part_clean, stream), "clear partials");
+    if (!alloc_scratch) return fail(-1, "null scratch allocator");
+    float* partial = static_cast<float*>(alloc_scratch(ctx, PartLayout(cap).total));
+    if (!partial) return fail(-2, "allocation failed (scratch, %lld instances)", cap);
+    // only the per-entry flag bytes are zeroed: the gather reads the entries B1 flagged
+    GSR_STAGE(GSR_STAGE_MISC, launch_clear_flags(partial, cap, stream), "clear partial flags");
     GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.rect, v.rec,
-                                                         v.final_T, v.accum, dL_dpix, partial, cap, v.term, v.ck,
-                                                         v.part_clean, stream),
+                                                         v.final_T, v.accum, dL_dpix, partial, cap, v.term, v.ck, stream),
               "blend backward");
     GSR_STAGE(GSR_STAGE_GATHER, launch_gather_grad2d(v.offsets, partial, v.rec, cam->width, cam->height, cap, (int)n,
                                                      grad2d, stream),
@@ -469,10 +462,7 @@ const char* gsr_last_error(void) { return g_err.c_str(); }
 size_t gsr_geom_bytes(int32_t P) { return GeomLayout(P).total; }
 size_t gsr_binning_bytes(int32_t capacity) { return BinLayout(capacity).total; }
 size_t gsr_image_bytes(int32_t w, int32_t h) { return ImgLayout(w, h).total; }
-size_t gsr_scratch_bytes(int32_t capacity) {
-    (void)capacity;  // the B1 partials moved into the binning allocation (BinLayout.part)
-    return 0;
-}
+size_t gsr_scratch_bytes(int32_t capacity) { return PartLayout(capacity).total; }
 size_t gsr_exchange_block_bytes(int32_t pair_cap) { return exchange_block_bytes(pair_cap > 0 ? pair_cap : 0); }
 size_t gsr_shard_state_bytes(int32_t P, int32_t nbands, int32_t pair_cap) {
     (void)pair_cap;

@@ -316,7 +316,7 @@ constexpr int kPark = 4;
 // ~1 conflict cycle per LDS instruction of B1 in the PMC pass).
 constexpr int kParkSlot = 16 * 12 + 12;
 __device__ __forceinline__ void park_flush(const float* qpark, const uint32_t* qjl, int parked, float* p8f,
-                                           float* p1, int lane) {
+                                           float* p1, uint8_t* fl, int lane) {
     __syncthreads();  // one-wave block: orders the quad leaders' LDS writes before the reads
     if (lane < parked * 9) {
         const int slot = lane / 9, c = lane - 9 * slot;
@@ -327,6 +327,7 @@ __device__ __forceinline__ void park_flush(const float* qpark, const uint32_t* q
         const uint32_t j = qjl[slot];
         float* dst = c < 8 ? p8f + 8 * (size_t)j + c : p1 + j;
         *dst = (t[0] + t[1]) + (t[2] + t[3]);
+        if (c == 8) fl[j] = 1;  // the gather reads flagged entries only
     }
     __syncthreads();
 }
@@ -363,12 +364,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                                                             const float* __restrict__ dL_dpix,
                                                             float* __restrict__ p8f,
                                                             float* __restrict__ p1,
+                                                            uint8_t* __restrict__ fl,
                                                             const uint32_t* __restrict__ term,
-                                                            const float4* __restrict__ ck,
-                                                            uint32_t* __restrict__ part_clean) {
+                                                            const float4* __restrict__ ck) {
     __shared__ float4 srec[64 * 3];
-    // this backward dirties the partial block: a later backward of the same forward re-clears
-    if (blockIdx.x == 0 && threadIdx.x == 0) *part_clean = 0u;
     __shared__ float qpark[kPark * kParkSlot];  // [slot][quad][9 of 12]
     __shared__ uint32_t qjl[kPark];
     const int lane = threadIdx.x;
@@ -436,8 +435,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
 #pragma unroll
         for (int p = 0; p < kPPL; ++p) live |= __any(T[p] > 0.0f) ? (1u << p) : 0u;
         // Every pixel of the tile has terminated: the rest of this chunk (and every later chunk,
-        // which starts from a dead checkpoint) contributes nothing, and its partials keep the
-        // zeros the launcher cleared them to.
+        // which starts from a dead checkpoint) contributes nothing; its entries stay unflagged.
         if (live == 0) break;
         uint32_t jl = 0, smask = 0;
         if (lane < cnt) {
@@ -516,7 +514,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                 }
                 if (lane == 0) qjl[parked] = (uint32_t)__builtin_amdgcn_readlane((int)jl, k);
                 if (++parked == kPark) {
-                    park_flush(qpark, qjl, parked, p8f, p1, lane);
+                    park_flush(qpark, qjl, parked, p8f, p1, fl, lane);
                     parked = 0;
                 }
             }
@@ -528,7 +526,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                 if (live == 0) break;
             }
         }
-        if (parked) park_flush(qpark, qjl, parked, p8f, p1, lane);
+        if (parked) park_flush(qpark, qjl, parked, p8f, p1, fl, lane);
         __syncthreads();  // srec / qpark are rewritten by the next batch
     }
 }
@@ -568,38 +566,11 @@ int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int 
     return (int)hipGetLastError();
 }
 
-// Partials of records no pixel takes a gradient from -- including every record after a tile's
-// pixels have all terminated -- are never written by blend_backward_kernel: one streaming clear
-// of the K live entries (36 B each at the fill rate) before it replaces their scattered 36-B
-// zero stores and the gid / rect reads that located them (at 5M Gaussians most of a tile list
-// lies past termination).  K is read on the device (the binning may be sized by a bound).
-__global__ __launch_bounds__(256) void clear_partial_kernel(float4* __restrict__ p8, float* __restrict__ p1,
-                                                            long long cap, const uint32_t* __restrict__ K_dev,
-                                                            const uint32_t* __restrict__ part_clean) {
-    if (*part_clean == 1u) return;  // zeroed by the forward's per-tile depth sort
-    const long long K = (long long)*K_dev < cap ? (long long)*K_dev : cap;
-    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < 2 * K; i += (long long)gridDim.x * 256) p8[i] = z;
-    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < K; i += (long long)gridDim.x * 256) p1[i] = 0.f;
-}
-
-int launch_clear_partial(float* partial, long long cap, const uint32_t* K_dev, const uint32_t* part_clean,
-                         hipStream_t s) {
-    if (cap <= 0) return 0;
-    const PartLayout pl(cap);
-    char* base = reinterpret_cast<char*>(partial);
-    const long long blocks = (2 * cap + 255) / 256;
-    hipLaunchKernelGGL(clear_partial_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s,
-                       reinterpret_cast<float4*>(base + pl.p8), reinterpret_cast<float*>(base + pl.p1), cap, K_dev,
-                       part_clean);
-    return (int)hipGetLastError();
-}
-
 int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
                           const uint2* ranges, const uint32_t* sorted_gid, const uint4* rect,
                           const float4* rec, const float* final_T,
                           const float* accum, const float* dL_dpix, float* partial, long long cap,
-                          const uint32_t* term, const float4* ck, uint32_t* part_clean, hipStream_t s) {
+                          const uint32_t* term, const float4* ck, hipStream_t s) {
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1);
     if (geo.nwg <= 0) return 0;
     const PartLayout pl(cap);
@@ -607,8 +578,14 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
     const int blocks = 8 * (geo.nwg / 8 + 1) * kMaxChunks;
     hipLaunchKernelGGL(blend_backward_kernel, dim3(blocks), dim3(64), 0, s, geo, ranges, sorted_gid, rect, rec,
                        final_T, accum, dL_dpix, reinterpret_cast<float*>(base + pl.p8),
-                       reinterpret_cast<float*>(base + pl.p1), term, ck, part_clean);
+                       reinterpret_cast<float*>(base + pl.p1), reinterpret_cast<uint8_t*>(base + pl.fl), term, ck);
     return (int)hipGetLastError();
+}
+
+int launch_clear_flags(float* partial, long long cap, hipStream_t s) {
+    if (cap <= 0) return 0;
+    const PartLayout pl(cap);
+    return (int)hipMemsetAsync(reinterpret_cast<char*>(partial) + pl.fl, 0, (size_t)cap, s);
 }
 
 }  // namespace gsr

@@ -58,14 +58,9 @@ struct GeomLayout {
 };
 
 // Binning for up to `cap` instances (the exact K, or a caller-given bound).  The tile-key sort
-// ping-pongs (kA, vA) <-> (kB, vB); F3 emits into (kA, vA).  `part` is B1's partial block
-// (PartLayout, declared below), owned by the forward so that the per-tile depth sort -- a
-// latency-bound LDS kernel -- zeroes it in its memory shadow instead of a separate clear pass
-// in the backward.
-struct PartLayout;
-inline size_t part_bytes(long long K);
+// ping-pongs (kA, vA) <-> (kB, vB); F3 emits into (kA, vA).
 struct BinLayout {
-    size_t kA, vA, kB, vB, hist, part, total;
+    size_t kA, vA, kB, vB, hist, total;
     BinLayout(long long cap) {
         size_t o = 0, n = (size_t)(cap > 0 ? cap : 1);
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
@@ -74,7 +69,6 @@ struct BinLayout {
         kB = take(4 * n);
         vB = take(4 * n);
         hist = take(4 * sort_scratch_words(n));
-        part = take(part_bytes((long long)n));
         total = o;
     }
 };
@@ -113,16 +107,19 @@ struct ImgLayout {
 // B1 output, one entry per (tile, instance) at emission index j: 8 floats (two float4:
 // d mean2D x/y, d conic A/B/C, d opacity, d colour r/g) and a ninth float (d colour b) in a
 // separate array, so the entry is 36 B and every store/load stays 16-B aligned.
+// `fl`: one byte per entry, 1 where B1 wrote the entry (a record that changed a pixel).  Only
+// the flags are zeroed before B1 (K bytes instead of the 36-B entries), and the gather reads
+// the entries whose flag is set.
 struct PartLayout {
-    size_t p8, p1, total;
+    size_t p8, p1, fl, total;
     explicit PartLayout(long long K) {
         const size_t n = (size_t)(K > 0 ? K : 1);
         p8 = 0;
         p1 = align_up(32 * n);
-        total = p1 + align_up(4 * n);
+        fl = p1 + align_up(4 * n);
+        total = fl + align_up(n);
     }
 };
-inline size_t part_bytes(long long K) { return PartLayout(K).total; }
 
 // ---- multi-GPU exchange (gsr_shard.hip) ----
 constexpr int kMaxBands = 16;       // tile-row bands (ranks) of one exchange
@@ -159,9 +156,6 @@ struct ShardLayout {
 constexpr int kTotalSlot = 2 * kCountSlots;          // K = sum of tiles_touched, written by the scan
 constexpr int kOvfCountSlot = 2 * kCountSlots + 8;   // tiles queued for the large per-tile depth sort
 constexpr int kOvf2CountSlot = 2 * kCountSlots + 9;  // ... and for its global-memory form
-// 1: the binning's B1 partial block holds zeros for the live K entries (set by the per-tile
-// depth sort that zeroed it); 0 (the forward's memset, or B1 having written it): not known
-constexpr int kPartCleanSlot = 2 * kCountSlots + 10;
 
 // number of 8-bit LSD passes to sort tile ids of a grid with `tiles` tiles
 inline int tile_bits(int tiles) {

@@ -56,12 +56,9 @@ int launch_duplicate(const uint32_t* tiles, uint4* rect, int n, int grid_x, int 
 // queued in `ovf` (count at *ovf_count, zeroed) for 8192-entry blocks, longer ones again in
 // ovf2 for a global-memory form using scratch_hi / scratch_lo (K u32 each, free after the tile
 // sort).  K: the binning's capacity (it sizes the LDS form from the mean slice).
-// The first kernel also zeroes B1's partial block (`part`: PartLayout(K), the live
-// min(*K_dev, K) entries, one slice per block) and sets *part_clean = 1.
 int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long K, const uint32_t* depth_key,
                            uint32_t* gid, uint32_t* ovf, uint32_t* ovf_count, uint32_t* ovf2, uint32_t* ovf2_count,
-                           uint32_t* scratch_hi, uint32_t* scratch_lo, float* part, const uint32_t* K_dev,
-                           uint32_t* part_clean, hipStream_t s);
+                           uint32_t* scratch_hi, uint32_t* scratch_lo, hipStream_t s);
 
 // F5: ranges[tile] = [start, end) of the sorted tile keys (K = min(*K_dev, cap))
 int launch_finalize(const uint32_t* sorted_tile, long long cap, const uint32_t* K_dev, uint2* ranges, hipStream_t s);
@@ -76,17 +73,15 @@ int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int 
 // F6 writes term[t] (see kMaxChunks) and the B1 chunk checkpoints `ck` (ImgLayout.ck).
 // B1: per-tile front-to-back gradients -> per-instance partial entry j (PartLayout(cap)), where
 // the emission index j = inst_start[g] + row-major index of the tile in g's band-clipped rect.
-// launch_clear_partial zeroes the live part (K = min(*K_dev, cap) entries) of the partial
-// block launch_blend_backward fills unless *part_clean says the forward already did; it must
-// precede B1 on the stream.  B1 sets *part_clean = 0 (a second backward of the same forward
-// clears again).
-int launch_clear_partial(float* partial, long long cap, const uint32_t* K_dev, const uint32_t* part_clean,
-                         hipStream_t s);
+// B1 writes the entries of the records that changed a pixel and sets their flag byte
+// (PartLayout.fl); launch_clear_flags zeroes the flags (K bytes) and must precede it.  The
+// gather reads only flagged entries, so the 36-B entries are never cleared.
+int launch_clear_flags(float* partial, long long cap, hipStream_t s);
 int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
                           const uint2* ranges, const uint32_t* sorted_gid, const uint4* rect,
                           const float4* rec, const float* final_T,
                           const float* accum, const float* dL_dpix, float* partial, long long cap,
-                          const uint32_t* term, const float4* ck, uint32_t* part_clean, hipStream_t s);
+                          const uint32_t* term, const float4* ck, hipStream_t s);
 
 // record layout constants shared by preprocess and the blend kernels
 constexpr float kLn2 = 0.6931471805599453f;  // conic A = -2 ln2 a', B = -ln2 b', C = -2 ln2 c' 

@@ -30,20 +30,24 @@ constexpr float kC1 = 0.4886025119029199f;
 // Per-Gaussian sum of its per-(tile, instance) partials in emission order.  A block owns 256
 // consecutive Gaussians; their segments [offsets[g-1], offsets[g]) tile one contiguous
 // stretch of the partial arrays, which the block streams through LDS in coalesced windows of
-// kGatherWin entries.  Each thread then adds the part of its own segment that lies in the
-// window, in order, from LDS.  The partials are B1's raw tile moments (Sx, Sy, Sxx, Sxy, Syy,
-// S0, colour x3, gsr_blend.hip); they are linear in the 2D gradients, so the conversion
-// runs once on the per-Gaussian sum, with the Gaussian's own conic and opacity from its blend
-// record.  The 48-B result lands at grad2d[gid].
+// kGatherWin entries.  Only entries B1 flagged (records that changed a pixel) are loaded; the
+// rest count as zeros, so the partial block itself is never cleared and entries of records past
+// a tile's termination are never read.  Each thread then adds the part of its own segment that
+// lies in the window, in order, from LDS.  The partials are B1's raw tile moments (Sx, Sy, Sxx,
+// Sxy, Syy, S0, colour x3, gsr_blend.hip); they are linear in the 2D gradients, so the
+// conversion runs once on the per-Gaussian sum, with the Gaussian's own conic and opacity from
+// its blend record.  The 48-B result lands at grad2d[gid].
 constexpr int kGatherWin = 512;
 
 __global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __restrict__ offsets,
                                                             const float4* __restrict__ p8,
                                                             const float* __restrict__ p1,
+                                                            const uint8_t* __restrict__ fl,
                                                             const float4* __restrict__ rec, float hw, float hh,
                                                             int P, uint32_t cap, float* __restrict__ grad2d) {
     __shared__ float4 w8[2 * kGatherWin];
     __shared__ float w1[kGatherWin];
+    __shared__ uint32_t wv[kGatherWin / 4];
     const int g0 = blockIdx.x * 256, g = g0 + threadIdx.x;
     const int gl = (P - g0 < 256 ? P - g0 : 256) + g0;  // one past the block's last Gaussian
     // emission indices past the binning's capacity were never emitted (overflow): clamped
@@ -60,10 +64,14 @@ __global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __re
     float a[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) a[k] = 0.f;
+    const uint8_t* wvb = reinterpret_cast<const uint8_t*>(wv);
     for (uint32_t W = J0; W < J1; W += kGatherWin) {
         const uint32_t n = J1 - W < (uint32_t)kGatherWin ? J1 - W : (uint32_t)kGatherWin;
-        for (uint32_t i = threadIdx.x; i < 2 * n; i += 256) w8[i] = p8[2 * (size_t)W + i];
-        for (uint32_t i = threadIdx.x; i < n; i += 256) w1[i] = p1[(size_t)W + i];
+        for (uint32_t i = threadIdx.x; i < n; i += 256) reinterpret_cast<uint8_t*>(wv)[i] = fl[(size_t)W + i];
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < 2 * n; i += 256)
+            w8[i] = wvb[i >> 1] ? p8[2 * (size_t)W + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (uint32_t i = threadIdx.x; i < n; i += 256) w1[i] = wvb[i] ? p1[(size_t)W + i] : 0.f;
         __syncthreads();
         const uint32_t lo = s > W ? s : W, hi = e < W + n ? e : W + n;
         for (uint32_t j = lo; j < hi; ++j) {
@@ -442,7 +450,8 @@ int launch_gather_grad2d(const uint32_t* offsets, const float* partial, const fl
     const char* base = reinterpret_cast<const char*>(partial);
     hipLaunchKernelGGL(gather_grad2d_kernel, dim3(div_up(P, 256)), dim3(256), 0, s, offsets,
                        reinterpret_cast<const float4*>(base + pl.p8), reinterpret_cast<const float*>(base + pl.p1),
-                       rec, 0.5f * (float)W, 0.5f * (float)H, P, (uint32_t)cap, grad2d);
+                       reinterpret_cast<const uint8_t*>(base + pl.fl), rec, 0.5f * (float)W, 0.5f * (float)H, P,
+                       (uint32_t)cap, grad2d);
     return (int)hipGetLastError();
 }
 

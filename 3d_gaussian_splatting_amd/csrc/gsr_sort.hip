@@ -654,35 +654,12 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
     __syncthreads();  // red[] is rewritten by the next slice
 }
 
-// B1's partial block, zeroed by the per-tile depth sort: slice b of nb (the live K entries:
-// 2 K float4 of p8, K floats of p1), plain coalesced stores in the shadow of the sort's LDS
-// work.  Block 0 marks the block clean for the backward (kPartCleanSlot); the backward reads
-// the mark only after this kernel has completed.
-struct PartClear {
-    float4* p8;
-    float* p1;
-    long long cap;
-    const uint32_t* K_dev;
-    uint32_t* clean;
-};
-__device__ __forceinline__ void clear_part_slice(const PartClear& pc, int b, int nb) {
-    if (!pc.p8) return;
-    const long long K = (long long)*pc.K_dev < pc.cap ? (long long)*pc.K_dev : pc.cap;
-    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-    const long long lo8 = 2 * K * b / nb, hi8 = 2 * K * (b + 1) / nb;
-    for (long long i = lo8 + threadIdx.x; i < hi8; i += blockDim.x) pc.p8[i] = z;
-    const long long lo1 = K * b / nb, hi1 = K * (b + 1) / nb;
-    for (long long i = lo1 + threadIdx.x; i < hi1; i += blockDim.x) pc.p1[i] = 0.f;
-    if (b == 0 && threadIdx.x == 0) *pc.clean = 1u;
-}
-
 // One block per tile of the launch; slices longer than NT * I go to the queue `ovf`.
 template <int NT, int I, int DB>
 __global__ __launch_bounds__(NT) void tile_depth_radix(const uint2* __restrict__ ranges, int tile0,
                                                       const uint32_t* __restrict__ depth_key,
                                                       uint32_t* __restrict__ gid, uint32_t* __restrict__ ovf,
-                                                      uint32_t* __restrict__ ovf_count, const PartClear pc) {
-    clear_part_slice(pc, blockIdx.x, gridDim.x);
+                                                      uint32_t* __restrict__ ovf_count) {
     const int tile = tile0 + blockIdx.x;
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
@@ -826,15 +803,8 @@ int launch_duplicate(const uint32_t* tiles, uint4* rect, int n, int grid_x, int 
 
 int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long K, const uint32_t* depth_key,
                            uint32_t* gid, uint32_t* ovf, uint32_t* ovf_count, uint32_t* ovf2, uint32_t* ovf2_count,
-                           uint32_t* scratch_hi, uint32_t* scratch_lo, float* part, const uint32_t* K_dev,
-                           uint32_t* part_clean, hipStream_t s) {
+                           uint32_t* scratch_hi, uint32_t* scratch_lo, hipStream_t s) {
     if (ntiles <= 0 || K <= 0) return 0;
-    PartClear pc{nullptr, nullptr, K, K_dev, part_clean};
-    if (part) {
-        const PartLayout pl(K);
-        pc.p8 = reinterpret_cast<float4*>(reinterpret_cast<char*>(part) + pl.p8);
-        pc.p1 = reinterpret_cast<float*>(reinterpret_cast<char*>(part) + pl.p1);
-    }
     // one block per tile holding up to cap entries in LDS, a power of two >= 1.5x the mean slice
     // (1024 .. 4096: <= 43 KB of LDS, 3 blocks per CU); longer slices queue for 512-thread blocks
     // of up to 8192 (73 KB: 2 per CU) walking the queue, and beyond that for the global form
@@ -843,7 +813,7 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
     while (cap < 4096 && cap < mean + mean / 2) cap <<= 1;
 #define GSR_TILE_RADIX(NT_, I_)                                                                          \
     hipLaunchKernelGGL((tile_depth_radix<NT_, I_, 9>), dim3(ntiles), dim3(NT_), 0, s, ranges, tile0, depth_key, \
-                       gid, ovf, ovf_count, pc)
+                       gid, ovf, ovf_count)
     if (cap == 1024) GSR_TILE_RADIX(256, 4);
     else if (cap == 2048) GSR_TILE_RADIX(256, 8);
     else GSR_TILE_RADIX(256, 16);

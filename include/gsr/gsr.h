@@ -113,7 +113,7 @@ typedef struct gsr_buffers {
     void* image;             /* returned by the image allocation */
     int32_t num_rendered;    /* K = number of (Gaussian, tile) instances; -1 while it is only on
                                 the device (max_rendered > 0; see gsr_read_num_rendered) */
-    int32_t capacity;        /* instances the binning (including B1's partial block) holds */
+    int32_t capacity;        /* instances the binning (and the backward's scratch) hold */
     int32_t n_local;         /* Gaussians (or received splat slots, gsr_band_forward) indexed */
     int32_t reserved;
 } gsr_buffers;
@@ -147,10 +147,9 @@ int gsr_forward_batch(int32_t V, const gsr_camera* cams, const gsr_gaussians* gs
                       gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_binning, gsr_alloc_fn alloc_image,
                       void* alloc_ctx, gsr_buffers* bufs, void* stream);
 
-/* Full backward (B1 + gather + B2).  dL_dout_color: 3 x H x W.  scratch: asked for once
- * through alloc_scratch (48 * P bytes for the per-Gaussian screen-space gradient), valid for
- * the duration of the call.  B1's per-instance partials live in the forward's binning
- * allocation, zeroed by the forward; a second backward of the same forward re-zeroes them. */
+/* Full backward (B1 + gather + B2).  dL_dout_color: 3 x H x W.  scratch: asked for twice
+ * through alloc_scratch (gsr_scratch_bytes(capacity) for per-instance partial gradients, then
+ * 48 * P bytes for the per-Gaussian screen-space gradient), valid for the duration of the call. */
 int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs,
                  const gsr_buffers* bufs, const float* dL_dout_color, gsr_alloc_fn alloc_scratch,
                  void* alloc_ctx, const gsr_grads* grads, void* stream);
@@ -260,7 +259,7 @@ const char* gsr_stage_name(int stage);
 size_t gsr_geom_bytes(int32_t P);
 size_t gsr_binning_bytes(int32_t capacity);
 size_t gsr_image_bytes(int32_t width, int32_t height);
-size_t gsr_scratch_bytes(int32_t capacity); /* 0: the B1 partials are in the binning (kept for ABI 2) */
+size_t gsr_scratch_bytes(int32_t capacity);
 
 #ifdef __cplusplus
 }

@@ -64,11 +64,10 @@ def test_library_loads_and_reports_sizes():
     L = native.load_hip()
     assert L.gsr_abi_version() == native.ABI_VERSION == 2
     assert L.gsr_geom_bytes(1000) > 1000 * 64
-    # binning: tile key / gid ping-pong (16 B) + B1's 36-B partial block per instance
-    assert L.gsr_binning_bytes(10) >= 10 * (16 + 36)
+    assert L.gsr_binning_bytes(10) >= 10 * 24
     assert L.gsr_image_bytes(1920, 1080) >= 1920 * 1080 * 8
-    assert L.gsr_scratch_bytes(100) == 0  # the partials moved into the binning allocation
-    assert L.gsr_binning_bytes(1 << 20) - L.gsr_binning_bytes(1) >= (16 + 36) * ((1 << 20) - 1)
+    assert L.gsr_scratch_bytes(100) >= 100 * 37  # 36-B partial + 1 flag byte per instance
+    assert L.gsr_scratch_bytes(1 << 20) == (32 << 20) + (4 << 20) + (1 << 20)
     assert L.gsr_exchange_block_bytes(100) == 64 * 101
     assert L.gsr_shard_state_bytes(1000, 8, 100) > L.gsr_geom_bytes(1000) + 8 * 1000 * 4 + 1000 * 48
 
