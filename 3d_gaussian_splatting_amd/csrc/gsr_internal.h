@@ -36,7 +36,12 @@ constexpr int kPackTile = kSortBlock * kPackItems;
 inline int pack_blocks(long long n) { return n > 0 ? div_up(n, kPackTile) : 0; }
 // reduce-then-scan radix-sort scratch (u32 words): 256 digit columns of (blocks + 1) counts
 // plus 256 digit totals
-inline size_t sort_scratch_words(long long n) { return 256 * ((size_t)sort_blocks(n) + 1) + 256; }
+// LSD radix passes (tile keys, Morton codes): kRadixItems rounds of 64 per wave (4096 keys
+// per block; 2048 measured slower: 0.137 vs 0.120 ms for the 1M / 1080p tile sort)
+constexpr int kRadixItems = 16;
+constexpr int kRadixTile = kSortBlock * kRadixItems;
+inline int radix_blocks(long long n) { return n > 0 ? div_up(n, kRadixTile) : 0; }
+inline size_t sort_scratch_words(long long n) { return 256 * ((size_t)radix_blocks(n) + 1) + 256; }
 
 // lengths and emission index bases are u32: n instances must stay below 2^32, and the blend's
 // per-tile index arithmetic below 2^31

@@ -33,6 +33,8 @@ constexpr int kB = kSortBlock;       // 256 threads = 4 waves
 constexpr int kI = kSortItems;       // 16 rounds per wave
 constexpr int kWaves = kB / 64;
 constexpr int kWaveItems = kI * 64;  // 1024 contiguous items per wave
+constexpr int kRI = kRadixItems;     // radix passes: rounds per wave
+constexpr int kRadixWaveItems = kRI * 64;
 
 __device__ inline uint64_t lanemask_lt() {
     const int lane = threadIdx.x & 63;
@@ -75,9 +77,9 @@ __global__ __launch_bounds__(kB) void radix_upsweep(const uint32_t* __restrict__
     for (int k = 0; k < kWaves; ++k) cnt[k][tid] = 0;
     __syncthreads();
     const uint32_t mask = (1u << nbits) - 1u;
-    const long long base = (long long)blockIdx.x * kSortTile + (long long)w * kWaveItems;
+    const long long base = (long long)blockIdx.x * kRadixTile + (long long)w * kRadixWaveItems;
 #pragma unroll 4
-    for (int r = 0; r < kI; ++r) {
+    for (int r = 0; r < kRI; ++r) {
         const long long idx = base + r * 64 + (tid & 63);
         if (idx < n) atomicAdd(&cnt[w][(keys[idx] >> shift) & mask], 1u);
     }
@@ -132,10 +134,10 @@ __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict
     __shared__ uint32_t gbase[256];   // global position of this block's first item of digit d
     __shared__ uint32_t lbase[256];   // block-local position of the first item of digit d
     __shared__ uint32_t wsum[kWaves];
-    __shared__ uint32_t skey[kSortTile];
-    __shared__ uint32_t sval[kSortTile];
+    __shared__ uint32_t skey[kRadixTile];
+    __shared__ uint32_t sval[kRadixTile];
     const long long n = live_count(cap, n_dev);
-    const long long bbase = (long long)blockIdx.x * kSortTile;
+    const long long bbase = (long long)blockIdx.x * kRadixTile;
     if (bbase >= n) return;  // block-uniform: nothing of this block is live
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const uint32_t mask = (1u << nbits) - 1u;
@@ -158,18 +160,18 @@ __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict
         gbase[tid] = pre + x - v + hist[(size_t)tid * nb + blockIdx.x];
     }
     __syncthreads();
-    const long long base = bbase + (long long)w * kWaveItems;
-    uint32_t key[kI], val[kI], rank[kI];
+    const long long base = bbase + (long long)w * kRadixWaveItems;
+    uint32_t key[kRI], val[kRI], rank[kRI];
     const uint64_t lt = lanemask_lt();
 #pragma unroll
-    for (int r = 0; r < kI; ++r) {
+    for (int r = 0; r < kRI; ++r) {
         const long long idx = base + r * 64 + lane;
         const bool valid = idx < n;
         key[r] = valid ? keys_in[idx] : 0xFFFFFFFFu;
         val[r] = valid ? (vals_in ? vals_in[idx] : (uint32_t)idx) : 0u;
     }
 #pragma unroll
-    for (int r = 0; r < kI; ++r) {
+    for (int r = 0; r < kRI; ++r) {
         const long long idx = base + r * 64 + lane;
         const bool valid = idx < n;
         const uint32_t d = (key[r] >> shift) & mask;
@@ -205,7 +207,7 @@ __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kI; ++r) {
+    for (int r = 0; r < kRI; ++r) {
         const long long idx = base + r * 64 + lane;
         if (idx < n) {
             const uint32_t d = (key[r] >> shift) & mask;
@@ -215,7 +217,7 @@ __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict
         }
     }
     __syncthreads();
-    const int count = (n - bbase) < kSortTile ? (int)(n - bbase) : kSortTile;
+    const int count = (n - bbase) < kRadixTile ? (int)(n - bbase) : kRadixTile;
 #pragma unroll 4
     for (int i = tid; i < count; i += kB) {
         const uint32_t k = skey[i];
@@ -753,13 +755,17 @@ int radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* k0, u
                int* which, hipStream_t s) {
     *which = -1;
     if (cap <= 0) return 0;
-    const int nb = sort_blocks(cap);
+    const int nb = radix_blocks(cap);
     uint32_t* totals = hist + (size_t)256 * (nb + 1);
     const uint32_t* kin = keys_in;
     const uint32_t* vin = vals_in;
     int dst = 0;
-    for (int shift = 0; shift < nbits; shift += 8) {
-        const int bits = (nbits - shift) < 8 ? (nbits - shift) : 8;
+    // the fewest 8-bit-or-narrower passes, digits split evenly (13 tile bits: 7 + 6, not 8 + 5:
+    // half the buckets in the first pass, so each block's runs to scatter are twice as long;
+    // 0.114 vs 0.120 ms at 1M / 1080p, 0.486 vs 0.512 at 5M)
+    const int passes = (nbits + 7) / 8, per = (nbits + passes - 1) / passes;
+    for (int shift = 0; shift < nbits; shift += per) {
+        const int bits = (nbits - shift) < per ? (nbits - shift) : per;
         uint32_t* ko = dst == 0 ? k0 : k1;
         uint32_t* vo = dst == 0 ? v0 : v1;
         hipLaunchKernelGGL(radix_upsweep, dim3(nb), dim3(kB), 0, s, kin, cap, n_dev, shift, bits, nb, hist);
