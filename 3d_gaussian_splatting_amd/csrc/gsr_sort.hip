@@ -809,7 +809,8 @@ int launch_duplicate(const uint32_t* tiles, uint4* rect, int n, int grid_x, int 
 
 int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long K, const uint32_t* depth_key,
                            uint32_t* gid, uint32_t* ovf, uint32_t* ovf_count, uint32_t* ovf2, uint32_t* ovf2_count,
-                           uint32_t* scratch_hi, uint32_t* scratch_lo, hipStream_t s) {
+                           uint32_t* ovf3, uint32_t* ovf3_count, uint32_t* scratch_hi, uint32_t* scratch_lo,
+                           hipStream_t s) {
     if (ntiles <= 0 || K <= 0) return 0;
     // one block per tile holding up to cap entries in LDS, a power of two >= 1.5x the mean slice
     // (1024 .. 4096: <= 43 KB of LDS, 3 blocks per CU); longer slices queue for 512-thread blocks
@@ -827,8 +828,14 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
     const int qgrid = ntiles < 512 ? ntiles : 512;
     hipLaunchKernelGGL((tile_depth_radix_queue<512, 16, 8>), dim3(qgrid), dim3(512), 0, s, ranges, depth_key, gid, ovf,
                        ovf_count, ovf2, ovf2_count);
+    // slices of 8193 .. 16384 (dense tiles of real captures): one 1024-thread block per slice
+    // with the whole slice in LDS (~145 KB: gfx950 gives one workgroup up to 160 KiB); the
+    // global-memory bitonic form it replaces took ~0.9 ms per training-loop frame
+    const int q2grid = ntiles < 256 ? ntiles : 256;
+    hipLaunchKernelGGL((tile_depth_radix_queue<1024, 16, 8>), dim3(q2grid), dim3(1024), 0, s, ranges, depth_key, gid,
+                       ovf2, ovf2_count, ovf3, ovf3_count);
     const int grid = ntiles < 64 ? ntiles : 64;
-    hipLaunchKernelGGL(tile_depth_sort_global, dim3(grid), dim3(1024), 0, s, ranges, depth_key, gid, ovf2, ovf2_count,
+    hipLaunchKernelGGL(tile_depth_sort_global, dim3(grid), dim3(1024), 0, s, ranges, depth_key, gid, ovf3, ovf3_count,
                        scratch_hi, scratch_lo);
     return (int)hipGetLastError();
 }
