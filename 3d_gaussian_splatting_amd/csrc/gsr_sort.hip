@@ -695,25 +695,62 @@ __global__ __launch_bounds__(NT) void tile_depth_radix_queue(const uint2* __rest
     }
 }
 
-// Slices beyond the LDS forms (> 8192 instances in one tile: dense real scenes): a bitonic
-// network in the all-ascending ("flip") form on the slice in global memory, with the 64-bit
-// (depth << 32 | gid) key split into two u32 arrays (the tile sort's free ping-pong pair),
-// virtually padded to a power of two with +inf keys.  Integer work, latency-bound; rare.
+// Slices beyond the LDS tiers (> 16384 instances in one tile: dense training views).  The
+// 64-bit (depth << 32 | gid) key is split into two u32 arrays (the tile sort's free ping-pong pair).
+constexpr int kGlobalChunk = 16384;  // LDS chunk (128 KB of packed key:gid) of the global form
+
+// One bitonic half-cleaner stage (pairs i <-> i + d) over the LDS chunk.  The chunk is padded
+// with ~0 sentinels, which no real (depth, gid) pair reaches (gid < 2^32-1).
+__device__ __forceinline__ void lds_half_cleaner(uint64_t* sk, int d) {
+    for (int t = threadIdx.x; t < kGlobalChunk / 2; t += 1024) {
+        const int i = ((t & ~(d - 1)) << 1) | (t & (d - 1));
+        const uint64_t a = sk[i], b = sk[i + d];
+        if (a > b) sk[i] = b, sk[i + d] = a;
+    }
+    __syncthreads();
+}
+
+// Tiles beyond the 16384-entry LDS tier, step 1: every 16384-entry chunk of the slice sorted in
+// place by the LDS radix slice sort (the chunk is in gid order, so a stable depth sort leaves it
+// in (depth, gid) order).  Up to 8 blocks share a tile (work item w: tile w / 8, chunks w % 8,
+// w % 8 + 8, ...).
+__global__ __launch_bounds__(1024) void tile_depth_chunk_radix(const uint2* __restrict__ ranges,
+                                                               const uint32_t* __restrict__ depth_key,
+                                                               uint32_t* __restrict__ gid,
+                                                               const uint32_t* __restrict__ ovf,
+                                                               const uint32_t* __restrict__ ovf_count) {
+    const uint32_t cnt = *ovf_count;
+    for (uint32_t w = blockIdx.x; (w >> 3) < cnt; w += gridDim.x) {
+        const uint2 r = ranges[ovf[w >> 3]];
+        for (uint32_t c0 = r.x + (w & 7u) * kGlobalChunk; c0 < r.y; c0 += 8u * kGlobalChunk) {
+            const uint32_t c1 = c0 + kGlobalChunk < r.y ? c0 + kGlobalChunk : r.y;
+            radix_sort_slice<1024, 16, 8>(make_uint2(c0, c1), depth_key, gid);
+        }
+    }
+}
+
+// Step 2: the sorted chunks merged by the rest of a bitonic sort of the padded power-of-two
+// range (the all-ascending "flip" form, whose stages through size 16384 the sorted chunks
+// already satisfy).  Strides >= 16384 go through global memory (hi/lo scratch at the tile's
+// offset); the strides below run in LDS one chunk at a time.  A 40k-entry tile takes 3 global
+// passes and 2 x 3 LDS chunk passes instead of the 136 global passes of a plain bitonic sort.
 __global__ __launch_bounds__(1024) void tile_depth_sort_global(const uint2* __restrict__ ranges,
                                                                const uint32_t* __restrict__ depth_key,
                                                                uint32_t* __restrict__ gid,
                                                                const uint32_t* __restrict__ ovf,
                                                                const uint32_t* __restrict__ ovf_count,
                                                                uint32_t* __restrict__ hi, uint32_t* __restrict__ lo) {
+    __shared__ uint64_t sk[kGlobalChunk];
     const uint32_t cnt = *ovf_count;
     for (uint32_t q = blockIdx.x; q < cnt; q += gridDim.x) {
         const uint2 r = ranges[ovf[q]];
         const int n = (int)(r.y - r.x);
-        int m = 1;
+        int m = kGlobalChunk;
         while (m < n) m <<= 1;
+        const int nch = (n + kGlobalChunk - 1) / kGlobalChunk;
         uint32_t* H = hi + r.x;
         uint32_t* L = lo + r.x;
-        for (int i = threadIdx.x; i < n; i += 1024) {
+        for (int i = threadIdx.x; i < n && m > kGlobalChunk; i += 1024) {
             const uint32_t g = gid[r.x + i];
             H[i] = depth_key[g];
             L[i] = g;
@@ -727,25 +764,36 @@ __global__ __launch_bounds__(1024) void tile_depth_sort_global(const uint2* __re
                 H[j] = (uint32_t)(a >> 32), L[j] = (uint32_t)a;
             }
         };
-        for (int size = 2; size <= m; size <<= 1) {
-            const int half = size >> 1;
-            for (int t = threadIdx.x; t < (m >> 1); t += 1024) {
-                const int i = ((t & ~(half - 1)) << 1) | (t & (half - 1));
-                cex(i, i ^ (size - 1));
-            }
-            __threadfence_block();
-            __syncthreads();
-            for (int d = half >> 1; d >= 1; d >>= 1) {
+        for (int size = 2 * kGlobalChunk; size <= m; size <<= 1) {
+            for (int d = size >> 1; d >= kGlobalChunk; d >>= 1) {
+                const bool flip = d == (size >> 1);
                 for (int t = threadIdx.x; t < (m >> 1); t += 1024) {
                     const int i = ((t & ~(d - 1)) << 1) | (t & (d - 1));
-                    cex(i, i + d);
+                    cex(i, flip ? (i ^ (size - 1)) : (i + d));
+                }
+                __threadfence_block();
+                __syncthreads();
+            }
+            const bool last = size == m;
+            for (int c = 0; c < nch; ++c) {
+                const int base = c * kGlobalChunk;
+                for (int i = threadIdx.x; i < kGlobalChunk; i += 1024)
+                    sk[i] = base + i < n ? (((uint64_t)H[base + i] << 32) | L[base + i]) : ~0ull;
+                __syncthreads();
+                for (int d = kGlobalChunk >> 1; d >= 1; d >>= 1) lds_half_cleaner(sk, d);
+                for (int i = threadIdx.x; i < kGlobalChunk && base + i < n; i += 1024) {
+                    const uint64_t v = sk[i];
+                    if (last) {
+                        gid[r.x + base + i] = (uint32_t)v;
+                    } else {
+                        H[base + i] = (uint32_t)(v >> 32);
+                        L[base + i] = (uint32_t)v;
+                    }
                 }
                 __threadfence_block();
                 __syncthreads();
             }
         }
-        for (int i = threadIdx.x; i < n; i += 1024) gid[r.x + i] = L[i];
-        __syncthreads();
     }
 }
 }  // namespace
@@ -834,8 +882,9 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
     const int q2grid = ntiles < 256 ? ntiles : 256;
     hipLaunchKernelGGL((tile_depth_radix_queue<1024, 16, 8>), dim3(q2grid), dim3(1024), 0, s, ranges, depth_key, gid,
                        ovf2, ovf2_count, ovf3, ovf3_count);
-    const int grid = ntiles < 64 ? ntiles : 64;
-    hipLaunchKernelGGL(tile_depth_sort_global, dim3(grid), dim3(1024), 0, s, ranges, depth_key, gid, ovf3, ovf3_count,
+    hipLaunchKernelGGL(tile_depth_chunk_radix, dim3(q2grid), dim3(1024), 0, s, ranges, depth_key, gid, ovf3,
+                       ovf3_count);
+    hipLaunchKernelGGL(tile_depth_sort_global, dim3(q2grid), dim3(1024), 0, s, ranges, depth_key, gid, ovf3, ovf3_count,
                        scratch_hi, scratch_lo);
     return (int)hipGetLastError();
 }

@@ -278,12 +278,24 @@ def test_reference_kat_inputs_through_f1(rast):
 
 
 def test_dense_tiles_sort_paths(rast, oracle):
-    """Tiles holding more instances than the per-tile depth sort's shared-memory form takes:
+    """Tiles holding more instances than the per-tile depth sort's smaller forms take:
     (a) 60k Gaussians on a 64x48 image (12 tiles, ~10^4 instances each) exercise the
-    global-memory form beyond 8192; (b) a cluster of 6000 Gaussians in the middle of a
-    sparse 256x256 scene overflows a 1024-slot tile into the 8192-slot LDS form.  Canonical
-    order, ranges and outputs must still match the oracle."""
+    16384-slot LDS tier beyond 8192; (b) a cluster of 6000 Gaussians in the middle of a
+    sparse 256x256 scene overflows a 1024-slot tile into the 8192-slot LDS form; (c) 200k
+    Gaussians on 64x48 push tiles past 32768 into the chunked global bitonic form (global
+    strides 32768 and 16384, LDS strides below).  Canonical order, ranges and outputs must
+    still match the oracle."""
     gr, sc = pkg("graphics"), pkg("scene")
+    cam = gr.synthetic_camera(64, 48)
+    s = sc.make_scene(cam, 200000, max_sh_degree=0, seed=15)
+    args = (cam, s.means3D, s.opacities, s.scales, s.rotations, s.sh_dc, s.sh_rest)
+    st = rast.forward(*args, sh_degree=0)
+    f = oracle.forward(*args, sh_degree=0)
+    tiles = cam.grid[0] * cam.grid[1]
+    rng = _np(st.view(pkg("native").VIEW_RANGES, torch.int32, 2 * tiles)).view(np.uint32).reshape(-1, 2)
+    assert int((rng[:, 1] - rng[:, 0]).max()) > 32768
+    _compare(st, f, sc.make_dL_dpix(cam, seed=16), rast)
+
     cam = gr.synthetic_camera(64, 48)
     s = sc.make_scene(cam, 60000, max_sh_degree=1, seed=11)
     args = (cam, s.means3D, s.opacities, s.scales, s.rotations, s.sh_dc, s.sh_rest)
