@@ -207,7 +207,7 @@ struct Views {
     float4* rec;
     uint4* rect;
     uint2* ranges;
-    uint32_t *counters, *K_dev, *ovf, *ovf2, *ovf3, *term;
+    uint32_t *counters, *K_dev, *ovf, *ovf2, *done, *term;
     float *final_T, *accum;
     float4* ck;
     uint32_t *kA, *vA, *kB, *vB, *hist;
@@ -232,7 +232,7 @@ Views views(const gsr_camera* cam, long long n, const gsr_buffers* b) {
     v.K_dev = v.counters + kTotalSlot;
     v.ovf = at<uint32_t>(b->image, il.ovf);
     v.ovf2 = at<uint32_t>(b->image, il.ovf2);
-    v.ovf3 = at<uint32_t>(b->image, il.ovf3);
+    v.done = at<uint32_t>(b->image, il.done);
     v.term = at<uint32_t>(b->image, il.term);
     v.final_T = at<float>(b->image, il.final_T);
     v.accum = at<float>(b->image, il.accum);
@@ -334,8 +334,8 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
         GSR_STAGE(GSR_STAGE_FINALIZE, launch_finalize(v.sorted_tile, cap, v.K_dev, v.ranges, stream), "finalize");
         GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_tile_depth_sort(v.ranges, j.ty0 * j.gx, ntiles, cap, v.depth_key,
                                                                v.sorted_gid, v.ovf, v.counters + kOvfCountSlot, v.ovf2,
-                                                               v.counters + kOvf2CountSlot, v.ovf3,
-                                                               v.counters + kOvf3CountSlot, v.free_k, v.free_v, stream),
+                                                               v.counters + kOvf2CountSlot, v.done, v.free_k,
+                                                               v.free_v, stream),
                   "per-tile depth order");
     }
     GSR_STAGE(GSR_STAGE_BLEND_FWD, launch_blend_forward(*cam, j.rs->bg, j.ty0, j.ty1, v.ranges, v.sorted_gid, v.rec,

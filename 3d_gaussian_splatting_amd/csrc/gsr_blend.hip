@@ -150,6 +150,10 @@ __device__ __forceinline__ float pair_alpha_keep(float e, float L, float& oG, bo
 #define GSR_CHUNK_WORK 192
 #endif
 constexpr int kChunkWork = GSR_CHUNK_WORK;
+// Band launches (multi-GPU, < 4096 tiles, 4-wave F6): the chunk bound for B1 there
+#ifndef GSR_BAND_CHUNK_WORK
+#define GSR_BAND_CHUNK_WORK GSR_CHUNK_WORK
+#endif
 
 // F6.  T > 0: pixel live; T <= 0: done, |T| = final transmittance (the T after the last
 // contributor -- the reference's final_T).  A pair is blended when the next transmittance
@@ -168,6 +172,7 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
                                                                 float4* __restrict__ ck) {
     constexpr int PPL = kPPL / NW;
     constexpr int BATCH = 64 * NW;
+    constexpr int kCW = NW > 2 ? GSR_BAND_CHUNK_WORK : kChunkWork;
     __shared__ float4 srec[BATCH * 3];
     __shared__ uint32_t smk[BATCH];
     __shared__ uint32_t slive[NW];
@@ -230,7 +235,7 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
         int visited = 0;
         for (int c0 = 0; c0 < cnt; c0 += 64) {
             const uint32_t sm = smk[c0 + lane];  // 0 past cnt
-            if (work >= kChunkWork && nck < kMaxChunks - 1) {  // chunk nck + 1 starts at base + c0
+            if (work >= kCW && nck < kMaxChunks - 1) {  // chunk nck + 1 starts at base + c0
                 checkpoint(nck);
                 ++nck;
                 if (tid == 0) table[nck] = (uint32_t)(base + c0);

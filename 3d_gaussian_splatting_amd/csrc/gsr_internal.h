@@ -89,7 +89,7 @@ struct BinLayout {
 constexpr int kMaxChunks = 8;
 
 struct ImgLayout {
-    size_t ranges, counters, ovf, ovf2, ovf3, term, final_T, accum, ck, total;
+    size_t ranges, counters, done, ovf, ovf2, term, final_T, accum, ck, total;
     ImgLayout(int W, int H) {
         size_t o = 0;
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
@@ -97,11 +97,10 @@ struct ImgLayout {
         size_t pix = (size_t)W * H;
         if (!tiles) tiles = 1;
         ranges = take(8 * tiles);
-        counters = take(4 * (2 * kCountSlots + 16));  // ranges and counters are contiguous: one
-                                                      // memset clears both
+        counters = take(4 * (2 * kCountSlots + 16));  // ranges, counters and done are contiguous:
+        done = take(4 * tiles);  // one memset clears them (done: chunks sorted per queued tile)
         ovf = take(4 * tiles);   // tiles the per-tile depth sort hands to its larger
-        ovf2 = take(4 * tiles);  // forms (queues: 8192- and 16384-entry LDS forms, then global memory)
-        ovf3 = take(4 * tiles);
+        ovf2 = take(4 * tiles);  // forms (queues: the 8192-entry form, then the 16384-entry / chunked one)
         term = take(4 * tiles * kMaxChunks);  // F6: per tile [termination index, chunk 1..7 starts]
         final_T = take(4 * (pix ? pix : 1));
         accum = take(12 * (pix ? pix : 1));  // colour sum without background, 3 x H x W
@@ -161,8 +160,7 @@ struct ShardLayout {
 // counters[] slots past the preprocess partials (2 x kCountSlots)
 constexpr int kTotalSlot = 2 * kCountSlots;          // K = sum of tiles_touched, written by the scan
 constexpr int kOvfCountSlot = 2 * kCountSlots + 8;   // tiles queued for the large per-tile depth sort
-constexpr int kOvf2CountSlot = 2 * kCountSlots + 9;  // ... then for its 16384-entry LDS form
-constexpr int kOvf3CountSlot = 2 * kCountSlots + 10; // ... and for its global-memory form
+constexpr int kOvf2CountSlot = 2 * kCountSlots + 9;  // ... then for its 16384-entry / chunked form
 
 // number of 8-bit LSD passes to sort tile ids of a grid with `tiles` tiles
 inline int tile_bits(int tiles) {

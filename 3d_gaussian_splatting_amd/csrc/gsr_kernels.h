@@ -58,7 +58,7 @@ int launch_duplicate(const uint32_t* tiles, uint4* rect, int n, int grid_x, int 
 // sort).  K: the binning's capacity (it sizes the LDS form from the mean slice).
 int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long K, const uint32_t* depth_key,
                            uint32_t* gid, uint32_t* ovf, uint32_t* ovf_count, uint32_t* ovf2, uint32_t* ovf2_count,
-                           uint32_t* ovf3, uint32_t* ovf3_count, uint32_t* scratch_hi, uint32_t* scratch_lo,
+                           uint32_t* done, uint32_t* scratch_hi, uint32_t* scratch_lo,
                            hipStream_t s);
 
 // F5: ranges[tile] = [start, end) of the sorted tile keys (K = min(*K_dev, cap))

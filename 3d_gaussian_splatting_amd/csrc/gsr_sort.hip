@@ -526,15 +526,24 @@ __global__ __launch_bounds__(256) void finalize_kernel(const uint32_t* __restric
 // One slice [rg.x, rg.y) of n <= NT * I entries, sorted by the whole block.  Ends with every
 // LDS access behind a barrier, so a block may call it again for another slice.
 template <int NT, int I, int DB>
+struct SliceLds {
+    uint32_t wcnt[NT / 64][1 << DB];
+    uint32_t lbase[1 << DB];
+    uint32_t red[2][NT / 64];
+    uint32_t skey[NT * I];
+    uint32_t sval[NT * I];
+};
+
+template <int NT, int I, int DB>
 __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t* __restrict__ depth_key,
-                                                 uint32_t* __restrict__ gid) {
-    constexpr int NWV = NT / 64, CAP = NT * I, BINS = 1 << DB;
+                                                 uint32_t* __restrict__ gid, SliceLds<NT, I, DB>& lds) {
+    constexpr int NWV = NT / 64, BINS = 1 << DB;
     constexpr uint32_t DMASK = BINS - 1u;
-    __shared__ uint32_t wcnt[NWV][BINS];
-    __shared__ uint32_t lbase[BINS];
-    __shared__ uint32_t red[2][NWV];
-    __shared__ uint32_t skey[CAP];
-    __shared__ uint32_t sval[CAP];
+    auto& wcnt = lds.wcnt;
+    auto& lbase = lds.lbase;
+    auto& red = lds.red;
+    auto& skey = lds.skey;
+    auto& sval = lds.sval;
     const int n = (int)(rg.y - rg.x);
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     // wave w owns [w * per, (w + 1) * per): per = the slice split evenly over the waves in whole
@@ -670,7 +679,8 @@ __global__ __launch_bounds__(NT) void tile_depth_radix(const uint2* __restrict__
         if (threadIdx.x == 0) ovf[atomicAdd(ovf_count, 1u)] = (uint32_t)tile;
         return;
     }
-    radix_sort_slice<NT, I, DB>(rg, depth_key, gid);
+    __shared__ SliceLds<NT, I, DB> lds;
+    radix_sort_slice<NT, I, DB>(rg, depth_key, gid, lds);
 }
 
 // The queued (longer) slices: blocks walk the queue; slices longer than NT * I go on to the
@@ -683,6 +693,7 @@ __global__ __launch_bounds__(NT) void tile_depth_radix_queue(const uint2* __rest
                                                             const uint32_t* __restrict__ ovf,
                                                             const uint32_t* __restrict__ ovf_count,
                                                             uint32_t* __restrict__ ovf2, uint32_t* __restrict__ ovf2_count) {
+    __shared__ SliceLds<NT, I, DB> lds;
     const uint32_t cnt = *ovf_count;
     for (uint32_t q = blockIdx.x; q < cnt; q += gridDim.x) {
         const uint32_t tile = ovf[q];
@@ -691,18 +702,29 @@ __global__ __launch_bounds__(NT) void tile_depth_radix_queue(const uint2* __rest
             if (threadIdx.x == 0) ovf2[atomicAdd(ovf2_count, 1u)] = tile;
             continue;  // block-uniform
         }
-        radix_sort_slice<NT, I, DB>(rg, depth_key, gid);
+        radix_sort_slice<NT, I, DB>(rg, depth_key, gid, lds);
     }
 }
 
-// Slices beyond the LDS tiers (> 16384 instances in one tile: dense training views).  The
-// 64-bit (depth << 32 | gid) key is split into two u32 arrays (the tile sort's free ping-pong pair).
-constexpr int kGlobalChunk = 16384;  // LDS chunk (128 KB of packed key:gid) of the global form
+// Slices of 8193 and more entries (dense tiles of training views): one kernel, 1024-thread
+// blocks, 8 work items per queued tile.  A slice of <= 16384 entries is sorted whole in LDS by
+// item 0 (~145 KB: gfx950 gives one workgroup up to 160 KiB).  A longer slice is cut into
+// 16384-entry chunks, sorted in place by the tile's items in parallel (a chunk is in gid order,
+// so the stable depth sort leaves it in (depth, gid) order), and the item that finishes last
+// (a per-tile counter, device-scope fences on both sides) merges them: the rest of an
+// all-ascending ("flip") bitonic network over the range padded to a power of two, whose stages
+// through size 16384 the sorted chunks already satisfy.  Strides >= 16384 run in global memory
+// on the 64-bit (depth << 32 | gid) key split over two u32 arrays (the tile sort's free
+// ping-pong pair); shorter strides in LDS one chunk at a time.  A 40k-entry tile takes 3 global
+// passes and 2 x 3 LDS chunk passes instead of the 136 global passes of a plain bitonic sort.
+constexpr int kBigChunk = 16384;
+using BigSliceLds = SliceLds<1024, 16, 8>;
+static_assert(sizeof(BigSliceLds) >= kBigChunk * sizeof(uint64_t), "merge chunk aliases the slice LDS");
 
 // One bitonic half-cleaner stage (pairs i <-> i + d) over the LDS chunk.  The chunk is padded
 // with ~0 sentinels, which no real (depth, gid) pair reaches (gid < 2^32-1).
 __device__ __forceinline__ void lds_half_cleaner(uint64_t* sk, int d) {
-    for (int t = threadIdx.x; t < kGlobalChunk / 2; t += 1024) {
+    for (int t = threadIdx.x; t < kBigChunk / 2; t += 1024) {
         const int i = ((t & ~(d - 1)) << 1) | (t & (d - 1));
         const uint64_t a = sk[i], b = sk[i + d];
         if (a > b) sk[i] = b, sk[i + d] = a;
@@ -710,90 +732,105 @@ __device__ __forceinline__ void lds_half_cleaner(uint64_t* sk, int d) {
     __syncthreads();
 }
 
-// Tiles beyond the 16384-entry LDS tier, step 1: every 16384-entry chunk of the slice sorted in
-// place by the LDS radix slice sort (the chunk is in gid order, so a stable depth sort leaves it
-// in (depth, gid) order).  Up to 8 blocks share a tile (work item w: tile w / 8, chunks w % 8,
-// w % 8 + 8, ...).
-__global__ __launch_bounds__(1024) void tile_depth_chunk_radix(const uint2* __restrict__ ranges,
-                                                               const uint32_t* __restrict__ depth_key,
-                                                               uint32_t* __restrict__ gid,
-                                                               const uint32_t* __restrict__ ovf,
-                                                               const uint32_t* __restrict__ ovf_count) {
-    const uint32_t cnt = *ovf_count;
-    for (uint32_t w = blockIdx.x; (w >> 3) < cnt; w += gridDim.x) {
-        const uint2 r = ranges[ovf[w >> 3]];
-        for (uint32_t c0 = r.x + (w & 7u) * kGlobalChunk; c0 < r.y; c0 += 8u * kGlobalChunk) {
-            const uint32_t c1 = c0 + kGlobalChunk < r.y ? c0 + kGlobalChunk : r.y;
-            radix_sort_slice<1024, 16, 8>(make_uint2(c0, c1), depth_key, gid);
+// The big form's LDS: the slice sort's arrays, or the merge's 16384 packed keys.  At namespace
+// scope so that the two out-of-line phases below address it as LDS directly; each has the
+// 128-VGPR budget of a 1024-thread block to itself (inlined into one loop nest, the slice
+// sort's 48 key / value / rank registers spilled).
+__shared__ union BigLds {
+    BigSliceLds slice;
+    uint64_t sk[kBigChunk];
+} g_big;
+
+__device__ __attribute__((noinline)) void big_slice_sort(const uint2 rg, const uint32_t* __restrict__ depth_key,
+                                                         uint32_t* __restrict__ gid) {
+    radix_sort_slice<1024, 16, 8>(rg, depth_key, gid, g_big.slice);
+}
+
+__device__ __attribute__((noinline)) void merge_sorted_chunks(const uint2 r, const uint32_t* __restrict__ depth_key,
+                                                              uint32_t* __restrict__ gid, uint32_t* __restrict__ hi,
+                                                              uint32_t* __restrict__ lo) {
+    uint64_t* const sk = g_big.sk;
+    const int n = (int)(r.y - r.x);
+    int m = kBigChunk;
+    while (m < n) m <<= 1;
+    const int nch = (n + kBigChunk - 1) / kBigChunk;
+    uint32_t* H = hi + r.x;
+    uint32_t* L = lo + r.x;
+    for (int i = threadIdx.x; i < n; i += 1024) {
+        const uint32_t g = gid[r.x + i];
+        H[i] = depth_key[g];
+        L[i] = g;
+    }
+    __syncthreads();
+    auto cex = [&](int i, int j) {  // i < j; indices >= n are +inf padding
+        if (j >= n) return;
+        const uint64_t a = ((uint64_t)H[i] << 32) | L[i], b = ((uint64_t)H[j] << 32) | L[j];
+        if (a > b) {
+            H[i] = (uint32_t)(b >> 32), L[i] = (uint32_t)b;
+            H[j] = (uint32_t)(a >> 32), L[j] = (uint32_t)a;
+        }
+    };
+    for (int size = 2 * kBigChunk; size <= m; size <<= 1) {
+        for (int d = size >> 1; d >= kBigChunk; d >>= 1) {
+            const bool flip = d == (size >> 1);
+            for (int t = threadIdx.x; t < (m >> 1); t += 1024) {
+                const int i = ((t & ~(d - 1)) << 1) | (t & (d - 1));
+                cex(i, flip ? (i ^ (size - 1)) : (i + d));
+            }
+            __syncthreads();
+        }
+        const bool last = size == m;
+        for (int c = 0; c < nch; ++c) {
+            const int base = c * kBigChunk;
+            for (int i = threadIdx.x; i < kBigChunk; i += 1024)
+                sk[i] = base + i < n ? (((uint64_t)H[base + i] << 32) | L[base + i]) : ~0ull;
+            __syncthreads();
+            for (int d = kBigChunk >> 1; d >= 1; d >>= 1) lds_half_cleaner(sk, d);
+            for (int i = threadIdx.x; i < kBigChunk && base + i < n; i += 1024) {
+                const uint64_t v = sk[i];
+                if (last) {
+                    gid[r.x + base + i] = (uint32_t)v;
+                } else {
+                    H[base + i] = (uint32_t)(v >> 32);
+                    L[base + i] = (uint32_t)v;
+                }
+            }
+            __syncthreads();
         }
     }
 }
 
-// Step 2: the sorted chunks merged by the rest of a bitonic sort of the padded power-of-two
-// range (the all-ascending "flip" form, whose stages through size 16384 the sorted chunks
-// already satisfy).  Strides >= 16384 go through global memory (hi/lo scratch at the tile's
-// offset); the strides below run in LDS one chunk at a time.  A 40k-entry tile takes 3 global
-// passes and 2 x 3 LDS chunk passes instead of the 136 global passes of a plain bitonic sort.
-__global__ __launch_bounds__(1024) void tile_depth_sort_global(const uint2* __restrict__ ranges,
-                                                               const uint32_t* __restrict__ depth_key,
-                                                               uint32_t* __restrict__ gid,
-                                                               const uint32_t* __restrict__ ovf,
-                                                               const uint32_t* __restrict__ ovf_count,
-                                                               uint32_t* __restrict__ hi, uint32_t* __restrict__ lo) {
-    __shared__ uint64_t sk[kGlobalChunk];
+__global__ __launch_bounds__(1024) void tile_depth_sort_big(const uint2* __restrict__ ranges,
+                                                            const uint32_t* __restrict__ depth_key,
+                                                            uint32_t* __restrict__ gid,
+                                                            const uint32_t* __restrict__ ovf,
+                                                            const uint32_t* __restrict__ ovf_count,
+                                                            uint32_t* __restrict__ done,
+                                                            uint32_t* __restrict__ hi, uint32_t* __restrict__ lo) {
+    __shared__ uint32_t last;
     const uint32_t cnt = *ovf_count;
-    for (uint32_t q = blockIdx.x; q < cnt; q += gridDim.x) {
+    // item-major: the first cnt work items are every tile's item 0, spread over all blocks
+    for (uint32_t w = blockIdx.x; w < 8u * cnt; w += gridDim.x) {
+        const uint32_t q = w % cnt, item = w / cnt;
         const uint2 r = ranges[ovf[q]];
-        const int n = (int)(r.y - r.x);
-        int m = kGlobalChunk;
-        while (m < n) m <<= 1;
-        const int nch = (n + kGlobalChunk - 1) / kGlobalChunk;
-        uint32_t* H = hi + r.x;
-        uint32_t* L = lo + r.x;
-        for (int i = threadIdx.x; i < n && m > kGlobalChunk; i += 1024) {
-            const uint32_t g = gid[r.x + i];
-            H[i] = depth_key[g];
-            L[i] = g;
+        const uint32_t n = r.y - r.x;
+        // a slice of <= kBigChunk entries is item 0's whole; a longer one is cut into chunks
+        const bool whole = n <= (uint32_t)kBigChunk;
+        const uint32_t nch = whole ? 1u : (n + kBigChunk - 1) / kBigChunk;
+        const uint32_t parts = nch < 8u ? nch : 8u;
+        if (item >= parts) continue;  // block-uniform
+        for (uint32_t c0 = r.x + item * kBigChunk; c0 < r.y; c0 += 8u * kBigChunk) {
+            const uint32_t c1 = whole || c0 + kBigChunk >= r.y ? r.y : c0 + kBigChunk;
+            big_slice_sort(make_uint2(c0, c1), depth_key, gid);
         }
+        if (whole) continue;
+        __threadfence();  // this item's chunks visible device-wide before it counts itself done
         __syncthreads();
-        auto cex = [&](int i, int j) {  // i < j; indices >= n are +inf padding
-            if (j >= n) return;
-            const uint64_t a = ((uint64_t)H[i] << 32) | L[i], b = ((uint64_t)H[j] << 32) | L[j];
-            if (a > b) {
-                H[i] = (uint32_t)(b >> 32), L[i] = (uint32_t)b;
-                H[j] = (uint32_t)(a >> 32), L[j] = (uint32_t)a;
-            }
-        };
-        for (int size = 2 * kGlobalChunk; size <= m; size <<= 1) {
-            for (int d = size >> 1; d >= kGlobalChunk; d >>= 1) {
-                const bool flip = d == (size >> 1);
-                for (int t = threadIdx.x; t < (m >> 1); t += 1024) {
-                    const int i = ((t & ~(d - 1)) << 1) | (t & (d - 1));
-                    cex(i, flip ? (i ^ (size - 1)) : (i + d));
-                }
-                __threadfence_block();
-                __syncthreads();
-            }
-            const bool last = size == m;
-            for (int c = 0; c < nch; ++c) {
-                const int base = c * kGlobalChunk;
-                for (int i = threadIdx.x; i < kGlobalChunk; i += 1024)
-                    sk[i] = base + i < n ? (((uint64_t)H[base + i] << 32) | L[base + i]) : ~0ull;
-                __syncthreads();
-                for (int d = kGlobalChunk >> 1; d >= 1; d >>= 1) lds_half_cleaner(sk, d);
-                for (int i = threadIdx.x; i < kGlobalChunk && base + i < n; i += 1024) {
-                    const uint64_t v = sk[i];
-                    if (last) {
-                        gid[r.x + base + i] = (uint32_t)v;
-                    } else {
-                        H[base + i] = (uint32_t)(v >> 32);
-                        L[base + i] = (uint32_t)v;
-                    }
-                }
-                __threadfence_block();
-                __syncthreads();
-            }
-        }
+        if (threadIdx.x == 0) last = atomicAdd(done + q, 1u) == parts - 1u ? 1u : 0u;
+        __syncthreads();
+        if (!last) continue;  // block-uniform
+        __threadfence();      // acquire: the other items' chunks
+        merge_sorted_chunks(r, depth_key, gid, hi, lo);
     }
 }
 }  // namespace
@@ -857,35 +894,40 @@ int launch_duplicate(const uint32_t* tiles, uint4* rect, int n, int grid_x, int 
 
 int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long K, const uint32_t* depth_key,
                            uint32_t* gid, uint32_t* ovf, uint32_t* ovf_count, uint32_t* ovf2, uint32_t* ovf2_count,
-                           uint32_t* ovf3, uint32_t* ovf3_count, uint32_t* scratch_hi, uint32_t* scratch_lo,
+                           uint32_t* done, uint32_t* scratch_hi, uint32_t* scratch_lo,
                            hipStream_t s) {
     if (ntiles <= 0 || K <= 0) return 0;
     // one block per tile holding up to cap entries in LDS, a power of two >= 1.5x the mean slice
     // (1024 .. 4096: <= 43 KB of LDS, 3 blocks per CU); longer slices queue for 512-thread blocks
-    // of up to 8192 (73 KB: 2 per CU) walking the queue, and beyond that for the global form
+    // of up to 8192 (73 KB: 2 per CU) walking the queue, and beyond that for tile_depth_sort_big
     const long long mean = K / ntiles;
     int cap = 1024;
     while (cap < 4096 && cap < mean + mean / 2) cap <<= 1;
 #define GSR_TILE_RADIX(NT_, I_)                                                                          \
     hipLaunchKernelGGL((tile_depth_radix<NT_, I_, 9>), dim3(ntiles), dim3(NT_), 0, s, ranges, tile0, depth_key, \
                        gid, ovf, ovf_count)
-    if (cap == 1024) GSR_TILE_RADIX(256, 4);
+#ifndef GSR_BAND_SORT_NT
+#define GSR_BAND_SORT_NT 512
+#endif
+    if (ntiles < 4096 && GSR_BAND_SORT_NT == 512) {  // band launches: fewer tiles, wider blocks
+        if (cap == 1024) GSR_TILE_RADIX(512, 2);
+        else if (cap == 2048) GSR_TILE_RADIX(512, 4);
+        else GSR_TILE_RADIX(512, 8);
+    } else if (ntiles < 4096 && GSR_BAND_SORT_NT == 1024) {
+        if (cap == 1024) GSR_TILE_RADIX(1024, 1);
+        else if (cap == 2048) GSR_TILE_RADIX(1024, 2);
+        else GSR_TILE_RADIX(1024, 4);
+    } else if (cap == 1024) GSR_TILE_RADIX(256, 4);
     else if (cap == 2048) GSR_TILE_RADIX(256, 8);
     else GSR_TILE_RADIX(256, 16);
 #undef GSR_TILE_RADIX
     const int qgrid = ntiles < 512 ? ntiles : 512;
     hipLaunchKernelGGL((tile_depth_radix_queue<512, 16, 8>), dim3(qgrid), dim3(512), 0, s, ranges, depth_key, gid, ovf,
                        ovf_count, ovf2, ovf2_count);
-    // slices of 8193 .. 16384 (dense tiles of real captures): one 1024-thread block per slice
-    // with the whole slice in LDS (~145 KB: gfx950 gives one workgroup up to 160 KiB); the
-    // global-memory bitonic form it replaces took ~0.9 ms per training-loop frame
-    const int q2grid = ntiles < 256 ? ntiles : 256;
-    hipLaunchKernelGGL((tile_depth_radix_queue<1024, 16, 8>), dim3(q2grid), dim3(1024), 0, s, ranges, depth_key, gid,
-                       ovf2, ovf2_count, ovf3, ovf3_count);
-    hipLaunchKernelGGL(tile_depth_chunk_radix, dim3(q2grid), dim3(1024), 0, s, ranges, depth_key, gid, ovf3,
-                       ovf3_count);
-    hipLaunchKernelGGL(tile_depth_sort_global, dim3(q2grid), dim3(1024), 0, s, ranges, depth_key, gid, ovf3, ovf3_count,
-                       scratch_hi, scratch_lo);
+    // slices beyond 8192: the 16384-entry LDS form and the chunked form (tile_depth_sort_big)
+    const int bgrid = ntiles < 256 ? ntiles : 256;
+    hipLaunchKernelGGL(tile_depth_sort_big, dim3(bgrid), dim3(1024), 0, s, ranges, depth_key, gid, ovf2, ovf2_count,
+                       done, scratch_hi, scratch_lo);
     return (int)hipGetLastError();
 }
 

@@ -32,7 +32,10 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--config", default="5m_1080p", choices=sorted(bench.CONFIGS))
     ap.add_argument("--no-single", action="store_true", help="skip the single-GPU reference step (kernel traces)")
+    ap.add_argument("--lib", default=None, help="an experimental libgsr_hip.so (_build.build_variant)")
     args = ap.parse_args()
+    if args.lib:
+        importlib.import_module(f"{PKG}.native").HIP_LIB = os.path.abspath(args.lib)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     cfg = bench.CONFIGS[args.config]
