@@ -418,6 +418,10 @@ __device__ __forceinline__ void preprocess_backward_one(const gsr_camera& cam, c
     out.rots[4 * o + 3] = 2.f * (-2.f * z * dR[0] - r * dR[1] + x * dR[2] + r * dR[3] - 2.f * z * dR[4] + y * dR[5] + x * dR[6] + y * dR[7]);
 }
 
+#ifndef GSR_B2_VEC4
+#define GSR_B2_VEC4 1
+#endif
+
 // Gaussians [g0, g0 + n): inputs indexed by g, grad2d and every output by o = g - g0.
 __global__ __launch_bounds__(256) void preprocess_backward_kernel(
     const gsr_camera cam, const GaussIn in, int g0, int n, const uint32_t* __restrict__ depth_key,
@@ -430,14 +434,32 @@ __global__ __launch_bounds__(256) void preprocess_backward_kernel(
     const size_t obase = (size_t)blockIdx.x * 256 * M3, ibase = (size_t)g0 * M3 + obase;
     BwdIn bi{};
     if (o < n) bi = load_bwd_in(in, g0 + o, o, depth_key, flags, grad2d);
+    // 16-B staging when the rows start 16-B aligned (always for g0 = 0: a block's 256 rows are
+    // 46080 B); 4-B otherwise
+    const bool v4 = GSR_B2_VEC4 && ((reinterpret_cast<uintptr_t>(in.sh_rest + ibase) |
+                                     reinterpret_cast<uintptr_t>(out.sh_rest + obase)) & 15u) == 0;
     if (stage) {  // coalesced staging of the block's SH-rest rows (see preprocess_kernel)
-        for (int i = threadIdx.x; i < rows * M3; i += 256) sh_lds[i] = in.sh_rest[ibase + i];
+        const int nf = rows * M3;
+        if (v4) {
+            const float4* src = reinterpret_cast<const float4*>(in.sh_rest + ibase);
+            for (int i = threadIdx.x; i < nf / 4; i += 256) reinterpret_cast<float4*>(sh_lds)[i] = src[i];
+            for (int i = (nf & ~3) + threadIdx.x; i < nf; i += 256) sh_lds[i] = in.sh_rest[ibase + i];
+        } else {
+            for (int i = threadIdx.x; i < nf; i += 256) sh_lds[i] = in.sh_rest[ibase + i];
+        }
         __syncthreads();
     }
     if (o < n) preprocess_backward_one(cam, in, g0 + o, o, bi, flags, out, stage ? sh_lds + threadIdx.x * M3 : nullptr);
     if (stage) {  // coalesced write-back of the SH-rest gradient rows
         __syncthreads();
-        for (int i = threadIdx.x; i < rows * M3; i += 256) out.sh_rest[obase + i] = sh_lds[i];
+        const int nf = rows * M3;
+        if (v4) {
+            float4* dst = reinterpret_cast<float4*>(out.sh_rest + obase);
+            for (int i = threadIdx.x; i < nf / 4; i += 256) dst[i] = reinterpret_cast<const float4*>(sh_lds)[i];
+            for (int i = (nf & ~3) + threadIdx.x; i < nf; i += 256) out.sh_rest[obase + i] = sh_lds[i];
+        } else {
+            for (int i = threadIdx.x; i < nf; i += 256) out.sh_rest[obase + i] = sh_lds[i];
+        }
     }
 }
 
