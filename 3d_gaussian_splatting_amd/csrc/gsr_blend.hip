@@ -198,7 +198,7 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
     // live (anywhere in the tile) at the start of its batch -- block-uniform, so every wave takes
     // the same chunk decisions, including a wave whose own pixels have all finished (it keeps
     // writing its final state at the later checkpoints).
-    uint32_t* const table = term + (size_t)tl * kMaxChunks;  // [term, chunk 1..7 starts]
+    uint32_t* const table = term + (size_t)tl * kMaxChunks;  // [term, chunk 1.. starts]
     int nck = 0;   // checkpoints written
     int work = 0;  // pairs in the current chunk
     int tend = n;  // termination index: every pixel of the tile has finished before record tend
@@ -390,7 +390,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
     const int tile = tl + geo.ty0 * geo.grid_x;
     const uint2 range = ranges[tile];
     const int n_all = (int)(range.y - range.x);
-    // F6's chunk table: [termination index, chunk 1..7 starts (UINT32_MAX: none)]
+    // F6's chunk table: [termination index, chunk 1..kMaxChunks-1 starts (UINT32_MAX: none)]
     const uint32_t* table = term + (size_t)tl * kMaxChunks;
     const uint32_t tend = table[0];
     const uint32_t start_u = chunk == 0 ? 0u : table[chunk];

@@ -86,7 +86,10 @@ struct BinLayout {
 // current chunk holds kChunkWork of them.  Chunks are therefore balanced in work whatever the
 // list length, no checkpoint is written past the tile's termination (every pixel finished),
 // and the per-tile chunk table (term[]) tells B1 where each chunk starts.
-constexpr int kMaxChunks = 8;
+#ifndef GSR_MAX_CHUNKS
+#define GSR_MAX_CHUNKS 32
+#endif
+constexpr int kMaxChunks = GSR_MAX_CHUNKS;  // = GSR_TERM_STRIDE (gsr.h) in the shipped build
 
 struct ImgLayout {
     size_t ranges, counters, done, ovf, ovf2, term, final_T, accum, ck, total;
@@ -101,7 +104,7 @@ struct ImgLayout {
         done = take(4 * tiles);  // one memset clears them (done: chunks sorted per queued tile)
         ovf = take(4 * tiles);   // tiles the per-tile depth sort hands to its larger
         ovf2 = take(4 * tiles);  // forms (queues: the 8192-entry form, then the 16384-entry / chunked one)
-        term = take(4 * tiles * kMaxChunks);  // F6: per tile [termination index, chunk 1..7 starts]
+        term = take(4 * tiles * kMaxChunks);  // F6: per tile [termination index, chunk 1..kMaxChunks-1 starts]
         final_T = take(4 * (pix ? pix : 1));
         accum = take(12 * (pix ? pix : 1));  // colour sum without background, 3 x H x W
         ck = take(tiles * (kMaxChunks - 1) * 256 * 16);  // float4 (T, C) checkpoints

@@ -227,9 +227,10 @@ int gsr_shard_backward(const gsr_camera* cam, const gsr_gaussians* shard, const 
 #define GSR_VIEW_DEPTH_KEY 6        /* uint32[P]: depth bits, 0xFFFFFFFF when culled       */
 #define GSR_VIEW_TILES_TOUCHED 7    /* uint32[P]                                           */
 #define GSR_VIEW_COUNTS 9           /* uint32[1]: K, written by the scan (device)          */
-#define GSR_VIEW_TERM 10            /* uint32[tiles*8]: per tile the F6 termination index,
-                                       then the B1 chunk 1..7 start records (UINT32_MAX:
-                                       no such chunk)                                      */
+#define GSR_VIEW_TERM 10            /* uint32[tiles*GSR_TERM_STRIDE]: per tile the F6
+                                       termination index, then the B1 chunk 1..31 start
+                                       records (UINT32_MAX: no such chunk)                 */
+#define GSR_TERM_STRIDE 32          /* words per tile of GSR_VIEW_TERM                     */
 #define GSR_VIEW_RECORDS 8          /* float4[3*P]: {x,y,a',b'},{c',o,r,g},{b,ext_x,ext_y,log2 o};
                                        a',b',c' = -log2(e) * (A/2, B, C/2) of the conic */
 const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, int what);

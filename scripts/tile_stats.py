@@ -34,7 +34,8 @@ def main():
                                        sh_dc=t(s.sh_dc), sh_rest=t(s.sh_rest), sh_degree=cfg["D"])
     gx, gy = cam.grid
     ranges = st.view(native.VIEW_RANGES, torch.int32, 2 * gx * gy).cpu().numpy().reshape(-1, 2)
-    table = st.view(native.VIEW_TERM, torch.int32, 8 * gx * gy).cpu().numpy().view(np.uint32).reshape(-1, 8)
+    table = st.view(native.VIEW_TERM, torch.int32, native.TERM_STRIDE * gx * gy).cpu().numpy().view(np.uint32)
+    table = table.reshape(-1, native.TERM_STRIDE)
     term = table[:, 0].astype(np.int64)
     n = ranges[:, 1] - ranges[:, 0]
     chunks = 1 + (table[:, 1:] != 0xFFFFFFFF).sum(1)
