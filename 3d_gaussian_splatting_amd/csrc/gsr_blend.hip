@@ -541,7 +541,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
 // has too few tiles to fill the chip (multi-GPU bands).  Measured at 1M/1080p with the
 // branchless stripe pair: 2 waves 0.258 ms, 1 wave 0.269 (with branches) / 0.343 (branchless,
 // 4 stripes), 4 waves 0.299.
-constexpr int kF6FullWaves = 2, kF6BandWaves = 4, kF6BandTiles = 4096;
+#ifndef GSR_F6_BAND_TILES
+#define GSR_F6_BAND_TILES 4096
+#endif
+constexpr int kF6FullWaves = 2, kF6BandWaves = 4, kF6BandTiles = GSR_F6_BAND_TILES;
 
 static BlendGeom make_geo(const gsr_camera& cam, const float bg[3], int ty0, int ty1) {
     BlendGeom g;

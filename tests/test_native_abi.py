@@ -49,6 +49,15 @@ def test_train_abi_validation_without_gpu():
     assert L.gsr_densify_stats(None, None, 4, None, None, None, None) < 0
 
 
+def test_header_constants_match_the_python_mirror():
+    """#define constants of gsr.h that the Python mirror restates (native.py)."""
+    native = pkg("native")
+    text = open(HEADER).read()
+    val = lambda name: int(re.search(rf"#define {name} (\d+)", text).group(1))
+    assert val("GSR_TERM_STRIDE") == native.TERM_STRIDE
+    assert val("GSR_VIEW_TERM") == native.VIEW_TERM
+
+
 def test_library_exports_every_symbol():
     native = pkg("native")
     so = native.hip_library_path()
