@@ -5,7 +5,8 @@
 //                         src/scene/gaussian_model.cpp:270-298), one thread per Gaussian.
 //  * ssim_forward_kernel  L1 + SSIM terms of one 64 x 16 output tile per block: the raw tile
 //                         plus a 5-pixel halo is staged in LDS, blurred horizontally (5 moment
-//                         maps) into LDS and vertically in registers; writes the three SSIM
+//                         maps) into LDS and vertically in registers (each pass slides the
+//                         11-tap window over 4 outputs per thread); writes the three SSIM
 //                         derivative maps the backward blurs, and one (sum S, sum |x - y|)
 //                         partial per block (fixed-order sums, no atomics).
 //  * ssim_backward_kernel the adjoint: blur of the three maps (same separable window) combined
@@ -103,23 +104,35 @@ __global__ __launch_bounds__(256) void ssim_forward_kernel(const float* __restri
         sy[r * kRXP + cc] = in ? Y[o] : 0.0f;
     }
     __syncthreads();
-    for (int i = tid; i < kRY * kTX; i += 256) {
-        const int r = i / kTX, cc = i - r * kTX;
-        float mx = 0.f, my = 0.f, xx = 0.f, yy = 0.f, xy = 0.f;
+    // horizontal pass: a thread slides the window over 4 adjacent columns of one row (14 LDS reads
+    // of x and y for 4 outputs instead of 44); each output still sums its taps in k order
+    for (int i = tid; i < kRY * (kTX / 4); i += 256) {
+        const int r = i / (kTX / 4), c0 = 4 * (i - r * (kTX / 4));
+        float m[4][5];
 #pragma unroll
-        for (int k = 0; k < kWin; ++k) {
-            const float a = sx[r * kRXP + cc + k], b = sy[r * kRXP + cc + k], w = win.w[k];
-            mx = fmaf(w, a, mx);
-            my = fmaf(w, b, my);
-            xx = fmaf(w, a * a, xx);
-            yy = fmaf(w, b * b, yy);
-            xy = fmaf(w, a * b, xy);
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int q = 0; q < 5; ++q) m[j][q] = 0.f;
+#pragma unroll
+        for (int t = 0; t < kWin + 3; ++t) {
+            const float a = sx[r * kRXP + c0 + t], b = sy[r * kRXP + c0 + t];
+            const float aa = a * a, bb = b * b, ab = a * b;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int k = t - j;
+                if (k < 0 || k >= kWin) continue;
+                const float w = win.w[k];
+                m[j][0] = fmaf(w, a, m[j][0]);
+                m[j][1] = fmaf(w, b, m[j][1]);
+                m[j][2] = fmaf(w, aa, m[j][2]);
+                m[j][3] = fmaf(w, bb, m[j][3]);
+                m[j][4] = fmaf(w, ab, m[j][4]);
+            }
         }
-        hs[0][i] = mx;
-        hs[1][i] = my;
-        hs[2][i] = xx;
-        hs[3][i] = yy;
-        hs[4][i] = xy;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int q = 0; q < 5; ++q) hs[q][r * kTX + c0 + j] = m[j][q];
     }
     __syncthreads();
     float ssum = 0.f, l1sum = 0.f;
@@ -127,16 +140,33 @@ __global__ __launch_bounds__(256) void ssim_forward_kernel(const float* __restri
     float* A = maps;
     float* B = maps + all;
     float* Cm = maps + 2 * all;
-    for (int i = tid; i < kTY * kTX; i += 256) {
-        const int r = i / kTX, cc = i - r * kTX;
-        const int gx = x0 + cc, gy = y0 + r;
-        float m[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    // vertical pass: thread (column cc, row group rg) slides over rows 4 rg .. 4 rg + 3 (14 LDS
+    // reads per moment for 4 outputs instead of 44), taps summed in k order as before
+    const int cc = tid & (kTX - 1), r0 = 4 * (tid >> 6);
+    float mv[4][5];
 #pragma unroll
-        for (int k = 0; k < kWin; ++k) {
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < 5; ++q) mv[j][q] = 0.f;
+#pragma unroll
+    for (int t = 0; t < kWin + 3; ++t) {
+        float h[5];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) h[q] = hs[q][(r0 + t) * kTX + cc];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = t - j;
+            if (k < 0 || k >= kWin) continue;
             const float w = win.w[k];
 #pragma unroll
-            for (int q = 0; q < 5; ++q) m[q] = fmaf(w, hs[q][(r + k) * kTX + cc], m[q]);
+            for (int q = 0; q < 5; ++q) mv[j][q] = fmaf(w, h[q], mv[j][q]);
         }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int r = r0 + j;
+        const int gx = x0 + cc, gy = y0 + r;
+        const float* m = mv[j];
         if (gx >= W || gy >= H) continue;
         const float mu1 = m[0], mu2 = m[1];
         const float mu1_sq = mu1 * mu1, mu2_sq = mu2 * mu2, mu12 = mu1 * mu2;
@@ -203,35 +233,62 @@ __global__ __launch_bounds__(256) void ssim_backward_kernel(const float* __restr
         for (int q = 0; q < 3; ++q) sm[q][r * kRXP + cc] = in ? maps[q * all + o] : 0.0f;
     }
     __syncthreads();
-    for (int i = tid; i < kRY * kTX; i += 256) {
-        const int r = i / kTX, cc = i - r * kTX;
-        float m[3] = {0.f, 0.f, 0.f};
+    for (int i = tid; i < kRY * (kTX / 4); i += 256) {  // horizontal, 4 columns per thread
+        const int r = i / (kTX / 4), c0 = 4 * (i - r * (kTX / 4));
+        float m[4][3];
 #pragma unroll
-        for (int k = 0; k < kWin; ++k) {
-            const float w = win.w[k];
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int q = 0; q < 3; ++q) m[q] = fmaf(w, sm[q][r * kRXP + cc + k], m[q]);
+            for (int q = 0; q < 3; ++q) m[j][q] = 0.f;
+#pragma unroll
+        for (int t = 0; t < kWin + 3; ++t) {
+            float v[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) v[q] = sm[q][r * kRXP + c0 + t];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int k = t - j;
+                if (k < 0 || k >= kWin) continue;
+                const float w = win.w[k];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) m[j][q] = fmaf(w, v[q], m[j][q]);
+            }
         }
 #pragma unroll
-        for (int q = 0; q < 3; ++q) hs[q][i] = m[q];
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) hs[q][r * kTX + c0 + j] = m[j][q];
     }
     __syncthreads();
-    for (int i = tid; i < kTY * kTX; i += 256) {
-        const int r = i / kTX, cc = i - r * kTX;
-        const int gx = x0 + cc, gy = y0 + r;
-        if (gx >= W || gy >= H) continue;
-        float m[3] = {0.f, 0.f, 0.f};
+    const int cc = tid & (kTX - 1), r0 = 4 * (tid >> 6);  // vertical, 4 rows per thread
+    float mv[4][3];
 #pragma unroll
-        for (int k = 0; k < kWin; ++k) {
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) mv[j][q] = 0.f;
+#pragma unroll
+    for (int t = 0; t < kWin + 3; ++t) {
+        float h[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) h[q] = hs[q][(r0 + t) * kTX + cc];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = t - j;
+            if (k < 0 || k >= kWin) continue;
             const float w = win.w[k];
 #pragma unroll
-            for (int q = 0; q < 3; ++q) m[q] = fmaf(w, hs[q][(r + k) * kTX + cc], m[q]);
+            for (int q = 0; q < 3; ++q) mv[j][q] = fmaf(w, h[q], mv[j][q]);
         }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int gx = x0 + cc, gy = y0 + r0 + j;
+        if (gx >= W || gy >= H) continue;
         const size_t o = c * plane + (size_t)gy * W + gx;
         const float x = img[o], y = gt[o];
         const float d = x - y;
         const float sgn = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
-        dimg[o] = fmaf(l1scale, sgn, m[0] + 2.0f * x * m[1] + y * m[2]);
+        dimg[o] = fmaf(l1scale, sgn, mv[j][0] + 2.0f * x * mv[j][1] + y * mv[j][2]);
     }
 }
 
