@@ -782,6 +782,7 @@ const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, 
         case GSR_VIEW_RECORDS: return v.rec;
         case GSR_VIEW_COUNTS: return v.K_dev;
         case GSR_VIEW_TERM: return v.term;
+        case GSR_VIEW_CK_LIVE: return v.ck + ck_live_offset(ImgLayout::tile_count(cam->width, cam->height));
         default: return nullptr;
     }
 }

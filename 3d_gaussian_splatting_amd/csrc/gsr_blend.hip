@@ -71,7 +71,7 @@ __device__ __forceinline__ void quad_reduce(float (&v)[N]) {
 
 
 struct BlendGeom {
-    int W, H, grid_x, ty0, nwg;
+    int W, H, grid_x, ty0, nwg, ntiles;  // ntiles: the full image's tiles (checkpoint layout)
     float bg0, bg1, bg2;
 };
 
@@ -202,10 +202,19 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
     int nck = 0;   // checkpoints written
     int work = 0;  // pairs in the current chunk
     int tend = n;  // termination index: every pixel of the tile has finished before record tend
-    auto checkpoint = [&](int c) {
-        float4* dst = ck + ((size_t)tl * (kMaxChunks - 1) + c) * 256;
+    // A stripe with no live pixel (its `live` bit clear: conservative, the bit is cleared only
+    // once every T <= 0) is not written; its byte tells B1 to start it dead (T = -1), which is
+    // all B1 needs of a finished pixel.
+    uint8_t* const ckm = reinterpret_cast<uint8_t*>(ck + ck_live_offset(geo.ntiles));
+    auto checkpoint = [&](int c, uint32_t lv) {
+        const size_t slot = (size_t)tl * (kMaxChunks - 1) + c;
+        float4* dst = ck + slot * 256;
 #pragma unroll
-        for (int p = 0; p < PPL; ++p) dst[64 * (w * PPL + p) + lane] = make_float4(T[p], C0[p], C1[p], C2[p]);
+        for (int p = 0; p < PPL; ++p) {
+            const bool on = (lv >> p) & 1u;  // wave-uniform
+            if (on) dst[64 * (w * PPL + p) + lane] = make_float4(T[p], C0[p], C1[p], C2[p]);
+            if (lane == 0) ckm[4 * slot + w * PPL + p] = on ? 1 : 0;
+        }
     };
     for (int base = 0; base < n; base += BATCH) {
         uint32_t live = 0;
@@ -236,7 +245,7 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
         for (int c0 = 0; c0 < cnt; c0 += 64) {
             const uint32_t sm = smk[c0 + lane];  // 0 past cnt
             if (work >= kCW && nck < kMaxChunks - 1) {  // chunk nck + 1 starts at base + c0
-                checkpoint(nck);
+                checkpoint(nck, live);
                 ++nck;
                 if (tid == 0) table[nck] = (uint32_t)(base + c0);
                 work = 0;
@@ -316,6 +325,12 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
 // from LDS in fixed quad order and stored straight to the partial arrays at the record's
 // emission index j (8 moments in part8[2j..2j+1], the 9th in part1[j]).
 constexpr int kPark = 4;
+#ifndef GSR_B1_ILP
+#define GSR_B1_ILP 0
+#endif
+#ifndef GSR_B1_NOBRANCH
+#define GSR_B1_NOBRANCH 0
+#endif
 // Parking slot stride: 16 quads x 12 floats, padded by 12 so that the flush's 36 lanes (4 slots
 // x 9 moments) read 36 distinct banks -- at 192 the 4 slots alias (4-way LDS bank conflicts,
 // ~1 conflict cycle per LDS instruction of B1 in the PMC pass).
@@ -426,12 +441,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
         T[p] = in ? 1.0f : -1.0f;
     }
     if (chunk > 0) {  // resume from F6's checkpoint: T, and R less dL/dpix . (colour sum so far)
-        const float4* src = ck + ((size_t)tl * (kMaxChunks - 1) + (chunk - 1)) * 256;
+        const size_t slot = (size_t)tl * (kMaxChunks - 1) + (chunk - 1);
+        const float4* src = ck + slot * 256;
+        // F6's live-stripe bytes: a stripe it did not write had finished (start it dead)
+        const uint32_t on = *reinterpret_cast<const uint32_t*>(
+            reinterpret_cast<const uint8_t*>(ck + ck_live_offset(geo.ntiles)) + 4 * slot);
 #pragma unroll
         for (int p = 0; p < kPPL; ++p) {
-            const float4 c4 = src[64 * p + col + 16 * row];  // F6's lane of this pixel
-            T[p] = c4.x;
-            R[p] -= fmaf(c4.y, dp0[p], fmaf(c4.z, dp1[p], c4.w * dp2[p]));
+            if ((on >> (8 * p)) & 0xFFu) {  // wave-uniform
+                const float4 c4 = src[64 * p + col + 16 * row];  // F6's lane of this pixel
+                T[p] = c4.x;
+                R[p] -= fmaf(c4.y, dp0[p], fmaf(c4.z, dp1[p], c4.w * dp2[p]));
+            } else {
+                T[p] = -1.0f;
+            }
         }
     }
     for (int base = start; base < n; base += 64) {
@@ -487,12 +510,37 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                 const float w = a * T[p];
                 const float tT = T[p] - w;
                 const bool ok = tT >= 0.0001f;
+#if GSR_B1_NOBRANCH
+                {  // experiment: every lane of a visited stripe runs the contribution, masked
+                    const bool c = ok && keep;
+                    any |= c;
+                    const float wc = c ? w : 0.0f;
+                    const float cdp = fmaf(r1.z, dp0[p], fmaf(r1.w, dp1[p], r2.x * dp2[p]));
+                    const float num = fmaf(T[p], cdp, -R[p]);
+                    R[p] = fmaf(-wc, cdp, R[p]);
+                    g0 = fmaf(wc, dp0[p], g0);
+                    g1 = fmaf(wc, dp1[p], g1);
+                    g2 = fmaf(wc, dp2[p], g2);
+                    const float sv = c ? oG * (num * __builtin_amdgcn_rcpf(1.0f - a)) : 0.0f;
+                    s0 += sv;
+                    const float svy = sv * dy;
+                    sy += svy;
+                    syy = fmaf(svy, dy, syy);
+                }
+#else
                 if (ok && keep) {
                     any = true;
                     const float one_m = 1.0f - a;
                     const float cdp = fmaf(r1.z, dp0[p], fmaf(r1.w, dp1[p], r2.x * dp2[p]));
+#if GSR_B1_ILP
+                    // experiment: dL/dalpha = (T c.dp - R_old) / (1 - alpha), independent of the R update
+                    const float num = fmaf(T[p], cdp, -R[p]);
+                    R[p] = fmaf(-w, cdp, R[p]);
+                    const float dLda = num * __builtin_amdgcn_rcpf(one_m);
+#else
                     R[p] = fmaf(-w, cdp, R[p]);
                     const float dLda = fmaf(T[p], cdp, -R[p] * __builtin_amdgcn_rcpf(one_m));
+#endif
                     g0 = fmaf(w, dp0[p], g0);
                     g1 = fmaf(w, dp1[p], g1);
                     g2 = fmaf(w, dp2[p], g2);
@@ -502,6 +550,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                     sy += svy;
                     syy = fmaf(svy, dy, syy);
                 }
+#endif
                 T[p] = ok ? tT : -fabsf(T[p]);
             }
             if (__any(any)) {
@@ -553,6 +602,7 @@ static BlendGeom make_geo(const gsr_camera& cam, const float bg[3], int ty0, int
     g.grid_x = div_up(cam.width, kTile);
     g.ty0 = ty0;
     g.nwg = (ty1 - ty0) * g.grid_x;
+    g.ntiles = div_up(cam.height, kTile) * g.grid_x;
     g.bg0 = bg[0];
     g.bg1 = bg[1];
     g.bg2 = bg[2];

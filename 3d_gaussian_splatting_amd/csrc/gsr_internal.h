@@ -91,14 +91,21 @@ struct BinLayout {
 #endif
 constexpr int kMaxChunks = GSR_MAX_CHUNKS;  // = GSR_TERM_STRIDE (gsr.h) in the shipped build
 
+// The live-stripe bytes of the checkpoint region start after the float4 checkpoints of all
+// `tiles` tiles of the image (the full image's tile count, also for band launches).
+__host__ __device__ inline size_t ck_live_offset(size_t tiles) { return tiles * (kMaxChunks - 1) * 256; }
+
 struct ImgLayout {
     size_t ranges, counters, done, ovf, ovf2, term, final_T, accum, ck, total;
+    static size_t tile_count(int W, int H) {
+        const size_t t = (size_t)div_up(W, kTile) * div_up(H, kTile);
+        return t ? t : 1;
+    }
     ImgLayout(int W, int H) {
         size_t o = 0;
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
-        size_t tiles = (size_t)div_up(W, kTile) * div_up(H, kTile);
+        const size_t tiles = tile_count(W, H);
         size_t pix = (size_t)W * H;
-        if (!tiles) tiles = 1;
         ranges = take(8 * tiles);
         counters = take(4 * (2 * kCountSlots + 16));  // ranges, counters and done are contiguous:
         done = take(4 * tiles);  // one memset clears them (done: chunks sorted per queued tile)
@@ -107,7 +114,9 @@ struct ImgLayout {
         term = take(4 * tiles * kMaxChunks);  // F6: per tile [termination index, chunk 1..kMaxChunks-1 starts]
         final_T = take(4 * (pix ? pix : 1));
         accum = take(12 * (pix ? pix : 1));  // colour sum without background, 3 x H x W
-        ck = take(tiles * (kMaxChunks - 1) * 256 * 16);  // float4 (T, C) checkpoints
+        // float4 (T, C) checkpoints, then one byte per (tile, chunk, stripe): 1 where F6 wrote
+        // that stripe's checkpoint (it skips stripes with no live pixel; see ck_live_bytes)
+        ck = take(tiles * (kMaxChunks - 1) * (256 * 16 + 4));
         total = o;
     }
 };

@@ -28,7 +28,7 @@ GSR_SPLAT_BYTES = 64
 GSR_SPLAT_GRAD_BYTES = 48
 MAX_BANDS = 16
 VIEW_SORTED_GID, VIEW_SORTED_TILE, VIEW_RANGES, VIEW_FINAL_T, VIEW_N_CONTRIB, VIEW_DEPTH_KEY, \
-    VIEW_TILES_TOUCHED, VIEW_RECORDS, VIEW_COUNTS, VIEW_TERM = range(1, 11)
+    VIEW_TILES_TOUCHED, VIEW_RECORDS, VIEW_COUNTS, VIEW_TERM, VIEW_CK_LIVE = range(1, 12)
 TERM_STRIDE = 32  # GSR_TERM_STRIDE: words per tile of VIEW_TERM
 EXPORTS = ["gsr_abi_version", "gsr_last_error", "gsr_forward", "gsr_read_num_rendered", "gsr_forward_batch",
            "gsr_backward", "gsr_backward_blend", "gsr_backward_preprocess", "gsr_shard_forward",

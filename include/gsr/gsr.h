@@ -231,6 +231,10 @@ int gsr_shard_backward(const gsr_camera* cam, const gsr_gaussians* shard, const 
                                        termination index, then the B1 chunk 1..31 start
                                        records (UINT32_MAX: no such chunk)                 */
 #define GSR_TERM_STRIDE 32          /* words per tile of GSR_VIEW_TERM                     */
+#define GSR_VIEW_CK_LIVE 11         /* uint8[tiles*(GSR_TERM_STRIDE-1)*4]: per tile and B1
+                                       chunk 1..31, per 16x4 pixel stripe, 1 where F6 wrote
+                                       that stripe's checkpoint (0: it had finished; only
+                                       the entries of chunks the tile opened are defined)  */
 #define GSR_VIEW_RECORDS 8          /* float4[3*P]: {x,y,a',b'},{c',o,r,g},{b,ext_x,ext_y,log2 o};
                                        a',b',c' = -log2(e) * (A/2, B, C/2) of the conic */
 const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, int what);

@@ -56,6 +56,7 @@ def test_header_constants_match_the_python_mirror():
     val = lambda name: int(re.search(rf"#define {name} (\d+)", text).group(1))
     assert val("GSR_TERM_STRIDE") == native.TERM_STRIDE
     assert val("GSR_VIEW_TERM") == native.VIEW_TERM
+    assert val("GSR_VIEW_CK_LIVE") == native.VIEW_CK_LIVE
 
 
 def test_library_exports_every_symbol():
