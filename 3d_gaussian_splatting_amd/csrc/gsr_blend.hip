@@ -325,12 +325,6 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
 // from LDS in fixed quad order and stored straight to the partial arrays at the record's
 // emission index j (8 moments in part8[2j..2j+1], the 9th in part1[j]).
 constexpr int kPark = 4;
-#ifndef GSR_B1_ILP
-#define GSR_B1_ILP 0
-#endif
-#ifndef GSR_B1_NOBRANCH
-#define GSR_B1_NOBRANCH 0
-#endif
 // Parking slot stride: 16 quads x 12 floats, padded by 12 so that the flush's 36 lanes (4 slots
 // x 9 moments) read 36 distinct banks -- at 192 the 4 slots alias (4-way LDS bank conflicts,
 // ~1 conflict cycle per LDS instruction of B1 in the PMC pass).
@@ -510,37 +504,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                 const float w = a * T[p];
                 const float tT = T[p] - w;
                 const bool ok = tT >= 0.0001f;
-#if GSR_B1_NOBRANCH
-                {  // experiment: every lane of a visited stripe runs the contribution, masked
-                    const bool c = ok && keep;
-                    any |= c;
-                    const float wc = c ? w : 0.0f;
-                    const float cdp = fmaf(r1.z, dp0[p], fmaf(r1.w, dp1[p], r2.x * dp2[p]));
-                    const float num = fmaf(T[p], cdp, -R[p]);
-                    R[p] = fmaf(-wc, cdp, R[p]);
-                    g0 = fmaf(wc, dp0[p], g0);
-                    g1 = fmaf(wc, dp1[p], g1);
-                    g2 = fmaf(wc, dp2[p], g2);
-                    const float sv = c ? oG * (num * __builtin_amdgcn_rcpf(1.0f - a)) : 0.0f;
-                    s0 += sv;
-                    const float svy = sv * dy;
-                    sy += svy;
-                    syy = fmaf(svy, dy, syy);
-                }
-#else
                 if (ok && keep) {
                     any = true;
                     const float one_m = 1.0f - a;
                     const float cdp = fmaf(r1.z, dp0[p], fmaf(r1.w, dp1[p], r2.x * dp2[p]));
-#if GSR_B1_ILP
-                    // experiment: dL/dalpha = (T c.dp - R_old) / (1 - alpha), independent of the R update
-                    const float num = fmaf(T[p], cdp, -R[p]);
-                    R[p] = fmaf(-w, cdp, R[p]);
-                    const float dLda = num * __builtin_amdgcn_rcpf(one_m);
-#else
                     R[p] = fmaf(-w, cdp, R[p]);
                     const float dLda = fmaf(T[p], cdp, -R[p] * __builtin_amdgcn_rcpf(one_m));
-#endif
                     g0 = fmaf(w, dp0[p], g0);
                     g1 = fmaf(w, dp1[p], g1);
                     g2 = fmaf(w, dp2[p], g2);
@@ -550,7 +519,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                     sy += svy;
                     syy = fmaf(svy, dy, syy);
                 }
-#endif
                 T[p] = ok ? tT : -fabsf(T[p]);
             }
             if (__any(any)) {
