@@ -52,6 +52,22 @@ CONFIGS = {
     "1m_1080p": dict(P=1_000_000, W=1920, H=1080, D=3),
     "5m_1080p": dict(P=5_000_000, W=1920, H=1080, D=3),
 }
+BASELINE_METRIC = "forward+backward iters/s at 1080p, 1M Gaussians; PSNR vs CPU ref"  # BASELINE.json
+
+
+def config_label(name: str) -> str:
+    c = CONFIGS[name]
+    size = "1080p" if (c["W"], c["H"]) == (1920, 1080) else f"{c['W']}x{c['H']}"
+    n = f"{c['P'] // 1_000_000}M" if c["P"] % 1_000_000 == 0 else f"{c['P'] // 1000}k"
+    return f"{size}, {n} Gaussians"
+
+
+def config_metric(name: str) -> str:
+    """BASELINE.json's metric string for its config (1m_1080p); the same metric named after the
+    workload for the others (parity-test sizes and configs[3]'s 5M scene)."""
+    return f"forward+backward iters/s at {config_label(name)}; PSNR vs CPU ref"
+
+
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 # wave64 VALU issue peak: 256 CUs x 4 SIMD-32 units, one wave64 op per 2 cycles per SIMD at
 # 2.4 GHz (MI355X_MICROARCH constants table, `v_fma_f32 (wave64) 2 cyc (SIMD-32)`).  The
@@ -250,7 +266,7 @@ def main():
         P_local, pix_local, tiles_local = P, W * H, tiles
     alg = algorithmic_bytes(P_local, V, K, pix_local, tiles_local, M)
     result = {
-        "metric": "forward+backward iters/s at 1080p, 1M Gaussians; PSNR vs CPU ref",
+        "metric": config_metric(args.config),
         "value": round(value, 3), "unit": "iters/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
@@ -405,8 +421,8 @@ def train_main(args):
     adam_bytes = floats * 28  # p, m, v read + written, grad read (f32)
     adam_mean = adam_ms / args.steps
     stats = out["stats"].cpu().tolist()
-    res = {"metric": "training iterations/s at 1080p, 1M Gaussians (activations + render + L1/D-SSIM loss + "
-                     "backward + densification statistics + fused Adam)",
+    res = {"metric": f"training iterations/s at {config_label(args.config)} (activations + render + L1/D-SSIM "
+                     "loss + backward + densification statistics + fused Adam)",
            "value": round(args.steps / elapsed, 3), "unit": "iters/s", "n_gpus": 1, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "strong",
            "vs_baseline": None, "dtype": "f32", "data": "synthetic",

@@ -192,3 +192,16 @@ def test_dropin_executable_has_one_hip_runtime():
     hip = [l.split("=>")[1].split("(")[0].strip() for l in out.splitlines() if "libamdhip64" in l and "=>" in l]
     hsa = [l for l in out.splitlines() if "libhsa-runtime64" in l]
     assert len(hip) == 1 and len(hsa) == 1, out
+
+
+def test_bench_metric_names():
+    """bench.py reports BASELINE.json's metric string verbatim for the headline config, and a
+    workload-named one for every other config (no mislabelled lines)."""
+    import json
+    import bench
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        base = json.load(f)["metric"]
+    assert bench.config_metric("1m_1080p") == base
+    names = {bench.config_metric(k) for k in bench.CONFIGS}
+    assert len(names) == len(bench.CONFIGS)
+    assert "5M Gaussians" in bench.config_metric("5m_1080p")
