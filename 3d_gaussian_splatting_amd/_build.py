@@ -162,16 +162,10 @@ def build_variant(name: str, defines: list, verbose: bool = False) -> str:
     return so
 
 
-def build_dropin(verbose: bool = False, force: bool = False) -> str:
-    """tests/cpp/dropin_main.cpp + csrc/torch/gsr_torch.cpp (-DGSR_NO_PYBIND) into the C++
-    executable lib/gsr_dropin: gsr::render() compiled against the reference's call surface
-    (tests/test_gpu_dropin.py runs it)."""
+def _exe_flags():
     import torch
     from torch.utils import cpp_extension
 
-    os.makedirs(LIB, exist_ok=True)
-    out = os.path.join(LIB, "gsr_dropin")
-    srcs = [os.path.join(ROOT, "tests", "cpp", "dropin_main.cpp"), os.path.join(CSRC, "torch", "gsr_torch.cpp")]
     tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
     flags = ["-O2", "-std=c++17", "-DGSR_NO_PYBIND", "-D__HIP_PLATFORM_AMD__=1",
              f"-D_GLIBCXX_USE_CXX11_ABI={int(torch._C._GLIBCXX_USE_CXX11_ABI)}",
@@ -187,24 +181,73 @@ def build_dropin(verbose: bool = False, force: bool = False) -> str:
     libs = ["-L" + tlib, "-Wl,--no-as-needed", "-ltorch_hip", "-lc10_hip",
             "-Wl,--as-needed", "-ltorch", "-ltorch_cpu", "-lc10", "-L" + LIB, "-lgsr_hip",
             "-Wl,-rpath," + tlib, "-Wl,-rpath,$ORIGIN"]
-    stamp = _stamp(srcs + _headers() + [os.path.join(CSRC, "torch", "gsr_render.h")], " ".join(flags + libs))
+    return flags, libs
+
+
+# the libtorch layer shared by the C++ executables (compiled once, -DGSR_NO_PYBIND)
+EXE_LIB_SOURCES = [os.path.join(CSRC, "torch", "gsr_torch.cpp"), os.path.join(CSRC, "torch", "gsr_trainer.cpp")]
+EXE_HEADERS = [os.path.join(CSRC, "torch", h) for h in ("gsr_render.h", "gsr_trainer.h")]
+
+
+def _compile_exe_objs(flags, force: bool) -> list:
+    """gsr_torch.cpp + gsr_trainer.cpp -> lib/obj/*.o (content-stamped)."""
+    obj_dir = os.path.join(LIB, "obj")
+    os.makedirs(obj_dir, exist_ok=True)
+    cxx = shutil.which("g++") or "c++"
+
+    def one(src):
+        obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
+        stamp = _stamp([src] + _headers() + EXE_HEADERS, " ".join(flags))
+        if not force and os.path.exists(obj) and os.path.exists(obj + ".stamp") and open(obj + ".stamp").read() == stamp:
+            return obj
+        cmd = [cxx] + flags + ["-c", src, "-o", obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        with open(obj + ".stamp", "w") as fh:
+            fh.write(stamp)
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=len(EXE_LIB_SOURCES)) as ex:
+        return list(ex.map(one, EXE_LIB_SOURCES))
+
+
+def _build_exe(name: str, main_src: str, force: bool = False) -> str:
+    flags, libs = _exe_flags()
+    objs = _compile_exe_objs(flags, force)
+    out = os.path.join(LIB, name)
+    stamp = _stamp([main_src] + EXE_LIB_SOURCES + _headers() + EXE_HEADERS, " ".join(flags + libs))
     stamp_file = out + ".stamp"
     if not force and os.path.exists(out) and os.path.exists(stamp_file) and open(stamp_file).read() == stamp:
         return out
     cxx = shutil.which("g++") or "c++"
-    cmd = [cxx] + flags + srcs + ["-o", out] + libs
+    cmd = [cxx] + flags + [main_src] + objs + ["-o", out] + libs
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        raise RuntimeError(f"drop-in executable build failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        raise RuntimeError(f"{name} build failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
     with open(stamp_file, "w") as fh:
         fh.write(stamp)
     return out
+
+
+def build_dropin(verbose: bool = False, force: bool = False) -> str:
+    """tests/cpp/dropin_main.cpp + the libtorch layer into the C++ executable lib/gsr_dropin:
+    gsr::render() compiled against the reference's call surface (tests/test_gpu_dropin.py)."""
+    return _build_exe("gsr_dropin", os.path.join(ROOT, "tests", "cpp", "dropin_main.cpp"), force)
+
+
+def build_train_loop(verbose: bool = False, force: bool = False) -> str:
+    """tests/cpp/train_main.cpp + the libtorch layer into lib/gsr_train_loop: the reference's
+    train() loop (train_utils.cpp:128-145) over gsr::Trainer (tests/test_gpu_train_loop.py,
+    bench.py --mode loop)."""
+    return _build_exe("gsr_train_loop", os.path.join(ROOT, "tests", "cpp", "train_main.cpp"), force)
 
 
 def build_all(verbose: bool = False, force: bool = False):
     so = build_hip(verbose, force)
     ext = build_torch_ext(verbose, force)
     build_dropin(verbose, force)
+    build_train_loop(verbose, force)
     return so, ext
 
 

@@ -122,19 +122,89 @@ def all_to_all_blocks(send: torch.Tensor, world: int, dist, group=None) -> torch
     return recv
 
 
+class ShardOverflowError(RuntimeError):
+    """A step's splats or band instances exceeded the capacities ``plan`` sized: that step's
+    render was truncated (the kernels drop what does not fit and stay inside their buffers).
+    ``step`` is the index of the offending step, ``counts`` the per-band splat counts that
+    rank packed (against ``pair_cap``) and ``band_k`` its band's instance count (against
+    ``capacity``).  Re-plan (``ShardStep.plan``) and re-run from that step."""
+
+    def __init__(self, step: int, counts, pair_cap: int, band_k: int, capacity: int):
+        self.step, self.counts, self.pair_cap = step, list(counts), pair_cap
+        self.band_k, self.capacity = band_k, capacity
+        super().__init__(f"multi-GPU step {step} overflowed: splats per band {self.counts} vs pair_cap {pair_cap}, "
+                         f"band instances {band_k} vs capacity {capacity}")
+
+
+class _CountRing:
+    """Each step's per-band splat counts and band instance count, copied to pinned host memory
+    without waiting; read once the copy's event has completed (one or more steps later)."""
+
+    def __init__(self, nb: int, device, ring: int = 4):
+        pin = torch.cuda.is_available() and torch.device(device).type == "cuda"
+        self.slots = [torch.zeros(nb + 1, dtype=torch.int64, pin_memory=pin) for _ in range(ring)]
+        self.pending: list = []  # (step, slot, event or None, pair_cap, capacity)
+        self.next = 0
+
+    def push(self, step: int, counts: torch.Tensor, band_k: torch.Tensor, pair_cap: int, capacity: int):
+        if len(self.pending) == len(self.slots):
+            self.wait_oldest()
+        slot = self.slots[self.next]
+        self.next = (self.next + 1) % len(self.slots)
+        vals = torch.cat([counts.to(torch.int64).reshape(-1), band_k.to(torch.int64).reshape(-1)])
+        ev = None
+        if vals.is_cuda:
+            slot.copy_(vals, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(vals.device))
+        else:
+            slot.copy_(vals)
+        self.pending.append((step, slot, ev, pair_cap, capacity))
+
+    def wait_oldest(self):
+        ev = self.pending[0][2]
+        if ev is not None:
+            ev.synchronize()
+        self.poll()
+
+    def poll(self, wait: bool = False):
+        """Check every completed entry (all of them with wait=True); raise on an overflow."""
+        while self.pending and (wait or self.pending[0][2] is None or self.pending[0][2].query()):
+            step, slot, ev, pair_cap, capacity = self.pending.pop(0)
+            if ev is not None:
+                ev.synchronize()
+            v = slot.tolist()
+            counts, band_k = v[:-1], v[-1]
+            if max(counts) > pair_cap or band_k > capacity:
+                self.pending.clear()
+                raise ShardOverflowError(step, counts, pair_cap, band_k, capacity)
+
+
 class ShardStep:
     """Forward + backward of one rank of the multi-GPU path (rasterizer.ShardRasterizer calls,
     the exchanges above in between).  `inputs`: the full Gaussian arrays (device tensors) --
     each rank reads only its shard's rows.  ``plan`` sizes the exchange once from a probe:
     the band cuts from the summed row histogram, ``pair_cap`` and the band's instance capacity
-    from the true counts, each with ``headroom``."""
+    from the true counts, each with ``headroom``.
 
-    def __init__(self, rast, cam, inputs: dict, sh_degree: int, dist, group=None, headroom: float = 1.25):
+    Overflow: a step whose splats exceed ``pair_cap`` (any send block's header count) or whose
+    band holds more instances than ``capacity`` is truncated by the kernels.  Every step's
+    counts are copied to pinned memory without a host wait and checked when the copy has landed
+    -- at the next ``step`` / ``check`` call -- which raises ``ShardOverflowError`` naming the
+    step (``strict=True`` checks every step before returning it, at the cost of one host
+    wait per step).  Each rank checks its own counts: a rank that overflowed raises, the
+    others see the error through the collective that the raising rank no longer joins, so
+    re-planning is a job restart (or a caller-level agreement) rather than a silent
+    divergence."""
+
+    def __init__(self, rast, cam, inputs: dict, sh_degree: int, dist, group=None, headroom: float = 1.25,
+                 strict: bool = False):
         self.rast, self.cam, self.dist, self.group = rast, cam, dist, group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.D = sh_degree
         self.headroom = headroom
+        self.strict = strict
         P = int(inputs["means3D"].shape[0])
         self.P = P
         self.g0, self.g1 = gaussian_shard(P, self.world, self.rank)
@@ -143,6 +213,8 @@ class ShardStep:
         self.rows = equal_bands(self.gy, self.world)
         self.pair_cap = 0
         self.capacity = 0
+        self.steps = 0
+        self._ring = _CountRing(self.world, self.shard["means3D"].device)
 
     def _shard_forward(self, pair_cap, row_hist=None):
         return self.rast.shard_forward(self.cam, self.rows, pair_cap, **self.shard, sh_degree=self.D,
@@ -150,12 +222,14 @@ class ShardStep:
 
     def plan(self):
         """Probe (synchronous, setup only): balanced band cuts, then the pair capacity and the
-        band's instance capacity."""
+        band's instance capacity.  The row histogram is u32 per shard on the device and summed
+        over ranks in int64; a band above 2^31 - 1 instances is refused (int32 capacities)."""
         dev = self.shard["means3D"].device
         hist = torch.zeros(self.gy, dtype=torch.int32, device=dev)
         self._shard_forward(0, hist)  # pair_cap 0: headers only
-        self.dist.all_reduce(hist, group=self.group)
-        counts = hist.cpu().numpy().astype(np.int64)
+        hist64 = hist.to(torch.int64) & 0xFFFFFFFF  # the kernel's u32 counts, widened before the sum
+        self.dist.all_reduce(hist64, group=self.group)
+        counts = hist64.cpu().numpy().astype(np.int64)
         self.rows = balance_bands(counts, self.world)
         sh = self._shard_forward(0)
         pc = sh.counts.to(torch.int64)
@@ -163,7 +237,10 @@ class ShardStep:
         self.pair_cap = round_up(max(int(pc.max()), 1) * self.headroom)
         band_k = [int(counts[self.rows[b]:self.rows[b + 1]].sum()) for b in range(self.world)]
         self.capacity = round_up(max(max(band_k), 1) * self.headroom)
+        if self.capacity >= 2**31 or self.pair_cap * self.world >= 2**31:
+            raise ValueError(f"band capacity {self.capacity} / pair_cap {self.pair_cap} exceed int32: use more ranks")
         self.band_instances = band_k
+        self._ring.pending.clear()
         return self
 
     @property
@@ -174,24 +251,37 @@ class ShardStep:
         sh = self._shard_forward(self.pair_cap)
         recv = all_to_all_blocks(sh.send, self.world, self.dist, self.group)
         st = self.rast.band_forward(self.cam, self.band, self.world, self.pair_cap, recv, self.capacity)
+        self._ring.push(self.steps, sh.counts, st.k_device(), self.pair_cap, self.capacity)
         return sh, st
 
+    def check(self, wait: bool = True):
+        """Raise ShardOverflowError if a finished step overflowed (wait=True: every step so far)."""
+        self._ring.poll(wait=wait)
+
     def step(self, dL_dpix: torch.Tensor):
-        """-> (full image, this shard's leaf gradients, shard state, band state)."""
+        """-> (full image, this shard's leaf gradients, shard state, band state).  Raises
+        ShardOverflowError for an earlier step found to have overflowed (see the class doc)."""
+        self._ring.poll()
         sh, st = self.forward()
         img = ImageGather(st.color, self.rows, self.rank, self.dist, self.group)  # overlaps B1
         g2 = self.rast.band_backward(st, self.world, self.pair_cap, dL_dpix)
         back = all_to_all_blocks(g2, self.world, self.dist, self.group)
         grads = self.rast.shard_backward(sh, back)
-        return img.wait(), grads, sh, st
+        self.steps += 1
+        out = img.wait(), grads, sh, st
+        if self.strict:
+            self._ring.poll(wait=True)
+        return out
 
 
 def simulate_ranks(rast, cam, inputs: dict, sh_degree: int, world: int, dL_dpix: torch.Tensor,
-                   headroom: float = 1.25, rows=None, timer=None):
+                   headroom: float = 1.25, rows=None, timer=None, pair_cap=None, capacity=None):
     """Every rank's compute of one multi-GPU step, in one process on one GPU, with the
     collectives replaced by block copies (same layouts as the RCCL exchange): the rehearsal of
     scripts/band_sim.py and the GPU parity tests.  `timer(name, rank, fn)` (optional) wraps each
-    per-rank call.  Returns (image, leaf gradients of all P, plan dict)."""
+    per-rank call.  `pair_cap` / `capacity` override the probed capacities (overflow tests).
+    Returns (image, leaf gradients of all P, plan dict); the plan's ``overflow`` lists the
+    (rank, per-band counts, band K) of every rank whose step exceeded them."""
     run = timer or (lambda name, r, fn: fn())
     P = int(inputs["means3D"].shape[0])
     gy = (cam.height + TILE - 1) // TILE
@@ -209,9 +299,12 @@ def simulate_ranks(rast, cam, inputs: dict, sh_degree: int, world: int, dL_dpix:
         for r in range(world):
             rast.shard_forward(cam, rows, 0, **sub(r), sh_degree=sh_degree, row_hist=hist)
         counts = hist.cpu().numpy().astype(np.int64)
-    pc = max(int(rast.shard_forward(cam, rows, 0, **sub(r), sh_degree=sh_degree).counts.max()) for r in range(world))
-    pair_cap = round_up(max(pc, 1) * headroom)
-    capacity = round_up(max(max(int(counts[rows[b]:rows[b + 1]].sum()) for b in range(world)), 1) * headroom)
+    if pair_cap is None:
+        pc = max(int(rast.shard_forward(cam, rows, 0, **sub(r), sh_degree=sh_degree).counts.max())
+                 for r in range(world))
+        pair_cap = round_up(max(pc, 1) * headroom)
+    if capacity is None:
+        capacity = round_up(max(max(int(counts[rows[b]:rows[b + 1]].sum()) for b in range(world)), 1) * headroom)
     shs = [run("shard_forward", r, lambda r=r: rast.shard_forward(cam, rows, pair_cap, **sub(r), sh_degree=sh_degree))
            for r in range(world)]
     blk = shs[0].send.numel() // world
@@ -232,5 +325,12 @@ def simulate_ranks(rast, cam, inputs: dict, sh_degree: int, world: int, dL_dpix:
     grad_recv = [torch.cat(back_parts[r]) for r in range(world)]
     grads = [run("shard_backward", r, lambda r=r: rast.shard_backward(shs[r], grad_recv[r])) for r in range(world)]
     full = {k: torch.cat([g[k] for g in grads]) for k in grads[0]}
+    overflow = []
+    for r in range(world):
+        cnt = [int(c) for c in shs[r].counts.tolist()]
+        k = int(bsts[r].k_device().item())
+        if max(cnt) > pair_cap or k > capacity:
+            overflow.append((r, cnt, k))
     return image, full, dict(rows=rows, pair_cap=pair_cap, capacity=capacity, shards=shs, bands=bsts,
-                             band_instances=[int(counts[rows[b]:rows[b + 1]].sum()) for b in range(world)])
+                             band_instances=[int(counts[rows[b]:rows[b + 1]].sum()) for b in range(world)],
+                             overflow=overflow)

@@ -697,7 +697,7 @@ int gsr_band_backward(const gsr_camera* cam, const gsr_raster_settings* rs, int3
 }
 
 int gsr_shard_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_settings* rs, int32_t nbands,
-                       const int32_t* band_rows, int32_t pair_cap, const void* shard_state, const void* grad_recv,
+                       const int32_t* band_rows, int32_t pair_cap, void* shard_state, const void* grad_recv,
                        const gsr_grads* grads, void* stream_) {
     g_err.clear();
     if (int e = validate(cam, gs, rs)) return e;
@@ -713,7 +713,7 @@ int gsr_shard_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr
     const GeomLayout& gl = sl.geo;
     const uint32_t* tiles = at<uint32_t>(shard_state, gl.tiles);
     const uint4* rect = at<uint4>(shard_state, gl.rect);
-    float* grad2d = const_cast<float*>(at<float>(shard_state, sl.grad2d));
+    float* grad2d = at<float>(shard_state, sl.grad2d);  // the summed 2D gradients (written)
     GSR_STAGE(GSR_STAGE_EXCHANGE, launch_grad_sum(tiles, rect, P, br, at<uint32_t>(shard_state, sl.slot_of),
                                                   static_cast<const float*>(grad_recv), pair_cap, grad2d, stream),
               "gradient sum");

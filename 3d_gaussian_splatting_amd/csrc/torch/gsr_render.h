@@ -3,8 +3,11 @@
 // The reference (seiya-kumada/3d_gaussian_splatting) has no renderer; its loop body is a stub
 // at src/utils/train_utils.cpp:128-145.  This header gives that loop the call it is missing:
 //
-//     auto out = gsr::render(cam, *gaussians, pipeline_params, background);
-//     auto loss = l1(out.render, gt);  loss.backward();
+//     auto out = gsr::render(cam, *gaussians, pipeline_params, bg, 1.f, std::nullopt, &binning);
+//     auto loss = gsr::photometric_loss(out.render, gt, lambda_dssim);  loss.backward();
+//
+// (bg: gsr::background(background_tensor), read once before the loop; binning: a
+// gsr::BinningCapacity, so no forward waits on the host for the instance count K.)
 //
 // `Model` is the reference's GaussianModel (src/scene/gaussian_model.h): render() only uses
 // its public getters (get_xyz / get_opacity / get_scaling / get_rotation / get_covariance,
@@ -18,7 +21,9 @@
 
 #include <array>
 #include <cmath>
+#include <cstdint>
 #include <optional>
+#include <vector>
 
 #include "gsr/gsr.h"
 
@@ -57,10 +62,61 @@ struct RenderOutput {
     torch::Tensor viewspace_points;   // (P,3) zeros requiring grad: receives dL/dmeans2D
     torch::Tensor visibility_filter;  // (P,) bool, radii > 0
     torch::Tensor radii;              // (P,) int32
+    torch::Tensor num_rendered_device;  // (1,) int32 on the device: K (no host wait to get it)
+    int num_rendered = -1;              // K when the forward read it back (max_rendered == 0), else -1
+    int capacity = 0;                   // instances the forward's binning held
 };
 
+// K of a render, read back now (waits for the render's stream): gsr_read_num_rendered's
+// contract -- throws std::overflow_error when K exceeded the capacity (the render dropped
+// instances past it; re-run with a larger bound).
+int read_num_rendered(const RenderOutput& out);
+
+// A binning bound for a training loop's renders (the C++ twin of trainer.BinningCapacity):
+// bound() is 0 right after the point set changes (that render sizes its binning exactly: one
+// host read of K), afterwards headroom x the largest K seen; observe() copies each bounded
+// render's K to pinned memory without waiting and checks it once the copy has landed, one or
+// more iterations later (overflows() counts renders found above their bound; the bound grows).
+class BinningCapacity {
+   public:
+    explicit BinningCapacity(double headroom = 1.5, int ring = 8);
+    ~BinningCapacity();
+    BinningCapacity(const BinningCapacity&) = delete;
+    BinningCapacity& operator=(const BinningCapacity&) = delete;
+    int bound();                        // max_rendered for the next render (0 = exact)
+    void observe(const RenderOutput& out);
+    void observe(const torch::Tensor& k_device, int host_k);
+    void reset();                       // the point set changed
+    void sync();                        // wait for every pending check
+    int64_t overflows() const { return overflows_; }
+    int64_t exact_reads() const { return exact_reads_; }
+    int64_t k_max() const { return k_max_; }
+    int cap() const { return cap_; }
+
+   private:
+    struct Pending {
+        int slot;
+        void* event;
+        int cap;
+    };
+    void poll(bool wait);
+    void grow();
+    double headroom_;
+    int cap_ = 0;
+    int64_t k_max_ = 0, overflows_ = 0, exact_reads_ = 0;
+    std::vector<torch::Tensor> slots_;
+    std::vector<void*> events_;
+    std::vector<Pending> pending_;
+    int next_ = 0;
+};
+
+// Background colour as host floats (one device read; do it once, outside the loop -- the
+// reference keeps its background as a device tensor, train_utils.cpp:115-117).
+std::array<float, 3> background(const torch::Tensor& bg);
+
 // Differentiable rasterization (RasterizeGaussians autograd Function).  Absent optional
-// inputs are undefined tensors.  Returns {color (3,H,W), radii (P,) int32}.
+// inputs are undefined tensors.  Returns {color (3,H,W), radii (P,) int32, K (1,) int32 on the
+// device, {host K or -1, capacity} (2,) int32 on the host}.
 std::vector<torch::Tensor> rasterize_gaussians(
     const RasterCamera& cam, const RasterSettings& rs, const torch::Tensor& means3D,
     const torch::Tensor& means2D, const torch::Tensor& sh_dc, const torch::Tensor& sh_rest,
@@ -72,18 +128,18 @@ std::vector<torch::Tensor> rasterize_gaussians(
 torch::Tensor eval_sh_colors(int D, const torch::Tensor& sh, const torch::Tensor& dirs);
 
 template <class Model, class Pipe>
-RenderOutput render(const RasterCamera& cam, Model& pc, const Pipe& pipe, const torch::Tensor& bg,
-                    float scaling_modifier = 1.f,
-                    std::optional<torch::Tensor> override_color = std::nullopt) {
+RenderOutput render(const RasterCamera& cam, Model& pc, const Pipe& pipe, const std::array<float, 3>& bg,
+                    float scaling_modifier = 1.f, std::optional<torch::Tensor> override_color = std::nullopt,
+                    BinningCapacity* binning = nullptr) {
     const auto& xyz = pc.get_xyz();
     auto screenspace = torch::zeros_like(xyz).requires_grad_(true);
     RasterSettings rs;
-    auto bgc = bg.to(torch::kCPU, torch::kFloat32).contiguous();
-    for (int c = 0; c < 3; ++c) rs.bg[c] = bgc.data_ptr<float>()[c];
+    rs.bg = bg;
     rs.scale_modifier = scaling_modifier;
     auto& core = pc.get_core_params();
     rs.sh_degree = core.active_sh_degree_;
     rs.debug = pipe.debug_;
+    rs.max_rendered = binning ? binning->bound() : 0;
     torch::Tensor scales, rotations, cov3D, sh_dc, sh_rest, colors;
     // The reference's GaussianModel::get_covariance takes an int modifier
     // (gaussian_model.h:89), so it is called only with an integral one; any other modifier is
@@ -108,9 +164,46 @@ RenderOutput render(const RasterCamera& cam, Model& pc, const Pipe& pipe, const 
         sh_dc = core.features_dc_;
         sh_rest = core.features_rest_;
     }
-    auto outs = rasterize_gaussians(cam, rs, xyz, screenspace, sh_dc, sh_rest, colors, pc.get_opacity(),
+    std::vector<torch::Tensor> outs = rasterize_gaussians(cam, rs, xyz, screenspace, sh_dc, sh_rest, colors, pc.get_opacity(),
                                     scales, rotations, cov3D);
-    return RenderOutput{outs[0], screenspace, outs[1] > 0, outs[1]};
+    RenderOutput o{outs[0], screenspace, outs[1] > 0, outs[1], outs[2]};
+    o.num_rendered = outs[3][0].item<int32_t>();  // host tensor: no device wait
+    o.capacity = outs[3][1].item<int32_t>();
+    if (binning) binning->observe(o);
+    return o;
 }
+
+// The reference keeps the background as a device tensor (train_utils.cpp:115-117): this
+// overload reads it back on every call (one host wait); a loop should convert it once with
+// gsr::background() and call the overload above.
+template <class Model, class Pipe>
+RenderOutput render(const RasterCamera& cam, Model& pc, const Pipe& pipe, const torch::Tensor& bg,
+                    float scaling_modifier = 1.f, std::optional<torch::Tensor> override_color = std::nullopt,
+                    BinningCapacity* binning = nullptr) {
+    return render(cam, pc, pipe, background(bg), scaling_modifier, std::move(override_color), binning);
+}
+
+namespace detail {
+// The forward / backward of RasterizeGaussians without autograd (the native trainer's path,
+// gsr_trainer.h): torch owns every scratch byte; `Frame` keeps them from forward to backward.
+struct Frame {
+    torch::Tensor color, radii, geom, binning, image;
+    gsr_buffers bufs{};
+    gsr_camera cam{};
+    gsr_raster_settings settings{};
+    torch::Tensor k_device() const;  // (1,) int32 device copy of the scan's K
+};
+Frame forward(const RasterCamera& cam, const RasterSettings& rs, const torch::Tensor& means3D,
+              const torch::Tensor& sh_dc, const torch::Tensor& sh_rest, const torch::Tensor& colors,
+              const torch::Tensor& opac, const torch::Tensor& scales, const torch::Tensor& rots,
+              const torch::Tensor& cov3D);
+// gsr_backward into the given gradient tensors (undefined = not requested where nullable)
+void backward(const Frame& f, const RasterSettings& rs, const torch::Tensor& means3D, const torch::Tensor& sh_dc,
+              const torch::Tensor& sh_rest, const torch::Tensor& colors, const torch::Tensor& opac,
+              const torch::Tensor& scales, const torch::Tensor& rots, const torch::Tensor& cov3D,
+              const torch::Tensor& dL_dcolor, const gsr_grads& grads);
+void check(int rc, const char* what);
+void* current_stream();
+}  // namespace detail
 
 }  // namespace gsr

@@ -5,6 +5,8 @@
 // Scratch buffers (geometry / binning / image) are uint8 tensors from torch's caching
 // allocator, created inside the C ABI's allocation callbacks and kept in the autograd context
 // until backward -- the library itself allocates nothing persistent.
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <c10/core/Event.h>
 #include <c10/hip/HIPStream.h>
 #ifdef GSR_NO_PYBIND
 #include <torch/torch.h>
@@ -18,12 +20,16 @@
 #include "gsr_render.h"
 
 namespace gsr {
-namespace {
-
+namespace detail {
 void check(int rc, const char* what) {
     if (rc != 0) throw std::runtime_error(std::string(what) + " failed (" + std::to_string(rc) + "): " +
                                           gsr_last_error());
 }
+void* current_stream() { return (void*)c10::hip::getCurrentHIPStream().stream(); }
+}  // namespace detail
+
+namespace {
+using detail::check;
 
 struct AllocCtx {
     torch::Device device;
@@ -93,12 +99,9 @@ gsr_raster_settings make_settings(const RasterSettings& rs) {
     return s;
 }
 
-void* cur_stream() { return (void*)c10::hip::getCurrentHIPStream().stream(); }
+void* cur_stream() { return detail::current_stream(); }
 
-struct FwdResult {
-    torch::Tensor color, radii, geom, binning, image;
-    gsr_buffers bufs;
-};
+using FwdResult = detail::Frame;
 
 FwdResult forward_impl(const RasterCamera& cam, const RasterSettings& rs, const torch::Tensor& means3D,
                        const torch::Tensor& sh_dc, const torch::Tensor& sh_rest,
@@ -128,6 +131,8 @@ FwdResult forward_impl(const RasterCamera& cam, const RasterSettings& rs, const 
     r.binning = bin.keep.empty() ? torch::Tensor() : bin.keep.at(0);
     r.image = img.keep.at(0);
     r.bufs = b;
+    r.cam = c;
+    r.settings = s;
     return r;
 }
 
@@ -173,8 +178,10 @@ class RasterizeGaussians : public torch::autograd::Function<RasterizeGaussians> 
         ctx->saved_data["ty1"] = (int64_t)rs.tile_y1;
         ctx->saved_data["debug"] = rs.debug;
         ctx->saved_data["max_rendered"] = (int64_t)rs.max_rendered;
-        ctx->mark_non_differentiable({r.radii});
-        return {r.color, r.radii};
+        auto kdev = r.k_device();
+        auto kinfo = torch::tensor({r.bufs.num_rendered, r.bufs.capacity}, torch::kInt32);
+        ctx->mark_non_differentiable({r.radii, kdev, kinfo});
+        return {r.color, r.radii, kdev, kinfo};
     }
 
     static variable_list backward(AutogradContext* ctx, variable_list grad_out) {
@@ -249,6 +256,117 @@ class RasterizeGaussians : public torch::autograd::Function<RasterizeGaussians> 
 };
 
 }  // namespace
+
+namespace detail {
+torch::Tensor Frame::k_device() const {
+    const void* p = gsr_view(&cam, bufs.n_local, &bufs, GSR_VIEW_COUNTS);
+    TORCH_CHECK(p != nullptr, "gsr_view(COUNTS) returned NULL");
+    const int64_t off = static_cast<const uint8_t*>(p) - static_cast<const uint8_t*>(image.data_ptr());
+    TORCH_CHECK(off >= 0 && off + 4 <= image.numel(), "K counter outside the image buffer");
+    return image.narrow(0, off, 4).view(torch::kInt32).clone();  // async device copy
+}
+
+Frame forward(const RasterCamera& cam, const RasterSettings& rs, const torch::Tensor& means3D,
+              const torch::Tensor& sh_dc, const torch::Tensor& sh_rest, const torch::Tensor& colors,
+              const torch::Tensor& opac, const torch::Tensor& scales, const torch::Tensor& rots,
+              const torch::Tensor& cov3D) {
+    return forward_impl(cam, rs, means3D, sh_dc, sh_rest, colors, opac, scales, rots, cov3D);
+}
+
+void backward(const Frame& f, const RasterSettings& rs, const torch::Tensor& means3D, const torch::Tensor& sh_dc,
+              const torch::Tensor& sh_rest, const torch::Tensor& colors, const torch::Tensor& opac,
+              const torch::Tensor& scales, const torch::Tensor& rots, const torch::Tensor& cov3D,
+              const torch::Tensor& dL_dcolor, const gsr_grads& grads) {
+    const gsr_gaussians g = make_gaussians(rs, means3D, sh_dc, sh_rest, colors, opac, scales, rots, cov3D);
+    TORCH_CHECK(dL_dcolor.is_contiguous() && dL_dcolor.numel() == 3LL * f.cam.width * f.cam.height,
+                "dL_dcolor must be a contiguous (3,H,W) tensor");
+    AllocCtx scratch{means3D.device(), {}};
+    check(gsr_backward(&f.cam, &g, &f.settings, &f.bufs, dL_dcolor.data_ptr<float>(), alloc_cb, &scratch, &grads,
+                       cur_stream()),
+          "gsr_backward");
+}
+}  // namespace detail
+
+int read_num_rendered(const RenderOutput& out) {
+    const int k = out.num_rendered_device.item<int32_t>();  // waits for the render's stream
+    if (k > out.capacity)
+        throw std::overflow_error("num_rendered " + std::to_string(k) + " exceeded the binning capacity " +
+                                  std::to_string(out.capacity) + " (GSR_ERR_OVERFLOW): re-render with a larger bound");
+    return k;
+}
+
+std::array<float, 3> background(const torch::Tensor& bg) {
+    TORCH_CHECK(bg.numel() == 3, "background must have 3 values");
+    auto h = bg.to(torch::kCPU, torch::kFloat32).contiguous();
+    return {h.data_ptr<float>()[0], h.data_ptr<float>()[1], h.data_ptr<float>()[2]};
+}
+
+BinningCapacity::BinningCapacity(double headroom, int ring) : headroom_(headroom) {
+    const bool pin = torch::cuda::is_available();
+    for (int i = 0; i < ring; ++i) {
+        slots_.push_back(torch::zeros({1}, torch::TensorOptions().dtype(torch::kInt32).pinned_memory(pin)));
+        events_.push_back(new c10::Event(c10::DeviceType::CUDA));  // torch's event: one HIP runtime
+    }
+}
+
+BinningCapacity::~BinningCapacity() {
+    for (void* e : events_) delete static_cast<c10::Event*>(e);
+}
+
+void BinningCapacity::grow() { cap_ = (int)(((int64_t)(k_max_ * headroom_) + 65536 + 4095) / 4096 * 4096); }
+
+int BinningCapacity::bound() {
+    poll(false);
+    return cap_;
+}
+
+void BinningCapacity::reset() {
+    pending_.clear();
+    cap_ = 0;
+    k_max_ = 0;
+}
+
+void BinningCapacity::observe(const RenderOutput& out) { observe(out.num_rendered_device, out.num_rendered); }
+
+void BinningCapacity::observe(const torch::Tensor& k_device, int host_k) {
+    if (cap_ == 0) {  // an exactly sized render: its K was read back by the forward
+        ++exact_reads_;
+        k_max_ = std::max<int64_t>(k_max_, host_k);
+        grow();
+        return;
+    }
+    if (pending_.size() == slots_.size()) poll(true);  // ring full: wait for the oldest
+    const int slot = next_;
+    next_ = (next_ + 1) % (int)slots_.size();
+    slots_[slot].copy_(k_device, /*non_blocking=*/true);
+    static_cast<c10::Event*>(events_[slot])->record(at::hip::getCurrentHIPStreamMasqueradingAsCUDA().unwrap());
+    pending_.push_back({slot, events_[slot], cap_});
+}
+
+void BinningCapacity::sync() {
+    while (!pending_.empty()) poll(true);
+}
+
+void BinningCapacity::poll(bool wait_one) {
+    bool waited = false;
+    while (!pending_.empty()) {
+        auto* e = static_cast<c10::Event*>(pending_.front().event);
+        if (wait_one && !waited) {
+            e->synchronize();
+            waited = true;
+        } else if (!e->query()) {
+            break;
+        }
+        const Pending p = pending_.front();
+        pending_.erase(pending_.begin());
+        const int64_t k = slots_[p.slot].data_ptr<int32_t>()[0];
+        if (k > p.cap) ++overflows_;
+        if (k > k_max_) {
+            k_max_ = k;
+            if (k * 1.2 > cap_) grow();
+        }
+    }
+}
 
 RasterCamera RasterCamera::from_tensors(int width, int height, double FoVx, double FoVy,
                                         const torch::Tensor& wv, const torch::Tensor& fp,

@@ -145,6 +145,50 @@ class LoopResult:
     exact_k_reads: int = 0       # renders sized by a host read of K (after each point-set change)
 
 
+def view_sequence(n_views: int, iterations: int, seed: int = 0) -> np.ndarray:
+    """The camera of each iteration: the viewpoint stack refilled with a random permutation of
+    the training views whenever it runs empty and popped from its end, as upstream."""
+    rng = np.random.default_rng(seed)
+    stack: list = []
+    out = np.empty(iterations, np.int32)
+    for i in range(iterations):
+        if not stack:
+            stack = list(rng.permutation(n_views))
+        out[i] = int(stack.pop())
+    return out
+
+
+def write_scene(path: str, scene: LoopScene, iterations: int, opt: OptimizationParams | None = None,
+                max_sh_degree: int = 3, seed: int = 0, log_every: int = 100, densify: bool = True,
+                progress_every: int = 0, views=None) -> None:
+    """The GSRLOOP1 file tests/cpp/train_main.cpp (lib/gsr_train_loop) reads: the scene, the
+    OptimizationParams (as the reference's float fields) and the camera of every iteration."""
+    opt = opt or OptimizationParams()
+    views = view_sequence(len(scene.cams), iterations, seed) if views is None else np.asarray(views, np.int32)
+    H, W = int(scene.gts[0].shape[1]), int(scene.gts[0].shape[2])
+    with open(path, "wb") as f:
+        f.write(b"GSRLOOP1")
+        f.write(np.array([len(scene.cams), W, H, len(scene.points), iterations, max_sh_degree, seed, log_every,
+                          int(densify), progress_every], np.int32).tobytes())
+        f.write(np.array([opt.iterations, opt.position_lr_max_steps, opt.densification_interval,
+                          opt.opacity_reset_interval, opt.densify_from_iter, opt.densify_until_iter,
+                          int(opt.random_background)], np.int32).tobytes())
+        f.write(np.array([opt.position_lr_init, opt.position_lr_final, opt.position_lr_delay_mult, opt.feature_lr,
+                          opt.opacity_lr, opt.scaling_lr, opt.rotation_lr, opt.percent_dense, opt.lambda_dssim,
+                          opt.densify_grad_threshold], np.float32).tobytes())
+        f.write(np.array([scene.extent], np.float64).tobytes())
+        f.write(np.zeros(3, np.float32).tobytes())  # black background (train_utils.cpp:115-116)
+        for c in scene.cams:
+            f.write(np.concatenate([[c.tanfovx, c.tanfovy], np.asarray(c.viewmatrix, np.float32).ravel(),
+                                    np.asarray(c.projmatrix, np.float32).ravel(),
+                                    np.asarray(c.campos, np.float32).ravel()]).astype(np.float32).tobytes())
+        for g in scene.gts:
+            f.write(g.detach().cpu().numpy().astype(np.float32).tobytes())
+        f.write(np.ascontiguousarray(scene.points, np.float32).tobytes())
+        f.write(np.ascontiguousarray(scene.colors, np.float32).tobytes())
+        f.write(views.astype(np.int32).tobytes())
+
+
 def train(scene: LoopScene, iterations: int | None = None, opt: OptimizationParams | None = None,
           max_sh_degree: int = 3, seed: int = 0, log_every: int = 100, device="cuda",
           progress_every: int = 0) -> LoopResult:
@@ -155,16 +199,13 @@ def train(scene: LoopScene, iterations: int | None = None, opt: OptimizationPara
     iterations = iterations or opt.iterations
     tr = GaussianTrainer.from_point_cloud(scene.points, scene.colors, max_sh_degree, spatial_lr_scale=scene.extent,
                                           opt=opt, device=device, seed=seed)
-    rng = np.random.default_rng(seed)
-    stack: list = []
+    views = view_sequence(len(scene.cams), iterations, seed)
     res = LoopResult(iterations=iterations, seconds=0.0, iters_per_s=0.0)
     logged = []
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for it in range(1, iterations + 1):
-        if not stack:  # viewpoint_stack refilled and popped at random, as upstream
-            stack = list(rng.permutation(len(scene.cams)))
-        v = int(stack.pop())
+        v = int(views[it - 1])
         out = tr.step(it, scene.cams[v], scene.gts[v])
         if it % log_every == 0 or it == 1 or it == iterations:
             logged.append((it, out["stats"]))

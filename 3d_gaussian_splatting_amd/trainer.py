@@ -50,25 +50,31 @@ ACTS = {"xyz": native.ACT_NONE, "f_dc": native.ACT_NONE, "f_rest": native.ACT_NO
         "opacity": native.ACT_SIGMOID, "scaling": native.ACT_EXP, "rotation": native.ACT_NORMALIZE4}
 
 
+def _f32(x: float) -> float:
+    return float(np.float32(x))
+
+
 @dataclass
 class OptimizationParams:
-    """src/arguments/params.h:50-91."""
+    """src/arguments/params.h:50-91.  The reference's fields are C++ float: the defaults here are
+    those float values (so the C++ gsr::Trainer, which keeps the reference's struct, computes
+    from the same numbers)."""
     iterations: int = 30_000
-    position_lr_init: float = 0.00016
-    position_lr_final: float = 0.0000016
-    position_lr_delay_mult: float = 0.01
+    position_lr_init: float = _f32(0.00016)
+    position_lr_final: float = _f32(0.0000016)
+    position_lr_delay_mult: float = _f32(0.01)
     position_lr_max_steps: int = 30_000
-    feature_lr: float = 0.0025
-    opacity_lr: float = 0.05
-    scaling_lr: float = 0.005
-    rotation_lr: float = 0.001
-    percent_dense: float = 0.01
-    lambda_dssim: float = 0.2
+    feature_lr: float = _f32(0.0025)
+    opacity_lr: float = _f32(0.05)
+    scaling_lr: float = _f32(0.005)
+    rotation_lr: float = _f32(0.001)
+    percent_dense: float = _f32(0.01)
+    lambda_dssim: float = _f32(0.2)
     densification_interval: int = 100
     opacity_reset_interval: int = 3000
     densify_from_iter: int = 500
     densify_until_iter: int = 15_000
-    densify_grad_threshold: float = 0.0002
+    densify_grad_threshold: float = _f32(0.0002)
     random_background: bool = False
 
 

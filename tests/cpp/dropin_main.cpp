@@ -16,7 +16,13 @@
 //     camera.cpp:66-71 builds them, and the one accessor INTEGRATION.md §2 adds.
 // The Adam groups and learning rates are GaussianModel::setup's (gaussian_model.cpp:316-345).
 //
-// usage: gsr_dropin IN.bin OUT.bin   (layouts: tests/test_gpu_dropin.py)
+// usage: gsr_dropin IN.bin OUT.bin [ITERS]   (layouts: tests/test_gpu_dropin.py)
+//
+// With ITERS, the loop body instead: ITERS iterations of render under a gsr::BinningCapacity
+// (no host read of K after the first) -> gsr::photometric_loss (L1 + D-SSIM autograd Function)
+// -> backward -> gsr::densify_stats into max_radii2D_ / xyz_gradient_accum_ / denom_ ->
+// gsr::fused_adam_step over the six torch::optim::Adam (one launch on libtorch's own Adam
+// state), then gsr::read_num_rendered of the last render.
 #include <torch/torch.h>
 
 #include <chrono>
@@ -30,6 +36,7 @@
 #include <vector>
 
 #include "gsr_render.h"
+#include "gsr_trainer.h"
 
 class GaussianModel {
    public:
@@ -176,10 +183,11 @@ void write_t(std::ofstream& f, const torch::Tensor& t) {
 }  // namespace
 
 int main(int argc, char** argv) {
-    if (argc != 3) {
-        std::fprintf(stderr, "usage: %s IN.bin OUT.bin\n", argv[0]);
+    if (argc != 3 && argc != 4) {
+        std::fprintf(stderr, "usage: %s IN.bin OUT.bin [ITERS]\n", argv[0]);
         return 2;
     }
+    const int iters = argc == 4 ? std::atoi(argv[3]) : 0;
     std::setvbuf(stdout, nullptr, _IONBF, 0);
     try {
         mark("start");
@@ -228,6 +236,49 @@ int main(int argc, char** argv) {
         const gsr::RasterCamera rcam = camera.raster_camera();
         auto background = torch::zeros({3}, torch::TensorOptions().dtype(torch::kFloat32).device(torch::kCUDA));
         auto gt = to_dev(target, {3, H, W});
+
+        if (iters > 0) {  // the loop body with the sync-free bound, the fused loss and Adam
+            const auto bg = gsr::background(background);  // once, outside the loop
+            gsr::BinningCapacity binning;
+            core.max_radii2D_ = torch::zeros({P}, core.xyz_.options().requires_grad(false));
+            core.xyz_gradient_accum_ = torch::zeros({P}, core.max_radii2D_.options());
+            core.denom_ = torch::zeros({P}, core.max_radii2D_.options());
+            std::vector<int32_t> host_k;
+            std::vector<torch::Tensor> stats;
+            gsr::RenderOutput out;
+            for (int it = 0; it < iters; ++it) {
+                out = gsr::render(rcam, gaussians, pipe, bg, smod, std::nullopt, &binning);
+                host_k.push_back(out.num_rendered);
+                host_k.push_back(out.capacity);
+                torch::Tensor st;
+                auto loss = gsr::photometric_loss(out.render, gt, 0.2, &st);
+                loss.backward();
+                {
+                    torch::NoGradGuard ng;
+                    gsr::densify_stats(out.radii, out.viewspace_points.grad(), core.max_radii2D_,
+                                       core.xyz_gradient_accum_, core.denom_);
+                    gsr::fused_adam_step(core.optimizers_);
+                }
+                for (auto& kv : core.optimizers_) kv.second->zero_grad();
+                stats.push_back(st);
+            }
+            const int k_last = gsr::read_num_rendered(out);
+            binning.sync();
+            mark("loop");
+            std::ofstream o(argv[2], std::ios::binary);
+            o.write(reinterpret_cast<const char*>(host_k.data()), host_k.size() * sizeof(int32_t));
+            const int32_t tail[3] = {k_last, (int32_t)binning.overflows(), (int32_t)binning.exact_reads()};
+            o.write(reinterpret_cast<const char*>(tail), sizeof(tail));
+            for (auto& st : stats) write_t(o, st);
+            write_t(o, out.render);
+            for (auto* t : {&core.xyz_, &core.features_dc_, &core.features_rest_, &core.opacity_, &core.scaling_,
+                            &core.rotation_, &core.max_radii2D_, &core.xyz_gradient_accum_, &core.denom_})
+                write_t(o, *t);
+            torch::cuda::synchronize();
+            std::printf("gsr_dropin loop ok: %d iterations, K=%d\n", iters, k_last);
+            core.optimizers_.clear();
+            return 0;
+        }
 
         // the loop body train_utils.cpp:137-144 would hold
         auto out = gsr::render(rcam, gaussians, pipe, background, smod);

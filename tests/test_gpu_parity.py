@@ -167,7 +167,8 @@ def test_band_render_equals_full(rast):
         assert rel_l2(_np(g[k]), _np(g_full[k])) <= 1e-5, k
 
 
-@pytest.mark.parametrize("world,P,W,H", [(2, 30000, 640, 480), (3, 50000, 800, 600), (8, 200000, 1920, 1080)])
+@pytest.mark.parametrize("world,P,W,H", [(2, 30000, 640, 480), (3, 50000, 800, 600), (8, 200000, 1920, 1080),
+                                         (8, 5_000_000, 1920, 1080)])  # BASELINE configs[3]
 def test_shard_path_equals_full(world, P, W, H):
     """The multi-GPU split (gsr_shard_forward -> splat blocks -> gsr_band_forward ->
     gsr_band_backward -> gradient blocks -> gsr_shard_backward), every rank simulated in this
@@ -190,8 +191,34 @@ def test_shard_path_equals_full(world, P, W, H):
     assert torch.equal(torch.cat([sh.radii for sh in plan["shards"]]), full.radii)
     assert sum(st.num_rendered for st in plan["bands"]) == full.num_rendered
     assert all(int(sh.counts.max()) <= plan["pair_cap"] for sh in plan["shards"])
+    assert plan["overflow"] == []
     for k, v in g.items():
         assert rel_l2(_np(v), _np(gf[k])) <= 1e-5, k
+
+
+def test_shard_path_overflow_is_reported():
+    """Capacities below the true counts: the step stays in bounds (finite outputs) and the plan
+    names the ranks whose splats (pair_cap) or band instances (capacity) did not fit -- the
+    counts ShardStep checks one step late (test_gpu_multiproc covers the raise)."""
+    R, gr, sc, bands = pkg("rasterizer"), pkg("graphics"), pkg("scene"), pkg("bands")
+    dev = torch.device("cuda", 0)
+    cam = gr.synthetic_camera(640, 480)
+    s = sc.make_scene(cam, 30000, max_sh_degree=3, seed=33)
+    t = lambda a: torch.tensor(a, device=dev)
+    inputs = dict(means3D=t(s.means3D), opacities=t(s.opacities), scales=t(s.scales), rotations=t(s.rotations),
+                  sh_dc=t(s.sh_dc), sh_rest=t(s.sh_rest))
+    dpix = t(sc.make_dL_dpix(cam, seed=34))
+    rast = R.ShardRasterizer(dev)
+    _, _, ok = bands.simulate_ranks(rast, cam, inputs, 3, 2, dpix)
+    assert ok["overflow"] == []
+    true_pc = max(int(sh.counts.max()) for sh in ok["shards"])
+    img, g, plan = bands.simulate_ranks(rast, cam, inputs, 3, 2, dpix, rows=ok["rows"], pair_cap=true_pc // 2)
+    assert plan["overflow"] and all(max(c) > plan["pair_cap"] for _, c, _ in plan["overflow"])
+    assert bool(torch.isfinite(img).all()) and all(bool(torch.isfinite(v).all()) for v in g.values())
+    cap = max(ok["band_instances"]) // 2
+    img, g, plan = bands.simulate_ranks(rast, cam, inputs, 3, 2, dpix, rows=ok["rows"], capacity=cap)
+    assert plan["overflow"] and all(k > cap for _, _, k in plan["overflow"])
+    assert bool(torch.isfinite(img).all()) and all(bool(torch.isfinite(v).all()) for v in g.values())
 
 
 def test_capacity_bound_and_overflow(rast):

@@ -179,13 +179,15 @@ def test_product_does_not_reference_oracle():
                                      r"sys\.path[^\n]*oracle", text, re.M), f
 
 
-def test_dropin_executable_has_one_hip_runtime():
-    """The C++ drop-in (lib/gsr_dropin) must resolve libgsr_hip.so's libamdhip64.so.7 to the
-    torch wheel's bundled runtime, not load /opt/rocm's as a second one (_build.build_dropin:
-    libtorch_hip ahead of libgsr_hip in NEEDED order)."""
+@pytest.mark.parametrize("name", ["gsr_dropin", "gsr_train_loop"])
+def test_dropin_executable_has_one_hip_runtime(name):
+    """The C++ executables (lib/gsr_dropin: render(); lib/gsr_train_loop: the training loop)
+    must resolve libgsr_hip.so's libamdhip64.so.7 to the torch wheel's bundled runtime, not load
+    /opt/rocm's as a second one (_build._exe_flags: libtorch_hip ahead of libgsr_hip in NEEDED
+    order, and no direct libamdhip64 dependency of their own)."""
     import shutil
     import subprocess
-    exe = os.path.join(ROOT, "3d_gaussian_splatting_amd", "lib", "gsr_dropin")
+    exe = os.path.join(ROOT, "3d_gaussian_splatting_amd", "lib", name)
     if not os.path.exists(exe) or not shutil.which("ldd"):
         pytest.skip("drop-in executable not built")
     out = subprocess.run(["ldd", exe], capture_output=True, text=True).stdout

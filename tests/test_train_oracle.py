@@ -89,13 +89,16 @@ def test_expon_lr_func_reference_kats():
 
 
 def test_optimization_params_defaults_match_reference():
-    """src/arguments/params.h:50-68."""
+    """src/arguments/params.h:50-68: the same fields and defaults; the float fields hold the
+    values of the reference's C++ floats (what gsr::OptimizationParams, the reference's own
+    struct, holds in the C++ loop)."""
     O = pkg("trainer").OptimizationParams()
+    f = lambda x: float(np.float32(x))
     assert (O.iterations, O.position_lr_max_steps, O.densification_interval, O.opacity_reset_interval,
             O.densify_from_iter, O.densify_until_iter) == (30000, 30000, 100, 3000, 500, 15000)
-    assert O.lambda_dssim == 0.2 and O.percent_dense == 0.01 and O.densify_grad_threshold == 0.0002
-    assert (O.position_lr_init, O.position_lr_final, O.position_lr_delay_mult) == (0.00016, 0.0000016, 0.01)
-    assert (O.feature_lr, O.opacity_lr, O.scaling_lr, O.rotation_lr) == (0.0025, 0.05, 0.005, 0.001)
+    assert O.lambda_dssim == f(0.2) and O.percent_dense == f(0.01) and O.densify_grad_threshold == f(0.0002)
+    assert (O.position_lr_init, O.position_lr_final, O.position_lr_delay_mult) == (f(0.00016), f(0.0000016), f(0.01))
+    assert (O.feature_lr, O.opacity_lr, O.scaling_lr, O.rotation_lr) == (f(0.0025), f(0.05), f(0.005), f(0.001))
 
 
 def _state(n, seed=4):
