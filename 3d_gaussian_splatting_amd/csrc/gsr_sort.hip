@@ -525,6 +525,9 @@ __global__ __launch_bounds__(256) void finalize_kernel(const uint32_t* __restric
 // [w * 64 I, (w + 1) * 64 I) of the slice, ranked round by round in index order (stable).
 // One slice [rg.x, rg.y) of n <= NT * I entries, sorted by the whole block.  Ends with every
 // LDS access behind a barrier, so a block may call it again for another slice.
+#ifndef GSR_SLICE_RANK_ATOMIC
+#define GSR_SLICE_RANK_ATOMIC 1
+#endif
 template <int NT, int I, int DB>
 struct SliceLds {
     uint32_t wcnt[NT / 64][1 << DB];
@@ -590,6 +593,33 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
         if (((diff >> shift) & DMASK) == 0u) continue;  // block-uniform
         for (int d = tid; d < NWV * BINS; d += NT) (&wcnt[0][0])[d] = 0u;
         __syncthreads();
+#if GSR_SLICE_RANK_ATOMIC
+        // Each round's peer-group leader adds its group's size to the wave's digit counter with
+        // an LDS atomic (ds_add_rtn: one wave's LDS operations complete in issue order, so the
+        // returned bases are cumulative over the rounds) and the group reads the base back from
+        // its leader afterwards.  No round waits for the previous round's counter read: the
+        // rounds' atomics issue back to back instead of one LDS round trip each.
+        uint64_t pr[I];
+        uint32_t ob[I];
+#pragma unroll
+        for (int r = 0; r < I; ++r) {
+            pr[r] = 0ull;
+            ob[r] = 0u;
+            if (base + r * 64 >= end) continue;  // wave-uniform: only the rounds holding keys
+            const int idx = base + r * 64 + lane;
+            const bool valid = idx < end;
+            const uint32_t d = (key[r] >> shift) & DMASK;
+            const uint64_t peers = match_digit<DB>(d, DB, __ballot(valid));
+            pr[r] = valid ? peers : 0ull;
+            if (valid && (peers & lt) == 0) ob[r] = atomicAdd(&wcnt[w][d], (uint32_t)__popcll(peers));
+        }
+#pragma unroll
+        for (int r = 0; r < I; ++r) {
+            if (base + r * 64 >= end) break;
+            const int src = pr[r] ? (int)__builtin_ctzll(pr[r]) : lane;
+            rank[r] = (uint32_t)__shfl((int)ob[r], src, 64) + (uint32_t)__popcll(pr[r] & lt);
+        }
+#else
 #pragma unroll
         for (int r = 0; r < I; ++r) {
             if (base + r * 64 >= end) break;  // wave-uniform: only the rounds holding keys
@@ -601,6 +631,7 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
             rank[r] = old + (uint32_t)__popcll(peers & lt);
             if (valid && (peers & lt) == 0) wcnt[w][d] = old + (uint32_t)__popcll(peers);
         }
+#endif
         __syncthreads();
         // per digit: wave prefixes in place, then the digit-major block scan -> lbase
         for (int d = tid; d < BINS; d += NT) {
@@ -909,11 +940,24 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
 #ifndef GSR_BAND_SORT_NT
 #define GSR_BAND_SORT_NT 512
 #endif
+// full images: 256-thread blocks, or 512 when the mean slice is long (cap 4096; 0 = that rule):
+// 5M / 1080p 0.550 -> 0.490 ms with 512, 1M / 1080p (cap 2048) 0.103 -> 0.111 ms, so per cap
+#ifndef GSR_FULL_SORT_NT
+#define GSR_FULL_SORT_NT 0
+#endif
     if (ntiles < 4096 && GSR_BAND_SORT_NT == 512) {  // band launches: fewer tiles, wider blocks
         if (cap == 1024) GSR_TILE_RADIX(512, 2);
         else if (cap == 2048) GSR_TILE_RADIX(512, 4);
         else GSR_TILE_RADIX(512, 8);
     } else if (ntiles < 4096 && GSR_BAND_SORT_NT == 1024) {
+        if (cap == 1024) GSR_TILE_RADIX(1024, 1);
+        else if (cap == 2048) GSR_TILE_RADIX(1024, 2);
+        else GSR_TILE_RADIX(1024, 4);
+    } else if (GSR_FULL_SORT_NT == 512 || (GSR_FULL_SORT_NT == 0 && cap == 4096)) {
+        if (cap == 1024) GSR_TILE_RADIX(512, 2);
+        else if (cap == 2048) GSR_TILE_RADIX(512, 4);
+        else GSR_TILE_RADIX(512, 8);
+    } else if (GSR_FULL_SORT_NT == 1024) {
         if (cap == 1024) GSR_TILE_RADIX(1024, 1);
         else if (cap == 2048) GSR_TILE_RADIX(1024, 2);
         else GSR_TILE_RADIX(1024, 4);

@@ -76,10 +76,12 @@ int read_num_rendered(const RenderOutput& out);
 // bound() is 0 right after the point set changes (that render sizes its binning exactly: one
 // host read of K), afterwards headroom x the largest K seen; observe() copies each bounded
 // render's K to pinned memory without waiting and checks it once the copy has landed, one or
-// more iterations later (overflows() counts renders found above their bound; the bound grows).
+// more iterations later.  A render found above its bound was truncated and the iteration that
+// used it already applied: overflows() counts it, the next render is sized exactly, and with
+// strict = true the check throws std::overflow_error instead.
 class BinningCapacity {
    public:
-    explicit BinningCapacity(double headroom = 1.5, int ring = 8);
+    explicit BinningCapacity(double headroom = 1.5, int ring = 8, bool strict = false);
     ~BinningCapacity();
     BinningCapacity(const BinningCapacity&) = delete;
     BinningCapacity& operator=(const BinningCapacity&) = delete;
@@ -102,6 +104,7 @@ class BinningCapacity {
     void poll(bool wait);
     void grow();
     double headroom_;
+    bool strict_;
     int cap_ = 0;
     int64_t k_max_ = 0, overflows_ = 0, exact_reads_ = 0;
     std::vector<torch::Tensor> slots_;

@@ -301,7 +301,7 @@ std::array<float, 3> background(const torch::Tensor& bg) {
     return {h.data_ptr<float>()[0], h.data_ptr<float>()[1], h.data_ptr<float>()[2]};
 }
 
-BinningCapacity::BinningCapacity(double headroom, int ring) : headroom_(headroom) {
+BinningCapacity::BinningCapacity(double headroom, int ring, bool strict) : headroom_(headroom), strict_(strict) {
     const bool pin = torch::cuda::is_available();
     for (int i = 0; i < ring; ++i) {
         slots_.push_back(torch::zeros({1}, torch::TensorOptions().dtype(torch::kInt32).pinned_memory(pin)));
@@ -360,7 +360,16 @@ void BinningCapacity::poll(bool wait_one) {
         const Pending p = pending_.front();
         pending_.erase(pending_.begin());
         const int64_t k = slots_[p.slot].data_ptr<int32_t>()[0];
-        if (k > p.cap) ++overflows_;
+        if (k > p.cap) {  // that render was truncated and its iteration applied
+            ++overflows_;
+            k_max_ = std::max(k_max_, k);
+            pending_.clear();
+            cap_ = 0;  // the next render is sized exactly
+            if (strict_)
+                throw std::overflow_error("a render's K = " + std::to_string(k) + " exceeded its bound " +
+                                          std::to_string(p.cap));
+            return;
+        }
         if (k > k_max_) {
             k_max_ = k;
             if (k * 1.2 > cap_) grow();

@@ -240,7 +240,7 @@ Trainer::Trainer(torch::Tensor xyz, torch::Tensor f_dc, torch::Tensor f_rest, to
                  double spatial_lr_scale, double cameras_extent, uint64_t seed)
     : opt_(opt),
       max_sh_degree_(max_sh_degree),
-      spatial_lr_scale_(spatial_lr_scale),
+      spatial_lr_scale_((float)spatial_lr_scale),  // CoreParams::spatial_lr_scale_ is a float
       cameras_extent_(cameras_extent),
       percent_dense_(opt.percent_dense_),
       device_(xyz.device()),

@@ -464,7 +464,10 @@ def save_checkpoint(path: str, state: dict) -> None:
     """One file holding the reference's CoreParams tensor list in its order -- [active_sh_degree,
     xyz, f_dc, f_rest, scaling, rotation, opacity, max_radii2D, xyz_gradient_accum, denom,
     spatial_lr_scale] (gaussian_model.cpp:85-98) -- and, in place of its six per-group
-    torch::optim::Adam archives (:100-130), each group's exp_avg / exp_avg_sq / step."""
+    torch::optim::Adam archives (:100-130), each group's exp_avg / exp_avg_sq / step.
+    spatial_lr_scale is a float32 scalar, as the reference's CoreParams::spatial_lr_scale_ is a
+    float; the densification extent (cameras_extent, not a reference field) rides along in
+    float64."""
     import torch
     cpu = lambda t: t.detach().to("cpu").contiguous()
     p = state["params"]
@@ -472,7 +475,10 @@ def save_checkpoint(path: str, state: dict) -> None:
     core += [cpu(state[k]) for k in _STATS] + [torch.tensor(float(state["spatial_lr_scale"]))]
     optim = {k: {"exp_avg": cpu(state["exp_avg"][k]), "exp_avg_sq": cpu(state["exp_avg_sq"][k]),
                  "step": torch.tensor(int(state["steps"][k]))} for k in p if k in state["exp_avg"]}
-    torch.save({"core": core, "optim": optim}, path)
+    extra = {}
+    if "cameras_extent" in state:
+        extra["cameras_extent"] = torch.tensor(float(state["cameras_extent"]), dtype=torch.float64)
+    torch.save({"core": core, "optim": optim, "extra": extra}, path)
 
 
 def load_checkpoint(path: str, device="cpu") -> dict:
@@ -486,6 +492,8 @@ def load_checkpoint(path: str, device="cpu") -> dict:
     st["exp_avg"] = {k: v["exp_avg"] for k, v in raw["optim"].items()}
     st["exp_avg_sq"] = {k: v["exp_avg_sq"] for k, v in raw["optim"].items()}
     st["steps"] = {k: int(v["step"].item()) for k, v in raw["optim"].items()}
+    for k, v in raw.get("extra", {}).items():
+        st[k] = float(v.item())
     return st
 
 

@@ -202,6 +202,11 @@ class TrainKernels:
         return outs
 
 
+class BinningOverflowError(OverflowError):
+    """A bounded render's K exceeded its bound (strict BinningCapacity): that render dropped
+    instances, and the iteration that used it has been applied."""
+
+
 class BinningCapacity:
     """max_rendered for the trainer's renders without a per-iteration host read of K.
 
@@ -209,12 +214,17 @@ class BinningCapacity:
     ``headroom`` x the largest K seen, rounded up.  Each bounded render's K (the scan's device
     counter) is copied to a pinned slot and checked once its event has completed -- one or two
     iterations later, never waiting.  K above the bound at that check means that render was
-    truncated (its kernels clamp to the bound; GSR_ERR_OVERFLOW semantics): it is counted in
-    ``overflows`` and the bound grows.  The next exact sizing happens at the next
-    densification or opacity reset."""
+    truncated (its kernels clamp to the bound; GSR_ERR_OVERFLOW semantics) and the iteration
+    that used it -- loss, gradients, statistics, Adam step -- has already been applied: it is
+    counted in ``overflows``, the next render is sized exactly again, and with ``strict=True``
+    a BinningOverflowError is raised at that check instead.  The bound covers the largest K of
+    the views rendered since the last point-set change with 1.5x + 64k headroom; views are
+    re-rendered every len(views) iterations, so a view larger than that bound can only be one
+    not yet seen since the change (the 30k-iteration loop: 0 overflows)."""
 
-    def __init__(self, device, headroom: float = 1.5, ring: int = 8):
+    def __init__(self, device, headroom: float = 1.5, ring: int = 8, strict: bool = False):
         self.headroom = float(headroom)
+        self.strict = bool(strict)
         self.cap = 0
         self.k_max = 0
         self.overflows = 0
@@ -260,6 +270,12 @@ class BinningCapacity:
             k = int(slot.item())
             if k > cap:
                 self.overflows += 1
+                self.k_max = max(self.k_max, k)
+                self.pending.clear()
+                self.cap = 0  # the next render is sized exactly
+                if self.strict:
+                    raise BinningOverflowError(f"a render's K = {k} exceeded its bound {cap}")
+                return
             if k > self.k_max:
                 self.k_max = k
                 if k * 1.2 > self.cap:
@@ -282,7 +298,9 @@ class GaussianTrainer:
                        "scaling": f(scaling, (P, 3)), "rotation": f(rotation, (P, 4))}
         self.max_sh_degree = int(max_sh_degree)
         self.active_sh_degree = 0
-        self.spatial_lr_scale = float(spatial_lr_scale)
+        # the reference's CoreParams::spatial_lr_scale_ is a float (gaussian_model.h): held at
+        # f32 precision, so a capture / restore round trip (which stores it as float) is exact
+        self.spatial_lr_scale = _f32(spatial_lr_scale)
         # scene extent for the clone / split threshold and the world-size prune; upstream sets
         # spatial_lr_scale to this same value (the nerf++ radius of the training cameras)
         self.cameras_extent = float(spatial_lr_scale if cameras_extent is None else cameras_extent)

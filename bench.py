@@ -75,11 +75,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 # blend kernels exceed it with their mix of moves, selects and DPP adds).
 VALU_ISSUE_PER_S = 256 * 4 * 2.4e9 / 2
 # SURVEY §8d secondary bound for F6 + B1: exact (pixel, list-entry) pairs from the CPU oracle x
-# VALU lane-ops per pair (the per-stripe loop bodies in the ISA, DESIGN §5.1: F6 ~20, B1 ~30
-# wave64 instructions per 64-pixel stripe evaluation; per-record overhead left out, so a floor)
-# over 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
+# VALU lane-ops per pair, over 256 CU x 4 SIMD x 32 lanes x 2.4 GHz.  The lane-ops per pair are
+# MEASURED: each kernel's PMC SQ_INSTS_VALU per launch (wave64 instructions) x 64 / the oracle's
+# pairs (profiles/pmc_traffic.json, this build only) -- all of the kernel's VALU work, per-record
+# overhead and culled-stripe savings included, so the floor is the issue-bound time of the
+# instruction streams the kernels actually run.
 VALU_LANE_OPS_PER_S = 256 * 4 * 32 * 2.4e9
-C_F6_PER_PAIR, C_B1_PER_PAIR = 20, 30
 
 
 ALG_STAGES = ("preprocess", "scan", "duplicate", "tile_sort", "finalize", "blend_fwd", "blend_bwd",
@@ -150,6 +151,9 @@ def main():
     ap.add_argument("--loop-size", default="1280x832", help="--mode loop: image size WxH")
     ap.add_argument("--loop-views", type=int, default=128, help="--mode loop: training cameras")
     ap.add_argument("--loop-texture", type=float, default=1.0, help="--mode loop: ground-truth colour noise")
+    ap.add_argument("--loop-engine", default="cpp", choices=("cpp", "python"),
+                    help="--mode loop: the C++ loop executable (lib/gsr_train_loop over gsr::Trainer, the "
+                         "train.cpp drop-in) or the Python mirror (train_loop.train)")
     ap.add_argument("--mode", default="render", choices=("render", "train", "views", "loop"),
                     help="render: the BASELINE metric (rasterizer forward+backward); train: one full "
                          "training iteration (activations, render, L1+D-SSIM loss, backward, "
@@ -289,7 +293,12 @@ def main():
         kernel_name = {"blend_fwd": "blend_forward_kernel", "blend_bwd": "blend_backward_kernel",
                        "preprocess": "preprocess_kernel", "preprocess_bwd": "preprocess_backward_kernel"}.get(dom, dom)
         pmc = pmc_record(kernel_name, args.config)
-        result["roofline"] = {"bound": "hbm", "kernel": kernel_name, "achieved": round(achieved, 2),
+        # the roofline that binds the dominant kernel: the blend loops issue VALU work per
+        # (pixel, record) pair and reuse LDS-staged records 256x per tile, so they are VALU-issue
+        # bound; achieved / peak / frac below are their HBM figures (the contract's
+        # fields), valu_issue the binding ones
+        bound = "valu" if dom in ("blend_fwd", "blend_bwd") else "hbm"
+        result["roofline"] = {"bound": bound, "kernel": kernel_name, "achieved": round(achieved, 2),
                               "lib_stamp": (lib_stamp() or "")[:16],
                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                               # PMC passes are of the N = 1 launch; a band launch has no committed counts
@@ -335,12 +344,16 @@ def main():
                                   f"OpenMP {cores} threads)",
                                   "cpu_model": cpu_model(), "nproc": os.cpu_count(),
                                   "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
-        if "roofline" in result:
+        f6, b1 = pmc_record("blend_forward_kernel", args.config), pmc_record("blend_backward_kernel", args.config)
+        if "roofline" in result and "valu_insts_per_launch" in f6 and "valu_insts_per_launch" in b1:
             pairs = f.state.forward_pairs()
-            floor_ms = pairs * (C_F6_PER_PAIR + C_B1_PER_PAIR) / VALU_LANE_OPS_PER_S * 1e3
+            c_f6 = f6["valu_insts_per_launch"] * 64 / pairs
+            c_b1 = b1["valu_insts_per_launch"] * 64 / pairs
+            floor_ms = pairs * (c_f6 + c_b1) / VALU_LANE_OPS_PER_S * 1e3
             meas = sum(result.get("stage_ms", {}).get(k, 0.0) for k in ("blend_fwd", "blend_bwd"))
             result["roofline"]["valu_pair_bound"] = {
-                "pairs": pairs, "lane_ops_per_pair": {"f6": C_F6_PER_PAIR, "b1": C_B1_PER_PAIR},
+                "pairs": pairs, "lane_ops_per_pair": {"f6": round(c_f6, 3), "b1": round(c_b1, 3)},
+                "lane_ops_source": "PMC SQ_INSTS_VALU x 64 / oracle pairs (profiles/pmc_traffic.json)",
                 "peak_lane_ops_per_s": VALU_LANE_OPS_PER_S, "floor_ms_f6_b1": round(floor_ms, 4),
                 "measured_ms_f6_b1": round(meas, 4), "frac": round(floor_ms / meas, 4) if meas else None}
         result["parity"] = {"psnr_db_vs_cpu": round(10 * math.log10(1.0 / mse), 2) if mse > 0 else float("inf"),
@@ -506,7 +519,10 @@ def loop_main(args):
                               texture=args.loop_texture)
     setup_s = time.perf_counter() - t0
     opt = T.OptimizationParams(iterations=args.iters)
-    res = L.train(scene, opt=opt, max_sh_degree=3, log_every=500, device=dev, progress_every=1000)
+    if args.loop_engine == "cpp":
+        res = _loop_cpp(L, scene, opt, args)
+    else:
+        res = L.train(scene, opt=opt, max_sh_degree=3, log_every=500, device=dev, progress_every=1000)
     print(json.dumps({
         "metric": "training iterations/s, full train.cpp loop (render + L1/D-SSIM + backward + densification + Adam)",
         "value": round(res.iters_per_s, 3), "unit": "iters/s", "n_gpus": 1, "steps": res.iterations, "warmup": 0,
@@ -514,12 +530,34 @@ def loop_main(args):
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": f"configs[4]: {args.iters} iterations, {args.loop_views} views {W}x{H}, ground truth "
                                f"{args.loop_gt} Gaussians (texture {args.loop_texture}), init {args.loop_init} points, "
-                               f"SH 3", "width": W, "height": H, "views": args.loop_views},
+                               f"SH 3", "width": W, "height": H, "views": args.loop_views,
+                   "engine": ("C++ loop tests/cpp/train_main.cpp over gsr::Trainer" if args.loop_engine == "cpp"
+                              else "Python train_loop.train over trainer.GaussianTrainer")},
         "seconds": round(res.seconds, 2), "setup_seconds": round(setup_s, 2),
         "final_gaussians": res.final_points, "peak_gaussians": res.peak_points,
         "binning_overflows": res.binning_overflows, "exact_k_reads": res.exact_k_reads,
         "gaussians_after_densify": res.num_points[::10] + res.num_points[-1:],
         "loss_curve": [(i, round(l, 5)) for i, l, _, _ in res.loss][::4] + [(res.loss[-1][0], round(res.loss[-1][1], 5))]}))
+
+
+def _loop_cpp(L, scene, opt, args):
+    """Run the C++ loop executable on `scene` (written to a GSRLOOP1 file); returns a LoopResult."""
+    import subprocess
+    import tempfile
+    exe = os.path.join(ROOT, PKG, "lib", "gsr_train_loop")
+    if not os.path.exists(exe):
+        raise SystemExit(f"{exe} missing: run __graft_entry__.build()")
+    with tempfile.TemporaryDirectory() as d:
+        fin, fres = os.path.join(d, "scene.bin"), os.path.join(d, "res.json")
+        L.write_scene(fin, scene, args.iters, opt, max_sh_degree=3, log_every=500, progress_every=1000)
+        r = subprocess.run([exe, fin, fres], stdout=subprocess.PIPE, text=True)
+        if r.returncode != 0:
+            raise SystemExit(f"gsr_train_loop failed ({r.returncode}): {r.stdout}")
+        j = json.load(open(fres))
+    return L.LoopResult(iterations=j["iterations"], seconds=j["seconds"], iters_per_s=j["iters_per_s"],
+                        num_points=[tuple(x) for x in j["num_points"]], loss=[tuple(x) for x in j["loss"]],
+                        final_points=j["final_points"], peak_points=j["peak_points"],
+                        binning_overflows=j["binning_overflows"], exact_k_reads=j["exact_k_reads"])
 
 
 if __name__ == "__main__":
