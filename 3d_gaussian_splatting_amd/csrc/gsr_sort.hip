@@ -123,6 +123,9 @@ __global__ __launch_bounds__(kB) void radix_colscan(uint32_t* __restrict__ hist,
 }
 
 // ---- downsweep: stable scatter, reordered through LDS so global writes are coalesced ----
+#ifndef GSR_RADIX_RANK_ATOMIC
+#define GSR_RADIX_RANK_ATOMIC 1
+#endif
 __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict__ keys_in,
                                                       const uint32_t* __restrict__ vals_in,
                                                       uint32_t* __restrict__ keys_out,
@@ -170,6 +173,26 @@ __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict
         key[r] = valid ? keys_in[idx] : 0xFFFFFFFFu;
         val[r] = valid ? (vals_in ? vals_in[idx] : (uint32_t)idx) : 0u;
     }
+#if GSR_RADIX_RANK_ATOMIC
+    // LDS-atomic ranking (as in radix_sort_slice): each round's peer-group leader adds its group
+    // to the wave's digit counter with ds_add_rtn; the bases come back after all rounds issued
+    {
+        uint32_t ob[kRI];
+#pragma unroll
+        for (int r = 0; r < kRI; ++r) {
+            const long long idx = base + r * 64 + lane;
+            const bool valid = idx < n;
+            const uint32_t d = (key[r] >> shift) & mask;
+            const uint64_t peers = match_digit(d, nbits, __ballot(valid));
+            rank[r] = valid ? ((uint32_t)__builtin_ctzll(peers) << 8) | (uint32_t)__popcll(peers & lt) : 0u;
+            ob[r] = 0u;
+            if (valid && (peers & lt) == 0) ob[r] = atomicAdd(&wcnt[w][d], (uint32_t)__popcll(peers));
+        }
+#pragma unroll
+        for (int r = 0; r < kRI; ++r)
+            rank[r] = (uint32_t)__shfl((int)ob[r], (int)(rank[r] >> 8), 64) + (rank[r] & 0xFFu);
+    }
+#else
 #pragma unroll
     for (int r = 0; r < kRI; ++r) {
         const long long idx = base + r * 64 + lane;
@@ -181,6 +204,7 @@ __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict
         rank[r] = old + (uint32_t)__popcll(peers & lt);
         if (valid && (peers & lt) == 0) wcnt[w][d] = old + (uint32_t)__popcll(peers);
     }
+#endif
     __syncthreads();
     {
         // per digit: wave prefixes (in place) and the block count; block-local digit starts
@@ -599,25 +623,24 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
         // returned bases are cumulative over the rounds) and the group reads the base back from
         // its leader afterwards.  No round waits for the previous round's counter read: the
         // rounds' atomics issue back to back instead of one LDS round trip each.
-        uint64_t pr[I];
         uint32_t ob[I];
 #pragma unroll
         for (int r = 0; r < I; ++r) {
-            pr[r] = 0ull;
             ob[r] = 0u;
+            rank[r] = 0u;
             if (base + r * 64 >= end) continue;  // wave-uniform: only the rounds holding keys
             const int idx = base + r * 64 + lane;
             const bool valid = idx < end;
             const uint32_t d = (key[r] >> shift) & DMASK;
             const uint64_t peers = match_digit<DB>(d, DB, __ballot(valid));
-            pr[r] = valid ? peers : 0ull;
+            // (group leader lane << 8) | rank within the round, until the bases are back
+            rank[r] = valid ? ((uint32_t)__builtin_ctzll(peers) << 8) | (uint32_t)__popcll(peers & lt) : 0u;
             if (valid && (peers & lt) == 0) ob[r] = atomicAdd(&wcnt[w][d], (uint32_t)__popcll(peers));
         }
 #pragma unroll
         for (int r = 0; r < I; ++r) {
             if (base + r * 64 >= end) break;
-            const int src = pr[r] ? (int)__builtin_ctzll(pr[r]) : lane;
-            rank[r] = (uint32_t)__shfl((int)ob[r], src, 64) + (uint32_t)__popcll(pr[r] & lt);
+            rank[r] = (uint32_t)__shfl((int)ob[r], (int)(rank[r] >> 8), 64) + (rank[r] & 0xFFu);
         }
 #else
 #pragma unroll
