@@ -207,9 +207,9 @@ struct Views {
     float4* rec;
     uint4* rect;
     uint2* ranges;
-    uint32_t *counters, *K_dev, *ovf, *ovf2, *done, *term;
+    uint32_t *counters, *K_dev, *ovf, *ovf2, *done, *term, *ck_slot;
     float *final_T, *accum;
-    float4* ck;
+    float4* ck;  // the checkpoint pool (binning buffer)
     uint32_t *kA, *vA, *kB, *vB, *hist;
     uint32_t *sorted_tile, *sorted_gid;  // where the tile sort's result lands
     uint32_t *free_k, *free_v;           // the other ping-pong pair (scratch after the sort)
@@ -234,11 +234,12 @@ Views views(const gsr_camera* cam, long long n, const gsr_buffers* b) {
     v.ovf2 = at<uint32_t>(b->image, il.ovf2);
     v.done = at<uint32_t>(b->image, il.done);
     v.term = at<uint32_t>(b->image, il.term);
+    v.ck_slot = at<uint32_t>(b->image, il.ck_slot);
     v.final_T = at<float>(b->image, il.final_T);
     v.accum = at<float>(b->image, il.accum);
-    v.ck = at<float4>(b->image, il.ck);
     if (b->binning) {
-        const BinLayout bl(b->capacity);
+        const BinLayout bl(b->capacity, (long long)ImgLayout::tile_count(cam->width, cam->height));
+        v.ck = at<float4>(b->binning, bl.ck);
         v.kA = at<uint32_t>(b->binning, bl.kA);
         v.vA = at<uint32_t>(b->binning, bl.vA);
         v.kB = at<uint32_t>(b->binning, bl.kB);
@@ -317,7 +318,7 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
     gsr_buffers* bufs = j.bufs;
     if (cap > INT32_MAX) return fail(-3, "num_rendered overflow (%lld)", cap);
     bufs->capacity = (int32_t)cap;
-    bufs->binning = alloc_binning(ctx, BinLayout(cap).total);
+    bufs->binning = alloc_binning(ctx, BinLayout(cap, (long long)ImgLayout::tile_count(cam->width, cam->height)).total);
     if (!bufs->binning) return fail(-2, "allocation failed (binning, %lld instances)", cap);
     const Views v = views(cam, j.n, bufs);
     const int tiles = j.gx * j.gy, ntiles = (j.ty1 - j.ty0) * j.gx;
@@ -339,7 +340,8 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
                   "per-tile depth order");
     }
     GSR_STAGE(GSR_STAGE_BLEND_FWD, launch_blend_forward(*cam, j.rs->bg, j.ty0, j.ty1, v.ranges, v.sorted_gid, v.rec,
-                                                        j.out_color, v.final_T, v.accum, v.term, v.ck, stream),
+                                                        j.out_color, v.final_T, v.accum, v.term, v.ck_slot,
+                                                        v.counters + kCkPoolSlot, v.ck, cap, stream),
               "blend forward");
     return 0;
 }
@@ -392,7 +394,8 @@ int blend_backward(const gsr_camera* cam, const gsr_raster_settings* rs, const g
     // only the per-entry flag bytes are zeroed: the gather reads the entries B1 flagged
     GSR_STAGE(GSR_STAGE_MISC, launch_clear_flags(partial, cap, stream), "clear partial flags");
     GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.rect, v.rec,
-                                                         v.final_T, v.accum, dL_dpix, partial, cap, v.term, v.ck, stream),
+                                                         v.final_T, v.accum, dL_dpix, partial, cap, v.term, v.ck_slot,
+                                                         v.ck, stream),
               "blend backward");
     GSR_STAGE(GSR_STAGE_GATHER, launch_gather_grad2d(v.offsets, partial, v.rec, cam->width, cam->height, cap, (int)n,
                                                      grad2d, stream),
@@ -462,7 +465,12 @@ int gsr_abi_version(void) { return GSR_ABI_VERSION; }
 const char* gsr_last_error(void) { return g_err.c_str(); }
 
 size_t gsr_geom_bytes(int32_t P) { return GeomLayout(P).total; }
-size_t gsr_binning_bytes(int32_t capacity) { return BinLayout(capacity).total; }
+size_t gsr_ck_pool_slots(int32_t capacity, int32_t w, int32_t h) {
+    return ck_pool_slots(capacity, (long long)ImgLayout::tile_count(w, h));
+}
+size_t gsr_binning_bytes(int32_t capacity, int32_t w, int32_t h) {
+    return BinLayout(capacity, (long long)ImgLayout::tile_count(w, h)).total;
+}
 size_t gsr_image_bytes(int32_t w, int32_t h) { return ImgLayout(w, h).total; }
 size_t gsr_scratch_bytes(int32_t capacity) { return PartLayout(capacity).total; }
 size_t gsr_exchange_block_bytes(int32_t pair_cap) { return exchange_block_bytes(pair_cap > 0 ? pair_cap : 0); }
@@ -782,7 +790,12 @@ const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, 
         case GSR_VIEW_RECORDS: return v.rec;
         case GSR_VIEW_COUNTS: return v.K_dev;
         case GSR_VIEW_TERM: return v.term;
-        case GSR_VIEW_CK_LIVE: return v.ck + ck_live_offset(ImgLayout::tile_count(cam->width, cam->height));
+        case GSR_VIEW_CK_LIVE:
+            if (!bufs->binning) return nullptr;
+            return static_cast<const char*>(bufs->binning) +
+                   BinLayout(bufs->capacity, (long long)ImgLayout::tile_count(cam->width, cam->height)).ckm;
+        case GSR_VIEW_CK_SLOT: return v.ck_slot;
+        case GSR_VIEW_CK_POOL: return v.counters + kCkPoolSlot;
         default: return nullptr;
     }
 }

@@ -71,7 +71,8 @@ __device__ __forceinline__ void quad_reduce(float (&v)[N]) {
 
 
 struct BlendGeom {
-    int W, H, grid_x, ty0, nwg, ntiles;  // ntiles: the full image's tiles (checkpoint layout)
+    int W, H, grid_x, ty0, nwg;
+    uint32_t ck_slots;  // checkpoint pool size (slots); the live bytes follow the float4 slots
     float bg0, bg1, bg2;
 };
 
@@ -169,6 +170,8 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
                                                                 float* __restrict__ final_T,
                                                                 float* __restrict__ accum,
                                                                 uint32_t* __restrict__ term,
+                                                                uint32_t* __restrict__ ck_slot,
+                                                                uint32_t* __restrict__ pool_ctr,
                                                                 float4* __restrict__ ck) {
     constexpr int PPL = kPPL / NW;
     constexpr int BATCH = 64 * NW;
@@ -176,6 +179,7 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
     __shared__ float4 srec[BATCH * 3];
     __shared__ uint32_t smk[BATCH];
     __shared__ uint32_t slive[NW];
+    __shared__ uint32_t s_slot0;
     const int tl = xcd_tile(blockIdx.x, geo.nwg);  // band-local tile index
     const int tile = tl + geo.ty0 * geo.grid_x;
     const int tx = tile % geo.grid_x, ty = tile / geo.grid_x;
@@ -199,21 +203,23 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
     // the same chunk decisions, including a wave whose own pixels have all finished (it keeps
     // writing its final state at the later checkpoints).
     uint32_t* const table = term + (size_t)tl * kMaxChunks;  // [term, chunk 1.. starts]
+    uint32_t* const slots = ck_slot + (size_t)tl * kMaxChunks;  // chunk c -> its pool slot
     int nck = 0;   // checkpoints written
     int work = 0;  // pairs in the current chunk
     int tend = n;  // termination index: every pixel of the tile has finished before record tend
+    bool pool_ok = true;     // block-uniform: the pool had room for every batch so far
+    uint32_t next_slot = 0;  // the batch's next claimed slot
     // A stripe with no live pixel (its `live` bit clear: conservative, the bit is cleared only
     // once every T <= 0) is not written; its byte tells B1 to start it dead (T = -1), which is
     // all B1 needs of a finished pixel.
-    uint8_t* const ckm = reinterpret_cast<uint8_t*>(ck + ck_live_offset(geo.ntiles));
-    auto checkpoint = [&](int c, uint32_t lv) {
-        const size_t slot = (size_t)tl * (kMaxChunks - 1) + c;
-        float4* dst = ck + slot * 256;
+    uint8_t* const ckm = reinterpret_cast<uint8_t*>(ck + (size_t)geo.ck_slots * 256);
+    auto checkpoint = [&](uint32_t slot, uint32_t lv) {
+        float4* dst = ck + (size_t)slot * 256;
 #pragma unroll
         for (int p = 0; p < PPL; ++p) {
             const bool on = (lv >> p) & 1u;  // wave-uniform
             if (on) dst[64 * (w * PPL + p) + lane] = make_float4(T[p], C0[p], C1[p], C2[p]);
-            if (lane == 0) ckm[4 * slot + w * PPL + p] = on ? 1 : 0;
+            if (lane == 0) ckm[4 * (size_t)slot + w * PPL + p] = on ? 1 : 0;
         }
     };
     for (int base = 0; base < n; base += BATCH) {
@@ -241,13 +247,38 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
 #pragma unroll
         for (int i = 0; i < NW; ++i) tile_live |= slive[i];
         const int cnt = (n - base) < BATCH ? (n - base) : BATCH;
+        if (pool_ok) {
+            // the chunks this batch opens, decided ahead by the rule the loop below applies (all
+            // its inputs are in LDS already), so the block claims their pool slots in one atomic
+            int sw = work, sn = nck, opens = 0;
+            for (int c0 = 0; c0 < cnt; c0 += 64) {
+                if (sw >= kCW && sn < kMaxChunks - 1) {
+                    ++opens;
+                    ++sn;
+                    sw = 0;
+                }
+                const uint32_t tm = smk[c0 + lane] & tile_live;
+                sw += __popcll(__ballot(tm & 1u)) + __popcll(__ballot(tm & 2u)) + __popcll(__ballot(tm & 4u)) +
+                      __popcll(__ballot(tm & 8u));
+            }
+            if (opens) {  // block-uniform
+                if (tid == 0) s_slot0 = atomicAdd(pool_ctr, (uint32_t)opens);
+                __syncthreads();
+                next_slot = s_slot0;  // rewritten only after the batch-end barrier
+                pool_ok = next_slot + (uint32_t)opens <= geo.ck_slots;
+            }
+        }
         int visited = 0;
         for (int c0 = 0; c0 < cnt; c0 += 64) {
             const uint32_t sm = smk[c0 + lane];  // 0 past cnt
-            if (work >= kCW && nck < kMaxChunks - 1) {  // chunk nck + 1 starts at base + c0
-                checkpoint(nck, live);
+            if (work >= kCW && nck < kMaxChunks - 1 && pool_ok) {  // chunk nck + 1 starts at base + c0
+                checkpoint(next_slot, live);
                 ++nck;
-                if (tid == 0) table[nck] = (uint32_t)(base + c0);
+                if (tid == 0) {
+                    table[nck] = (uint32_t)(base + c0);
+                    slots[nck] = next_slot;
+                }
+                ++next_slot;
                 work = 0;
             }
             const uint32_t tm = sm & tile_live;
@@ -380,6 +411,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                                                             float* __restrict__ p1,
                                                             uint8_t* __restrict__ fl,
                                                             const uint32_t* __restrict__ term,
+                                                            const uint32_t* __restrict__ ck_slot,
                                                             const float4* __restrict__ ck) {
     __shared__ float4 srec[64 * 3];
     __shared__ float qpark[kPark * kParkSlot];  // [slot][quad][9 of 12]
@@ -435,11 +467,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
         T[p] = in ? 1.0f : -1.0f;
     }
     if (chunk > 0) {  // resume from F6's checkpoint: T, and R less dL/dpix . (colour sum so far)
-        const size_t slot = (size_t)tl * (kMaxChunks - 1) + (chunk - 1);
+        const size_t slot = ck_slot[(size_t)tl * kMaxChunks + chunk];
         const float4* src = ck + slot * 256;
         // F6's live-stripe bytes: a stripe it did not write had finished (start it dead)
         const uint32_t on = *reinterpret_cast<const uint32_t*>(
-            reinterpret_cast<const uint8_t*>(ck + ck_live_offset(geo.ntiles)) + 4 * slot);
+            reinterpret_cast<const uint8_t*>(ck + (size_t)geo.ck_slots * 256) + 4 * slot);
 #pragma unroll
         for (int p = 0; p < kPPL; ++p) {
             if ((on >> (8 * p)) & 0xFFu) {  // wave-uniform
@@ -563,14 +595,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
 #endif
 constexpr int kF6FullWaves = 2, kF6BandWaves = 4, kF6BandTiles = GSR_F6_BAND_TILES;
 
-static BlendGeom make_geo(const gsr_camera& cam, const float bg[3], int ty0, int ty1) {
+static BlendGeom make_geo(const gsr_camera& cam, const float bg[3], int ty0, int ty1, long long cap) {
     BlendGeom g;
     g.W = cam.width;
     g.H = cam.height;
     g.grid_x = div_up(cam.width, kTile);
     g.ty0 = ty0;
     g.nwg = (ty1 - ty0) * g.grid_x;
-    g.ntiles = div_up(cam.height, kTile) * g.grid_x;
+    g.ck_slots = (uint32_t)ck_pool_slots(cap, (long long)div_up(cam.height, kTile) * g.grid_x);  // = BinLayout's
     g.bg0 = bg[0];
     g.bg1 = bg[1];
     g.bg2 = bg[2];
@@ -579,16 +611,16 @@ static BlendGeom make_geo(const gsr_camera& cam, const float bg[3], int ty0, int
 
 int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
                          const uint2* ranges, const uint32_t* sorted_gid, const float4* rec,
-                         float* out_color, float* final_T, float* accum, uint32_t* term, float4* ck,
-                         hipStream_t s) {
-    const BlendGeom geo = make_geo(cam, bg, ty0, ty1);
+                         float* out_color, float* final_T, float* accum, uint32_t* term, uint32_t* ck_slot,
+                         uint32_t* pool_ctr, float4* ck, long long cap, hipStream_t s) {
+    const BlendGeom geo = make_geo(cam, bg, ty0, ty1, cap);
     if (geo.nwg <= 0) return 0;
     if (geo.nwg >= kF6BandTiles)
         hipLaunchKernelGGL(blend_forward_kernel<kF6FullWaves>, dim3(geo.nwg), dim3(64 * kF6FullWaves), 0, s, geo,
-                           ranges, sorted_gid, rec, out_color, final_T, accum, term, ck);
+                           ranges, sorted_gid, rec, out_color, final_T, accum, term, ck_slot, pool_ctr, ck);
     else
         hipLaunchKernelGGL(blend_forward_kernel<kF6BandWaves>, dim3(geo.nwg), dim3(64 * kF6BandWaves), 0, s, geo,
-                           ranges, sorted_gid, rec, out_color, final_T, accum, term, ck);
+                           ranges, sorted_gid, rec, out_color, final_T, accum, term, ck_slot, pool_ctr, ck);
     return (int)hipGetLastError();
 }
 
@@ -596,15 +628,16 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
                           const uint2* ranges, const uint32_t* sorted_gid, const uint4* rect,
                           const float4* rec, const float* final_T,
                           const float* accum, const float* dL_dpix, float* partial, long long cap,
-                          const uint32_t* term, const float4* ck, hipStream_t s) {
-    const BlendGeom geo = make_geo(cam, bg, ty0, ty1);
+                          const uint32_t* term, const uint32_t* ck_slot, const float4* ck, hipStream_t s) {
+    const BlendGeom geo = make_geo(cam, bg, ty0, ty1, cap);
     if (geo.nwg <= 0) return 0;
     const PartLayout pl(cap);
     char* base = reinterpret_cast<char*>(partial);
     const int blocks = 8 * (geo.nwg / 8 + 1) * kMaxChunks;
     hipLaunchKernelGGL(blend_backward_kernel, dim3(blocks), dim3(64), 0, s, geo, ranges, sorted_gid, rect, rec,
                        final_T, accum, dL_dpix, reinterpret_cast<float*>(base + pl.p8),
-                       reinterpret_cast<float*>(base + pl.p1), reinterpret_cast<uint8_t*>(base + pl.fl), term, ck);
+                       reinterpret_cast<float*>(base + pl.p1), reinterpret_cast<uint8_t*>(base + pl.fl), term, ck_slot,
+                       ck);
     return (int)hipGetLastError();
 }
 

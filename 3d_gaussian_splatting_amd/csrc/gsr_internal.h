@@ -62,22 +62,6 @@ struct GeomLayout {
     }
 };
 
-// Binning for up to `cap` instances (the exact K, or a caller-given bound).  The tile-key sort
-// ping-pongs (kA, vA) <-> (kB, vB); F3 emits into (kA, vA).
-struct BinLayout {
-    size_t kA, vA, kB, vB, hist, total;
-    BinLayout(long long cap) {
-        size_t o = 0, n = (size_t)(cap > 0 ? cap : 1);
-        auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
-        kA = take(4 * n);
-        vA = take(4 * n);
-        kB = take(4 * n);
-        vB = take(4 * n);
-        hist = take(4 * sort_scratch_words(n));
-        total = o;
-    }
-};
-
 // Chunked B1: F6 checkpoints every pixel's (T, colour sum) at up to kMaxChunks - 1 points of each
 // tile's list, so B1 sweeps the chunks of one tile in parallel blocks (a shorter tail; essential
 // for multi-GPU bands, which hold 1/N of the tiles).  The points are chosen by B1's own cost:
@@ -91,12 +75,43 @@ struct BinLayout {
 #endif
 constexpr int kMaxChunks = GSR_MAX_CHUNKS;  // = GSR_TERM_STRIDE (gsr.h) in the shipped build
 
-// The live-stripe bytes of the checkpoint region start after the float4 checkpoints of all
-// `tiles` tiles of the image (the full image's tile count, also for band launches).
-__host__ __device__ inline size_t ck_live_offset(size_t tiles) { return tiles * (kMaxChunks - 1) * 256; }
+// Checkpoint pool.  A checkpoint (4 KB: float4 (T, C) per pixel of a tile) is taken from a pool
+// of slots that F6 claims batch by batch (one atomic per batch that opens a chunk), instead of
+// a fixed tiles x 31 array (1.0 GB at 1080p, 4.1 GB at 4K, whether or not a chunk opens).  A
+// chunk opens after kChunkWork visited (record, stripe) pairs, so a tile's opens are bounded by
+// its list, and the whole image opens ~K / 240 chunks at 1M / 1080p (27k of the 253k fixed
+// slots): the pool holds 2 per tile plus one per 96 instances of capacity, capped at the fixed
+// array.  A tile that finds the pool exhausted opens no more chunks (its last chunk runs longer
+// in B1; results stay exact); GSR_VIEW_CK_POOL reports the slots claimed against the pool.
+inline size_t ck_pool_slots(long long cap, long long tiles) {
+    const size_t t = (size_t)(tiles > 0 ? tiles : 1);
+    const size_t full = t * (kMaxChunks - 1);
+    const size_t want = 2 * t + (size_t)(cap > 0 ? cap : 0) / 96;
+    return want < full ? want : full;
+}
+
+// Binning for up to `cap` instances (the exact K, or a caller-given bound) of a launch over
+// `tiles` tiles.  The tile-key sort ping-pongs (kA, vA) <-> (kB, vB); F3 emits into (kA, vA).
+// Then the checkpoint pool: ck_slots x 256 float4, and one live byte per (slot, 16x4 stripe).
+struct BinLayout {
+    size_t kA, vA, kB, vB, hist, ck, ckm, total, ck_slots;
+    BinLayout(long long cap, long long tiles) {
+        size_t o = 0, n = (size_t)(cap > 0 ? cap : 1);
+        auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
+        kA = take(4 * n);
+        vA = take(4 * n);
+        kB = take(4 * n);
+        vB = take(4 * n);
+        hist = take(4 * sort_scratch_words(n));
+        ck_slots = ck_pool_slots(cap, tiles);
+        ck = take(ck_slots * 256 * 16);
+        ckm = take(ck_slots * 4);
+        total = o;
+    }
+};
 
 struct ImgLayout {
-    size_t ranges, counters, done, ovf, ovf2, term, final_T, accum, ck, total;
+    size_t ranges, counters, done, ovf, ovf2, term, ck_slot, final_T, accum, total;
     static size_t tile_count(int W, int H) {
         const size_t t = (size_t)div_up(W, kTile) * div_up(H, kTile);
         return t ? t : 1;
@@ -112,11 +127,9 @@ struct ImgLayout {
         ovf = take(4 * tiles);   // tiles the per-tile depth sort hands to its larger
         ovf2 = take(4 * tiles);  // forms (queues: the 8192-entry form, then the 16384-entry / chunked one)
         term = take(4 * tiles * kMaxChunks);  // F6: per tile [termination index, chunk 1..kMaxChunks-1 starts]
+        ck_slot = take(4 * tiles * kMaxChunks);  // F6: per tile and chunk c >= 1, its checkpoint pool slot
         final_T = take(4 * (pix ? pix : 1));
         accum = take(12 * (pix ? pix : 1));  // colour sum without background, 3 x H x W
-        // float4 (T, C) checkpoints, then one byte per (tile, chunk, stripe): 1 where F6 wrote
-        // that stripe's checkpoint (it skips stripes with no live pixel; see ck_live_bytes)
-        ck = take(tiles * (kMaxChunks - 1) * (256 * 16 + 4));
         total = o;
     }
 };
@@ -173,6 +186,7 @@ struct ShardLayout {
 constexpr int kTotalSlot = 2 * kCountSlots;          // K = sum of tiles_touched, written by the scan
 constexpr int kOvfCountSlot = 2 * kCountSlots + 8;   // tiles queued for the large per-tile depth sort
 constexpr int kOvf2CountSlot = 2 * kCountSlots + 9;  // ... then for its 16384-entry / chunked form
+constexpr int kCkPoolSlot = 2 * kCountSlots + 10;    // checkpoint pool slots F6 claimed
 
 // number of 8-bit LSD passes to sort tile ids of a grid with `tiles` tiles
 inline int tile_bits(int tiles) {

@@ -19,7 +19,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(PKG, "lib")
 HIP_LIB = os.path.join(LIB_DIR, "libgsr_hip.so")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 GSR_FLAG_DEBUG = 1
 GSR_ERR_OVERFLOW = -4
 GSR_GRAD2D_STRIDE = 12
@@ -28,13 +28,13 @@ GSR_SPLAT_BYTES = 64
 GSR_SPLAT_GRAD_BYTES = 48
 MAX_BANDS = 16
 VIEW_SORTED_GID, VIEW_SORTED_TILE, VIEW_RANGES, VIEW_FINAL_T, VIEW_N_CONTRIB, VIEW_DEPTH_KEY, \
-    VIEW_TILES_TOUCHED, VIEW_RECORDS, VIEW_COUNTS, VIEW_TERM, VIEW_CK_LIVE = range(1, 12)
+    VIEW_TILES_TOUCHED, VIEW_RECORDS, VIEW_COUNTS, VIEW_TERM, VIEW_CK_LIVE, VIEW_CK_SLOT, VIEW_CK_POOL = range(1, 14)
 TERM_STRIDE = 32  # GSR_TERM_STRIDE: words per tile of VIEW_TERM
 EXPORTS = ["gsr_abi_version", "gsr_last_error", "gsr_forward", "gsr_read_num_rendered", "gsr_forward_batch",
            "gsr_backward", "gsr_backward_blend", "gsr_backward_preprocess", "gsr_shard_forward",
            "gsr_band_forward", "gsr_band_backward", "gsr_shard_backward", "gsr_exchange_block_bytes",
            "gsr_shard_state_bytes", "gsr_view", "gsr_geom_bytes", "gsr_binning_bytes",
-           "gsr_image_bytes", "gsr_scratch_bytes", "gsr_profile_enable", "gsr_profile_read",
+           "gsr_image_bytes", "gsr_scratch_bytes", "gsr_ck_pool_slots", "gsr_profile_enable", "gsr_profile_read",
            "gsr_stage_name"]
 # include/gsr/gsr_train.h (training-step kernels)
 TRAIN_EXPORTS = ["gsr_activate", "gsr_loss_scratch_bytes", "gsr_loss_forward", "gsr_loss_backward", "gsr_adam_step",
@@ -149,9 +149,12 @@ def load_hip() -> ctypes.CDLL:
                                          i32, pi32, i32, vp, vp, ctypes.POINTER(Grads), vp]
         L.gsr_view.restype = vp
         L.gsr_view.argtypes = [ctypes.POINTER(Camera), i32, ctypes.POINTER(Buffers), ctypes.c_int]
-        for n in ("gsr_geom_bytes", "gsr_binning_bytes", "gsr_scratch_bytes"):
+        for n in ("gsr_geom_bytes", "gsr_scratch_bytes"):
             getattr(L, n).restype = ctypes.c_size_t
             getattr(L, n).argtypes = [i32]
+        for n in ("gsr_binning_bytes", "gsr_ck_pool_slots"):
+            getattr(L, n).restype = ctypes.c_size_t
+            getattr(L, n).argtypes = [i32, i32, i32]
         L.gsr_profile_enable.restype = ctypes.c_int
         L.gsr_profile_enable.argtypes = [ctypes.c_uint32]
         L.gsr_profile_read.restype = ctypes.c_int

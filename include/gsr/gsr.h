@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 2
+#define GSR_ABI_VERSION 3
 #define GSR_TILE 16 /* screen tiles are GSR_TILE x GSR_TILE pixels */
 #define GSR_GRAD2D_STRIDE 12 /* floats per Gaussian in a grad2d buffer (9 used) */
 
@@ -233,10 +233,17 @@ int gsr_shard_backward(const gsr_camera* cam, const gsr_gaussians* shard, const 
                                        termination index, then the B1 chunk 1..31 start
                                        records (UINT32_MAX: no such chunk)                 */
 #define GSR_TERM_STRIDE 32          /* words per tile of GSR_VIEW_TERM                     */
-#define GSR_VIEW_CK_LIVE 11         /* uint8[tiles*(GSR_TERM_STRIDE-1)*4]: per tile and B1
-                                       chunk 1..31, per 16x4 pixel stripe, 1 where F6 wrote
-                                       that stripe's checkpoint (0: it had finished; only
-                                       the entries of chunks the tile opened are defined)  */
+#define GSR_VIEW_CK_LIVE 11         /* uint8[slots*4]: per checkpoint-pool slot and 16x4
+                                       pixel stripe, 1 where F6 wrote that stripe's
+                                       checkpoint (0: it had finished); only the slots F6
+                                       claimed are defined (GSR_VIEW_CK_SLOT / _CK_POOL)    */
+#define GSR_VIEW_CK_SLOT 12         /* uint32[tiles*GSR_TERM_STRIDE]: per tile, the pool
+                                       slot of chunk c in word c (c >= 1; defined where
+                                       GSR_VIEW_TERM says the chunk opened)                 */
+#define GSR_VIEW_CK_POOL 13         /* uint32[1]: checkpoint-pool slots F6 claimed (may
+                                       exceed the pool: a tile that found it exhausted
+                                       opened no more chunks); the pool holds
+                                       gsr_ck_pool_slots(capacity, width, height) slots     */
 #define GSR_VIEW_RECORDS 8          /* float4[3*P]: {x,y,a',b'},{c',o,r,g},{b,ext_x,ext_y,log2 o};
                                        a',b',c' = -log2(e) * (A/2, B, C/2) of the conic */
 const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, int what);
@@ -262,9 +269,12 @@ int gsr_profile_enable(uint32_t stage_mask);
 int gsr_profile_read(double* ms, uint32_t* counts);
 const char* gsr_stage_name(int stage);
 
-/* Byte sizes the allocation callbacks will be asked for (for pre-sizing pools). */
+/* Byte sizes the allocation callbacks will be asked for (for pre-sizing pools).  The binning
+ * buffer holds the instance arrays for `capacity` instances and the B1 checkpoint pool (ABI 3:
+ * sized by capacity and image, no longer a fixed 31 checkpoints per tile in the image buffer). */
 size_t gsr_geom_bytes(int32_t P);
-size_t gsr_binning_bytes(int32_t capacity);
+size_t gsr_binning_bytes(int32_t capacity, int32_t width, int32_t height);
+size_t gsr_ck_pool_slots(int32_t capacity, int32_t width, int32_t height);
 size_t gsr_image_bytes(int32_t width, int32_t height);
 size_t gsr_scratch_bytes(int32_t capacity);
 

@@ -502,10 +502,16 @@ def test_chunk_checkpoints_with_finished_stripes(W, H, P_back, rast, oracle):
     tiles = cam.grid[0] * cam.grid[1]
     S = native.TERM_STRIDE
     term = _np(st.view(native.VIEW_TERM, torch.int32, tiles * S)).view(np.uint32).reshape(tiles, S)
-    live = _np(st.view(native.VIEW_CK_LIVE, torch.uint8, tiles * (S - 1) * 4)).reshape(tiles, S - 1, 4)
+    slot = _np(st.view(native.VIEW_CK_SLOT, torch.int32, tiles * S)).view(np.uint32).reshape(tiles, S)
+    pool = int(native.load_hip().gsr_ck_pool_slots(st.buffers.capacity, W, H))
+    used = int(_np(st.view(native.VIEW_CK_POOL, torch.int32, 1))[0])
+    live = _np(st.view(native.VIEW_CK_LIVE, torch.uint8, pool * 4)).reshape(pool, 4)
     opened = term[:, 1:] != 0xFFFFFFFF
     assert opened.sum() > tiles  # more than one chunk per tile on average
-    on = live[opened]
+    assert used == opened.sum() <= pool  # every opened chunk holds its own claimed slot
+    ids = slot[:, 1:][opened]
+    assert len(np.unique(ids)) == len(ids) and ids.max() < pool
+    on = live[ids]
     assert set(np.unique(on)) <= {0, 1}
     # the top stripes start finished in a large share of the opened chunks (a tile's first
     # chunk can open while the sheets are still being blended), the bottom one mostly live
@@ -516,3 +522,28 @@ def test_chunk_checkpoints_with_finished_stripes(W, H, P_back, rast, oracle):
     # every tensor stays at the 1e-4 bar inside _compare).
     worst = _compare(st, f, sc.make_dL_dpix(cam, seed=22), rast, elem_grads=False)
     assert max(v[0] for v in worst.values()) <= 2e-3, worst
+
+
+def test_checkpoint_pool_exhaustion_stays_exact(rast, oracle):
+    """The B1 checkpoint pool (2 slots per tile + 1 per 96 instances) can run out for a scene whose
+    every tile holds ~2000 faint records that never terminate (each opens 31 chunks): tiles that
+    find it exhausted open no more chunks, and the image and every gradient still match the
+    oracle (the chunks only split B1's work)."""
+    gr, sc = pkg("graphics"), pkg("scene")
+    native = pkg("native")
+    cam = gr.synthetic_camera(64, 64)
+    s = sc.make_scene(cam, 2000, max_sh_degree=1, seed=71)
+    P = s.P
+    rng = np.random.default_rng(71)
+    z = np.linspace(4.0, 8.0, P)
+    xy = rng.uniform(-0.4, 0.4, (P, 2)) * z[:, None] * np.array([cam.tanfovx, cam.tanfovy])
+    s.means3D = np.concatenate([xy, z[:, None]], 1).astype(np.float32)
+    s.scales = np.full((P, 3), 2.0, np.float32)  # ~40-80 px: every Gaussian spans most tiles
+    s.opacities = np.full((P, 1), 0.01, np.float32)  # faint: lists run ~1000 records deep
+    args = (cam, s.means3D, s.opacities, s.scales, s.rotations, s.sh_dc, s.sh_rest)
+    st = rast.forward(*args, sh_degree=1)
+    f = oracle.forward(*args, sh_degree=1)
+    pool = int(native.load_hip().gsr_ck_pool_slots(st.buffers.capacity, cam.width, cam.height))
+    used = int(_np(st.view(native.VIEW_CK_POOL, torch.int32, 1))[0])
+    assert used > pool, (used, pool)  # the fallback ran
+    _compare(st, f, sc.make_dL_dpix(cam, seed=72), rast)

@@ -57,6 +57,7 @@ def test_header_constants_match_the_python_mirror():
     assert val("GSR_TERM_STRIDE") == native.TERM_STRIDE
     assert val("GSR_VIEW_TERM") == native.VIEW_TERM
     assert val("GSR_VIEW_CK_LIVE") == native.VIEW_CK_LIVE
+    assert val("GSR_VIEW_CK_SLOT") == native.VIEW_CK_SLOT and val("GSR_VIEW_CK_POOL") == native.VIEW_CK_POOL
 
 
 def test_library_exports_every_symbol():
@@ -72,10 +73,17 @@ def test_library_exports_every_symbol():
 def test_library_loads_and_reports_sizes():
     native = pkg("native")
     L = native.load_hip()
-    assert L.gsr_abi_version() == native.ABI_VERSION == 2
+    assert L.gsr_abi_version() == native.ABI_VERSION == 3
     assert L.gsr_geom_bytes(1000) > 1000 * 64
-    assert L.gsr_binning_bytes(10) >= 10 * 24
+    assert L.gsr_binning_bytes(10, 64, 64) >= 10 * 24
     assert L.gsr_image_bytes(1920, 1080) >= 1920 * 1080 * 8
+    # the B1 checkpoint pool (binning buffer): 2 slots per tile + 1 per 96 instances of capacity,
+    # at most the 31 per tile a fixed array would hold -- 1080p, 7.2M instances: ~0.37 GB, not 1.0
+    tiles = 120 * 68
+    assert L.gsr_ck_pool_slots(7_200_000, 1920, 1080) == 2 * tiles + 7_200_000 // 96
+    assert L.gsr_ck_pool_slots(2**31 - 1, 1920, 1080) == 31 * tiles
+    assert L.gsr_binning_bytes(7_200_000, 1920, 1080) < 16 * 7_200_000 + 4100 * (2 * tiles + 7_200_000 // 96) + (64 << 20)
+    assert L.gsr_image_bytes(1920, 1080) < 64 << 20  # no per-tile checkpoint array any more
     assert L.gsr_scratch_bytes(100) >= 100 * 37  # 36-B partial + 1 flag byte per instance
     assert L.gsr_scratch_bytes(1 << 20) == (32 << 20) + (4 << 20) + (1 << 20)
     assert L.gsr_exchange_block_bytes(100) == 64 * 101
@@ -163,7 +171,7 @@ def test_validation_rejects_bad_arguments_without_gpu():
 def test_torch_extension_loads():
     native = pkg("native")
     ext = native.load_torch_ext()
-    assert ext.abi_version() == 2
+    assert ext.abi_version() == 3
     cam = ext.RasterCamera(16, 16, 0.5, 0.5, [0.0] * 16, [0.0] * 16, [0.0] * 3)
     assert cam.width == 16
 
