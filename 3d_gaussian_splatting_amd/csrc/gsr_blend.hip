@@ -26,15 +26,16 @@
 // four records at a time (one (record, moment) output per lane, stored straight to HBM) --
 // ~40% fewer VALU ops than a full 64-lane DPP/permlane reduction per record, and no per-batch
 // moment buffer in LDS (more waves per SIMD).  It writes ONE 36-B partial per contributing
-// (tile, instance) with plain stores, indexed by the instance's emission index j; the rest stay
-// at the zeros the launcher clears the partial block to, and a tile stops at the first batch
-// whose pixels have all terminated.
+// (tile, instance) with plain stores, indexed by the instance's emission index j, and sets that
+// entry's flag byte; the gather reads flagged entries only (the launcher zeroes the K flag bytes,
+// never the 36-B entries), and a tile stops at the first batch whose pixels have all terminated.
 //
-// Measured and rejected (scripts/ablate.py): packing two stripes per VGPR pair
-// (v_pk_fma_f32 issues 2 FMAs in 4 cycles -- no gain over v_fma_f32 on gfx950, and the
-// register shuffles cost extra); 4 waves per tile; record prefetch into registers.  The
-// per-Gaussian sum happens later in fixed emission order (gsr_preprocess_bwd.hip), so
-// gradients are deterministic and no float atomics are issued.
+// Measured and rejected (experiments are separate builds,
+// _build.build_variant + scripts/ab.sh): packing two stripes per VGPR pair (v_pk_fma_f32 issues
+// 2 FMAs in 4 cycles -- no gain over v_fma_f32 on gfx950, and the register shuffles cost extra);
+// 4 waves per tile; record prefetch into registers.  The per-Gaussian sum happens later in fixed
+// emission order (gsr_preprocess_bwd.hip), so gradients are deterministic and no float atomics
+// are issued.
 #include "gsr_kernels.h"
 
 namespace gsr {
@@ -72,7 +73,8 @@ __device__ __forceinline__ void quad_reduce(float (&v)[N]) {
 
 struct BlendGeom {
     int W, H, grid_x, ty0, nwg;
-    uint32_t ck_slots;  // checkpoint pool size (slots); the live bytes follow the float4 slots
+    uint32_t ck_slots;   // checkpoint pool size (slots); the live bytes follow the float4 slots
+    uint32_t ck_shards;  // its sub-pools (ck_shards of the full image)
     float bg0, bg1, bg2;
 };
 
@@ -262,10 +264,12 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
                       __popcll(__ballot(tm & 8u));
             }
             if (opens) {  // block-uniform
-                if (tid == 0) s_slot0 = atomicAdd(pool_ctr, (uint32_t)opens);
+                const uint32_t shard = (uint32_t)tl % geo.ck_shards, per = geo.ck_slots / geo.ck_shards;
+                if (tid == 0) s_slot0 = atomicAdd(pool_ctr + shard, (uint32_t)opens);
                 __syncthreads();
-                next_slot = s_slot0;  // rewritten only after the batch-end barrier
-                pool_ok = next_slot + (uint32_t)opens <= geo.ck_slots;
+                const uint32_t got = s_slot0;  // rewritten only after the batch-end barrier
+                pool_ok = got + (uint32_t)opens <= per;
+                next_slot = shard * per + got;
             }
         }
         int visited = 0;
@@ -602,7 +606,9 @@ static BlendGeom make_geo(const gsr_camera& cam, const float bg[3], int ty0, int
     g.grid_x = div_up(cam.width, kTile);
     g.ty0 = ty0;
     g.nwg = (ty1 - ty0) * g.grid_x;
-    g.ck_slots = (uint32_t)ck_pool_slots(cap, (long long)div_up(cam.height, kTile) * g.grid_x);  // = BinLayout's
+    const long long full_tiles = (long long)div_up(cam.height, kTile) * g.grid_x;
+    g.ck_slots = (uint32_t)ck_pool_slots(cap, full_tiles);  // = BinLayout's
+    g.ck_shards = (uint32_t)ck_shards(full_tiles);
     g.bg0 = bg[0];
     g.bg1 = bg[1];
     g.bg2 = bg[2];

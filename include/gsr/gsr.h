@@ -240,10 +240,12 @@ int gsr_shard_backward(const gsr_camera* cam, const gsr_gaussians* shard, const 
 #define GSR_VIEW_CK_SLOT 12         /* uint32[tiles*GSR_TERM_STRIDE]: per tile, the pool
                                        slot of chunk c in word c (c >= 1; defined where
                                        GSR_VIEW_TERM says the chunk opened)                 */
-#define GSR_VIEW_CK_POOL 13         /* uint32[1]: checkpoint-pool slots F6 claimed (may
-                                       exceed the pool: a tile that found it exhausted
-                                       opened no more chunks); the pool holds
-                                       gsr_ck_pool_slots(capacity, width, height) slots     */
+#define GSR_VIEW_CK_POOL 13         /* uint32[S]: checkpoint-pool slots F6 claimed per
+                                       sub-pool, S = min(GSR_CK_SHARDS, tiles) (tile t draws
+                                       from sub-pool t % S, which holds
+                                       gsr_ck_pool_slots(...) / S slots; a count above that
+                                       means it ran out and its tiles opened fewer chunks) */
+#define GSR_CK_SHARDS 64
 #define GSR_VIEW_RECORDS 8          /* float4[3*P]: {x,y,a',b'},{c',o,r,g},{b,ext_x,ext_y,log2 o};
                                        a',b',c' = -log2(e) * (A/2, B, C/2) of the conic */
 const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, int what);
