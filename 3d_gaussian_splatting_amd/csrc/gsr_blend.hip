@@ -153,6 +153,11 @@ __device__ __forceinline__ float pair_alpha_keep(float e, float L, float& oG, bo
 #define GSR_CHUNK_WORK 192
 #endif
 constexpr int kChunkWork = GSR_CHUNK_WORK;
+// checkpoint slots a tile claims up front (gsr_internal.h, checkpoint pool)
+#ifndef GSR_CK_GRANULE
+#define GSR_CK_GRANULE 4
+#endif
+constexpr int kCkGranule = GSR_CK_GRANULE;
 // Band launches (multi-GPU, < 4096 tiles, 4-wave F6): the chunk bound for B1 there
 #ifndef GSR_BAND_CHUNK_WORK
 #define GSR_BAND_CHUNK_WORK GSR_CHUNK_WORK
@@ -209,8 +214,17 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
     int nck = 0;   // checkpoints written
     int work = 0;  // pairs in the current chunk
     int tend = n;  // termination index: every pixel of the tile has finished before record tend
-    bool pool_ok = true;     // block-uniform: the pool had room for every batch so far
-    uint32_t next_slot = 0;  // the batch's next claimed slot
+    bool pool_ok = true;     // block-uniform: the pool had room for every claim so far
+    uint32_t next_slot = 0;  // next claimed, unused slot
+    int avail = 0;           // claimed, unused slots left (block-uniform)
+    // Up front, a tile whose list can open chunks claims min(kCkGranule, the most it can open)
+    // slots of its sub-pool: that atomic's latency hides behind the first batch's loads, and
+    // most tiles never claim again (1M / 1080p: ~3.3 opens per tile).
+    const uint32_t shard = (uint32_t)tl % geo.ck_shards, per_shard = geo.ck_slots / geo.ck_shards;
+    int want0 = (4 * n) / kCW;
+    want0 = want0 < kCkGranule ? want0 : kCkGranule;
+    if (want0 > 0 && tid == 0) s_slot0 = atomicAdd(pool_ctr + shard, (uint32_t)want0);
+    bool first_claim = want0 > 0;  // read s_slot0 after the first batch's barrier
     // A stripe with no live pixel (its `live` bit clear: conservative, the bit is cleared only
     // once every T <= 0) is not written; its byte tells B1 to start it dead (T = -1), which is
     // all B1 needs of a finished pixel.
@@ -249,6 +263,14 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
 #pragma unroll
         for (int i = 0; i < NW; ++i) tile_live |= slive[i];
         const int cnt = (n - base) < BATCH ? (n - base) : BATCH;
+        if (first_claim) {  // the barrier above published the up-front claim
+            const uint32_t got = s_slot0;
+            pool_ok = got + (uint32_t)want0 <= per_shard;
+            next_slot = shard * per_shard + got;
+            avail = pool_ok ? want0 : 0;
+            first_claim = false;
+            __syncthreads();  // s_slot0 may be rewritten by a claim below
+        }
         if (pool_ok) {
             // the chunks this batch opens, decided ahead by the rule the loop below applies (all
             // its inputs are in LDS already), so the block claims their pool slots in one atomic
@@ -263,13 +285,13 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
                 sw += __popcll(__ballot(tm & 1u)) + __popcll(__ballot(tm & 2u)) + __popcll(__ballot(tm & 4u)) +
                       __popcll(__ballot(tm & 8u));
             }
-            if (opens) {  // block-uniform
-                const uint32_t shard = (uint32_t)tl % geo.ck_shards, per = geo.ck_slots / geo.ck_shards;
+            if (opens > avail) {  // block-uniform: claim this batch's opens afresh
                 if (tid == 0) s_slot0 = atomicAdd(pool_ctr + shard, (uint32_t)opens);
                 __syncthreads();
                 const uint32_t got = s_slot0;  // rewritten only after the batch-end barrier
-                pool_ok = got + (uint32_t)opens <= per;
-                next_slot = shard * per + got;
+                pool_ok = got + (uint32_t)opens <= per_shard;
+                next_slot = shard * per_shard + got;
+                avail = pool_ok ? opens : 0;
             }
         }
         int visited = 0;
@@ -283,6 +305,7 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
                     slots[nck] = next_slot;
                 }
                 ++next_slot;
+                --avail;
                 work = 0;
             }
             const uint32_t tm = sm & tile_live;

@@ -509,8 +509,9 @@ def test_chunk_checkpoints_with_finished_stripes(W, H, P_back, rast, oracle):
     live = _np(st.view(native.VIEW_CK_LIVE, torch.uint8, pool * 4)).reshape(pool, 4)
     opened = term[:, 1:] != 0xFFFFFFFF
     assert opened.sum() > tiles  # more than one chunk per tile on average
-    # every opened chunk holds its own claimed slot, and no sub-pool ran out
-    assert used.sum() == opened.sum() and used.max() <= pool // ns
+    # every opened chunk holds its own claimed slot (a tile claims a few slots up front, so some
+    # claimed slots stay unused), and no sub-pool ran out
+    assert used.sum() >= opened.sum() and used.max() <= pool // ns
     ids = slot[:, 1:][opened]
     assert len(np.unique(ids)) == len(ids) and ids.max() < pool
     on = live[ids]
