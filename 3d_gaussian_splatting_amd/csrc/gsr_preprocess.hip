@@ -257,9 +257,18 @@ __device__ __forceinline__ void write_record(int g, float opac, const Geo& G, co
 // Measured at 1M/SH3: direct 0.53 ms -- each lane's 180-B row at a 180-B lane stride touches
 // ~90 cache lines per load instruction; whole rows staged in LDS (46 KB, 3 waves per SIMD)
 // 0.106 ms; chunks 0.082 ms.
-enum { kShDirect = 0, kShChunks = 2 };
+//  kShWave   : wave w's 64 rows are one contiguous, 16-B aligned span; it stages them 16 rows at
+//              a time with 16-B buffer loads (3 per lane at SH3) into a wave-private LDS window
+//              (16 rows: 2.9 KB per wave at SH3) -- every cache line is read once, with a quarter
+//              of the load instructions and no block barrier -- and the 16 lanes owning those
+//              rows accumulate them (same k order: bit-identical).
+enum { kShDirect = 0, kShChunks = 2, kShWave = 3 };
 constexpr int kChunkK = 5;               // SH coefficients per staged chunk
 constexpr int kChunkF = 3 * kChunkK;     // floats per row per chunk
+constexpr int kSubRows = 16;             // kShWave: rows per staged window
+#ifndef GSR_F1_SH_MODE
+#define GSR_F1_SH_MODE kShWave
+#endif
 
 // The block also adds its candidate count (Gaussians with tiles in the band) and instance
 // count (sum of tiles_touched) into counters[slot] / counters[kCountSlots + slot], so the host
@@ -291,9 +300,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void p
             pre[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                                    rsrc, voff, j * 16 * M3 * (int)sizeof(float), 0));
     };
+    // kShWave: this wave's rows [64 w, 64 w + 64) of the block, staged kSubRows at a time
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const int sub_f4 = kSubRows * M3 / 4;          // 16-B words per window (16 M3 floats)
+    constexpr int kWin = 4;                        // 16-B loads per lane per window (M3 <= 64)
+    uint4 win[kWin];
+    // the block's rows only (offsets stay 32-bit for any P; rows past the end read as zero)
+    const auto wsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in.sh_rest + base), 0,
+                                                        rows * M3 * (int)sizeof(float), 0x00020000);
+    auto load_window = [&](int sub) {
+        const int voff = ((wv * 64 + kSubRows * sub) * M3) * (int)sizeof(float);
+#pragma unroll
+        for (int q = 0; q < kWin; ++q) {
+            const int i = q * 64 + ln;
+            win[q] = make_uint4(0u, 0u, 0u, 0u);
+            if (i < sub_f4) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(wsrc, voff + 16 * i, 0, 0);
+                win[q] = make_uint4(v[0], v[1], v[2], v[3]);
+            }
+        }
+    };
     Params I{};
     if (g < in.P) I = load_params(in, g);
     if (SH == kShChunks && sh) load_chunk(0);
+    if (SH == kShWave && sh) load_window(0);
     Geo G{};
     G.key = 0xFFFFFFFFu;
     if (g < in.P) {
@@ -315,7 +345,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void p
         }
     }
     if (sh) {
-        if (SH == kShChunks) {
+        if (SH == kShWave) {
+            // wave-private window: wave wv's kSubRows x M3 floats
+            float* const wnd = sh_lds + wv * kSubRows * M3;
+            for (int sub = 0; sub < 64 / kSubRows; ++sub) {
+                if (sub > 0) {  // the lanes of the previous window have read it
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                }
+#pragma unroll
+                for (int q = 0; q < kWin; ++q) {
+                    const int i = q * 64 + ln;
+                    if (i < sub_f4) *reinterpret_cast<uint4*>(wnd + 4 * i) = win[q];
+                }
+                if (sub + 1 < 64 / kSubRows) load_window(sub + 1);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (need && (ln >> 4) == sub) {
+                    const float* rest = wnd + (ln & 15) * M3;
+#pragma unroll
+                    for (int ch = 0; ch < 3; ++ch) {
+                        float r = rgb[ch];
+#pragma unroll
+                        for (int k = 1; k < 16; ++k)
+                            if (k < nb) r = r + basis[k] * rest[3 * (k - 1) + ch];
+                        rgb[ch] = r;
+                    }
+                }
+            }
+        } else if (SH == kShChunks) {
 #pragma unroll
             for (int c = 0; c < 3; ++c) {  // k = 1 + 5c .. 5 + 5c; SH degree <= 3 => k < 16
                 const int k0 = 1 + kChunkK * c;
@@ -391,7 +451,10 @@ int launch_preprocess(const gsr_camera& cam, const GaussIn& in, int ty0, int ty1
     const int gx = div_up(cam.width, kTile), gy = div_up(cam.height, kTile);
     const bool sh = in.sh_rest && !in.colors && in.D > 0;
     const dim3 grid(div_up(in.P, 256)), block(256);
-    if (sh)
+    if (sh && GSR_F1_SH_MODE == kShWave && in.M_rest * 3 <= 64 && (reinterpret_cast<uintptr_t>(in.sh_rest) & 15) == 0)
+        hipLaunchKernelGGL(preprocess_kernel<kShWave>, grid, block, sizeof(float) * 4 * kSubRows * in.M_rest * 3, s,
+                           cam, in, gx, gy, ty0, ty1, out);
+    else if (sh)
         hipLaunchKernelGGL(preprocess_kernel<kShChunks>, grid, block, sizeof(float) * 256 * kChunkF, s, cam, in, gx,
                            gy, ty0, ty1, out);
     else
