@@ -207,7 +207,7 @@ struct Views {
     float4* rec;
     uint4* rect;
     uint2* ranges;
-    uint32_t *counters, *K_dev, *ovf, *ovf2, *done, *term, *ck_slot;
+    uint32_t *counters, *K_dev, *ovf, *ovf2, *done, *term;
     float *final_T, *accum;
     float4* ck;  // the checkpoint pool (binning buffer)
     uint32_t *kA, *vA, *kB, *vB, *hist;
@@ -234,7 +234,6 @@ Views views(const gsr_camera* cam, long long n, const gsr_buffers* b) {
     v.ovf2 = at<uint32_t>(b->image, il.ovf2);
     v.done = at<uint32_t>(b->image, il.done);
     v.term = at<uint32_t>(b->image, il.term);
-    v.ck_slot = at<uint32_t>(b->image, il.ck_slot);
     v.final_T = at<float>(b->image, il.final_T);
     v.accum = at<float>(b->image, il.accum);
     if (b->binning) {
@@ -340,8 +339,7 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
                   "per-tile depth order");
     }
     GSR_STAGE(GSR_STAGE_BLEND_FWD, launch_blend_forward(*cam, j.rs->bg, j.ty0, j.ty1, v.ranges, v.sorted_gid, v.rec,
-                                                        j.out_color, v.final_T, v.accum, v.term, v.ck_slot,
-                                                        v.counters + kCkPoolSlot, v.ck, cap, stream),
+                                                        j.out_color, v.final_T, v.accum, v.term, v.ck, cap, stream),
               "blend forward");
     return 0;
 }
@@ -394,8 +392,8 @@ int blend_backward(const gsr_camera* cam, const gsr_raster_settings* rs, const g
     // only the per-entry flag bytes are zeroed: the gather reads the entries B1 flagged
     GSR_STAGE(GSR_STAGE_MISC, launch_clear_flags(partial, cap, stream), "clear partial flags");
     GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.rect, v.rec,
-                                                         v.final_T, v.accum, dL_dpix, partial, cap, v.term, v.ck_slot,
-                                                         v.ck, stream),
+                                                         v.final_T, v.accum, dL_dpix, partial, cap, v.term, v.ck,
+                                                         stream),
               "blend backward");
     GSR_STAGE(GSR_STAGE_GATHER, launch_gather_grad2d(v.offsets, partial, v.rec, cam->width, cam->height, cap, (int)n,
                                                      grad2d, stream),
@@ -794,8 +792,6 @@ const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, 
             if (!bufs->binning) return nullptr;
             return static_cast<const char*>(bufs->binning) +
                    BinLayout(bufs->capacity, (long long)ImgLayout::tile_count(cam->width, cam->height)).ckm;
-        case GSR_VIEW_CK_SLOT: return v.ck_slot;
-        case GSR_VIEW_CK_POOL: return v.counters + kCkPoolSlot;
         default: return nullptr;
     }
 }

@@ -73,8 +73,8 @@ __device__ __forceinline__ void quad_reduce(float (&v)[N]) {
 
 struct BlendGeom {
     int W, H, grid_x, ty0, nwg;
-    uint32_t ck_slots;   // checkpoint pool size (slots); the live bytes follow the float4 slots
-    uint32_t ck_shards;  // its sub-pools (ck_shards of the full image)
+    uint32_t ck_slots;  // checkpoint slots (gsr_internal.h); the live bytes follow the float4 slots
+    int ck_fixed;       // 1: slot = tile * 31 + chunk - 1; 0: from the tile's start in the list
     float bg0, bg1, bg2;
 };
 
@@ -149,19 +149,7 @@ __device__ __forceinline__ float pair_alpha_keep(float e, float L, float& oG, bo
 // 175; 256: 0.473, 141; 384: 0.481, ~115; 512: 0.501, 100; 768: 0.526, 87.  F6's time does not
 // move with its checkpoint writes (0.253-0.259 ms across the range: they overlap the blend),
 // B1's does, so the bound is set for B1.  At 5M / 1080p: 128: 0.488, 256: 0.492, 512: 0.524.
-#ifndef GSR_CHUNK_WORK
-#define GSR_CHUNK_WORK 192
-#endif
-constexpr int kChunkWork = GSR_CHUNK_WORK;
-// checkpoint slots a tile claims up front (gsr_internal.h, checkpoint pool)
-#ifndef GSR_CK_GRANULE
-#define GSR_CK_GRANULE 4
-#endif
-constexpr int kCkGranule = GSR_CK_GRANULE;
-// Band launches (multi-GPU, < 4096 tiles, 4-wave F6): the chunk bound for B1 there
-#ifndef GSR_BAND_CHUNK_WORK
-#define GSR_BAND_CHUNK_WORK GSR_CHUNK_WORK
-#endif
+// (kChunkWork / GSR_CHUNK_WORK and the band launches' GSR_BAND_CHUNK_WORK: gsr_internal.h)
 
 // F6.  T > 0: pixel live; T <= 0: done, |T| = final transmittance (the T after the last
 // contributor -- the reference's final_T).  A pair is blended when the next transmittance
@@ -177,16 +165,13 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
                                                                 float* __restrict__ final_T,
                                                                 float* __restrict__ accum,
                                                                 uint32_t* __restrict__ term,
-                                                                uint32_t* __restrict__ ck_slot,
-                                                                uint32_t* __restrict__ pool_ctr,
                                                                 float4* __restrict__ ck) {
     constexpr int PPL = kPPL / NW;
     constexpr int BATCH = 64 * NW;
-    constexpr int kCW = NW > 2 ? GSR_BAND_CHUNK_WORK : kChunkWork;
+    constexpr int kCW = NW > 2 ? kBandChunkWork : kChunkWork;
     __shared__ float4 srec[BATCH * 3];
     __shared__ uint32_t smk[BATCH];
     __shared__ uint32_t slive[NW];
-    __shared__ uint32_t s_slot0;
     const int tl = xcd_tile(blockIdx.x, geo.nwg);  // band-local tile index
     const int tile = tl + geo.ty0 * geo.grid_x;
     const int tx = tile % geo.grid_x, ty = tile / geo.grid_x;
@@ -210,26 +195,14 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
     // the same chunk decisions, including a wave whose own pixels have all finished (it keeps
     // writing its final state at the later checkpoints).
     uint32_t* const table = term + (size_t)tl * kMaxChunks;  // [term, chunk 1.. starts]
-    uint32_t* const slots = ck_slot + (size_t)tl * kMaxChunks;  // chunk c -> its pool slot
     int nck = 0;   // checkpoints written
     int work = 0;  // pairs in the current chunk
     int tend = n;  // termination index: every pixel of the tile has finished before record tend
-    bool pool_ok = true;     // block-uniform: the pool had room for every claim so far
-    uint32_t next_slot = 0;  // next claimed, unused slot
-    int avail = 0;           // claimed, unused slots left (block-uniform)
-    // Up front, a tile whose list can open chunks claims min(kCkGranule, the most it can open)
-    // slots of its sub-pool: that atomic's latency hides behind the first batch's loads, and
-    // most tiles never claim again (1M / 1080p: ~3.3 opens per tile).
-    const uint32_t shard = (uint32_t)tl % geo.ck_shards, per_shard = geo.ck_slots / geo.ck_shards;
-    int want0 = (4 * n) / kCW;
-    want0 = want0 < kCkGranule ? want0 : kCkGranule;
-    if (want0 > 0 && tid == 0) s_slot0 = atomicAdd(pool_ctr + shard, (uint32_t)want0);
-    bool first_claim = want0 > 0;  // read s_slot0 after the first batch's barrier
     // A stripe with no live pixel (its `live` bit clear: conservative, the bit is cleared only
     // once every T <= 0) is not written; its byte tells B1 to start it dead (T = -1), which is
     // all B1 needs of a finished pixel.
     uint8_t* const ckm = reinterpret_cast<uint8_t*>(ck + (size_t)geo.ck_slots * 256);
-    auto checkpoint = [&](uint32_t slot, uint32_t lv) {
+    auto checkpoint = [&](size_t slot, uint32_t lv) {
         float4* dst = ck + (size_t)slot * 256;
 #pragma unroll
         for (int p = 0; p < PPL; ++p) {
@@ -263,49 +236,13 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
 #pragma unroll
         for (int i = 0; i < NW; ++i) tile_live |= slive[i];
         const int cnt = (n - base) < BATCH ? (n - base) : BATCH;
-        if (first_claim) {  // the barrier above published the up-front claim
-            const uint32_t got = s_slot0;
-            pool_ok = got + (uint32_t)want0 <= per_shard;
-            next_slot = shard * per_shard + got;
-            avail = pool_ok ? want0 : 0;
-            first_claim = false;
-            __syncthreads();  // s_slot0 may be rewritten by a claim below
-        }
-        if (pool_ok) {
-            // the chunks this batch opens, decided ahead by the rule the loop below applies (all
-            // its inputs are in LDS already), so the block claims their pool slots in one atomic
-            int sw = work, sn = nck, opens = 0;
-            for (int c0 = 0; c0 < cnt; c0 += 64) {
-                if (sw >= kCW && sn < kMaxChunks - 1) {
-                    ++opens;
-                    ++sn;
-                    sw = 0;
-                }
-                const uint32_t tm = smk[c0 + lane] & tile_live;
-                sw += __popcll(__ballot(tm & 1u)) + __popcll(__ballot(tm & 2u)) + __popcll(__ballot(tm & 4u)) +
-                      __popcll(__ballot(tm & 8u));
-            }
-            if (opens > avail) {  // block-uniform: claim this batch's opens afresh
-                if (tid == 0) s_slot0 = atomicAdd(pool_ctr + shard, (uint32_t)opens);
-                __syncthreads();
-                const uint32_t got = s_slot0;  // rewritten only after the batch-end barrier
-                pool_ok = got + (uint32_t)opens <= per_shard;
-                next_slot = shard * per_shard + got;
-                avail = pool_ok ? opens : 0;
-            }
-        }
         int visited = 0;
         for (int c0 = 0; c0 < cnt; c0 += 64) {
             const uint32_t sm = smk[c0 + lane];  // 0 past cnt
-            if (work >= kCW && nck < kMaxChunks - 1 && pool_ok) {  // chunk nck + 1 starts at base + c0
-                checkpoint(next_slot, live);
+            if (work >= kCW && nck < kMaxChunks - 1) {  // chunk nck + 1 starts at base + c0
                 ++nck;
-                if (tid == 0) {
-                    table[nck] = (uint32_t)(base + c0);
-                    slots[nck] = next_slot;
-                }
-                ++next_slot;
-                --avail;
+                checkpoint(ck_slot_of(geo.ck_fixed, range.x, tl, nck), live);
+                if (tid == 0) table[nck] = (uint32_t)(base + c0);
                 work = 0;
             }
             const uint32_t tm = sm & tile_live;
@@ -438,7 +375,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                                                             float* __restrict__ p1,
                                                             uint8_t* __restrict__ fl,
                                                             const uint32_t* __restrict__ term,
-                                                            const uint32_t* __restrict__ ck_slot,
                                                             const float4* __restrict__ ck) {
     __shared__ float4 srec[64 * 3];
     __shared__ float qpark[kPark * kParkSlot];  // [slot][quad][9 of 12]
@@ -494,7 +430,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
         T[p] = in ? 1.0f : -1.0f;
     }
     if (chunk > 0) {  // resume from F6's checkpoint: T, and R less dL/dpix . (colour sum so far)
-        const size_t slot = ck_slot[(size_t)tl * kMaxChunks + chunk];
+        const size_t slot = ck_slot_of(geo.ck_fixed, range.x, tl, chunk);
         const float4* src = ck + slot * 256;
         // F6's live-stripe bytes: a stripe it did not write had finished (start it dead)
         const uint32_t on = *reinterpret_cast<const uint32_t*>(
@@ -631,7 +567,7 @@ static BlendGeom make_geo(const gsr_camera& cam, const float bg[3], int ty0, int
     g.nwg = (ty1 - ty0) * g.grid_x;
     const long long full_tiles = (long long)div_up(cam.height, kTile) * g.grid_x;
     g.ck_slots = (uint32_t)ck_pool_slots(cap, full_tiles);  // = BinLayout's
-    g.ck_shards = (uint32_t)ck_shards(full_tiles);
+    g.ck_fixed = ck_fixed_layout(cap, full_tiles) ? 1 : 0;
     g.bg0 = bg[0];
     g.bg1 = bg[1];
     g.bg2 = bg[2];
@@ -640,16 +576,16 @@ static BlendGeom make_geo(const gsr_camera& cam, const float bg[3], int ty0, int
 
 int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
                          const uint2* ranges, const uint32_t* sorted_gid, const float4* rec,
-                         float* out_color, float* final_T, float* accum, uint32_t* term, uint32_t* ck_slot,
-                         uint32_t* pool_ctr, float4* ck, long long cap, hipStream_t s) {
+                         float* out_color, float* final_T, float* accum, uint32_t* term, float4* ck, long long cap,
+                         hipStream_t s) {
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1, cap);
     if (geo.nwg <= 0) return 0;
     if (geo.nwg >= kF6BandTiles)
         hipLaunchKernelGGL(blend_forward_kernel<kF6FullWaves>, dim3(geo.nwg), dim3(64 * kF6FullWaves), 0, s, geo,
-                           ranges, sorted_gid, rec, out_color, final_T, accum, term, ck_slot, pool_ctr, ck);
+                           ranges, sorted_gid, rec, out_color, final_T, accum, term, ck);
     else
         hipLaunchKernelGGL(blend_forward_kernel<kF6BandWaves>, dim3(geo.nwg), dim3(64 * kF6BandWaves), 0, s, geo,
-                           ranges, sorted_gid, rec, out_color, final_T, accum, term, ck_slot, pool_ctr, ck);
+                           ranges, sorted_gid, rec, out_color, final_T, accum, term, ck);
     return (int)hipGetLastError();
 }
 
@@ -657,7 +593,7 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
                           const uint2* ranges, const uint32_t* sorted_gid, const uint4* rect,
                           const float4* rec, const float* final_T,
                           const float* accum, const float* dL_dpix, float* partial, long long cap,
-                          const uint32_t* term, const uint32_t* ck_slot, const float4* ck, hipStream_t s) {
+                          const uint32_t* term, const float4* ck, hipStream_t s) {
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1, cap);
     if (geo.nwg <= 0) return 0;
     const PartLayout pl(cap);
@@ -665,8 +601,7 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
     const int blocks = 8 * (geo.nwg / 8 + 1) * kMaxChunks;
     hipLaunchKernelGGL(blend_backward_kernel, dim3(blocks), dim3(64), 0, s, geo, ranges, sorted_gid, rect, rec,
                        final_T, accum, dL_dpix, reinterpret_cast<float*>(base + pl.p8),
-                       reinterpret_cast<float*>(base + pl.p1), reinterpret_cast<uint8_t*>(base + pl.fl), term, ck_slot,
-                       ck);
+                       reinterpret_cast<float*>(base + pl.p1), reinterpret_cast<uint8_t*>(base + pl.fl), term, ck);
     return (int)hipGetLastError();
 }
 

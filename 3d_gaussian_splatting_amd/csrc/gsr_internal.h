@@ -75,34 +75,39 @@ struct GeomLayout {
 #endif
 constexpr int kMaxChunks = GSR_MAX_CHUNKS;  // = GSR_TERM_STRIDE (gsr.h) in the shipped build
 
-// Checkpoint pool.  A checkpoint (4 KB: float4 (T, C) per pixel of a tile) is taken from a pool
-// of slots that F6 claims batch by batch (one atomic per batch that opens a chunk), instead of
-// a fixed tiles x 31 array (1.0 GB at 1080p, 4.1 GB at 4K, whether or not a chunk opens).  A
-// chunk opens after kChunkWork visited (record, stripe) pairs, so a tile's opens are bounded by
-// its list, and the whole image opens ~K / 240 chunks at 1M / 1080p (27k of the 253k fixed
-// slots): the pool holds 2 per tile plus one per 96 instances of capacity, capped at the fixed
-// array.  It is cut into kCkShards sub-pools (fewer below 64 tiles), tile t drawing from sub-pool t % that with
-// that sub-pool's own counter (one counter for the whole image serialises every block's claim
-// on one L2 word: F6 0.26 -> 0.38 ms).  A tile that finds its sub-pool exhausted opens no more
-// chunks (its last chunk runs longer in B1; results stay exact); GSR_VIEW_CK_POOL reports the
-// slots claimed per sub-pool against its size.
-constexpr int kCkShards = 64;
-// sub-pools of an image of `tiles` tiles (one per tile below kCkShards tiles)
-__host__ __device__ inline int ck_shards(long long tiles) {
-    return tiles < kCkShards ? (tiles > 0 ? (int)tiles : 1) : kCkShards;
+// Checkpoint slots.  A checkpoint is 4 KB (float4 (T, C) per pixel of a tile).  A chunk opens
+// only after kChunkWork visited (record, stripe) pairs and a record has at most 4 stripes, so a
+// tile of n records opens at most floor(n / kCkDiv) chunks (kCkDiv = kChunkWork / 4 = 48).  Tile
+// t's chunk c >= 1 therefore takes slot  floor(start_t / kCkDiv) + t + (c - 1)  (start_t: the
+// tile's first index in the sorted list): the tiles' slot ranges never overlap, no counter or
+// atomic is needed, and the slots in use are bounded by K / kCkDiv + tiles -- instead of a
+// fixed 31 per tile (1.0 GB at 1080p, 4.1 GB at 4K, whether or not a chunk opens).  When that
+// bound is larger than the fixed array anyway (deep lists: > 31 * 48 instances per tile on
+// average, e.g. 5M / 1080p), the fixed layout t * 31 + (c - 1) is used.
+// B1 chunk size in (record, stripe) pairs (measured in gsr_blend.hip), and for band launches
+#ifndef GSR_CHUNK_WORK
+#define GSR_CHUNK_WORK 192
+#endif
+#ifndef GSR_BAND_CHUNK_WORK
+#define GSR_BAND_CHUNK_WORK GSR_CHUNK_WORK
+#endif
+constexpr int kChunkWork = GSR_CHUNK_WORK;
+constexpr int kBandChunkWork = GSR_BAND_CHUNK_WORK;
+constexpr int kCkDiv = (kChunkWork < kBandChunkWork ? kChunkWork : kBandChunkWork) / 4;  // records per possible open
+__host__ __device__ inline bool ck_fixed_layout(long long cap, long long tiles) {
+    return cap / kCkDiv + tiles + 1 >= tiles * (kMaxChunks - 1);
 }
 inline size_t ck_pool_slots(long long cap, long long tiles) {
-    const size_t t = (size_t)(tiles > 0 ? tiles : 1);
-    const size_t full = t * (kMaxChunks - 1);
-    const size_t want = 2 * t + (size_t)(cap > 0 ? cap : 0) / 96;
-    const size_t n = want < full ? want : full;
-    const size_t ns = (size_t)ck_shards(tiles);
-    return (n + ns - 1) / ns * ns;  // whole sub-pools
+    const long long t = tiles > 0 ? tiles : 1, c = cap > 0 ? cap : 0;
+    return (size_t)(ck_fixed_layout(c, t) ? t * (kMaxChunks - 1) : c / kCkDiv + t + 1);
+}
+__host__ __device__ inline size_t ck_slot_of(bool fixed, uint32_t start, int tile, int chunk) {
+    return fixed ? (size_t)tile * (kMaxChunks - 1) + (chunk - 1) : (size_t)(start / kCkDiv) + tile + (chunk - 1);
 }
 
-// Binning for up to `cap` instances (the exact K, or a caller-given bound) of a launch over
+// Binning for up to `cap` instances (the exact K, or a caller-given bound) of an image of
 // `tiles` tiles.  The tile-key sort ping-pongs (kA, vA) <-> (kB, vB); F3 emits into (kA, vA).
-// Then the checkpoint pool: ck_slots x 256 float4, and one live byte per (slot, 16x4 stripe).
+// Then the checkpoint slots: ck_slots x 256 float4, and one live byte per (slot, 16x4 stripe).
 struct BinLayout {
     size_t kA, vA, kB, vB, hist, ck, ckm, total, ck_slots;
     BinLayout(long long cap, long long tiles) {
@@ -121,7 +126,7 @@ struct BinLayout {
 };
 
 struct ImgLayout {
-    size_t ranges, counters, done, ovf, ovf2, term, ck_slot, final_T, accum, total;
+    size_t ranges, counters, done, ovf, ovf2, term, final_T, accum, total;
     static size_t tile_count(int W, int H) {
         const size_t t = (size_t)div_up(W, kTile) * div_up(H, kTile);
         return t ? t : 1;
@@ -132,12 +137,11 @@ struct ImgLayout {
         const size_t tiles = tile_count(W, H);
         size_t pix = (size_t)W * H;
         ranges = take(8 * tiles);
-        counters = take(4 * (2 * kCountSlots + 16 + kCkShards));  // ranges, counters and done are contiguous:
+        counters = take(4 * (2 * kCountSlots + 16));  // ranges, counters and done are contiguous:
         done = take(4 * tiles);  // one memset clears them (done: chunks sorted per queued tile)
         ovf = take(4 * tiles);   // tiles the per-tile depth sort hands to its larger
         ovf2 = take(4 * tiles);  // forms (queues: the 8192-entry form, then the 16384-entry / chunked one)
         term = take(4 * tiles * kMaxChunks);  // F6: per tile [termination index, chunk 1..kMaxChunks-1 starts]
-        ck_slot = take(4 * tiles * kMaxChunks);  // F6: per tile and chunk c >= 1, its checkpoint pool slot
         final_T = take(4 * (pix ? pix : 1));
         accum = take(12 * (pix ? pix : 1));  // colour sum without background, 3 x H x W
         total = o;
@@ -196,7 +200,6 @@ struct ShardLayout {
 constexpr int kTotalSlot = 2 * kCountSlots;          // K = sum of tiles_touched, written by the scan
 constexpr int kOvfCountSlot = 2 * kCountSlots + 8;   // tiles queued for the large per-tile depth sort
 constexpr int kOvf2CountSlot = 2 * kCountSlots + 9;  // ... then for its 16384-entry / chunked form
-constexpr int kCkPoolSlot = 2 * kCountSlots + 16;    // [kCkShards]: checkpoint slots F6 claimed per sub-pool
 
 // number of 8-bit LSD passes to sort tile ids of a grid with `tiles` tiles
 inline int tile_bits(int tiles) {

@@ -65,13 +65,12 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
 int launch_finalize(const uint32_t* sorted_tile, long long cap, const uint32_t* K_dev, uint2* ranges, hipStream_t s);
 
 // F6: per-tile front-to-back blend -> colour, final T, colour sum without background, the
-// tile's termination index term[], the B1 chunk checkpoints (ck: the binning's pool of
-// ck_pool_slots(cap, tiles of the launch) slots, claimed through *pool_ctr (zeroed), each
-// chunk's slot in ck_slot[tile * kMaxChunks + chunk])
+// tile's termination index term[], the B1 chunk checkpoints (ck: the binning buffer's
+// ck_pool_slots(cap, tiles of the image) slots, chunk slot ck_slot_of(...), gsr_internal.h)
 int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
                          const uint2* ranges, const uint32_t* sorted_gid, const float4* rec,
-                         float* out_color, float* final_T, float* accum, uint32_t* term, uint32_t* ck_slot,
-                         uint32_t* pool_ctr, float4* ck, long long cap, hipStream_t s);
+                         float* out_color, float* final_T, float* accum, uint32_t* term, float4* ck, long long cap,
+                         hipStream_t s);
 
 // F6 writes term[t] (see kMaxChunks) and the B1 chunk checkpoints `ck` (ImgLayout.ck).
 // B1: per-tile front-to-back gradients -> per-instance partial entry j (PartLayout(cap)), where
@@ -84,7 +83,7 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
                           const uint2* ranges, const uint32_t* sorted_gid, const uint4* rect,
                           const float4* rec, const float* final_T,
                           const float* accum, const float* dL_dpix, float* partial, long long cap,
-                          const uint32_t* term, const uint32_t* ck_slot, const float4* ck, hipStream_t s);
+                          const uint32_t* term, const float4* ck, hipStream_t s);
 
 // record layout constants shared by preprocess and the blend kernels
 constexpr float kLn2 = 0.6931471805599453f;  // conic A = -2 ln2 a', B = -ln2 b', C = -2 ln2 c' 

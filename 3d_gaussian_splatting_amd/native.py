@@ -28,9 +28,14 @@ GSR_SPLAT_BYTES = 64
 GSR_SPLAT_GRAD_BYTES = 48
 MAX_BANDS = 16
 VIEW_SORTED_GID, VIEW_SORTED_TILE, VIEW_RANGES, VIEW_FINAL_T, VIEW_N_CONTRIB, VIEW_DEPTH_KEY, \
-    VIEW_TILES_TOUCHED, VIEW_RECORDS, VIEW_COUNTS, VIEW_TERM, VIEW_CK_LIVE, VIEW_CK_SLOT, VIEW_CK_POOL = range(1, 14)
+    VIEW_TILES_TOUCHED, VIEW_RECORDS, VIEW_COUNTS, VIEW_TERM, VIEW_CK_LIVE = range(1, 12)
 TERM_STRIDE = 32  # GSR_TERM_STRIDE: words per tile of VIEW_TERM
-CK_SHARDS = 64    # GSR_CK_SHARDS: checkpoint sub-pools (VIEW_CK_POOL)
+CK_DIV = 48       # a tile of n instances opens at most n // CK_DIV B1 chunks (gsr.h, VIEW_CK_LIVE)
+
+
+def ck_slot(fixed: bool, start: int, tile: int, chunk: int) -> int:
+    """B1 checkpoint slot of a tile's chunk >= 1 (gsr.h GSR_VIEW_CK_LIVE)."""
+    return tile * (TERM_STRIDE - 1) + chunk - 1 if fixed else start // CK_DIV + tile + chunk - 1
 EXPORTS = ["gsr_abi_version", "gsr_last_error", "gsr_forward", "gsr_read_num_rendered", "gsr_forward_batch",
            "gsr_backward", "gsr_backward_blend", "gsr_backward_preprocess", "gsr_shard_forward",
            "gsr_band_forward", "gsr_band_backward", "gsr_shard_backward", "gsr_exchange_block_bytes",

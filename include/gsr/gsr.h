@@ -233,19 +233,13 @@ int gsr_shard_backward(const gsr_camera* cam, const gsr_gaussians* shard, const 
                                        termination index, then the B1 chunk 1..31 start
                                        records (UINT32_MAX: no such chunk)                 */
 #define GSR_TERM_STRIDE 32          /* words per tile of GSR_VIEW_TERM                     */
-#define GSR_VIEW_CK_LIVE 11         /* uint8[slots*4]: per checkpoint-pool slot and 16x4
+#define GSR_VIEW_CK_LIVE 11         /* uint8[slots*4]: per B1 checkpoint slot and 16x4
                                        pixel stripe, 1 where F6 wrote that stripe's
-                                       checkpoint (0: it had finished); only the slots F6
-                                       claimed are defined (GSR_VIEW_CK_SLOT / _CK_POOL)    */
-#define GSR_VIEW_CK_SLOT 12         /* uint32[tiles*GSR_TERM_STRIDE]: per tile, the pool
-                                       slot of chunk c in word c (c >= 1; defined where
-                                       GSR_VIEW_TERM says the chunk opened)                 */
-#define GSR_VIEW_CK_POOL 13         /* uint32[S]: checkpoint-pool slots F6 claimed per
-                                       sub-pool, S = min(GSR_CK_SHARDS, tiles) (tile t draws
-                                       from sub-pool t % S, which holds
-                                       gsr_ck_pool_slots(...) / S slots; a count above that
-                                       means it ran out and its tiles opened fewer chunks) */
-#define GSR_CK_SHARDS 64
+                                       checkpoint (0: it had finished).  Tile t's chunk
+                                       c >= 1 (opened per GSR_VIEW_TERM) uses slot
+                                       t*31 + c-1 when gsr_ck_pool_slots(cap, W, H) ==
+                                       31*tiles, else floor(start_t / 48) + t + c-1, start_t
+                                       = the tile's first index in the sorted list          */
 #define GSR_VIEW_RECORDS 8          /* float4[3*P]: {x,y,a',b'},{c',o,r,g},{b,ext_x,ext_y,log2 o};
                                        a',b',c' = -log2(e) * (A/2, B, C/2) of the conic */
 const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, int what);
@@ -272,8 +266,10 @@ int gsr_profile_read(double* ms, uint32_t* counts);
 const char* gsr_stage_name(int stage);
 
 /* Byte sizes the allocation callbacks will be asked for (for pre-sizing pools).  The binning
- * buffer holds the instance arrays for `capacity` instances and the B1 checkpoint pool (ABI 3:
- * sized by capacity and image, no longer a fixed 31 checkpoints per tile in the image buffer). */
+ * buffer holds the instance arrays for `capacity` instances and the B1 checkpoint slots (ABI 3:
+ * min(31 per tile, capacity / 48 + tiles + 1) slots of 4 KB -- a chunk opens only after 192
+ * visited (record, stripe) pairs, so a tile of n instances opens at most n / 48 -- instead of a
+ * fixed 31 per tile in the image buffer). */
 size_t gsr_geom_bytes(int32_t P);
 size_t gsr_binning_bytes(int32_t capacity, int32_t width, int32_t height);
 size_t gsr_ck_pool_slots(int32_t capacity, int32_t width, int32_t height);

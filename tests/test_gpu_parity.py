@@ -502,17 +502,14 @@ def test_chunk_checkpoints_with_finished_stripes(W, H, P_back, rast, oracle):
     tiles = cam.grid[0] * cam.grid[1]
     S = native.TERM_STRIDE
     term = _np(st.view(native.VIEW_TERM, torch.int32, tiles * S)).view(np.uint32).reshape(tiles, S)
-    slot = _np(st.view(native.VIEW_CK_SLOT, torch.int32, tiles * S)).view(np.uint32).reshape(tiles, S)
     pool = int(native.load_hip().gsr_ck_pool_slots(st.buffers.capacity, W, H))
-    ns = min(native.CK_SHARDS, tiles)
-    used = _np(st.view(native.VIEW_CK_POOL, torch.int32, ns))
     live = _np(st.view(native.VIEW_CK_LIVE, torch.uint8, pool * 4)).reshape(pool, 4)
+    rng = _np(st.view(native.VIEW_RANGES, torch.int32, 2 * tiles)).view(np.uint32).reshape(tiles, 2)
     opened = term[:, 1:] != 0xFFFFFFFF
     assert opened.sum() > tiles  # more than one chunk per tile on average
-    # every opened chunk holds its own claimed slot (a tile claims a few slots up front, so some
-    # claimed slots stay unused), and no sub-pool ran out
-    assert used.sum() >= opened.sum() and used.max() <= pool // ns
-    ids = slot[:, 1:][opened]
+    fixed = pool == tiles * (S - 1)
+    ids = np.array([native.ck_slot(fixed, int(rng[t, 0]), t, c + 1) for t, c in zip(*np.nonzero(opened))])
+    # each opened chunk has its own slot: the start-indexed slot ranges of the tiles never overlap
     assert len(np.unique(ids)) == len(ids) and ids.max() < pool
     on = live[ids]
     assert set(np.unique(on)) <= {0, 1}
@@ -527,29 +524,35 @@ def test_chunk_checkpoints_with_finished_stripes(W, H, P_back, rast, oracle):
     assert max(v[0] for v in worst.values()) <= 2e-3, worst
 
 
-def test_checkpoint_pool_exhaustion_stays_exact(rast, oracle):
-    """The B1 checkpoint pool (2 slots per tile + 1 per 96 instances) can run out for a scene whose
-    every tile holds ~1000 faint, wide records that never terminate: each tile would open ~20
-    chunks (one per 48 records x 4 live stripes) against 2 + 1000 / 96 slots.  Tiles that find it
-    exhausted open no more chunks, and the image and every gradient still match the oracle (the
-    chunks only split B1's work)."""
+@pytest.mark.parametrize("P", [1000, 2000])
+def test_checkpoint_slots_deep_lists(P, rast, oracle):
+    """Tiles whose ~P faint, wide records never terminate open chunks up to the slot bound
+    (n / 48 per tile): P = 1000 runs the start-indexed slots near their bound (~20 chunks per
+    tile), P = 2000 (> 31 * 48 per tile) the fixed 31-per-tile layout.  Every opened chunk has
+    its own slot, and the image and every gradient match the oracle."""
     gr, sc = pkg("graphics"), pkg("scene")
     native = pkg("native")
     cam = gr.synthetic_camera(64, 64)
-    s = sc.make_scene(cam, 1000, max_sh_degree=1, seed=71)
-    P = s.P
+    s = sc.make_scene(cam, P, max_sh_degree=1, seed=71)
     rng = np.random.default_rng(71)
     z = np.linspace(4.0, 8.0, P)
     xy = rng.uniform(-0.4, 0.4, (P, 2)) * z[:, None] * np.array([cam.tanfovx, cam.tanfovy])
     s.means3D = np.concatenate([xy, z[:, None]], 1).astype(np.float32)
     s.scales = np.full((P, 3), 6.0, np.float32)  # sigma 40-80 px: every stripe of every tile
-    s.opacities = np.full((P, 1), 0.006, np.float32)  # alpha <= 0.006: T > 0.994^1000 > 1e-4
+    s.opacities = np.full((P, 1), 0.006 if P == 1000 else 0.004, np.float32)  # T stays > 1e-4
     args = (cam, s.means3D, s.opacities, s.scales, s.rotations, s.sh_dc, s.sh_rest)
     st = rast.forward(*args, sh_degree=1)
     f = oracle.forward(*args, sh_degree=1)
+    tiles, S = cam.grid[0] * cam.grid[1], native.TERM_STRIDE
     pool = int(native.load_hip().gsr_ck_pool_slots(st.buffers.capacity, cam.width, cam.height))
-    tiles = cam.grid[0] * cam.grid[1]
-    ns = min(native.CK_SHARDS, tiles)
-    used = _np(st.view(native.VIEW_CK_POOL, torch.int32, ns))
-    assert used.max() > pool // ns, (used, pool)  # a sub-pool ran out: the fallback ran
+    fixed = pool == tiles * (S - 1)
+    assert fixed == (P == 2000)
+    term = _np(st.view(native.VIEW_TERM, torch.int32, tiles * S)).view(np.uint32).reshape(tiles, S)
+    rng_t = _np(st.view(native.VIEW_RANGES, torch.int32, 2 * tiles)).view(np.uint32).reshape(tiles, 2)
+    opened = term[:, 1:] != 0xFFFFFFFF
+    assert opened.sum(1).mean() > 15  # deep lists: many chunks per tile
+    n = rng_t[:, 1] - rng_t[:, 0]
+    assert np.all(opened.sum(1) <= np.minimum(S - 1, n // native.CK_DIV))  # the slot bound holds
+    ids = np.array([native.ck_slot(fixed, int(rng_t[t, 0]), t, c + 1) for t, c in zip(*np.nonzero(opened))])
+    assert len(np.unique(ids)) == len(ids) and ids.max() < pool
     _compare(st, f, sc.make_dL_dpix(cam, seed=72), rast)
