@@ -74,7 +74,7 @@ def orbit_cameras(n_views: int, width: int, height: int, radius: float = 4.0, se
     return cams
 
 
-def procedural_cloud(n: int, seed: int = 0, texture: float = 0.25):
+def procedural_cloud(n: int, seed: int = 0, texture: float = 0.25, gt_scale: float = 0.012):
     """Ground-truth Gaussians: 60 % a textured ground disc (radius 3, y = 0.6), 40 % in five
     ellipsoidal blobs above it.  Returns raw leaves (means, f_dc, f_rest (SH1), opacity logits,
     log scales, quaternions) as numpy arrays."""
@@ -101,7 +101,7 @@ def procedural_cloud(n: int, seed: int = 0, texture: float = 0.25):
     base = base + texture * normal(seed, 27, 3 * n).reshape(n, 3)
     f_dc = ((np.clip(base, 0.02, 0.98) - 0.5) / 0.28209479177387814)[:, None, :]
     f_rest = 0.05 * normal(seed, 23, 9 * n).reshape(n, 3, 3)
-    log_s = np.log(0.012) + 0.4 * normal(seed, 24, 3 * n).reshape(n, 3)
+    log_s = np.log(gt_scale) + 0.4 * normal(seed, 24, 3 * n).reshape(n, 3)
     log_s[:n_ground, 1] = np.log(0.002)  # flat ground splats
     q = normal(seed, 25, 4 * n).reshape(n, 4)
     q[:n_ground] = [1.0, 0.0, 0.0, 0.0]
@@ -111,10 +111,10 @@ def procedural_cloud(n: int, seed: int = 0, texture: float = 0.25):
 
 
 def synthetic_scene(n_gt: int, n_init: int, n_views: int, width: int, height: int, seed: int = 0,
-                    device="cuda", texture: float = 0.25) -> LoopScene:
+                    device="cuda", texture: float = 0.25, gt_scale: float = 0.012) -> LoopScene:
     """Ground truth rendered once per view (the rasterizer's forward, no gradients), and a
     sparse noisy initial point cloud."""
-    means, f_dc, f_rest, opac, log_s, q, rgb = procedural_cloud(n_gt, seed, texture)
+    means, f_dc, f_rest, opac, log_s, q, rgb = procedural_cloud(n_gt, seed, texture, gt_scale)
     cams = orbit_cameras(n_views, width, height, seed=seed)
     dev = torch.device(device)
     t = lambda a: torch.as_tensor(a, device=dev)

@@ -151,6 +151,7 @@ def main():
     ap.add_argument("--loop-size", default="1280x832", help="--mode loop: image size WxH")
     ap.add_argument("--loop-views", type=int, default=128, help="--mode loop: training cameras")
     ap.add_argument("--loop-texture", type=float, default=1.0, help="--mode loop: ground-truth colour noise")
+    ap.add_argument("--loop-gt-scale", type=float, default=0.012, help="--mode loop: ground-truth splat size")
     ap.add_argument("--loop-engine", default="cpp", choices=("cpp", "python"),
                     help="--mode loop: the C++ loop executable (lib/gsr_train_loop over gsr::Trainer, the "
                          "train.cpp drop-in) or the Python mirror (train_loop.train)")
@@ -516,7 +517,7 @@ def loop_main(args):
     W, H = (int(v) for v in args.loop_size.split("x"))
     t0 = time.perf_counter()
     scene = L.synthetic_scene(args.loop_gt, args.loop_init, args.loop_views, W, H, seed=0, device=dev,
-                              texture=args.loop_texture)
+                              texture=args.loop_texture, gt_scale=args.loop_gt_scale)
     setup_s = time.perf_counter() - t0
     opt = T.OptimizationParams(iterations=args.iters)
     if args.loop_engine == "cpp":
@@ -529,7 +530,8 @@ def loop_main(args):
         "ms_per_step": round(1e3 * res.seconds / res.iterations, 4), "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": f"configs[4]: {args.iters} iterations, {args.loop_views} views {W}x{H}, ground truth "
-                               f"{args.loop_gt} Gaussians (texture {args.loop_texture}), init {args.loop_init} points, "
+                               f"{args.loop_gt} Gaussians (texture {args.loop_texture}, scale {args.loop_gt_scale}), init "
+                               f"{args.loop_init} points, "
                                f"SH 3", "width": W, "height": H, "views": args.loop_views,
                    "engine": ("C++ loop tests/cpp/train_main.cpp over gsr::Trainer" if args.loop_engine == "cpp"
                               else "Python train_loop.train over trainer.GaussianTrainer")},
