@@ -142,23 +142,23 @@ class _CountRing:
 
     def __init__(self, nb: int, device, ring: int = 4):
         pin = torch.cuda.is_available() and torch.device(device).type == "cuda"
-        self.slots = [torch.zeros(nb + 1, dtype=torch.int64, pin_memory=pin) for _ in range(ring)]
+        self.slots = [torch.zeros(nb + 1, dtype=torch.int32, pin_memory=pin) for _ in range(ring)]
         self.pending: list = []  # (step, slot, event or None, pair_cap, capacity)
         self.next = 0
 
     def push(self, step: int, counts: torch.Tensor, band_k: torch.Tensor, pair_cap: int, capacity: int):
+        """counts: (nb,) int32 device view of the send headers; band_k: (1,) int32 device."""
         if len(self.pending) == len(self.slots):
             self.wait_oldest()
         slot = self.slots[self.next]
         self.next = (self.next + 1) % len(self.slots)
-        vals = torch.cat([counts.to(torch.int64).reshape(-1), band_k.to(torch.int64).reshape(-1)])
+        nb = slot.numel() - 1
         ev = None
-        if vals.is_cuda:
-            slot.copy_(vals, non_blocking=True)
+        slot[:nb].copy_(counts.reshape(-1), non_blocking=True)  # two small D2H copies, no kernel
+        slot[nb:].copy_(band_k.reshape(-1), non_blocking=True)
+        if counts.is_cuda:
             ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(vals.device))
-        else:
-            slot.copy_(vals)
+            ev.record(torch.cuda.current_stream(counts.device))
         self.pending.append((step, slot, ev, pair_cap, capacity))
 
     def wait_oldest(self):
@@ -173,7 +173,7 @@ class _CountRing:
             step, slot, ev, pair_cap, capacity = self.pending.pop(0)
             if ev is not None:
                 ev.synchronize()
-            v = slot.tolist()
+            v = [int(x) & 0xFFFFFFFF for x in slot.tolist()]  # u32 counts
             counts, band_k = v[:-1], v[-1]
             if max(counts) > pair_cap or band_k > capacity:
                 self.pending.clear()
@@ -215,10 +215,12 @@ class ShardStep:
         self.capacity = 0
         self.steps = 0
         self._ring = _CountRing(self.world, self.shard["means3D"].device)
+        # buffers kept across steps (one stream: a step's kernels run after the previous step's)
+        self._reuse = {"shard": {}, "band": {}, "grads": {}}
 
     def _shard_forward(self, pair_cap, row_hist=None):
         return self.rast.shard_forward(self.cam, self.rows, pair_cap, **self.shard, sh_degree=self.D,
-                                       row_hist=row_hist)
+                                       row_hist=row_hist, reuse=self._reuse["shard"] if pair_cap else None)
 
     def plan(self):
         """Probe (synchronous, setup only): balanced band cuts, then the pair capacity and the
@@ -250,7 +252,8 @@ class ShardStep:
     def forward(self):
         sh = self._shard_forward(self.pair_cap)
         recv = all_to_all_blocks(sh.send, self.world, self.dist, self.group)
-        st = self.rast.band_forward(self.cam, self.band, self.world, self.pair_cap, recv, self.capacity)
+        st = self.rast.band_forward(self.cam, self.band, self.world, self.pair_cap, recv, self.capacity,
+                                    reuse=self._reuse["band"])
         self._ring.push(self.steps, sh.counts, st.k_device(), self.pair_cap, self.capacity)
         return sh, st
 
@@ -260,13 +263,15 @@ class ShardStep:
 
     def step(self, dL_dpix: torch.Tensor):
         """-> (full image, this shard's leaf gradients, shard state, band state).  Raises
-        ShardOverflowError for an earlier step found to have overflowed (see the class doc)."""
+        ShardOverflowError for an earlier step found to have overflowed (see the class doc).
+        The returned gradients and states live in buffers the next step reuses: consume them
+        (e.g. the optimizer step) before calling step() again."""
         self._ring.poll()
         sh, st = self.forward()
         img = ImageGather(st.color, self.rows, self.rank, self.dist, self.group)  # overlaps B1
-        g2 = self.rast.band_backward(st, self.world, self.pair_cap, dL_dpix)
+        g2 = self.rast.band_backward(st, self.world, self.pair_cap, dL_dpix, reuse=self._reuse["band"])
         back = all_to_all_blocks(g2, self.world, self.dist, self.group)
-        grads = self.rast.shard_backward(sh, back)
+        grads = self.rast.shard_backward(sh, back, reuse=self._reuse["grads"])
         self.steps += 1
         out = img.wait(), grads, sh, st
         if self.strict:

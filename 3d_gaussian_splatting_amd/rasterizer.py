@@ -36,15 +36,29 @@ def _f32(t, shape=None, device=None):
 
 
 class _Allocator:
-    """Allocation callbacks for the C ABI: uint8 tensors kept alive by the owner."""
+    """Allocation callbacks for the C ABI: uint8 tensors kept alive by the owner.  With `reuse`
+    (a list kept by the caller across calls), the i-th request of a call gets the i-th tensor
+    of the previous call when it is large enough -- a step loop then allocates nothing (the
+    previous step's buffers are dead by the time the next step's kernels run: one stream)."""
 
-    def __init__(self, device):
+    def __init__(self, device, reuse: list | None = None):
         self.device = device
         self.tensors = []
+        self.reuse = reuse
         self.cb = native.ALLOC_FN(self._alloc)
 
     def _alloc(self, _ctx, nbytes):
-        t = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=self.device)
+        n = max(int(nbytes), 16)
+        i = len(self.tensors)
+        if self.reuse is not None and i < len(self.reuse) and self.reuse[i].numel() >= n:
+            t = self.reuse[i]
+        else:
+            t = torch.empty(n, dtype=torch.uint8, device=self.device)
+            if self.reuse is not None:
+                if i < len(self.reuse):
+                    self.reuse[i] = t
+                else:
+                    self.reuse.append(t)
         self.tensors.append(t)
         return t.data_ptr()
 
@@ -113,6 +127,17 @@ class CAbiRasterizer:
     def __init__(self, device="cuda"):
         self.device = torch.device(device)
         self.L = native.load_hip()
+        self._cams = {}  # id(cam) -> (cam, gsr_camera struct): built once per camera object
+
+    def _cam(self, cam):
+        hit = self._cams.get(id(cam))
+        if hit is not None and hit[0] is cam:
+            return hit[1]
+        c = native.camera_struct(cam)
+        if len(self._cams) > 256:
+            self._cams.clear()
+        self._cams[id(cam)] = (cam, c)
+        return c
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
@@ -164,7 +189,7 @@ class CAbiRasterizer:
         radii = torch.empty((P,), dtype=torch.int32, device=dev)
         ag, ab, ai = _Allocator(dev), _Allocator(dev), _Allocator(dev)
         bufs = native.Buffers()
-        c = native.camera_struct(cam)
+        c = self._cam(cam)
         rc = self.L.gsr_forward(ctypes.byref(c), ctypes.byref(g), ctypes.byref(s), _ptr(color),
                                 _ptr(radii) if P else None, ag.cb, ab.cb, ai.cb, None, ctypes.byref(bufs),
                                 self._stream())
@@ -227,7 +252,7 @@ class CAbiRasterizer:
         dpix = _f32(dL_dpix, (3, st.cam.height, st.cam.width), self.device)
         out, gg = self._grad_tensors(st)
         scratch = _Allocator(self.device)
-        c = native.camera_struct(st.cam)
+        c = self._cam(st.cam)
         rc = self.L.gsr_backward(ctypes.byref(c), ctypes.byref(st.gauss), ctypes.byref(st.settings),
                                  ctypes.byref(st.buffers), _ptr(dpix), scratch.cb, None, ctypes.byref(gg),
                                  self._stream())
@@ -246,7 +271,7 @@ class CAbiRasterizer:
                 raise ValueError("backward_blend: out must be a contiguous f32 (>= P) x 12 tensor")
             grad2d = out
         scratch = _Allocator(self.device)
-        c = native.camera_struct(st.cam)
+        c = self._cam(st.cam)
         rc = self.L.gsr_backward_blend(ctypes.byref(c), ctypes.byref(st.gauss), ctypes.byref(st.settings),
                                        ctypes.byref(st.buffers), _ptr(dpix), scratch.cb, None, _ptr(grad2d),
                                        self._stream())
@@ -256,7 +281,7 @@ class CAbiRasterizer:
     def backward_preprocess(self, st: ForwardState, grad2d: torch.Tensor) -> dict:
         out, gg = self._grad_tensors(st)
         grad2d = grad2d.contiguous()
-        c = native.camera_struct(st.cam)
+        c = self._cam(st.cam)
         rc = self.L.gsr_backward_preprocess(ctypes.byref(c), ctypes.byref(st.gauss), ctypes.byref(st.settings),
                                             ctypes.byref(st.buffers), _ptr(grad2d), ctypes.byref(gg),
                                             self._stream())
@@ -285,7 +310,7 @@ class ShardState:
         """Splats packed per band (device u32 headers; > pair_cap = overflow)."""
         nb = len(self.band_rows) - 1
         blk = self.send.numel() // nb
-        return self.send.view(nb, blk)[:, :4].contiguous().view(torch.int32)[:, 0]
+        return self.send.view(nb, blk).view(torch.int32)[:, 0]  # strided view of the headers
 
 
 class ShardRasterizer(CAbiRasterizer):
@@ -297,17 +322,37 @@ class ShardRasterizer(CAbiRasterizer):
     def shard_forward(self, cam: RasterCamera, band_rows, pair_cap: int, means3D, opacities, scales=None,
                       rotations=None, sh_dc=None, sh_rest=None, sh_degree=0, colors_precomp=None,
                       cov3D_precomp=None, scale_modifier=1.0, row_hist: torch.Tensor | None = None,
-                      debug=False) -> ShardState:
+                      debug=False, reuse: dict | None = None) -> ShardState:
+        """`reuse` (a dict the caller keeps across steps): the send / state / radii buffers and the
+        prepared input structs of the previous call with the same sizes are used again."""
         dev = self.device
-        inputs, g, s = self._prepare(means3D, opacities, scales, rotations, sh_dc, sh_rest, sh_degree,
-                                     colors_precomp, cov3D_precomp, scale_modifier, (0.0, 0.0, 0.0), None, 0, debug)
+        srcs = (means3D, opacities, scales, rotations, sh_dc, sh_rest, colors_precomp, cov3D_precomp)
+        key = None
+        if all(t is None or (torch.is_tensor(t) and t.is_contiguous() and t.dtype == torch.float32
+                             and t.device == dev) for t in srcs):
+            key = tuple(None if t is None else (t.data_ptr(), tuple(t.shape)) for t in srcs) + \
+                (int(sh_degree), float(scale_modifier), bool(debug))
+        if reuse is not None and key is not None and reuse.get("key") == key:
+            inputs, g, s = reuse["prep"]
+        else:
+            inputs, g, s = self._prepare(means3D, opacities, scales, rotations, sh_dc, sh_rest, sh_degree,
+                                         colors_precomp, cov3D_precomp, scale_modifier, (0.0, 0.0, 0.0), None, 0,
+                                         debug)
+            if reuse is not None:
+                reuse["key"], reuse["prep"] = key, (inputs, g, s)
         nb = len(band_rows) - 1
         rows = (ctypes.c_int32 * (nb + 1))(*[int(r) for r in band_rows])
-        send = torch.empty(nb * self.block_bytes(pair_cap), dtype=torch.uint8, device=dev)
-        state = torch.empty(int(self.L.gsr_shard_state_bytes(g.P, nb, int(pair_cap))), dtype=torch.uint8,
-                            device=dev)
-        radii = torch.empty((g.P,), dtype=torch.int32, device=dev)
-        c = native.camera_struct(cam)
+        nsend = nb * self.block_bytes(pair_cap)
+        nstate = int(self.L.gsr_shard_state_bytes(g.P, nb, int(pair_cap)))
+        if reuse is not None and reuse.get("sizes") == (nsend, nstate, g.P):
+            send, state, radii = reuse["bufs"]
+        else:
+            send = torch.empty(nsend, dtype=torch.uint8, device=dev)
+            state = torch.empty(nstate, dtype=torch.uint8, device=dev)
+            radii = torch.empty((g.P,), dtype=torch.int32, device=dev)
+            if reuse is not None:
+                reuse["sizes"], reuse["bufs"] = (nsend, nstate, g.P), (send, state, radii)
+        c = self._cam(cam)
         rc = self.L.gsr_shard_forward(ctypes.byref(c), ctypes.byref(g), ctypes.byref(s), nb, rows, int(pair_cap),
                                       _ptr(send), _ptr(radii) if g.P else None, _ptr(state), _ptr(row_hist),
                                       self._stream())
@@ -317,20 +362,27 @@ class ShardRasterizer(CAbiRasterizer):
 
     def band_forward(self, cam: RasterCamera, tile_rows, nsrc: int, pair_cap: int, recv: torch.Tensor,
                      max_rendered: int, out_color: torch.Tensor | None = None, bg=(0.0, 0.0, 0.0),
-                     debug=False) -> ForwardState:
+                     debug=False, reuse: dict | None = None) -> ForwardState:
         """F2..F6 over the splats received from nsrc shards; only the band's pixels of
-        out_color are written."""
+        out_color are written.  `reuse`: the caller's dict of buffers kept across steps."""
         dev = self.device
         s = native.Settings()
         s.bg[:] = [float(v) for v in bg]
         s.tile_y0, s.tile_y1 = int(tile_rows[0]), int(tile_rows[1])
         s.flags = native.GSR_FLAG_DEBUG if debug else 0
         s.max_rendered = int(max_rendered)
-        color = out_color if out_color is not None else torch.zeros((3, cam.height, cam.width),
-                                                                     dtype=torch.float32, device=dev)
-        ag, ab, ai = _Allocator(dev), _Allocator(dev), _Allocator(dev)
+        if out_color is not None:
+            color = out_color
+        elif reuse is not None and "color" in reuse and tuple(reuse["color"].shape) == (3, cam.height, cam.width):
+            color = reuse["color"]  # the band's pixels are rewritten; the rest stay as they were
+        else:
+            color = torch.zeros((3, cam.height, cam.width), dtype=torch.float32, device=dev)
+            if reuse is not None:
+                reuse["color"] = color
+        r = (lambda k: reuse.setdefault(k, [])) if reuse is not None else (lambda k: None)
+        ag, ab, ai = _Allocator(dev, r("geom")), _Allocator(dev, r("bin")), _Allocator(dev, r("img"))
         bufs = native.Buffers()
-        c = native.camera_struct(cam)
+        c = self._cam(cam)
         rc = self.L.gsr_band_forward(ctypes.byref(c), ctypes.byref(s), int(nsrc), int(pair_cap), _ptr(recv),
                                      _ptr(color), ag.cb, ab.cb, ai.cb, None, ctypes.byref(bufs), self._stream())
         self._check(rc, "gsr_band_forward")
@@ -339,27 +391,37 @@ class ShardRasterizer(CAbiRasterizer):
         return ForwardState(cam=cam, inputs={"recv": recv}, settings=s, gauss=g, buffers=bufs, color=color,
                             radii=torch.empty(0, dtype=torch.int32, device=dev), allocs=[ag, ab, ai])
 
-    def band_backward(self, st: ForwardState, nsrc: int, pair_cap: int, dL_dpix) -> torch.Tensor:
+    def band_backward(self, st: ForwardState, nsrc: int, pair_cap: int, dL_dpix, reuse: dict | None = None) -> torch.Tensor:
         """B1 + per-splat 2D gradients in the received slot layout: (nsrc * pair_cap, 12) f32."""
         dpix = _f32(dL_dpix, (3, st.cam.height, st.cam.width), self.device)
-        out = torch.empty((int(nsrc) * int(pair_cap), native.GSR_GRAD2D_STRIDE), dtype=torch.float32,
-                          device=self.device)
-        scratch = _Allocator(self.device)
-        c = native.camera_struct(st.cam)
+        shape = (int(nsrc) * int(pair_cap), native.GSR_GRAD2D_STRIDE)
+        if reuse is not None and "g2" in reuse and tuple(reuse["g2"].shape) == shape:
+            out = reuse["g2"]
+        else:
+            out = torch.empty(shape, dtype=torch.float32, device=self.device)
+            if reuse is not None:
+                reuse["g2"] = out
+        scratch = _Allocator(self.device, reuse.setdefault("scratch", []) if reuse is not None else None)
+        c = self._cam(st.cam)
         rc = self.L.gsr_band_backward(ctypes.byref(c), ctypes.byref(st.settings), int(nsrc), int(pair_cap),
                                       ctypes.byref(st.buffers), _ptr(dpix), scratch.cb, None, _ptr(out),
                                       self._stream())
         self._check(rc, "gsr_band_backward")
         return out
 
-    def shard_backward(self, sh: ShardState, grad_recv: torch.Tensor) -> dict:
+    def shard_backward(self, sh: ShardState, grad_recv: torch.Tensor, reuse: dict | None = None) -> dict:
         """Sum of the bands' 2D gradients per Gaussian (band order), then B2 on the shard."""
         st = ForwardState(cam=sh.cam, inputs=sh.inputs, settings=sh.settings, gauss=sh.gauss,
                           buffers=native.Buffers(), color=sh.radii, radii=sh.radii)
-        out, gg = self._grad_tensors(st)
+        if reuse is not None and reuse.get("grads_P") == sh.gauss.P:
+            out, gg = reuse["grads"]
+        else:
+            out, gg = self._grad_tensors(st)
+            if reuse is not None:
+                reuse["grads_P"], reuse["grads"] = sh.gauss.P, (out, gg)
         nb = len(sh.band_rows) - 1
         rows = (ctypes.c_int32 * (nb + 1))(*[int(r) for r in sh.band_rows])
-        c = native.camera_struct(sh.cam)
+        c = self._cam(sh.cam)
         rc = self.L.gsr_shard_backward(ctypes.byref(c), ctypes.byref(sh.gauss), ctypes.byref(sh.settings), nb, rows,
                                        sh.pair_cap, _ptr(sh.state), _ptr(grad_recv.contiguous()), ctypes.byref(gg),
                                        self._stream())
