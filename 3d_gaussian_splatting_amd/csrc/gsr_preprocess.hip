@@ -262,12 +262,17 @@ __device__ __forceinline__ void write_record(int g, float opac, const Geo& G, co
 //              (16 rows: 2.9 KB per wave at SH3) -- every cache line is read once, with a quarter
 //              of the load instructions and no block barrier -- and the 16 lanes owning those
 //              rows accumulate them (same k order: bit-identical).
-enum { kShDirect = 0, kShChunks = 2, kShWave = 3 };
+//  kShGlds   : wave w's whole 64-row span goes to a wave-private LDS region at kernel start by
+//              buffer-load-to-LDS DMA (16 B per lane, no VGPRs; the descriptor's range check
+//              zero-fills past the block's rows), overlapping the geometry; each lane then reads
+//              its own row (180-B stride: conflict-free) in the same k order.  One HBM round trip
+//              per wave instead of one per window, at 12 KB of LDS per wave (3 waves per SIMD).
+enum { kShDirect = 0, kShChunks = 2, kShWave = 3, kShGlds = 4 };
 constexpr int kChunkK = 5;               // SH coefficients per staged chunk
 constexpr int kChunkF = 3 * kChunkK;     // floats per row per chunk
 constexpr int kSubRows = 16;             // kShWave: rows per staged window
 #ifndef GSR_F1_SH_MODE
-#define GSR_F1_SH_MODE kShWave
+#define GSR_F1_SH_MODE kShGlds
 #endif
 
 // The block also adds its candidate count (Gaussians with tiles in the band) and instance
@@ -320,6 +325,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void p
             }
         }
     };
+    // kShGlds: wave wv's LDS region (gq KB); the q-th DMA moves bytes [1024 q, 1024 q + 1024) of its
+    // span.  Issued before the parameter loads: loads return in order, so one wait covers both
+    const int gq = (64 * M3 * 4 + 1023) / 1024;
+    if (SH == kShGlds && sh) {
+        const int wu = __builtin_amdgcn_readfirstlane(wv);
+        auto* dst = (__attribute__((address_space(3))) char*)(sh_lds + wu * gq * 256);
+        const int wbase = wu * 64 * M3 * 4;
+#pragma unroll
+        for (int q = 0; q < 12; ++q)
+            if (q < gq)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(wsrc, dst + 1024 * q, 16, ln * 16, wbase + 1024 * q, 0, 0);
+    }
     Params I{};
     if (g < in.P) I = load_params(in, g);
     if (SH == kShChunks && sh) load_chunk(0);
@@ -345,7 +362,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void p
         }
     }
     if (sh) {
-        if (SH == kShWave) {
+        if (SH == kShGlds) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs have landed
+            if (need) {
+                const float* rest = sh_lds + wv * gq * 256 + ln * M3;
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) {
+                    float r = rgb[ch];
+#pragma unroll
+                    for (int k = 1; k < 16; ++k)
+                        if (k < nb) r = r + basis[k] * rest[3 * (k - 1) + ch];
+                    rgb[ch] = r;
+                }
+            }
+        } else if (SH == kShWave) {
             // wave-private window: wave wv's kSubRows x M3 floats
             float* const wnd = sh_lds + wv * kSubRows * M3;
             for (int sub = 0; sub < 64 / kSubRows; ++sub) {
@@ -451,7 +481,10 @@ int launch_preprocess(const gsr_camera& cam, const GaussIn& in, int ty0, int ty1
     const int gx = div_up(cam.width, kTile), gy = div_up(cam.height, kTile);
     const bool sh = in.sh_rest && !in.colors && in.D > 0;
     const dim3 grid(div_up(in.P, 256)), block(256);
-    if (sh && GSR_F1_SH_MODE == kShWave && in.M_rest * 3 <= 64 && (reinterpret_cast<uintptr_t>(in.sh_rest) & 15) == 0)
+    if (sh && GSR_F1_SH_MODE == kShGlds && in.M_rest * 3 <= 48 && (reinterpret_cast<uintptr_t>(in.sh_rest) & 15) == 0)
+        hipLaunchKernelGGL(preprocess_kernel<kShGlds>, grid, block, 4 * 1024 * ((64 * in.M_rest * 3 * 4 + 1023) / 1024),
+                           s, cam, in, gx, gy, ty0, ty1, out);
+    else if (sh && GSR_F1_SH_MODE == kShWave && in.M_rest * 3 <= 64 && (reinterpret_cast<uintptr_t>(in.sh_rest) & 15) == 0)
         hipLaunchKernelGGL(preprocess_kernel<kShWave>, grid, block, sizeof(float) * 4 * kSubRows * in.M_rest * 3, s,
                            cam, in, gx, gy, ty0, ty1, out);
     else if (sh)
