@@ -432,19 +432,32 @@ __global__ __launch_bounds__(256) void preprocess_backward_kernel(
     const bool stage = in.sh_rest != nullptr && !in.colors;  // block-uniform
     const int rows = n - blockIdx.x * 256 < 256 ? n - blockIdx.x * 256 : 256;
     const size_t obase = (size_t)blockIdx.x * 256 * M3, ibase = (size_t)g0 * M3 + obase;
-    BwdIn bi{};
-    if (o < n) bi = load_bwd_in(in, g0 + o, o, depth_key, flags, grad2d);
     // 16-B staging when the rows start 16-B aligned (always for g0 = 0: a block's 256 rows are
     // 46080 B); 4-B otherwise
     const bool v4 = GSR_B2_VEC4 && ((reinterpret_cast<uintptr_t>(in.sh_rest + ibase) |
                                      reinterpret_cast<uintptr_t>(out.sh_rest + obase)) & 15u) == 0;
+    // Aligned rows are staged by buffer-load-to-LDS DMA: the block's 256 * M3 floats are M3 pieces
+    // of 1 KB (64 lanes x 16 B), piece q by wave q % 4, all issued before the per-Gaussian inputs
+    // (loads return in order: one wait covers both); the descriptor's range check zero-fills
+    // the rows past n.
+    if (stage && v4) {
+        const auto src = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in.sh_rest + ibase), 0,
+                                                           rows * M3 * (int)sizeof(float), 0x00020000);
+        const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
+        auto* dst = (__attribute__((address_space(3))) char*)sh_lds;
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {  // M3 <= 45 pieces: <= 12 per wave
+            const int q = 4 * j + wu;
+            if (q < M3) __builtin_amdgcn_raw_ptr_buffer_load_lds(src, dst + 1024 * q, 16, ln * 16, 1024 * q, 0, 0);
+        }
+    }
+    BwdIn bi{};
+    if (o < n) bi = load_bwd_in(in, g0 + o, o, depth_key, flags, grad2d);
     if (stage) {  // coalesced staging of the block's SH-rest rows (see preprocess_kernel)
-        const int nf = rows * M3;
         if (v4) {
-            const float4* src = reinterpret_cast<const float4*>(in.sh_rest + ibase);
-            for (int i = threadIdx.x; i < nf / 4; i += 256) reinterpret_cast<float4*>(sh_lds)[i] = src[i];
-            for (int i = (nf & ~3) + threadIdx.x; i < nf; i += 256) sh_lds[i] = in.sh_rest[ibase + i];
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces have landed
         } else {
+            const int nf = rows * M3;
             for (int i = threadIdx.x; i < nf; i += 256) sh_lds[i] = in.sh_rest[ibase + i];
         }
         __syncthreads();
