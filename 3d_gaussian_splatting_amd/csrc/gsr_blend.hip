@@ -211,12 +211,6 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
             if (lane == 0) ckm[4 * (size_t)slot + w * PPL + p] = on ? 1 : 0;
         }
     };
-#ifndef GSR_F6_GID_PREFETCH
-#define GSR_F6_GID_PREFETCH 1
-#endif
-    // the next batch's gids are loaded one batch ahead, so a batch waits for its records only
-    uint32_t gnext = 0;
-    if (GSR_F6_GID_PREFETCH && tid < n) gnext = sorted_gid[range.x + tid];
     for (int base = 0; base < n; base += BATCH) {
         uint32_t live = 0;
 #pragma unroll
@@ -226,10 +220,8 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
             tend = base;
             break;
         }
-        const uint32_t gcur = gnext;
-        if (GSR_F6_GID_PREFETCH && base + BATCH + tid < n) gnext = sorted_gid[range.x + base + BATCH + tid];
         if (base + tid < n) {
-            const uint32_t g = GSR_F6_GID_PREFETCH ? gcur : sorted_gid[range.x + base + tid];
+            const uint32_t g = sorted_gid[range.x + base + tid];
             const float4* r = rec + 3 * (size_t)g;
             const float4 r0 = r[0], r1 = r[1], r2 = r[2];
             srec[3 * tid + 0] = r0;
