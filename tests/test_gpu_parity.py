@@ -116,6 +116,8 @@ CONFIGS = [  # (P, W, H, active D, seed)
     (5000, 300, 200, 3, 1),      # partial tiles, SH3
     (20000, 640, 360, 2, 2),
     (100000, 800, 800, 3, 0),    # BASELINE configs[1]
+    (1001, 256, 256, 3, 5),      # P % 4 != 0: the SH rows' DMA pieces of the last block end
+    (4097, 300, 200, 3, 6),      #   inside a 16-B piece (F1 and B2 staging)
 ]
 
 
