@@ -251,6 +251,58 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
             if (!live) continue;
             const uint32_t mine = (sm >> (w * PPL)) & ((1u << PPL) - 1u);
             uint64_t todo = __ballot((mine & live) != 0u && c0 + lane < cnt);
+#ifndef GSR_F6_BAND_PAIRS
+#define GSR_F6_BAND_PAIRS 1
+#endif
+            // Band launches (NW = 4: one stripe per wave, every block resident at once) are bound
+            // by one wave's dependent chain per record, not by issue: there two records are taken
+            // per pass -- both alphas first (they do not depend on T), then the T / colour
+            // updates in list order, so the result is bit-identical.
+            if constexpr (GSR_F6_BAND_PAIRS && PPL == 1) {
+                while (todo) {
+                    const int ka = c0 + __builtin_ctzll(todo);
+                    todo &= todo - 1;
+                    const bool two = todo != 0;  // wave-uniform
+                    const int kb = two ? c0 + __builtin_ctzll(todo) : ka;
+                    if (two) todo &= todo - 1;
+                    const float4 a0 = srec[3 * ka + 0], a1 = srec[3 * ka + 1], a2 = srec[3 * ka + 2];
+                    const float4 b0 = srec[3 * kb + 0], b1 = srec[3 * kb + 1], b2 = srec[3 * kb + 2];
+                    const float dxa = a0.x - pfx, dxb = b0.x - pfx;
+                    const float dya = a0.y - pfy[0], dyb = b0.y - pfy[0];
+                    const float ea = fmaf(fmaf(a1.x, dya, a0.w * dxa), dya, fmaf(a0.z * dxa, dxa, a2.w));
+                    const float eb = fmaf(fmaf(b1.x, dyb, b0.w * dxb), dyb, fmaf(b0.z * dxb, dxb, b2.w));
+                    float oGa, oGb;
+                    const float aa = pair_alpha(ea, a2.w, oGa);
+                    const float ab = pair_alpha(eb, b2.w, oGb);
+                    {
+                        const float w = aa * T[0];
+                        const float tT = T[0] - w;
+                        const bool ok = tT >= 0.0001f;
+                        const float wgt = ok ? w : 0.0f;
+                        C0[0] = fmaf(a1.z, wgt, C0[0]);
+                        C1[0] = fmaf(a1.w, wgt, C1[0]);
+                        C2[0] = fmaf(a2.x, wgt, C2[0]);
+                        T[0] = ok ? tT : -fabsf(T[0]);
+                    }
+                    if (two) {
+                        const float w = ab * T[0];
+                        const float tT = T[0] - w;
+                        const bool ok = tT >= 0.0001f;
+                        const float wgt = ok ? w : 0.0f;
+                        C0[0] = fmaf(b1.z, wgt, C0[0]);
+                        C1[0] = fmaf(b1.w, wgt, C1[0]);
+                        C2[0] = fmaf(b2.x, wgt, C2[0]);
+                        T[0] = ok ? tT : -fabsf(T[0]);
+                    }
+                    const int before = visited;
+                    visited += two ? 2 : 1;
+                    if ((before >> 3) != (visited >> 3)) {
+                        live = __any(T[0] > 0.0f) ? 1u : 0u;
+                        if (live == 0) break;
+                    }
+                }
+                continue;
+            }
             while (todo) {
                 const int kk = __builtin_ctzll(todo);
                 todo &= todo - 1;
