@@ -283,7 +283,7 @@ __global__ __launch_bounds__(1024) void scan_partials(uint32_t* __restrict__ par
 
 __global__ __launch_bounds__(kB) void scan_downsweep(const uint32_t* __restrict__ in, int n,
                                                      const uint32_t* __restrict__ partials,
-                                                     uint32_t* __restrict__ out) {
+                                                     uint32_t* __restrict__ out, uint4* __restrict__ rect) {
     __shared__ uint32_t buf[kSortTile + kSortTile / 32];
     __shared__ uint32_t wsum[kWaves];
     const int base = blockIdx.x * kSortTile;
@@ -313,6 +313,17 @@ __global__ __launch_bounds__(kB) void scan_downsweep(const uint32_t* __restrict_
     for (int r = 0; r < kI; ++r) {
         const int i = r * kB + tid;
         if (base + i < n) out[base + i] = buf[pad(i)];
+    }
+    // inst_start (rect.z) of every Gaussian with instances: the binning expands from the rect
+    if (rect) {
+#pragma unroll
+        for (int r = 0; r < kI; ++r) {
+            const int g = base + r * kB + tid;
+            if (g < n) {
+                const uint32_t nt = in[g];
+                if (nt) reinterpret_cast<uint32_t*>(rect + g)[2] = buf[pad(r * kB + tid)] - nt;
+            }
+        }
     }
 }
 
@@ -443,6 +454,7 @@ __global__ __launch_bounds__(256) void scan_duplicate_kernel(const uint32_t* __r
         if (nt) rect[g].z = excl + lex;  // inst_start
     }
     if (total_out && tid == 0 && (b + 1) * 256 >= n) *total_out = excl + total;  // the last block: K
+    if (!tkey) return;  // scan only: the counting binning (gsr_bin.hip) emits the instances
     // emission: this wave's instances [excl + pre_w, + wsum[w]) with pre_w = first lane's lex
     const uint32_t wbase = pre;  // = lex of lane 0 of this wave
     // the owner search needs starts non-decreasing across the wave: a Gaussian without tiles
@@ -884,13 +896,13 @@ int radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* k0, u
 }
 
 int launch_scan(const uint32_t* tiles, int n, uint32_t* offsets, uint32_t* scan_partials_buf, uint32_t* total_out,
-                hipStream_t s) {
+                uint4* rect, hipStream_t s) {
     if (n <= 0) return (int)hipMemsetAsync(total_out, 0, sizeof(uint32_t), s);
     if (n <= kFusedScanMax) return 0;  // scanned by the fused kernel in launch_duplicate
     const int nb = sort_blocks(n);
     hipLaunchKernelGGL(scan_reduce, dim3(nb), dim3(kB), 0, s, tiles, n, scan_partials_buf);
     hipLaunchKernelGGL(scan_partials, dim3(1), dim3(1024), 0, s, scan_partials_buf, nb, total_out);
-    hipLaunchKernelGGL(scan_downsweep, dim3(nb), dim3(kB), 0, s, tiles, n, scan_partials_buf, offsets);
+    hipLaunchKernelGGL(scan_downsweep, dim3(nb), dim3(kB), 0, s, tiles, n, scan_partials_buf, offsets, rect);
     return (int)hipGetLastError();
 }
 
@@ -905,6 +917,7 @@ int launch_duplicate(const uint32_t* tiles, uint4* rect, int n, int grid_x, int 
                            tkey, tgid, cap, lookback + 16, lookback, total_out);
         return (int)hipGetLastError();
     }
+    if (!tkey) return 0;  // scanned by launch_scan; the counting binning emits
     hipLaunchKernelGGL(duplicate_kernel, dim3(div_up(n, 256)), dim3(256), 0, s, offsets, tiles, rect, n, grid_x, ty0,
                        tkey, tgid, cap);
     return (int)hipGetLastError();

@@ -17,7 +17,8 @@ import os
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(PKG, "lib")
-HIP_LIB = os.path.join(LIB_DIR, "libgsr_hip.so")
+# GSR_HIP_LIB: an experiment build (lib/variants/<name>/libgsr_hip.so) instead of the shipped one
+HIP_LIB = os.environ.get("GSR_HIP_LIB") or os.path.join(LIB_DIR, "libgsr_hip.so")
 
 ABI_VERSION = 3
 GSR_FLAG_DEBUG = 1
