@@ -27,8 +27,6 @@ ARCH = "gfx950"
 HIP_SOURCES = {
     "gsr_preprocess.hip": ["-ffp-contract=off"],
     "gsr_sort.hip": [],
-    # counting-sort binning (integer work)
-    "gsr_bin.hip": [],
     # F6 and B1 must evaluate alpha / T identically; no SLP packing (it splits DPP-fused adds)
     "gsr_blend.hip": ["-ffp-contract=off", "-fno-slp-vectorize"],
     # recomputes the forward's SH clamp bits: must round exactly like gsr_preprocess.hip

@@ -203,7 +203,7 @@ void band(const gsr_camera* cam, const gsr_raster_settings* rs, int* y0, int* y1
 // Device pointers into the caller's buffers (layouts in gsr_internal.h).  n: Gaussians (or
 // received splat slots) indexed; cap: the binning's instance capacity.
 struct Views {
-    uint32_t *depth_key, *tiles, *flags, *offsets, *partials, *lookback, *dsort, *dhist;
+    uint32_t *depth_key, *tiles, *flags, *offsets, *partials, *lookback;
     float4* rec;
     uint4* rect;
     uint2* ranges;
@@ -227,8 +227,6 @@ Views views(const gsr_camera* cam, long long n, const gsr_buffers* b) {
     v.offsets = at<uint32_t>(b->geom, gl.offsets);
     v.partials = at<uint32_t>(b->geom, gl.partials);
     v.lookback = at<uint32_t>(b->geom, gl.lookback);
-    v.dsort = at<uint32_t>(b->geom, gl.dsort);
-    v.dhist = at<uint32_t>(b->geom, gl.dhist);
     v.ranges = at<uint2>(b->image, il.ranges);
     v.counters = at<uint32_t>(b->image, il.counters);
     v.K_dev = v.counters + kTotalSlot;
@@ -247,8 +245,7 @@ Views views(const gsr_camera* cam, long long n, const gsr_buffers* b) {
         v.vB = at<uint32_t>(b->binning, bl.vB);
         v.hist = at<uint32_t>(b->binning, bl.hist);
         const int tiles = div_up(cam->width, kTile) * div_up(cam->height, kTile);
-        // the counting binning writes (kA, vA); the LSD sort ends in (kB, vB) after odd passes
-        const bool odd = !bin_counting(tiles) && (tile_passes(tiles) & 1) != 0;
+        const bool odd = (tile_passes(tiles) & 1) != 0;  // the sort ends in (kB, vB) after odd passes
         v.sorted_tile = odd ? v.kB : v.kA;
         v.sorted_gid = odd ? v.vB : v.vA;
         v.free_k = odd ? v.kA : v.kB;
@@ -309,8 +306,7 @@ int fwd_phase1(FwdJob& j, gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_image, voi
     }
     GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(v.ranges, 0, il.ovf - il.ranges, stream), "clear ranges");
     if (int e = pre(v)) return e;
-    GSR_STAGE(GSR_STAGE_SCAN, launch_scan(v.tiles, (int)j.n, v.offsets, v.partials, v.K_dev,
-                                          bin_counting((long long)j.gx * j.gy) ? v.rect : nullptr, stream), "scan");
+    GSR_STAGE(GSR_STAGE_SCAN, launch_scan(v.tiles, (int)j.n, v.offsets, v.partials, v.K_dev, stream), "scan");
     return 0;
 }
 
@@ -325,34 +321,10 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
     if (!bufs->binning) return fail(-2, "allocation failed (binning, %lld instances)", cap);
     const Views v = views(cam, j.n, bufs);
     const int tiles = j.gx * j.gy, ntiles = (j.ty1 - j.ty0) * j.gx;
-    const bool counting = bin_counting(tiles);
-    // the counting binning needs only the scan first (fused with nothing to emit for small n)
-    GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate(v.tiles, v.rect, (int)j.n, j.gx, j.ty0, v.offsets, v.lookback,
-                                                    counting ? nullptr : v.kA, v.vA, cap, v.K_dev, stream),
+    GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate(v.tiles, v.rect, (int)j.n, j.gx, j.ty0, v.offsets, v.lookback, v.kA,
+                                                    v.vA, cap, v.K_dev, stream),
               "duplicate");
-    if (counting) {
-        // (depth, gid) order of the Gaussians: a stable LSD sort of the 32-bit depth keys over gid
-        // order; the binning then emits every tile's list in the canonical order directly
-        const uint32_t* perm = nullptr;
-        if (GSR_BIN_DEPTH && j.n > 0 && cap > 0) {
-            const size_t n = (size_t)j.n;
-            uint32_t* d = v.dsort;
-            int which = -1;
-            GSR_STAGE(GSR_STAGE_DEPTH_SORT, radix_sort(v.depth_key, nullptr, d, d + n, d + 2 * n, d + 3 * n, j.n,
-                                                       nullptr, 32, v.dhist, &which, stream),
-                      "depth order");
-            perm = which == 0 ? d + n : d + 3 * n;
-        }
-        GSR_STAGE(GSR_STAGE_TILE_SORT, launch_bin(v.rect, perm, (int)j.n, j.gx, j.ty0, ntiles, cap, v.hist,
-                                                  v.sorted_gid, v.sorted_tile, v.ranges, stream),
-                  "tile binning");
-        if (cap > 0 && !perm)
-            GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_tile_depth_sort(v.ranges, j.ty0 * j.gx, ntiles, cap, v.depth_key,
-                                                                   v.sorted_gid, v.ovf, v.counters + kOvfCountSlot,
-                                                                   v.ovf2, v.counters + kOvf2CountSlot, v.done,
-                                                                   v.free_k, v.free_v, stream),
-                      "per-tile depth order");
-    } else if (cap > 0) {
+    if (cap > 0) {
         int which = -1;
         GSR_STAGE(GSR_STAGE_TILE_SORT, radix_sort(v.kA, v.vA, v.kB, v.vB, v.kA, v.vA, cap, v.K_dev, tile_bits(tiles),
                                                   v.hist, &which, stream),

@@ -46,7 +46,7 @@ inline size_t sort_scratch_words(long long n) { return 256 * ((size_t)radix_bloc
 // lengths and emission index bases are u32: n instances must stay below 2^32, and the blend's
 // per-tile index arithmetic below 2^31
 struct GeomLayout {
-    size_t depth_key, tiles, flags, rec, rect, offsets, partials, lookback, dsort, dhist, total;
+    size_t depth_key, tiles, flags, rec, rect, offsets, partials, lookback, total;
     GeomLayout(long long P) {
         size_t o = 0, n = (size_t)(P > 0 ? P : 1);
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
@@ -58,8 +58,6 @@ struct GeomLayout {
         offsets = take(4 * n);
         partials = take(4 * ((size_t)sort_blocks(n) + 16));  // three-kernel scan
         lookback = take(4 * (16 + (n + 255) / 256));        // fused scan + duplicate
-        dsort = take(4 * 4 * n);                             // (depth, gid) order: key/value ping-pong
-        dhist = take(4 * sort_scratch_words(n));
         total = o;
     }
 };
@@ -107,49 +105,9 @@ __host__ __device__ inline size_t ck_slot_of(bool fixed, uint32_t start, int til
     return fixed ? (size_t)tile * (kMaxChunks - 1) + (chunk - 1) : (size_t)(start / kCkDiv) + tile + (chunk - 1);
 }
 
-// Counting-sort binning (gsr_bin.hip) for images of up to kBinMaxTiles tiles (the per-tile
-// counters live in LDS); larger images take F3 + the LSD tile-key sort + finalize.  The
-// Gaussians are cut into at most bin_max_segments(cap) segments (about kBinSegInst instances
-// each, at most kBinMaxSeg: the segment x tile count matrix is nseg * T u32).
-constexpr int kBinMaxTiles = 16384;
-constexpr long long kBinSegInst = 8192;
-constexpr int kBinMaxSeg = 2048;
-#ifndef GSR_BIN_COUNTING
-#define GSR_BIN_COUNTING 0  // 1: the counting binning for images of <= kBinMaxTiles tiles
-#endif
-inline bool bin_counting(long long tiles) { return GSR_BIN_COUNTING && tiles <= kBinMaxTiles; }
-// the counting binning expands the Gaussians in (depth, gid) order (a global LSD sort of the P
-// depth keys), so the tile lists need no per-tile depth sort; 0: gid order + per-tile sort
-#ifndef GSR_BIN_DEPTH
-#define GSR_BIN_DEPTH 1
-#endif
-inline int bin_max_segments(long long cap) {
-    const long long s = cap > 0 ? (cap + kBinSegInst - 1) / kBinSegInst : 1;
-    return (int)(s < 1 ? 1 : (s > kBinMaxSeg ? kBinMaxSeg : s));
-}
-// segments of one launch over n Gaussians (S a multiple of 64, nseg <= bin_max_segments(cap))
-struct BinSeg {
-    int S, nseg;
-    size_t mat_words;
-    BinSeg(long long n, long long cap, int T) {
-        const long long ms = bin_max_segments(cap);
-        long long s = n > 0 ? (n + ms - 1) / ms : 1;
-        s = (s + 63) / 64 * 64;
-        S = (int)s;
-        nseg = n > 0 ? (int)((n + s - 1) / s) : 0;
-        mat_words = (size_t)nseg * (size_t)(T > 0 ? T : 0);
-    }
-};
-// scratch of the counting binning (u32): the matrix, tile totals, tile starts
-inline size_t bin_scratch_words(long long cap, long long tiles) {
-    return bin_counting(tiles) ? (size_t)bin_max_segments(cap) * (size_t)tiles + 2 * (size_t)tiles + 64 : 0;
-}
-
 // Binning for up to `cap` instances (the exact K, or a caller-given bound) of an image of
-// `tiles` tiles.  Counting binning: the gids land in vA (tile ids in kA); the LSD form emits
-// into (kA, vA) and ping-pongs with (kB, vB).  (kB, vB) are then the per-tile depth sort's
-// scratch.  Then the checkpoint slots: ck_slots x 256 float4, and one live byte per (slot, 16x4
-// stripe).
+// `tiles` tiles.  The tile-key sort ping-pongs (kA, vA) <-> (kB, vB); F3 emits into (kA, vA).
+// Then the checkpoint slots: ck_slots x 256 float4, and one live byte per (slot, 16x4 stripe).
 struct BinLayout {
     size_t kA, vA, kB, vB, hist, ck, ckm, total, ck_slots;
     BinLayout(long long cap, long long tiles) {
@@ -159,8 +117,7 @@ struct BinLayout {
         vA = take(4 * n);
         kB = take(4 * n);
         vB = take(4 * n);
-        const size_t lsd = sort_scratch_words(n), cnt = bin_scratch_words(cap, tiles);
-        hist = take(4 * (lsd > cnt ? lsd : cnt));
+        hist = take(4 * sort_scratch_words(n));
         ck_slots = ck_pool_slots(cap, tiles);
         ck = take(ck_slots * 256 * 16);
         ckm = take(ck_slots * 4);

@@ -18,7 +18,7 @@ struct PreOut {
     uint32_t* depth_key;
     uint32_t* tiles;
     float4* rec;   // blend records: {x, y, a', b'}, {c', o, r, g}, {b, ext_x, ext_y, log2 o}
-    uint4* rect;   // (minx | miny << 16, maxx | maxy << 16, inst_start (set by F2), band tile count)
+    uint4* rect;   // (minx | miny << 16, maxx | maxy << 16, inst_start (set by F3), 0)
     uint32_t* flags;     // nullable: SH clamp bits per Gaussian (B2 recomputes them when absent)
     uint32_t* counters;  // nullable, zeroed: [slot] += Gaussians with tiles in the band,
                          // [kCountSlots + slot] += K (slot = block % kCountSlots)
@@ -41,25 +41,14 @@ int radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* k0, u
 // F2: inclusive scan of tiles[0..n) (gid order) -> offsets and the total K -> *total_out
 // (device), as three kernels for n > kFusedScanMax (nothing to do below: the fused kernel of
 // launch_duplicate scans).  scan_partials_buf: sort_blocks(n) + 16 u32.
-// rect (nullable): inst_start -> rect.z of every Gaussian with tiles.
 int launch_scan(const uint32_t* tiles, int n, uint32_t* offsets, uint32_t* scan_partials_buf, uint32_t* total_out,
-                uint4* rect, hipStream_t s);
+                hipStream_t s);
 // F3: inst_start (rect[g].z) and the emitted (tile key, gid) pairs in gid order, rect row-major,
 // band rows from ty0 -- at most `cap` of them.  For n <= kFusedScanMax one look-back kernel
 // also does F2 (offsets, *total_out); lookback: 16 + ceil(n / 256) u32.
 int launch_duplicate(const uint32_t* tiles, uint4* rect, int n, int grid_x, int ty0, uint32_t* offsets,
                      uint32_t* lookback, uint32_t* tkey, uint32_t* tgid, long long cap, uint32_t* total_out,
                      hipStream_t s);
-
-// F3 + F4 + F5 (+ the per-tile depth order) as one counting sort by tile (gsr_bin.hip; ntiles <=
-// kBinMaxTiles).  The Gaussians are expanded in the order perm[0..n) (their (depth, gid) order:
-// the tile lists come out in the canonical (tile, depth, gid) order), or gid order when perm is
-// null (then each tile's list is in gid order and needs launch_tile_depth_sort).  rect: F1's rect
-// with inst_start (.z, the F2 scan) and the band tile count (.w).  Out: the band's instances
-// grouped by tile -> out_gid (and their global tile ids -> out_tile when non-null),
-// ranges[ty0 * grid_x ..] for the band's ntiles tiles.  mat_buf: bin_scratch_words(cap, tiles).
-int launch_bin(const uint4* rect, const uint32_t* perm, int n, int grid_x, int ty0, int ntiles, long long cap,
-               uint32_t* mat_buf, uint32_t* out_gid, uint32_t* out_tile, uint2* ranges, hipStream_t s);
 
 // Per-tile depth order: every tile's slice of `gid` (tile-sorted, gid order within a tile) is
 // sorted in place by (depth_key[gid], gid) -- the canonical (tile, depth, gid) order -- with a

@@ -244,10 +244,8 @@ __device__ __forceinline__ void write_record(int g, float opac, const Geo& G, co
     rec[0] = make_float4(G.xs, G.ys, -0.5f * kL2E * G.cA, -kL2E * G.cB);
     rec[1] = make_float4(-0.5f * kL2E * G.cC, opac, rgb[0], rgb[1]);
     rec[2] = make_float4(rgb[2], ex, ey, log2f(opac));
-    // .z = inst_start (written by the F2 scan), .w = the band-clipped tile count (the binning
-    // expands instances from the rect alone)
     out.rect[g] = make_uint4((uint32_t)G.minx | ((uint32_t)G.miny << 16), (uint32_t)G.maxx | ((uint32_t)G.maxy << 16),
-                             0u, G.tiles);
+                             0u, 0u);
     if (out.flags) out.flags[g] = clamped;
 }
 
@@ -350,7 +348,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void p
         out.radii[g] = G.radius;
         out.depth_key[g] = G.key;
         out.tiles[g] = G.tiles;
-        if (G.tiles == 0) out.rect[g] = make_uint4(0u, 0u, 0u, 0u);  // no instances (rect.w = 0)
     }
     const bool need = G.tiles != 0;  // colour and record only for Gaussians this band blends
     float rgb[3] = {0.f, 0.f, 0.f}, basis[16];

@@ -217,15 +217,13 @@ __global__ __launch_bounds__(256) void unpack_kernel(const char* __restrict__ re
             rec[3 * i + 2] = sp[2];
             const uint32_t lo = __float_as_uint(a.y), hi = __float_as_uint(a.z);
             depth_key[i] = __float_as_uint(a.x);
+            rect[i] = make_uint4(lo, hi, 0u, 0u);
             const int miny = (int)(lo >> 16), maxy = (int)(hi >> 16);
             const int y0 = miny > ty0 ? miny : ty0, y1 = maxy < ty1 ? maxy : ty1;
-            const uint32_t nt = y1 > y0 ? ((hi & 0xFFFF) - (lo & 0xFFFF)) * (uint32_t)(y1 - y0) : 0u;
-            tiles[i] = nt;
-            rect[i] = make_uint4(lo, hi, 0u, nt);  // .w: the band-clipped tile count (as F1 writes it)
+            tiles[i] = y1 > y0 ? ((hi & 0xFFFF) - (lo & 0xFFFF)) * (uint32_t)(y1 - y0) : 0u;
         } else {
             depth_key[i] = 0xFFFFFFFFu;
             tiles[i] = 0u;
-            rect[i] = make_uint4(0u, 0u, 0u, 0u);
         }
     }
 }

@@ -118,7 +118,7 @@ CONFIGS = [  # (P, W, H, active D, seed)
     (100000, 800, 800, 3, 0),    # BASELINE configs[1]
     (1001, 256, 256, 3, 5),      # P % 4 != 0: the SH rows' DMA pieces of the last block end
     (4097, 300, 200, 3, 6),      #   inside a 16-B piece (F1 and B2 staging)
-    (20000, 2400, 1800, 1, 3),   # 16950 tiles > kBinMaxTiles: the LSD tile-key sort + finalize
+    (20000, 2400, 1800, 1, 3),   # 16950 tiles: 15 tile bits (8 + 7 per radix pass)
 ]
 
 
