@@ -91,10 +91,17 @@ __global__ __launch_bounds__(kB) void radix_upsweep(const uint32_t* __restrict__
     const uint32_t mask = (1u << nbits) - 1u;
     const int chunk = radix_chunk(blockIdx.x, nb);
     const long long base = (long long)chunk * kRadixTile + (long long)w * kRadixWaveItems;
-#pragma unroll 4
+    // all kRI loads in flight before the first atomic (one HBM round trip per wave, not kRI / 4)
+    uint32_t k[kRI];
+#pragma unroll
     for (int r = 0; r < kRI; ++r) {
         const long long idx = base + r * 64 + (tid & 63);
-        if (idx < n) atomicAdd(&cnt[w][(keys[idx] >> shift) & mask], 1u);
+        k[r] = idx < n ? keys[idx] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int r = 0; r < kRI; ++r) {
+        const long long idx = base + r * 64 + (tid & 63);
+        if (idx < n) atomicAdd(&cnt[w][(k[r] >> shift) & mask], 1u);
     }
     __syncthreads();
     uint32_t s = 0;
