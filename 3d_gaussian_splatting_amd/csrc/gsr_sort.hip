@@ -941,6 +941,8 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
     // of up to 8192 (73 KB: 2 per CU) walking the queue, and beyond that for tile_depth_sort_big
     const long long mean = K / ntiles;
     int cap = 1024;
+    // (one 8192-entry block per tile at 5M / 1080p: 0.89 ms with 512 threads, 0.79 with 1024,
+    // against 0.49 for 4096-entry blocks + the queue: 1 block per CU)
     while (cap < 4096 && cap < mean + mean / 2) cap <<= 1;
 #define GSR_TILE_RADIX(NT_, I_)                                                                          \
     hipLaunchKernelGGL((tile_depth_radix<NT_, I_, 9>), dim3(ntiles), dim3(NT_), 0, s, ranges, tile0, depth_key, \
