@@ -40,7 +40,16 @@ inline int pack_blocks(long long n) { return n > 0 ? div_up(n, kPackTile) : 0; }
 // per block; 2048 measured slower: 0.137 vs 0.120 ms for the 1M / 1080p tile sort)
 constexpr int kRadixItems = 16;
 constexpr int kRadixTile = kSortBlock * kRadixItems;
-inline int radix_blocks(long long n) { return n > 0 ? div_up(n, kRadixTile) : 0; }
+// Sorts of fewer than kRadixSmallN keys (multi-GPU band launches, ~1M keys at 1M / 1080p, N = 8)
+// use 1024-key blocks (kRadixItemsSmall rounds per wave), so that they still launch several
+// blocks per CU.
+#ifndef GSR_RADIX_SMALL_N
+#define GSR_RADIX_SMALL_N (1 << 21)
+#endif
+constexpr long long kRadixSmallN = GSR_RADIX_SMALL_N;
+constexpr int kRadixItemsSmall = 4;
+inline int radix_tile_for(long long n) { return n < kRadixSmallN ? kSortBlock * kRadixItemsSmall : kRadixTile; }
+inline int radix_blocks(long long n) { return n > 0 ? div_up(n, radix_tile_for(n)) : 0; }
 inline size_t sort_scratch_words(long long n) { return 256 * ((size_t)radix_blocks(n) + 1) + 256; }
 
 // lengths and emission index bases are u32: n instances must stay below 2^32, and the blend's

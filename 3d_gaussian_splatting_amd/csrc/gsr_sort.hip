@@ -33,8 +33,6 @@ constexpr int kB = kSortBlock;       // 256 threads = 4 waves
 constexpr int kI = kSortItems;       // 16 rounds per wave
 constexpr int kWaves = kB / 64;
 constexpr int kWaveItems = kI * 64;  // 1024 contiguous items per wave
-constexpr int kRI = kRadixItems;     // radix passes: rounds per wave
-constexpr int kRadixWaveItems = kRI * 64;
 
 __device__ inline uint64_t lanemask_lt() {
     const int lane = threadIdx.x & 63;
@@ -79,6 +77,8 @@ __device__ __forceinline__ int radix_chunk(int b, int nb) {
 // Counting needs no stable rank, so per-wave LDS sub-histograms with atomics suffice (the
 // 8-ballot peer match of the downsweep measured slower here).  Blocks past the live count
 // write zero columns.
+// RI: rounds of 64 keys per wave (kRadixItems, or kRadixItemsSmall for small sorts)
+template <int RI>
 __global__ __launch_bounds__(kB) void radix_upsweep(const uint32_t* __restrict__ keys, long long cap,
                                                     const uint32_t* __restrict__ n_dev, int shift, int nbits,
                                                     int nb, uint32_t* __restrict__ hist) {
@@ -90,16 +90,16 @@ __global__ __launch_bounds__(kB) void radix_upsweep(const uint32_t* __restrict__
     __syncthreads();
     const uint32_t mask = (1u << nbits) - 1u;
     const int chunk = radix_chunk(blockIdx.x, nb);
-    const long long base = (long long)chunk * kRadixTile + (long long)w * kRadixWaveItems;
-    // all kRI loads in flight before the first atomic (one HBM round trip per wave, not kRI / 4)
-    uint32_t k[kRI];
+    const long long base = (long long)chunk * (kB * RI) + (long long)w * (64 * RI);
+    // all RI loads in flight before the first atomic (one HBM round trip per wave, not RI / 4)
+    uint32_t k[RI];
 #pragma unroll
-    for (int r = 0; r < kRI; ++r) {
+    for (int r = 0; r < RI; ++r) {
         const long long idx = base + r * 64 + (tid & 63);
         k[r] = idx < n ? keys[idx] : 0xFFFFFFFFu;
     }
 #pragma unroll
-    for (int r = 0; r < kRI; ++r) {
+    for (int r = 0; r < RI; ++r) {
         const long long idx = base + r * 64 + (tid & 63);
         if (idx < n) atomicAdd(&cnt[w][(k[r] >> shift) & mask], 1u);
     }
@@ -143,6 +143,7 @@ __global__ __launch_bounds__(kB) void radix_colscan(uint32_t* __restrict__ hist,
 }
 
 // ---- downsweep: stable scatter, reordered through LDS so global writes are coalesced ----
+template <int RI>
 __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict__ keys_in,
                                                       const uint32_t* __restrict__ vals_in,
                                                       uint32_t* __restrict__ keys_out,
@@ -154,11 +155,12 @@ __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict
     __shared__ uint32_t gbase[256];   // global position of this block's first item of digit d
     __shared__ uint32_t lbase[256];   // block-local position of the first item of digit d
     __shared__ uint32_t wsum[kWaves];
-    __shared__ uint32_t skey[kRadixTile];
-    __shared__ uint32_t sval[kRadixTile];
+    constexpr int TILE = kB * RI;
+    __shared__ uint32_t skey[TILE];
+    __shared__ uint32_t sval[TILE];
     const long long n = live_count(cap, n_dev);
     const int chunk = radix_chunk(blockIdx.x, nb);
-    const long long bbase = (long long)chunk * kRadixTile;
+    const long long bbase = (long long)chunk * TILE;
     if (bbase >= n) return;  // block-uniform: nothing of this block is live
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const uint32_t mask = (1u << nbits) - 1u;
@@ -181,18 +183,18 @@ __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict
         gbase[tid] = pre + x - v + hist[(size_t)tid * nb + chunk];
     }
     __syncthreads();
-    const long long base = bbase + (long long)w * kRadixWaveItems;
-    uint32_t key[kRI], val[kRI], rank[kRI];
+    const long long base = bbase + (long long)w * (64 * RI);
+    uint32_t key[RI], val[RI], rank[RI];
     const uint64_t lt = lanemask_lt();
 #pragma unroll
-    for (int r = 0; r < kRI; ++r) {
+    for (int r = 0; r < RI; ++r) {
         const long long idx = base + r * 64 + lane;
         const bool valid = idx < n;
         key[r] = valid ? keys_in[idx] : 0xFFFFFFFFu;
         val[r] = valid ? (vals_in ? vals_in[idx] : (uint32_t)idx) : 0u;
     }
 #pragma unroll
-    for (int r = 0; r < kRI; ++r) {
+    for (int r = 0; r < RI; ++r) {
         const long long idx = base + r * 64 + lane;
         const bool valid = idx < n;
         const uint32_t d = (key[r] >> shift) & mask;
@@ -228,7 +230,7 @@ __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kRI; ++r) {
+    for (int r = 0; r < RI; ++r) {
         const long long idx = base + r * 64 + lane;
         if (idx < n) {
             const uint32_t d = (key[r] >> shift) & mask;
@@ -238,7 +240,7 @@ __global__ __launch_bounds__(kB) void radix_downsweep(const uint32_t* __restrict
         }
     }
     __syncthreads();
-    const int count = (n - bbase) < kRadixTile ? (int)(n - bbase) : kRadixTile;
+    const int count = (n - bbase) < TILE ? (int)(n - bbase) : TILE;
 #pragma unroll 4
     for (int i = tid; i < count; i += kB) {
         const uint32_t k = skey[i];
@@ -892,10 +894,19 @@ int radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* k0, u
         const int bits = (nbits - shift) < per ? (nbits - shift) : per;
         uint32_t* ko = dst == 0 ? k0 : k1;
         uint32_t* vo = dst == 0 ? v0 : v1;
-        hipLaunchKernelGGL(radix_upsweep, dim3(nb), dim3(kB), 0, s, kin, cap, n_dev, shift, bits, nb, hist);
-        hipLaunchKernelGGL(radix_colscan, dim3(256), dim3(kB), 0, s, hist, nb, totals);
-        hipLaunchKernelGGL(radix_downsweep, dim3(nb), dim3(kB), 0, s, kin, vin, ko, vo, cap, n_dev, shift, bits, nb,
-                           hist, totals);
+        if (radix_tile_for(cap) == kRadixTile) {
+            hipLaunchKernelGGL(radix_upsweep<kRadixItems>, dim3(nb), dim3(kB), 0, s, kin, cap, n_dev, shift, bits, nb,
+                               hist);
+            hipLaunchKernelGGL(radix_colscan, dim3(256), dim3(kB), 0, s, hist, nb, totals);
+            hipLaunchKernelGGL(radix_downsweep<kRadixItems>, dim3(nb), dim3(kB), 0, s, kin, vin, ko, vo, cap, n_dev,
+                               shift, bits, nb, hist, totals);
+        } else {
+            hipLaunchKernelGGL(radix_upsweep<kRadixItemsSmall>, dim3(nb), dim3(kB), 0, s, kin, cap, n_dev, shift, bits,
+                               nb, hist);
+            hipLaunchKernelGGL(radix_colscan, dim3(256), dim3(kB), 0, s, hist, nb, totals);
+            hipLaunchKernelGGL(radix_downsweep<kRadixItemsSmall>, dim3(nb), dim3(kB), 0, s, kin, vin, ko, vo, cap,
+                               n_dev, shift, bits, nb, hist, totals);
+        }
         kin = ko;
         vin = vo;
         *which = dst;
