@@ -111,17 +111,25 @@ __global__ __launch_bounds__(kB) void radix_upsweep(const uint32_t* __restrict__
 }
 
 // ---- column scan: block d turns hist[d*nb .. +nb) into an exclusive scan; totals[d] ----
+// Four consecutive counts per thread per round (1024 per block round: 8 rounds for the 7936
+// blocks of a 5M / 1080p tile sort instead of 31).
+constexpr int kColQ = 4;
 __global__ __launch_bounds__(kB) void radix_colscan(uint32_t* __restrict__ hist, int nb,
                                                     uint32_t* __restrict__ totals) {
     __shared__ uint32_t wsum[kWaves];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     uint32_t* col = hist + (size_t)blockIdx.x * nb;
     uint32_t carry = 0;
-    for (int base = 0; base < nb; base += kB) {
-        const int i = base + tid;
-        const uint32_t v = i < nb ? col[i] : 0u;
-        // inclusive wave scan
-        uint32_t x = v;
+    for (int base = 0; base < nb; base += kB * kColQ) {
+        const int i0 = base + tid * kColQ;
+        uint32_t v[kColQ], sv = 0;
+#pragma unroll
+        for (int q = 0; q < kColQ; ++q) {
+            v[q] = i0 + q < nb ? col[i0 + q] : 0u;
+            sv += v[q];
+        }
+        // inclusive wave scan of the per-thread sums
+        uint32_t x = sv;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t y = __shfl_up(x, o, 64);
@@ -132,7 +140,12 @@ __global__ __launch_bounds__(kB) void radix_colscan(uint32_t* __restrict__ hist,
         uint32_t pre = 0;
 #pragma unroll
         for (int k = 0; k < kWaves; ++k) pre += (k < w) ? wsum[k] : 0u;
-        if (i < nb) col[i] = carry + pre + x - v;
+        uint32_t run = carry + pre + x - sv;
+#pragma unroll
+        for (int q = 0; q < kColQ; ++q) {
+            if (i0 + q < nb) col[i0 + q] = run;
+            run += v[q];
+        }
         uint32_t tot = 0;
 #pragma unroll
         for (int k = 0; k < kWaves; ++k) tot += wsum[k];
