@@ -38,7 +38,10 @@ HIP_SOURCES = {
     # multi-GPU splat pack / unpack / gradient sum (copies and integer work)
     "gsr_shard.hip": [],
     "gsr_api.cpp": [],
+    # RCCL transport of the multi-GPU step (include/gsr/gsr_comm.h)
+    "gsr_comm.cpp": [],
 }
+LINK_LIBS = ["-lrccl"]
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fno-fast-math",
           "-Wall", "-Wno-unused-function", "-I" + os.path.join(ROOT, "include")]
 
@@ -59,7 +62,7 @@ def _stamp(paths, extra=""):
 
 
 def _headers():
-    out = [os.path.join(ROOT, "include", "gsr", h) for h in ("gsr.h", "gsr_train.h")]
+    out = [os.path.join(ROOT, "include", "gsr", h) for h in ("gsr.h", "gsr_train.h", "gsr_comm.h")]
     out += [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     return out
 
@@ -89,7 +92,7 @@ def build_hip(verbose: bool = False, force: bool = False) -> str:
 
     with cf.ThreadPoolExecutor(max_workers=min(8, len(HIP_SOURCES))) as ex:
         objs = list(ex.map(compile_one, HIP_SOURCES))
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", so] + objs
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", so] + objs + LINK_LIBS
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
@@ -112,7 +115,7 @@ def build_torch_ext(verbose: bool = False, force: bool = False) -> str:
 
     os.makedirs(LIB, exist_ok=True)
     out = os.path.join(LIB, torch_ext_name())
-    src = os.path.join(CSRC, "torch", "gsr_torch.cpp")
+    srcs = [os.path.join(CSRC, "torch", f) for f in ("gsr_torch.cpp", "gsr_shard.cpp")]
     tinc = cpp_extension.include_paths()
     flags = ["-O2", "-std=c++17", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__=1",
              "-DTORCH_EXTENSION_NAME=_gsr_torch", "-DTORCH_API_INCLUDE_EXTENSION_H",
@@ -122,12 +125,12 @@ def build_torch_ext(verbose: bool = False, force: bool = False) -> str:
     tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
     libs = ["-L" + LIB, "-lgsr_hip", "-Wl,-rpath,$ORIGIN", "-L" + tlib, "-lc10", "-ltorch",
             "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-Wl,-rpath," + tlib]
-    stamp = _stamp([src] + _headers(), " ".join(flags))
+    stamp = _stamp(srcs + _headers() + EXE_HEADERS, " ".join(flags))
     stamp_file = out + ".stamp"
     if not force and os.path.exists(out) and os.path.exists(stamp_file) and open(stamp_file).read() == stamp:
         return out
     cxx = shutil.which("g++") or "c++"
-    cmd = [cxx] + flags + [src, "-o", out] + libs
+    cmd = [cxx] + flags + ["-I" + os.path.join(CSRC, "torch")] + srcs + ["-o", out] + libs
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"torch extension build failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
@@ -136,24 +139,28 @@ def build_torch_ext(verbose: bool = False, force: bool = False) -> str:
     return out
 
 
-def build_variant(name: str, defines: list, verbose: bool = False) -> str:
+def build_variant(name: str, defines: list, verbose: bool = False, csrc: str | None = None) -> str:
     """An experimental build of libgsr_hip.so with extra -D flags into lib/variants/<name>/ (for
-    A/B timing with `bench.py --lib`; the product library is build_hip's)."""
+    A/B timing with `bench.py --lib`; the product library is build_hip's).  `csrc`: build from
+    another copy of the kernel sources (e.g. an earlier commit's, for a before / after A/B)."""
+    src_dir = csrc or CSRC
     out_dir = os.path.join(LIB, "variants", name)
     os.makedirs(out_dir, exist_ok=True)
     so = os.path.join(out_dir, "libgsr_hip.so")
     hipcc = _hipcc()
     objs = []
     for src_name, flags in HIP_SOURCES.items():
+        if not os.path.exists(os.path.join(src_dir, src_name)):  # an older commit's sources
+            continue
         obj = os.path.join(out_dir, src_name + ".o")
         lang = ["-x", "hip"] if src_name.endswith(".cpp") else []
-        cmd = [hipcc] + COMMON + flags + ["-D" + d for d in defines] + lang + ["-c", os.path.join(CSRC, src_name),
-                                                                              "-o", obj]
+        cmd = [hipcc] + COMMON + flags + ["-D" + d for d in defines] + lang + ["-I" + src_dir, "-c",
+                                                                              os.path.join(src_dir, src_name), "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src_name}:\n{r.stderr}")
         objs.append(obj)
-    r = subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", so] + objs,
+    r = subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", so] + objs + LINK_LIBS,
                        capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")
@@ -178,6 +185,7 @@ def _exe_flags():
     # first and libgsr_hip's request is then satisfied by soname with that same copy.  With
     # libgsr_hip first, /opt/rocm's runtime is loaded as a second one (two HIP and HSA runtimes,
     # torch's streams handed to the other, a double free at exit).
+    # RCCL: the wheel's own librccl.so (the one libtorch_hip loads), so the process has one RCCL
     libs = ["-L" + tlib, "-Wl,--no-as-needed", "-ltorch_hip", "-lc10_hip",
             "-Wl,--as-needed", "-ltorch", "-ltorch_cpu", "-lc10", "-L" + LIB, "-lgsr_hip",
             "-Wl,-rpath," + tlib, "-Wl,-rpath,$ORIGIN"]
@@ -185,8 +193,8 @@ def _exe_flags():
 
 
 # the libtorch layer shared by the C++ executables (compiled once, -DGSR_NO_PYBIND)
-EXE_LIB_SOURCES = [os.path.join(CSRC, "torch", "gsr_torch.cpp"), os.path.join(CSRC, "torch", "gsr_trainer.cpp")]
-EXE_HEADERS = [os.path.join(CSRC, "torch", h) for h in ("gsr_render.h", "gsr_trainer.h")]
+EXE_LIB_SOURCES = [os.path.join(CSRC, "torch", f) for f in ("gsr_torch.cpp", "gsr_trainer.cpp", "gsr_shard.cpp")]
+EXE_HEADERS = [os.path.join(CSRC, "torch", h) for h in ("gsr_render.h", "gsr_trainer.h", "gsr_shard.h")]
 
 
 def _compile_exe_objs(flags, force: bool) -> list:
@@ -243,11 +251,18 @@ def build_train_loop(verbose: bool = False, force: bool = False) -> str:
     return _build_exe("gsr_train_loop", os.path.join(ROOT, "tests", "cpp", "train_main.cpp"), force)
 
 
+def build_shard_step(verbose: bool = False, force: bool = False) -> str:
+    """tests/cpp/shard_main.cpp + the libtorch layer into lib/gsr_shard_step: one rank of the
+    C++ multi-GPU step (gsr::ShardStep over RCCL or a store exchange; tests/test_gpu_shard_cpp.py)."""
+    return _build_exe("gsr_shard_step", os.path.join(ROOT, "tests", "cpp", "shard_main.cpp"), force)
+
+
 def build_all(verbose: bool = False, force: bool = False):
     so = build_hip(verbose, force)
     ext = build_torch_ext(verbose, force)
     build_dropin(verbose, force)
     build_train_loop(verbose, force)
+    build_shard_step(verbose, force)
     return so, ext
 
 

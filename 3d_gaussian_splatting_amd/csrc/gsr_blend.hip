@@ -376,16 +376,20 @@ constexpr int kPark = 4;
 // x 9 moments) read 36 distinct banks -- at 192 the 4 slots alias (4-way LDS bank conflicts,
 // ~1 conflict cycle per LDS instruction of B1 in the PMC pass).
 constexpr int kParkSlot = 16 * 12 + 12;
-__device__ __forceinline__ void park_flush(const float* qpark, const uint32_t* qjl, int parked, float* p8f,
-                                           float* p1, uint8_t* fl, int lane) {
+// The parked records' batch indices ride in one scalar word (6 bits per slot: `kpack`); the
+// flush lane of slot s reads its record's emission index from the batch's jl table (`sjl`,
+// written once per batch), so a record costs no per-record readlane / LDS write for it.
+__device__ __forceinline__ void park_flush(const float* qpark, const uint32_t* sjl, uint32_t kpack, int parked,
+                                           float* p8f, float* p1, uint8_t* fl, int lane) {
     __syncthreads();  // one-wave block: orders the quad leaders' LDS writes before the reads
     if (lane < parked * 9) {
         const int slot = lane / 9, c = lane - 9 * slot;
         const float* q = qpark + slot * kParkSlot + c;
-        float t[4] = {0.f, 0.f, 0.f, 0.f};
+        // -0 is the identity of IEEE addition, so the first add of each chain folds into a move
+        float t[4] = {-0.f, -0.f, -0.f, -0.f};
 #pragma unroll
         for (int i = 0; i < 16; ++i) t[i & 3] += q[i * 12];
-        const uint32_t j = qjl[slot];
+        const uint32_t j = sjl[(kpack >> (6 * slot)) & 63u];
         float* dst = c < 8 ? p8f + 8 * (size_t)j + c : p1 + j;
         *dst = (t[0] + t[1]) + (t[2] + t[3]);
         if (c == 8) fl[j] = 1;  // the gather reads flagged entries only
@@ -428,9 +432,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                                                             uint8_t* __restrict__ fl,
                                                             const uint32_t* __restrict__ term,
                                                             const float4* __restrict__ ck) {
-    __shared__ float4 srec[64 * 3];
-    __shared__ float qpark[kPark * kParkSlot];  // [slot][quad][9 of 12]
-    __shared__ uint32_t qjl[kPark];
+    // One block of LDS with srec first: the record fields then sit within the immediate offsets
+    // of the record reads (8-bit dword offsets of ds_read2), so a record costs no address add.
+    __shared__ struct {
+        float4 srec[64 * 3];
+        uint32_t sjl[64];                  // the batch's emission indices, by batch slot
+        float qpark[kPark * kParkSlot];    // [slot][quad][9 of 12]
+    } lds;
+    float4* const srec = lds.srec;
+    uint32_t* const sjl = lds.sjl;
+    float* const qpark = lds.qpark;
     const int lane = threadIdx.x;
     float* const qlane = qpark + (lane >> 2) * 12;  // this quad's parking row
     int tl, chunk;
@@ -522,9 +533,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                 smask = stripe_mask(r0, r1, r2, bx0, by0);
             }
         }
+        sjl[lane] = jl;
         __syncthreads();
         uint64_t todo = __ballot((smask & live) != 0u);
         int visited = 0, parked = 0;
+        uint32_t kpack = 0;  // batch slots of the parked records, 6 bits each
         while (todo) {
             const int k = __builtin_ctzll(todo);
             todo &= todo - 1;
@@ -581,10 +594,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                     *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
                     dst[8] = v[8];
                 }
-                if (lane == 0) qjl[parked] = (uint32_t)__builtin_amdgcn_readlane((int)jl, k);
+                kpack |= (uint32_t)k << (6 * parked);
                 if (++parked == kPark) {
-                    park_flush(qpark, qjl, parked, p8f, p1, fl, lane);
+                    park_flush(qpark, sjl, kpack, parked, p8f, p1, fl, lane);
                     parked = 0;
+                    kpack = 0;
                 }
             }
             if ((++visited & 7) == 0) {
@@ -595,7 +609,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                 if (live == 0) break;
             }
         }
-        if (parked) park_flush(qpark, qjl, parked, p8f, p1, fl, lane);
+        if (parked) park_flush(qpark, sjl, kpack, parked, p8f, p1, fl, lane);
         __syncthreads();  // srec / qpark are rewritten by the next batch
     }
 }

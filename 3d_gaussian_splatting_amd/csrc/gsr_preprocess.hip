@@ -293,8 +293,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void p
     const int col = threadIdx.x & 15, r0 = threadIdx.x >> 4;
     const size_t base = (size_t)blockIdx.x * 256 * M3;
     const int nb = (in.D + 1) * (in.D + 1);
-    // Buffer loads over the block's rows: one 32-bit lane offset, the row step in the scalar
-    // offset, and the descriptor's range check zero-fills rows past the end of the array.
+    // Buffer loads over the block's rows: the whole byte offset goes in the 32-bit lane offset
+    // (a raw buffer's range check covers voffset + inst_offset, never soffset), so the
+    // descriptor's range check zero-fills rows past the end of the array.
     float pre[16];
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in.sh_rest + base), 0,
                                                         rows * M3 * (int)sizeof(float), 0x00020000);
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void p
 #pragma unroll
         for (int j = 0; j < 16; ++j)
             pre[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                   rsrc, voff, j * 16 * M3 * (int)sizeof(float), 0));
+                                                   rsrc, voff + j * 16 * M3 * (int)sizeof(float), 0, 0));
     };
     // kShWave: this wave's rows [64 w, 64 w + 64) of the block, staged kSubRows at a time
     const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
@@ -326,7 +327,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void p
         }
     };
     // kShGlds: wave wv's LDS region (gq KB); the q-th DMA moves bytes [1024 q, 1024 q + 1024) of its
-    // span.  Issued before the parameter loads: loads return in order, so one wait covers both
+    // span, addressed by voffset alone so that pieces past the block's rows are range-checked
+    // (zero-filled, never read).  Issued before the parameter loads: loads return in order, so
+    // one wait covers both
     const int gq = (64 * M3 * 4 + 1023) / 1024;
     if (SH == kShGlds && sh) {
         const int wu = __builtin_amdgcn_readfirstlane(wv);
@@ -335,7 +338,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void p
 #pragma unroll
         for (int q = 0; q < 12; ++q)
             if (q < gq)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(wsrc, dst + 1024 * q, 16, ln * 16, wbase + 1024 * q, 0, 0);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(wsrc, dst + 1024 * q, 16, ln * 16 + wbase + 1024 * q, 0, 0, 0);
     }
     Params I{};
     if (g < in.P) I = load_params(in, g);

@@ -438,8 +438,8 @@ __global__ __launch_bounds__(256) void preprocess_backward_kernel(
                                      reinterpret_cast<uintptr_t>(out.sh_rest + obase)) & 15u) == 0;
     // Aligned rows are staged by buffer-load-to-LDS DMA: the block's 256 * M3 floats are M3 pieces
     // of 1 KB (64 lanes x 16 B), piece q by wave q % 4, all issued before the per-Gaussian inputs
-    // (loads return in order: one wait covers both); the descriptor's range check zero-fills
-    // the rows past n.
+    // (loads return in order: one wait covers both); the piece offset is in voffset, which the
+    // descriptor's range check covers (soffset is not checked), so the rows past n zero-fill.
     if (stage && v4) {
         const auto src = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in.sh_rest + ibase), 0,
                                                            rows * M3 * (int)sizeof(float), 0x00020000);
@@ -448,7 +448,7 @@ __global__ __launch_bounds__(256) void preprocess_backward_kernel(
 #pragma unroll
         for (int j = 0; j < 12; ++j) {  // M3 <= 45 pieces: <= 12 per wave
             const int q = 4 * j + wu;
-            if (q < M3) __builtin_amdgcn_raw_ptr_buffer_load_lds(src, dst + 1024 * q, 16, ln * 16, 1024 * q, 0, 0);
+            if (q < M3) __builtin_amdgcn_raw_ptr_buffer_load_lds(src, dst + 1024 * q, 16, ln * 16 + 1024 * q, 0, 0, 0);
         }
     }
     BwdIn bi{};

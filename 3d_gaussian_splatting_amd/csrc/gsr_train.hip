@@ -300,7 +300,17 @@ struct AdamArgs {
     float bc2_sqrt[GSR_ADAM_MAX_GROUPS];   // sqrt(1 - beta2^step)
     int ngroups;
     float b1, b2, eps, omb1, omb2;          // omb = 1 - beta (rounded once, as libtorch's alpha)
+    const uint32_t* guard_k;                // skip the whole step when *guard_k > guard_cap
+    uint32_t guard_cap;
 };
+
+// The device-side step guard: a render under a binning bound whose true instance count K (the
+// scan's device counter) exceeded the bound was truncated; the optimizer step / statistics of
+// that iteration are then dropped here, on the device, with no host wait (the host learns of
+// the overflow one iteration later from its pinned copy and re-sizes).
+__device__ __forceinline__ bool guard_tripped(const uint32_t* k, uint32_t cap) {
+    return k != nullptr && *k > cap;  // written by an earlier kernel of the stream
+}
 constexpr int kAdamBlock = 256, kAdamPerBlock = 4 * kAdamBlock;
 
 __device__ __forceinline__ float adam_one(float& p, float g, float& m, float& v, float ss, float b2s, const AdamArgs& a) {
@@ -312,6 +322,7 @@ __device__ __forceinline__ float adam_one(float& p, float g, float& m, float& v,
 }
 
 __global__ __launch_bounds__(kAdamBlock) void adam_kernel(const AdamArgs a) {
+    if (guard_tripped(a.guard_k, a.guard_cap)) return;
     int gi = 0;
     while (gi + 1 < a.ngroups && (int)blockIdx.x >= a.blk_start[gi + 1]) ++gi;  // wave-uniform
     const gsr_adam_group& G = a.g[gi];
@@ -376,9 +387,10 @@ __global__ __launch_bounds__(kAdamBlock) void adam_kernel(const AdamArgs a) {
 // ---------------------------------------------------------------- densification statistics
 __global__ __launch_bounds__(256) void densify_stats_kernel(const int* __restrict__ radii, const float* __restrict__ dm2,
                                                             int P, float* __restrict__ maxr, float* __restrict__ acc,
-                                                            float* __restrict__ den) {
+                                                            float* __restrict__ den, const uint32_t* guard_k,
+                                                            uint32_t guard_cap) {
     const int g = blockIdx.x * 256 + threadIdx.x;
-    if (g >= P) return;
+    if (g >= P || guard_tripped(guard_k, guard_cap)) return;
     const int r = radii[g];
     if (r <= 0) return;
     maxr[g] = fmaxf(maxr[g], (float)r);
@@ -547,6 +559,11 @@ int gsr_loss_backward(const float* img, const float* gt, int32_t C, int32_t H, i
 }
 
 int gsr_adam_step(const gsr_adam_group* groups, int32_t ngroups, float beta1, float beta2, float eps, void* stream) {
+    return gsr_adam_step_guarded(groups, ngroups, beta1, beta2, eps, nullptr, 0, stream);
+}
+
+int gsr_adam_step_guarded(const gsr_adam_group* groups, int32_t ngroups, float beta1, float beta2, float eps,
+                          const uint32_t* guard_k, uint32_t guard_cap, void* stream) {
     if (ngroups < 0 || ngroups > GSR_ADAM_MAX_GROUPS) return set_error(-1, "adam: 0..8 groups");
     if (ngroups == 0) return 0;
     if (!groups) return set_error(-1, "adam: null groups");
@@ -558,6 +575,8 @@ int gsr_adam_step(const gsr_adam_group* groups, int32_t ngroups, float beta1, fl
     a.eps = eps;
     a.omb1 = (float)(1.0 - (double)beta1);
     a.omb2 = (float)(1.0 - (double)beta2);
+    a.guard_k = guard_k;
+    a.guard_cap = guard_cap;
     long long blocks = 0;
     for (int i = 0; i < ngroups; ++i) {
         const gsr_adam_group& g = groups[i];
@@ -586,11 +605,17 @@ int gsr_adam_step(const gsr_adam_group* groups, int32_t ngroups, float beta1, fl
 
 int gsr_densify_stats(const int32_t* radii, const float* dmeans2D, int32_t P, float* max_radii2D, float* grad_accum,
                       float* denom, void* stream) {
+    return gsr_densify_stats_guarded(radii, dmeans2D, P, max_radii2D, grad_accum, denom, nullptr, 0, stream);
+}
+
+int gsr_densify_stats_guarded(const int32_t* radii, const float* dmeans2D, int32_t P, float* max_radii2D,
+                              float* grad_accum, float* denom, const uint32_t* guard_k, uint32_t guard_cap,
+                              void* stream) {
     if (P < 0) return set_error(-1, "densify_stats: negative P");
     if (P == 0) return 0;
     if (!radii || !dmeans2D || !max_radii2D || !grad_accum || !denom) return set_error(-1, "densify_stats: null tensor");
     hipLaunchKernelGGL(densify_stats_kernel, dim3((P + 255) / 256), dim3(256), 0, (hipStream_t)stream, radii, dmeans2D, P,
-                       max_radii2D, grad_accum, denom);
+                       max_radii2D, grad_accum, denom, guard_k, guard_cap);
     return (int)hipGetLastError();
 }
 

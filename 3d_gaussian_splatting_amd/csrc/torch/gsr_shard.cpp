@@ -1,0 +1,678 @@
+// gsr_shard.cpp -- the multi-GPU step in C++ over RCCL (see gsr_shard.h).
+#include "gsr_shard.h"
+
+#include <ATen/hip/HIPGraph.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <c10/core/Event.h>
+#include <c10/core/StreamGuard.h>
+#include <torch/csrc/distributed/c10d/Store.hpp>
+
+#include "gsr/gsr_comm.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <thread>
+
+namespace gsr {
+namespace {
+
+int64_t round_up(int64_t x, int64_t m = 256) { return (x + m - 1) / m * m; }
+
+using Stream = c10::hip::HIPStreamMasqueradingAsCUDA;
+// c10's device-generic guard and events (they dispatch through the registered HIP guard
+// implementation): this file then references no HIP runtime symbol itself, so an executable
+// linking it keeps libtorch's one HIP runtime (tests/test_native_abi.py).
+using StreamGuard = c10::StreamGuard;
+
+Stream current_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(); }
+// a device tensor over raw device memory (no ownership)
+torch::Tensor dev_view(void* p, int64_t n, torch::ScalarType t) {
+    return torch::from_blob(p, {n}, torch::TensorOptions().dtype(t).device(torch::kCUDA, c10::hip::current_device()));
+}
+
+// ---- RCCL exchange: the C ABI of libgsr_hip.so (include/gsr/gsr_comm.h) ----
+class RcclExchange final : public Exchange {
+   public:
+    RcclExchange(const std::vector<uint8_t>& id, int rank, int world) : rank_(rank), world_(world) {
+        if (id.size() != GSR_COMM_ID_BYTES) throw std::invalid_argument("rccl: bad unique id size");
+        detail::check(gsr_comm_init(&comm_, id.data(), world, rank), "gsr_comm_init");
+    }
+    ~RcclExchange() override { (void)gsr_comm_destroy(comm_); }
+    int rank() const override { return rank_; }
+    int world() const override { return world_; }
+    bool capturable() const override { return true; }
+    const char* name() const override { return "rccl"; }
+    void all_to_all(const void* send, void* recv, size_t bb, hipStream_t s) override {
+        detail::check(gsr_comm_all_to_all(comm_, send, recv, bb, s), "gsr_comm_all_to_all");
+    }
+    void all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+        detail::check(gsr_comm_all_gather(comm_, send, recv, bytes, s), "gsr_comm_all_gather");
+    }
+    void all_reduce_i64(int64_t* buf, size_t n, bool max, hipStream_t s) override {
+        detail::check(gsr_comm_all_reduce_i64(comm_, buf, n, max ? 1 : 0, s), "gsr_comm_all_reduce_i64");
+    }
+
+   private:
+    int rank_, world_;
+    gsr_comm* comm_ = nullptr;
+};
+
+// ---- host-staged exchange through a c10d::Store (ranks sharing one GPU) ----
+class StoreExchange final : public Exchange {
+   public:
+    StoreExchange(std::shared_ptr<c10d::Store> store, int rank, int world)
+        : store_(std::move(store)), rank_(rank), world_(world) {}
+    int rank() const override { return rank_; }
+    int world() const override { return world_; }
+    bool capturable() const override { return false; }
+    const char* name() const override { return "store"; }
+    void all_to_all(const void* send, void* recv, size_t bb, hipStream_t s) override {
+        const std::string tag = "gsr/a2a/" + std::to_string(seq_++) + "/";
+        std::vector<uint8_t> h((size_t)world_ * bb);
+        d2h(h.data(), send, h.size(), s);
+        for (int p = 0; p < world_; ++p)
+            store_->set(tag + std::to_string(rank_) + ">" + std::to_string(p),
+                        std::vector<uint8_t>(h.begin() + (size_t)p * bb, h.begin() + (size_t)(p + 1) * bb));
+        for (int p = 0; p < world_; ++p) {
+            const std::string key = tag + std::to_string(p) + ">" + std::to_string(rank_);
+            auto v = store_->get(key);
+            if (v.size() != bb) throw std::runtime_error("store exchange: block size mismatch");
+            std::memcpy(h.data() + (size_t)p * bb, v.data(), bb);
+            store_->deleteKey(key);
+        }
+        h2d(recv, h.data(), h.size(), s);
+    }
+    void all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+        const std::string tag = "gsr/ag/" + std::to_string(seq_++) + "/";
+        std::vector<uint8_t> h(bytes);
+        d2h(h.data(), send, bytes, s);
+        store_->set(tag + std::to_string(rank_), h);
+        std::vector<uint8_t> all((size_t)world_ * bytes);
+        for (int p = 0; p < world_; ++p) {
+            auto v = store_->get(tag + std::to_string(p));
+            std::memcpy(all.data() + (size_t)p * bytes, v.data(), bytes);
+        }
+        barrier(tag);
+        if (rank_ == 0)
+            for (int p = 0; p < world_; ++p) store_->deleteKey(tag + std::to_string(p));
+        h2d(recv, all.data(), all.size(), s);
+    }
+    void all_reduce_i64(int64_t* buf, size_t n, bool max, hipStream_t s) override {
+        std::vector<int64_t> mine(n), acc(n);
+        all_gather_host(mine, buf, n, s, acc, max);
+        h2d(buf, acc.data(), n * sizeof(int64_t), s);
+    }
+
+   private:
+    void all_gather_host(std::vector<int64_t>& mine, const int64_t* dev, size_t n, hipStream_t s,
+                         std::vector<int64_t>& acc, bool max) {
+        d2h(mine.data(), dev, n * sizeof(int64_t), s);
+        const std::string tag = "gsr/ar/" + std::to_string(seq_++) + "/";
+        std::vector<uint8_t> b(n * sizeof(int64_t));
+        std::memcpy(b.data(), mine.data(), b.size());
+        store_->set(tag + std::to_string(rank_), b);
+        for (int p = 0; p < world_; ++p) {
+            auto v = store_->get(tag + std::to_string(p));
+            const int64_t* x = reinterpret_cast<const int64_t*>(v.data());
+            for (size_t i = 0; i < n; ++i) acc[i] = p == 0 ? x[i] : (max ? std::max(acc[i], x[i]) : acc[i] + x[i]);
+        }
+        barrier(tag);
+    }
+    void barrier(const std::string& tag) {
+        store_->add(tag + "done", 1);
+        while (store_->add(tag + "done", 0) < world_) std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    // synchronous copies on the caller's current stream (the step runs with it set to its own)
+    static void d2h(void* h, const void* d, size_t n, hipStream_t) {
+        auto src = dev_view(const_cast<void*>(d), (int64_t)n, torch::kUInt8);
+        torch::from_blob(h, {(int64_t)n}, torch::kUInt8).copy_(src);
+    }
+    static void h2d(void* d, const void* h, size_t n, hipStream_t) {
+        dev_view(d, (int64_t)n, torch::kUInt8).copy_(torch::from_blob(const_cast<void*>(h), {(int64_t)n}, torch::kUInt8));
+        current_stream().unwrap().synchronize();  // h is a host buffer of this call
+    }
+    std::shared_ptr<c10d::Store> store_;
+    int rank_, world_;
+    int64_t seq_ = 0;
+};
+
+// Fixed-address arena behind one gsr_alloc_fn role: the i-th request of a step gets slot i,
+// grown only when a request is larger (never during a captured step: capacities are fixed).
+struct Arena {
+    torch::Device dev;
+    std::vector<torch::Tensor> slots;
+    size_t next = 0;
+    bool frozen = false;
+    static void* cb(void* ctx, size_t bytes) {
+        auto* a = static_cast<Arena*>(ctx);
+        const size_t i = a->next++;
+        if (i == a->slots.size()) {
+            if (a->frozen) return nullptr;
+            a->slots.push_back(torch::empty({(int64_t)std::max<size_t>(bytes, 16)},
+                                            torch::TensorOptions().dtype(torch::kUInt8).device(a->dev)));
+        } else if ((size_t)a->slots[i].numel() < bytes) {
+            if (a->frozen) return nullptr;
+            a->slots[i] = torch::empty({(int64_t)bytes}, torch::TensorOptions().dtype(torch::kUInt8).device(a->dev));
+        }
+        return a->slots[i].data_ptr();
+    }
+};
+
+}  // namespace
+
+std::vector<uint8_t> rccl_unique_id() {
+    std::vector<uint8_t> out(GSR_COMM_ID_BYTES);
+    detail::check(gsr_comm_unique_id(out.data()), "gsr_comm_unique_id");
+    return out;
+}
+
+std::unique_ptr<Exchange> rccl_exchange(const std::vector<uint8_t>& unique_id, int rank, int world) {
+    return std::make_unique<RcclExchange>(unique_id, rank, world);
+}
+
+std::unique_ptr<Exchange> rccl_exchange(c10d::Store& store, int rank, int world) {
+    std::vector<uint8_t> id;
+    if (rank == 0) {
+        id = rccl_unique_id();
+        store.set("gsr/rccl_id", id);
+    } else {
+        id = store.get("gsr/rccl_id");
+    }
+    return rccl_exchange(id, rank, world);
+}
+
+std::unique_ptr<Exchange> store_exchange(std::shared_ptr<c10d::Store> store, int rank, int world) {
+    return std::make_unique<StoreExchange>(std::move(store), rank, world);
+}
+
+// ---- partition: the same arithmetic as bands.py ----
+std::pair<int64_t, int64_t> gaussian_shard(int64_t P, int world, int rank) {
+    const int64_t S = (P + world - 1) / world;
+    return {std::min<int64_t>(rank * S, P), std::min<int64_t>((int64_t)(rank + 1) * S, P)};
+}
+
+std::vector<int> equal_bands(int grid_y, int world) {
+    std::vector<int> r(world + 1);
+    for (int i = 0; i <= world; ++i) r[i] = (int)((int64_t)i * grid_y / world);
+    return r;
+}
+
+std::vector<int> balance_bands(const std::vector<int64_t>& c, int world) {
+    const int gy = (int)c.size();
+    if (world > gy) throw std::invalid_argument("balance_bands: more bands than tile rows");
+    std::vector<double> pre(gy + 1, 0.0);
+    for (int i = 0; i < gy; ++i) pre[i + 1] = pre[i] + (double)c[i];
+    const double total = pre[gy];
+    if (total <= 0) return equal_bands(gy, world);
+    std::vector<int> rows{0};
+    for (int k = 1; k < world; ++k) {
+        const double t = k * total / world;
+        int y = 0;
+        double best = std::fabs(pre[0] - t);
+        for (int i = 1; i <= gy; ++i)  // first index of the minimum, as numpy.argmin
+            if (std::fabs(pre[i] - t) < best) best = std::fabs(pre[i] - t), y = i;
+        y = std::max(y, rows.back() + 1);
+        y = std::min(y, gy - (world - k));
+        rows.push_back(y);
+    }
+    rows.push_back(gy);
+    return rows;
+}
+
+ShardOverflowError::ShardOverflowError(int64_t step_, int rank_, std::vector<int64_t> counts_, int pair_cap_,
+                                       int64_t band_k_, int capacity_)
+    : std::overflow_error([&] {
+          std::string s = "multi-GPU step " + std::to_string(step_) + " overflowed on rank " + std::to_string(rank_) +
+                          ": splats per band [";
+          for (size_t i = 0; i < counts_.size(); ++i) s += (i ? ", " : "") + std::to_string(counts_[i]);
+          return s + "] vs pair_cap " + std::to_string(pair_cap_) + ", band instances " + std::to_string(band_k_) +
+                 " vs capacity " + std::to_string(capacity_);
+      }()),
+      step(step_), rank(rank_), counts(std::move(counts_)), pair_cap(pair_cap_), band_k(band_k_),
+      capacity(capacity_) {}
+
+// ---- the step ----
+// gsr_band_forward takes one ctx for its three allocation roles: ctx = the Pool, one callback
+// per role.  Streams, events and the captured graph are libtorch's (no HIP runtime call here).
+struct ShardStep::Pool {
+    torch::Device dev;
+    torch::Tensor send, recv, state, radii, color, g2, back, mine, gathered, image;
+    std::map<std::string, torch::Tensor> grads;
+    gsr_grads gg{};
+    Arena geom{dev}, bin{dev}, img{dev}, scratch{dev};
+    gsr_buffers bufs{};
+    size_t block_bytes = 0, grad_block = 0, mine_floats = 0, status_off = 0;
+    int tall = 0;
+    Stream main, side;  // the step's stream (capturable) and the all-gather's
+    c10::Event enter{c10::DeviceType::CUDA}, leave{c10::DeviceType::CUDA}, fork{c10::DeviceType::CUDA},
+        join{c10::DeviceType::CUDA};
+    std::vector<torch::Tensor> ring;  // pinned (world x kStatusWords) int32 per slot
+    std::vector<std::unique_ptr<c10::Event>> ring_ev;
+    std::unique_ptr<at::cuda::CUDAGraph> graph;
+    const void* graph_dpix = nullptr;
+    explicit Pool(torch::Device d)
+        : dev(d),
+          main(c10::hip::getStreamFromPoolMasqueradingAsCUDA(false, d.index())),
+          side(c10::hip::getStreamFromPoolMasqueradingAsCUDA(false, d.index())) {}
+    static void* geom_cb(void* c, size_t n) { return Arena::cb(&static_cast<Pool*>(c)->geom, n); }
+    static void* bin_cb(void* c, size_t n) { return Arena::cb(&static_cast<Pool*>(c)->bin, n); }
+    static void* img_cb(void* c, size_t n) { return Arena::cb(&static_cast<Pool*>(c)->img, n); }
+};
+
+static constexpr int kStatusWords = 16;  // per rank: nb header counts, band K (nb <= 15)
+
+ShardStep::ShardStep(Exchange& ex, const RasterCamera& cam, const ShardInputs& in, std::array<float, 3> bg,
+                     double headroom, bool graph, int lag)
+    : ex_(ex), cam_(cam), ccam_(cam.to_c()), in_(in), bg_(bg), headroom_(headroom),
+      graph_(graph && ex.capturable()), lag_(std::max(lag, 1)), world_(ex.world()), rank_(ex.rank()) {
+    TORCH_CHECK(in.means3D.defined() && in.means3D.is_cuda(), "ShardStep: means3D must be a device tensor");
+    TORCH_CHECK(world_ >= 1 && world_ < kStatusWords, "ShardStep: 1..15 ranks");
+    P_ = in.means3D.size(0);
+    std::tie(g0_, g1_) = gaussian_shard(P_, world_, rank_);
+    grid_y_ = (cam.height + GSR_TILE - 1) / GSR_TILE;
+    TORCH_CHECK(world_ <= grid_y_, "ShardStep: more ranks than tile rows");
+    rows_ = equal_bands(grid_y_, world_);
+    pool_ = std::make_unique<Pool>(in.means3D.device());
+    for (int i = 0; i < lag_ + 2; ++i) {
+        pool_->ring.push_back(torch::empty({(int64_t)world_, kStatusWords},
+                                           torch::TensorOptions().dtype(torch::kInt32).pinned_memory(true)));
+        pool_->ring_ev.push_back(std::make_unique<c10::Event>(c10::DeviceType::CUDA));
+    }
+}
+
+ShardStep::~ShardStep() = default;
+
+bool ShardStep::graph_active() const { return pool_ && pool_->graph != nullptr; }
+
+void ShardStep::drop_graph() {
+    pool_->graph.reset();
+    pool_->graph_dpix = nullptr;
+}
+
+gsr_gaussians ShardStep::shard_struct() const {
+    gsr_gaussians g{};
+    g.P = (int32_t)(g1_ - g0_);
+    g.sh_degree = in_.sh_degree;
+    g.scale_modifier = in_.scale_modifier;
+    auto row = [&](const torch::Tensor& t) -> const float* {
+        if (!t.defined()) return nullptr;
+        TORCH_CHECK(t.is_contiguous() && t.scalar_type() == torch::kFloat32 && t.size(0) == P_,
+                    "ShardStep: inputs must be contiguous f32 with P rows");
+        return t.data_ptr<float>() + g0_ * (t.numel() / std::max<int64_t>(P_, 1));
+    };
+    g.means3D = row(in_.means3D);
+    g.sh_dc = row(in_.sh_dc);
+    g.sh_rest = in_.sh_rest.defined() && in_.sh_rest.numel() ? row(in_.sh_rest) : nullptr;
+    g.sh_rest_coeffs = g.sh_rest ? (int32_t)(in_.sh_rest.numel() / std::max<int64_t>(P_, 1) / 3) : 0;
+    g.colors_precomp = row(in_.colors_precomp);
+    g.opacities = row(in_.opacities);
+    g.scales = row(in_.scales);
+    g.rotations = row(in_.rotations);
+    g.cov3D_precomp = row(in_.cov3D_precomp);
+    return g;
+}
+
+gsr_raster_settings ShardStep::shard_settings() const {
+    gsr_raster_settings s{};
+    for (int i = 0; i < 3; ++i) s.bg[i] = bg_[i];
+    s.tile_y0 = 0;
+    s.tile_y1 = INT32_MAX;
+    return s;
+}
+
+gsr_raster_settings ShardStep::band_settings() const {
+    gsr_raster_settings s = shard_settings();
+    s.tile_y0 = rows_[rank_];
+    s.tile_y1 = rows_[rank_ + 1];
+    s.max_rendered = capacity_;
+    return s;
+}
+
+void ShardStep::size_buffers() {
+    Pool& p = *pool_;
+    drop_graph();
+    const int nb = world_;
+    const auto u8 = torch::TensorOptions().dtype(torch::kUInt8).device(p.dev);
+    const auto f32 = torch::TensorOptions().dtype(torch::kFloat32).device(p.dev);
+    const int64_t Ps = g1_ - g0_;
+    p.block_bytes = gsr_exchange_block_bytes(pair_cap_);
+    p.grad_block = (size_t)pair_cap_ * GSR_SPLAT_GRAD_BYTES;
+    p.send = torch::empty({(int64_t)(nb * p.block_bytes)}, u8);
+    p.recv = torch::empty({(int64_t)(nb * p.block_bytes)}, u8);
+    p.state = torch::empty({(int64_t)gsr_shard_state_bytes((int32_t)Ps, nb, pair_cap_)}, u8);
+    p.radii = torch::empty({Ps}, f32.dtype(torch::kInt32));
+    p.color = torch::zeros({3, cam_.height, cam_.width}, f32);
+    p.g2 = torch::empty({(int64_t)nb * pair_cap_, GSR_GRAD2D_STRIDE}, f32);
+    p.back = torch::empty({(int64_t)(nb * p.grad_block)}, u8);
+    int tall = 1;
+    for (int r = 0; r < world_; ++r) {
+        const int a = std::min(rows_[r] * GSR_TILE, cam_.height), b = std::min(rows_[r + 1] * GSR_TILE, cam_.height);
+        tall = std::max(tall, b - a);
+    }
+    p.tall = tall;
+    p.status_off = (size_t)3 * tall * cam_.width;
+    p.mine_floats = p.status_off + kStatusWords;
+    p.mine = torch::zeros({(int64_t)p.mine_floats}, f32);
+    p.gathered = torch::empty({(int64_t)world_, (int64_t)p.mine_floats}, f32);
+    p.image = torch::empty({3, cam_.height, cam_.width}, f32);
+    auto e = [&](std::initializer_list<int64_t> sh) { return torch::empty(sh, f32); };
+    p.grads.clear();
+    p.grads["means2D"] = e({Ps, 3});
+    p.grads["conic"] = e({Ps, 3});
+    p.grads["opacities"] = e({Ps, 1});
+    p.grads["means3D"] = e({Ps, 3});
+    if (in_.colors_precomp.defined()) {
+        p.grads["colors"] = e({Ps, 3});
+    } else {
+        p.grads["sh_dc"] = e({Ps, 1, 3});
+        const gsr_gaussians g = shard_struct();
+        if (g.sh_rest) p.grads["sh_rest"] = e({Ps, g.sh_rest_coeffs, 3});
+    }
+    if (in_.cov3D_precomp.defined()) {
+        p.grads["cov3D"] = e({Ps, 6});
+    } else {
+        p.grads["scales"] = e({Ps, 3});
+        p.grads["rotations"] = e({Ps, 4});
+    }
+    auto ptr = [&](const char* k) -> float* {
+        auto it = p.grads.find(k);
+        return it == p.grads.end() ? nullptr : it->second.data_ptr<float>();
+    };
+    p.gg = gsr_grads{};
+    p.gg.dL_dmeans2D = ptr("means2D");
+    p.gg.dL_dconic = ptr("conic");
+    p.gg.dL_dopacity = ptr("opacities");
+    p.gg.dL_dcolors = ptr("colors");
+    p.gg.dL_dmeans3D = ptr("means3D");
+    p.gg.dL_dsh_dc = ptr("sh_dc");
+    p.gg.dL_dsh_rest = ptr("sh_rest");
+    p.gg.dL_dscales = ptr("scales");
+    p.gg.dL_drotations = ptr("rotations");
+    p.gg.dL_dcov3D = ptr("cov3D");
+    for (Arena* a : {&p.geom, &p.bin, &p.img, &p.scratch}) {
+        a->slots.clear();
+        a->frozen = false;
+    }
+}
+
+void ShardStep::plan() {
+    const Stream cs = current_stream();
+    const hipStream_t s = cs.stream();
+    const gsr_gaussians g = shard_struct();
+    const gsr_raster_settings rs = shard_settings();
+    auto i32 = torch::TensorOptions().dtype(torch::kInt32).device(pool_->dev);
+    const int nb = world_;
+    rows_ = equal_bands(grid_y_, world_);
+    std::vector<int32_t> rows32(rows_.begin(), rows_.end());
+    // probe 1: the shard's per-tile-row instance histogram (pair_cap 0: headers only)
+    auto hist = torch::zeros({grid_y_}, i32);
+    auto send0 = torch::empty({(int64_t)(nb * gsr_exchange_block_bytes(0))}, i32.dtype(torch::kUInt8));
+    auto state0 = torch::empty({(int64_t)gsr_shard_state_bytes(g.P, nb, 0)}, i32.dtype(torch::kUInt8));
+    auto radii0 = torch::empty({(int64_t)std::max(g.P, 1)}, i32);
+    detail::check(gsr_shard_forward(&ccam_, &g, &rs, nb, rows32.data(), 0, send0.data_ptr(), radii0.data_ptr<int32_t>(),
+                                    state0.data_ptr(), reinterpret_cast<uint32_t*>(hist.data_ptr<int32_t>()), s),
+                  "gsr_shard_forward (probe)");
+    auto hist64 = hist.to(torch::kInt64).bitwise_and(0xFFFFFFFFLL).contiguous();  // u32 counts, widened
+    ex_.all_reduce_i64(hist64.data_ptr<int64_t>(), (size_t)grid_y_, false, s);
+    auto hc = hist64.cpu();
+    std::vector<int64_t> counts(hc.data_ptr<int64_t>(), hc.data_ptr<int64_t>() + grid_y_);
+    rows_ = balance_bands(counts, world_);
+    rows32.assign(rows_.begin(), rows_.end());
+    // probe 2: splats per (shard, band) with the balanced cuts
+    detail::check(gsr_shard_forward(&ccam_, &g, &rs, nb, rows32.data(), 0, send0.data_ptr(), radii0.data_ptr<int32_t>(),
+                                    state0.data_ptr(), nullptr, s),
+                  "gsr_shard_forward (probe)");
+    const int64_t bb0 = (int64_t)gsr_exchange_block_bytes(0);
+    auto heads = send0.view(torch::kInt32).view({nb, bb0 / 4}).select(1, 0).to(torch::kInt64);
+    heads = heads.bitwise_and(0xFFFFFFFFLL).max().reshape({1}).contiguous();
+    ex_.all_reduce_i64(heads.data_ptr<int64_t>(), 1, true, s);
+    const int64_t pc = heads.cpu().item<int64_t>();
+    pair_cap_ = (int)round_up((int64_t)std::ceil(std::max<int64_t>(pc, 1) * headroom_));
+    band_k_.assign(world_, 0);
+    for (int b = 0; b < world_; ++b)
+        for (int y = rows_[b]; y < rows_[b + 1]; ++y) band_k_[b] += counts[y];
+    const int64_t kmax = *std::max_element(band_k_.begin(), band_k_.end());
+    const int64_t cap = round_up((int64_t)std::ceil(std::max<int64_t>(kmax, 1) * headroom_));
+    if (cap >= INT32_MAX || (int64_t)pair_cap_ * world_ >= INT32_MAX)
+        throw std::overflow_error("ShardStep: band capacity / pair_cap exceed int32: use more ranks");
+    capacity_ = (int)cap;
+    pending_.clear();
+    size_buffers();
+}
+
+void ShardStep::set_pair_cap(int pair_cap) {
+    pair_cap_ = pair_cap;
+    size_buffers();
+}
+
+// One step's work on the current stream (= the Pool's main stream, set by step()).  Called
+// eagerly, or once under stream capture to record the graph that later steps replay.
+void ShardStep::run(const torch::Tensor& dpix) {
+    Pool& p = *pool_;
+    const hipStream_t s = p.main.stream();
+    const int nb = world_;
+    const gsr_gaussians g = shard_struct();
+    const gsr_raster_settings rs = shard_settings(), bs = band_settings();
+    std::vector<int32_t> rows32(rows_.begin(), rows_.end());
+    for (Arena* a : {&p.geom, &p.bin, &p.img, &p.scratch}) a->next = 0;
+    // 1. F1 on the shard + splat packing
+    detail::check(gsr_shard_forward(&ccam_, &g, &rs, nb, rows32.data(), pair_cap_, p.send.data_ptr(),
+                                    g.P ? p.radii.data_ptr<int32_t>() : nullptr, p.state.data_ptr(), nullptr, s),
+                  "gsr_shard_forward");
+    // 2. splats -> bands
+    ex_.all_to_all(p.send.data_ptr(), p.recv.data_ptr(), p.block_bytes, s);
+    // 3. F2..F6 on this band
+    detail::check(gsr_band_forward(&ccam_, &bs, nb, pair_cap_, p.recv.data_ptr(), p.color.data_ptr<float>(),
+                                   Pool::geom_cb, Pool::bin_cb, Pool::img_cb, &p, &p.bufs, s),
+                  "gsr_band_forward");
+    // 4. the band's pixels + status footer (send-header counts, band K) -> all-gather on the side
+    //    stream, overlapping B1
+    const int W = cam_.width, H = cam_.height;
+    const int py0 = std::min(rows_[rank_] * GSR_TILE, H), py1 = std::min(rows_[rank_ + 1] * GSR_TILE, H);
+    auto mine_img = p.mine.narrow(0, 0, (int64_t)p.status_off).view({3, p.tall, W});
+    if (py1 > py0) mine_img.narrow(1, 0, py1 - py0).copy_(p.color.narrow(1, py0, py1 - py0));
+    auto status = p.mine.narrow(0, (int64_t)p.status_off, kStatusWords).view(torch::kInt32);
+    status.narrow(0, 0, nb).copy_(p.send.view(torch::kInt32).view({nb, (int64_t)p.block_bytes / 4}).select(1, 0));
+    void* kdev = const_cast<void*>(gsr_view(&ccam_, nb * pair_cap_, &p.bufs, GSR_VIEW_COUNTS));
+    TORCH_CHECK(kdev != nullptr, "ShardStep: no K counter");
+    status.narrow(0, nb, 1).copy_(dev_view(kdev, 1, torch::kInt32));
+    const bool overlap = ex_.capturable();
+    if (overlap) {
+        p.fork.record(p.main.unwrap());
+        p.fork.block(p.side.unwrap());
+    }
+    ex_.all_gather(p.mine.data_ptr<float>(), p.gathered.data_ptr<float>(), p.mine_floats * sizeof(float),
+                   overlap ? p.side.stream() : s);
+    if (overlap) p.join.record(p.side.unwrap());
+    // 5. B1 on the band, per-splat 2D gradients in the received slot layout
+    detail::check(gsr_band_backward(&ccam_, &bs, nb, pair_cap_, &p.bufs, dpix.data_ptr<float>(), Arena::cb,
+                                    &p.scratch, p.g2.data_ptr<float>(), s),
+                  "gsr_band_backward");
+    // 6. gradients -> owning shards
+    ex_.all_to_all(p.g2.data_ptr<float>(), p.back.data_ptr(), p.grad_block, s);
+    // 7. band-order sums + B2 on the shard
+    detail::check(gsr_shard_backward(&ccam_, &g, &rs, nb, rows32.data(), pair_cap_, p.state.data_ptr(),
+                                     p.back.data_ptr(), &p.gg, s),
+                  "gsr_shard_backward");
+    // 8. join the all-gather, unpack the bands into the full image
+    if (overlap) p.join.block(p.main.unwrap());
+    for (int r = 0; r < world_; ++r) {
+        const int a = std::min(rows_[r] * GSR_TILE, H), b = std::min(rows_[r + 1] * GSR_TILE, H);
+        if (b > a)
+            p.image.narrow(1, a, b - a).copy_(
+                p.gathered.select(0, r).narrow(0, 0, (int64_t)p.status_off).view({3, p.tall, W}).narrow(1, 0, b - a));
+    }
+}
+
+void ShardStep::push_status() {
+    Pool& p = *pool_;
+    // poll(false) at the start of every step leaves at most lag_ older entries pending
+    TORCH_CHECK(pending_.size() < p.ring.size(), "ShardStep: overflow ring full");
+    const int slot = ring_next_;
+    ring_next_ = (ring_next_ + 1) % (int)p.ring.size();
+    auto st = p.gathered.narrow(1, (int64_t)p.status_off, kStatusWords).contiguous().view(torch::kInt32);
+    p.ring[slot].copy_(st, /*non_blocking=*/true);
+    p.ring_ev[slot]->record(p.main.unwrap());
+    pending_.push_back({steps_, slot});
+}
+
+void ShardStep::poll(bool wait_all) {
+    // the step exactly lag_ back (and anything older) is checked on every rank at the same call
+    while (!pending_.empty() && (wait_all || pending_.front().step <= steps_ - lag_)) {
+        const Pending q = pending_.front();
+        pool_->ring_ev[q.slot]->synchronize();
+        pending_.erase(pending_.begin());
+        const int32_t* st = pool_->ring[q.slot].data_ptr<int32_t>();
+        for (int r = 0; r < world_; ++r) {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(st + r * kStatusWords);
+            std::vector<int64_t> counts(w, w + world_);
+            const int64_t k = w[world_];
+            if (*std::max_element(counts.begin(), counts.end()) > pair_cap_ || k > capacity_) {
+                pending_.clear();
+                throw ShardOverflowError(q.step, r, counts, pair_cap_, k, capacity_);
+            }
+        }
+    }
+}
+
+void ShardStep::check() { poll(true); }
+
+ShardStep::Result ShardStep::step(const torch::Tensor& dL_dpix) {
+    TORCH_CHECK(pair_cap_ > 0 && capacity_ > 0, "ShardStep: call plan() first");
+    TORCH_CHECK(dL_dpix.is_cuda() && dL_dpix.scalar_type() == torch::kFloat32 && dL_dpix.is_contiguous() &&
+                    dL_dpix.numel() == (int64_t)3 * cam_.height * cam_.width,
+                "ShardStep: dL_dpix must be a contiguous (3,H,W) f32 device tensor");
+    poll(false);
+    Pool& p = *pool_;
+    // the step runs on its own stream (capturable), ordered after / before the caller's
+    const Stream caller = current_stream();
+    p.enter.record(caller.unwrap());
+    p.enter.block(p.main.unwrap());
+    {
+        StreamGuard guard(p.main.unwrap());
+        if (graph_ && p.graph && p.graph_dpix == dL_dpix.data_ptr()) {
+            p.graph->replay();
+        } else {
+            run(dL_dpix);  // this step's result, eagerly
+            if (graph_) {
+                // every arena slot now exists: capture the same calls on the same buffers
+                drop_graph();
+                for (Arena* a : {&p.geom, &p.bin, &p.img, &p.scratch}) a->frozen = true;
+                p.main.unwrap().synchronize();
+                p.graph = std::make_unique<at::cuda::CUDAGraph>();
+                p.graph->capture_begin({0, 0}, hipStreamCaptureModeRelaxed);
+                try {
+                    run(dL_dpix);
+                } catch (...) {
+                    try {
+                        p.graph->capture_end();
+                    } catch (...) {
+                    }
+                    drop_graph();
+                    throw;
+                }
+                p.graph->capture_end();
+                p.graph_dpix = dL_dpix.data_ptr();
+            }
+        }
+        push_status();
+    }
+    p.leave.record(p.main.unwrap());
+    p.leave.block(caller.unwrap());
+    ++steps_;
+    return {p.image, p.grads, p.radii};
+}
+
+}  // namespace gsr
+
+// ---- Python binding (the benchmark's multi-GPU path; off in the C++ executables) ----
+#ifndef GSR_NO_PYBIND
+#include <pybind11/stl.h>
+#include <torch/extension.h>
+
+namespace gsr {
+namespace py = pybind11;
+void bind_shard(py::module& m) {
+    static py::exception<ShardOverflowError> ovf(m, "ShardOverflowError", PyExc_OverflowError);
+    py::register_exception_translator([](std::exception_ptr p) {
+        try {
+            if (p) std::rethrow_exception(p);
+        } catch (const ShardOverflowError& e) {
+            py::object cls = py::reinterpret_borrow<py::object>(ovf.ptr());
+            py::object err = cls(e.what());
+            err.attr("step") = e.step;
+            err.attr("rank") = e.rank;
+            err.attr("counts") = e.counts;
+            err.attr("pair_cap") = e.pair_cap;
+            err.attr("band_k") = e.band_k;
+            err.attr("capacity") = e.capacity;
+            PyErr_SetObject(ovf.ptr(), err.ptr());
+        }
+    });
+    py::class_<Exchange>(m, "Exchange")
+        .def_property_readonly("rank", &Exchange::rank)
+        .def_property_readonly("world", &Exchange::world)
+        .def_property_readonly("name", &Exchange::name)
+        .def_property_readonly("capturable", &Exchange::capturable);
+    m.def("rccl_unique_id", []() {
+        auto v = rccl_unique_id();
+        return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+    });
+    m.def(
+        "rccl_exchange",
+        [](py::bytes id, int rank, int world) {
+            const std::string b = id;
+            return rccl_exchange(std::vector<uint8_t>(b.begin(), b.end()), rank, world);
+        },
+        py::arg("unique_id"), py::arg("rank"), py::arg("world"));
+    py::class_<ShardStep>(m, "ShardStep")
+        .def(py::init([](Exchange& ex, const RasterCamera& cam, py::dict inputs, int sh_degree,
+                         std::array<float, 3> bg, double headroom, bool graph, int lag) {
+                 ShardInputs in;
+                 auto get = [&](const char* k) {
+                     return inputs.contains(k) && !inputs[k].is_none() ? inputs[k].cast<torch::Tensor>()
+                                                                        : torch::Tensor();
+                 };
+                 in.means3D = get("means3D");
+                 in.opacities = get("opacities");
+                 in.scales = get("scales");
+                 in.rotations = get("rotations");
+                 in.sh_dc = get("sh_dc");
+                 in.sh_rest = get("sh_rest");
+                 in.colors_precomp = get("colors_precomp");
+                 in.cov3D_precomp = get("cov3D_precomp");
+                 in.sh_degree = sh_degree;
+                 return std::make_unique<ShardStep>(ex, cam, in, bg, headroom, graph, lag);
+             }),
+             py::arg("exchange"), py::arg("cam"), py::arg("inputs"), py::arg("sh_degree"),
+             py::arg("bg") = std::array<float, 3>{0.f, 0.f, 0.f}, py::arg("headroom") = 1.25,
+             py::arg("graph") = true, py::arg("lag") = 2, py::keep_alive<1, 2>())
+        .def("plan", &ShardStep::plan, py::call_guard<py::gil_scoped_release>())
+        .def(
+            "step",
+            [](ShardStep& s, const torch::Tensor& dpix) {
+                ShardStep::Result r;
+                {
+                    py::gil_scoped_release nogil;
+                    r = s.step(dpix);
+                }
+                return py::make_tuple(r.image, r.grads, r.radii);
+            },
+            py::arg("dL_dpix"))
+        .def("check", &ShardStep::check, py::call_guard<py::gil_scoped_release>())
+        .def("set_pair_cap", &ShardStep::set_pair_cap)
+        .def_property_readonly("rows", &ShardStep::rows)
+        .def_property_readonly("pair_cap", &ShardStep::pair_cap)
+        .def_property_readonly("capacity", &ShardStep::capacity)
+        .def_property_readonly("band_instances", &ShardStep::band_instances)
+        .def_property_readonly("g0", &ShardStep::g0)
+        .def_property_readonly("g1", &ShardStep::g1)
+        .def_property_readonly("graph_active", &ShardStep::graph_active)
+        .def_property_readonly("steps", &ShardStep::steps);
+}
+}  // namespace gsr
+#endif  // GSR_NO_PYBIND

@@ -1,0 +1,165 @@
+// gsr_shard.h -- the multi-GPU step in C++ (SURVEY §8e "scaling version"): the
+// native twin of bands.ShardStep, so that a C++ training loop (src/utils/train_utils.cpp:97-146,
+// src/train.cpp:12-47 -- host code stays C++) runs the sharded path without Python.
+//
+// Rank r of N owns the Gaussian shard [g0, g1) and the band of tile rows [rows[r], rows[r+1]).
+// One step on the rank's stream:
+//   gsr_shard_forward -> all-to-all of the splat blocks -> gsr_band_forward
+//   -> all-gather of the band images (on a second stream, overlapping B1)
+//   -> gsr_band_backward -> all-to-all of the 2D-gradient rows back -> gsr_shard_backward.
+// The collectives go through an `Exchange`: RCCL over xGMI (grouped ncclSend / ncclRecv for the
+// all-to-alls, ncclAllGather for the bands) on the GPU box, or a host-staged exchange through a
+// c10d::Store for ranks that share one GPU (the two-process test; RCCL refuses two ranks on one
+// device).  The step is sync-free (fixed capacities from plan(); K stays on the device), so with
+// an RCCL exchange it is captured once into a hipGraph and replayed: one graph launch per step.
+//
+// Overflow agreement: each rank's send-header counts and band K ride in a status footer of its
+// band image, so the all-gather hands every rank the status of ALL ranks; the gathered footers
+// are copied to pinned memory after the step and checked exactly `lag` steps later (waiting on
+// that step's event if needed).  Every rank therefore sees the same counts at the same step and
+// raises ShardOverflowError together -- no rank is left blocked in a collective its peers no
+// longer join.
+#pragma once
+#include <hip/hip_runtime.h>  // hipStream_t only: the step itself uses libtorch streams / graphs
+#include <torch/torch.h>
+
+#include <array>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "gsr/gsr.h"
+#include "gsr_render.h"
+
+namespace c10d {
+class Store;
+}
+
+namespace gsr {
+
+// ---- transport -----------------------------------------------------------------------------
+class Exchange {
+   public:
+    virtual ~Exchange() = default;
+    virtual int rank() const = 0;
+    virtual int world() const = 0;
+    virtual bool capturable() const = 0;  // may be recorded into a hipGraph
+    virtual const char* name() const = 0;
+    // block b of `send` (block_bytes each) -> rank b; block s of `recv` <- rank s
+    virtual void all_to_all(const void* send, void* recv, size_t block_bytes, hipStream_t s) = 0;
+    // `bytes` from every rank into recv, rank-major
+    virtual void all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
+    // in place over ranks (setup only)
+    virtual void all_reduce_i64(int64_t* buf, size_t n, bool max, hipStream_t s) = 0;
+};
+
+// RCCL: rank 0 makes the unique id, the caller broadcasts it (torch.distributed, a store, ...).
+std::vector<uint8_t> rccl_unique_id();
+std::unique_ptr<Exchange> rccl_exchange(const std::vector<uint8_t>& unique_id, int rank, int world);
+// RCCL with the id passed through a c10d::Store (key "gsr/rccl_id").
+std::unique_ptr<Exchange> rccl_exchange(c10d::Store& store, int rank, int world);
+// Host-staged through a c10d::Store (device -> host -> store -> host -> device); not capturable.
+std::unique_ptr<Exchange> store_exchange(std::shared_ptr<c10d::Store> store, int rank, int world);
+
+// ---- partition (bands.py) -------------------------------------------------------------------
+std::pair<int64_t, int64_t> gaussian_shard(int64_t P, int world, int rank);
+std::vector<int> equal_bands(int grid_y, int world);
+std::vector<int> balance_bands(const std::vector<int64_t>& row_counts, int world);
+
+class ShardOverflowError : public std::overflow_error {
+   public:
+    ShardOverflowError(int64_t step, int rank, std::vector<int64_t> counts, int pair_cap, int64_t band_k,
+                       int capacity);
+    int64_t step;
+    int rank;                     // the (first) rank whose counts exceeded a capacity
+    std::vector<int64_t> counts;  // that rank's splats per band
+    int pair_cap;
+    int64_t band_k;
+    int capacity;
+};
+
+// The shard's input rows (activated values, as gsr_gaussians): device f32 tensors over ALL P
+// Gaussians; the step reads rows [g0, g1) only.  Unused ones undefined.
+struct ShardInputs {
+    torch::Tensor means3D, opacities, scales, rotations, sh_dc, sh_rest, colors_precomp, cov3D_precomp;
+    int sh_degree = 0;
+    float scale_modifier = 1.f;
+};
+
+class ShardStep {
+   public:
+    // graph: capture the step into a hipGraph on the first step after plan() (RCCL exchange
+    // only; the host-staged one always runs eagerly).  lag: steps between a step and its
+    // overflow check (>= 1).  headroom: capacity factor over the probed counts.
+    ShardStep(Exchange& ex, const RasterCamera& cam, const ShardInputs& in, std::array<float, 3> bg = {0, 0, 0},
+              double headroom = 1.25, bool graph = true, int lag = 2);
+    ~ShardStep();
+    ShardStep(const ShardStep&) = delete;
+    ShardStep& operator=(const ShardStep&) = delete;
+
+    // Probe (synchronous, setup only): balanced band cuts from the summed row histogram, then
+    // pair_cap and the band capacity with headroom.  Drops a captured graph.
+    void plan();
+    struct Result {
+        torch::Tensor image;                         // (3,H,W): every band, gathered
+        std::map<std::string, torch::Tensor> grads;  // the shard's leaf gradients (rows g0..g1)
+        torch::Tensor radii;                         // (g1 - g0) int32
+    };
+    // One forward + backward; raises ShardOverflowError for the step `lag` earlier if any rank
+    // overflowed there.  The returned tensors are the step's own buffers: consume them before
+    // the next step().  dL_dpix: (3,H,W) f32 device (its band rows are read).
+    Result step(const torch::Tensor& dL_dpix);
+    // Check every completed step now (waits); raises like step().
+    void check();
+
+    const std::vector<int>& rows() const { return rows_; }
+    int pair_cap() const { return pair_cap_; }
+    int capacity() const { return capacity_; }
+    const std::vector<int64_t>& band_instances() const { return band_k_; }
+    int64_t g0() const { return g0_; }
+    int64_t g1() const { return g1_; }
+    bool graph_active() const;
+    int64_t steps() const { return steps_; }
+    // test hook: force a (smaller) pair capacity after plan()
+    void set_pair_cap(int pair_cap);
+
+   private:
+    struct Pool;  // buffers (stable addresses across steps: graph-replayable), streams, events, graph
+    void run(const torch::Tensor& dpix);
+    void push_status();
+    void poll(bool wait_all);
+    gsr_gaussians shard_struct() const;
+    gsr_raster_settings shard_settings() const;
+    gsr_raster_settings band_settings() const;
+    void size_buffers();
+    void drop_graph();
+
+    Exchange& ex_;
+    RasterCamera cam_;
+    gsr_camera ccam_;
+    ShardInputs in_;
+    std::array<float, 3> bg_;
+    double headroom_;
+    bool graph_;
+    int lag_;
+    int world_, rank_;
+    int64_t P_ = 0, g0_ = 0, g1_ = 0;
+    int grid_y_ = 0;
+    std::vector<int> rows_;
+    int pair_cap_ = 0, capacity_ = 0;
+    std::vector<int64_t> band_k_;
+    int64_t steps_ = 0;
+    std::unique_ptr<Pool> pool_;
+    // overflow ring: gathered status footers (pinned), checked `lag_` steps later
+    struct Pending {
+        int64_t step;
+        int slot;
+    };
+    std::vector<Pending> pending_;
+    int ring_next_ = 0;
+};
+
+}  // namespace gsr

@@ -15,6 +15,7 @@
 #endif
 
 #include <cmath>
+#include <cstdio>
 #include <stdexcept>
 
 #include "gsr_render.h"
@@ -360,7 +361,11 @@ void BinningCapacity::poll(bool wait_one) {
         const Pending p = pending_.front();
         pending_.erase(pending_.begin());
         const int64_t k = slots_[p.slot].data_ptr<int32_t>()[0];
-        if (k > p.cap) {  // that render was truncated and its iteration applied
+        if (k > p.cap) {  // that render was truncated (its statistics / Adam step skipped on the device)
+            if (overflows_ == 0)
+                std::fprintf(stderr, "[gsr] BinningCapacity: a render's K = %lld exceeded its bound %d; that "
+                             "iteration's update was skipped on the device, renders are sized exactly again\n",
+                             (long long)k, p.cap);
             ++overflows_;
             k_max_ = std::max(k_max_, k);
             pending_.clear();
@@ -481,6 +486,10 @@ static gsr::RasterSettings settings_from_py(const std::vector<float>& bg, float 
 
 static torch::Tensor opt(const c10::optional<torch::Tensor>& t) { return t.has_value() ? *t : torch::Tensor(); }
 
+namespace gsr {
+void bind_shard(pybind11::module& m);  // gsr_shard.cpp
+}
+
 PYBIND11_MODULE(_gsr_torch, m) {
     m.doc() = "libtorch RasterizeGaussians over the gsr C ABI (libgsr_hip.so)";
     py::class_<gsr::RasterCamera>(m, "RasterCamera")
@@ -519,5 +528,6 @@ PYBIND11_MODULE(_gsr_torch, m) {
         py::arg("width"), py::arg("height"), py::arg("FoVx"), py::arg("FoVy"), py::arg("world_view_transform"),
         py::arg("full_proj_transform"), py::arg("camera_center"));
     m.def("abi_version", []() { return gsr_abi_version(); });
+    gsr::bind_shard(m);
 }
 #endif  // GSR_NO_PYBIND

@@ -86,13 +86,23 @@ torch::Tensor photometric_loss(const torch::Tensor& image, const torch::Tensor& 
     return outs[0];
 }
 
-void fused_adam_step(const std::vector<torch::optim::Adam*>& optimizers) {
+namespace {
+// (K device pointer, bound) of a bounded render, or (nullptr, 0)
+std::pair<const uint32_t*, uint32_t> guard_of(const RenderOutput* r) {
+    if (!r || r->num_rendered >= 0 || !r->num_rendered_device.defined()) return {nullptr, 0u};
+    return {reinterpret_cast<const uint32_t*>(r->num_rendered_device.data_ptr<int32_t>()), (uint32_t)r->capacity};
+}
+}  // namespace
+
+void fused_adam_step(const std::vector<torch::optim::Adam*>& optimizers, const RenderOutput* guard) {
     std::vector<gsr_adam_group> groups;
     std::vector<torch::Tensor> keep;
     double beta1 = -1, beta2 = -1, eps = -1;
+    const auto gk = guard_of(guard);
     auto launch = [&]() {
         if (groups.empty()) return;
-        check(gsr_adam_step(groups.data(), (int32_t)groups.size(), (float)beta1, (float)beta2, (float)eps, stream()),
+        check(gsr_adam_step_guarded(groups.data(), (int32_t)groups.size(), (float)beta1, (float)beta2, (float)eps,
+                                    gk.first, gk.second, stream()),
               "gsr_adam_step");
         groups.clear();
         keep.clear();
@@ -140,7 +150,7 @@ void fused_adam_step(const std::vector<torch::optim::Adam*>& optimizers) {
 }
 
 void densify_stats(const torch::Tensor& radii, const torch::Tensor& viewspace_grad, torch::Tensor& max_radii2D,
-                   torch::Tensor& grad_accum, torch::Tensor& denom) {
+                   torch::Tensor& grad_accum, torch::Tensor& denom, const RenderOutput* guard) {
     const int64_t P = radii.size(0);
     TORCH_CHECK(radii.scalar_type() == torch::kInt32 && radii.is_contiguous(), "radii must be contiguous int32");
     auto g = viewspace_grad.contiguous();
@@ -150,8 +160,10 @@ void densify_stats(const torch::Tensor& radii, const torch::Tensor& viewspace_gr
         require_f32(*t, "statistics");
         TORCH_CHECK(t->numel() == P, "statistics must have P entries");
     }
-    check(gsr_densify_stats(radii.data_ptr<int32_t>(), g.data_ptr<float>(), (int32_t)P, max_radii2D.data_ptr<float>(),
-                            grad_accum.data_ptr<float>(), denom.data_ptr<float>(), stream()),
+    const auto gk = guard_of(guard);
+    check(gsr_densify_stats_guarded(radii.data_ptr<int32_t>(), g.data_ptr<float>(), (int32_t)P,
+                                    max_radii2D.data_ptr<float>(), grad_accum.data_ptr<float>(),
+                                    denom.data_ptr<float>(), gk.first, gk.second, stream()),
           "gsr_densify_stats");
 }
 
@@ -325,11 +337,14 @@ detail::Frame Trainer::render(const RasterCamera& cam, const std::array<float, 3
     RasterSettings rs;
     rs.bg = bg;
     rs.sh_degree = active_sh_degree_;
-    rs.max_rendered = binning_.bound();
+    const int bound = binning_.bound();
+    rs.max_rendered = bound;
     o = o.reshape({-1});
     const auto& rest = params_["f_rest"];
     auto f = detail::forward(cam, rs, params_["xyz"], params_["f_dc"], rest.size(1) ? rest : torch::Tensor(),
                              torch::Tensor(), o, s, q, torch::Tensor());
+    guard_k_ = bound > 0 ? f.k_device() : torch::Tensor();
+    guard_cap_ = bound;
     binning_.observe(f.k_device(), f.bufs.num_rendered);
     return f;
 }
@@ -378,8 +393,9 @@ Trainer::StepResult Trainer::step(int iteration, const RasterCamera& cam, const 
     if (rest.size(1)) grads["f_rest"] = g_rest;
     std::vector<std::string> replaced;
     if (iteration < opt_.densify_until_iter_) {
-        check(gsr_densify_stats(fr.radii.data_ptr<int32_t>(), fp(g_means2D), (int32_t)P, fp(max_radii2D_),
-                                fp(xyz_gradient_accum_), fp(denom_), stream()),
+        check(gsr_densify_stats_guarded(fr.radii.data_ptr<int32_t>(), fp(g_means2D), (int32_t)P, fp(max_radii2D_),
+                                        fp(xyz_gradient_accum_), fp(denom_), guard_ptr(), (uint32_t)guard_cap_,
+                                        stream()),
               "gsr_densify_stats");
         if (densify) {
             if (iteration > opt_.densify_from_iter_ && iteration % opt_.densification_interval_ == 0) {
@@ -425,7 +441,9 @@ void Trainer::optimizer_step(const std::map<std::string, torch::Tensor>& grads) 
         groups.push_back(ag);
     }
     if (!groups.empty())
-        check(gsr_adam_step(groups.data(), (int32_t)groups.size(), 0.9f, 0.999f, 1e-8f, stream()), "gsr_adam_step");
+        check(gsr_adam_step_guarded(groups.data(), (int32_t)groups.size(), 0.9f, 0.999f, 1e-8f, guard_ptr(),
+                                    (uint32_t)guard_cap_, stream()),
+              "gsr_adam_step");
 }
 
 // ---- densification (upstream semantics; trainer.py) ----

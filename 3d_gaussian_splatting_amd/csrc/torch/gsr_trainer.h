@@ -74,19 +74,23 @@ torch::Tensor photometric_loss(const torch::Tensor& image, const torch::Tensor& 
 // as libtorch creates it): the same update as calling opt->step() on each.  Parameters without
 // a gradient are skipped as libtorch skips them.  Options the kernel does not implement
 // (amsgrad, weight_decay != 0) are refused with an exception.
-void fused_adam_step(const std::vector<torch::optim::Adam*>& optimizers);
+// `guard`: the render whose gradients these are.  When it ran under a binning bound
+// (RenderOutput::num_rendered < 0), the step is skipped ON THE DEVICE if its K exceeded that
+// bound (gsr_adam_step_guarded): a truncated render never updates the model, with no host wait.
+void fused_adam_step(const std::vector<torch::optim::Adam*>& optimizers, const RenderOutput* guard = nullptr);
 template <class Map>
-void fused_adam_step(Map& optimizers) {  // e.g. CoreParams::optimizers_ (name -> unique_ptr<Adam>)
+void fused_adam_step(Map& optimizers, const RenderOutput* guard = nullptr) {  // e.g. CoreParams::optimizers_
     std::vector<torch::optim::Adam*> v;
     for (auto& kv : optimizers) v.push_back(kv.second.get());
-    fused_adam_step(static_cast<const std::vector<torch::optim::Adam*>&>(v));
+    fused_adam_step(static_cast<const std::vector<torch::optim::Adam*>&>(v), guard);
 }
 
 // Densification statistics of one render (gaussian_model.h:18-20, upstream
 // add_densification_stats): for radii > 0, max_radii2D = max(max_radii2D, radii),
-// grad_accum += |viewspace_grad[:, :2]|, denom += 1.  All (P) f32 device tensors.
+// grad_accum += |viewspace_grad[:, :2]|, denom += 1.  All (P) f32 device tensors.  `guard`: as
+// fused_adam_step's (skipped on the device for a render truncated by its bound).
 void densify_stats(const torch::Tensor& radii, const torch::Tensor& viewspace_grad, torch::Tensor& max_radii2D,
-                   torch::Tensor& grad_accum, torch::Tensor& denom);
+                   torch::Tensor& grad_accum, torch::Tensor& denom, const RenderOutput* guard = nullptr);
 // Ascending int32 indices of the nonzero entries of a bool / uint8 mask (one host read of the count).
 torch::Tensor compact_index(const torch::Tensor& mask);
 // [t[idx] for t in tensors] (rows of contiguous f32 tensors) in one launch per 24 tensors.
@@ -142,6 +146,9 @@ class Trainer {
                          torch::Tensor& q, torch::Tensor& o);
     void setup();
     void optimizer_step(const std::map<std::string, torch::Tensor>& grads);
+    const uint32_t* guard_ptr() const {
+        return guard_k_.defined() ? reinterpret_cast<const uint32_t*>(guard_k_.data_ptr<int32_t>()) : nullptr;
+    }
     void append(const std::map<std::string, torch::Tensor>& rows);
     std::map<std::string, torch::Tensor> rows(const torch::Tensor& mask);
     void densify_and_clone(const torch::Tensor& grads, double threshold, double extent);
@@ -159,6 +166,10 @@ class Trainer {
     torch::Tensor max_radii2D_, xyz_gradient_accum_, denom_;
     at::Generator gen_;
     BinningCapacity binning_;
+    // the last render's K (device counter) and the bound it ran under (0: exact, no guard):
+    // the device-side guard of that iteration's statistics and Adam step
+    torch::Tensor guard_k_;
+    int guard_cap_ = 0;
 };
 
 }  // namespace gsr

@@ -45,8 +45,11 @@ EXPORTS = ["gsr_abi_version", "gsr_last_error", "gsr_forward", "gsr_read_num_ren
            "gsr_stage_name"]
 # include/gsr/gsr_train.h (training-step kernels)
 TRAIN_EXPORTS = ["gsr_activate", "gsr_loss_scratch_bytes", "gsr_loss_forward", "gsr_loss_backward", "gsr_adam_step",
-                 "gsr_densify_stats", "gsr_compact_scratch_bytes", "gsr_compact_index", "gsr_gather_rows",
+                 "gsr_adam_step_guarded", "gsr_densify_stats", "gsr_densify_stats_guarded", "gsr_compact_scratch_bytes", "gsr_compact_index", "gsr_gather_rows",
                  "gsr_knn_scratch_bytes", "gsr_knn_mean_dist2"]
+COMM_EXPORTS = ["gsr_comm_unique_id", "gsr_comm_init", "gsr_comm_destroy", "gsr_comm_all_to_all",
+                "gsr_comm_all_gather", "gsr_comm_all_reduce_i64"]  # include/gsr/gsr_comm.h
+COMM_ID_BYTES = 128
 ACT_NONE, ACT_EXP, ACT_SIGMOID, ACT_NORMALIZE4 = range(4)
 ADAM_MAX_GROUPS = 8
 GATHER_MAX = 24
@@ -182,8 +185,12 @@ def load_hip() -> ctypes.CDLL:
         L.gsr_loss_backward.argtypes = [vp, vp, i32, i32, i32, f32, vp, vp, vp]
         L.gsr_adam_step.restype = ctypes.c_int
         L.gsr_adam_step.argtypes = [ctypes.POINTER(AdamGroup), i32, f32, f32, f32, vp]
+        L.gsr_adam_step_guarded.restype = ctypes.c_int
+        L.gsr_adam_step_guarded.argtypes = [ctypes.POINTER(AdamGroup), i32, f32, f32, f32, vp, ctypes.c_uint32, vp]
         L.gsr_densify_stats.restype = ctypes.c_int
         L.gsr_densify_stats.argtypes = [vp, vp, i32, vp, vp, vp, vp]
+        L.gsr_densify_stats_guarded.restype = ctypes.c_int
+        L.gsr_densify_stats_guarded.argtypes = [vp, vp, i32, vp, vp, vp, vp, ctypes.c_uint32, vp]
         L.gsr_compact_scratch_bytes.restype = ctypes.c_size_t
         L.gsr_compact_scratch_bytes.argtypes = [i32]
         L.gsr_compact_index.restype = ctypes.c_int

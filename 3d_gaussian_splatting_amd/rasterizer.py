@@ -14,6 +14,7 @@ from __future__ import annotations
 import ctypes
 from dataclasses import dataclass, field
 
+import numpy as np
 import torch
 
 from . import native
@@ -127,16 +128,26 @@ class CAbiRasterizer:
     def __init__(self, device="cuda"):
         self.device = torch.device(device)
         self.L = native.load_hip()
-        self._cams = {}  # id(cam) -> (cam, gsr_camera struct): built once per camera object
+        self._cams = {}  # camera contents -> gsr_camera struct
+
+    @staticmethod
+    def _cam_key(cam):
+        """Everything camera_struct reads, by value: an in-place edit of a camera's matrices or
+        size gives a new key, never a stale struct (a stale width / height would size the
+        kernels' writes differently from the colour tensor made from the new camera)."""
+        return (int(cam.width), int(cam.height), float(cam.tanfovx), float(cam.tanfovy),
+                np.asarray(cam.viewmatrix, np.float32).tobytes(), np.asarray(cam.projmatrix, np.float32).tobytes(),
+                np.asarray(cam.campos, np.float32).tobytes())
 
     def _cam(self, cam):
-        hit = self._cams.get(id(cam))
-        if hit is not None and hit[0] is cam:
-            return hit[1]
+        key = self._cam_key(cam)
+        c = self._cams.get(key)
+        if c is not None:
+            return c
         c = native.camera_struct(cam)
         if len(self._cams) > 256:
             self._cams.clear()
-        self._cams[id(cam)] = (cam, c)
+        self._cams[key] = c
         return c
 
     def _stream(self):

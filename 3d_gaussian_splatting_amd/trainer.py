@@ -36,6 +36,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import warnings
 from dataclasses import dataclass
 
 import numpy as np
@@ -132,8 +133,10 @@ class TrainKernels:
                                              _stream(self.device)), "gsr_loss_backward")
         return out
 
-    def adam_step(self, groups, beta1=0.9, beta2=0.999, eps=1e-8):
-        """groups: list of dicts(param, grad, exp_avg, exp_avg_sq, act, step, lr), one launch."""
+    def adam_step(self, groups, beta1=0.9, beta2=0.999, eps=1e-8, guard=None):
+        """groups: list of dicts(param, grad, exp_avg, exp_avg_sq, act, step, lr), one launch.
+        guard = (k_device, bound): the step is skipped on the device when the render's K
+        exceeded the bound it ran under (gsr_adam_step_guarded)."""
         arr = (native.AdamGroup * len(groups))()
         for i, g in enumerate(groups):
             for k in ("param", "grad", "exp_avg", "exp_avg_sq"):
@@ -147,13 +150,15 @@ class TrainKernels:
             arr[i].act = int(g["act"])
             arr[i].step = int(g["step"])
             arr[i].lr = float(g["lr"])
-        self._check(self.L.gsr_adam_step(arr, len(groups), float(beta1), float(beta2), float(eps),
-                                         _stream(self.device)), "gsr_adam_step")
+        gk, gcap = _guard(guard)
+        self._check(self.L.gsr_adam_step_guarded(arr, len(groups), float(beta1), float(beta2), float(eps), gk, gcap,
+                                                 _stream(self.device)), "gsr_adam_step")
 
-    def densify_stats(self, radii, dmeans2D, max_radii2D, grad_accum, denom):
+    def densify_stats(self, radii, dmeans2D, max_radii2D, grad_accum, denom, guard=None):
         P = int(radii.shape[0])
-        self._check(self.L.gsr_densify_stats(_p(radii), _p(dmeans2D), P, _p(max_radii2D), _p(grad_accum),
-                                             _p(denom), _stream(self.device)), "gsr_densify_stats")
+        gk, gcap = _guard(guard)
+        self._check(self.L.gsr_densify_stats_guarded(_p(radii), _p(dmeans2D), P, _p(max_radii2D), _p(grad_accum),
+                                                     _p(denom), gk, gcap, _stream(self.device)), "gsr_densify_stats")
 
     def compact_index(self, mask: torch.Tensor) -> torch.Tensor:
         """Ascending int32 indices of the nonzero entries of a bool / uint8 mask (one D2H read)."""
@@ -202,6 +207,14 @@ class TrainKernels:
         return outs
 
 
+def _guard(guard):
+    """(device pointer of K, bound) for the *_guarded entry points; (None, 0) = no guard."""
+    if guard is None:
+        return None, 0
+    k, cap = guard
+    return ctypes.c_void_p(k.data_ptr()), int(cap)
+
+
 class BinningOverflowError(OverflowError):
     """A bounded render's K exceeded its bound (strict BinningCapacity): that render dropped
     instances, and the iteration that used it has been applied."""
@@ -215,9 +228,11 @@ class BinningCapacity:
     counter) is copied to a pinned slot and checked once its event has completed -- one or two
     iterations later, never waiting.  K above the bound at that check means that render was
     truncated (its kernels clamp to the bound; GSR_ERR_OVERFLOW semantics) and the iteration
-    that used it -- loss, gradients, statistics, Adam step -- has already been applied: it is
-    counted in ``overflows``, the next render is sized exactly again, and with ``strict=True``
-    a BinningOverflowError is raised at that check instead.  The bound covers the largest K of
+    that used it has already run: its densification statistics and Adam step were skipped ON
+    THE DEVICE (the trainer passes the render's K and bound to the *_guarded kernels, so a
+    truncated render never updates the model), it is counted in ``overflows`` (with a warning
+    the first time), the next render is sized exactly again, and with ``strict=True`` a
+    BinningOverflowError is raised at that check instead.  The bound covers the largest K of
     the views rendered since the last point-set change with 1.5x + 64k headroom; views are
     re-rendered every len(views) iterations, so a view larger than that bound can only be one
     not yet seen since the change (the 30k-iteration loop: 0 overflows)."""
@@ -269,6 +284,10 @@ class BinningCapacity:
             slot, _, cap = self.pending.pop(0)
             k = int(slot.item())
             if k > cap:
+                if self.overflows == 0:
+                    warnings.warn(f"BinningCapacity: a render's K = {k} exceeded its bound {cap}; that iteration's "
+                                  "update was skipped on the device and renders are sized exactly again",
+                                  RuntimeWarning, stacklevel=2)
                 self.overflows += 1
                 self.k_max = max(self.k_max, k)
                 self.pending.clear()
@@ -298,6 +317,7 @@ class GaussianTrainer:
                        "scaling": f(scaling, (P, 3)), "rotation": f(rotation, (P, 4))}
         self.max_sh_degree = int(max_sh_degree)
         self.active_sh_degree = 0
+        self._guard = None  # (K device counter, bound) of the last bounded render
         # the reference's CoreParams::spatial_lr_scale_ is a float (gaussian_model.h): held at
         # f32 precision, so a capture / restore round trip (which stores it as float) is exact
         self.spatial_lr_scale = _f32(spatial_lr_scale)
@@ -408,9 +428,12 @@ class GaussianTrainer:
     def render(self, cam, bg=(0.0, 0.0, 0.0)):
         s, q, o = self.k.activate(self.params["scaling"], self.params["rotation"], self.params["opacity"])
         p = self.params
+        bound = self.binning.bound()
         st = self.rast.forward(cam, p["xyz"], o.reshape(-1), scales=s, rotations=q, sh_dc=p["f_dc"],
                                sh_rest=p["f_rest"] if p["f_rest"].shape[1] else None,
-                               sh_degree=self.active_sh_degree, bg=bg, max_rendered=self.binning.bound())
+                               sh_degree=self.active_sh_degree, bg=bg, max_rendered=bound)
+        # device-side guard of this iteration's statistics / Adam step (see BinningCapacity)
+        self._guard = (st.k_device(), bound) if bound > 0 else None
         self.binning.observe(st)
         return st
 
@@ -437,7 +460,8 @@ class GaussianTrainer:
             grads["f_rest"] = g["sh_rest"]
         replaced = set()
         if iteration < opt.densify_until_iter:
-            self.k.densify_stats(st.radii, g["means2D"], self.max_radii2D, self.xyz_gradient_accum, self.denom)
+            self.k.densify_stats(st.radii, g["means2D"], self.max_radii2D, self.xyz_gradient_accum, self.denom,
+                                 guard=self._guard)
             if densify:
                 if iteration > opt.densify_from_iter and iteration % opt.densification_interval == 0:
                     size_threshold = 20 if iteration > opt.opacity_reset_interval else None
@@ -462,7 +486,7 @@ class GaussianTrainer:
                                exp_avg=self.exp_avg[k], exp_avg_sq=self.exp_avg_sq[k], act=ACTS[k],
                                step=self.steps[k], lr=self.lr[k]))
         if groups:
-            self.k.adam_step(groups)
+            self.k.adam_step(groups, guard=self._guard)
 
     # ---------------------------------------------------------------- densification (upstream)
     def _append(self, new: dict):

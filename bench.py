@@ -307,12 +307,14 @@ def main():
         kernel_name = {"blend_fwd": "blend_forward_kernel", "blend_bwd": "blend_backward_kernel",
                        "preprocess": "preprocess_kernel", "preprocess_bwd": "preprocess_backward_kernel"}.get(dom, dom)
         pmc = pmc_record(kernel_name, args.config)
-        # the roofline that binds the dominant kernel: the blend loops issue VALU work per
-        # (pixel, record) pair and reuse LDS-staged records 256x per tile, so they are VALU-issue
-        # bound; achieved / peak / frac below are their HBM figures (the contract's
-        # fields), valu_issue the binding ones
-        bound = "valu" if dom in ("blend_fwd", "blend_bwd") else "hbm"
-        result["roofline"] = {"bound": bound, "kernel": kernel_name, "achieved": round(achieved, 2),
+        # The contract's fields (bound / achieved / peak / unit / frac / traffic) are all the HBM
+        # roofline of the dominant kernel, consistently.  The blend loops issue VALU work per
+        # (pixel, record) pair and reuse LDS-staged records 256x per tile, so the roofline that
+        # BINDS them is VALU issue: `binding` names it and `valu_issue` carries its
+        # own achieved / peak / frac.
+        binding = "valu_issue" if dom in ("blend_fwd", "blend_bwd") else "hbm"
+        result["roofline"] = {"bound": "hbm", "binding": binding, "kernel": kernel_name,
+                              "achieved": round(achieved, 2),
                               "lib_stamp": (lib_stamp() or "")[:16],
                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                               # PMC passes are of the N = 1 launch; a band launch has no committed counts
@@ -325,8 +327,9 @@ def main():
             slots = VALU_ISSUE_PER_S * mean_ms * 1e-3
             result["roofline"]["valu_issue"] = {
                 "insts_per_launch": pmc["valu_insts_per_launch"],
-                "frac": round(pmc["valu_insts_per_launch"] / slots, 4),
-                "peak_insts_per_s": VALU_ISSUE_PER_S}
+                "achieved": round(pmc["valu_insts_per_launch"] / (mean_ms * 1e-3), 1),
+                "peak": VALU_ISSUE_PER_S, "unit": "wave64 VALU insts/s",
+                "frac": round(pmc["valu_insts_per_launch"] / slots, 4)}
         total_alg = sum(alg.values())
         result["pipeline_roofline"] = {
             "algorithmic_bytes_per_step": int(total_alg),
@@ -357,7 +360,12 @@ def main():
                                   f"oracle, median of 3 after 1 warm-up ({', '.join(f'{x:.2f}' for x in times)} s; "
                                   f"OpenMP {cores} threads)",
                                   "cpu_model": cpu_model(), "nproc": os.cpu_count(),
-                                  "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+                                  "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+                                  # the GPU box grants this job OMP_NUM_THREADS host threads (the
+                                  # harness sets 16 per GPU and forbids raising it); nproc counts
+                                  # the whole machine.  A whole-machine figure is an estimate,
+                                  # linear in threads (an upper bound for the CPU):
+                                  "full_machine_linear_estimate": round(os.cpu_count() / cores / cpu_s, 4)}
         f6, b1 = pmc_record("blend_forward_kernel", args.config), pmc_record("blend_backward_kernel", args.config)
         if "roofline" in result and "valu_insts_per_launch" in f6 and "valu_insts_per_launch" in b1:
             pairs = f.state.forward_pairs()

@@ -75,12 +75,25 @@ typedef struct gsr_adam_group {
  * to GSR_ADAM_MAX_GROUPS groups in ONE launch; `groups` is a HOST array. */
 int gsr_adam_step(const gsr_adam_group* groups, int32_t ngroups, float beta1, float beta2, float eps,
                   void* stream);
+/* The same step behind a device-side guard: it is skipped ON THE DEVICE when
+ * *guard_k > guard_cap (guard_k NULL: never skipped).  guard_k is the forward's instance count K
+ * (gsr_view(GSR_VIEW_COUNTS) word 0, the scan's counter: the true K, not clamped) and guard_cap
+ * the max_rendered bound that render ran under.  A render above its bound was truncated; a
+ * training loop that renders without a per-iteration host read of K passes them so that the
+ * truncated iteration's update is dropped instead of applied (the groups' step counts the host
+ * already advanced are not rolled back). */
+int gsr_adam_step_guarded(const gsr_adam_group* groups, int32_t ngroups, float beta1, float beta2, float eps,
+                          const uint32_t* guard_k, uint32_t guard_cap, void* stream);
 
 /* Densification statistics for the visible Gaussians (radii > 0):
  *   max_radii2D = max(max_radii2D, radii); grad_accum += |dL/dmeans2D[:, :2]|; denom += 1.
  * dmeans2D: P x 3 (the rasterizer's dL_dmeans2D, the reference's viewspace_points grad). */
 int gsr_densify_stats(const int32_t* radii, const float* dmeans2D, int32_t P, float* max_radii2D,
                       float* grad_accum, float* denom, void* stream);
+/* ... skipped on the device when *guard_k > guard_cap (as gsr_adam_step_guarded). */
+int gsr_densify_stats_guarded(const int32_t* radii, const float* dmeans2D, int32_t P, float* max_radii2D,
+                              float* grad_accum, float* denom, const uint32_t* guard_k, uint32_t guard_cap,
+                              void* stream);
 
 /* Stream compaction: idx_out[0 .. count) = the i with mask[i] != 0, ascending; *count_out
  * (device int32).  scratch: gsr_compact_scratch_bytes(n). */

@@ -1,0 +1,45 @@
+"""Write a GSRLOOP1 scene file for the C++ training loop (lib/gsr_train_loop) and exit, so that
+the loop runs as its own process (e.g. under rocprofv3 --kernel-trace).  Used to size the
+configs[4] test (tests/test_gpu_train_loop.py::test_configs4_at_scale): point count over a
+30k-iteration run and the per-kernel split of an iteration at ~6M Gaussians.
+
+usage: python scripts/loop_probe.py OUT.bin [--gt N] [--init N] [--size WxH] [--views V]
+                                    [--iters N] [--texture T] [--gt-scale S] [--progress N]
+"""
+import argparse
+import importlib
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PKG = "3d_gaussian_splatting_amd"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("out")
+    ap.add_argument("--gt", type=int, default=8_000_000)
+    ap.add_argument("--init", type=int, default=6_000_000)
+    ap.add_argument("--size", default="1280x832")
+    ap.add_argument("--views", type=int, default=48)
+    ap.add_argument("--iters", type=int, default=30000)
+    ap.add_argument("--texture", type=float, default=1.0)
+    ap.add_argument("--gt-scale", type=float, default=0.012)
+    ap.add_argument("--progress", type=int, default=1000)
+    a = ap.parse_args()
+    L = importlib.import_module(f"{PKG}.train_loop")
+    T = importlib.import_module(f"{PKG}.trainer")
+    W, H = (int(v) for v in a.size.split("x"))
+    t0 = time.perf_counter()
+    scene = L.synthetic_scene(a.gt, a.init, a.views, W, H, seed=0, texture=a.texture, gt_scale=a.gt_scale)
+    t1 = time.perf_counter()
+    L.write_scene(a.out, scene, a.iters, T.OptimizationParams(iterations=a.iters), max_sh_degree=3,
+                  log_every=500, progress_every=a.progress)
+    print(f"scene {a.gt} gt / {a.init} init, {a.views} views {W}x{H}: built {t1 - t0:.1f} s, "
+          f"written {time.perf_counter() - t1:.1f} s -> {a.out}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -255,9 +255,10 @@ int main(int argc, char** argv) {
                 loss.backward();
                 {
                     torch::NoGradGuard ng;
+                    // guarded by the render: skipped on the device if it overflowed its bound
                     gsr::densify_stats(out.radii, out.viewspace_points.grad(), core.max_radii2D_,
-                                       core.xyz_gradient_accum_, core.denom_);
-                    gsr::fused_adam_step(core.optimizers_);
+                                       core.xyz_gradient_accum_, core.denom_, &out);
+                    gsr::fused_adam_step(core.optimizers_, &out);
                 }
                 for (auto& kv : core.optimizers_) kv.second->zero_grad();
                 stats.push_back(st);

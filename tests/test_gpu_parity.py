@@ -383,6 +383,33 @@ def test_deterministic(rast):
         assert torch.equal(ga[k], gb[k]), k
 
 
+def test_sh_rows_at_allocation_end(rast):
+    """F1 and B2 stage the SH-rest rows by buffer-load-to-LDS DMA in 1-KB pieces; the last
+    block's pieces run past its rows, and the descriptor's range check must drop them (the
+    whole offset is in voffset).  Here sh_rest ends exactly at the end of a 2-MiB-multiple
+    allocation (the caching allocator hands such sizes out whole), with P % 256 != 0, and the
+    results must equal the same scene from ordinary tensors bit for bit."""
+    gr, sc = pkg("graphics"), pkg("scene")
+    cam = gr.synthetic_camera(640, 480)
+    P = 256 * 40 + 7
+    s = sc.make_scene(cam, P, max_sh_degree=3, seed=11)
+    dpix = sc.make_dL_dpix(cam, seed=12)
+    rows = s.sh_rest.numel()
+    total = (rows * 4 + (2 << 20) - 1) // (2 << 20) * (2 << 20) // 4
+    big = torch.zeros(total, dtype=torch.float32, device="cuda")
+    tail = big[total - rows:].view(s.sh_rest.shape)
+    tail.copy_(s.sh_rest)
+    assert tail.data_ptr() + rows * 4 == big.data_ptr() + total * 4
+    base = (cam, s.means3D, s.opacities, s.scales, s.rotations, s.sh_dc)
+    a = rast.forward(*base, s.sh_rest, sh_degree=3)
+    b = rast.forward(*base, tail, sh_degree=3)
+    torch.cuda.synchronize()
+    assert torch.equal(a.color, b.color)
+    ga, gb = rast.backward(a, dpix), rast.backward(b, dpix)
+    for k in ga:
+        assert torch.equal(ga[k], gb[k]), k
+
+
 def test_full_size_properties(rast):
     """1M Gaussians at 1080p (BASELINE configs[2]): size-independent properties -- canonical
     sortedness of (tile, depth bits, gid), ranges consistent, transmittance in [0,1]."""

@@ -120,6 +120,34 @@ def test_densify_stats(K):
     np.testing.assert_array_equal(td.cpu().numpy(), den)
 
 
+def test_step_guard_skips_truncated_iterations(K):
+    """gsr_adam_step_guarded / gsr_densify_stats_guarded: with the render's K above the bound it
+    ran under, nothing changes (the truncated iteration is dropped on the device); at or below
+    it, the guarded calls equal the unguarded ones bit for bit."""
+    rng = np.random.default_rng(11)
+    P = 5003
+    p0 = rng.standard_normal((P, 3)).astype(np.float32)
+    g = (rng.standard_normal((P, 3)) * 1e-2).astype(np.float32)
+    radii = rng.integers(0, 30, P).astype(np.int32)
+    dm = (rng.standard_normal((P, 3)) * 1e-3).astype(np.float32)
+    acts = pkg("trainer").ACTS
+    outs = {}
+    for label, k in (("over", 1001), ("at", 1000), ("none", None)):
+        p, m, v = _t(p0), torch.zeros(P, 3, device=DEV), torch.zeros(P, 3, device=DEV)
+        stats = [torch.zeros(P, device=DEV) for _ in range(3)]
+        guard = None if k is None else (torch.tensor([k], dtype=torch.int32, device=DEV), 1000)
+        K.adam_step([dict(param=p, grad=_t(g), exp_avg=m, exp_avg_sq=v, act=acts["xyz"], step=1, lr=1e-3)],
+                    guard=guard)
+        K.densify_stats(torch.as_tensor(radii, device=DEV), _t(dm), *stats, guard=guard)
+        outs[label] = [p, m, v] + stats
+    for t, t0 in zip(outs["over"], [_t(p0)] + [torch.zeros_like(outs["over"][1])] * 2 +
+                     [torch.zeros(P, device=DEV)] * 3):
+        assert torch.equal(t, t0)
+    for a, b in zip(outs["at"], outs["none"]):
+        assert torch.equal(a, b)
+    assert not torch.equal(outs["at"][0], _t(p0))
+
+
 @pytest.mark.parametrize("n,frac", [(1, 1.0), (1023, 0.5), (1024, 0.0), (4097, 1.0), (1_000_003, 0.3)])
 def test_compact_and_gather_bit_exact(K, n, frac):
     g = torch.Generator().manual_seed(n)

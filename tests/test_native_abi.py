@@ -11,10 +11,11 @@ from conftest import ROOT, pkg
 
 HEADER = os.path.join(ROOT, "include", "gsr", "gsr.h")
 TRAIN_HEADER = os.path.join(ROOT, "include", "gsr", "gsr_train.h")
+COMM_HEADER = os.path.join(ROOT, "include", "gsr", "gsr_comm.h")
 
 
 def declared_functions(header=None):
-    headers = [header] if header else [HEADER, TRAIN_HEADER]
+    headers = [header] if header else [HEADER, TRAIN_HEADER, COMM_HEADER]
     out = set()
     for h in headers:
         text = open(h).read()
@@ -26,6 +27,23 @@ def test_header_declares_expected_entry_points():
     native = pkg("native")
     assert set(native.EXPORTS) == set(declared_functions(HEADER)), declared_functions(HEADER)
     assert set(native.TRAIN_EXPORTS) == set(declared_functions(TRAIN_HEADER)), declared_functions(TRAIN_HEADER)
+    assert set(native.COMM_EXPORTS) == set(declared_functions(COMM_HEADER)), declared_functions(COMM_HEADER)
+
+
+def test_comm_abi_validation_without_gpu():
+    """gsr_comm.h: the RCCL transport's entry points reject bad arguments before touching a
+    device; the unique-id size matches the header."""
+    native = pkg("native")
+    L = native.load_hip()
+    text = open(COMM_HEADER).read()
+    assert int(re.search(r"#define GSR_COMM_ID_BYTES (\d+)", text).group(1)) == native.COMM_ID_BYTES
+    comm = ctypes.c_void_p()
+    id_ = (ctypes.c_uint8 * native.COMM_ID_BYTES)()
+    L.gsr_comm_init.restype = ctypes.c_int
+    assert L.gsr_comm_init(ctypes.byref(comm), id_, 2, 5) < 0 and "rank" in native.last_error()
+    assert L.gsr_comm_init(None, id_, 1, 0) < 0
+    assert L.gsr_comm_all_to_all(None, None, None, ctypes.c_size_t(0), None) < 0
+    assert L.gsr_comm_destroy(None) == 0
 
 
 def test_train_abi_validation_without_gpu():
@@ -186,7 +204,7 @@ def test_product_does_not_reference_oracle():
                                      r"sys\.path[^\n]*oracle", text, re.M), f
 
 
-@pytest.mark.parametrize("name", ["gsr_dropin", "gsr_train_loop"])
+@pytest.mark.parametrize("name", ["gsr_dropin", "gsr_train_loop", "gsr_shard_step"])
 def test_dropin_executable_has_one_hip_runtime(name):
     """The C++ executables (lib/gsr_dropin: render(); lib/gsr_train_loop: the training loop)
     must resolve libgsr_hip.so's libamdhip64.so.7 to the torch wheel's bundled runtime, not load
