@@ -204,6 +204,9 @@ void band(const gsr_camera* cam, const gsr_raster_settings* rs, int* y0, int* y1
 // received splat slots) indexed; cap: the binning's instance capacity.
 struct Views {
     uint32_t *depth_key, *tiles, *flags, *offsets, *partials, *lookback;
+    bool presort;                                          // gsr_internal.h use_presort
+    uint32_t *dk0, *dv0, *dk1, *dv1, *dhist, *rtiles;      // presort only
+    uint4* rrect;
     float4* rec;
     uint4* rect;
     uint2* ranges;
@@ -227,6 +230,16 @@ Views views(const gsr_camera* cam, long long n, const gsr_buffers* b) {
     v.offsets = at<uint32_t>(b->geom, gl.offsets);
     v.partials = at<uint32_t>(b->geom, gl.partials);
     v.lookback = at<uint32_t>(b->geom, gl.lookback);
+    v.presort = use_presort(n);
+    if (v.presort) {
+        v.dk0 = at<uint32_t>(b->geom, gl.dk0);
+        v.dv0 = at<uint32_t>(b->geom, gl.dv0);
+        v.dk1 = at<uint32_t>(b->geom, gl.dk1);
+        v.dv1 = at<uint32_t>(b->geom, gl.dv1);
+        v.dhist = at<uint32_t>(b->geom, gl.dhist);
+        v.rtiles = at<uint32_t>(b->geom, gl.rtiles);
+        v.rrect = at<uint4>(b->geom, gl.rrect);
+    }
     v.ranges = at<uint2>(b->image, il.ranges);
     v.counters = at<uint32_t>(b->image, il.counters);
     v.K_dev = v.counters + kTotalSlot;
@@ -306,6 +319,13 @@ int fwd_phase1(FwdJob& j, gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_image, voi
     }
     GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(v.ranges, 0, il.ovf - il.ranges, stream), "clear ranges");
     if (int e = pre(v)) return e;
+    if (v.presort) {  // global (depth, gid) order, then the scan of tiles_touched in that order
+        GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_depth_presort(v.depth_key, v.tiles, v.rect, (int)j.n, v.dk0, v.dv0,
+                                                             v.dk1, v.dv1, v.dhist, v.rtiles, v.rrect, stream),
+                  "depth presort");
+        GSR_STAGE(GSR_STAGE_SCAN, launch_scan(v.rtiles, (int)j.n, v.offsets, v.partials, v.K_dev, stream), "scan");
+        return 0;
+    }
     GSR_STAGE(GSR_STAGE_SCAN, launch_scan(v.tiles, (int)j.n, v.offsets, v.partials, v.K_dev, stream), "scan");
     return 0;
 }
@@ -321,9 +341,14 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
     if (!bufs->binning) return fail(-2, "allocation failed (binning, %lld instances)", cap);
     const Views v = views(cam, j.n, bufs);
     const int tiles = j.gx * j.gy, ntiles = (j.ty1 - j.ty0) * j.gx;
-    GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate(v.tiles, v.rect, (int)j.n, j.gx, j.ty0, v.offsets, v.lookback, v.kA,
-                                                    v.vA, cap, v.K_dev, stream),
-              "duplicate");
+    if (v.presort)
+        GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate_ranked(v.rtiles, v.rrect, v.rect, (int)j.n, j.gx, j.ty0,
+                                                               v.offsets, v.kA, v.vA, cap, stream),
+                  "duplicate (rank order)");
+    else
+        GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate(v.tiles, v.rect, (int)j.n, j.gx, j.ty0, v.offsets, v.lookback,
+                                                        v.kA, v.vA, cap, v.K_dev, stream),
+                  "duplicate");
     if (cap > 0) {
         int which = -1;
         GSR_STAGE(GSR_STAGE_TILE_SORT, radix_sort(v.kA, v.vA, v.kB, v.vB, v.kA, v.vA, cap, v.K_dev, tile_bits(tiles),
@@ -332,7 +357,9 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
         // pass 1 writes (kB, vB), the next (kA, vA): which == 0 means the result is in (kB, vB)
         if ((which == 0) != (v.sorted_tile == v.kB)) return fail(-12, "tile sort ended in an unexpected buffer");
         GSR_STAGE(GSR_STAGE_FINALIZE, launch_finalize(v.sorted_tile, cap, v.K_dev, v.ranges, stream), "finalize");
-        GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_tile_depth_sort(v.ranges, j.ty0 * j.gx, ntiles, cap, v.depth_key,
+        // presort mode: the stable tile sort of rank-ordered instances is already canonical
+        if (!v.presort)
+            GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_tile_depth_sort(v.ranges, j.ty0 * j.gx, ntiles, cap, v.depth_key,
                                                                v.sorted_gid, v.ovf, v.counters + kOvfCountSlot, v.ovf2,
                                                                v.counters + kOvf2CountSlot, v.done, v.free_k,
                                                                v.free_v, stream),
@@ -396,7 +423,7 @@ int blend_backward(const gsr_camera* cam, const gsr_raster_settings* rs, const g
                                                          stream),
               "blend backward");
     GSR_STAGE(GSR_STAGE_GATHER, launch_gather_grad2d(v.offsets, partial, v.rec, cam->width, cam->height, cap, (int)n,
-                                                     grad2d, stream),
+                                                     v.presort ? v.rrect : nullptr, grad2d, stream),
               "gather grad2d");
     return 0;
 }

@@ -538,13 +538,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
         uint64_t todo = __ballot((smask & live) != 0u);
         int visited = 0, parked = 0;
         uint32_t kpack = 0;  // batch slots of the parked records, 6 bits each
-        while (todo) {
-            const int k = __builtin_ctzll(todo);
-            todo &= todo - 1;
+#ifndef GSR_B1_PREFETCH
+#define GSR_B1_PREFETCH 0
+#endif
+        // one visited record (batch slot k): its stripes, then its moments parked / flushed;
+        // true when every pixel of the tile has finished
+        auto record = [&](const int k, const float4 r0, const float4 r1, const float4 r2) -> bool {
             const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)smask, k) & live;
-            const float4 r0 = srec[3 * k + 0];
-            const float4 r1 = srec[3 * k + 1];
-            const float4 r2 = srec[3 * k + 2];
             const float dx = r0.x - pfx;
             const float bdx = r0.w * dx;
             const float K = fmaf(r0.z * dx, dx, r2.w);
@@ -606,9 +606,45 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
 #pragma unroll
                 for (int p = 0; p < kPPL; ++p) lv |= __any(T[p] > 0.0f) ? (1u << p) : 0u;
                 live = lv;
-                if (live == 0) break;
+                if (live == 0) return true;
+            }
+            return false;
+        };
+#if GSR_B1_PREFETCH
+        // software pipeline, unrolled by two so the two records' registers never need copies:
+        // the next visited record's LDS reads are issued before the current one's stripes run
+        if (todo) {
+            int ka = __builtin_ctzll(todo);
+            float4 a0 = srec[3 * ka + 0], a1 = srec[3 * ka + 1], a2 = srec[3 * ka + 2];
+            while (true) {
+                todo &= todo - 1;
+                int kb = -1;
+                float4 b0, b1, b2;
+                if (todo) {  // wave-uniform
+                    kb = __builtin_ctzll(todo);
+                    b0 = srec[3 * kb + 0];
+                    b1 = srec[3 * kb + 1];
+                    b2 = srec[3 * kb + 2];
+                }
+                if (record(ka, a0, a1, a2) || kb < 0) break;
+                todo &= todo - 1;
+                ka = -1;
+                if (todo) {
+                    ka = __builtin_ctzll(todo);
+                    a0 = srec[3 * ka + 0];
+                    a1 = srec[3 * ka + 1];
+                    a2 = srec[3 * ka + 2];
+                }
+                if (record(kb, b0, b1, b2) || ka < 0) break;
             }
         }
+#else
+        while (todo) {
+            const int k = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            if (record(k, srec[3 * k + 0], srec[3 * k + 1], srec[3 * k + 2])) break;
+        }
+#endif
         if (parked) park_flush(qpark, sjl, kpack, parked, p8f, p1, fl, lane);
         __syncthreads();  // srec / qpark are rewritten by the next batch
     }

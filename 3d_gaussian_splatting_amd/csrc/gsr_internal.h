@@ -54,8 +54,22 @@ inline size_t sort_scratch_words(long long n) { return 256 * ((size_t)radix_bloc
 
 // lengths and emission index bases are u32: n instances must stay below 2^32, and the blend's
 // per-tile index arithmetic below 2^31
+// Global depth pre-sort: at and above kPresortMin Gaussians (or splat slots) the binning sorts
+// the Gaussians by their 32-bit depth key once (stable LSD, gid as value) and emits the
+// instances in that (depth, gid) rank order, so the stable tile-key sort that follows leaves
+// every tile's slice already in canonical (tile, depth, gid) order and the per-tile depth sort
+// goes away.  Each rank's binning payload (tiles, rect, gid) is gathered once into rank order
+// (rtiles / rrect) so the scan, F3 and the gather stream it coalesced.  Below the threshold the
+// fused look-back scan + duplicate and the per-tile sort are kept (small scenes).
+#ifndef GSR_PRESORT_MIN
+#define GSR_PRESORT_MIN ((1 << 19) + 1)
+#endif
+constexpr long long kPresortMin = GSR_PRESORT_MIN;
+inline bool use_presort(long long n) { return n >= kPresortMin; }
+
 struct GeomLayout {
     size_t depth_key, tiles, flags, rec, rect, offsets, partials, lookback, total;
+    size_t dk0 = 0, dv0 = 0, dk1 = 0, dv1 = 0, dhist = 0, rtiles = 0, rrect = 0;  // presort only
     GeomLayout(long long P) {
         size_t o = 0, n = (size_t)(P > 0 ? P : 1);
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
@@ -67,6 +81,15 @@ struct GeomLayout {
         offsets = take(4 * n);
         partials = take(4 * ((size_t)sort_blocks(n) + 16));  // three-kernel scan
         lookback = take(4 * (16 + (n + 255) / 256));        // fused scan + duplicate
+        if (use_presort(P)) {
+            dk0 = take(4 * n);
+            dv0 = take(4 * n);
+            dk1 = take(4 * n);
+            dv1 = take(4 * n);
+            dhist = take(4 * sort_scratch_words(n));
+            rtiles = take(4 * n);   // tiles_touched in rank order
+            rrect = take(16 * n);   // uint4 (rect lo, rect hi, gid, 0) in rank order
+        }
         total = o;
     }
 };

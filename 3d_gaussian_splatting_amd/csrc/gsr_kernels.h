@@ -56,6 +56,14 @@ int launch_duplicate(const uint32_t* tiles, uint4* rect, int n, int grid_x, int 
 // queued in `ovf` (count at *ovf_count, zeroed) for 8192-entry blocks, longer ones again in
 // ovf2 for a global-memory form using scratch_hi / scratch_lo (K u32 each, free after the tile
 // sort).  K: the binning's capacity (it sizes the LDS form from the mean slice).
+// Presort mode (gsr_internal.h use_presort): the P depth keys sorted (stable, gid values), then
+// each rank's (tiles, rect, gid) gathered into rank order.
+int launch_depth_presort(const uint32_t* depth_key, const uint32_t* tiles, const uint4* rect, int n, uint32_t* dk0,
+                         uint32_t* dv0, uint32_t* dk1, uint32_t* dv1, uint32_t* hist, uint32_t* rtiles, uint4* rrect,
+                         hipStream_t s);
+// F3 in rank order (offsets = the scan of rtiles); writes inst_start into rect[gid].z.
+int launch_duplicate_ranked(const uint32_t* rtiles, const uint4* rrect, uint4* rect, int n, int grid_x, int ty0,
+                            const uint32_t* offsets, uint32_t* tkey, uint32_t* tgid, long long cap, hipStream_t s);
 int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long K, const uint32_t* depth_key,
                            uint32_t* gid, uint32_t* ovf, uint32_t* ovf_count, uint32_t* ovf2, uint32_t* ovf2_count,
                            uint32_t* done, uint32_t* scratch_hi, uint32_t* scratch_lo,
@@ -90,8 +98,9 @@ constexpr float kLn2 = 0.6931471805599453f;  // conic A = -2 ln2 a', B = -ln2 b'
 
 // sum partials per Gaussian (emission order) -> grad2d (kPart floats per Gaussian; zeros for
 // culled Gaussians).  offsets: the inclusive tile scan in gid order; partial: PartLayout(cap).
+// rrect: the rank-order payload in presort mode (offsets then in rank order), else nullptr
 int launch_gather_grad2d(const uint32_t* offsets, const float* partial, const float4* rec, int W, int H,
-                         long long cap, int P, float* grad2d, hipStream_t s);
+                         long long cap, int P, const uint4* rrect, float* grad2d, hipStream_t s);
 
 struct GradOut {
     float *means2D, *conic, *opac, *colors, *means3D, *sh_dc, *sh_rest, *scales, *rots, *cov3D;

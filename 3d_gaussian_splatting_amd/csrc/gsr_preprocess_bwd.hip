@@ -39,12 +39,15 @@ constexpr float kC1 = 0.4886025119029199f;
 // its blend record.  The 48-B result lands at grad2d[gid].
 constexpr int kGatherWin = 512;
 
+// rrect (presort mode): index i is a depth rank whose emission range the rank-order offsets give;
+// its Gaussian (record read, grad2d row written) is rrect[i].z.  nullptr: i is the gid itself.
 __global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __restrict__ offsets,
                                                             const float4* __restrict__ p8,
                                                             const float* __restrict__ p1,
                                                             const uint8_t* __restrict__ fl,
                                                             const float4* __restrict__ rec, float hw, float hh,
-                                                            int P, uint32_t cap, float* __restrict__ grad2d) {
+                                                            int P, uint32_t cap, const uint4* __restrict__ rrect,
+                                                            float* __restrict__ grad2d) {
     __shared__ float4 w8[2 * kGatherWin];
     __shared__ float w1[kGatherWin];
     __shared__ uint32_t wv[kGatherWin / 4];
@@ -55,11 +58,12 @@ __global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __re
     const uint32_t J0 = g0 ? off(g0 - 1) : 0u, J1 = off(gl - 1);
     const uint32_t s = g < P ? (g ? off(g - 1) : 0u) : 0u;
     const uint32_t e = g < P ? off(g) : 0u;
+    const uint32_t gid = g < P ? (rrect ? rrect[g].z : (uint32_t)g) : 0u;
     // the Gaussian's conic and opacity, loaded before the window loop (latency overlaps it)
     float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0;
     if (g < P && e > s) {
-        q0 = rec[3 * (size_t)g];
-        q1 = rec[3 * (size_t)g + 1];
+        q0 = rec[3 * (size_t)gid];
+        q1 = rec[3 * (size_t)gid + 1];
     }
     float a[9];
 #pragma unroll
@@ -86,7 +90,7 @@ __global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __re
     // moments -> d mean2D (NDC), d conic, d opacity (sum G dL/dalpha = S0 / o), d colour
     const float A = -2.0f * kLn2 * q0.z, B = -kLn2 * q0.w, C = -2.0f * kLn2 * q1.x;
     const float Sx = a[0], Sy = a[1], S0 = a[5];
-    float4* dst = reinterpret_cast<float4*>(grad2d + (size_t)kPart * g);
+    float4* dst = reinterpret_cast<float4*>(grad2d + (size_t)kPart * gid);
     dst[0] = make_float4((-A * Sx - B * Sy) * hw, (-C * Sy - B * Sx) * hh, -0.5f * a[2], -a[3]);
     dst[1] = make_float4(-0.5f * a[4], S0 != 0.0f ? S0 / q1.y : 0.0f, a[6], a[7]);
     dst[2] = make_float4(a[8], 0.f, 0.f, 0.f);
@@ -479,14 +483,14 @@ __global__ __launch_bounds__(256) void preprocess_backward_kernel(
 }  // namespace
 
 int launch_gather_grad2d(const uint32_t* offsets, const float* partial, const float4* rec, int W, int H,
-                         long long cap, int P, float* grad2d, hipStream_t s) {
+                         long long cap, int P, const uint4* rrect, float* grad2d, hipStream_t s) {
     if (P <= 0) return 0;
     const PartLayout pl(cap);
     const char* base = reinterpret_cast<const char*>(partial);
     hipLaunchKernelGGL(gather_grad2d_kernel, dim3(div_up(P, 256)), dim3(256), 0, s, offsets,
                        reinterpret_cast<const float4*>(base + pl.p8), reinterpret_cast<const float*>(base + pl.p1),
                        reinterpret_cast<const uint8_t*>(base + pl.fl), rec, 0.5f * (float)W, 0.5f * (float)H, P,
-                       (uint32_t)cap, grad2d);
+                       (uint32_t)cap, rrect, grad2d);
     return (int)hipGetLastError();
 }
 

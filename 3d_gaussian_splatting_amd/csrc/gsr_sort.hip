@@ -494,25 +494,36 @@ __global__ __launch_bounds__(256) void scan_duplicate_kernel(const uint32_t* __r
     emit_wave(s_start[w], s_g[w], s_w[w], s_x0[w], s_y0[w], excl + wbase, wsum[w], grid_x, cap, tkey, tgid);
 }
 
+// RANKED (presort mode): lane i is depth rank i; its tiles / rect / gid come from the rank-order
+// payload (rtiles / rrect, coalesced) and inst_start goes to rect[gid] (one scattered word).
+template <bool RANKED>
 __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restrict__ offsets,
                                                         const uint32_t* __restrict__ tiles,
-                                                        uint4* __restrict__ rect, int P, int grid_x, int ty0,
+                                                        uint4* __restrict__ rect, const uint4* __restrict__ rrect,
+                                                        int P, int grid_x, int ty0,
                                                         uint32_t* __restrict__ tkey, uint32_t* __restrict__ tgid,
                                                         long long cap) {
     __shared__ uint32_t s_start[kWaves][64], s_g[kWaves][64], s_w[kWaves][64], s_x0[kWaves][64],
         s_y0[kWaves][64];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const int g = blockIdx.x * 256 + tid;
-    const bool valid = g < P;
-    uint32_t nt = 0, end = 0;
+    const int i = blockIdx.x * 256 + tid;  // gid, or depth rank (RANKED)
+    const bool valid = i < P;
+    uint32_t nt = 0, end = 0, g = (uint32_t)i;
     if (valid) {
-        nt = tiles[g];
-        end = offsets[g];
+        nt = tiles[i];
+        end = offsets[i];
     }
     uint32_t minx = 0, maxx = 0, y0 = 0;
     if (nt) {
-        rect[g].z = end - nt;  // inst_start
-        const uint4 rr = rect[g];
+        uint4 rr;
+        if (RANKED) {
+            rr = rrect[i];
+            g = rr.z;
+            rect[g].z = end - nt;  // inst_start
+        } else {
+            rect[g].z = end - nt;  // inst_start
+            rr = rect[g];
+        }
         minx = rr.x & 0xFFFF;
         maxx = rr.y & 0xFFFF;
         const uint32_t miny = rr.x >> 16;
@@ -524,7 +535,7 @@ __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restri
     const int last_lane = 63 - __builtin_clzll(vmask);
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)end, last_lane) - first;
     s_start[w][lane] = valid ? end - nt - first : 0xFFFFFFFFu;
-    s_g[w][lane] = (uint32_t)g;
+    s_g[w][lane] = g;
     s_w[w][lane] = maxx - minx;
     s_x0[w][lane] = minx;
     s_y0[w][lane] = y0;
@@ -532,6 +543,29 @@ __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restri
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     emit_wave(s_start[w], s_g[w], s_w[w], s_x0[w], s_y0[w], first, total, grid_x, cap, tkey, tgid);
+}
+
+// ---- presort: each depth rank's binning payload, gathered once into rank order ----
+// rtiles[r] = tiles[g], rrect[r] = (rect lo, rect hi, g, 0) for g = the sorted gid at rank r.  The
+// reads are random (16 B per visible Gaussian, L2 / MALL-resident), the writes coalesced; the
+// scan, F3 and the gather then stream the payload instead of each making random reads.
+__global__ __launch_bounds__(256) void rank_payload_kernel(const uint32_t* __restrict__ sgid,
+                                                           const uint32_t* __restrict__ tiles,
+                                                           const uint4* __restrict__ rect, int n,
+                                                           uint32_t* __restrict__ rtiles,
+                                                           uint4* __restrict__ rrect) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= n) return;
+    const uint32_t g = sgid[r];
+    const uint32_t nt = tiles[g];
+    uint4 q = make_uint4(0u, 0u, g, 0u);
+    if (nt) {
+        const uint4 rr = rect[g];
+        q.x = rr.x;
+        q.y = rr.y;
+    }
+    rtiles[r] = nt;
+    rrect[r] = q;
 }
 
 // ---- F5 finalize: tile ranges from the sorted keys ----
@@ -950,8 +984,27 @@ int launch_duplicate(const uint32_t* tiles, uint4* rect, int n, int grid_x, int 
                            tkey, tgid, cap, lookback + 16, lookback, total_out);
         return (int)hipGetLastError();
     }
-    hipLaunchKernelGGL(duplicate_kernel, dim3(div_up(n, 256)), dim3(256), 0, s, offsets, tiles, rect, n, grid_x, ty0,
-                       tkey, tgid, cap);
+    hipLaunchKernelGGL(duplicate_kernel<false>, dim3(div_up(n, 256)), dim3(256), 0, s, offsets, tiles, rect,
+                       nullptr, n, grid_x, ty0, tkey, tgid, cap);
+    return (int)hipGetLastError();
+}
+
+int launch_depth_presort(const uint32_t* depth_key, const uint32_t* tiles, const uint4* rect, int n, uint32_t* dk0,
+                         uint32_t* dv0, uint32_t* dk1, uint32_t* dv1, uint32_t* hist, uint32_t* rtiles, uint4* rrect,
+                         hipStream_t s) {
+    if (n <= 0) return 0;
+    int which = -1;  // 4 passes of 8 bits: the result lands in (dk1, dv1)
+    if (int e = radix_sort(depth_key, nullptr, dk0, dv0, dk1, dv1, n, nullptr, 32, hist, &which, s)) return e;
+    const uint32_t* sgid = which == 0 ? dv0 : dv1;
+    hipLaunchKernelGGL(rank_payload_kernel, dim3(div_up(n, 256)), dim3(256), 0, s, sgid, tiles, rect, n, rtiles, rrect);
+    return (int)hipGetLastError();
+}
+
+int launch_duplicate_ranked(const uint32_t* rtiles, const uint4* rrect, uint4* rect, int n, int grid_x, int ty0,
+                            const uint32_t* offsets, uint32_t* tkey, uint32_t* tgid, long long cap, hipStream_t s) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(duplicate_kernel<true>, dim3(div_up(n, 256)), dim3(256), 0, s, offsets, rtiles, rect, rrect, n,
+                       grid_x, ty0, tkey, tgid, cap);
     return (int)hipGetLastError();
 }
 

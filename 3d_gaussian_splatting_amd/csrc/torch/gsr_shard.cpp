@@ -541,6 +541,12 @@ void ShardStep::poll(bool wait_all) {
 
 void ShardStep::check() { poll(true); }
 
+int64_t ShardStep::band_num_rendered() const {
+    void* k = const_cast<void*>(gsr_view(&ccam_, world_ * pair_cap_, &pool_->bufs, GSR_VIEW_COUNTS));
+    TORCH_CHECK(k != nullptr && steps_ > 0, "ShardStep: no step yet");
+    return (int64_t)(uint32_t)dev_view(k, 1, torch::kInt32).item<int32_t>();
+}
+
 ShardStep::Result ShardStep::step(const torch::Tensor& dL_dpix) {
     TORCH_CHECK(pair_cap_ > 0 && capacity_ > 0, "ShardStep: call plan() first");
     TORCH_CHECK(dL_dpix.is_cuda() && dL_dpix.scalar_type() == torch::kFloat32 && dL_dpix.is_contiguous() &&
@@ -665,6 +671,7 @@ void bind_shard(py::module& m) {
             py::arg("dL_dpix"))
         .def("check", &ShardStep::check, py::call_guard<py::gil_scoped_release>())
         .def("set_pair_cap", &ShardStep::set_pair_cap)
+        .def("band_num_rendered", &ShardStep::band_num_rendered)
         .def_property_readonly("rows", &ShardStep::rows)
         .def_property_readonly("pair_cap", &ShardStep::pair_cap)
         .def_property_readonly("capacity", &ShardStep::capacity)

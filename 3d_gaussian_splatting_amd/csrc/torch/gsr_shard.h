@@ -123,6 +123,8 @@ class ShardStep {
     int64_t g1() const { return g1_; }
     bool graph_active() const;
     int64_t steps() const { return steps_; }
+    // the last step's band instance count K (reads the device counter back: waits)
+    int64_t band_num_rendered() const;
     // test hook: force a (smaller) pair capacity after plan()
     void set_pair_cap(int pair_cap);
 

@@ -138,6 +138,41 @@ def cpu_model() -> str:
     return "unknown"
 
 
+class CppShard:
+    """bench's view of the C++ multi-GPU step (ext.ShardStep over ext.rccl_exchange): the same
+    attributes bands.ShardStep offers the reporting code below.  The RCCL unique id travels over
+    the torch.distributed group that the launcher already set up."""
+
+    class _Band:  # num_rendered of the band (read back after the timed loop)
+        def __init__(self, st):
+            self._st = st
+
+        @property
+        def num_rendered(self):
+            return int(self._st.band_num_rendered())
+
+    class _Shard:
+        def __init__(self, radii):
+            self.radii = radii
+
+    def __init__(self, cam, inputs, D, dist, rank, world):
+        ext = native.load_torch_ext()
+        uid = [ext.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        self.exchange = ext.rccl_exchange(uid[0], rank, world)
+        self.st = ext.ShardStep(self.exchange, R.ext_camera(cam), inputs, D, graph=True)
+        self.st.plan()
+        self.rank = rank
+        self.rows, self.pair_cap, self.capacity = list(self.st.rows), self.st.pair_cap, self.st.capacity
+        self.band_instances = list(self.st.band_instances)
+        self.g0, self.g1 = self.st.g0, self.st.g1
+        self.band = (self.rows[rank], self.rows[rank + 1])
+
+    def step(self, dpix):
+        img, g, radii = self.st.step(dpix)
+        return self._Band(self.st), g, self._Shard(radii)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -163,6 +198,9 @@ def main():
                          "densification statistics, fused Adam), SURVEY §8f")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank) or gloo (rehearsal: ranks may share a GPU)")
+    ap.add_argument("--dist-impl", default="cpp", choices=("cpp", "python"),
+                    help="N > 1 with --dist-backend nccl: the C++ gsr::ShardStep over RCCL with hipGraph "
+                         "replay (cpp), or bands.ShardStep over torch.distributed (python; always with gloo)")
     ap.add_argument("--exact-k", action="store_true",
                     help="size the binning from K every step (one host read per forward) instead of a bound")
     ap.add_argument("--lib", default=None, help="load this libgsr_hip.so instead of the in-tree one "
@@ -201,7 +239,15 @@ def main():
                   rotations=t(scene.rotations), sh_dc=t(scene.sh_dc), sh_rest=t(scene.sh_rest))
     dpix = t(dpix_np)
     gx, gy = cam.grid
-    if world > 1:
+    if world > 1 and args.dist_impl == "cpp" and args.dist_backend == "nccl":
+        # the C++ step (csrc/torch/gsr_shard.h) over RCCL, captured into a hipGraph on its first
+        # step and replayed: one graph launch per rank and step
+        plan = CppShard(cam, inputs, D, dist, rank, world)
+        band = plan.band
+
+        def step():
+            return plan.step(dpix)
+    elif world > 1:
         rast = R.ShardRasterizer(dev)
         plan = bands.ShardStep(rast, cam, inputs, D, dist).plan()
         band = plan.band
@@ -295,7 +341,9 @@ def main():
         "counts": {"visible": V, "num_rendered": K, "tiles": tiles},
     }
     if world > 1:
-        result["exchange"] = {"band_rows": plan.rows, "pair_cap": plan.pair_cap, "band_capacity": plan.capacity,
+        result["exchange"] = {"impl": ("C++ gsr::ShardStep over RCCL, hipGraph replay"
+                                       if isinstance(plan, CppShard) else "bands.ShardStep over torch.distributed"),
+                              "band_rows": plan.rows, "pair_cap": plan.pair_cap, "band_capacity": plan.capacity,
                               "band_instances": plan.band_instances, "counts_are": "rank 0's shard / band"}
     if stages and rank == 0 and dom_stage in live and live[dom_stage][1]:
         result["stage_ms"] = {k: round(ms / args.steps, 4) for k, (ms, n) in stages.items() if n}
