@@ -288,6 +288,7 @@ struct FwdJob {
     gsr_buffers* bufs;
     long long n = 0;  // Gaussians (or splat slots) indexed
     int ty0 = 0, ty1 = 0, gx = 0, gy = 0;
+    int vgy = 0, vh = 0;  // views mode: tile rows per view band, pixel rows per view (0: one image)
 };
 
 // Allocations (geometry from the caller when geom_ready), range / counter clears, background
@@ -366,7 +367,8 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
                   "per-tile depth order");
     }
     GSR_STAGE(GSR_STAGE_BLEND_FWD, launch_blend_forward(*cam, j.rs->bg, j.ty0, j.ty1, v.ranges, v.sorted_gid, v.rec,
-                                                        j.out_color, v.final_T, v.accum, v.term, v.ck, cap, stream),
+                                                        j.out_color, v.final_T, v.accum, v.term, v.ck, cap, stream,
+                                                        j.vgy, j.vh),
               "blend forward");
     return 0;
 }
@@ -405,7 +407,8 @@ int run_preprocess(const gsr_camera* cam, const gsr_gaussians* gs, int ty0, int 
 
 // B1 (+ the per-Gaussian gather into grad2d): shared by every backward entry point.
 int blend_backward(const gsr_camera* cam, const gsr_raster_settings* rs, const gsr_buffers* bufs, const float* dL_dpix,
-                   gsr_alloc_fn alloc_scratch, void* ctx, float* grad2d, hipStream_t stream, bool debug) {
+                   gsr_alloc_fn alloc_scratch, void* ctx, float* grad2d, hipStream_t stream, bool debug, int vgy = 0,
+                   int vh = 0) {
     if (!bufs || !bufs->geom || !bufs->image || !bufs->binning || !dL_dpix) return fail(-1, "missing forward buffers / dL_dpix");
     if (!grad2d) return fail(-1, "null grad2d");
     const long long n = bufs->n_local, cap = bufs->capacity;
@@ -420,9 +423,10 @@ int blend_backward(const gsr_camera* cam, const gsr_raster_settings* rs, const g
     GSR_STAGE(GSR_STAGE_MISC, launch_clear_flags(partial, cap, stream), "clear partial flags");
     GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.rect, v.rec,
                                                          v.final_T, v.accum, dL_dpix, partial, cap, v.term, v.ck,
-                                                         stream),
+                                                         stream, vgy, vh),
               "blend backward");
-    GSR_STAGE(GSR_STAGE_GATHER, launch_gather_grad2d(v.offsets, partial, v.rec, cam->width, cam->height, cap, (int)n,
+    GSR_STAGE(GSR_STAGE_GATHER, launch_gather_grad2d(v.offsets, partial, v.rec, cam->width, vgy > 0 ? vh : cam->height,
+                                                     cap, (int)n,
                                                      v.presort ? v.rrect : nullptr, grad2d, stream),
               "gather grad2d");
     return 0;
@@ -469,6 +473,26 @@ int band_rows_of(int32_t nbands, const int32_t* band_rows, int gy, BandRows& br)
             return fail(-1, "band_rows must be non-decreasing within [0, %d]", gy);
     }
     if (band_rows[0] != 0 || band_rows[nbands] != gy) return fail(-1, "band_rows must cover tile rows [0, %d)", gy);
+    return 0;
+}
+
+// Views mode: the tall camera whose tile rows stack the V views' bands (gsr.h gsr_forward_views)
+int views_camera(int32_t V, const gsr_camera* cams, const gsr_gaussians* gs, const gsr_raster_settings* rs,
+                 gsr_camera* tall) {
+    if (V < 1 || V > GSR_MAX_VIEWS || V > kMaxViews) return fail(-1, "views: 1..%d views, got %d", GSR_MAX_VIEWS, V);
+    if (!cams) return fail(-1, "views: null cameras");
+    for (int v = 0; v < V; ++v) {
+        if (int e = validate(&cams[v], gs, rs)) return e;
+        if (cams[v].width != cams[0].width || cams[v].height != cams[0].height)
+            return fail(-1, "views: every view must be %dx%d (view %d is %dx%d)", cams[0].width, cams[0].height, v,
+                        cams[v].width, cams[v].height);
+    }
+    const int gy = div_up(cams[0].height, kTile);
+    if (rs->tile_y0 > 0 || rs->tile_y1 < gy) return fail(-1, "views: full-image views only");
+    if ((long long)V * gy >= 65535) return fail(-1, "views: %d views of %d tile rows exceed the tile grid", V, gy);
+    if ((long long)V * gs->P > INT32_MAX / 2) return fail(-1, "views: V * P too large");
+    *tall = cams[0];
+    tall->height = V * gy * kTile;
     return 0;
 }
 
@@ -607,6 +631,102 @@ int gsr_forward_batch(int32_t V, const gsr_camera* cams, const gsr_gaussians* gs
     }
     for (int v = 0; v < V; ++v)
         if (int e = fwd_phase2(jobs[v], cap[v], alloc_binning, ctx, stream, debug)) return e;
+    return 0;
+}
+
+int gsr_forward_views(int32_t V, const gsr_camera* cams, const gsr_gaussians* gs, const gsr_raster_settings* rs,
+                      float* out_color, int32_t* radii, gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_binning,
+                      gsr_alloc_fn alloc_image, void* ctx, gsr_buffers* bufs, void* stream_) {
+    g_err.clear();
+    if (!gs || !rs) return fail(-1, "null gaussians/settings");
+    gsr_camera tall;
+    if (int e = views_camera(V, cams, gs, rs, &tall)) return e;
+    if (!out_color || (gs->P > 0 && !radii) || !bufs || !alloc_geom || !alloc_binning || !alloc_image)
+        return fail(-1, "null output / allocator");
+    if (rs->max_rendered < 0) return fail(-1, "negative max_rendered");
+    gsr_raster_settings rv = *rs;  // the whole tall image
+    rv.tile_y0 = 0;
+    rv.tile_y1 = INT32_MAX;
+    hipStream_t stream = (hipStream_t)stream_;
+    const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
+    FwdJob j{&tall, &rv, out_color, bufs};
+    j.n = (long long)V * gs->P;
+    j.vgy = div_up(cams[0].height, kTile);
+    j.vh = cams[0].height;
+    const bool exact = rs->max_rendered == 0;
+    if (int e = fwd_phase1(j, alloc_geom, alloc_image, ctx, stream, debug, false, [&](const Views& v) {
+            if (gs->P <= 0) return 0;
+            PreOut po{radii, v.depth_key, v.tiles, v.rec, v.rect, v.flags, v.counters};
+            GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess_views(cams, V, gauss_in(gs), po, stream),
+                      "preprocess (views)");
+            if (exact) GSR_CHECK_HIP(begin_read(v.counters, 2 * kCountSlots, stream), "read counts");
+            return 0;
+        }))
+        return e;
+    long long cap = rs->max_rendered;
+    if (exact) {
+        uint64_t ksum = 0;
+        if (gs->P > 0) {
+            uint32_t cw[2 * kCountSlots];
+            const Views v = views(&tall, j.n, bufs);
+            GSR_STAGE(GSR_STAGE_MISC, end_read(v.counters, cw, 2 * kCountSlots, stream), "read counts");
+            for (int i = 0; i < kCountSlots; ++i) ksum += cw[kCountSlots + i];
+        }
+        if (ksum > (uint64_t)INT32_MAX) return fail(-3, "num_rendered overflow (%llu)", (unsigned long long)ksum);
+        cap = (long long)ksum;
+        bufs->num_rendered = (int32_t)ksum;
+    }
+    return fwd_phase2(j, cap, alloc_binning, ctx, stream, debug);
+}
+
+int gsr_backward_views(int32_t V, const gsr_camera* cams, const gsr_gaussians* gs, const gsr_raster_settings* rs,
+                       const gsr_buffers* bufs, const float* dL_dpix, gsr_alloc_fn alloc_scratch, void* ctx,
+                       const gsr_grads* grads, void* stream_) {
+    g_err.clear();
+    if (!gs || !rs) return fail(-1, "null gaussians/settings");
+    gsr_camera tall;
+    if (int e = views_camera(V, cams, gs, rs, &tall)) return e;
+    if (gs->P == 0) return 0;
+    if (int e = check_grads(gs, grads)) return e;
+    const long long n = (long long)V * gs->P;
+    if (!bufs || bufs->n_local != n) return fail(-1, "forward buffers do not match V * P view entries");
+    if (!alloc_scratch) return fail(-1, "null scratch allocator");
+    hipStream_t stream = (hipStream_t)stream_;
+    const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
+    gsr_raster_settings rv = *rs;
+    rv.tile_y0 = 0;
+    rv.tile_y1 = INT32_MAX;
+    float* grad2d = static_cast<float*>(alloc_scratch(ctx, sizeof(float) * kPart * (size_t)n));
+    if (!grad2d) return fail(-2, "allocation failed (grad2d, %lld entries)", n);
+    if (int e = blend_backward(&tall, &rv, bufs, dL_dpix, alloc_scratch, ctx, grad2d, stream, debug,
+                               div_up(cams[0].height, kTile), cams[0].height))
+        return e;
+    const GaussIn in = gauss_in(gs);
+    const GradOut out = grad_out(grads);
+    // leaf-gradient slices of views 1..V-1 (only the arrays the caller asked for)
+    GradOut scratch{};
+    if (V > 1) {
+        const size_t P = (size_t)gs->P, k = (size_t)(V - 1) * P;
+        const size_t widths[8] = {1, 3, 3, 3, 3 * (size_t)in.M_rest, 3, 4, 6};
+        float* const dst[8] = {out.opac, out.colors, out.means3D, out.sh_dc, out.sh_rest, out.scales, out.rots,
+                               out.cov3D};
+        size_t total = 0;
+        for (int a = 0; a < 8; ++a) total += dst[a] ? widths[a] * k : 0;
+        float* base = static_cast<float*>(alloc_scratch(ctx, sizeof(float) * (total > 0 ? total : 1)));
+        if (!base) return fail(-2, "allocation failed (per-view leaf gradients)");
+        float** const slot[8] = {&scratch.opac, &scratch.colors, &scratch.means3D, &scratch.sh_dc, &scratch.sh_rest,
+                                 &scratch.scales, &scratch.rots, &scratch.cov3D};
+        for (int a = 0; a < 8; ++a)
+            if (dst[a]) {
+                *slot[a] = base;
+                base += widths[a] * k;
+            }
+    }
+    const Views v = views(&tall, n, bufs);
+    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward_views(cams, V, in, v.depth_key, v.flags, grad2d, out,
+                                                                         scratch, stream),
+              "preprocess backward (views)");
+    if (V > 1) GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_views_sum(in, V, out, scratch, stream), "views sum");
     return 0;
 }
 

@@ -73,6 +73,10 @@ __device__ __forceinline__ void quad_reduce(float (&v)[N]) {
 
 struct BlendGeom {
     int W, H, grid_x, ty0, nwg;
+    // views mode (gsr_forward_views): the image is V views stacked as bands of vgy tile rows;
+    // a tile's pixel y is taken relative to its view's band (records are in view coordinates)
+    // and rows at or past vh inside a band are padding.  One image: vgy = all rows, vh = H.
+    int vgy, vh;
     uint32_t ck_slots;  // checkpoint slots (gsr_internal.h); the live bytes follow the float4 slots
     int ck_fixed;       // 1: slot = tile * 31 + chunk - 1; 0: from the tile's start in the list
     float bg0, bg1, bg2;
@@ -178,13 +182,14 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int px = tx * kTile + (lane & 15);
     const float pfx = (float)px;
-    const float bx0 = (float)(tx * kTile), by0 = (float)(ty * kTile);
+    const int view = ty / geo.vgy, tyl = ty - view * geo.vgy;  // tile row inside its view's band
+    const float bx0 = (float)(tx * kTile), by0 = (float)(tyl * kTile);
     float pfy[PPL], T[PPL], C0[PPL], C1[PPL], C2[PPL];
 #pragma unroll
     for (int p = 0; p < PPL; ++p) {
-        const int py = ty * kTile + (lane >> 4) + 4 * (w * PPL + p);
-        pfy[p] = (float)py;
-        T[p] = (px < geo.W && py < geo.H) ? 1.0f : -1.0f;
+        const int pyl = tyl * kTile + (lane >> 4) + 4 * (w * PPL + p);
+        pfy[p] = (float)pyl;
+        T[p] = (px < geo.W && pyl < geo.vh) ? 1.0f : -1.0f;
         C0[p] = C1[p] = C2[p] = 0.0f;
     }
     const uint2 range = ranges[tile];
@@ -349,20 +354,24 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
         table[0] = (uint32_t)tend;
         for (int c = nck + 1; c < kMaxChunks; ++c) table[c] = 0xFFFFFFFFu;
     }
-    const size_t npix = (size_t)geo.W * geo.H;
+    // per view: [3, vh, W] colour planes and a [vh, W] transmittance plane (one image: view 0)
+    const size_t npix = (size_t)geo.W * geo.vh;
+    float* const oc = out_color + (size_t)view * 3 * npix;
+    float* const ac = accum + (size_t)view * 3 * npix;
+    float* const fT = final_T + (size_t)view * npix;
 #pragma unroll
     for (int p = 0; p < PPL; ++p) {
-        const int py = ty * kTile + (lane >> 4) + 4 * (w * PPL + p);
-        if (px < geo.W && py < geo.H) {
-            const size_t pix = (size_t)py * geo.W + px;
+        const int pyl = tyl * kTile + (lane >> 4) + 4 * (w * PPL + p);
+        if (px < geo.W && pyl < geo.vh) {
+            const size_t pix = (size_t)pyl * geo.W + px;
             const float Tf = fabsf(T[p]);
-            final_T[pix] = Tf;
-            accum[pix] = C0[p];
-            accum[npix + pix] = C1[p];
-            accum[2 * npix + pix] = C2[p];
-            out_color[pix] = C0[p] + Tf * geo.bg0;
-            out_color[npix + pix] = C1[p] + Tf * geo.bg1;
-            out_color[2 * npix + pix] = C2[p] + Tf * geo.bg2;
+            fT[pix] = Tf;
+            ac[pix] = C0[p];
+            ac[npix + pix] = C1[p];
+            ac[2 * npix + pix] = C2[p];
+            oc[pix] = C0[p] + Tf * geo.bg0;
+            oc[npix + pix] = C1[p] + Tf * geo.bg1;
+            oc[2 * npix + pix] = C2[p] + Tf * geo.bg2;
         }
     }
 }
@@ -473,16 +482,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
     const int col = lane >> 2, row = lane & 3;
     const int px = tx * kTile + col;
     const float pfx = (float)px;
-    const float bx0 = (float)(tx * kTile), by0 = (float)(ty * kTile);
-    const size_t npix = (size_t)geo.W * geo.H;
+    const int view = ty / geo.vgy, tyl = ty - view * geo.vgy;  // tile row inside its view's band
+    const float bx0 = (float)(tx * kTile), by0 = (float)(tyl * kTile);
+    // F6's per-view planes (one image: view 0)
+    const size_t npix = (size_t)geo.W * geo.vh;
+    final_T += (size_t)view * npix;
+    accum += (size_t)view * 3 * npix;
+    dL_dpix += (size_t)view * 3 * npix;
     // R = S . dL/dpix - Sp + T_final bg . dL/dpix: the colour term behind the current record
     float pfy[kPPL], T[kPPL], R[kPPL], dp0[kPPL], dp1[kPPL], dp2[kPPL];
 #pragma unroll
     for (int p = 0; p < kPPL; ++p) {
-        const int py = ty * kTile + row + 4 * p;
-        pfy[p] = (float)py;
-        const bool in = px < geo.W && py < geo.H;
-        const size_t pix = in ? (size_t)py * geo.W + px : 0;
+        const int pyl = tyl * kTile + row + 4 * p;
+        pfy[p] = (float)pyl;
+        const bool in = px < geo.W && pyl < geo.vh;
+        const size_t pix = in ? (size_t)pyl * geo.W + px : 0;
         const float Tfin = in ? final_T[pix] : 1.0f;
         dp0[p] = in ? dL_dpix[pix] : 0.0f;
         dp1[p] = in ? dL_dpix[npix + pix] : 0.0f;
@@ -660,10 +674,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
 #endif
 constexpr int kF6FullWaves = 2, kF6BandWaves = 4, kF6BandTiles = GSR_F6_BAND_TILES;
 
-static BlendGeom make_geo(const gsr_camera& cam, const float bg[3], int ty0, int ty1, long long cap) {
+static BlendGeom make_geo(const gsr_camera& cam, const float bg[3], int ty0, int ty1, long long cap, int vgy, int vh) {
     BlendGeom g;
     g.W = cam.width;
     g.H = cam.height;
+    g.vgy = vgy > 0 ? vgy : div_up(cam.height, kTile);
+    g.vh = vgy > 0 ? vh : cam.height;
     g.grid_x = div_up(cam.width, kTile);
     g.ty0 = ty0;
     g.nwg = (ty1 - ty0) * g.grid_x;
@@ -679,10 +695,13 @@ static BlendGeom make_geo(const gsr_camera& cam, const float bg[3], int ty0, int
 int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
                          const uint2* ranges, const uint32_t* sorted_gid, const float4* rec,
                          float* out_color, float* final_T, float* accum, uint32_t* term, float4* ck, long long cap,
-                         hipStream_t s) {
-    const BlendGeom geo = make_geo(cam, bg, ty0, ty1, cap);
+                         hipStream_t s, int vgy, int vh) {
+    const BlendGeom geo = make_geo(cam, bg, ty0, ty1, cap, vgy, vh);
     if (geo.nwg <= 0) return 0;
-    if (geo.nwg >= kF6BandTiles)
+    // the variant (and with it the B1 chunk work) follows the tiles of ONE image: views mode then
+    // chunks every tile as a per-view call does, which keeps its gradients bit-identical
+    const long long sel = vgy > 0 ? (long long)geo.vgy * geo.grid_x : geo.nwg;
+    if (sel >= kF6BandTiles)
         hipLaunchKernelGGL(blend_forward_kernel<kF6FullWaves>, dim3(geo.nwg), dim3(64 * kF6FullWaves), 0, s, geo,
                            ranges, sorted_gid, rec, out_color, final_T, accum, term, ck);
     else
@@ -695,8 +714,8 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
                           const uint2* ranges, const uint32_t* sorted_gid, const uint4* rect,
                           const float4* rec, const float* final_T,
                           const float* accum, const float* dL_dpix, float* partial, long long cap,
-                          const uint32_t* term, const float4* ck, hipStream_t s) {
-    const BlendGeom geo = make_geo(cam, bg, ty0, ty1, cap);
+                          const uint32_t* term, const float4* ck, hipStream_t s, int vgy, int vh) {
+    const BlendGeom geo = make_geo(cam, bg, ty0, ty1, cap, vgy, vh);
     if (geo.nwg <= 0) return 0;
     const PartLayout pl(cap);
     char* base = reinterpret_cast<char*>(partial);

@@ -65,6 +65,7 @@ inline size_t sort_scratch_words(long long n) { return 256 * ((size_t)radix_bloc
 #define GSR_PRESORT_MIN ((1 << 19) + 1)
 #endif
 constexpr long long kPresortMin = GSR_PRESORT_MIN;
+constexpr int kMaxViews = 8;  // gsr_forward_views: views per call (= GSR_MAX_VIEWS)
 inline bool use_presort(long long n) { return n >= kPresortMin; }
 
 struct GeomLayout {

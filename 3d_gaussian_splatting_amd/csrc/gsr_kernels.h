@@ -29,6 +29,14 @@ struct PreOut {
 // its first Gaussian and P = its length (outputs are indexed by the shard-local index).
 int launch_preprocess(const gsr_camera& cam, const GaussIn& in, int ty0, int ty1, const PreOut& out,
                       hipStream_t s);
+// Cameras by value in the kernel arguments: one, or up to kMaxViews (views mode, grid.y = view).
+template <int NV>
+struct CamArg {
+    gsr_camera c[NV];
+};
+// Views mode (gsr_forward_views): V <= kMaxViews views of the same size, one launch (grid.y =
+// view); view v's outputs at entries v * P + g, its tiles / pixel rows offset into a tall image.
+int launch_preprocess_views(const gsr_camera* cams, int V, const GaussIn& in, const PreOut& out, hipStream_t s);
 
 // LSD radix sort of (u32 key, u32 value) by key bits [0, nbits); vals_in == nullptr means the
 // identity permutation.  Ping-pongs between (k0,v0) and (k1,v1); returns in *which (0/1) where
@@ -78,7 +86,7 @@ int launch_finalize(const uint32_t* sorted_tile, long long cap, const uint32_t* 
 int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
                          const uint2* ranges, const uint32_t* sorted_gid, const float4* rec,
                          float* out_color, float* final_T, float* accum, uint32_t* term, float4* ck, long long cap,
-                         hipStream_t s);
+                         hipStream_t s, int vgy = 0, int vh = 0);
 
 // F6 writes term[t] (see kMaxChunks) and the B1 chunk checkpoints `ck` (ImgLayout.ck).
 // B1: per-tile front-to-back gradients -> per-instance partial entry j (PartLayout(cap)), where
@@ -91,7 +99,8 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
                           const uint2* ranges, const uint32_t* sorted_gid, const uint4* rect,
                           const float4* rec, const float* final_T,
                           const float* accum, const float* dL_dpix, float* partial, long long cap,
-                          const uint32_t* term, const float4* ck, hipStream_t s);
+                          const uint32_t* term, const float4* ck, hipStream_t s, int vgy = 0, int vh = 0);
+// (vgy, vh: views mode -- bands of vgy tile rows per view, vh valid pixel rows each; 0 = one image)
 
 // record layout constants shared by preprocess and the blend kernels
 constexpr float kLn2 = 0.6931471805599453f;  // conic A = -2 ln2 a', B = -ln2 b', C = -2 ln2 c' 
@@ -111,6 +120,14 @@ struct GradOut {
 int launch_preprocess_backward(const gsr_camera& cam, const GaussIn& in, int g0, int g1,
                                const uint32_t* depth_key, const uint32_t* flags, const float* grad2d,
                                const GradOut& out, hipStream_t s);
+// Views mode: B2 of V views in one launch (grid.y = view) from the per-(view, Gaussian) entries
+// v * P + g of depth_key / flags / grad2d; view v's 2D gradients (means2D, conic) go to rows
+// v * P.. of out's, its leaf gradients to `out` (v = 0) or to slice v - 1 of `scratch` (P rows per
+// slice), which launch_views_sum then adds to `out` in view order.
+int launch_preprocess_backward_views(const gsr_camera* cams, int V, const GaussIn& in, const uint32_t* depth_key,
+                                     const uint32_t* flags, const float* grad2d, const GradOut& out,
+                                     const GradOut& scratch, hipStream_t s);
+int launch_views_sum(const GaussIn& in, int V, const GradOut& out, const GradOut& scratch, hipStream_t s);
 
 // ---- multi-GPU exchange (gsr_shard.hip) ----
 // Shard side: pack every visible Gaussian of [0, P) into the send block of each band its rect

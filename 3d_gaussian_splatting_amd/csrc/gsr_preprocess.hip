@@ -234,7 +234,7 @@ __device__ __forceinline__ void sh_basis(const gsr_camera& cam, const GaussIn& i
 // directly; log2(o) rides along so o * G is one exp2) + the half-extents of the alpha >= 1/255
 // footprint: d^T Q d <= t, t = 2 ln(255 o)  =>  |dx| <= sqrt(t a), |dy| <= sqrt(t c), padded
 // (x1.02 + 0.5 px) so the per-stripe cull never drops a contributing pixel.
-__device__ __forceinline__ void write_record(int g, float opac, const Geo& G, const float (&rgb)[3],
+__device__ __forceinline__ void write_record(size_t g, float opac, const Geo& G, const float (&rgb)[3],
                                              uint32_t clamped, const PreOut& out) {
     const float kL2E = 1.4426950408889634f;
     const float tthr = 2.0f * logf(255.0f * opac);
@@ -278,13 +278,21 @@ constexpr int kSubRows = 16;             // kShWave: rows per staged window
 // The block also adds its candidate count (Gaussians with tiles in the band) and instance
 // count (sum of tiles_touched) into counters[slot] / counters[kCountSlots + slot], so the host
 // can read K right after this kernel -- while the depth sort runs -- instead of after the scan.
-template <int SH>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void preprocess_kernel(const gsr_camera cam, const GaussIn in,
+//
+// NV > 1 (gsr_forward_views): view v = blockIdx.y projects the same Gaussians with cams.c[v]; its
+// outputs go to entry e = v * P + g and its tile rows are offset by v * grid_y -- the views are
+// consecutive bands of tile rows of one tall image for every later stage.
+template <int SH, int NV>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void preprocess_kernel(const CamArg<NV> cams,
+                                                         const GaussIn in,
                                                          int grid_x, int grid_y, int ty0, int ty1,
                                                          PreOut out) {
     extern __shared__ __attribute__((aligned(16))) float sh_lds[];
     __shared__ uint32_t wk[4], wc[4];
+    const int view = NV > 1 ? (int)blockIdx.y : 0;
+    const gsr_camera& cam = cams.c[NV > 1 ? view : 0];
     const int g = blockIdx.x * 256 + threadIdx.x;
+    const size_t e = (size_t)view * in.P + g;  // output entry
     const int M3 = in.M_rest * 3;
     const int rows = in.P - blockIdx.x * 256 < 256 ? in.P - blockIdx.x * 256 : 256;
     const bool sh = in.sh_rest && !in.colors && in.D > 0;  // grid-uniform
@@ -348,9 +356,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void p
     G.key = 0xFFFFFFFFu;
     if (g < in.P) {
         G = preprocess_geom(cam, in, I, grid_x, grid_y, ty0, ty1);
-        out.radii[g] = G.radius;
-        out.depth_key[g] = G.key;
-        out.tiles[g] = G.tiles;
+        if (NV > 1) {  // view v's band of tile rows in the tall image (the record stays in the
+            G.miny += view * grid_y;  // view's own pixel coordinates: F6 / B1 take pixel y
+            G.maxy += view * grid_y;  // relative to the view's band, so every value is bit-equal
+        }                             // to a one-view render)
+        out.radii[e] = G.radius;
+        out.depth_key[e] = G.key;
+        out.tiles[e] = G.tiles;
     }
     const bool need = G.tiles != 0;  // colour and record only for Gaussians this band blends
     float rgb[3] = {0.f, 0.f, 0.f}, basis[16];
@@ -452,7 +464,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void p
                 rgb[ch] = fmaxf(r, 0.0f);
             }
         }
-        write_record(g, I.opac, G, rgb, clamped, out);
+        write_record(e, I.opac, G, rgb, clamped, out);
     }
     const uint32_t t = G.tiles;
     if (out.counters) {
@@ -478,23 +490,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void p
 
 }  // namespace
 
+template <int NV>
+static void launch_preprocess_nv(const CamArg<NV>& cams, int V, const GaussIn& in, int ty0, int ty1,
+                                 const PreOut& out, hipStream_t s) {
+    const int gx = div_up(cams.c[0].width, kTile), gy = div_up(cams.c[0].height, kTile);
+    const bool sh = in.sh_rest && !in.colors && in.D > 0;
+    const dim3 grid(div_up(in.P, 256), V), block(256);
+    if (sh && GSR_F1_SH_MODE == kShGlds && in.M_rest * 3 <= 48 && (reinterpret_cast<uintptr_t>(in.sh_rest) & 15) == 0)
+        hipLaunchKernelGGL((preprocess_kernel<kShGlds, NV>), grid, block,
+                           4 * 1024 * ((64 * in.M_rest * 3 * 4 + 1023) / 1024), s, cams, in, gx, gy, ty0, ty1, out);
+    else if (sh && GSR_F1_SH_MODE == kShWave && in.M_rest * 3 <= 64 && (reinterpret_cast<uintptr_t>(in.sh_rest) & 15) == 0)
+        hipLaunchKernelGGL((preprocess_kernel<kShWave, NV>), grid, block, sizeof(float) * 4 * kSubRows * in.M_rest * 3,
+                           s, cams, in, gx, gy, ty0, ty1, out);
+    else if (sh)
+        hipLaunchKernelGGL((preprocess_kernel<kShChunks, NV>), grid, block, sizeof(float) * 256 * kChunkF, s, cams, in,
+                           gx, gy, ty0, ty1, out);
+    else
+        hipLaunchKernelGGL((preprocess_kernel<kShDirect, NV>), grid, block, 0, s, cams, in, gx, gy, ty0, ty1, out);
+}
+
 int launch_preprocess(const gsr_camera& cam, const GaussIn& in, int ty0, int ty1, const PreOut& out,
                       hipStream_t s) {
     if (in.P <= 0) return 0;
-    const int gx = div_up(cam.width, kTile), gy = div_up(cam.height, kTile);
-    const bool sh = in.sh_rest && !in.colors && in.D > 0;
-    const dim3 grid(div_up(in.P, 256)), block(256);
-    if (sh && GSR_F1_SH_MODE == kShGlds && in.M_rest * 3 <= 48 && (reinterpret_cast<uintptr_t>(in.sh_rest) & 15) == 0)
-        hipLaunchKernelGGL(preprocess_kernel<kShGlds>, grid, block, 4 * 1024 * ((64 * in.M_rest * 3 * 4 + 1023) / 1024),
-                           s, cam, in, gx, gy, ty0, ty1, out);
-    else if (sh && GSR_F1_SH_MODE == kShWave && in.M_rest * 3 <= 64 && (reinterpret_cast<uintptr_t>(in.sh_rest) & 15) == 0)
-        hipLaunchKernelGGL(preprocess_kernel<kShWave>, grid, block, sizeof(float) * 4 * kSubRows * in.M_rest * 3, s,
-                           cam, in, gx, gy, ty0, ty1, out);
-    else if (sh)
-        hipLaunchKernelGGL(preprocess_kernel<kShChunks>, grid, block, sizeof(float) * 256 * kChunkF, s, cam, in, gx,
-                           gy, ty0, ty1, out);
-    else
-        hipLaunchKernelGGL(preprocess_kernel<kShDirect>, grid, block, 0, s, cam, in, gx, gy, ty0, ty1, out);
+    CamArg<1> c1{{cam}};
+    launch_preprocess_nv(c1, 1, in, ty0, ty1, out, s);
+    return (int)hipGetLastError();
+}
+
+int launch_preprocess_views(const gsr_camera* cams, int V, const GaussIn& in, const PreOut& out, hipStream_t s) {
+    if (in.P <= 0 || V <= 0) return 0;
+    if (V > kMaxViews) return -1;
+    CamArg<kMaxViews> cv{};
+    for (int v = 0; v < V; ++v) cv.c[v] = cams[v];
+    const int gy = div_up(cams[0].height, kTile);
+    launch_preprocess_nv(cv, V, in, 0, gy, out, s);
     return (int)hipGetLastError();
 }
 

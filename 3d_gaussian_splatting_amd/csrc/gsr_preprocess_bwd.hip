@@ -427,12 +427,41 @@ __device__ __forceinline__ void preprocess_backward_one(const gsr_camera& cam, c
 #endif
 
 // Gaussians [g0, g0 + n): inputs indexed by g, grad2d and every output by o = g - g0.
+// view v's leaf outputs: `out` for v = 0, slice v - 1 of `scratch`; its 2D gradients: rows v * P..
+__device__ __forceinline__ GradOut view_out(const GradOut& out, const GradOut& scratch, int v, size_t P, int M3) {
+    if (v == 0) return out;
+    const size_t k = (size_t)(v - 1) * P;
+    auto sl = [&](float* p, int width) { return p ? p + k * width : nullptr; };
+    GradOut o;
+    o.means2D = out.means2D ? out.means2D + (size_t)v * P * 3 : nullptr;
+    o.conic = out.conic ? out.conic + (size_t)v * P * 3 : nullptr;
+    o.opac = sl(scratch.opac, 1);
+    o.colors = sl(scratch.colors, 3);
+    o.means3D = sl(scratch.means3D, 3);
+    o.sh_dc = sl(scratch.sh_dc, 3);
+    o.sh_rest = sl(scratch.sh_rest, M3);
+    o.scales = sl(scratch.scales, 3);
+    o.rots = sl(scratch.rots, 4);
+    o.cov3D = sl(scratch.cov3D, 6);
+    return o;
+}
+
+template <int NV>
 __global__ __launch_bounds__(256) void preprocess_backward_kernel(
-    const gsr_camera cam, const GaussIn in, int g0, int n, const uint32_t* __restrict__ depth_key,
-    const uint32_t* __restrict__ flags, const float* __restrict__ grad2d, GradOut out) {
+    const CamArg<NV> cams, const GaussIn in, int g0, int n, const uint32_t* __restrict__ depth_key,
+    const uint32_t* __restrict__ flags, const float* __restrict__ grad2d, GradOut out, const GradOut scratch) {
     extern __shared__ __attribute__((aligned(16))) float sh_lds[];
     const int o = blockIdx.x * 256 + threadIdx.x;
     const int M3 = in.M_rest * 3;
+    const int view = NV > 1 ? (int)blockIdx.y : 0;
+    const gsr_camera& cam = cams.c[NV > 1 ? view : 0];
+    if (NV > 1) {  // views mode: this view's entries and outputs
+        const size_t e0 = (size_t)view * in.P;
+        depth_key += e0;
+        if (flags) flags += e0;
+        grad2d += e0 * kPart;
+        out = view_out(out, scratch, view, (size_t)in.P, M3);
+    }
     const bool stage = in.sh_rest != nullptr && !in.colors;  // block-uniform
     const int rows = n - blockIdx.x * 256 < 256 ? n - blockIdx.x * 256 : 256;
     const size_t obase = (size_t)blockIdx.x * 256 * M3, ibase = (size_t)g0 * M3 + obase;
@@ -500,8 +529,63 @@ int launch_preprocess_backward(const gsr_camera& cam, const GaussIn& in, int g0,
     const int n = g1 - g0;
     if (n <= 0) return 0;
     const size_t lds = (in.sh_rest && !in.colors) ? sizeof(float) * 256 * 3 * in.M_rest : 0;
-    hipLaunchKernelGGL(preprocess_backward_kernel, dim3(div_up(n, 256)), dim3(256), lds, s, cam, in, g0, n,
-                       depth_key, flags, grad2d, out);
+    const CamArg<1> c1{{cam}};
+    hipLaunchKernelGGL(preprocess_backward_kernel<1>, dim3(div_up(n, 256)), dim3(256), lds, s, c1, in, g0, n,
+                       depth_key, flags, grad2d, out, GradOut{});
+    return (int)hipGetLastError();
+}
+
+int launch_preprocess_backward_views(const gsr_camera* cams, int V, const GaussIn& in, const uint32_t* depth_key,
+                                     const uint32_t* flags, const float* grad2d, const GradOut& out,
+                                     const GradOut& scratch, hipStream_t s) {
+    if (in.P <= 0 || V <= 0) return 0;
+    if (V > kMaxViews) return -1;
+    CamArg<kMaxViews> cv{};
+    for (int v = 0; v < V; ++v) cv.c[v] = cams[v];
+    const size_t lds = (in.sh_rest && !in.colors) ? sizeof(float) * 256 * 3 * in.M_rest : 0;
+    hipLaunchKernelGGL(preprocess_backward_kernel<kMaxViews>, dim3(div_up(in.P, 256), V), dim3(256), lds, s, cv, in,
+                       0, in.P, depth_key, flags, grad2d, out, scratch);
+    return (int)hipGetLastError();
+}
+
+// out[i] = ((out[i] + s_1[i]) + s_2[i]) + ... over the views' leaf-gradient slices, in view order
+// (the same sum a caller forms from per-view backward calls).  blockIdx.y = output array.
+struct SumArrays {
+    float* dst[8];
+    const float* src[8];
+    long long n[8];
+};
+__global__ __launch_bounds__(256) void views_sum_kernel(const SumArrays a, int V) {
+    const int k = blockIdx.y;
+    float* d = a.dst[k];
+    if (!d) return;
+    const long long n = a.n[k];
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+        float acc = d[i];
+        for (int v = 0; v + 1 < V; ++v) acc = acc + a.src[k][(size_t)v * n + i];
+        d[i] = acc;
+    }
+}
+
+int launch_views_sum(const GaussIn& in, int V, const GradOut& out, const GradOut& scratch, hipStream_t s) {
+    if (in.P <= 0 || V <= 1) return 0;
+    SumArrays a{};
+    const long long P = in.P;
+    float* const dsts[8] = {out.opac, out.colors, out.means3D, out.sh_dc, out.sh_rest, out.scales, out.rots, out.cov3D};
+    const float* const srcs[8] = {scratch.opac, scratch.colors, scratch.means3D, scratch.sh_dc, scratch.sh_rest,
+                                  scratch.scales, scratch.rots, scratch.cov3D};
+    const long long widths[8] = {1, 3, 3, 3, 3LL * in.M_rest, 3, 4, 6};
+    long long nmax = 0;
+    for (int k = 0; k < 8; ++k) {
+        const bool on = dsts[k] && srcs[k] && widths[k] > 0;
+        a.dst[k] = on ? dsts[k] : nullptr;
+        a.src[k] = on ? srcs[k] : nullptr;
+        a.n[k] = on ? P * widths[k] : 0;
+        nmax = a.n[k] > nmax ? a.n[k] : nmax;
+    }
+    if (nmax == 0) return 0;
+    const long long blocks = div_up(nmax, 256) < 4096 ? div_up(nmax, 256) : 4096;
+    hipLaunchKernelGGL(views_sum_kernel, dim3((unsigned)blocks, 8), dim3(256), 0, s, a, V);
     return (int)hipGetLastError();
 }
 

@@ -25,6 +25,7 @@ GSR_FLAG_DEBUG = 1
 GSR_ERR_OVERFLOW = -4
 GSR_GRAD2D_STRIDE = 12
 GSR_MAX_BATCH = 64
+GSR_MAX_VIEWS = 8
 GSR_SPLAT_BYTES = 64
 GSR_SPLAT_GRAD_BYTES = 48
 MAX_BANDS = 16
@@ -38,7 +39,7 @@ def ck_slot(fixed: bool, start: int, tile: int, chunk: int) -> int:
     """B1 checkpoint slot of a tile's chunk >= 1 (gsr.h GSR_VIEW_CK_LIVE)."""
     return tile * (TERM_STRIDE - 1) + chunk - 1 if fixed else start // CK_DIV + tile + chunk - 1
 EXPORTS = ["gsr_abi_version", "gsr_last_error", "gsr_forward", "gsr_read_num_rendered", "gsr_forward_batch",
-           "gsr_backward", "gsr_backward_blend", "gsr_backward_preprocess", "gsr_shard_forward",
+           "gsr_forward_views", "gsr_backward_views", "gsr_backward", "gsr_backward_blend", "gsr_backward_preprocess", "gsr_shard_forward",
            "gsr_band_forward", "gsr_band_backward", "gsr_shard_backward", "gsr_exchange_block_bytes",
            "gsr_shard_state_bytes", "gsr_view", "gsr_geom_bytes", "gsr_binning_bytes",
            "gsr_image_bytes", "gsr_scratch_bytes", "gsr_ck_pool_slots", "gsr_profile_enable", "gsr_profile_read",
@@ -128,6 +129,14 @@ def load_hip() -> ctypes.CDLL:
         L.gsr_forward_batch.argtypes = [i32, ctypes.POINTER(Camera), ctypes.POINTER(Gaussians),
                                         ctypes.POINTER(Settings), ctypes.POINTER(vp), ctypes.POINTER(vp), ALLOC_FN,
                                         ALLOC_FN, ALLOC_FN, vp, ctypes.POINTER(Buffers), vp]
+        L.gsr_forward_views.restype = ctypes.c_int
+        L.gsr_forward_views.argtypes = [i32, ctypes.POINTER(Camera), ctypes.POINTER(Gaussians),
+                                        ctypes.POINTER(Settings), vp, vp, ALLOC_FN, ALLOC_FN, ALLOC_FN, vp,
+                                        ctypes.POINTER(Buffers), vp]
+        L.gsr_backward_views.restype = ctypes.c_int
+        L.gsr_backward_views.argtypes = [i32, ctypes.POINTER(Camera), ctypes.POINTER(Gaussians),
+                                         ctypes.POINTER(Settings), ctypes.POINTER(Buffers), vp, ALLOC_FN, vp,
+                                         ctypes.POINTER(Grads), vp]
         L.gsr_backward.restype = ctypes.c_int
         L.gsr_backward.argtypes = [ctypes.POINTER(Camera), ctypes.POINTER(Gaussians), ctypes.POINTER(Settings),
                                    ctypes.POINTER(Buffers), vp, ALLOC_FN, vp, ctypes.POINTER(Grads), vp]

@@ -122,6 +122,24 @@ class ForwardState:
         return t[off:off + nbytes].view(dtype).clone()
 
 
+@dataclass
+class ViewsState:
+    """gsr_forward_views' outputs, kept for gsr_backward_views (one set of buffers for all views)."""
+    cams: list
+    cstructs: object          # the gsr_camera array handed to the library
+    inputs: dict
+    settings: native.Settings
+    gauss: native.Gaussians
+    buffers: native.Buffers
+    color: torch.Tensor       # V x 3 x H x W
+    radii: torch.Tensor       # V x P
+    allocs: list
+
+    @property
+    def num_rendered(self) -> int:
+        return int(self.buffers.num_rendered)
+
+
 class CAbiRasterizer:
     """Thin ctypes front-end of gsr_forward / gsr_backward*."""
 
@@ -233,6 +251,45 @@ class CAbiRasterizer:
             ctypes.memmove(ctypes.byref(b), ctypes.byref(bufs[v]), ctypes.sizeof(b))
             out.append(ForwardState(cam=cam, inputs=inputs, settings=s, gauss=g, buffers=b, color=colors[v],
                                     radii=radii[v], allocs=[ag, ab, ai]))
+        return out
+
+    def forward_views(self, cams, means3D, opacities, scales=None, rotations=None, sh_dc=None, sh_rest=None,
+                      sh_degree=0, colors_precomp=None, cov3D_precomp=None, scale_modifier=1.0,
+                      bg=(0.0, 0.0, 0.0), max_rendered=0, debug=False) -> "ViewsState":
+        """gsr_forward_views: V same-size cameras in one pass (one launch per stage).  color is
+        V x 3 x H x W, radii V x P; bit-identical to V forward() calls."""
+        dev = self.device
+        inputs, g, s = self._prepare(means3D, opacities, scales, rotations, sh_dc, sh_rest, sh_degree,
+                                     colors_precomp, cov3D_precomp, scale_modifier, bg, None, max_rendered, debug)
+        V, P = len(cams), g.P
+        H, W = cams[0].height, cams[0].width
+        color = torch.empty((V, 3, H, W), dtype=torch.float32, device=dev)
+        radii = torch.empty((V, P), dtype=torch.int32, device=dev)
+        ag, ab, ai = _Allocator(dev), _Allocator(dev), _Allocator(dev)
+        bufs = native.Buffers()
+        cs = (native.Camera * V)(*[self._cam(c) for c in cams])
+        rc = self.L.gsr_forward_views(V, cs, ctypes.byref(g), ctypes.byref(s), _ptr(color),
+                                      _ptr(radii) if P else None, ag.cb, ab.cb, ai.cb, None, ctypes.byref(bufs),
+                                      self._stream())
+        self._check(rc, "gsr_forward_views")
+        return ViewsState(cams=list(cams), cstructs=cs, inputs=inputs, settings=s, gauss=g, buffers=bufs,
+                          color=color, radii=radii, allocs=[ag, ab, ai])
+
+    def backward_views(self, st: "ViewsState", dL_dpix) -> dict:
+        """gsr_backward_views: means2D / conic gradients per view (V x P x 3), leaf gradients
+        summed over the views in view order."""
+        V = len(st.cams)
+        dpix = _f32(dL_dpix, (V, 3, st.cams[0].height, st.cams[0].width), self.device)
+        out, gg = self._grad_tensors(st)
+        P = st.gauss.P
+        for k, name in (("means2D", "dL_dmeans2D"), ("conic", "dL_dconic")):
+            out[k] = torch.empty((V, P, 3), dtype=torch.float32, device=self.device)
+            setattr(gg, name, out[k].data_ptr())
+        scratch = _Allocator(self.device)
+        rc = self.L.gsr_backward_views(V, st.cstructs, ctypes.byref(st.gauss), ctypes.byref(st.settings),
+                                       ctypes.byref(st.buffers), _ptr(dpix), scratch.cb, None, ctypes.byref(gg),
+                                       self._stream())
+        self._check(rc, "gsr_backward_views")
         return out
 
     def _grad_tensors(self, st: ForwardState, P: int | None = None):

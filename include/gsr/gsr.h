@@ -147,6 +147,30 @@ int gsr_forward_batch(int32_t V, const gsr_camera* cams, const gsr_gaussians* gs
                       gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_binning, gsr_alloc_fn alloc_image,
                       void* alloc_ctx, gsr_buffers* bufs, void* stream);
 
+/* Views mode: V same-size cameras rendered as ONE pass -- one launch per
+ * stage for all views.  The views are stacked as bands of ceil(H/16) tile rows of one tall
+ * binning, so F1, the scan, F3, the tile sort, F6 and (in gsr_backward_views) B1, the gather
+ * and B2 each run once over V*P (view, Gaussian) entries.  The result is bit-identical to V
+ * gsr_forward / gsr_backward calls: a tile belongs to one view and keeps the canonical
+ * (depth, Gaussian) order.
+ *   cams: V cameras, all of one width and height (full image, no tile band in rs)
+ *   out_color: V x 3 x H x W;  radii: V x P;  bufs: ONE gsr_buffers for the whole pass
+ *   (geometry for V*P entries, image and binning for the tall V*ceil(H/16)*16 x W image).
+ * The backward reads dL_dout_color as V x 3 x H x W and writes dL_dmeans2D / dL_dconic as
+ * V x P x 3 (per view, as the reference's viewspace points are); every leaf gradient is the
+ * sum over the views, added in view order -- (((g_0 + g_1) + g_2) + ...) -- as a caller
+ * summing per-view backward results would.  alloc_scratch is asked for three blocks: the
+ * partial gradients, 48 * V * P bytes of grad2d, and (V > 1) the V-1 per-view leaf gradient
+ * slices.  1 <= V <= GSR_MAX_VIEWS. */
+#define GSR_MAX_VIEWS 8
+int gsr_forward_views(int32_t V, const gsr_camera* cams, const gsr_gaussians* gs,
+                      const gsr_raster_settings* rs, float* out_color, int32_t* radii,
+                      gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_binning, gsr_alloc_fn alloc_image,
+                      void* alloc_ctx, gsr_buffers* bufs, void* stream);
+int gsr_backward_views(int32_t V, const gsr_camera* cams, const gsr_gaussians* gs,
+                       const gsr_raster_settings* rs, const gsr_buffers* bufs, const float* dL_dout_color,
+                       gsr_alloc_fn alloc_scratch, void* alloc_ctx, const gsr_grads* grads, void* stream);
+
 /* Full backward (B1 + gather + B2).  dL_dout_color: 3 x H x W.  scratch: asked for twice
  * through alloc_scratch (gsr_scratch_bytes(capacity) for per-instance partial gradients, then
  * 48 * P bytes for the per-Gaussian screen-space gradient), valid for the duration of the call. */

@@ -1,0 +1,102 @@
+"""GPU: views mode -- V same-size cameras in ONE pass, one launch per stage (SURVEY §8f row 4,
+gsr_forward_views / gsr_backward_views).
+
+The pass must give, view by view, exactly what gsr_forward / gsr_backward give for that camera
+alone: colour, radii, means2D / conic gradients bit for bit, and leaf gradients bit for bit
+equal to the per-view results added in view order ((g0 + g1) + g2 ...).  A tile belongs to one
+view's band of the tall binning, and the canonical (tile, depth, Gaussian) order is the same
+whether the entries come from the global depth pre-sort (V * P >= 2^19 + 1) or the per-tile
+depth sort, so even a pass that switches sort paths is bit-identical.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import pkg
+
+pytestmark = pytest.mark.gpu
+
+
+def _rot_y(deg):
+    a = math.radians(deg)
+    return np.array([[math.cos(a), 0, math.sin(a)], [0, 1, 0], [-math.sin(a), 0, math.cos(a)]])
+
+
+def _cams(w, h, n):
+    gr = pkg("graphics")
+    poses = [(0, (0, 0, 0)), (8, (0.3, 0, 0)), (-12, (0, 0.2, 0.5)), (4, (0, 0, -0.5)), (90, (0, 0, 0)),
+             (20, (-0.2, 0.1, 0)), (-5, (0.1, -0.1, 0.2)), (2, (0, 0, 0.3))]
+    fx = math.radians(60.0)
+    fy = 2 * math.atan(math.tan(fx / 2) * h / w)
+    return [gr.make_camera(_rot_y(d), np.array(t, float), fx, fy, w, h) for d, t in poses[:n]]
+
+
+def _scene(P, seed, w=320, h=240):
+    gr, sc = pkg("graphics"), pkg("scene")
+    s = sc.make_scene(gr.synthetic_camera(w, h), P, max_sh_degree=3, seed=seed)
+    return (s.means3D, s.opacities, s.scales, s.rotations, s.sh_dc, s.sh_rest)
+
+
+def _check(rast, cams, args, bg=(0.1, 0.2, 0.3)):
+    V = len(cams)
+    st = rast.forward_views(cams, *args, sh_degree=3, bg=bg)
+    H, W = cams[0].height, cams[0].width
+    assert st.color.shape == (V, 3, H, W)
+    gen = torch.Generator("cuda").manual_seed(5)
+    dpix = torch.rand((V, 3, H, W), device="cuda", generator=gen)
+    gv = rast.backward_views(st, dpix)
+    total, leaf = 0, None
+    for v, cam in enumerate(cams):
+        a = rast.forward(cam, *args, sh_degree=3, bg=bg)
+        assert torch.equal(a.color, st.color[v]), v
+        assert torch.equal(a.radii, st.radii[v]), v
+        total += a.num_rendered
+        ga = rast.backward(a, dpix[v])
+        for k in ("means2D", "conic"):
+            assert torch.equal(ga[k], gv[k][v]), (k, v)
+        leaf = {k: t.clone() for k, t in ga.items() if k not in ("means2D", "conic")} if leaf is None else \
+            {k: leaf[k] + ga[k] for k in leaf}
+    assert st.num_rendered == total
+    for k in leaf:
+        assert torch.equal(leaf[k], gv[k]), k
+    return st
+
+
+def test_views_equal_single_views():
+    rast = pkg("rasterizer").CAbiRasterizer("cuda")
+    cams = _cams(320, 250, 5)  # 250 rows: the last tile row of every view is part padding
+    _check(rast, cams, _scene(20000, 21))
+
+
+def test_views_presort_switch():
+    """V * P crosses the pre-sort threshold, each view alone does not."""
+    native = pkg("native")
+    rast = pkg("rasterizer").CAbiRasterizer("cuda")
+    cams = _cams(400, 304, 4)
+    P = 160000
+    assert P < (1 << 19) + 1 <= 4 * P
+    _check(rast, cams, _scene(P, 22, 400, 304))
+    assert native.GSR_MAX_VIEWS == 8
+
+
+def test_views_full_and_one():
+    rast = pkg("rasterizer").CAbiRasterizer("cuda")
+    args = _scene(12000, 23, 192, 128)
+    _check(rast, _cams(192, 128, 8), args)
+    _check(rast, _cams(192, 128, 1), args)
+
+
+def test_views_limits():
+    rast = pkg("rasterizer").CAbiRasterizer("cuda")
+    args = _scene(2000, 24, 128, 96)
+    cams = _cams(128, 96, 2)
+    with pytest.raises(RuntimeError, match="views"):
+        rast.forward_views(cams * 5, *args, sh_degree=3)  # 10 > GSR_MAX_VIEWS
+    other = _cams(96, 96, 1)
+    with pytest.raises(RuntimeError, match="every view"):
+        rast.forward_views(cams + other, *args, sh_degree=3)
+    empty = rast.forward_views(cams, np.zeros((0, 3)), np.zeros(0), np.zeros((0, 3)), np.zeros((0, 4)),
+                               np.zeros((0, 1, 3)), None, sh_degree=0, bg=(1, 1, 1))
+    assert float(empty.color.min()) == 1.0 and float(empty.color.max()) == 1.0
