@@ -8,7 +8,7 @@ cd $R
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py \
   -k "allocation_end or golden or synthetic_parity or deterministic or checkpoint or headline" > $O/tests.log 2>&1 && \
-timeout -k 10 240 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_views.py tests/test_gpu_batch.py > $O/tests_views.log 2>&1 ; \
+{ timeout -k 10 240 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_views.py tests/test_gpu_batch.py > $O/tests_views.log 2>&1; r=$?; [ $r -le 1 ]; } && \
 timeout -k 10 400 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_shard_cpp.py tests/test_gpu_train.py tests/test_gpu_dropin.py tests/test_gpu_train_loop.py -k "not configs4" > $O/tests_train.log 2>&1 && \
 timeout -k 10 200 python bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err && \
 timeout -k 10 600 bash scripts/ab.sh $O/ab_b1.jsonl 3 r03head b1pf nopresort && \
