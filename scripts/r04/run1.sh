@@ -11,6 +11,8 @@ timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method threa
 { timeout -k 10 240 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_views.py tests/test_gpu_batch.py > $O/tests_views.log 2>&1; r=$?; [ $r -le 1 ]; } && \
 timeout -k 10 400 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_shard_cpp.py tests/test_gpu_train.py tests/test_gpu_dropin.py tests/test_gpu_train_loop.py -k "not configs4" > $O/tests_train.log 2>&1 && \
 timeout -k 10 200 python bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err && \
+timeout -k 10 200 python bench.py --mode views --config 1k_256 --steps 100 --warmup 10 > $O/views_1k.json 2> $O/views_1k.err && \
+timeout -k 10 200 python bench.py --mode views --config 100k_800 --steps 20 --warmup 3 > $O/views_100k.json 2> $O/views_100k.err && \
 timeout -k 10 600 bash scripts/ab.sh $O/ab_b1.jsonl 3 r03head b1pf nopresort && \
 AB_CONFIG=5m_1080p timeout -k 10 400 bash scripts/ab.sh $O/ab_5m.jsonl 2 nopresort && \
 timeout -k 10 300 python scripts/loop_probe.py /tmp/loop6m.bin --gt 8000000 --init 6000000 --views 48 --iters 2000 --progress 250 > $O/probe_write.log 2>&1 && \
