@@ -394,11 +394,12 @@ def test_sh_rows_at_allocation_end(rast):
     P = 256 * 40 + 7
     s = sc.make_scene(cam, P, max_sh_degree=3, seed=11)
     dpix = sc.make_dL_dpix(cam, seed=12)
-    rows = s.sh_rest.numel()
+    sh_rest = torch.from_numpy(np.ascontiguousarray(s.sh_rest, np.float32))
+    rows = sh_rest.numel()
     total = (rows * 4 + (2 << 20) - 1) // (2 << 20) * (2 << 20) // 4
     big = torch.zeros(total, dtype=torch.float32, device="cuda")
-    tail = big[total - rows:].view(s.sh_rest.shape)
-    tail.copy_(s.sh_rest)
+    tail = big[total - rows:].view(sh_rest.shape)
+    tail.copy_(sh_rest)
     assert tail.data_ptr() + rows * 4 == big.data_ptr() + total * 4
     base = (cam, s.means3D, s.opacities, s.scales, s.rotations, s.sh_dc)
     a = rast.forward(*base, s.sh_rest, sh_degree=3)
