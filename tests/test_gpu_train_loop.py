@@ -108,6 +108,7 @@ def _progress_file():
     return os.path.join(d, "configs4_progress.log")
 
 
+@pytest.mark.timeout(900)
 def test_configs4_at_scale(oracle):
     import time
     L, T = pkg("train_loop"), pkg("trainer")
