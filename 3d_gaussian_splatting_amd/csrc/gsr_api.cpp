@@ -866,15 +866,13 @@ int gsr_shard_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr
     const GeomLayout& gl = sl.geo;
     const uint32_t* tiles = at<uint32_t>(shard_state, gl.tiles);
     const uint4* rect = at<uint4>(shard_state, gl.rect);
-    float* grad2d = at<float>(shard_state, sl.grad2d);  // the summed 2D gradients (written)
-    GSR_STAGE(GSR_STAGE_EXCHANGE, launch_grad_sum(tiles, rect, P, br, at<uint32_t>(shard_state, sl.slot_of),
-                                                  static_cast<const float*>(grad_recv), pair_cap, grad2d, stream),
-              "gradient sum");
-    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, shard_in(gs), 0, P,
-                                                                   at<uint32_t>(shard_state, gl.depth_key),
-                                                                   at<uint32_t>(shard_state, gl.flags), grad2d,
-                                                                   grad_out(grads), stream),
-              "preprocess backward");
+    // B2 sums the bands' returned rows itself (no grad2d round trip, one launch fewer)
+    BandSum bs{tiles, rect, at<uint32_t>(shard_state, sl.slot_of), static_cast<const float4*>(grad_recv), pair_cap, br};
+    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward_banded(*cam, shard_in(gs),
+                                                                          at<uint32_t>(shard_state, gl.depth_key),
+                                                                          at<uint32_t>(shard_state, gl.flags), bs,
+                                                                          grad_out(grads), stream),
+              "preprocess backward (band sum)");
     return 0;
 }
 

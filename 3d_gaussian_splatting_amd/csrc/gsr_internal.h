@@ -213,10 +213,10 @@ struct BandRows {
 };
 
 // State a shard keeps from gsr_shard_forward to gsr_shard_backward: its geometry (F1), the slot
-// each splat took in each band's send block, the pack's per-block counts, and the summed 2D
-// gradients.
+// each splat took in each band's send block and the pack's per-block counts (B2 sums the
+// returned 2D gradients itself: launch_preprocess_backward_banded).
 struct ShardLayout {
-    size_t slot_of, partials, grad2d, total;
+    size_t slot_of, partials, total;
     GeomLayout geo;
     ShardLayout(long long P, int nbands) : geo(P) {
         size_t o = geo.total;
@@ -224,7 +224,6 @@ struct ShardLayout {
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
         slot_of = take(4 * n * (size_t)nbands);
         partials = take(4 * ((size_t)pack_blocks(n) + 1) * (size_t)nbands);
-        grad2d = take(4 * (size_t)kPart * n);
         total = o;
     }
 };

@@ -140,8 +140,30 @@ int launch_pack_splats(const uint32_t* tiles, const uint4* rect, const uint32_t*
 // Band side: nsrc received blocks -> local arrays of nsrc * pair_cap entries (empty slots: no tiles)
 int launch_unpack_splats(const char* recv, int nsrc, int pair_cap, int ty0, int ty1, float4* rec, uint32_t* depth_key,
                          uint32_t* tiles, uint4* rect, hipStream_t s);
-// Shard side: grad2d[g] = sum over g's bands (band order) of back[b][slot_of[b][g]]
-int launch_grad_sum(const uint32_t* tiles, const uint4* rect, int P, const BandRows& br, const uint32_t* slot_of,
-                    const float* back, int pair_cap, float* grad2d, hipStream_t s);
+
+// the bands [b_lo, b_hi] a rect's tile rows [miny, maxy) overlap (b_lo > b_hi: none)
+__device__ __forceinline__ void band_span(const BandRows& br, uint32_t miny, uint32_t maxy, int& b_lo, int& b_hi) {
+    b_lo = br.n;
+    b_hi = -1;
+    for (int b = 0; b < br.n; ++b) {
+        if ((int)miny < br.row[b + 1] && (int)maxy > br.row[b]) {
+            b_lo = b < b_lo ? b : b_lo;
+            b_hi = b;
+        }
+    }
+}
+
+// The shard's returned 2D gradients as B2 reads them when the band sum is fused into it: g's
+// row is the sum, in band order, of back[b][slot_of[b][g]] over the bands g was sent to .
+struct BandSum {
+    const uint32_t* tiles;
+    const uint4* rect;
+    const uint32_t* slot_of;
+    const float4* back;
+    int pair_cap;
+    BandRows br;
+};
+int launch_preprocess_backward_banded(const gsr_camera& cam, const GaussIn& in, const uint32_t* depth_key,
+                                      const uint32_t* flags, const BandSum& bs, const GradOut& out, hipStream_t s);
 
 }  // namespace gsr

@@ -107,12 +107,37 @@ struct BwdIn {
     uint32_t cl;  // stored SH clamp bits (flags != nullptr)
 };
 
+template <bool SUM>
 __device__ __forceinline__ BwdIn load_bwd_in(const GaussIn& in, int g, int o, const uint32_t* __restrict__ depth_key,
-                                             const uint32_t* __restrict__ flags, const float* __restrict__ grad2d) {
+                                             const uint32_t* __restrict__ flags, const float* __restrict__ grad2d,
+                                             const BandSum& bs) {
     BwdIn b;
     b.visible = depth_key[g] != 0xFFFFFFFFu;
-    const float4* src = reinterpret_cast<const float4*>(grad2d + (size_t)kPart * o);
-    const float4 v0 = src[0], v1 = src[1], v2 = src[2];
+    float4 v0, v1, v2;
+    if (SUM) {  // the bands' returned rows, summed in band order
+        v0 = make_float4(0.f, 0.f, 0.f, 0.f);
+        v1 = v0;
+        v2 = v0;
+        if (bs.tiles[g] != 0u) {
+            const uint4 rr = bs.rect[g];
+            int b_lo, b_hi;
+            band_span(bs.br, rr.x >> 16, rr.y >> 16, b_lo, b_hi);
+            for (int k = b_lo; k <= b_hi; ++k) {
+                const uint32_t slot = bs.slot_of[(size_t)k * in.P + g];
+                if (slot >= (uint32_t)bs.pair_cap) continue;  // overflowed: never sent
+                const float4* src = bs.back + ((size_t)k * bs.pair_cap + slot) * 3;
+                const float4 u = src[0], v = src[1], w = src[2];
+                v0.x += u.x; v0.y += u.y; v0.z += u.z; v0.w += u.w;
+                v1.x += v.x; v1.y += v.y; v1.z += v.z; v1.w += v.w;
+                v2.x += w.x;
+            }
+        }
+    } else {
+        const float4* src = reinterpret_cast<const float4*>(grad2d + (size_t)kPart * o);
+        v0 = src[0];
+        v1 = src[1];
+        v2 = src[2];
+    }
     b.g2[0] = v0.x; b.g2[1] = v0.y; b.g2[2] = v0.z; b.g2[3] = v0.w;
     b.g2[4] = v1.x; b.g2[5] = v1.y; b.g2[6] = v1.z; b.g2[7] = v1.w;
     b.g2[8] = v2.x;
@@ -446,10 +471,12 @@ __device__ __forceinline__ GradOut view_out(const GradOut& out, const GradOut& s
     return o;
 }
 
-template <int NV>
+// SUM: the 2D gradients are the shard's band returns (BandSum), summed here (g0 = 0).
+template <int NV, bool SUM>
 __global__ __launch_bounds__(256) void preprocess_backward_kernel(
     const CamArg<NV> cams, const GaussIn in, int g0, int n, const uint32_t* __restrict__ depth_key,
-    const uint32_t* __restrict__ flags, const float* __restrict__ grad2d, GradOut out, const GradOut scratch) {
+    const uint32_t* __restrict__ flags, const float* __restrict__ grad2d, GradOut out, const GradOut scratch,
+    const BandSum bs) {
     extern __shared__ __attribute__((aligned(16))) float sh_lds[];
     const int o = blockIdx.x * 256 + threadIdx.x;
     const int M3 = in.M_rest * 3;
@@ -485,7 +512,7 @@ __global__ __launch_bounds__(256) void preprocess_backward_kernel(
         }
     }
     BwdIn bi{};
-    if (o < n) bi = load_bwd_in(in, g0 + o, o, depth_key, flags, grad2d);
+    if (o < n) bi = load_bwd_in<SUM>(in, g0 + o, o, depth_key, flags, grad2d, bs);
     if (stage) {  // coalesced staging of the block's SH-rest rows (see preprocess_kernel)
         if (v4) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces have landed
@@ -530,8 +557,18 @@ int launch_preprocess_backward(const gsr_camera& cam, const GaussIn& in, int g0,
     if (n <= 0) return 0;
     const size_t lds = (in.sh_rest && !in.colors) ? sizeof(float) * 256 * 3 * in.M_rest : 0;
     const CamArg<1> c1{{cam}};
-    hipLaunchKernelGGL(preprocess_backward_kernel<1>, dim3(div_up(n, 256)), dim3(256), lds, s, c1, in, g0, n,
-                       depth_key, flags, grad2d, out, GradOut{});
+    hipLaunchKernelGGL((preprocess_backward_kernel<1, false>), dim3(div_up(n, 256)), dim3(256), lds, s, c1, in, g0,
+                       n, depth_key, flags, grad2d, out, GradOut{}, BandSum{});
+    return (int)hipGetLastError();
+}
+
+int launch_preprocess_backward_banded(const gsr_camera& cam, const GaussIn& in, const uint32_t* depth_key,
+                                      const uint32_t* flags, const BandSum& bs, const GradOut& out, hipStream_t s) {
+    if (in.P <= 0) return 0;
+    const size_t lds = (in.sh_rest && !in.colors) ? sizeof(float) * 256 * 3 * in.M_rest : 0;
+    const CamArg<1> c1{{cam}};
+    hipLaunchKernelGGL((preprocess_backward_kernel<1, true>), dim3(div_up(in.P, 256)), dim3(256), lds, s, c1, in, 0,
+                       in.P, depth_key, flags, nullptr, out, GradOut{}, bs);
     return (int)hipGetLastError();
 }
 
@@ -543,8 +580,8 @@ int launch_preprocess_backward_views(const gsr_camera* cams, int V, const GaussI
     CamArg<kMaxViews> cv{};
     for (int v = 0; v < V; ++v) cv.c[v] = cams[v];
     const size_t lds = (in.sh_rest && !in.colors) ? sizeof(float) * 256 * 3 * in.M_rest : 0;
-    hipLaunchKernelGGL(preprocess_backward_kernel<kMaxViews>, dim3(div_up(in.P, 256), V), dim3(256), lds, s, cv, in,
-                       0, in.P, depth_key, flags, grad2d, out, scratch);
+    hipLaunchKernelGGL((preprocess_backward_kernel<kMaxViews, false>), dim3(div_up(in.P, 256), V), dim3(256), lds, s,
+                       cv, in, 0, in.P, depth_key, flags, grad2d, out, scratch, BandSum{});
     return (int)hipGetLastError();
 }
 

@@ -1,7 +1,7 @@
 // gsr_shard.hip -- the multi-GPU split of the path (the scaling version): pack the
 // projected Gaussians ("splats") of a Gaussian shard into per-band send blocks, unpack the
-// blocks a band owner receives into its local geometry arrays, and sum the 2D gradients the
-// bands send back, per Gaussian in band order.
+// blocks a band owner receives into its local geometry arrays.  (The 2D gradients the bands
+// send back are summed per Gaussian, in band order, by B2 itself: gsr_preprocess_bwd.hip.)
 //
 // Splat (64 B, GSR_SPLAT_BYTES): the F1 blend record (3 float4) and {depth key, rect lo,
 // rect hi, 0}.  A band owner needs nothing else: its binning (F2..F5), blend (F6) and blend
@@ -23,18 +23,6 @@ constexpr int kWaves = kB / 64;
 __device__ inline uint64_t lanemask_lt() {
     const int lane = threadIdx.x & 63;
     return (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-}
-
-// the bands [b_lo, b_hi] a rect's tile rows [miny, maxy) overlap (b_lo > b_hi: none)
-__device__ __forceinline__ void band_span(const BandRows& br, uint32_t miny, uint32_t maxy, int& b_lo, int& b_hi) {
-    b_lo = br.n;
-    b_hi = -1;
-    for (int b = 0; b < br.n; ++b) {
-        if ((int)miny < br.row[b + 1] && (int)maxy > br.row[b]) {
-            b_lo = b < b_lo ? b : b_lo;
-            b_hi = b;
-        }
-    }
 }
 
 // Per block: splats per band (partials[b * nblk + blk]); optionally the per-tile-row instance
@@ -121,7 +109,7 @@ __global__ __launch_bounds__(1024) void pack_scan_kernel(uint32_t* __restrict__ 
 }
 
 // Scatter: every splat of band b goes to slot partials[b][blk] + (earlier waves' and lanes'
-// splats of the band), in shard order; slot_of[b * P + g] remembers it for the gradient sum.
+// splats of the band), in shard order; slot_of[b * P + g] remembers it for B2's band sum.
 __global__ __launch_bounds__(kB) void pack_scatter_kernel(const uint32_t* __restrict__ tiles,
                                                           const uint4* __restrict__ rect,
                                                           const uint32_t* __restrict__ depth_key,
@@ -228,35 +216,6 @@ __global__ __launch_bounds__(256) void unpack_kernel(const char* __restrict__ re
     }
 }
 
-// Source: grad2d[g] = sum over the bands g was sent to, in band order, of the 2D gradient the
-// band sent back for g's slot (fixed order: deterministic).
-__global__ __launch_bounds__(256) void grad_sum_kernel(const uint32_t* __restrict__ tiles,
-                                                       const uint4* __restrict__ rect, int P, BandRows br,
-                                                       const uint32_t* __restrict__ slot_of,
-                                                       const float4* __restrict__ back, int pair_cap,
-                                                       float4* __restrict__ grad2d) {
-    const int g = blockIdx.x * 256 + threadIdx.x;
-    if (g >= P) return;
-    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b4 = a, c4 = a;
-    if (tiles[g] != 0u) {
-        const uint4 rr = rect[g];
-        int b_lo, b_hi;
-        band_span(br, rr.x >> 16, rr.y >> 16, b_lo, b_hi);
-        for (int b = b_lo; b <= b_hi; ++b) {
-            const uint32_t slot = slot_of[(size_t)b * P + g];
-            if (slot >= (uint32_t)pair_cap) continue;  // overflowed: never sent
-            const float4* src = back + ((size_t)b * pair_cap + slot) * 3;
-            const float4 u = src[0], v = src[1], w = src[2];
-            a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
-            b4.x += v.x; b4.y += v.y; b4.z += v.z; b4.w += v.w;
-            c4.x += w.x;
-        }
-    }
-    grad2d[3 * (size_t)g] = a;
-    grad2d[3 * (size_t)g + 1] = b4;
-    grad2d[3 * (size_t)g + 2] = c4;
-}
-
 }  // namespace
 
 int launch_pack_splats(const uint32_t* tiles, const uint4* rect, const uint32_t* depth_key, const float4* rec, int P,
@@ -284,14 +243,6 @@ int launch_unpack_splats(const char* recv, int nsrc, int pair_cap, int ty0, int 
     const long long blocks = (n + 255) / 256;
     hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0, s, recv,
                        exchange_block_bytes(pair_cap), nsrc, pair_cap, ty0, ty1, rec, depth_key, tiles, rect);
-    return (int)hipGetLastError();
-}
-
-int launch_grad_sum(const uint32_t* tiles, const uint4* rect, int P, const BandRows& br, const uint32_t* slot_of,
-                    const float* back, int pair_cap, float* grad2d, hipStream_t s) {
-    if (P <= 0) return 0;
-    hipLaunchKernelGGL(grad_sum_kernel, dim3(div_up(P, 256)), dim3(256), 0, s, tiles, rect, P, br, slot_of,
-                       reinterpret_cast<const float4*>(back), pair_cap, reinterpret_cast<float4*>(grad2d));
     return (int)hipGetLastError();
 }
 

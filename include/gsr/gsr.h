@@ -234,9 +234,9 @@ int gsr_band_backward(const gsr_camera* cam, const gsr_raster_settings* rs, int3
                       void* alloc_ctx, void* grad_send, void* stream);
 
 /* grad_recv: nbands x pair_cap x GSR_SPLAT_GRAD_BYTES (what gsr_band_backward wrote for this
- * shard, one block per band).  band_rows: the forward's.  grads: the shard's rows.
- * shard_state is written too (the summed per-Gaussian 2D gradients live in it): one backward
- * per state at a time. */
+ * shard, one block per band).  band_rows: the forward's.  grads: the shard's rows.  B2 sums
+ * each Gaussian's returned rows in band order as it loads them (one launch; shard_state is
+ * only read). */
 int gsr_shard_backward(const gsr_camera* cam, const gsr_gaussians* shard, const gsr_raster_settings* rs,
                        int32_t nbands, const int32_t* band_rows, int32_t pair_cap, void* shard_state,
                        const void* grad_recv, const gsr_grads* grads, void* stream);

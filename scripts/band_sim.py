@@ -2,7 +2,7 @@
 """Single-GPU rehearsal of the N-GPU path (bands.simulate_ranks: every rank's calls in one
 process, collectives replaced by block copies).  For each N it times every rank's compute --
 gsr_shard_forward (F1 + splat pack), gsr_band_forward (unpack + F2..F6), gsr_band_backward
-(B1 + per-splat gather), gsr_shard_backward (gradient sum + B2) -- with HIP events on the
+(B1 + per-splat gather), gsr_shard_backward (B2 with the band sum fused) -- with HIP events on the
 launch stream, median over --steps runs, and reports the slowest rank's total: the per-step
 compute an N-GPU run adds to its communication.  Also the bytes each rank moves per step
 (splat blocks out, gradient blocks back, its image band), for the xGMI estimate in DESIGN §7.
