@@ -31,7 +31,10 @@ inline int sort_blocks(long long n) { return n > 0 ? div_up(n, kSortTile) : 0; }
 // multi-GPU splat packing: 256 threads x 4 rounds = 1024 Gaussians per block, so a 1/8 shard
 // (~600k at 5M) still launches ~600 blocks (at the sort's 4096 per block it left 3/4 of the
 // SIMDs idle)
-constexpr int kPackItems = 4;
+#ifndef GSR_PACK_ITEMS
+#define GSR_PACK_ITEMS 4
+#endif
+constexpr int kPackItems = GSR_PACK_ITEMS;
 constexpr int kPackTile = kSortBlock * kPackItems;
 inline int pack_blocks(long long n) { return n > 0 ? div_up(n, kPackTile) : 0; }
 // reduce-then-scan radix-sort scratch (u32 words): 256 digit columns of (blocks + 1) counts
