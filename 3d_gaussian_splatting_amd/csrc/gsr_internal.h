@@ -226,7 +226,11 @@ struct ShardLayout {
         const size_t n = (size_t)(P > 0 ? P : 1);
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
         slot_of = take(4 * n * (size_t)nbands);
-        partials = take(4 * ((size_t)pack_blocks(n) + 1) * (size_t)nbands);
+        // the three-kernel pack's per-block counts, or the fused pack's per-(band, 256-block)
+        // look-back words + ticket
+        const size_t words = ((size_t)pack_blocks(n) + 1) * (size_t)nbands;
+        const size_t fused = (size_t)div_up((long long)n, 256) * (size_t)nbands + 1;
+        partials = take(4 * (words > fused ? words : fused));
         total = o;
     }
 };

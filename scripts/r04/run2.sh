@@ -12,5 +12,5 @@ timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method threa
 timeout -k 10 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_parity.py -k "shard" > $O/tests_shard_parity.log 2>&1 && \
 timeout -k 10 300 python scripts/band_sim.py --config 1m_1080p --worlds 1,2,4,8 > $O/band_sim_1m.jsonl 2> $O/band_sim_1m.err && \
 timeout -k 10 400 python scripts/band_sim.py --config 5m_1080p --worlds 1,8 > $O/band_sim_5m.jsonl 2> $O/band_sim_5m.err && \
-timeout -k 10 600 bash scripts/band_ab.sh $O/band_ab_1m.jsonl 2 1m_1080p 8 pack1 pack2 && \
-timeout -k 10 600 bash scripts/band_ab.sh $O/band_ab_5m.jsonl 2 5m_1080p 8 pack1 pack2
+timeout -k 10 600 bash scripts/band_ab.sh $O/band_ab_1m.jsonl 2 1m_1080p 8 packold pack1 pack2 && \
+timeout -k 10 600 bash scripts/band_ab.sh $O/band_ab_5m.jsonl 2 5m_1080p 8 packold pack1
