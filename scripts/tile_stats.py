@@ -42,6 +42,15 @@ def main():
     np.savez(args.out, n=n, term=term, table=table, grid=np.array([gx, gy]))
     print(f"B1 chunks per tile: mean {chunks.mean():.2f} max {chunks.max()}  checkpoint bytes "
           f"{int((chunks - 1).sum()) * 4096}")
+    # F6 / B1 give XCD x (blocks b with b % 8 == x) a contiguous tile range (xcd_tile): the work
+    # of each XCD's range (terminated records), against an interleaved tile -> XCD assignment
+    T = gx * gy
+    q, r = T // 8, T % 8
+    starts = [x * (q + 1) if x < r else r * (q + 1) + (x - r) * q for x in range(8)] + [T]
+    contig = np.array([term[starts[x]:starts[x + 1]].sum() for x in range(8)], np.float64)
+    inter = np.array([term[x::8].sum() for x in range(8)], np.float64)
+    print(f"XCD work (sum of term): contiguous max/mean {contig.max() / contig.mean():.3f}, "
+          f"interleaved max/mean {inter.max() / inter.mean():.3f}")
     print(f"tiles {gx * gy}  n: mean {n.mean():.0f} p50 {np.median(n):.0f} p99 {np.percentile(n, 99):.0f} "
           f"max {n.max()}  term: mean {term.mean():.0f} p50 {np.median(term):.0f} p99 {np.percentile(term, 99):.0f} "
           f"max {term.max()}")
