@@ -7,6 +7,8 @@ O=$R/gpurun_out/r04_2
 mkdir -p $O
 cd $R
 export TMPDIR=/tmp
+timeout -k 10 700 python -u -m pytest -x -v -s --timeout 120 --timeout-method thread tests/test_gpu_train_loop.py -k configs4 \
+  > $O/tests_configs4.log 2>&1 ; r=$?; [ $r -le 1 ] && \
 timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_multiproc.py tests/test_gpu_shard_cpp.py \
   > $O/tests_shard.log 2>&1 && \
 timeout -k 10 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_parity.py -k "shard" > $O/tests_shard_parity.log 2>&1 && \
