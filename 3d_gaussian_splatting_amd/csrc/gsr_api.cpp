@@ -320,11 +320,12 @@ int fwd_phase1(FwdJob& j, gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_image, voi
     }
     GSR_STAGE(GSR_STAGE_MISC, hipMemsetAsync(v.ranges, 0, il.ovf - il.ranges, stream), "clear ranges");
     if (int e = pre(v)) return e;
-    if (v.presort) {  // global (depth, gid) order, then the scan of tiles_touched in that order
+    if (v.presort) {  // global (depth, gid) order, the rank-order payload and its block sums + K
+        // (the lookback words, unused by the presort path, hold the block sums; F3 finishes the scan)
         GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_depth_presort(v.depth_key, v.tiles, v.rect, (int)j.n, v.dk0, v.dv0,
-                                                             v.dk1, v.dv1, v.dhist, v.rtiles, v.rrect, stream),
+                                                             v.dk1, v.dv1, v.dhist, v.rtiles, v.rrect, v.lookback,
+                                                             v.K_dev, stream),
                   "depth presort");
-        GSR_STAGE(GSR_STAGE_SCAN, launch_scan(v.rtiles, (int)j.n, v.offsets, v.partials, v.K_dev, stream), "scan");
         return 0;
     }
     GSR_STAGE(GSR_STAGE_SCAN, launch_scan(v.tiles, (int)j.n, v.offsets, v.partials, v.K_dev, stream), "scan");
@@ -344,7 +345,7 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
     const int tiles = j.gx * j.gy, ntiles = (j.ty1 - j.ty0) * j.gx;
     if (v.presort)
         GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate_ranked(v.rtiles, v.rrect, v.rect, (int)j.n, j.gx, j.ty0,
-                                                               v.offsets, v.kA, v.vA, cap, stream),
+                                                               v.lookback, v.offsets, v.kA, v.vA, cap, stream),
                   "duplicate (rank order)");
     else
         GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate(v.tiles, v.rect, (int)j.n, j.gx, j.ty0, v.offsets, v.lookback,

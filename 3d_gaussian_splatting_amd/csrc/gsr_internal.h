@@ -84,7 +84,7 @@ struct GeomLayout {
         rect = take(16 * n);  // uint4: minx|miny<<16, maxx|maxy<<16, inst_start, 0
         offsets = take(4 * n);
         partials = take(4 * ((size_t)sort_blocks(n) + 16));  // three-kernel scan
-        lookback = take(4 * (16 + (n + 255) / 256));        // fused scan + duplicate
+        lookback = take(4 * (16 + (n + 255) / 256));        // fused scan + duplicate; presort: block sums
         if (use_presort(P)) {
             dk0 = take(4 * n);
             dv0 = take(4 * n);

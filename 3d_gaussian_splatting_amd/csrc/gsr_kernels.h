@@ -65,13 +65,17 @@ int launch_duplicate(const uint32_t* tiles, uint4* rect, int n, int grid_x, int 
 // ovf2 for a global-memory form using scratch_hi / scratch_lo (K u32 each, free after the tile
 // sort).  K: the binning's capacity (it sizes the LDS form from the mean slice).
 // Presort mode (gsr_internal.h use_presort): the P depth keys sorted (stable, gid values), then
-// each rank's (tiles, rect, gid) gathered into rank order.
+// each rank's (tiles, rect, gid) gathered into rank order with its 256-rank block's tiles_touched
+// sum in bsum (div_up(n, 256) words), which are then scanned in place (exclusive) with the total
+// K into *total_out.
 int launch_depth_presort(const uint32_t* depth_key, const uint32_t* tiles, const uint4* rect, int n, uint32_t* dk0,
                          uint32_t* dv0, uint32_t* dk1, uint32_t* dv1, uint32_t* hist, uint32_t* rtiles, uint4* rrect,
-                         hipStream_t s);
-// F3 in rank order (offsets = the scan of rtiles); writes inst_start into rect[gid].z.
+                         uint32_t* bsum, uint32_t* total_out, hipStream_t s);
+// F3 in rank order: each 256-rank block scans its rtiles from its offset bexcl[block] (writing
+// `offsets`, the inclusive scan the gather reads) and writes inst_start into rect[gid].z.
 int launch_duplicate_ranked(const uint32_t* rtiles, const uint4* rrect, uint4* rect, int n, int grid_x, int ty0,
-                            const uint32_t* offsets, uint32_t* tkey, uint32_t* tgid, long long cap, hipStream_t s);
+                            const uint32_t* bexcl, uint32_t* offsets, uint32_t* tkey, uint32_t* tgid, long long cap,
+                            hipStream_t s);
 int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long K, const uint32_t* depth_key,
                            uint32_t* gid, uint32_t* ovf, uint32_t* ovf_count, uint32_t* ovf2, uint32_t* ovf2_count,
                            uint32_t* done, uint32_t* scratch_hi, uint32_t* scratch_lo,

@@ -496,20 +496,29 @@ __global__ __launch_bounds__(256) void scan_duplicate_kernel(const uint32_t* __r
 
 // RANKED (presort mode): lane i is depth rank i; its tiles / rect / gid come from the rank-order
 // payload (rtiles / rrect, coalesced) and inst_start goes to rect[gid] (one scattered word).
+// RANKED also scans: `bexcl` holds the exclusive offsets of the 256-rank blocks (rank_payload_kernel
+// summed each block, scan_partials scanned the sums), the block scans its own ranks and writes
+// `offsets` (the gather reads them) -- the three-kernel scan's reduce and downsweep passes gone.
 template <bool RANKED>
-__global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restrict__ offsets,
+__global__ __launch_bounds__(256) void duplicate_kernel(uint32_t* __restrict__ offsets,
                                                         const uint32_t* __restrict__ tiles,
                                                         uint4* __restrict__ rect, const uint4* __restrict__ rrect,
                                                         int P, int grid_x, int ty0,
                                                         uint32_t* __restrict__ tkey, uint32_t* __restrict__ tgid,
-                                                        long long cap) {
+                                                        long long cap, const uint32_t* __restrict__ bexcl) {
     __shared__ uint32_t s_start[kWaves][64], s_g[kWaves][64], s_w[kWaves][64], s_x0[kWaves][64],
         s_y0[kWaves][64];
+    __shared__ uint32_t wsum[kWaves];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int i = blockIdx.x * 256 + tid;  // gid, or depth rank (RANKED)
     const bool valid = i < P;
     uint32_t nt = 0, end = 0, g = (uint32_t)i;
-    if (valid) {
+    if (RANKED) {
+        if (valid) nt = tiles[i];
+        uint32_t tot;
+        end = bexcl[blockIdx.x] + block_exclusive_scan(nt, wsum, &tot) + nt;
+        if (valid) offsets[i] = end;
+    } else if (valid) {
         nt = tiles[i];
         end = offsets[i];
     }
@@ -549,23 +558,33 @@ __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restri
 // rtiles[r] = tiles[g], rrect[r] = (rect lo, rect hi, g, 0) for g = the sorted gid at rank r.  The
 // reads are random (16 B per visible Gaussian, L2 / MALL-resident), the writes coalesced; the
 // scan, F3 and the gather then stream the payload instead of each making random reads.
+// It also sums each 256-rank block's tiles_touched into bsum[block] (for the ranked F3's scan).
 __global__ __launch_bounds__(256) void rank_payload_kernel(const uint32_t* __restrict__ sgid,
                                                            const uint32_t* __restrict__ tiles,
                                                            const uint4* __restrict__ rect, int n,
                                                            uint32_t* __restrict__ rtiles,
-                                                           uint4* __restrict__ rrect) {
+                                                           uint4* __restrict__ rrect, uint32_t* __restrict__ bsum) {
+    __shared__ uint32_t wsum[kWaves];
     const int r = blockIdx.x * 256 + threadIdx.x;
-    if (r >= n) return;
-    const uint32_t g = sgid[r];
-    const uint32_t nt = tiles[g];
-    uint4 q = make_uint4(0u, 0u, g, 0u);
-    if (nt) {
-        const uint4 rr = rect[g];
-        q.x = rr.x;
-        q.y = rr.y;
+    uint32_t nt = 0;
+    if (r < n) {
+        const uint32_t g = sgid[r];
+        nt = tiles[g];
+        uint4 q = make_uint4(0u, 0u, g, 0u);
+        if (nt) {
+            const uint4 rr = rect[g];
+            q.x = rr.x;
+            q.y = rr.y;
+        }
+        rtiles[r] = nt;
+        rrect[r] = q;
     }
-    rtiles[r] = nt;
-    rrect[r] = q;
+    uint32_t s = nt;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) bsum[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
 }
 
 // ---- F5 finalize: tile ranges from the sorted keys ----
@@ -985,26 +1004,30 @@ int launch_duplicate(const uint32_t* tiles, uint4* rect, int n, int grid_x, int 
         return (int)hipGetLastError();
     }
     hipLaunchKernelGGL(duplicate_kernel<false>, dim3(div_up(n, 256)), dim3(256), 0, s, offsets, tiles, rect,
-                       nullptr, n, grid_x, ty0, tkey, tgid, cap);
+                       nullptr, n, grid_x, ty0, tkey, tgid, cap, nullptr);
     return (int)hipGetLastError();
 }
 
 int launch_depth_presort(const uint32_t* depth_key, const uint32_t* tiles, const uint4* rect, int n, uint32_t* dk0,
                          uint32_t* dv0, uint32_t* dk1, uint32_t* dv1, uint32_t* hist, uint32_t* rtiles, uint4* rrect,
-                         hipStream_t s) {
-    if (n <= 0) return 0;
+                         uint32_t* bsum, uint32_t* total_out, hipStream_t s) {
+    if (n <= 0) return (int)hipMemsetAsync(total_out, 0, sizeof(uint32_t), s);
     int which = -1;  // 4 passes of 8 bits: the result lands in (dk1, dv1)
     if (int e = radix_sort(depth_key, nullptr, dk0, dv0, dk1, dv1, n, nullptr, 32, hist, &which, s)) return e;
     const uint32_t* sgid = which == 0 ? dv0 : dv1;
-    hipLaunchKernelGGL(rank_payload_kernel, dim3(div_up(n, 256)), dim3(256), 0, s, sgid, tiles, rect, n, rtiles, rrect);
+    const int nb = div_up(n, 256);
+    hipLaunchKernelGGL(rank_payload_kernel, dim3(nb), dim3(256), 0, s, sgid, tiles, rect, n, rtiles, rrect, bsum);
+    // the 256-rank blocks' exclusive offsets and K: F3 (launch_duplicate_ranked) scans inside them
+    hipLaunchKernelGGL(scan_partials, dim3(1), dim3(1024), 0, s, bsum, nb, total_out);
     return (int)hipGetLastError();
 }
 
 int launch_duplicate_ranked(const uint32_t* rtiles, const uint4* rrect, uint4* rect, int n, int grid_x, int ty0,
-                            const uint32_t* offsets, uint32_t* tkey, uint32_t* tgid, long long cap, hipStream_t s) {
+                            const uint32_t* bexcl, uint32_t* offsets, uint32_t* tkey, uint32_t* tgid, long long cap,
+                            hipStream_t s) {
     if (n <= 0) return 0;
     hipLaunchKernelGGL(duplicate_kernel<true>, dim3(div_up(n, 256)), dim3(256), 0, s, offsets, rtiles, rect, rrect, n,
-                       grid_x, ty0, tkey, tgid, cap);
+                       grid_x, ty0, tkey, tgid, cap, bexcl);
     return (int)hipGetLastError();
 }
 
