@@ -13,7 +13,7 @@ timeout -k 10 400 python -u -m pytest -x -v --timeout 240 --timeout-method threa
 timeout -k 10 200 python bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err && \
 timeout -k 10 200 python bench.py --mode views --config 1k_256 --steps 100 --warmup 10 > $O/views_1k.json 2> $O/views_1k.err && \
 timeout -k 10 200 python bench.py --mode views --config 100k_800 --steps 20 --warmup 3 > $O/views_100k.json 2> $O/views_100k.err && \
-timeout -k 10 600 bash scripts/ab.sh $O/ab_b1.jsonl 2 r03head b1pf b1cmp f1persist b2persist nopresort && \
+timeout -k 10 600 bash scripts/ab.sh $O/ab_b1.jsonl 2 b1pf b1cmp f1persist b2persist f1b2persist && \
 AB_CONFIG=5m_1080p timeout -k 10 400 bash scripts/ab.sh $O/ab_5m.jsonl 2 nopresort f1b2persist && \
 for v in f1b2persist b1cmp b1pf; do
   { GSR_HIP_LIB=$R/3d_gaussian_splatting_amd/lib/variants/$v/libgsr_hip.so timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "golden or synthetic_parity or headline" > $O/parity_$v.log 2>&1; r=$?; [ $r -le 1 ]; } || exit 9

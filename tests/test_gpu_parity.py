@@ -251,12 +251,13 @@ def test_capacity_bound_and_overflow(rast):
     assert bool(torch.isfinite(st.color).all()) and all(bool(torch.isfinite(v).all()) for v in g.values())
 
 
-@pytest.mark.parametrize("P", [600_000, 1_000_000])
+@pytest.mark.parametrize("P", [600_000, 1_000_000, 2_500_000])  # 2.5M: past the presort threshold
 def test_headline_config_vs_oracle(P, rast, oracle):
     """BASELINE configs[2] at 1920x1080 / SH3: 1M Gaussians is the bench's own workload (the same
-    make_scene seed), 600k a second draw of the same shape (both > 2^19: the three-kernel scan;
-    8160 tiles: the two-wave F6), against the oracle: bit-exact keys, sort, ranges; RGB and every
-    gradient within the §8d bars, element-wise included."""
+    make_scene seed), 600k a second draw of the same shape (both > 2^19: the three-kernel scan and
+    the per-tile depth sort; 8160 tiles: the two-wave F6), 2.5M past the global depth pre-sort's
+    threshold (rank-order payload, scan and F3), against the oracle: bit-exact keys, sort, ranges;
+    RGB and every gradient within the §8d bars, element-wise included."""
     gr, sc = pkg("graphics"), pkg("scene")
     cam = gr.synthetic_camera(1920, 1080)
     s = sc.make_scene(cam, P, max_sh_degree=3, seed=0)

@@ -75,8 +75,8 @@ def test_views_presort_switch():
     native = pkg("native")
     rast = pkg("rasterizer").CAbiRasterizer("cuda")
     cams = _cams(400, 304, 4)
-    P = 160000
-    assert P < (1 << 19) + 1 <= 4 * P
+    P = 600000
+    assert P < (1 << 21) + 1 <= 4 * P  # gsr_internal.h GSR_PRESORT_MIN
     _check(rast, cams, _scene(P, 22, 400, 304))
     assert native.GSR_MAX_VIEWS == 8
 
