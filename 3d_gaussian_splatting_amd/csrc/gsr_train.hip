@@ -311,7 +311,27 @@ struct AdamArgs {
 __device__ __forceinline__ bool guard_tripped(const uint32_t* k, uint32_t cap) {
     return k != nullptr && *k > cap;  // written by an earlier kernel of the stream
 }
-constexpr int kAdamBlock = 256, kAdamPerBlock = 4 * kAdamBlock;
+#ifndef GSR_ADAM_NT
+#define GSR_ADAM_NT 0  // streaming (non-temporal) loads / stores: the moments are touched once per step
+#endif
+#ifndef GSR_ADAM_VEC
+#define GSR_ADAM_VEC 1  // float4s per thread and array
+#endif
+constexpr int kAdamBlock = 256, kAdamVec = GSR_ADAM_VEC, kAdamPerBlock = 4 * kAdamVec * kAdamBlock;
+__device__ __forceinline__ float4 ld4(const float* p) {
+#if GSR_ADAM_NT
+    return __builtin_nontemporal_load(reinterpret_cast<const float4*>(p));
+#else
+    return *reinterpret_cast<const float4*>(p);
+#endif
+}
+__device__ __forceinline__ void st4(float* p, float4 v) {
+#if GSR_ADAM_NT
+    __builtin_nontemporal_store(v, reinterpret_cast<float4*>(p));
+#else
+    *reinterpret_cast<float4*>(p) = v;
+#endif
+}
 
 __device__ __forceinline__ float adam_one(float& p, float g, float& m, float& v, float ss, float b2s, const AdamArgs& a) {
     m = fmaf(a.omb1, g, m * a.b1);
@@ -321,45 +341,18 @@ __device__ __forceinline__ float adam_one(float& p, float g, float& m, float& v,
     return p;
 }
 
-__global__ __launch_bounds__(kAdamBlock) void adam_kernel(const AdamArgs a) {
-    if (guard_tripped(a.guard_k, a.guard_cap)) return;
-    int gi = 0;
-    while (gi + 1 < a.ngroups && (int)blockIdx.x >= a.blk_start[gi + 1]) ++gi;  // wave-uniform
-    const gsr_adam_group& G = a.g[gi];
-    const long long e0 = ((long long)(blockIdx.x - a.blk_start[gi]) * kAdamBlock + threadIdx.x) * 4;
-    if (e0 >= G.n) return;
-    const float ss = a.step_size[gi], b2s = a.bc2_sqrt[gi];
-    float p[4], g[4], m[4], v[4];
-    const int cnt = (int)(G.n - e0 < 4 ? G.n - e0 : 4);
-    if (cnt == 4) {
-        const float4 P4 = *reinterpret_cast<const float4*>(G.param + e0);
-        const float4 G4 = *reinterpret_cast<const float4*>(G.grad + e0);
-        const float4 M4 = *reinterpret_cast<const float4*>(G.exp_avg + e0);
-        const float4 V4 = *reinterpret_cast<const float4*>(G.exp_avg_sq + e0);
-        p[0] = P4.x, p[1] = P4.y, p[2] = P4.z, p[3] = P4.w;
-        g[0] = G4.x, g[1] = G4.y, g[2] = G4.z, g[3] = G4.w;
-        m[0] = M4.x, m[1] = M4.y, m[2] = M4.z, m[3] = M4.w;
-        v[0] = V4.x, v[1] = V4.y, v[2] = V4.z, v[3] = V4.w;
-    } else {
-        for (int k = 0; k < 4; ++k) {
-            const bool in = k < cnt;
-            p[k] = in ? G.param[e0 + k] : 0.f;
-            g[k] = in ? G.grad[e0 + k] : 0.f;
-            m[k] = in ? G.exp_avg[e0 + k] : 0.f;
-            v[k] = in ? G.exp_avg_sq[e0 + k] : 0.f;
-        }
-    }
+__device__ __forceinline__ void adam_act_grad(int act, float (&p)[4], float (&g)[4]) {
     // activation backward: gradient w.r.t. the raw leaf
-    if (G.act == GSR_ACT_EXP) {
+    if (act == GSR_ACT_EXP) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) g[k] = g[k] * expf(p[k]);
-    } else if (G.act == GSR_ACT_SIGMOID) {
+    } else if (act == GSR_ACT_SIGMOID) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const float s = 1.0f / (1.0f + expf(-p[k]));
             g[k] = g[k] * (1.0f - s) * s;
         }
-    } else if (G.act == GSR_ACT_NORMALIZE4) {  // one row of 4 (n % 4 == 0 checked on the host)
+    } else if (act == GSR_ACT_NORMALIZE4) {  // one row of 4 (n % 4 == 0 checked on the host)
         const float nr = sqrtf(p[0] * p[0] + p[1] * p[1] + p[2] * p[2] + p[3] * p[3]);
         const float n = fmaxf(nr, 1e-12f);
         const float dot = g[0] * p[0] + g[1] * p[1] + g[2] * p[2] + g[3] * p[3];
@@ -369,17 +362,59 @@ __global__ __launch_bounds__(kAdamBlock) void adam_kernel(const AdamArgs a) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) g[k] = g[k] / n - c * p[k];
     }
+}
+
+// kAdamVec float4 columns per thread (column u of a block is coalesced); all loads of the
+// thread are issued before any update so that its bytes are in flight together.
+__global__ __launch_bounds__(kAdamBlock) void adam_kernel(const AdamArgs a) {
+    if (guard_tripped(a.guard_k, a.guard_cap)) return;
+    int gi = 0;
+    while (gi + 1 < a.ngroups && (int)blockIdx.x >= a.blk_start[gi + 1]) ++gi;  // wave-uniform
+    const gsr_adam_group& G = a.g[gi];
+    const float ss = a.step_size[gi], b2s = a.bc2_sqrt[gi];
+    float p[kAdamVec][4], g[kAdamVec][4], m[kAdamVec][4], v[kAdamVec][4];
+    long long e0[kAdamVec];
+    int cnt[kAdamVec];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) adam_one(p[k], g[k], m[k], v[k], ss, b2s, a);
-    if (cnt == 4) {
-        *reinterpret_cast<float4*>(G.param + e0) = make_float4(p[0], p[1], p[2], p[3]);
-        *reinterpret_cast<float4*>(G.exp_avg + e0) = make_float4(m[0], m[1], m[2], m[3]);
-        *reinterpret_cast<float4*>(G.exp_avg_sq + e0) = make_float4(v[0], v[1], v[2], v[3]);
-    } else {
-        for (int k = 0; k < cnt; ++k) {
-            G.param[e0 + k] = p[k];
-            G.exp_avg[e0 + k] = m[k];
-            G.exp_avg_sq[e0 + k] = v[k];
+    for (int u = 0; u < kAdamVec; ++u) {
+        e0[u] = (((long long)(blockIdx.x - a.blk_start[gi]) * kAdamVec + u) * kAdamBlock + threadIdx.x) * 4;
+        const long long left = G.n - e0[u];
+        cnt[u] = left <= 0 ? 0 : (left < 4 ? (int)left : 4);
+        if (cnt[u] == 4) {
+            const float4 P4 = ld4(G.param + e0[u]);
+            const float4 G4 = ld4(G.grad + e0[u]);
+            const float4 M4 = ld4(G.exp_avg + e0[u]);
+            const float4 V4 = ld4(G.exp_avg_sq + e0[u]);
+            p[u][0] = P4.x, p[u][1] = P4.y, p[u][2] = P4.z, p[u][3] = P4.w;
+            g[u][0] = G4.x, g[u][1] = G4.y, g[u][2] = G4.z, g[u][3] = G4.w;
+            m[u][0] = M4.x, m[u][1] = M4.y, m[u][2] = M4.z, m[u][3] = M4.w;
+            v[u][0] = V4.x, v[u][1] = V4.y, v[u][2] = V4.z, v[u][3] = V4.w;
+        } else {
+            for (int k = 0; k < 4; ++k) {
+                const bool in = k < cnt[u];
+                p[u][k] = in ? G.param[e0[u] + k] : 0.f;
+                g[u][k] = in ? G.grad[e0[u] + k] : 0.f;
+                m[u][k] = in ? G.exp_avg[e0[u] + k] : 0.f;
+                v[u][k] = in ? G.exp_avg_sq[e0[u] + k] : 0.f;
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < kAdamVec; ++u) {
+        if (cnt[u] == 0) continue;
+        adam_act_grad(G.act, p[u], g[u]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) adam_one(p[u][k], g[u][k], m[u][k], v[u][k], ss, b2s, a);
+        if (cnt[u] == 4) {
+            st4(G.param + e0[u], make_float4(p[u][0], p[u][1], p[u][2], p[u][3]));
+            st4(G.exp_avg + e0[u], make_float4(m[u][0], m[u][1], m[u][2], m[u][3]));
+            st4(G.exp_avg_sq + e0[u], make_float4(v[u][0], v[u][1], v[u][2], v[u][3]));
+        } else {
+            for (int k = 0; k < cnt[u]; ++k) {
+                G.param[e0[u] + k] = p[u][k];
+                G.exp_avg[e0[u] + k] = m[u][k];
+                G.exp_avg_sq[e0[u] + k] = v[u][k];
+            }
         }
     }
 }
