@@ -318,16 +318,19 @@ __device__ __forceinline__ bool guard_tripped(const uint32_t* k, uint32_t cap) {
 #define GSR_ADAM_VEC 1  // float4s per thread and array
 #endif
 constexpr int kAdamBlock = 256, kAdamVec = GSR_ADAM_VEC, kAdamPerBlock = 4 * kAdamVec * kAdamBlock;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 ld4(const float* p) {
 #if GSR_ADAM_NT
-    return __builtin_nontemporal_load(reinterpret_cast<const float4*>(p));
+    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
 #else
     return *reinterpret_cast<const float4*>(p);
 #endif
 }
 __device__ __forceinline__ void st4(float* p, float4 v) {
 #if GSR_ADAM_NT
-    __builtin_nontemporal_store(v, reinterpret_cast<float4*>(p));
+    const f32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<f32x4*>(p));
 #else
     *reinterpret_cast<float4*>(p) = v;
 #endif
