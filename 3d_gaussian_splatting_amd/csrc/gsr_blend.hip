@@ -460,16 +460,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                                                             const float4* __restrict__ lay) {
     // One block of LDS with srec first: the record fields then sit within the immediate offsets
     // of the record reads (8-bit dword offsets of ds_read2), so a record costs no address add.
-#ifndef GSR_B1_COMPACT
-#define GSR_B1_COMPACT 0
-#endif
     __shared__ struct {
         float4 srec[64 * 3];
         uint32_t sjl[64];                  // the batch's emission indices, by batch slot
         float qpark[kPark * kParkSlot];    // [slot][quad][9 of 12]
-#if GSR_B1_COMPACT
-        uint32_t smk[64];                  // the visited records' stripe masks, in visit order
-#endif
     } lds;
     float4* const srec = lds.srec;
     uint32_t* const sjl = lds.sjl;
@@ -562,36 +556,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
         // which starts from a dead checkpoint) contributes nothing; its entries stay unflagged.
         if (live == 0) break;
         uint32_t jl = 0, smask = 0;
-#if GSR_B1_COMPACT
-        // the records with a live stripe, compacted into visit order (slot = rank among them):
-        // the walk below is a uniform counter, with no bit scan or readlane per record
-        float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
-        if (lane < cnt) {
-            const uint32_t g = sorted_gid[range.x + base + lane];
-            const uint4 rr = rect[g];
-            const int minx = rr.x & 0xFFFF, miny = rr.x >> 16, maxx = rr.y & 0xFFFF;
-            const int y0 = miny > geo.ty0 ? miny : geo.ty0;
-            jl = rr.z + (uint32_t)((ty - y0) * (maxx - minx) + (tx - minx));
-            const float4* r = rec + 3 * (size_t)g;
-            r0 = r[0];
-            r1 = r[1];
-            r2 = r[2];
-            smask = stripe_mask(r0, r1, r2, bx0, by0);
-        }
-        const bool vis = (smask & live) != 0u;
-        const uint64_t vmask = __ballot(vis);
-        const int nvis = __popcll(vmask);
-        if (vis) {
-            const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(vmask >> 32),
-                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)vmask, 0u));
-            srec[3 * pos + 0] = r0;
-            srec[3 * pos + 1] = r1;
-            srec[3 * pos + 2] = r2;
-            sjl[pos] = jl;
-            lds.smk[pos] = smask;
-        }
-        __syncthreads();
-#elif GSR_B1_LAYOUT
+#if GSR_B1_LAYOUT
         if (lane < cnt) {  // F6's copy: one coalesced 64-B read, no gid -> rect / record chain
             const float4* src = lay + 4 * ((size_t)range.x + base + lane);
             const float4 r0 = src[0], r1 = src[1], r2 = src[2], r3 = src[3];
@@ -626,17 +591,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
 #endif
         int visited = 0, parked = 0;
         uint32_t kpack = 0;  // batch slots of the parked records, 6 bits each
-#ifndef GSR_B1_PREFETCH
-#define GSR_B1_PREFETCH 0
-#endif
         // one visited record (batch slot k): its stripes, then its moments parked / flushed;
         // true when every pixel of the tile has finished
         auto record = [&](const int k, const float4 r0, const float4 r1, const float4 r2) -> bool {
-#if GSR_B1_COMPACT
-            const uint32_t m = lds.smk[k] & live;
-#else
             const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)smask, k) & live;
-#endif
             const float dx = r0.x - pfx;
             const float bdx = r0.w * dx;
             const float K = fmaf(r0.z * dx, dx, r2.w);
@@ -702,44 +660,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
             }
             return false;
         };
-#if GSR_B1_COMPACT
-        for (int k = 0; k < nvis; ++k)
-            if (record(k, srec[3 * k + 0], srec[3 * k + 1], srec[3 * k + 2])) break;
-#elif GSR_B1_PREFETCH
-        // software pipeline, unrolled by two so the two records' registers never need copies:
-        // the next visited record's LDS reads are issued before the current one's stripes run
-        if (todo) {
-            int ka = __builtin_ctzll(todo);
-            float4 a0 = srec[3 * ka + 0], a1 = srec[3 * ka + 1], a2 = srec[3 * ka + 2];
-            while (true) {
-                todo &= todo - 1;
-                int kb = -1;
-                float4 b0, b1, b2;
-                if (todo) {  // wave-uniform
-                    kb = __builtin_ctzll(todo);
-                    b0 = srec[3 * kb + 0];
-                    b1 = srec[3 * kb + 1];
-                    b2 = srec[3 * kb + 2];
-                }
-                if (record(ka, a0, a1, a2) || kb < 0) break;
-                todo &= todo - 1;
-                ka = -1;
-                if (todo) {
-                    ka = __builtin_ctzll(todo);
-                    a0 = srec[3 * ka + 0];
-                    a1 = srec[3 * ka + 1];
-                    a2 = srec[3 * ka + 2];
-                }
-                if (record(kb, b0, b1, b2) || ka < 0) break;
-            }
-        }
-#else
         while (todo) {
             const int k = __builtin_ctzll(todo);
             todo &= todo - 1;
             if (record(k, srec[3 * k + 0], srec[3 * k + 1], srec[3 * k + 2])) break;
         }
-#endif
         if (parked) park_flush(qpark, sjl, kpack, parked, p8f, p1, fl, lane);
         __syncthreads();  // srec / qpark are rewritten by the next batch
     }

@@ -488,112 +488,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void p
     }
 }
 
-// F1, persistent and double-buffered (GSR_F1_PERSIST): one-wave blocks, each looping over groups
-// of 64 Gaussians (group i = blockIdx.x + k * gridDim.x).  A wave owns two 12-KB LDS buffers:
-// the SH-rest rows of group k + 1 are in flight by DMA while group k is projected and shaded,
-// so the SH stream (180 of F1's ~250 B per Gaussian) keeps HBM busy through the compute phase
-// instead of waiting for the next block's launch.  12 DMA pieces per group always (the pieces
-// past the group's rows are range-checked: zero-filled, no memory traffic), so one immediate
-// vmcnt covers "everything but the next group's DMA" -- gfx9 counts stores in vmcnt too, and
-// every load / store issued before that DMA must have landed.  Same per-Gaussian functions as
-// preprocess_kernel: bit-identical outputs.
-constexpr int kPersistPieces = 12;  // 1-KB pieces per group (M3 <= 48)
-
-template <int NV>
-__global__ __launch_bounds__(64) void preprocess_persist_kernel(const CamArg<NV> cams, const GaussIn in, int grid_x,
-                                                                int grid_y, int ty0, int ty1, PreOut out) {
-    extern __shared__ __attribute__((aligned(16))) float sh_lds[];  // 2 x kPersistPieces KB
-    const int view = NV > 1 ? (int)blockIdx.y : 0;
-    const gsr_camera& cam = cams.c[NV > 1 ? view : 0];
-    const int ln = threadIdx.x;
-    const int M3 = in.M_rest * 3;
-    const int nb = (in.D + 1) * (in.D + 1);
-    const int groups = (in.P + 63) / 64;
-    auto* lds = (__attribute__((address_space(3))) char*)sh_lds;
-    auto issue = [&](int grp, int buf) {  // group grp's rows -> buffer buf (range-checked)
-        const int rows = in.P - grp * 64 < 64 ? in.P - grp * 64 : 64;
-        const auto src = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in.sh_rest + (size_t)grp * 64 * M3), 0,
-                                                           rows * M3 * (int)sizeof(float), 0x00020000);
-#pragma unroll
-        for (int q = 0; q < kPersistPieces; ++q)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(src, lds + buf * kPersistPieces * 1024 + 1024 * q, 16,
-                                                     ln * 16 + 1024 * q, 0, 0, 0);
-    };
-    uint32_t kacc = 0, cacc = 0;
-    int grp = blockIdx.x, buf = 0;
-    if (grp < groups) issue(grp, 0);
-    for (; grp < groups; grp += gridDim.x, buf ^= 1) {
-        const int g = grp * 64 + ln;
-        const size_t e = (size_t)view * in.P + g;
-        Params I{};
-        if (g < in.P) I = load_params(in, g);
-        const int nxt = grp + gridDim.x;
-        // the buffer the next DMA overwrites was last read by the previous group: its LDS reads
-        // have completed (their values were consumed before that group's stores)
-        if (nxt < groups) {
-            issue(nxt, buf ^ 1);
-            asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // all but the next group's DMA
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        Geo G{};
-        G.key = 0xFFFFFFFFu;
-        if (g < in.P) {
-            G = preprocess_geom(cam, in, I, grid_x, grid_y, ty0, ty1);
-            if (NV > 1) {
-                G.miny += view * grid_y;
-                G.maxy += view * grid_y;
-            }
-            out.radii[e] = G.radius;
-            out.depth_key[e] = G.key;
-            out.tiles[e] = G.tiles;
-        }
-        const bool need = G.tiles != 0;
-        if (need) {
-            float rgb[3] = {I.c0, I.c1, I.c2}, basis[16];
-            sh_basis(cam, in, I, basis);
-#pragma unroll
-            for (int ch = 0; ch < 3; ++ch) rgb[ch] = basis[0] * rgb[ch];
-            const float* rest = sh_lds + buf * kPersistPieces * 256 + ln * M3;
-#pragma unroll
-            for (int ch = 0; ch < 3; ++ch) {
-                float r = rgb[ch];
-#pragma unroll
-                for (int k = 1; k < 16; ++k)
-                    if (k < nb) r = r + basis[k] * rest[3 * (k - 1) + ch];
-                rgb[ch] = r;
-            }
-            uint32_t clamped = 0;
-#pragma unroll
-            for (int ch = 0; ch < 3; ++ch) {
-                const float r = rgb[ch] + 0.5f;
-                clamped |= (r < 0.0f ? 1u : 0u) << ch;
-                rgb[ch] = fmaxf(r, 0.0f);
-            }
-            write_record(e, I.opac, G, rgb, clamped, out);
-        }
-        kacc += G.tiles;
-        cacc += G.tiles ? 1u : 0u;
-    }
-    if (out.counters) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            kacc += __shfl_xor(kacc, o, 64);
-            cacc += __shfl_xor(cacc, o, 64);
-        }
-        if (ln == 0) {
-            const int slot = blockIdx.x & (kCountSlots - 1);
-            if (kacc) atomicAdd(out.counters + kCountSlots + slot, kacc);
-            if (cacc) atomicAdd(out.counters + slot, cacc);
-        }
-    }
-}
-
 }  // namespace
-
-#ifndef GSR_F1_PERSIST
-#define GSR_F1_PERSIST 0
-#endif
 
 template <int NV>
 static void launch_preprocess_nv(const CamArg<NV>& cams, int V, const GaussIn& in, int ty0, int ty1,
@@ -601,15 +496,6 @@ static void launch_preprocess_nv(const CamArg<NV>& cams, int V, const GaussIn& i
     const int gx = div_up(cams.c[0].width, kTile), gy = div_up(cams.c[0].height, kTile);
     const bool sh = in.sh_rest && !in.colors && in.D > 0;
     const dim3 grid(div_up(in.P, 256), V), block(256);
-    if (GSR_F1_PERSIST && sh && in.M_rest * 3 <= 48 && (reinterpret_cast<uintptr_t>(in.sh_rest) & 15) == 0) {
-        // 6 one-wave blocks per CU by LDS (2 x 12 KB each); views share the waves by grid.y
-        const int groups = div_up(in.P, 64);
-        const int per_view = (256 * 6 + V - 1) / V;
-        const dim3 pgrid(groups < per_view ? groups : per_view, V);
-        hipLaunchKernelGGL((preprocess_persist_kernel<NV>), pgrid, dim3(64), 2 * kPersistPieces * 1024, s, cams, in, gx,
-                           gy, ty0, ty1, out);
-        return;
-    }
     if (sh && GSR_F1_SH_MODE == kShGlds && in.M_rest * 3 <= 48 && (reinterpret_cast<uintptr_t>(in.sh_rest) & 15) == 0)
         hipLaunchKernelGGL((preprocess_kernel<kShGlds, NV>), grid, block,
                            4 * 1024 * ((64 * in.M_rest * 3 * 4 + 1023) / 1024), s, cams, in, gx, gy, ty0, ty1, out);

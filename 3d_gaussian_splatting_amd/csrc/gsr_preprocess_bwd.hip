@@ -536,65 +536,7 @@ __global__ __launch_bounds__(256) void preprocess_backward_kernel(
     }
 }
 
-// B2, persistent and double-buffered (GSR_B2_PERSIST; the F1 twin in gsr_preprocess.hip): one-wave
-// blocks looping over groups of 64 Gaussians, two 12-KB LDS buffers per wave.  Group k + 1's
-// SH-rest rows are in flight by DMA while group k runs the chain rule into its buffer and writes
-// the gradient rows back from it; the buffer is reused two groups later, after its write-back's
-// LDS reads have returned.  Same per-Gaussian function: bit-identical outputs.
-constexpr int kPersistPieces = 12;
-
-__global__ __launch_bounds__(64) void preprocess_backward_persist_kernel(const gsr_camera cam, const GaussIn in,
-                                                                         const uint32_t* __restrict__ depth_key,
-                                                                         const uint32_t* __restrict__ flags,
-                                                                         const float* __restrict__ grad2d,
-                                                                         GradOut out) {
-    extern __shared__ __attribute__((aligned(16))) float sh_lds[];
-    const int ln = threadIdx.x;
-    const int M3 = in.M_rest * 3;
-    const int groups = (in.P + 63) / 64;
-    auto* lds = (__attribute__((address_space(3))) char*)sh_lds;
-    auto issue = [&](int grp, int buf) {
-        const int rows = in.P - grp * 64 < 64 ? in.P - grp * 64 : 64;
-        const auto src = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in.sh_rest + (size_t)grp * 64 * M3), 0,
-                                                           rows * M3 * (int)sizeof(float), 0x00020000);
-#pragma unroll
-        for (int q = 0; q < kPersistPieces; ++q)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(src, lds + buf * kPersistPieces * 1024 + 1024 * q, 16,
-                                                     ln * 16 + 1024 * q, 0, 0, 0);
-    };
-    int grp = blockIdx.x, buf = 0;
-    if (grp < groups) issue(grp, 0);
-    for (; grp < groups; grp += gridDim.x, buf ^= 1) {
-        const int g = grp * 64 + ln;
-        BwdIn bi{};
-        if (g < in.P) bi = load_bwd_in<false>(in, g, g, depth_key, flags, grad2d, BandSum{});
-        const int nxt = grp + gridDim.x;
-        if (nxt < groups) {
-            issue(nxt, buf ^ 1);
-            asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // all but the next group's DMA
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        float* const rows_lds = sh_lds + buf * kPersistPieces * 256;
-        if (g < in.P) preprocess_backward_one(cam, in, g, g, bi, flags, out, rows_lds + ln * M3);
-        // the lanes' gradient rows are in LDS: write the group's rows back coalesced
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int rows = in.P - grp * 64 < 64 ? in.P - grp * 64 : 64;
-        const int nf = rows * M3;
-        float* const dst = out.sh_rest + (size_t)grp * 64 * M3;
-        for (int i = ln; i < nf / 4; i += 64)
-            reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(rows_lds)[i];
-        for (int i = (nf & ~3) + ln; i < nf; i += 64) dst[i] = rows_lds[i];
-    }
-}
-
 }  // namespace
-
-#ifndef GSR_B2_PERSIST
-#define GSR_B2_PERSIST 0
-#endif
 
 int launch_gather_grad2d(const uint32_t* offsets, const float* partial, const float4* rec, int W, int H,
                          long long cap, int P, const uint4* rrect, float* grad2d, hipStream_t s) {
@@ -614,13 +556,6 @@ int launch_preprocess_backward(const gsr_camera& cam, const GaussIn& in, int g0,
     const int n = g1 - g0;
     if (n <= 0) return 0;
     const size_t lds = (in.sh_rest && !in.colors) ? sizeof(float) * 256 * 3 * in.M_rest : 0;
-    if (GSR_B2_PERSIST && g0 == 0 && in.sh_rest && !in.colors && in.M_rest * 3 <= 48 &&
-        ((reinterpret_cast<uintptr_t>(in.sh_rest) | reinterpret_cast<uintptr_t>(out.sh_rest)) & 15) == 0) {
-        const int groups = div_up(n, 64), waves = 256 * 6;
-        hipLaunchKernelGGL(preprocess_backward_persist_kernel, dim3(groups < waves ? groups : waves), dim3(64),
-                           2 * kPersistPieces * 1024, s, cam, in, depth_key, flags, grad2d, out);
-        return (int)hipGetLastError();
-    }
     const CamArg<1> c1{{cam}};
     hipLaunchKernelGGL((preprocess_backward_kernel<1, false>), dim3(div_up(n, 256)), dim3(256), lds, s, c1, in, g0,
                        n, depth_key, flags, grad2d, out, GradOut{}, BandSum{});
