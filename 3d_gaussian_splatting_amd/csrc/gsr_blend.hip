@@ -169,9 +169,7 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
                                                                 float* __restrict__ final_T,
                                                                 float* __restrict__ accum,
                                                                 uint32_t* __restrict__ term,
-                                                                float4* __restrict__ ck,
-                                                                const uint4* __restrict__ rect,
-                                                                float4* __restrict__ lay) {
+                                                                float4* __restrict__ ck) {
     constexpr int PPL = kPPL / NW;
     constexpr int BATCH = 64 * NW;
     constexpr int kCW = NW > 2 ? kBandChunkWork : kChunkWork;
@@ -234,21 +232,7 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
             srec[3 * tid + 0] = r0;
             srec[3 * tid + 1] = r1;
             srec[3 * tid + 2] = r2;
-            const uint32_t sm4 = stripe_mask(r0, r1, r2, bx0, by0);
-            smk[tid] = sm4;
-#if GSR_B1_LAYOUT
-            {  // B1's copy of this entry: record, emission index, stripe mask (64 B, coalesced)
-                const uint4 rr = rect[g];
-                const int minx = rr.x & 0xFFFF, miny = rr.x >> 16, maxx = rr.y & 0xFFFF;
-                const int y0 = miny > geo.ty0 ? miny : geo.ty0;
-                const uint32_t jl = rr.z + (uint32_t)((ty - y0) * (maxx - minx) + (tx - minx));
-                float4* dst = lay + 4 * ((size_t)range.x + base + tid);
-                dst[0] = r0;
-                dst[1] = r1;
-                dst[2] = r2;
-                dst[3] = make_float4(__uint_as_float(jl), __uint_as_float(sm4), 0.f, 0.f);
-            }
-#endif
+            smk[tid] = stripe_mask(r0, r1, r2, bx0, by0);
         } else {
             smk[tid] = 0u;
         }
@@ -456,8 +440,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                                                             float* __restrict__ p1,
                                                             uint8_t* __restrict__ fl,
                                                             const uint32_t* __restrict__ term,
-                                                            const float4* __restrict__ ck,
-                                                            const float4* __restrict__ lay) {
+                                                            const float4* __restrict__ ck) {
     // One block of LDS with srec first: the record fields then sit within the immediate offsets
     // of the record reads (8-bit dword offsets of ds_read2), so a record costs no address add.
     __shared__ struct {
@@ -491,14 +474,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
     if (start_u >= (uint32_t)n_all || start_u >= tend) return;
     const int start = (int)start_u;
     const uint32_t next = chunk + 1 < kMaxChunks ? table[chunk + 1] : 0xFFFFFFFFu;
-#if GSR_B1_LAYOUT
-    // F6 laid out the entries it loaded, every one before its termination index: past tend no
-    // pixel is live, and the layout holds nothing
-    const int n_lim = n_all < (int)tend ? n_all : (int)tend;
-#else
-    const int n_lim = n_all;
-#endif
-    const int n = next < (uint32_t)n_lim ? (int)next : n_lim;
+    const int n = next < (uint32_t)n_all ? (int)next : n_all;
     const int tx = tile % geo.grid_x, ty = tile / geo.grid_x;
     // lane = 4 col + row: a quad holds one column's 4 rows of a stripe, so it shares dx and
     // the record's moments reduce over the quad before dx is applied (F6 lays a stripe out
@@ -556,20 +532,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
         // which starts from a dead checkpoint) contributes nothing; its entries stay unflagged.
         if (live == 0) break;
         uint32_t jl = 0, smask = 0;
-#if GSR_B1_LAYOUT
-        if (lane < cnt) {  // F6's copy: one coalesced 64-B read, no gid -> rect / record chain
-            const float4* src = lay + 4 * ((size_t)range.x + base + lane);
-            const float4 r0 = src[0], r1 = src[1], r2 = src[2], r3 = src[3];
-            jl = __float_as_uint(r3.x);
-            srec[3 * lane + 0] = r0;
-            srec[3 * lane + 1] = r1;
-            srec[3 * lane + 2] = r2;
-            smask = __float_as_uint(r3.y);
-        }
-        sjl[lane] = jl;
-        __syncthreads();
-        uint64_t todo = __ballot((smask & live) != 0u);
-#else
         if (lane < cnt) {
             const uint32_t g = sorted_gid[range.x + base + lane];
             const uint4 rr = rect[g];  // rect + inst_start in one 16-B load
@@ -588,7 +550,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
         sjl[lane] = jl;
         __syncthreads();
         uint64_t todo = __ballot((smask & live) != 0u);
-#endif
         int visited = 0, parked = 0;
         uint32_t kpack = 0;  // batch slots of the parked records, 6 bits each
         // one visited record (batch slot k): its stripes, then its moments parked / flushed;
@@ -701,7 +662,7 @@ static BlendGeom make_geo(const gsr_camera& cam, const float bg[3], int ty0, int
 int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
                          const uint2* ranges, const uint32_t* sorted_gid, const float4* rec,
                          float* out_color, float* final_T, float* accum, uint32_t* term, float4* ck, long long cap,
-                         hipStream_t s, int vgy, int vh, const uint4* rect, float4* lay) {
+                         hipStream_t s, int vgy, int vh) {
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1, cap, vgy, vh);
     if (geo.nwg <= 0) return 0;
     // the variant (and with it the B1 chunk work) follows the tiles of ONE image: views mode then
@@ -709,10 +670,10 @@ int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int 
     const long long sel = vgy > 0 ? (long long)geo.vgy * geo.grid_x : geo.nwg;
     if (sel >= kF6BandTiles)
         hipLaunchKernelGGL(blend_forward_kernel<kF6FullWaves>, dim3(geo.nwg), dim3(64 * kF6FullWaves), 0, s, geo,
-                           ranges, sorted_gid, rec, out_color, final_T, accum, term, ck, rect, lay);
+                           ranges, sorted_gid, rec, out_color, final_T, accum, term, ck);
     else
         hipLaunchKernelGGL(blend_forward_kernel<kF6BandWaves>, dim3(geo.nwg), dim3(64 * kF6BandWaves), 0, s, geo,
-                           ranges, sorted_gid, rec, out_color, final_T, accum, term, ck, rect, lay);
+                           ranges, sorted_gid, rec, out_color, final_T, accum, term, ck);
     return (int)hipGetLastError();
 }
 
@@ -720,8 +681,7 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
                           const uint2* ranges, const uint32_t* sorted_gid, const uint4* rect,
                           const float4* rec, const float* final_T,
                           const float* accum, const float* dL_dpix, float* partial, long long cap,
-                          const uint32_t* term, const float4* ck, hipStream_t s, int vgy, int vh,
-                          const float4* lay) {
+                          const uint32_t* term, const float4* ck, hipStream_t s, int vgy, int vh) {
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1, cap, vgy, vh);
     if (geo.nwg <= 0) return 0;
     const PartLayout pl(cap);
@@ -729,8 +689,7 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
     const int blocks = 8 * (geo.nwg / 8 + 1) * kMaxChunks;
     hipLaunchKernelGGL(blend_backward_kernel, dim3(blocks), dim3(64), 0, s, geo, ranges, sorted_gid, rect, rec,
                        final_T, accum, dL_dpix, reinterpret_cast<float*>(base + pl.p8),
-                       reinterpret_cast<float*>(base + pl.p1), reinterpret_cast<uint8_t*>(base + pl.fl), term, ck,
-                       lay);
+                       reinterpret_cast<float*>(base + pl.p1), reinterpret_cast<uint8_t*>(base + pl.fl), term, ck);
     return (int)hipGetLastError();
 }
 

@@ -148,11 +148,8 @@ __host__ __device__ inline size_t ck_slot_of(bool fixed, uint32_t start, int til
 // Binning for up to `cap` instances (the exact K, or a caller-given bound) of an image of
 // `tiles` tiles.  The tile-key sort ping-pongs (kA, vA) <-> (kB, vB); F3 emits into (kA, vA).
 // Then the checkpoint slots: ck_slots x 256 float4, and one live byte per (slot, 16x4 stripe).
-#ifndef GSR_B1_LAYOUT
-#define GSR_B1_LAYOUT 0
-#endif
 struct BinLayout {
-    size_t kA, vA, kB, vB, hist, ck, ckm, lay = 0, total, ck_slots;
+    size_t kA, vA, kB, vB, hist, ck, ckm, total, ck_slots;
     BinLayout(long long cap, long long tiles) {
         size_t o = 0, n = (size_t)(cap > 0 ? cap : 1);
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
@@ -164,9 +161,6 @@ struct BinLayout {
         ck_slots = ck_pool_slots(cap, tiles);
         ck = take(ck_slots * 256 * 16);
         ckm = take(ck_slots * 4);
-        // GSR_B1_LAYOUT: F6 lays out each loaded list entry for B1 (record, emission index,
-        // stripe mask: 64 B) at its list position
-        if (GSR_B1_LAYOUT) lay = take(64 * n);
         total = o;
     }
 };
