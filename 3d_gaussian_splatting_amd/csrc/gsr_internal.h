@@ -28,13 +28,11 @@ constexpr int kFusedScanMax = 1 << 19;      // Gaussian counts up to this scan +
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 inline int div_up(long long a, long long b) { return (int)((a + b - 1) / b); }
 inline int sort_blocks(long long n) { return n > 0 ? div_up(n, kSortTile) : 0; }
-// multi-GPU splat packing: 256 threads x 4 rounds = 1024 Gaussians per block, so a 1/8 shard
-// (~600k at 5M) still launches ~600 blocks (at the sort's 4096 per block it left 3/4 of the
-// SIMDs idle)
-#ifndef GSR_PACK_ITEMS
-#define GSR_PACK_ITEMS 4
-#endif
-constexpr int kPackItems = GSR_PACK_ITEMS;
+// multi-GPU splat packing: 256 threads x 1 round = 256 Gaussians per block (a 1/8 shard of 1M
+// launches ~490 blocks).  Measured at 1M / 1080p, N = 8 (slowest rank, scripts/band_ab.sh):
+// 1 round 0.386-0.388 ms, 2 rounds 0.398-0.404, 4 rounds 0.409-0.439, and a one-launch pack with
+// a decoupled look-back 0.403-0.406 (slower still on whole-image shards: its look-back chain)
+constexpr int kPackItems = 1;
 constexpr int kPackTile = kSortBlock * kPackItems;
 inline int pack_blocks(long long n) { return n > 0 ? div_up(n, kPackTile) : 0; }
 // reduce-then-scan radix-sort scratch (u32 words): 256 digit columns of (blocks + 1) counts
@@ -230,11 +228,7 @@ struct ShardLayout {
         const size_t n = (size_t)(P > 0 ? P : 1);
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
         slot_of = take(4 * n * (size_t)nbands);
-        // the three-kernel pack's per-block counts, or the fused pack's per-(band, 256-block)
-        // look-back words + ticket
-        const size_t words = ((size_t)pack_blocks(n) + 1) * (size_t)nbands;
-        const size_t fused = (size_t)div_up((long long)n, 256) * (size_t)nbands + 1;
-        partials = take(4 * (words > fused ? words : fused));
+        partials = take(4 * ((size_t)pack_blocks(n) + 1) * (size_t)nbands);
         total = o;
     }
 };

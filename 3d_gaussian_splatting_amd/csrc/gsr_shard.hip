@@ -186,116 +186,6 @@ __global__ __launch_bounds__(kB) void pack_scatter_kernel(const uint32_t* __rest
     }
 }
 
-// ---- the same pack in ONE launch (steady-state steps: no row histogram) ----
-// Block b (in launch order, atomic ticket) owns Gaussians [256 b, 256 b + 256).  Per band: the
-// waves' splat counts (ballot), the block's offset among all earlier blocks by a decoupled
-// look-back on per-(band, block) flag|count words (wave w follows bands w, w + 4, ...: the
-// bands' chains run in parallel), then every lane writes its splats straight from the loads it
-// already holds.  The slots are the three-kernel pack's (same shard-order compaction), and the
-// last block writes the send headers.  Replaces pack_count + pack_scan + pack_scatter: one
-// launch, one pass over tiles / rect / records.
-constexpr uint32_t kAggF = 1u << 30, kIncF = 2u << 30, kCntF = kAggF - 1u;
-
-__global__ __launch_bounds__(256) void pack_fused_kernel(const uint32_t* __restrict__ tiles,
-                                                         const uint4* __restrict__ rect,
-                                                         const uint32_t* __restrict__ depth_key,
-                                                         const float4* __restrict__ rec, int P, BandRows br, int nblk,
-                                                         uint32_t* __restrict__ status, uint32_t* __restrict__ ticket,
-                                                         char* __restrict__ send, size_t block_bytes, int pair_cap,
-                                                         uint32_t* __restrict__ slot_of) {
-    __shared__ uint32_t cnt[kWaves][kMaxBands];
-    __shared__ uint32_t s_excl[kMaxBands];
-    __shared__ int s_b;
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    if (tid == 0) s_b = (int)atomicAdd(ticket, 1u);
-    __syncthreads();
-    const int b = s_b;
-    const int g = b * 256 + tid;
-    int b_lo = kMaxBands, b_hi = -1;
-    uint4 rr = make_uint4(0u, 0u, 0u, 0u);
-    if (g < P && tiles[g] != 0u) {
-        rr = rect[g];
-        band_span(br, rr.x >> 16, rr.y >> 16, b_lo, b_hi);
-    }
-    // the record loads fly while the block counts and looks back
-    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
-    uint32_t dk = 0u;
-    if (b_lo <= b_hi) {
-        r0 = rec[3 * (size_t)g];
-        r1 = rec[3 * (size_t)g + 1];
-        r2 = rec[3 * (size_t)g + 2];
-        dk = depth_key[g];
-    }
-    for (int bb = 0; bb < br.n; ++bb) {
-        const uint64_t m = __ballot(bb >= b_lo && bb <= b_hi);
-        if (lane == 0) cnt[w][bb] = (uint32_t)__popcll(m);
-    }
-    __syncthreads();
-    for (int bb = w; bb < br.n; bb += kWaves) {  // wave-uniform
-        uint32_t total = 0;
-#pragma unroll
-        for (int k = 0; k < kWaves; ++k) total += cnt[k][bb];
-        uint32_t* st = status + (size_t)bb * nblk;
-        uint32_t excl = 0;
-        if (b == 0) {
-            if (lane == 0) __hip_atomic_store(st, kIncF | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            if (lane == 0) __hip_atomic_store(st + b, kAggF | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int pos = b - 1;
-            uint32_t spins = 0;
-            while (true) {
-                const int idx = pos - lane;
-                uint32_t v = kIncF;  // before block 0: an inclusive zero
-                if (idx >= 0) v = __hip_atomic_load(st + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                while (__ballot((v & ~kCntF) == 0u)) {  // some predecessor not published yet
-                    if (++spins > (1u << 24)) break;    // never expected; bounded so a bug cannot hang
-                    __builtin_amdgcn_s_sleep(1);
-                    if (idx >= 0 && (v & ~kCntF) == 0u)
-                        v = __hip_atomic_load(st + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                const uint64_t inc = __ballot((v & kIncF) != 0u);
-                const int k = inc ? __builtin_ctzll(inc) : 64;  // nearest inclusive predecessor
-                uint32_t c = lane <= k ? (v & kCntF) : 0u;
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-                excl += c;
-                if (inc || spins > (1u << 24)) break;
-                pos -= 64;
-            }
-            if (lane == 0) __hip_atomic_store(st + b, kIncF | (excl + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (lane == 0) {
-            s_excl[bb] = excl;
-            if (b == nblk - 1) {  // the last block: the band's true splat count (may exceed pair_cap)
-                uint32_t* hdr = reinterpret_cast<uint32_t*>(send + (size_t)bb * block_bytes);
-                hdr[0] = excl + total;
-                hdr[1] = 0u;
-                hdr[2] = 0u;
-                hdr[3] = 0u;
-            }
-        }
-    }
-    __syncthreads();
-    const uint64_t lt = lanemask_lt();
-    for (int bb = 0; bb < br.n; ++bb) {
-        const bool in = bb >= b_lo && bb <= b_hi;
-        const uint64_t m = __ballot(in);
-        if (in) {
-            uint32_t slot = s_excl[bb] + (uint32_t)__popcll(m & lt);
-            for (int k = 0; k < w; ++k) slot += cnt[k][bb];
-            slot_of[(size_t)bb * P + g] = slot;
-            if (slot < (uint32_t)pair_cap) {
-                float4* dst = reinterpret_cast<float4*>(send + (size_t)bb * block_bytes + kSplatBytes +
-                                                        (size_t)slot * kSplatBytes);
-                dst[0] = r0;
-                dst[1] = r1;
-                dst[2] = r2;
-                dst[3] = make_float4(__uint_as_float(dk), __uint_as_float(rr.x), __uint_as_float(rr.y), 0.f);
-            }
-        }
-    }
-}
-
 // Band owner: local index i = src * pair_cap + slot.  Live slots get their record, depth key,
 // rect and the tile count of the rect clipped to the band's rows; empty slots get no tiles.
 __global__ __launch_bounds__(256) void unpack_kernel(const char* __restrict__ recv, size_t block_bytes, int nsrc,
@@ -336,18 +226,6 @@ int launch_pack_splats(const uint32_t* tiles, const uint4* rect, const uint32_t*
         for (int b = 0; b < br.n; ++b)
             if (hipError_t e = hipMemsetAsync(send + (size_t)b * bb, 0, kSplatBytes, s)) return (int)e;
         return 0;
-    }
-#ifndef GSR_PACK_FUSED
-#define GSR_PACK_FUSED 1
-#endif
-    if (GSR_PACK_FUSED && !row_hist) {  // steady state: one launch (the plan's pass keeps the histogram)
-        const int nb = div_up(P, 256);
-        uint32_t* status = partials;  // (nb + 1) * nbands words: per (band, block), then the ticket
-        uint32_t* ticket = partials + (size_t)nb * br.n;
-        if (hipError_t e = hipMemsetAsync(partials, 0, sizeof(uint32_t) * ((size_t)nb * br.n + 1), s)) return (int)e;
-        hipLaunchKernelGGL(pack_fused_kernel, dim3(nb), dim3(256), 0, s, tiles, rect, depth_key, rec, P, br, nb, status,
-                           ticket, send, bb, pair_cap, slot_of);
-        return (int)hipGetLastError();
     }
     const int nblk = pack_blocks(P);
     hipLaunchKernelGGL(pack_count_kernel, dim3(nblk), dim3(kB), 0, s, tiles, rect, P, br, partials, nblk, row_hist,

@@ -311,13 +311,14 @@ struct AdamArgs {
 __device__ __forceinline__ bool guard_tripped(const uint32_t* k, uint32_t cap) {
     return k != nullptr && *k > cap;  // written by an earlier kernel of the stream
 }
+// Streaming (non-temporal) loads / stores: parameters, gradients and moments are touched once per
+// step, so they should not displace the L2 / MALL lines the rasterizer reuses.  Measured in the
+// configs[4] loop (6M Gaussians, 1280x832, 4000 iterations): 89.8 vs 87.2 iters/s; two float4
+// columns per thread: 87.6 (profiles/r04_experiments/loop_ab_4k.txt).
 #ifndef GSR_ADAM_NT
-#define GSR_ADAM_NT 0  // streaming (non-temporal) loads / stores: the moments are touched once per step
+#define GSR_ADAM_NT 1
 #endif
-#ifndef GSR_ADAM_VEC
-#define GSR_ADAM_VEC 1  // float4s per thread and array
-#endif
-constexpr int kAdamBlock = 256, kAdamVec = GSR_ADAM_VEC, kAdamPerBlock = 4 * kAdamVec * kAdamBlock;
+constexpr int kAdamBlock = 256, kAdamVec = 1, kAdamPerBlock = 4 * kAdamVec * kAdamBlock;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 ld4(const float* p) {
 #if GSR_ADAM_NT
