@@ -214,6 +214,7 @@ struct Views {
     float *final_T, *accum;
     float4* ck;  // the checkpoint pool (binning buffer)
     uint32_t *kA, *vA, *kB, *vB, *hist;
+    uint8_t* mk;                         // GSR_B1_MASKS: F6's per-entry stripe masks
     uint32_t *sorted_tile, *sorted_gid;  // where the tile sort's result lands
     uint32_t *free_k, *free_v;           // the other ping-pong pair (scratch after the sort)
 };
@@ -257,6 +258,7 @@ Views views(const gsr_camera* cam, long long n, const gsr_buffers* b) {
         v.kB = at<uint32_t>(b->binning, bl.kB);
         v.vB = at<uint32_t>(b->binning, bl.vB);
         v.hist = at<uint32_t>(b->binning, bl.hist);
+        v.mk = GSR_B1_MASKS ? at<uint8_t>(b->binning, bl.mk) : nullptr;
         const int tiles = div_up(cam->width, kTile) * div_up(cam->height, kTile);
         const bool odd = (tile_passes(tiles) & 1) != 0;  // the sort ends in (kB, vB) after odd passes
         v.sorted_tile = odd ? v.kB : v.kA;
@@ -369,7 +371,7 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
     }
     GSR_STAGE(GSR_STAGE_BLEND_FWD, launch_blend_forward(*cam, j.rs->bg, j.ty0, j.ty1, v.ranges, v.sorted_gid, v.rec,
                                                         j.out_color, v.final_T, v.accum, v.term, v.ck, cap, stream,
-                                                        j.vgy, j.vh),
+                                                        j.vgy, j.vh, v.mk),
               "blend forward");
     return 0;
 }
@@ -424,7 +426,7 @@ int blend_backward(const gsr_camera* cam, const gsr_raster_settings* rs, const g
     GSR_STAGE(GSR_STAGE_MISC, launch_clear_flags(partial, cap, stream), "clear partial flags");
     GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.rect, v.rec,
                                                          v.final_T, v.accum, dL_dpix, partial, cap, v.term, v.ck,
-                                                         stream, vgy, vh),
+                                                         stream, vgy, vh, v.mk),
               "blend backward");
     GSR_STAGE(GSR_STAGE_GATHER, launch_gather_grad2d(v.offsets, partial, v.rec, cam->width, vgy > 0 ? vh : cam->height,
                                                      cap, (int)n,

@@ -169,7 +169,8 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
                                                                 float* __restrict__ final_T,
                                                                 float* __restrict__ accum,
                                                                 uint32_t* __restrict__ term,
-                                                                float4* __restrict__ ck) {
+                                                                float4* __restrict__ ck,
+                                                                uint8_t* __restrict__ mk) {
     constexpr int PPL = kPPL / NW;
     constexpr int BATCH = 64 * NW;
     constexpr int kCW = NW > 2 ? kBandChunkWork : kChunkWork;
@@ -233,6 +234,9 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
             srec[3 * tid + 1] = r1;
             srec[3 * tid + 2] = r2;
             smk[tid] = stripe_mask(r0, r1, r2, bx0, by0);
+#if GSR_B1_MASKS
+            mk[range.x + base + tid] = (uint8_t)smk[tid];  // B1's visit filter
+#endif
         } else {
             smk[tid] = 0u;
         }
@@ -440,13 +444,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                                                             float* __restrict__ p1,
                                                             uint8_t* __restrict__ fl,
                                                             const uint32_t* __restrict__ term,
-                                                            const float4* __restrict__ ck) {
+                                                            const float4* __restrict__ ck,
+                                                            const uint8_t* __restrict__ mk) {
     // One block of LDS with srec first: the record fields then sit within the immediate offsets
     // of the record reads (8-bit dword offsets of ds_read2), so a record costs no address add.
     __shared__ struct {
         float4 srec[64 * 3];
         uint32_t sjl[64];                  // the batch's emission indices, by batch slot
         float qpark[kPark * kParkSlot];    // [slot][quad][9 of 12]
+#if GSR_B1_MASKS
+        uint32_t sidx[64];                 // the batch's entries (list offsets), in list order
+        uint32_t smv[64];                  // and their stripe masks
+#endif
     } lds;
     float4* const srec = lds.srec;
     uint32_t* const sjl = lds.sjl;
@@ -523,6 +532,72 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
             }
         }
     }
+#if GSR_B1_MASKS
+    // F6 wrote the stripe mask of every entry it loaded, all before its termination index tend;
+    // past tend no pixel is live
+    const int n_lim = n < (int)tend ? n : (int)tend;
+    for (int base = start; base < n_lim;) {
+        uint32_t live = 0;
+#pragma unroll
+        for (int p = 0; p < kPPL; ++p) live |= __any(T[p] > 0.0f) ? (1u << p) : 0u;
+        if (live == 0) break;
+        // the batch: up to 64 entries with a live stripe among the next 256 (four mask bytes
+        // per lane from one aligned word), in list order; the next batch starts after the last
+        // one taken, or after the window
+        const uint32_t a0 = (range.x + (uint32_t)base) & ~3u;  // word-aligned window start
+        const uint32_t w4 = *reinterpret_cast<const uint32_t*>(mk + a0 + 4 * lane);
+        uint32_t vis = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int e = (int)(a0 + 4 * lane + i - range.x);  // list offset of byte i
+            const uint32_t m = (w4 >> (8 * i)) & 0xFu;
+            if (e >= base && e < n_lim && (m & live)) vis |= 1u << i;
+        }
+        const uint32_t c = (uint32_t)__popc(vis);
+        uint32_t incl = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        const uint32_t excl = incl - c;
+        const uint32_t total = (uint32_t)__shfl(incl, 63, 64);
+        const int cnt = total < 64u ? (int)total : 64;
+        uint32_t pos = excl;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if ((vis >> i) & 1u) {
+                if (pos < 64u) {
+                    lds.sidx[pos] = a0 + 4 * lane + i - range.x;
+                    lds.smv[pos] = (w4 >> (8 * i)) & 0xFu;
+                }
+                ++pos;
+            }
+        }
+        __syncthreads();
+        // next window: after the 64th taken entry when the window held more, else past it
+        base = total > 64u ? (int)lds.sidx[63] + 1 : (int)(a0 + 256 - range.x);
+        if (cnt == 0) {
+            __syncthreads();
+            continue;
+        }
+        uint32_t jl = 0, smask = 0;
+        if (lane < cnt) {
+            const uint32_t g = sorted_gid[range.x + lds.sidx[lane]];
+            const uint4 rr = rect[g];
+            const int minx = rr.x & 0xFFFF, miny = rr.x >> 16, maxx = rr.y & 0xFFFF;
+            const int y0 = miny > geo.ty0 ? miny : geo.ty0;
+            jl = rr.z + (uint32_t)((ty - y0) * (maxx - minx) + (tx - minx));
+            const float4* r = rec + 3 * (size_t)g;
+            srec[3 * lane + 0] = r[0];
+            srec[3 * lane + 1] = r[1];
+            srec[3 * lane + 2] = r[2];
+            smask = lds.smv[lane];
+        }
+        sjl[lane] = jl;
+        __syncthreads();
+        uint64_t todo = __ballot(lane < cnt);
+#else
     for (int base = start; base < n; base += 64) {
         const int cnt = (n - base) < 64 ? (n - base) : 64;
         uint32_t live = 0;
@@ -550,6 +625,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
         sjl[lane] = jl;
         __syncthreads();
         uint64_t todo = __ballot((smask & live) != 0u);
+#endif
         int visited = 0, parked = 0;
         uint32_t kpack = 0;  // batch slots of the parked records, 6 bits each
         // one visited record (batch slot k): its stripes, then its moments parked / flushed;
@@ -662,7 +738,7 @@ static BlendGeom make_geo(const gsr_camera& cam, const float bg[3], int ty0, int
 int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
                          const uint2* ranges, const uint32_t* sorted_gid, const float4* rec,
                          float* out_color, float* final_T, float* accum, uint32_t* term, float4* ck, long long cap,
-                         hipStream_t s, int vgy, int vh) {
+                         hipStream_t s, int vgy, int vh, uint8_t* mk) {
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1, cap, vgy, vh);
     if (geo.nwg <= 0) return 0;
     // the variant (and with it the B1 chunk work) follows the tiles of ONE image: views mode then
@@ -670,10 +746,10 @@ int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int 
     const long long sel = vgy > 0 ? (long long)geo.vgy * geo.grid_x : geo.nwg;
     if (sel >= kF6BandTiles)
         hipLaunchKernelGGL(blend_forward_kernel<kF6FullWaves>, dim3(geo.nwg), dim3(64 * kF6FullWaves), 0, s, geo,
-                           ranges, sorted_gid, rec, out_color, final_T, accum, term, ck);
+                           ranges, sorted_gid, rec, out_color, final_T, accum, term, ck, mk);
     else
         hipLaunchKernelGGL(blend_forward_kernel<kF6BandWaves>, dim3(geo.nwg), dim3(64 * kF6BandWaves), 0, s, geo,
-                           ranges, sorted_gid, rec, out_color, final_T, accum, term, ck);
+                           ranges, sorted_gid, rec, out_color, final_T, accum, term, ck, mk);
     return (int)hipGetLastError();
 }
 
@@ -681,7 +757,8 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
                           const uint2* ranges, const uint32_t* sorted_gid, const uint4* rect,
                           const float4* rec, const float* final_T,
                           const float* accum, const float* dL_dpix, float* partial, long long cap,
-                          const uint32_t* term, const float4* ck, hipStream_t s, int vgy, int vh) {
+                          const uint32_t* term, const float4* ck, hipStream_t s, int vgy, int vh,
+                          const uint8_t* mk) {
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1, cap, vgy, vh);
     if (geo.nwg <= 0) return 0;
     const PartLayout pl(cap);
@@ -689,7 +766,8 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
     const int blocks = 8 * (geo.nwg / 8 + 1) * kMaxChunks;
     hipLaunchKernelGGL(blend_backward_kernel, dim3(blocks), dim3(64), 0, s, geo, ranges, sorted_gid, rect, rec,
                        final_T, accum, dL_dpix, reinterpret_cast<float*>(base + pl.p8),
-                       reinterpret_cast<float*>(base + pl.p1), reinterpret_cast<uint8_t*>(base + pl.fl), term, ck);
+                       reinterpret_cast<float*>(base + pl.p1), reinterpret_cast<uint8_t*>(base + pl.fl), term, ck,
+                       mk);
     return (int)hipGetLastError();
 }
 

@@ -90,7 +90,7 @@ int launch_finalize(const uint32_t* sorted_tile, long long cap, const uint32_t* 
 int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
                          const uint2* ranges, const uint32_t* sorted_gid, const float4* rec,
                          float* out_color, float* final_T, float* accum, uint32_t* term, float4* ck, long long cap,
-                         hipStream_t s, int vgy = 0, int vh = 0);
+                         hipStream_t s, int vgy = 0, int vh = 0, uint8_t* mk = nullptr);
 
 // F6 writes term[t] (see kMaxChunks) and the B1 chunk checkpoints `ck` (ImgLayout.ck).
 // B1: per-tile front-to-back gradients -> per-instance partial entry j (PartLayout(cap)), where
@@ -103,7 +103,8 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
                           const uint2* ranges, const uint32_t* sorted_gid, const uint4* rect,
                           const float4* rec, const float* final_T,
                           const float* accum, const float* dL_dpix, float* partial, long long cap,
-                          const uint32_t* term, const float4* ck, hipStream_t s, int vgy = 0, int vh = 0);
+                          const uint32_t* term, const float4* ck, hipStream_t s, int vgy = 0, int vh = 0,
+                          const uint8_t* mk = nullptr);
 // (vgy, vh: views mode -- bands of vgy tile rows per view, vh valid pixel rows each; 0 = one image)
 
 // record layout constants shared by preprocess and the blend kernels
