@@ -214,7 +214,7 @@ struct Views {
     float *final_T, *accum;
     float4* ck;  // the checkpoint pool (binning buffer)
     uint32_t *kA, *vA, *kB, *vB, *hist;
-    uint8_t* mk;                         // GSR_B1_MASKS: F6's per-entry stripe masks
+    uint8_t* mk;                         // F6's per-entry stripe masks (B1's visit filter)
     uint32_t *sorted_tile, *sorted_gid;  // where the tile sort's result lands
     uint32_t *free_k, *free_v;           // the other ping-pong pair (scratch after the sort)
 };
@@ -258,7 +258,7 @@ Views views(const gsr_camera* cam, long long n, const gsr_buffers* b) {
         v.kB = at<uint32_t>(b->binning, bl.kB);
         v.vB = at<uint32_t>(b->binning, bl.vB);
         v.hist = at<uint32_t>(b->binning, bl.hist);
-        v.mk = GSR_B1_MASKS ? at<uint8_t>(b->binning, bl.mk) : nullptr;
+        v.mk = at<uint8_t>(b->binning, bl.mk);
         const int tiles = div_up(cam->width, kTile) * div_up(cam->height, kTile);
         const bool odd = (tile_passes(tiles) & 1) != 0;  // the sort ends in (kB, vB) after odd passes
         v.sorted_tile = odd ? v.kB : v.kA;

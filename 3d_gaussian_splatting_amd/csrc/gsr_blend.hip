@@ -234,9 +234,7 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
             srec[3 * tid + 1] = r1;
             srec[3 * tid + 2] = r2;
             smk[tid] = stripe_mask(r0, r1, r2, bx0, by0);
-#if GSR_B1_MASKS
             mk[range.x + base + tid] = (uint8_t)smk[tid];  // B1's visit filter
-#endif
         } else {
             smk[tid] = 0u;
         }
@@ -426,6 +424,10 @@ __device__ __forceinline__ void park_flush(const float* qpark, const uint32_t* s
 // B1 stores the raw tile sums (Sx, Sy, Sxx, Sxy, Syy, S0, colour x3); they are linear in the
 // gradients, so gather_grad2d converts them once per Gaussian after summing over tiles.
 //
+// Batches: F6 stores the stripe mask of every list entry it loads (one byte each, `mk`); B1 reads
+// 256 of them per step (one aligned word per lane), keeps the entries with a stripe still live
+// and takes up to 64 of them, in list order, as its batch -- records that cannot touch a live
+// stripe are never loaded (after an opacity reset most of a deep list is culled this way).
 // Grid: one 64-lane block per (tile, chunk slot); chunk c > 0 starts where F6's chunk table
 // says and resumes from F6's checkpoint, and slots the tile has no chunk for exit at once.  Each
 // XCD (blocks b with equal b % 8) takes a contiguous tile range as in xcd_tile, visited
@@ -452,10 +454,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
         float4 srec[64 * 3];
         uint32_t sjl[64];                  // the batch's emission indices, by batch slot
         float qpark[kPark * kParkSlot];    // [slot][quad][9 of 12]
-#if GSR_B1_MASKS
         uint32_t sidx[64];                 // the batch's entries (list offsets), in list order
         uint32_t smv[64];                  // and their stripe masks
-#endif
     } lds;
     float4* const srec = lds.srec;
     uint32_t* const sjl = lds.sjl;
@@ -532,7 +532,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
             }
         }
     }
-#if GSR_B1_MASKS
     // F6 wrote the stripe mask of every entry it loaded, all before its termination index tend;
     // past tend no pixel is live
     const int n_lim = n < (int)tend ? n : (int)tend;
@@ -597,35 +596,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
         sjl[lane] = jl;
         __syncthreads();
         uint64_t todo = __ballot(lane < cnt);
-#else
-    for (int base = start; base < n; base += 64) {
-        const int cnt = (n - base) < 64 ? (n - base) : 64;
-        uint32_t live = 0;
-#pragma unroll
-        for (int p = 0; p < kPPL; ++p) live |= __any(T[p] > 0.0f) ? (1u << p) : 0u;
-        // Every pixel of the tile has terminated: the rest of this chunk (and every later chunk,
-        // which starts from a dead checkpoint) contributes nothing; its entries stay unflagged.
-        if (live == 0) break;
-        uint32_t jl = 0, smask = 0;
-        if (lane < cnt) {
-            const uint32_t g = sorted_gid[range.x + base + lane];
-            const uint4 rr = rect[g];  // rect + inst_start in one 16-B load
-            const int minx = rr.x & 0xFFFF, miny = rr.x >> 16, maxx = rr.y & 0xFFFF;
-            const int y0 = miny > geo.ty0 ? miny : geo.ty0;
-            jl = rr.z + (uint32_t)((ty - y0) * (maxx - minx) + (tx - minx));
-            if (live) {
-                const float4* r = rec + 3 * (size_t)g;
-                const float4 r0 = r[0], r1 = r[1], r2 = r[2];
-                srec[3 * lane + 0] = r0;
-                srec[3 * lane + 1] = r1;
-                srec[3 * lane + 2] = r2;
-                smask = stripe_mask(r0, r1, r2, bx0, by0);
-            }
-        }
-        sjl[lane] = jl;
-        __syncthreads();
-        uint64_t todo = __ballot((smask & live) != 0u);
-#endif
         int visited = 0, parked = 0;
         uint32_t kpack = 0;  // batch slots of the parked records, 6 bits each
         // one visited record (batch slot k): its stripes, then its moments parked / flushed;

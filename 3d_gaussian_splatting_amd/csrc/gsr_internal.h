@@ -146,9 +146,6 @@ __host__ __device__ inline size_t ck_slot_of(bool fixed, uint32_t start, int til
 // Binning for up to `cap` instances (the exact K, or a caller-given bound) of an image of
 // `tiles` tiles.  The tile-key sort ping-pongs (kA, vA) <-> (kB, vB); F3 emits into (kA, vA).
 // Then the checkpoint slots: ck_slots x 256 float4, and one live byte per (slot, 16x4 stripe).
-#ifndef GSR_B1_MASKS
-#define GSR_B1_MASKS 0
-#endif
 struct BinLayout {
     size_t kA, vA, kB, vB, hist, ck, ckm, mk = 0, total, ck_slots;
     BinLayout(long long cap, long long tiles) {
@@ -162,9 +159,9 @@ struct BinLayout {
         ck_slots = ck_pool_slots(cap, tiles);
         ck = take(ck_slots * 256 * 16);
         ckm = take(ck_slots * 4);
-        // GSR_B1_MASKS: F6's stripe mask of every list entry it loads (one byte each), from
-        // which B1 picks the entries it has to visit before loading any record
-        if (GSR_B1_MASKS) mk = take(n + 256);  // + a 256-entry window read past the end
+        // F6's stripe mask of every list entry it loads (one byte each), from which B1 picks the
+        // entries it has to visit before loading any record (+ B1's 256-entry window past the end)
+        mk = take(n + 256);
         total = o;
     }
 };
