@@ -18,7 +18,6 @@
 #include <vector>
 
 #include "gsr_kernels.h"
-#include "gsr_stripe.h"
 
 using namespace gsr;
 
@@ -160,8 +159,6 @@ int validate(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster_se
     if ((long long)div_up(cam->width, kTile) >= 65535 || (long long)div_up(cam->height, kTile) >= 65535)
         return fail(-1, "image too large");
     if (gs->P < 0) return fail(-1, "negative P");
-    if (gs->P >= (1 << (32 - kValShift))) return fail(-1, "P must be below 2^%d (list values hold gid << %d)",
-                                                       32 - kValShift, kValShift);
     if (gs->P == 0) return 0;
     if (!gs->means3D || !gs->opacities) return fail(-1, "means3D/opacities required");
     if (gs->sh_degree < 0 || gs->sh_degree > 3) return fail(-1, "sh_degree must be 0..3");
@@ -217,6 +214,7 @@ struct Views {
     float *final_T, *accum;
     float4* ck;  // the checkpoint pool (binning buffer)
     uint32_t *kA, *vA, *kB, *vB, *hist;
+    uint8_t* mk;                         // F6's per-entry stripe masks (B1's visit filter)
     uint32_t *sorted_tile, *sorted_gid;  // where the tile sort's result lands
     uint32_t *free_k, *free_v;           // the other ping-pong pair (scratch after the sort)
 };
@@ -260,6 +258,7 @@ Views views(const gsr_camera* cam, long long n, const gsr_buffers* b) {
         v.kB = at<uint32_t>(b->binning, bl.kB);
         v.vB = at<uint32_t>(b->binning, bl.vB);
         v.hist = at<uint32_t>(b->binning, bl.hist);
+        v.mk = at<uint8_t>(b->binning, bl.mk);
         const int tiles = div_up(cam->width, kTile) * div_up(cam->height, kTile);
         const bool odd = (tile_passes(tiles) & 1) != 0;  // the sort ends in (kB, vB) after odd passes
         v.sorted_tile = odd ? v.kB : v.kA;
@@ -348,12 +347,11 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
     const int tiles = j.gx * j.gy, ntiles = (j.ty1 - j.ty0) * j.gx;
     if (v.presort)
         GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate_ranked(v.rtiles, v.rrect, v.rect, (int)j.n, j.gx, j.ty0,
-                                                               v.lookback, v.offsets, v.kA, v.vA, cap, v.rec, j.vgy,
-                                                               stream),
+                                                               v.lookback, v.offsets, v.kA, v.vA, cap, stream),
                   "duplicate (rank order)");
     else
         GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate(v.tiles, v.rect, (int)j.n, j.gx, j.ty0, v.offsets, v.lookback,
-                                                        v.kA, v.vA, cap, v.K_dev, v.rec, j.vgy, stream),
+                                                        v.kA, v.vA, cap, v.K_dev, stream),
                   "duplicate");
     if (cap > 0) {
         int which = -1;
@@ -373,7 +371,7 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
     }
     GSR_STAGE(GSR_STAGE_BLEND_FWD, launch_blend_forward(*cam, j.rs->bg, j.ty0, j.ty1, v.ranges, v.sorted_gid, v.rec,
                                                         j.out_color, v.final_T, v.accum, v.term, v.ck, cap, stream,
-                                                        j.vgy, j.vh),
+                                                        j.vgy, j.vh, v.mk),
               "blend forward");
     return 0;
 }
@@ -428,7 +426,7 @@ int blend_backward(const gsr_camera* cam, const gsr_raster_settings* rs, const g
     GSR_STAGE(GSR_STAGE_MISC, launch_clear_flags(partial, cap, stream), "clear partial flags");
     GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.rect, v.rec,
                                                          v.final_T, v.accum, dL_dpix, partial, cap, v.term, v.ck,
-                                                         stream, vgy, vh),
+                                                         stream, vgy, vh, v.mk),
               "blend backward");
     GSR_STAGE(GSR_STAGE_GATHER, launch_gather_grad2d(v.offsets, partial, v.rec, cam->width, vgy > 0 ? vh : cam->height,
                                                      cap, (int)n,
@@ -495,7 +493,7 @@ int views_camera(int32_t V, const gsr_camera* cams, const gsr_gaussians* gs, con
     const int gy = div_up(cams[0].height, kTile);
     if (rs->tile_y0 > 0 || rs->tile_y1 < gy) return fail(-1, "views: full-image views only");
     if ((long long)V * gy >= 65535) return fail(-1, "views: %d views of %d tile rows exceed the tile grid", V, gy);
-    if ((long long)V * gs->P >= (1LL << (32 - kValShift))) return fail(-1, "views: V * P must be below 2^%d", 32 - kValShift);
+    if ((long long)V * gs->P > INT32_MAX / 2) return fail(-1, "views: V * P too large");
     *tall = cams[0];
     tall->height = V * gy * kTile;
     return 0;
@@ -828,7 +826,7 @@ int gsr_band_forward(const gsr_camera* cam, const gsr_raster_settings* rs, int32
         return fail(-1, "band: null buffer / allocator");
     if (rs->max_rendered <= 0) return fail(-1, "band: max_rendered (the band's instance capacity) is required");
     const long long n = (long long)nsrc * pair_cap;
-    if (n >= (1LL << (32 - kValShift))) return fail(-1, "band: nsrc * pair_cap must be below 2^%d", 32 - kValShift);
+    if (n > INT32_MAX) return fail(-1, "band: nsrc * pair_cap too large");
     hipStream_t stream = (hipStream_t)stream_;
     const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
     FwdJob j{cam, rs, out_color, bufs};

@@ -37,11 +37,11 @@
 // emission order (gsr_preprocess_bwd.hip), so gradients are deterministic and no float atomics
 // are issued.
 #include "gsr_kernels.h"
-#include "gsr_stripe.h"
 
 namespace gsr {
 namespace {
 
+constexpr int kPPL = 4;  // pixels per lane
 
 __device__ inline int xcd_tile(int b, int nwg) {
     // bijective remap: the blocks one XCD receives (b % 8 equal) -> a contiguous tile range
@@ -82,6 +82,55 @@ struct BlendGeom {
     float bg0, bg1, bg2;
 };
 
+// Which of the tile's four 16x4 pixel stripes (slot p = rows 4p..4p+3) can hold a pixel
+// with alpha >= 1/255.  Two conservative tests, both on the record the loading lane holds:
+//  1. the padded footprint box (ext_x, ext_y) must overlap the stripe;
+//  2. the footprint ellipse itself must reach the stripe's pixel-centre rectangle: with the
+//     PD form Q(d) = -(a' dx^2 + b' dx dy + c' dy^2) (the exponent without log2 o), a pixel
+//     passes alpha >= 1/255 iff Q <= log2(255 o), so the stripe is needed iff the minimum of Q
+//     over the rectangle (0 if the mean is inside, else the minimum over its four edges,
+//     each a clamped 1-D quadratic) is within that bound -- padded by 2 % + 0.05 for float
+//     rounding.  Records whose form is not negative definite keep the box test only.
+// Exact culling: a skipped stripe has no pixel that the per-pixel test would accept, so no
+// output bit changes; the ellipse test removes ~22 % of the box test's stripe evaluations
+// and ~17 % of the visited records at 1M/1080p (scripts/cull_stats.py).
+// min over v in [v0, v1] of a u^2 + b u v + c v^2 (c > 0), given k = -b / (2c): the minimiser
+// k u clamped to the edge.  k comes from a hardware reciprocal (1 ulp), not an IEEE division
+// (~11 instructions each, 16 per record): a minimiser off by a few ulp raises q by c d^2, far
+// inside the 2 % + 0.05 pad, and any point of the edge bounds the minimum from above only by
+// that amount, so the test stays conservative.
+__device__ __forceinline__ float edge_min_q(float a, float b, float c, float k, float u, float v0, float v1) {
+    const float vs = fminf(fmaxf(k * u, v0), v1);
+    return fmaf(fmaf(c, vs, b * u), vs, a * u * u);
+}
+
+__device__ inline uint32_t stripe_mask(const float4 r0, const float4 r1, const float4 r2, float bx0, float by0) {
+    const float ex = r2.y, ey = r2.z;
+    if (!(ex >= 0.0f) || r0.x + ex < bx0 || r0.x - ex > bx0 + 15.0f) return 0u;
+    const float ylo = r0.y - ey, yhi = r0.y + ey;
+    // PD form coefficients (A dx^2 + B dx dy + C dy^2) and the log2-domain bound
+    const float A = -r0.z, B = -r0.w, C = -r1.x;
+    const bool pd = A > 0.0f && C > 0.0f && 4.0f * A * C - B * B > 0.0f;
+    const float bound = fmaf(fmaxf(r2.w + 7.99435343f, 0.0f), 1.02f, 0.05f);  // log2(255 o)
+    const float x0 = bx0 - r0.x, x1 = bx0 + 15.0f - r0.x;  // rect in mean-relative coords
+    const float kc = -B * __builtin_amdgcn_rcpf(2.0f * C), ka = -B * __builtin_amdgcn_rcpf(2.0f * A);
+    uint32_t m = 0;
+#pragma unroll
+    for (int p = 0; p < kPPL; ++p) {
+        const float s0 = by0 + 4.0f * p;
+        bool hit = yhi >= s0 && ylo <= s0 + 3.0f;
+        if (hit && pd) {
+            const float y0 = s0 - r0.y, y1 = s0 + 3.0f - r0.y;
+            const bool inside = x0 <= 0.0f && x1 >= 0.0f && y0 <= 0.0f && y1 >= 0.0f;
+            const float q = fminf(fminf(edge_min_q(A, B, C, kc, x0, y0, y1), edge_min_q(A, B, C, kc, x1, y0, y1)),
+                                  fminf(edge_min_q(C, B, A, ka, y0, x0, x1), edge_min_q(C, B, A, ka, y1, x0, x1)));
+            hit = inside || q <= bound;
+        }
+        m |= hit ? (1u << p) : 0u;
+    }
+    return m;
+}
+
 // alpha of one (pixel, record) pair, with the reference's two rejections folded into the
 // select: power > 0 (here: exponent above log2 o) and alpha < 1/255 give 0.
 __device__ __forceinline__ float pair_alpha(float e, float L, float& oG) {
@@ -120,7 +169,8 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
                                                                 float* __restrict__ final_T,
                                                                 float* __restrict__ accum,
                                                                 uint32_t* __restrict__ term,
-                                                                float4* __restrict__ ck) {
+                                                                float4* __restrict__ ck,
+                                                                uint8_t* __restrict__ mk) {
     constexpr int PPL = kPPL / NW;
     constexpr int BATCH = 64 * NW;
     constexpr int kCW = NW > 2 ? kBandChunkWork : kChunkWork;
@@ -134,6 +184,7 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
     const int px = tx * kTile + (lane & 15);
     const float pfx = (float)px;
     const int view = ty / geo.vgy, tyl = ty - view * geo.vgy;  // tile row inside its view's band
+    const float bx0 = (float)(tx * kTile), by0 = (float)(tyl * kTile);
     float pfy[PPL], T[PPL], C0[PPL], C1[PPL], C2[PPL];
 #pragma unroll
     for (int p = 0; p < PPL; ++p) {
@@ -175,20 +226,18 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
             tend = base;
             break;
         }
-        // the list value carries the entry's stripe mask (F3): an entry whose footprint reaches
-        // none of the tile's stripes is never loaded
-        uint32_t sm = 0u;
         if (base + tid < n) {
-            const uint32_t v = sorted_gid[range.x + base + tid];
-            sm = v & kValMask;
-            if (sm) {
-                const float4* r = rec + 3 * (size_t)(v >> kValShift);
-                srec[3 * tid + 0] = r[0];
-                srec[3 * tid + 1] = r[1];
-                srec[3 * tid + 2] = r[2];
-            }
+            const uint32_t g = sorted_gid[range.x + base + tid];
+            const float4* r = rec + 3 * (size_t)g;
+            const float4 r0 = r[0], r1 = r[1], r2 = r[2];
+            srec[3 * tid + 0] = r0;
+            srec[3 * tid + 1] = r1;
+            srec[3 * tid + 2] = r2;
+            smk[tid] = stripe_mask(r0, r1, r2, bx0, by0);
+            mk[range.x + base + tid] = (uint8_t)smk[tid];  // B1's visit filter
+        } else {
+            smk[tid] = 0u;
         }
-        smk[tid] = sm;
         __syncthreads();
         uint32_t tile_live = 0;
 #pragma unroll
@@ -375,8 +424,8 @@ __device__ __forceinline__ void park_flush(const float* qpark, const uint32_t* s
 // B1 stores the raw tile sums (Sx, Sy, Sxx, Sxy, Syy, S0, colour x3); they are linear in the
 // gradients, so gather_grad2d converts them once per Gaussian after summing over tiles.
 //
-// Batches: every list value carries its entry's stripe mask (F3, gsr_stripe.h); B1 reads 256
-// values per step (one aligned 16-B load per lane), keeps the entries with a stripe still live
+// Batches: F6 stores the stripe mask of every list entry it loads (one byte each, `mk`); B1 reads
+// 256 of them per step (one aligned word per lane), keeps the entries with a stripe still live
 // and takes up to 64 of them, in list order, as its batch -- records that cannot touch a live
 // stripe are never loaded (after an opacity reset most of a deep list is culled this way).
 // Grid: one 64-lane block per (tile, chunk slot); chunk c > 0 starts where F6's chunk table
@@ -397,15 +446,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
                                                             float* __restrict__ p1,
                                                             uint8_t* __restrict__ fl,
                                                             const uint32_t* __restrict__ term,
-                                                            const float4* __restrict__ ck) {
+                                                            const float4* __restrict__ ck,
+                                                            const uint8_t* __restrict__ mk) {
     // One block of LDS with srec first: the record fields then sit within the immediate offsets
     // of the record reads (8-bit dword offsets of ds_read2), so a record costs no address add.
     __shared__ struct {
         float4 srec[64 * 3];
         uint32_t sjl[64];                  // the batch's emission indices, by batch slot
         float qpark[kPark * kParkSlot];    // [slot][quad][9 of 12]
-        uint32_t sval[64];                 // the batch's list values (gid << 4 | mask), in list order
-        uint32_t last;                     // list offset of the batch's last entry
+        uint32_t sidx[64];                 // the batch's entries (list offsets), in list order
+        uint32_t smv[64];                  // and their stripe masks
     } lds;
     float4* const srec = lds.srec;
     uint32_t* const sjl = lds.sjl;
@@ -442,6 +492,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
     const int px = tx * kTile + col;
     const float pfx = (float)px;
     const int view = ty / geo.vgy, tyl = ty - view * geo.vgy;  // tile row inside its view's band
+    const float bx0 = (float)(tx * kTile), by0 = (float)(tyl * kTile);
     // F6's per-view planes (one image: view 0)
     const size_t npix = (size_t)geo.W * geo.vh;
     final_T += (size_t)view * npix;
@@ -481,24 +532,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
             }
         }
     }
-    // past F6's termination index tend no pixel is live
+    // F6 wrote the stripe mask of every entry it loaded, all before its termination index tend;
+    // past tend no pixel is live
     const int n_lim = n < (int)tend ? n : (int)tend;
     for (int base = start; base < n_lim;) {
         uint32_t live = 0;
 #pragma unroll
         for (int p = 0; p < kPPL; ++p) live |= __any(T[p] > 0.0f) ? (1u << p) : 0u;
         if (live == 0) break;
-        // the batch: up to 64 entries whose stripe mask (in the list value, F3) meets a live
-        // stripe, among the next 256 (four values per lane from one aligned 16-B load), in list
-        // order; the next batch starts after the last one taken, or after the window
-        const uint32_t a0 = (range.x + (uint32_t)base) & ~3u;  // 16-B aligned window start
-        const uint4 w4 = *reinterpret_cast<const uint4*>(sorted_gid + a0 + 4 * lane);
-        const uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
+        // the batch: up to 64 entries with a live stripe among the next 256 (four mask bytes
+        // per lane from one aligned word), in list order; the next batch starts after the last
+        // one taken, or after the window
+        const uint32_t a0 = (range.x + (uint32_t)base) & ~3u;  // word-aligned window start
+        const uint32_t w4 = *reinterpret_cast<const uint32_t*>(mk + a0 + 4 * lane);
         uint32_t vis = 0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int e = (int)(a0 + 4 * lane + i - range.x);  // list offset of value i
-            if (e >= base && e < n_lim && (wv[i] & kValMask & live)) vis |= 1u << i;
+            const int e = (int)(a0 + 4 * lane + i - range.x);  // list offset of byte i
+            const uint32_t m = (w4 >> (8 * i)) & 0xFu;
+            if (e >= base && e < n_lim && (m & live)) vis |= 1u << i;
         }
         const uint32_t c = (uint32_t)__popc(vis);
         uint32_t incl = c;
@@ -514,22 +566,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             if ((vis >> i) & 1u) {
-                if (pos < 64u) lds.sval[pos] = wv[i];
-                if (pos == 63u) lds.last = a0 + 4 * lane + i - range.x;
+                if (pos < 64u) {
+                    lds.sidx[pos] = a0 + 4 * lane + i - range.x;
+                    lds.smv[pos] = (w4 >> (8 * i)) & 0xFu;
+                }
                 ++pos;
             }
         }
         __syncthreads();
         // next window: after the 64th taken entry when the window held more, else past it
-        base = total > 64u ? (int)lds.last + 1 : (int)(a0 + 256 - range.x);
+        base = total > 64u ? (int)lds.sidx[63] + 1 : (int)(a0 + 256 - range.x);
         if (cnt == 0) {
             __syncthreads();
             continue;
         }
         uint32_t jl = 0, smask = 0;
         if (lane < cnt) {
-            const uint32_t v = lds.sval[lane];
-            const uint32_t g = v >> kValShift;
+            const uint32_t g = sorted_gid[range.x + lds.sidx[lane]];
             const uint4 rr = rect[g];
             const int minx = rr.x & 0xFFFF, miny = rr.x >> 16, maxx = rr.y & 0xFFFF;
             const int y0 = miny > geo.ty0 ? miny : geo.ty0;
@@ -538,7 +591,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
             srec[3 * lane + 0] = r[0];
             srec[3 * lane + 1] = r[1];
             srec[3 * lane + 2] = r[2];
-            smask = v & kValMask;
+            smask = lds.smv[lane];
         }
         sjl[lane] = jl;
         __syncthreads();
@@ -655,7 +708,7 @@ static BlendGeom make_geo(const gsr_camera& cam, const float bg[3], int ty0, int
 int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
                          const uint2* ranges, const uint32_t* sorted_gid, const float4* rec,
                          float* out_color, float* final_T, float* accum, uint32_t* term, float4* ck, long long cap,
-                         hipStream_t s, int vgy, int vh) {
+                         hipStream_t s, int vgy, int vh, uint8_t* mk) {
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1, cap, vgy, vh);
     if (geo.nwg <= 0) return 0;
     // the variant (and with it the B1 chunk work) follows the tiles of ONE image: views mode then
@@ -663,10 +716,10 @@ int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int 
     const long long sel = vgy > 0 ? (long long)geo.vgy * geo.grid_x : geo.nwg;
     if (sel >= kF6BandTiles)
         hipLaunchKernelGGL(blend_forward_kernel<kF6FullWaves>, dim3(geo.nwg), dim3(64 * kF6FullWaves), 0, s, geo,
-                           ranges, sorted_gid, rec, out_color, final_T, accum, term, ck);
+                           ranges, sorted_gid, rec, out_color, final_T, accum, term, ck, mk);
     else
         hipLaunchKernelGGL(blend_forward_kernel<kF6BandWaves>, dim3(geo.nwg), dim3(64 * kF6BandWaves), 0, s, geo,
-                           ranges, sorted_gid, rec, out_color, final_T, accum, term, ck);
+                           ranges, sorted_gid, rec, out_color, final_T, accum, term, ck, mk);
     return (int)hipGetLastError();
 }
 
@@ -674,7 +727,8 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
                           const uint2* ranges, const uint32_t* sorted_gid, const uint4* rect,
                           const float4* rec, const float* final_T,
                           const float* accum, const float* dL_dpix, float* partial, long long cap,
-                          const uint32_t* term, const float4* ck, hipStream_t s, int vgy, int vh) {
+                          const uint32_t* term, const float4* ck, hipStream_t s, int vgy, int vh,
+                          const uint8_t* mk) {
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1, cap, vgy, vh);
     if (geo.nwg <= 0) return 0;
     const PartLayout pl(cap);
@@ -682,7 +736,8 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
     const int blocks = 8 * (geo.nwg / 8 + 1) * kMaxChunks;
     hipLaunchKernelGGL(blend_backward_kernel, dim3(blocks), dim3(64), 0, s, geo, ranges, sorted_gid, rect, rec,
                        final_T, accum, dL_dpix, reinterpret_cast<float*>(base + pl.p8),
-                       reinterpret_cast<float*>(base + pl.p1), reinterpret_cast<uint8_t*>(base + pl.fl), term, ck);
+                       reinterpret_cast<float*>(base + pl.p1), reinterpret_cast<uint8_t*>(base + pl.fl), term, ck,
+                       mk);
     return (int)hipGetLastError();
 }
 

@@ -147,19 +147,21 @@ __host__ __device__ inline size_t ck_slot_of(bool fixed, uint32_t start, int til
 // `tiles` tiles.  The tile-key sort ping-pongs (kA, vA) <-> (kB, vB); F3 emits into (kA, vA).
 // Then the checkpoint slots: ck_slots x 256 float4, and one live byte per (slot, 16x4 stripe).
 struct BinLayout {
-    size_t kA, vA, kB, vB, hist, ck, ckm, total, ck_slots;
+    size_t kA, vA, kB, vB, hist, ck, ckm, mk = 0, total, ck_slots;
     BinLayout(long long cap, long long tiles) {
         size_t o = 0, n = (size_t)(cap > 0 ? cap : 1);
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
-        // + 256 entries: B1 reads list values in aligned 256-entry windows that may pass the end
-        kA = take(4 * (n + 256));
-        vA = take(4 * (n + 256));
-        kB = take(4 * (n + 256));
-        vB = take(4 * (n + 256));
+        kA = take(4 * n);
+        vA = take(4 * n);
+        kB = take(4 * n);
+        vB = take(4 * n);
         hist = take(4 * sort_scratch_words(n));
         ck_slots = ck_pool_slots(cap, tiles);
         ck = take(ck_slots * 256 * 16);
         ckm = take(ck_slots * 4);
+        // F6's stripe mask of every list entry it loads (one byte each), from which B1 picks the
+        // entries it has to visit before loading any record (+ B1's 256-entry window past the end)
+        mk = take(n + 256);
         total = o;
     }
 };

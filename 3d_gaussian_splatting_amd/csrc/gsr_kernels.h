@@ -54,11 +54,9 @@ int launch_scan(const uint32_t* tiles, int n, uint32_t* offsets, uint32_t* scan_
 // F3: inst_start (rect[g].z) and the emitted (tile key, gid) pairs in gid order, rect row-major,
 // band rows from ty0 -- at most `cap` of them.  For n <= kFusedScanMax one look-back kernel
 // also does F2 (offsets, *total_out); lookback: 16 + ceil(n / 256) u32.
-// F3 values are gid << kValShift | the instance's stripe mask (gsr_stripe.h), computed from rec;
-// vgy > 0: views mode (tile rows per view).
 int launch_duplicate(const uint32_t* tiles, uint4* rect, int n, int grid_x, int ty0, uint32_t* offsets,
                      uint32_t* lookback, uint32_t* tkey, uint32_t* tgid, long long cap, uint32_t* total_out,
-                     const float4* rec, int vgy, hipStream_t s);
+                     hipStream_t s);
 
 // Per-tile depth order: every tile's slice of `gid` (tile-sorted, gid order within a tile) is
 // sorted in place by (depth_key[gid], gid) -- the canonical (tile, depth, gid) order -- with a
@@ -77,7 +75,7 @@ int launch_depth_presort(const uint32_t* depth_key, const uint32_t* tiles, const
 // `offsets`, the inclusive scan the gather reads) and writes inst_start into rect[gid].z.
 int launch_duplicate_ranked(const uint32_t* rtiles, const uint4* rrect, uint4* rect, int n, int grid_x, int ty0,
                             const uint32_t* bexcl, uint32_t* offsets, uint32_t* tkey, uint32_t* tgid, long long cap,
-                            const float4* rec, int vgy, hipStream_t s);
+                            hipStream_t s);
 int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long K, const uint32_t* depth_key,
                            uint32_t* gid, uint32_t* ovf, uint32_t* ovf_count, uint32_t* ovf2, uint32_t* ovf2_count,
                            uint32_t* done, uint32_t* scratch_hi, uint32_t* scratch_lo,
@@ -92,7 +90,7 @@ int launch_finalize(const uint32_t* sorted_tile, long long cap, const uint32_t* 
 int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
                          const uint2* ranges, const uint32_t* sorted_gid, const float4* rec,
                          float* out_color, float* final_T, float* accum, uint32_t* term, float4* ck, long long cap,
-                         hipStream_t s, int vgy = 0, int vh = 0);
+                         hipStream_t s, int vgy = 0, int vh = 0, uint8_t* mk = nullptr);
 
 // F6 writes term[t] (see kMaxChunks) and the B1 chunk checkpoints `ck` (ImgLayout.ck).
 // B1: per-tile front-to-back gradients -> per-instance partial entry j (PartLayout(cap)), where
@@ -105,7 +103,8 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
                           const uint2* ranges, const uint32_t* sorted_gid, const uint4* rect,
                           const float4* rec, const float* final_T,
                           const float* accum, const float* dL_dpix, float* partial, long long cap,
-                          const uint32_t* term, const float4* ck, hipStream_t s, int vgy = 0, int vh = 0);
+                          const uint32_t* term, const float4* ck, hipStream_t s, int vgy = 0, int vh = 0,
+                          const uint8_t* mk = nullptr);
 // (vgy, vh: views mode -- bands of vgy tile rows per view, vh valid pixel rows each; 0 = one image)
 
 // record layout constants shared by preprocess and the blend kernels

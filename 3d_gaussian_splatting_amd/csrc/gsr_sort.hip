@@ -25,7 +25,6 @@
 #include <cstdlib>
 
 #include "gsr_kernels.h"
-#include "gsr_stripe.h"
 
 namespace gsr {
 namespace {
@@ -363,15 +362,11 @@ __device__ __forceinline__ uint32_t udiv_small(uint32_t a, uint32_t b) {
 
 // Emission of one wave's instances [first, first + wtotal): lane i finds its owner -- the last
 // lane whose start (s_start, relative to `first`) is <= i -- by binary search in LDS and writes
-// (tile key, value).  The value is gid << kValShift | the stripe mask of the Gaussian's record
-// over that tile (gsr_stripe.h: which 16x4 stripes its alpha >= 1/255 footprint reaches), so
-// the blend kernels know which entries they must load before loading any record.  vgy > 0:
-// views mode, the tile's pixel y is taken inside its view's band of vgy tile rows.  Instances
-// at or past `cap` are dropped (binning overflow).
+// (tile key, gid).  Instances at or past `cap` are dropped (binning overflow).
 __device__ __forceinline__ void emit_wave(const uint32_t* s_start, const uint32_t* s_g, const uint32_t* s_w,
                                           const uint32_t* s_x0, const uint32_t* s_y0, uint32_t first,
                                           uint32_t wtotal, int grid_x, long long cap, uint32_t* __restrict__ tkey,
-                                          uint32_t* __restrict__ tgid, const float4* __restrict__ rec, int vgy) {
+                                          uint32_t* __restrict__ tgid) {
     const int lane = threadIdx.x & 63;
     for (uint32_t i = lane; i < wtotal; i += 64) {
         if ((long long)first + i >= cap) break;
@@ -382,12 +377,8 @@ __device__ __forceinline__ void emit_wave(const uint32_t* s_start, const uint32_
         const uint32_t local = i - s_start[o];
         const uint32_t wd = s_w[o];
         const uint32_t dy = udiv_small(local, wd), dx = local - dy * wd;
-        const uint32_t tx = s_x0[o] + dx, ty = s_y0[o] + dy, g = s_g[o];
-        const uint32_t tyl = vgy > 0 ? ty - (ty / (uint32_t)vgy) * (uint32_t)vgy : ty;
-        const float4* r = rec + 3 * (size_t)g;
-        const uint32_t m = stripe_mask(r[0], r[1], r[2], (float)(tx * kTile), (float)(tyl * kTile));
-        tkey[first + i] = ty * (uint32_t)grid_x + tx;
-        tgid[first + i] = (g << kValShift) | m;
+        tkey[first + i] = (s_y0[o] + dy) * (uint32_t)grid_x + s_x0[o] + dx;
+        tgid[first + i] = s_g[o];
     }
 }
 
@@ -409,8 +400,7 @@ __global__ __launch_bounds__(256) void scan_duplicate_kernel(const uint32_t* __r
                                                              uint32_t* __restrict__ tgid, long long cap,
                                                              uint32_t* __restrict__ status,
                                                              uint32_t* __restrict__ ticket,
-                                                             uint32_t* __restrict__ total_out,
-                                                             const float4* __restrict__ rec, int vgy) {
+                                                             uint32_t* __restrict__ total_out) {
     __shared__ uint32_t s_start[kWaves][64], s_g[kWaves][64], s_w[kWaves][64], s_x0[kWaves][64],
         s_y0[kWaves][64];
     __shared__ uint32_t wsum[kWaves];
@@ -501,8 +491,7 @@ __global__ __launch_bounds__(256) void scan_duplicate_kernel(const uint32_t* __r
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    emit_wave(s_start[w], s_g[w], s_w[w], s_x0[w], s_y0[w], excl + wbase, wsum[w], grid_x, cap, tkey, tgid, rec,
-              vgy);
+    emit_wave(s_start[w], s_g[w], s_w[w], s_x0[w], s_y0[w], excl + wbase, wsum[w], grid_x, cap, tkey, tgid);
 }
 
 // RANKED (presort mode): lane i is depth rank i; its tiles / rect / gid come from the rank-order
@@ -516,8 +505,7 @@ __global__ __launch_bounds__(256) void duplicate_kernel(uint32_t* __restrict__ o
                                                         uint4* __restrict__ rect, const uint4* __restrict__ rrect,
                                                         int P, int grid_x, int ty0,
                                                         uint32_t* __restrict__ tkey, uint32_t* __restrict__ tgid,
-                                                        long long cap, const uint32_t* __restrict__ bexcl,
-                                                        const float4* __restrict__ rec, int vgy) {
+                                                        long long cap, const uint32_t* __restrict__ bexcl) {
     __shared__ uint32_t s_start[kWaves][64], s_g[kWaves][64], s_w[kWaves][64], s_x0[kWaves][64],
         s_y0[kWaves][64];
     __shared__ uint32_t wsum[kWaves];
@@ -563,7 +551,7 @@ __global__ __launch_bounds__(256) void duplicate_kernel(uint32_t* __restrict__ o
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    emit_wave(s_start[w], s_g[w], s_w[w], s_x0[w], s_y0[w], first, total, grid_x, cap, tkey, tgid, rec, vgy);
+    emit_wave(s_start[w], s_g[w], s_w[w], s_x0[w], s_y0[w], first, total, grid_x, cap, tkey, tgid);
 }
 
 // ---- presort: each depth rank's binning payload, gathered once into rank order ----
@@ -677,7 +665,7 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
         const int idx = base + r * 64 + lane;
         const bool valid = idx < end;
         val[r] = valid ? gid[rg.x + idx] : 0u;
-        key[r] = valid ? depth_key[val[r] >> kValShift] : 0xFFFFFFFFu;
+        key[r] = valid ? depth_key[val[r]] : 0xFFFFFFFFu;
         if (valid) {
             kor |= key[r];
             kand &= key[r];
@@ -876,8 +864,8 @@ __device__ __attribute__((noinline)) void merge_sorted_chunks(const uint2 r, con
     uint32_t* H = hi + r.x;
     uint32_t* L = lo + r.x;
     for (int i = threadIdx.x; i < n; i += 1024) {
-        const uint32_t g = gid[r.x + i];  // gid << kValShift | mask: orders like gid
-        H[i] = depth_key[g >> kValShift];
+        const uint32_t g = gid[r.x + i];
+        H[i] = depth_key[g];
         L[i] = g;
     }
     __syncthreads();
@@ -1006,17 +994,17 @@ int launch_scan(const uint32_t* tiles, int n, uint32_t* offsets, uint32_t* scan_
 
 int launch_duplicate(const uint32_t* tiles, uint4* rect, int n, int grid_x, int ty0, uint32_t* offsets,
                      uint32_t* lookback, uint32_t* tkey, uint32_t* tgid, long long cap, uint32_t* total_out,
-                     const float4* rec, int vgy, hipStream_t s) {
+                     hipStream_t s) {
     if (n <= 0) return 0;
     if (n <= kFusedScanMax) {  // fused look-back scan + duplicate
         const int nb = div_up(n, 256);
         if (hipError_t e = hipMemsetAsync(lookback, 0, sizeof(uint32_t) * (16 + (size_t)nb), s)) return (int)e;
         hipLaunchKernelGGL(scan_duplicate_kernel, dim3(nb), dim3(256), 0, s, tiles, rect, n, grid_x, ty0, offsets,
-                           tkey, tgid, cap, lookback + 16, lookback, total_out, rec, vgy);
+                           tkey, tgid, cap, lookback + 16, lookback, total_out);
         return (int)hipGetLastError();
     }
     hipLaunchKernelGGL(duplicate_kernel<false>, dim3(div_up(n, 256)), dim3(256), 0, s, offsets, tiles, rect,
-                       nullptr, n, grid_x, ty0, tkey, tgid, cap, nullptr, rec, vgy);
+                       nullptr, n, grid_x, ty0, tkey, tgid, cap, nullptr);
     return (int)hipGetLastError();
 }
 
@@ -1036,10 +1024,10 @@ int launch_depth_presort(const uint32_t* depth_key, const uint32_t* tiles, const
 
 int launch_duplicate_ranked(const uint32_t* rtiles, const uint4* rrect, uint4* rect, int n, int grid_x, int ty0,
                             const uint32_t* bexcl, uint32_t* offsets, uint32_t* tkey, uint32_t* tgid, long long cap,
-                            const float4* rec, int vgy, hipStream_t s) {
+                            hipStream_t s) {
     if (n <= 0) return 0;
     hipLaunchKernelGGL(duplicate_kernel<true>, dim3(div_up(n, 256)), dim3(256), 0, s, offsets, rtiles, rect, rrect, n,
-                       grid_x, ty0, tkey, tgid, cap, bexcl, rec, vgy);
+                       grid_x, ty0, tkey, tgid, cap, bexcl);
     return (int)hipGetLastError();
 }
 

@@ -32,7 +32,6 @@ MAX_BANDS = 16
 VIEW_SORTED_GID, VIEW_SORTED_TILE, VIEW_RANGES, VIEW_FINAL_T, VIEW_N_CONTRIB, VIEW_DEPTH_KEY, \
     VIEW_TILES_TOUCHED, VIEW_RECORDS, VIEW_COUNTS, VIEW_TERM, VIEW_CK_LIVE = range(1, 12)
 TERM_STRIDE = 32  # GSR_TERM_STRIDE: words per tile of VIEW_TERM
-VALUE_SHIFT = 4   # GSR_VALUE_SHIFT: VIEW_SORTED_GID values are gid << 4 | the entry's stripe mask
 CK_DIV = 48       # a tile of n instances opens at most n // CK_DIV B1 chunks (gsr.h, VIEW_CK_LIVE)
 
 

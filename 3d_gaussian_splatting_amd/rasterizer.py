@@ -111,9 +111,7 @@ class ForwardState:
         return t[off:off + 4].view(torch.int32)
 
     def view(self, what: int, dtype: torch.dtype, count: int) -> torch.Tensor:
-        """Copy of an internal array (gsr_view) as a torch tensor.  VIEW_SORTED_GID comes back as
-        the Gaussian ids (the list values carry each entry's stripe mask in their low
-        native.VALUE_SHIFT bits, gsr.h GSR_VIEW_SORTED_GID)."""
+        """Copy of an internal array (gsr_view) as a torch tensor."""
         L = native.load_hip()
         c = native.camera_struct(self.cam)
         p = L.gsr_view(ctypes.byref(c), self.gauss.P, ctypes.byref(self.buffers), what)
@@ -121,10 +119,7 @@ class ForwardState:
             return torch.empty(0, dtype=dtype, device=self.color.device)
         t, off = self._owner(p)
         nbytes = count * torch.empty(0, dtype=dtype).element_size()
-        out = t[off:off + nbytes].view(dtype).clone()
-        if what == native.VIEW_SORTED_GID:
-            out = ((out.view(torch.int32) >> native.VALUE_SHIFT) & ((1 << (32 - native.VALUE_SHIFT)) - 1)).view(dtype)
-        return out
+        return t[off:off + nbytes].view(dtype).clone()
 
 
 @dataclass

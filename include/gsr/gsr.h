@@ -243,10 +243,7 @@ int gsr_shard_backward(const gsr_camera* cam, const gsr_gaussians* shard, const 
 
 /* Introspection for tests / the benchmark (all device pointers into the caller's buffers,
  * or NULL when not applicable).  `what`: see gsr_view_* below. */
-#define GSR_VIEW_SORTED_GID 1       /* uint32[K]: sorted instance i's value: its Gaussian id
-                                       << GSR_VALUE_SHIFT | the 4-bit mask of the tile's 16x4
-                                       pixel stripes its alpha >= 1/255 footprint reaches    */
-#define GSR_VALUE_SHIFT 4           /* Gaussian ids (and V * P view entries) < 2^28           */
+#define GSR_VIEW_SORTED_GID 1       /* uint32[K]: Gaussian id of sorted instance i       */
 #define GSR_VIEW_SORTED_TILE 2      /* uint32[K]: tile id of sorted instance i             */
 #define GSR_VIEW_RANGES 3           /* uint32[2*tiles]: [start,end) per tile               */
 #define GSR_VIEW_FINAL_T 4          /* float[H*W]                                          */
