@@ -137,6 +137,22 @@ class ViewsState:
 
     @property
     def num_rendered(self) -> int:
+        """K over all views.  Under a binning bound (max_rendered > 0) it is read back on first
+        access through gsr_read_num_rendered with the pass's tall camera (the views stacked as
+        bands of ceil(H / 16) tile rows), raising on an overflow."""
+        if self.buffers.num_rendered < 0:
+            L = native.load_hip()
+            tall = native.Camera()
+            ctypes.memmove(ctypes.byref(tall), ctypes.byref(self.cstructs[0]), ctypes.sizeof(tall))
+            tall.height = len(self.cams) * ((self.cams[0].height + 15) // 16) * 16
+            k = ctypes.c_int32(0)
+            rc = L.gsr_read_num_rendered(ctypes.byref(tall), ctypes.byref(self.buffers), ctypes.byref(k),
+                                         ctypes.c_void_p(torch.cuda.current_stream(self.color.device).cuda_stream))
+            if rc == native.GSR_ERR_OVERFLOW:
+                raise OverflowError(native.last_error())
+            if rc != 0:
+                raise RuntimeError(f"gsr_read_num_rendered failed ({rc}): {native.last_error()}")
+            self.buffers.num_rendered = k.value
         return int(self.buffers.num_rendered)
 
 

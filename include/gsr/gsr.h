@@ -161,7 +161,9 @@ int gsr_forward_batch(int32_t V, const gsr_camera* cams, const gsr_gaussians* gs
  * sum over the views, added in view order -- (((g_0 + g_1) + g_2) + ...) -- as a caller
  * summing per-view backward results would.  alloc_scratch is asked for three blocks: the
  * partial gradients, 48 * V * P bytes of grad2d, and (V > 1) the V-1 per-view leaf gradient
- * slices.  1 <= V <= GSR_MAX_VIEWS. */
+ * slices.  1 <= V <= GSR_MAX_VIEWS.  Under a binning bound (rs->max_rendered > 0) the pass's K
+ * is read with gsr_read_num_rendered given the tall camera: cams[0] with height
+ * V * ceil(H / 16) * 16 (the layout of the pass's image buffer). */
 #define GSR_MAX_VIEWS 8
 int gsr_forward_views(int32_t V, const gsr_camera* cams, const gsr_gaussians* gs,
                       const gsr_raster_settings* rs, float* out_color, int32_t* radii,

@@ -88,6 +88,22 @@ def test_views_full_and_one():
     _check(rast, _cams(192, 128, 1), args)
 
 
+def test_views_bounded_count():
+    """Under a binning bound K stays on the device; ViewsState.num_rendered reads it back through
+    the pass's tall camera, and a bound below K is reported as an overflow."""
+    rast = pkg("rasterizer").CAbiRasterizer("cuda")
+    args = _scene(20000, 25, 320, 240)
+    cams = _cams(320, 240, 3)
+    exact = rast.forward_views(cams, *args, sh_degree=3)
+    K = exact.num_rendered
+    bounded = rast.forward_views(cams, *args, sh_degree=3, max_rendered=K + 100)
+    assert bounded.num_rendered == K
+    assert torch.equal(bounded.color, exact.color)
+    short = rast.forward_views(cams, *args, sh_degree=3, max_rendered=max(K // 2, 1))
+    with pytest.raises(OverflowError):
+        short.num_rendered
+
+
 def test_views_limits():
     rast = pkg("rasterizer").CAbiRasterizer("cuda")
     args = _scene(2000, 24, 128, 96)
