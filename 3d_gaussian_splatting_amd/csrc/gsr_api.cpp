@@ -205,7 +205,7 @@ void band(const gsr_camera* cam, const gsr_raster_settings* rs, int* y0, int* y1
 struct Views {
     uint32_t *depth_key, *tiles, *flags, *offsets, *partials, *lookback;
     bool presort;                                          // gsr_internal.h use_presort
-    uint32_t *dk0, *dv0, *dk1, *dv1, *dhist, *rtiles, *rank_of;  // presort only
+    uint32_t *dk0, *dv0, *dk1, *dv1, *dhist, *rtiles;      // presort only
     uint4* rrect;
     float4* rec;
     uint4* rect;
@@ -240,7 +240,6 @@ Views views(const gsr_camera* cam, long long n, const gsr_buffers* b) {
         v.dhist = at<uint32_t>(b->geom, gl.dhist);
         v.rtiles = at<uint32_t>(b->geom, gl.rtiles);
         v.rrect = at<uint4>(b->geom, gl.rrect);
-        v.rank_of = at<uint32_t>(b->geom, gl.rank_of);
     }
     v.ranges = at<uint2>(b->image, il.ranges);
     v.counters = at<uint32_t>(b->image, il.counters);
@@ -326,8 +325,8 @@ int fwd_phase1(FwdJob& j, gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_image, voi
     if (v.presort) {  // global (depth, gid) order, the rank-order payload and its block sums + K
         // (the lookback words, unused by the presort path, hold the block sums; F3 finishes the scan)
         GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_depth_presort(v.depth_key, v.tiles, v.rect, (int)j.n, v.dk0, v.dv0,
-                                                             v.dk1, v.dv1, v.dhist, v.rtiles, v.rrect, v.rank_of,
-                                                             v.lookback, v.K_dev, stream),
+                                                             v.dk1, v.dv1, v.dhist, v.rtiles, v.rrect, v.lookback,
+                                                             v.K_dev, stream),
                   "depth presort");
         return 0;
     }
@@ -410,12 +409,9 @@ int run_preprocess(const gsr_camera* cam, const gsr_gaussians* gs, int ty0, int 
 }
 
 // B1 (+ the per-Gaussian gather into grad2d): shared by every backward entry point.
-// rank_rows: in presort mode leave the gather's sums unconverted in rank order for a B2 that
-// follows in rank mode (gsr_backward / gsr_backward_views); the public B1-only entry points and
-// the band path keep per-Gaussian converted rows.
 int blend_backward(const gsr_camera* cam, const gsr_raster_settings* rs, const gsr_buffers* bufs, const float* dL_dpix,
                    gsr_alloc_fn alloc_scratch, void* ctx, float* grad2d, hipStream_t stream, bool debug, int vgy = 0,
-                   int vh = 0, bool rank_rows = false) {
+                   int vh = 0) {
     if (!bufs || !bufs->geom || !bufs->image || !bufs->binning || !dL_dpix) return fail(-1, "missing forward buffers / dL_dpix");
     if (!grad2d) return fail(-1, "null grad2d");
     const long long n = bufs->n_local, cap = bufs->capacity;
@@ -434,8 +430,7 @@ int blend_backward(const gsr_camera* cam, const gsr_raster_settings* rs, const g
               "blend backward");
     GSR_STAGE(GSR_STAGE_GATHER, launch_gather_grad2d(v.offsets, partial, v.rec, cam->width, vgy > 0 ? vh : cam->height,
                                                      cap, (int)n,
-                                                     v.presort ? v.rrect : nullptr, grad2d, stream,
-                                                     rank_rows && v.presort),
+                                                     v.presort ? v.rrect : nullptr, grad2d, stream),
               "gather grad2d");
     return 0;
 }
@@ -707,7 +702,7 @@ int gsr_backward_views(int32_t V, const gsr_camera* cams, const gsr_gaussians* g
     float* grad2d = static_cast<float*>(alloc_scratch(ctx, sizeof(float) * kPart * (size_t)n));
     if (!grad2d) return fail(-2, "allocation failed (grad2d, %lld entries)", n);
     if (int e = blend_backward(&tall, &rv, bufs, dL_dpix, alloc_scratch, ctx, grad2d, stream, debug,
-                               div_up(cams[0].height, kTile), cams[0].height, true))
+                               div_up(cams[0].height, kTile), cams[0].height))
         return e;
     const GaussIn in = gauss_in(gs);
     const GradOut out = grad_out(grads);
@@ -732,8 +727,7 @@ int gsr_backward_views(int32_t V, const gsr_camera* cams, const gsr_gaussians* g
     }
     const Views v = views(&tall, n, bufs);
     GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward_views(cams, V, in, v.depth_key, v.flags, grad2d, out,
-                                                                         scratch, stream,
-                                                                         v.presort ? v.rank_of : nullptr, v.rec),
+                                                                         scratch, stream),
               "preprocess backward (views)");
     if (V > 1) GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_views_sum(in, V, out, scratch, stream), "views sum");
     return 0;
@@ -752,13 +746,11 @@ int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raste
     if (!alloc_scratch) return fail(-1, "null scratch allocator");
     float* grad2d = static_cast<float*>(alloc_scratch(ctx, sizeof(float) * kPart * (size_t)gs->P));
     if (!grad2d) return fail(-2, "allocation failed (grad2d, P=%d)", gs->P);
-    if (int e = blend_backward(cam, rs, bufs, dL_dpix, alloc_scratch, ctx, grad2d, stream, debug, 0, 0, true))
-        return e;
+    if (int e = blend_backward(cam, rs, bufs, dL_dpix, alloc_scratch, ctx, grad2d, stream, debug)) return e;
     const Views v = views(cam, gs->P, bufs);
     GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_backward(*cam, gauss_in(gs), 0, gs->P, v.depth_key,
                                                                    stored_flags(cam, rs, v.flags), grad2d,
-                                                                   grad_out(grads), stream,
-                                                                   v.presort ? v.rank_of : nullptr, v.rec),
+                                                                   grad_out(grads), stream),
               "preprocess backward");
     return 0;
 }

@@ -75,7 +75,7 @@ inline bool use_presort(long long n) { return n >= kPresortMin; }
 
 struct GeomLayout {
     size_t depth_key, tiles, flags, rec, rect, offsets, partials, lookback, total;
-    size_t dk0 = 0, dv0 = 0, dk1 = 0, dv1 = 0, dhist = 0, rtiles = 0, rrect = 0, rank_of = 0;  // presort only
+    size_t dk0 = 0, dv0 = 0, dk1 = 0, dv1 = 0, dhist = 0, rtiles = 0, rrect = 0;  // presort only
     GeomLayout(long long P) {
         size_t o = 0, n = (size_t)(P > 0 ? P : 1);
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
@@ -95,7 +95,6 @@ struct GeomLayout {
             dhist = take(4 * sort_scratch_words(n));
             rtiles = take(4 * n);   // tiles_touched in rank order
             rrect = take(16 * n);   // uint4 (rect lo, rect hi, gid, 0) in rank order
-            rank_of = take(4 * n);  // each Gaussian's depth rank (B2 finds its gather row by it)
         }
         total = o;
     }

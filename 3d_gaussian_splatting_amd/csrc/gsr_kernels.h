@@ -70,7 +70,7 @@ int launch_duplicate(const uint32_t* tiles, uint4* rect, int n, int grid_x, int 
 // K into *total_out.
 int launch_depth_presort(const uint32_t* depth_key, const uint32_t* tiles, const uint4* rect, int n, uint32_t* dk0,
                          uint32_t* dv0, uint32_t* dk1, uint32_t* dv1, uint32_t* hist, uint32_t* rtiles, uint4* rrect,
-                         uint32_t* rank_of, uint32_t* bsum, uint32_t* total_out, hipStream_t s);
+                         uint32_t* bsum, uint32_t* total_out, hipStream_t s);
 // F3 in rank order: each 256-rank block scans its rtiles from its offset bexcl[block] (writing
 // `offsets`, the inclusive scan the gather reads) and writes inst_start into rect[gid].z.
 int launch_duplicate_ranked(const uint32_t* rtiles, const uint4* rrect, uint4* rect, int n, int grid_x, int ty0,
@@ -113,9 +113,8 @@ constexpr float kLn2 = 0.6931471805599453f;  // conic A = -2 ln2 a', B = -ln2 b'
 // sum partials per Gaussian (emission order) -> grad2d (kPart floats per Gaussian; zeros for
 // culled Gaussians).  offsets: the inclusive tile scan in gid order; partial: PartLayout(cap).
 // rrect: the rank-order payload in presort mode (offsets then in rank order), else nullptr
-// raw (with rrect): unconverted sums in rank order for a B2 in rank mode (rank_of / rec below)
 int launch_gather_grad2d(const uint32_t* offsets, const float* partial, const float4* rec, int W, int H,
-                         long long cap, int P, const uint4* rrect, float* grad2d, hipStream_t s, bool raw = false);
+                         long long cap, int P, const uint4* rrect, float* grad2d, hipStream_t s);
 
 struct GradOut {
     float *means2D, *conic, *opac, *colors, *means3D, *sh_dc, *sh_rest, *scales, *rots, *cov3D;
@@ -125,18 +124,14 @@ struct GradOut {
 // floats each).  Inputs are indexed by g; grad2d and all outputs by g - g0.
 int launch_preprocess_backward(const gsr_camera& cam, const GaussIn& in, int g0, int g1,
                                const uint32_t* depth_key, const uint32_t* flags, const float* grad2d,
-                               const GradOut& out, hipStream_t s, const uint32_t* rank_of = nullptr,
-                               const float4* rec = nullptr);
-// (rank_of / rec: rank mode -- grad2d then holds the presort gather's raw rank-order rows,
-// converted here with each Gaussian's record)
+                               const GradOut& out, hipStream_t s);
 // Views mode: B2 of V views in one launch (grid.y = view) from the per-(view, Gaussian) entries
 // v * P + g of depth_key / flags / grad2d; view v's 2D gradients (means2D, conic) go to rows
 // v * P.. of out's, its leaf gradients to `out` (v = 0) or to slice v - 1 of `scratch` (P rows per
 // slice), which launch_views_sum then adds to `out` in view order.
 int launch_preprocess_backward_views(const gsr_camera* cams, int V, const GaussIn& in, const uint32_t* depth_key,
                                      const uint32_t* flags, const float* grad2d, const GradOut& out,
-                                     const GradOut& scratch, hipStream_t s, const uint32_t* rank_of = nullptr,
-                                     const float4* rec = nullptr);
+                                     const GradOut& scratch, hipStream_t s);
 int launch_views_sum(const GaussIn& in, int V, const GradOut& out, const GradOut& scratch, hipStream_t s);
 
 // ---- multi-GPU exchange (gsr_shard.hip) ----

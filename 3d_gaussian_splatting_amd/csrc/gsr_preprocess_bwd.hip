@@ -39,29 +39,15 @@ constexpr float kC1 = 0.4886025119029199f;
 // its blend record.  The 48-B result lands at grad2d[gid].
 constexpr int kGatherWin = 512;
 
-// The moments -> 2D gradient conversion (d mean2D in NDC, d conic, d opacity = sum G dL/dalpha =
-// S0 / o, d colour) with the Gaussian's conic and opacity from its blend record (q0, q1; zeros
-// for a Gaussian without instances).  Shared by the gather and, in rank mode, by B2.
-__device__ __forceinline__ void moments_to_grad2d(const float (&a)[9], const float4 q0, const float4 q1, float hw,
-                                                  float hh, float4& d0, float4& d1, float4& d2) {
-    const float A = -2.0f * kLn2 * q0.z, B = -kLn2 * q0.w, C = -2.0f * kLn2 * q1.x;
-    const float Sx = a[0], Sy = a[1], S0 = a[5];
-    d0 = make_float4((-A * Sx - B * Sy) * hw, (-C * Sy - B * Sx) * hh, -0.5f * a[2], -a[3]);
-    d1 = make_float4(-0.5f * a[4], S0 != 0.0f ? S0 / q1.y : 0.0f, a[6], a[7]);
-    d2 = make_float4(a[8], 0.f, 0.f, 0.f);
-}
-
 // rrect (presort mode): index i is a depth rank whose emission range the rank-order offsets give;
-// its Gaussian is rrect[i].z.  nullptr: i is the gid itself.  raw (presort mode, B2 following):
-// the sums are written unconverted to row i (rank order, coalesced) with word 9 = 1 when the
-// Gaussian has instances, and B2 converts them (no record read, no scattered row here).
+// its Gaussian (record read, grad2d row written) is rrect[i].z.  nullptr: i is the gid itself.
 __global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __restrict__ offsets,
                                                             const float4* __restrict__ p8,
                                                             const float* __restrict__ p1,
                                                             const uint8_t* __restrict__ fl,
                                                             const float4* __restrict__ rec, float hw, float hh,
                                                             int P, uint32_t cap, const uint4* __restrict__ rrect,
-                                                            int raw, float* __restrict__ grad2d) {
+                                                            float* __restrict__ grad2d) {
     __shared__ float4 w8[2 * kGatherWin];
     __shared__ float w1[kGatherWin];
     __shared__ uint32_t wv[kGatherWin / 4];
@@ -72,10 +58,10 @@ __global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __re
     const uint32_t J0 = g0 ? off(g0 - 1) : 0u, J1 = off(gl - 1);
     const uint32_t s = g < P ? (g ? off(g - 1) : 0u) : 0u;
     const uint32_t e = g < P ? off(g) : 0u;
-    const uint32_t gid = g < P ? (rrect && !raw ? rrect[g].z : (uint32_t)g) : 0u;
+    const uint32_t gid = g < P ? (rrect ? rrect[g].z : (uint32_t)g) : 0u;
     // the Gaussian's conic and opacity, loaded before the window loop (latency overlaps it)
     float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0;
-    if (!raw && g < P && e > s) {
+    if (g < P && e > s) {
         q0 = rec[3 * (size_t)gid];
         q1 = rec[3 * (size_t)gid + 1];
     }
@@ -101,18 +87,13 @@ __global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __re
         __syncthreads();
     }
     if (g >= P) return;
+    // moments -> d mean2D (NDC), d conic, d opacity (sum G dL/dalpha = S0 / o), d colour
+    const float A = -2.0f * kLn2 * q0.z, B = -kLn2 * q0.w, C = -2.0f * kLn2 * q1.x;
+    const float Sx = a[0], Sy = a[1], S0 = a[5];
     float4* dst = reinterpret_cast<float4*>(grad2d + (size_t)kPart * gid);
-    if (raw) {
-        dst[0] = make_float4(a[0], a[1], a[2], a[3]);
-        dst[1] = make_float4(a[4], a[5], a[6], a[7]);
-        dst[2] = make_float4(a[8], e > s ? 1.0f : 0.0f, 0.f, 0.f);
-        return;
-    }
-    float4 d0, d1, d2;
-    moments_to_grad2d(a, q0, q1, hw, hh, d0, d1, d2);
-    dst[0] = d0;
-    dst[1] = d1;
-    dst[2] = d2;
+    dst[0] = make_float4((-A * Sx - B * Sy) * hw, (-C * Sy - B * Sx) * hh, -0.5f * a[2], -a[3]);
+    dst[1] = make_float4(-0.5f * a[4], S0 != 0.0f ? S0 / q1.y : 0.0f, a[6], a[7]);
+    dst[2] = make_float4(a[8], 0.f, 0.f, 0.f);
 }
 
 // Per-Gaussian inputs of B2, loaded before the SH rows are staged so that their HBM
@@ -126,33 +107,14 @@ struct BwdIn {
     uint32_t cl;  // stored SH clamp bits (flags != nullptr)
 };
 
-// Rank mode (presort): the gather left raw moment sums in rank order; row rank_of[g], converted
-// here with the Gaussian's own record (read in g order, coalesced).
-struct RankIn {
-    const uint32_t* rank_of;  // nullptr: grad2d holds converted rows by g
-    const float* rows;        // the gather's rank-order rows (all entries)
-    const float4* rec;
-    float hw, hh;
-};
-
 template <bool SUM>
 __device__ __forceinline__ BwdIn load_bwd_in(const GaussIn& in, int g, int o, const uint32_t* __restrict__ depth_key,
                                              const uint32_t* __restrict__ flags, const float* __restrict__ grad2d,
-                                             const BandSum& bs, const RankIn& rk) {
+                                             const BandSum& bs) {
     BwdIn b;
     b.visible = depth_key[g] != 0xFFFFFFFFu;
     float4 v0, v1, v2;
-    if (!SUM && rk.rank_of) {
-        const float4* src = reinterpret_cast<const float4*>(rk.rows + (size_t)kPart * rk.rank_of[g]);
-        const float4 u0 = src[0], u1 = src[1], u2 = src[2];
-        const float a[9] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w, u2.x};
-        float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0;
-        if (u2.y != 0.0f) {  // the Gaussian had instances (as the gather's own record load)
-            q0 = rk.rec[3 * (size_t)g];
-            q1 = rk.rec[3 * (size_t)g + 1];
-        }
-        moments_to_grad2d(a, q0, q1, rk.hw, rk.hh, v0, v1, v2);
-    } else if (SUM) {  // the bands' returned rows, summed in band order
+    if (SUM) {  // the bands' returned rows, summed in band order
         v0 = make_float4(0.f, 0.f, 0.f, 0.f);
         v1 = v0;
         v2 = v0;
@@ -514,7 +476,7 @@ template <int NV, bool SUM>
 __global__ __launch_bounds__(256) void preprocess_backward_kernel(
     const CamArg<NV> cams, const GaussIn in, int g0, int n, const uint32_t* __restrict__ depth_key,
     const uint32_t* __restrict__ flags, const float* __restrict__ grad2d, GradOut out, const GradOut scratch,
-    const BandSum bs, RankIn rk) {
+    const BandSum bs) {
     extern __shared__ __attribute__((aligned(16))) float sh_lds[];
     const int o = blockIdx.x * 256 + threadIdx.x;
     const int M3 = in.M_rest * 3;
@@ -526,14 +488,6 @@ __global__ __launch_bounds__(256) void preprocess_backward_kernel(
         if (flags) flags += e0;
         grad2d += e0 * kPart;
         out = view_out(out, scratch, view, (size_t)in.P, M3);
-        if (rk.rank_of) {  // ranks index all V * P entries' rows: only the per-entry arrays move
-            rk.rank_of += e0;
-            rk.rec += 3 * e0;
-        }
-    }
-    if (rk.rank_of) {  // this view's own pixel scale (hw, hh are per camera)
-        rk.hw = 0.5f * (float)cam.width;
-        rk.hh = 0.5f * (float)cam.height;
     }
     const bool stage = in.sh_rest != nullptr && !in.colors;  // block-uniform
     const int rows = n - blockIdx.x * 256 < 256 ? n - blockIdx.x * 256 : 256;
@@ -558,7 +512,7 @@ __global__ __launch_bounds__(256) void preprocess_backward_kernel(
         }
     }
     BwdIn bi{};
-    if (o < n) bi = load_bwd_in<SUM>(in, g0 + o, o, depth_key, flags, grad2d, bs, rk);
+    if (o < n) bi = load_bwd_in<SUM>(in, g0 + o, o, depth_key, flags, grad2d, bs);
     if (stage) {  // coalesced staging of the block's SH-rest rows (see preprocess_kernel)
         if (v4) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces have landed
@@ -585,27 +539,26 @@ __global__ __launch_bounds__(256) void preprocess_backward_kernel(
 }  // namespace
 
 int launch_gather_grad2d(const uint32_t* offsets, const float* partial, const float4* rec, int W, int H,
-                         long long cap, int P, const uint4* rrect, float* grad2d, hipStream_t s, bool raw) {
+                         long long cap, int P, const uint4* rrect, float* grad2d, hipStream_t s) {
     if (P <= 0) return 0;
     const PartLayout pl(cap);
     const char* base = reinterpret_cast<const char*>(partial);
     hipLaunchKernelGGL(gather_grad2d_kernel, dim3(div_up(P, 256)), dim3(256), 0, s, offsets,
                        reinterpret_cast<const float4*>(base + pl.p8), reinterpret_cast<const float*>(base + pl.p1),
                        reinterpret_cast<const uint8_t*>(base + pl.fl), rec, 0.5f * (float)W, 0.5f * (float)H, P,
-                       (uint32_t)cap, rrect, (raw && rrect) ? 1 : 0, grad2d);
+                       (uint32_t)cap, rrect, grad2d);
     return (int)hipGetLastError();
 }
 
 int launch_preprocess_backward(const gsr_camera& cam, const GaussIn& in, int g0, int g1,
                                const uint32_t* depth_key, const uint32_t* flags, const float* grad2d,
-                               const GradOut& out, hipStream_t s, const uint32_t* rank_of, const float4* rec) {
+                               const GradOut& out, hipStream_t s) {
     const int n = g1 - g0;
     if (n <= 0) return 0;
     const size_t lds = (in.sh_rest && !in.colors) ? sizeof(float) * 256 * 3 * in.M_rest : 0;
     const CamArg<1> c1{{cam}};
-    const RankIn rk{rank_of, grad2d, rec, 0.f, 0.f};
     hipLaunchKernelGGL((preprocess_backward_kernel<1, false>), dim3(div_up(n, 256)), dim3(256), lds, s, c1, in, g0,
-                       n, depth_key, flags, grad2d, out, GradOut{}, BandSum{}, rk);
+                       n, depth_key, flags, grad2d, out, GradOut{}, BandSum{});
     return (int)hipGetLastError();
 }
 
@@ -615,22 +568,20 @@ int launch_preprocess_backward_banded(const gsr_camera& cam, const GaussIn& in, 
     const size_t lds = (in.sh_rest && !in.colors) ? sizeof(float) * 256 * 3 * in.M_rest : 0;
     const CamArg<1> c1{{cam}};
     hipLaunchKernelGGL((preprocess_backward_kernel<1, true>), dim3(div_up(in.P, 256)), dim3(256), lds, s, c1, in, 0,
-                       in.P, depth_key, flags, nullptr, out, GradOut{}, bs, RankIn{});
+                       in.P, depth_key, flags, nullptr, out, GradOut{}, bs);
     return (int)hipGetLastError();
 }
 
 int launch_preprocess_backward_views(const gsr_camera* cams, int V, const GaussIn& in, const uint32_t* depth_key,
                                      const uint32_t* flags, const float* grad2d, const GradOut& out,
-                                     const GradOut& scratch, hipStream_t s, const uint32_t* rank_of,
-                                     const float4* rec) {
+                                     const GradOut& scratch, hipStream_t s) {
     if (in.P <= 0 || V <= 0) return 0;
     if (V > kMaxViews) return -1;
     CamArg<kMaxViews> cv{};
     for (int v = 0; v < V; ++v) cv.c[v] = cams[v];
     const size_t lds = (in.sh_rest && !in.colors) ? sizeof(float) * 256 * 3 * in.M_rest : 0;
-    const RankIn rk{rank_of, grad2d, rec, 0.f, 0.f};
     hipLaunchKernelGGL((preprocess_backward_kernel<kMaxViews, false>), dim3(div_up(in.P, 256), V), dim3(256), lds, s,
-                       cv, in, 0, in.P, depth_key, flags, grad2d, out, scratch, BandSum{}, rk);
+                       cv, in, 0, in.P, depth_key, flags, grad2d, out, scratch, BandSum{});
     return (int)hipGetLastError();
 }
 

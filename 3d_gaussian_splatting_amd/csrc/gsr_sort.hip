@@ -563,8 +563,7 @@ __global__ __launch_bounds__(256) void rank_payload_kernel(const uint32_t* __res
                                                            const uint32_t* __restrict__ tiles,
                                                            const uint4* __restrict__ rect, int n,
                                                            uint32_t* __restrict__ rtiles,
-                                                           uint4* __restrict__ rrect, uint32_t* __restrict__ rank_of,
-                                                           uint32_t* __restrict__ bsum) {
+                                                           uint4* __restrict__ rrect, uint32_t* __restrict__ bsum) {
     __shared__ uint32_t wsum[kWaves];
     const int r = blockIdx.x * 256 + threadIdx.x;
     uint32_t nt = 0;
@@ -579,7 +578,6 @@ __global__ __launch_bounds__(256) void rank_payload_kernel(const uint32_t* __res
         }
         rtiles[r] = nt;
         rrect[r] = q;
-        rank_of[g] = (uint32_t)r;
     }
     uint32_t s = nt;
 #pragma unroll
@@ -1012,14 +1010,13 @@ int launch_duplicate(const uint32_t* tiles, uint4* rect, int n, int grid_x, int 
 
 int launch_depth_presort(const uint32_t* depth_key, const uint32_t* tiles, const uint4* rect, int n, uint32_t* dk0,
                          uint32_t* dv0, uint32_t* dk1, uint32_t* dv1, uint32_t* hist, uint32_t* rtiles, uint4* rrect,
-                         uint32_t* rank_of, uint32_t* bsum, uint32_t* total_out, hipStream_t s) {
+                         uint32_t* bsum, uint32_t* total_out, hipStream_t s) {
     if (n <= 0) return (int)hipMemsetAsync(total_out, 0, sizeof(uint32_t), s);
     int which = -1;  // 4 passes of 8 bits: the result lands in (dk1, dv1)
     if (int e = radix_sort(depth_key, nullptr, dk0, dv0, dk1, dv1, n, nullptr, 32, hist, &which, s)) return e;
     const uint32_t* sgid = which == 0 ? dv0 : dv1;
     const int nb = div_up(n, 256);
-    hipLaunchKernelGGL(rank_payload_kernel, dim3(nb), dim3(256), 0, s, sgid, tiles, rect, n, rtiles, rrect, rank_of,
-                       bsum);
+    hipLaunchKernelGGL(rank_payload_kernel, dim3(nb), dim3(256), 0, s, sgid, tiles, rect, n, rtiles, rrect, bsum);
     // the 256-rank blocks' exclusive offsets and K: F3 (launch_duplicate_ranked) scans inside them
     hipLaunchKernelGGL(scan_partials, dim3(1), dim3(1024), 0, s, bsum, nb, total_out);
     return (int)hipGetLastError();
