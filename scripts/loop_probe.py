@@ -5,6 +5,7 @@ configs[4] test (tests/test_gpu_train_loop.py::test_configs4_at_scale): point co
 
 usage: python scripts/loop_probe.py OUT.bin [--gt N] [--init N] [--size WxH] [--views V]
                                     [--iters N] [--texture T] [--gt-scale S] [--progress N]
+                                    [--reset-interval N] [--densify-until N]
 """
 import argparse
 import importlib
@@ -28,6 +29,8 @@ def main():
     ap.add_argument("--texture", type=float, default=1.0)
     ap.add_argument("--gt-scale", type=float, default=0.012)
     ap.add_argument("--progress", type=int, default=1000)
+    ap.add_argument("--reset-interval", type=int, default=3000, help="opacity_reset_interval")
+    ap.add_argument("--densify-until", type=int, default=15000, help="densify_until_iter")
     a = ap.parse_args()
     L = importlib.import_module(f"{PKG}.train_loop")
     T = importlib.import_module(f"{PKG}.trainer")
@@ -35,7 +38,8 @@ def main():
     t0 = time.perf_counter()
     scene = L.synthetic_scene(a.gt, a.init, a.views, W, H, seed=0, texture=a.texture, gt_scale=a.gt_scale)
     t1 = time.perf_counter()
-    L.write_scene(a.out, scene, a.iters, T.OptimizationParams(iterations=a.iters), max_sh_degree=3,
+    L.write_scene(a.out, scene, a.iters, T.OptimizationParams(iterations=a.iters, opacity_reset_interval=a.reset_interval,
+                                       densify_until_iter=a.densify_until), max_sh_degree=3,
                   log_every=500, progress_every=a.progress)
     print(f"scene {a.gt} gt / {a.init} init, {a.views} views {W}x{H}: built {t1 - t0:.1f} s, "
           f"written {time.perf_counter() - t1:.1f} s -> {a.out}", flush=True)
