@@ -160,6 +160,12 @@ __device__ __forceinline__ float pair_alpha_keep(float e, float L, float& oG, bo
 // T - alpha T (the reference's T (1 - alpha), one op shorter) is >= 1e-4; otherwise the pixel
 // terminates with T unchanged (SURVEY B.3 / forward.cu renderCUDA).  The exponent is
 // Horner-form: ((c' dy + b' dx) dy) + (a' dx^2 + log2 o), 3 ops per stripe with dy.
+#ifndef GSR_F6_PREFETCH
+#define GSR_F6_PREFETCH 0
+#endif
+#ifndef GSR_F6_ONESYNC
+#define GSR_F6_ONESYNC 0
+#endif
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom geo,
                                                                 const uint2* __restrict__ ranges,
@@ -217,15 +223,50 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
             if (lane == 0) ckm[4 * (size_t)slot + w * PPL + p] = on ? 1 : 0;
         }
     };
+#if GSR_F6_PREFETCH
+    // software-pipelined batch loads: the records of the batch at `base` were loaded during the
+    // previous batch, and the gids one batch further, so the gid -> record chain of a batch
+    // overlaps the blending of the one before it (deep lists whose records are mostly culled
+    // are bound by that chain, not by the blend)
+    float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0, q2 = q0;
+    uint32_t gnx = 0;
+    if (tid < n) {
+        const float4* r = rec + 3 * (size_t)sorted_gid[range.x + tid];
+        q0 = r[0];
+        q1 = r[1];
+        q2 = r[2];
+    }
+    if (BATCH + tid < n) gnx = sorted_gid[range.x + BATCH + tid];
+#endif
     for (int base = 0; base < n; base += BATCH) {
         uint32_t live = 0;
 #pragma unroll
         for (int p = 0; p < PPL; ++p) live |= __any(T[p] > 0.0f) ? (1u << p) : 0u;
         if (lane == 0) slive[w] = live << (w * PPL);
+#if !GSR_F6_ONESYNC
         if (__syncthreads_or(live != 0) == 0) {
             tend = base;
             break;
         }
+#endif
+#if GSR_F6_PREFETCH
+        if (base + tid < n) {
+            srec[3 * tid + 0] = q0;
+            srec[3 * tid + 1] = q1;
+            srec[3 * tid + 2] = q2;
+            smk[tid] = stripe_mask(q0, q1, q2, bx0, by0);
+            mk[range.x + base + tid] = (uint8_t)smk[tid];
+        } else {
+            smk[tid] = 0u;
+        }
+        if (base + BATCH + tid < n) {
+            const float4* r = rec + 3 * (size_t)gnx;
+            q0 = r[0];
+            q1 = r[1];
+            q2 = r[2];
+        }
+        if (base + 2 * BATCH + tid < n) gnx = sorted_gid[range.x + base + 2 * BATCH + tid];
+#else
         if (base + tid < n) {
             const uint32_t g = sorted_gid[range.x + base + tid];
             const float4* r = rec + 3 * (size_t)g;
@@ -238,10 +279,20 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
         } else {
             smk[tid] = 0u;
         }
+#endif
         __syncthreads();
         uint32_t tile_live = 0;
 #pragma unroll
         for (int i = 0; i < NW; ++i) tile_live |= slive[i];
+#if GSR_F6_ONESYNC
+        // termination from the batch barrier's own slive words (__syncthreads_or is three
+        // barriers); the batch just loaded is then discarded, and its mask bytes lie at or past
+        // tend, where B1 never reads
+        if (tile_live == 0) {
+            tend = base;
+            break;
+        }
+#endif
         const int cnt = (n - base) < BATCH ? (n - base) : BATCH;
         int visited = 0;
         for (int c0 = 0; c0 < cnt; c0 += 64) {
