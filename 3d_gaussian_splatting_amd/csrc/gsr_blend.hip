@@ -485,6 +485,10 @@ __device__ __forceinline__ void park_flush(const float* qpark, const uint32_t* s
 // chunk-major, so every tile's first chunk is dispatched first.
 // 6 waves per SIMD: 80 VGPRs (no spills) and 6.2 KB of LDS per one-wave block.  Measured
 // 0.552 ms vs 0.564 at the compiler's own 85 VGPRs (5 waves); 7 and 8 waves spill.
+// Mask bytes per lane in one batch window (4: 256 entries per window; 16: 1024, for lists whose
+// entries are mostly culled, e.g. after an opacity reset -- fewer serial window loads).
+constexpr int kB1Win = GSR_B1_WIN;
+static_assert(kB1Win == 4 || kB1Win == 16, "B1 window: 4 or 16 mask bytes per lane");
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void blend_backward_kernel(const BlendGeom geo,
                                                             const uint2* __restrict__ ranges,
                                                             const uint32_t* __restrict__ sorted_gid,
@@ -594,13 +598,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
         // the batch: up to 64 entries with a live stripe among the next 256 (four mask bytes
         // per lane from one aligned word), in list order; the next batch starts after the last
         // one taken, or after the window
-        const uint32_t a0 = (range.x + (uint32_t)base) & ~3u;  // word-aligned window start
-        const uint32_t w4 = *reinterpret_cast<const uint32_t*>(mk + a0 + 4 * lane);
+        constexpr int kW = kB1Win / 4;  // mask words per lane
+        const uint32_t a0 = (range.x + (uint32_t)base) & ~(uint32_t)(kB1Win - 1);  // aligned window start
+        uint32_t wd[kW];
+        if constexpr (kW == 4) {
+            const uint4 v = *reinterpret_cast<const uint4*>(mk + a0 + kB1Win * lane);
+            wd[0] = v.x, wd[1] = v.y, wd[2] = v.z, wd[3] = v.w;
+        } else {
+            wd[0] = *reinterpret_cast<const uint32_t*>(mk + a0 + 4 * lane);
+        }
         uint32_t vis = 0;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int e = (int)(a0 + 4 * lane + i - range.x);  // list offset of byte i
-            const uint32_t m = (w4 >> (8 * i)) & 0xFu;
+        for (int i = 0; i < kB1Win; ++i) {
+            const int e = (int)(a0 + kB1Win * lane + i - range.x);  // list offset of byte i
+            const uint32_t m = (wd[i >> 2] >> (8 * (i & 3))) & 0xFu;
             if (e >= base && e < n_lim && (m & live)) vis |= 1u << i;
         }
         const uint32_t c = (uint32_t)__popc(vis);
@@ -615,18 +626,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
         const int cnt = total < 64u ? (int)total : 64;
         uint32_t pos = excl;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < kB1Win; ++i) {
             if ((vis >> i) & 1u) {
                 if (pos < 64u) {
-                    lds.sidx[pos] = a0 + 4 * lane + i - range.x;
-                    lds.smv[pos] = (w4 >> (8 * i)) & 0xFu;
+                    lds.sidx[pos] = a0 + kB1Win * lane + i - range.x;
+                    lds.smv[pos] = (wd[i >> 2] >> (8 * (i & 3))) & 0xFu;
                 }
                 ++pos;
             }
         }
         __syncthreads();
         // next window: after the 64th taken entry when the window held more, else past it
-        base = total > 64u ? (int)lds.sidx[63] + 1 : (int)(a0 + 256 - range.x);
+        base = total > 64u ? (int)lds.sidx[63] + 1 : (int)(a0 + 64 * kB1Win - range.x);
         if (cnt == 0) {
             __syncthreads();
             continue;

@@ -111,7 +111,11 @@ struct GeomLayout {
 #ifndef GSR_MAX_CHUNKS
 #define GSR_MAX_CHUNKS 32
 #endif
-constexpr int kMaxChunks = GSR_MAX_CHUNKS;  // = GSR_TERM_STRIDE (gsr.h) in the shipped build
+constexpr int kMaxChunks = GSR_MAX_CHUNKS;
+// B1 batch window: mask bytes per lane (gsr_blend.hip)
+#ifndef GSR_B1_WIN
+#define GSR_B1_WIN 4
+#endif  // = GSR_TERM_STRIDE (gsr.h) in the shipped build
 
 // Checkpoint slots.  A checkpoint is 4 KB (float4 (T, C) per pixel of a tile).  A chunk opens
 // only after kChunkWork visited (record, stripe) pairs and a record has at most 4 stripes, so a
@@ -161,7 +165,7 @@ struct BinLayout {
         ckm = take(ck_slots * 4);
         // F6's stripe mask of every list entry it loads (one byte each), from which B1 picks the
         // entries it has to visit before loading any record (+ B1's 256-entry window past the end)
-        mk = take(n + 256);
+        mk = take(n + 64 * GSR_B1_WIN);  // B1 reads whole windows of 64 * GSR_B1_WIN bytes
         total = o;
     }
 };
