@@ -164,7 +164,10 @@ __device__ __forceinline__ float pair_alpha_keep(float e, float L, float& oG, bo
 #define GSR_F6_PREFETCH 0
 #endif
 #ifndef GSR_F6_ONESYNC
-#define GSR_F6_ONESYNC 0
+#define GSR_F6_ONESYNC 1
+#endif
+#ifndef GSR_CK_MERGE
+#define GSR_CK_MERGE 1
 #endif
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom geo,
@@ -223,6 +226,39 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
             if (lane == 0) ckm[4 * (size_t)slot + w * PPL + p] = on ? 1 : 0;
         }
     };
+#if GSR_CK_MERGE
+    // Chunk merging.  When all kMaxChunks - 1 chunk starts are taken and the current chunk is
+    // full, neighbouring chunks are merged pairwise (the even starts are kept: chunk k of the
+    // merged table is chunk 2k of the old one, its checkpoint moved to slot k) and the quota
+    // doubles, so B1's chunks stay within ~2x of each other in work however long the list --
+    // without it the last chunk of a deep tile takes all the remaining work (after an opacity
+    // reset nothing terminates: 624 of 4160 tiles at 6M / 1280x832 had a 50k-entry last chunk,
+    // B1 7.9 ms of a 15.6 ms iteration).  Each thread moves exactly the checkpoint words it
+    // wrote (same index map as `checkpoint`), and slot k is read (as the source of k / 2)
+    // before it is overwritten, so the moves need no barrier.
+    int quota = kCW;
+    auto merge_chunks = [&]() {
+        constexpr int kKeep = (kMaxChunks - 1) / 2;
+        // a tile's chunk slots are consecutive in both layouts: chunk c at ck_slot_of(.., 1) + c - 1
+        float4* const ckt = ck + ck_slot_of(geo.ck_fixed, range.x, tl, 1) * 256 - 256;
+        uint8_t* const ckmt = ckm + (ck_slot_of(geo.ck_fixed, range.x, tl, 1) - 1) * 4;
+#pragma unroll 1
+        for (int k = 1; k <= kKeep; ++k) {
+#pragma unroll 1
+            for (int p = 0; p < PPL; ++p) {
+                const int i = 64 * (w * PPL + p) + lane;
+                ckt[256 * k + i] = ckt[512 * k + i];
+                if (lane == 0) ckmt[4 * k + w * PPL + p] = ckmt[8 * k + w * PPL + p];
+            }
+            if (tid == 0) table[k] = table[2 * k];
+        }
+        nck = kKeep;
+        work += quota;  // the merged current chunk: old chunk 2 kKeep (>= one quota) + the open one
+        quota *= 2;
+    };
+#else
+    constexpr int quota = kCW;
+#endif
 #if GSR_F6_PREFETCH
     // software-pipelined batch loads: the records of the batch at `base` were loaded during the
     // previous batch, and the gids one batch further, so the gid -> record chain of a batch
@@ -297,7 +333,7 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
         int visited = 0;
         for (int c0 = 0; c0 < cnt; c0 += 64) {
             const uint32_t sm = smk[c0 + lane];  // 0 past cnt
-            if (work >= kCW && nck < kMaxChunks - 1) {  // chunk nck + 1 starts at base + c0
+            if (work >= quota && nck < kMaxChunks - 1) {  // chunk nck + 1 starts at base + c0
                 ++nck;
                 checkpoint(ck_slot_of(geo.ck_fixed, range.x, tl, nck), live);
                 if (tid == 0) table[nck] = (uint32_t)(base + c0);
@@ -401,6 +437,11 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
                 }
             }
         }
+#if GSR_CK_MERGE
+        // (at the batch end, where the blend's temporaries are dead; the next chunk then opens
+        // at the next batch's first group)
+        if (work >= quota && nck == kMaxChunks - 1) merge_chunks();
+#endif
         __syncthreads();
     }
     if (tid == 0) {

@@ -557,12 +557,15 @@ def test_chunk_checkpoints_with_finished_stripes(W, H, P_back, rast, oracle):
     assert max(v[0] for v in worst.values()) <= 2e-3, worst
 
 
-@pytest.mark.parametrize("P", [1000, 2000])
+@pytest.mark.parametrize("P", [1000, 2000, 6000])
 def test_checkpoint_slots_deep_lists(P, rast, oracle):
     """Tiles whose ~P faint, wide records never terminate open chunks up to the slot bound
     (n / 48 per tile): P = 1000 runs the start-indexed slots near their bound (~20 chunks per
-    tile), P = 2000 (> 31 * 48 per tile) the fixed 31-per-tile layout.  Every opened chunk has
-    its own slot, and the image and every gradient match the oracle."""
+    tile), P = 2000 (> 31 * 48 per tile) the fixed 31-per-tile layout.  P = 2000 and 6000 need
+    more than 31 chunks of the base quota, so F6 merges neighbouring chunks (their checkpoints
+    moved, the quota doubled) once or more: the chunks must stay balanced -- no last chunk
+    holding the rest of the list.  Every opened chunk has its own slot, and the image and every
+    gradient match the oracle."""
     gr, sc = pkg("graphics"), pkg("scene")
     native = pkg("native")
     cam = gr.synthetic_camera(64, 64)
@@ -572,14 +575,14 @@ def test_checkpoint_slots_deep_lists(P, rast, oracle):
     xy = rng.uniform(-0.4, 0.4, (P, 2)) * z[:, None] * np.array([cam.tanfovx, cam.tanfovy])
     s.means3D = np.concatenate([xy, z[:, None]], 1).astype(np.float32)
     s.scales = np.full((P, 3), 6.0, np.float32)  # sigma 40-80 px: every stripe of every tile
-    s.opacities = np.full((P, 1), 0.006 if P == 1000 else 0.005, np.float32)  # deep, faint lists
+    s.opacities = np.full((P, 1), {1000: 0.006, 2000: 0.005, 6000: 0.0045}[P], np.float32)  # deep, faint lists
     args = (cam, s.means3D, s.opacities, s.scales, s.rotations, s.sh_dc, s.sh_rest)
     st = rast.forward(*args, sh_degree=1)
     f = oracle.forward(*args, sh_degree=1)
     tiles, S = cam.grid[0] * cam.grid[1], native.TERM_STRIDE
     pool = int(native.load_hip().gsr_ck_pool_slots(st.buffers.capacity, cam.width, cam.height))
     fixed = pool == tiles * (S - 1)
-    assert fixed == (P == 2000)
+    assert fixed == (P >= 2000)
     term = _np(st.view(native.VIEW_TERM, torch.int32, tiles * S)).view(np.uint32).reshape(tiles, S)
     rng_t = _np(st.view(native.VIEW_RANGES, torch.int32, 2 * tiles)).view(np.uint32).reshape(tiles, 2)
     opened = term[:, 1:] != 0xFFFFFFFF
@@ -588,4 +591,12 @@ def test_checkpoint_slots_deep_lists(P, rast, oracle):
     assert np.all(opened.sum(1) <= np.minimum(S - 1, n // native.CK_DIV))  # the slot bound holds
     ids = np.array([native.ck_slot(fixed, int(rng_t[t, 0]), t, c + 1) for t, c in zip(*np.nonzero(opened))])
     assert len(np.unique(ids)) == len(ids) and ids.max() < pool
+    # chunks in list order, and balanced: the longest (in entries, up to the termination index)
+    # within 4x of the median -- without merging, P = 2000 leaves ~10x in the last chunk
+    tend = np.minimum(term[:, 0], n)
+    for t in np.nonzero(opened.sum(1) >= 15)[0]:
+        starts = term[t, 1:][opened[t]].astype(np.int64)
+        assert np.all(np.diff(starts) > 0) and opened[t, :len(starts)].all()
+        lens = np.diff(np.concatenate([[0], starts, [int(tend[t])]]))
+        assert lens.max() <= 4 * np.median(lens), (t, lens)
     _compare(st, f, sc.make_dL_dpix(cam, seed=72), rast)
