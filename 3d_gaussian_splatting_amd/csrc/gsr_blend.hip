@@ -333,6 +333,11 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
         int visited = 0;
         for (int c0 = 0; c0 < cnt; c0 += 64) {
             const uint32_t sm = smk[c0 + lane];  // 0 past cnt
+#if GSR_CK_MERGE
+            // at the group boundary itself (not the batch end), so that the chunking does not
+            // depend on the batch size: NW = 2 and 4 (full image / band launches) chunk alike
+            if (work >= quota && nck == kMaxChunks - 1) merge_chunks();
+#endif
             if (work >= quota && nck < kMaxChunks - 1) {  // chunk nck + 1 starts at base + c0
                 ++nck;
                 checkpoint(ck_slot_of(geo.ck_fixed, range.x, tl, nck), live);
@@ -437,11 +442,6 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
                 }
             }
         }
-#if GSR_CK_MERGE
-        // (at the batch end, where the blend's temporaries are dead; the next chunk then opens
-        // at the next batch's first group)
-        if (work >= quota && nck == kMaxChunks - 1) merge_chunks();
-#endif
         __syncthreads();
     }
     if (tid == 0) {
