@@ -2,7 +2,7 @@
 # round 4, GPU call 17: F6 chunk merging (+ the one-barrier termination) in the in-tree library --
 # parity (incl. the deep-list checkpoint tests that now merge), the after-reset per-tile stats,
 # the post-reset loop A/B against `old` (neither) and `nomerge` (one-barrier termination only),
-# and the 1M / 5M bench A/B
+# and the 1M / 5M bench A/B; f6w4: four-wave F6 on every launch (deep lists)
 set -u
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r04_17
@@ -15,11 +15,11 @@ grep -q " passed" $O/parity.log && ! grep -q "failed" $O/parity.log || exit 1
 timeout -k 10 300 python -u scripts/deep_list_stats.py > $O/deep_list_stats.jsonl 2> $O/deep_list_stats.err
 rc=$?; [ $rc -le 1 ] || exit $rc
 timeout -k 10 300 python scripts/loop_probe.py /tmp/loop6m_reset.bin --gt 8000000 --init 6000000 --views 48 --iters 1200 --progress 100 --reset-interval 200 --densify-until 250 > $O/probe_write.log 2>&1 || exit 1
-for v in old nomerge base old base; do
+for v in old nomerge f6w4 base old base; do
   if [ $v = base ]; then LP=""; else LP=$R/3d_gaussian_splatting_amd/lib/variants/$v; fi
   LD_LIBRARY_PATH=$LP${LD_LIBRARY_PATH:+:$LD_LIBRARY_PATH} timeout -k 10 150 $EXE /tmp/loop6m_reset.bin $O/loop_$v.json > $O/loop_$v.log 2>&1 || { rc=$?; rm -f /tmp/loop6m_reset.bin; exit $rc; }
   python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['iters_per_s'], d['final_points'], d['binning_overflows'])" $O/loop_$v.json $v >> $O/loop_ab.txt
 done
 rm -f /tmp/loop6m_reset.bin
-timeout -k 10 300 bash scripts/ab.sh $O/ab_1m.jsonl 2 old nomerge || exit 1
-AB_CONFIG=5m_1080p timeout -k 10 300 bash scripts/ab.sh $O/ab_5m.jsonl 1 old
+timeout -k 10 300 bash scripts/ab.sh $O/ab_1m.jsonl 2 old nomerge f6w4 || exit 1
+AB_CONFIG=5m_1080p timeout -k 10 300 bash scripts/ab.sh $O/ab_5m.jsonl 1 old f6w4

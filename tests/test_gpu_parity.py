@@ -591,12 +591,13 @@ def test_checkpoint_slots_deep_lists(P, rast, oracle):
     assert np.all(opened.sum(1) <= np.minimum(S - 1, n // native.CK_DIV))  # the slot bound holds
     ids = np.array([native.ck_slot(fixed, int(rng_t[t, 0]), t, c + 1) for t, c in zip(*np.nonzero(opened))])
     assert len(np.unique(ids)) == len(ids) and ids.max() < pool
-    # chunks in list order, and balanced: the longest (in entries, up to the termination index)
-    # within 4x of the median -- without merging, P = 2000 leaves ~10x in the last chunk
+    # chunks in list order, none holding the rest of a deep list: chunks are cut by B1 work
+    # (pairs), which falls along the list as stripes finish, so entries per chunk grow toward
+    # the end; without merging, P = 6000 leaves ~2/3 of a tile's list in its 31st chunk
     tend = np.minimum(term[:, 0], n)
     for t in np.nonzero(opened.sum(1) >= 15)[0]:
         starts = term[t, 1:][opened[t]].astype(np.int64)
         assert np.all(np.diff(starts) > 0) and opened[t, :len(starts)].all()
         lens = np.diff(np.concatenate([[0], starts, [int(tend[t])]]))
-        assert lens.max() <= 4 * np.median(lens), (t, lens)
+        assert lens.max() <= tend[t] / 4, (t, lens)
     _compare(st, f, sc.make_dL_dpix(cam, seed=72), rast)
