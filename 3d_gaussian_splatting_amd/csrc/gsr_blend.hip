@@ -160,14 +160,14 @@ __device__ __forceinline__ float pair_alpha_keep(float e, float L, float& oG, bo
 // T - alpha T (the reference's T (1 - alpha), one op shorter) is >= 1e-4; otherwise the pixel
 // terminates with T unchanged (SURVEY B.3 / forward.cu renderCUDA).  The exponent is
 // Horner-form: ((c' dy + b' dx) dy) + (a' dx^2 + log2 o), 3 ops per stripe with dy.
-#ifndef GSR_F6_PREFETCH
-#define GSR_F6_PREFETCH 0
-#endif
 #ifndef GSR_F6_ONESYNC
 #define GSR_F6_ONESYNC 1
 #endif
 #ifndef GSR_CK_MERGE
 #define GSR_CK_MERGE 1
+#endif
+#ifndef GSR_F6_BATCH4
+#define GSR_F6_BATCH4 256
 #endif
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom geo,
@@ -181,7 +181,10 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
                                                                 float4* __restrict__ ck,
                                                                 uint8_t* __restrict__ mk) {
     constexpr int PPL = kPPL / NW;
-    constexpr int BATCH = 64 * NW;
+    // records per batch: one per thread, or (GSR_F6_BATCH4 = 128) four waves sharing the two-wave
+    // kernel's 128-record batches -- the same live-stripe refresh points, so the same chunks
+    constexpr int BATCH = NW > 2 ? GSR_F6_BATCH4 : 64 * NW;
+    static_assert(BATCH % 64 == 0 && BATCH <= 64 * NW, "F6 batch");
     constexpr int kCW = NW > 2 ? kBandChunkWork : kChunkWork;
     __shared__ float4 srec[BATCH * 3];
     __shared__ uint32_t smk[BATCH];
@@ -259,21 +262,6 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
 #else
     constexpr int quota = kCW;
 #endif
-#if GSR_F6_PREFETCH
-    // software-pipelined batch loads: the records of the batch at `base` were loaded during the
-    // previous batch, and the gids one batch further, so the gid -> record chain of a batch
-    // overlaps the blending of the one before it (deep lists whose records are mostly culled
-    // are bound by that chain, not by the blend)
-    float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0, q2 = q0;
-    uint32_t gnx = 0;
-    if (tid < n) {
-        const float4* r = rec + 3 * (size_t)sorted_gid[range.x + tid];
-        q0 = r[0];
-        q1 = r[1];
-        q2 = r[2];
-    }
-    if (BATCH + tid < n) gnx = sorted_gid[range.x + BATCH + tid];
-#endif
     for (int base = 0; base < n; base += BATCH) {
         uint32_t live = 0;
 #pragma unroll
@@ -285,25 +273,7 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
             break;
         }
 #endif
-#if GSR_F6_PREFETCH
-        if (base + tid < n) {
-            srec[3 * tid + 0] = q0;
-            srec[3 * tid + 1] = q1;
-            srec[3 * tid + 2] = q2;
-            smk[tid] = stripe_mask(q0, q1, q2, bx0, by0);
-            mk[range.x + base + tid] = (uint8_t)smk[tid];
-        } else {
-            smk[tid] = 0u;
-        }
-        if (base + BATCH + tid < n) {
-            const float4* r = rec + 3 * (size_t)gnx;
-            q0 = r[0];
-            q1 = r[1];
-            q2 = r[2];
-        }
-        if (base + 2 * BATCH + tid < n) gnx = sorted_gid[range.x + base + 2 * BATCH + tid];
-#else
-        if (base + tid < n) {
+        if (tid < BATCH && base + tid < n) {
             const uint32_t g = sorted_gid[range.x + base + tid];
             const float4* r = rec + 3 * (size_t)g;
             const float4 r0 = r[0], r1 = r[1], r2 = r[2];
@@ -312,10 +282,9 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
             srec[3 * tid + 2] = r2;
             smk[tid] = stripe_mask(r0, r1, r2, bx0, by0);
             mk[range.x + base + tid] = (uint8_t)smk[tid];  // B1's visit filter
-        } else {
+        } else if (tid < BATCH) {
             smk[tid] = 0u;
         }
-#endif
         __syncthreads();
         uint32_t tile_live = 0;
 #pragma unroll
@@ -334,9 +303,9 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
         for (int c0 = 0; c0 < cnt; c0 += 64) {
             const uint32_t sm = smk[c0 + lane];  // 0 past cnt
 #if GSR_CK_MERGE
-            // at the group boundary itself (not the batch end), so that the chunking does not
-            // depend on the batch size: NW = 2 and 4 (full image / band launches) chunk alike
-            if (work >= quota && nck == kMaxChunks - 1) merge_chunks();
+            // at the group boundary itself, not at the batch end: the chunk starts stay where the
+            // unmerged table would put them, whatever the batch size
+            if (__builtin_expect(work >= quota && nck == kMaxChunks - 1, 0)) merge_chunks();
 #endif
             if (work >= quota && nck < kMaxChunks - 1) {  // chunk nck + 1 starts at base + c0
                 ++nck;
