@@ -166,6 +166,9 @@ __device__ __forceinline__ float pair_alpha_keep(float e, float L, float& oG, bo
 #ifndef GSR_CK_MERGE
 #define GSR_CK_MERGE 1
 #endif
+#ifndef GSR_CK_MERGE_BATCH_END
+#define GSR_CK_MERGE_BATCH_END 0
+#endif
 #ifndef GSR_F6_BATCH4
 #define GSR_F6_BATCH4 256
 #endif
@@ -302,9 +305,8 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
         int visited = 0;
         for (int c0 = 0; c0 < cnt; c0 += 64) {
             const uint32_t sm = smk[c0 + lane];  // 0 past cnt
-#if GSR_CK_MERGE
-            // at the group boundary itself, not at the batch end: the chunk starts stay where the
-            // unmerged table would put them, whatever the batch size
+#if GSR_CK_MERGE && !GSR_CK_MERGE_BATCH_END
+            // at the group boundary where a 32nd chunk would open
             if (__builtin_expect(work >= quota && nck == kMaxChunks - 1, 0)) merge_chunks();
 #endif
             if (work >= quota && nck < kMaxChunks - 1) {  // chunk nck + 1 starts at base + c0
@@ -411,6 +413,10 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
                 }
             }
         }
+#if GSR_CK_MERGE && GSR_CK_MERGE_BATCH_END
+        // at the end of the batch in which the last start was taken (outside the blend loop)
+        if (nck == kMaxChunks - 1) merge_chunks();
+#endif
         __syncthreads();
     }
     if (tid == 0) {
