@@ -7,7 +7,7 @@ O=$R/gpurun_out/r04_15
 mkdir -p $O
 cd $R
 export TMPDIR=/tmp
-timeout -k 10 900 bash scripts/profile_round.sh r04_prof > $O/profile.log 2>&1 || exit 1
+timeout -k 10 900 bash scripts/profile_round.sh r04_prof2 > $O/profile.log 2>&1 || exit 1
 timeout -k 10 300 python bench.py > $O/bench_head.json 2> $O/bench_head.err || exit 1
 timeout -k 10 200 python bench.py --config 5m_1080p --no-cpu-baseline > $O/bench_5m.json 2> $O/bench_5m.err || exit 1
 timeout -k 10 200 python bench.py --mode train --no-cpu-baseline > $O/bench_train.json 2> $O/bench_train.err || exit 1
