@@ -195,16 +195,28 @@ class ShardStep:
     wait per step).  Each rank checks its own counts: a rank that overflowed raises, the
     others see the error through the collective that the raising rank no longer joins, so
     re-planning is a job restart (or a caller-level agreement) rather than a silent
-    divergence."""
+    divergence.
+
+    Moving cameras (training): ``set_camera`` renders from another view (same image size) from
+    the next step on, and ``rebalance_every`` = M > 0 re-plans before every M-th step -- the
+    row histogram, band cuts and capacities of the camera then in use (a collective every rank
+    takes at the same step count, after the pending count checks under the old plan).  The
+    reference's loop changes camera every iteration (train_utils.cpp:128-145), so a plan made
+    once for the first camera drifts out of balance; M trades the probe's cost (two headers-only
+    shard forwards, two all-reduces, one host wait) against that drift."""
 
     def __init__(self, rast, cam, inputs: dict, sh_degree: int, dist, group=None, headroom: float = 1.25,
-                 strict: bool = False):
+                 strict: bool = False, rebalance_every: int = 0):
         self.rast, self.cam, self.dist, self.group = rast, cam, dist, group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.D = sh_degree
         self.headroom = headroom
         self.strict = strict
+        if rebalance_every < 0:
+            raise ValueError("rebalance_every must be >= 0")
+        self.rebalance_every = int(rebalance_every)
+        self.replans = 0
         P = int(inputs["means3D"].shape[0])
         self.P = P
         self.g0, self.g1 = gaussian_shard(P, self.world, self.rank)
@@ -245,6 +257,14 @@ class ShardStep:
         self._ring.pending.clear()
         return self
 
+    def set_camera(self, cam):
+        """Render from `cam` from the next step on.  The band cuts and capacities stay those of the
+        last plan until the next re-plan (``rebalance_every`` or an explicit ``plan()``); a step
+        whose splats or band then exceed them raises ShardOverflowError as usual."""
+        if (cam.width, cam.height) != (self.cam.width, self.cam.height):
+            raise ValueError(f"camera size {cam.width}x{cam.height} != the plan's {self.cam.width}x{self.cam.height}")
+        self.cam = cam
+
     @property
     def band(self) -> tuple[int, int]:
         return self.rows[self.rank], self.rows[self.rank + 1]
@@ -266,6 +286,10 @@ class ShardStep:
         ShardOverflowError for an earlier step found to have overflowed (see the class doc).
         The returned gradients and states live in buffers the next step reuses: consume them
         (e.g. the optimizer step) before calling step() again."""
+        if self.rebalance_every and self.steps and self.steps % self.rebalance_every == 0:
+            self._ring.poll(wait=True)  # the old plan's pending checks first
+            self.plan()
+            self.replans += 1
         self._ring.poll()
         sh, st = self.forward()
         img = ImageGather(st.color, self.rows, self.rank, self.dist, self.group)  # overlaps B1

@@ -449,6 +449,20 @@ void ShardStep::set_pair_cap(int pair_cap) {
     size_buffers();
 }
 
+void ShardStep::set_camera(const RasterCamera& cam) {
+    TORCH_CHECK(cam.width == cam_.width && cam.height == cam_.height,
+                "ShardStep::set_camera: the image size must stay the plan's");
+    cam_ = cam;
+    ccam_ = cam.to_c();
+    drop_graph();  // the captured launches hold the old camera's values
+    for (Arena* a : {&pool_->geom, &pool_->bin, &pool_->img, &pool_->scratch}) a->frozen = false;
+}
+
+void ShardStep::set_rebalance_every(int m) {
+    TORCH_CHECK(m >= 0, "ShardStep: rebalance_every must be >= 0");
+    rebalance_every_ = m;
+}
+
 // One step's work on the current stream (= the Pool's main stream, set by step()).  Called
 // eagerly, or once under stream capture to record the graph that later steps replay.
 void ShardStep::run(const torch::Tensor& dpix) {
@@ -552,6 +566,11 @@ ShardStep::Result ShardStep::step(const torch::Tensor& dL_dpix) {
     TORCH_CHECK(dL_dpix.is_cuda() && dL_dpix.scalar_type() == torch::kFloat32 && dL_dpix.is_contiguous() &&
                     dL_dpix.numel() == (int64_t)3 * cam_.height * cam_.width,
                 "ShardStep: dL_dpix must be a contiguous (3,H,W) f32 device tensor");
+    if (rebalance_every_ > 0 && steps_ > 0 && steps_ % rebalance_every_ == 0) {
+        poll(true);  // the old plan's pending checks first
+        plan();      // drops the graph; this step runs eagerly and captures again
+        ++replans_;
+    }
     poll(false);
     Pool& p = *pool_;
     // the step runs on its own stream (capturable), ordered after / before the caller's
@@ -671,6 +690,9 @@ void bind_shard(py::module& m) {
             py::arg("dL_dpix"))
         .def("check", &ShardStep::check, py::call_guard<py::gil_scoped_release>())
         .def("set_pair_cap", &ShardStep::set_pair_cap)
+        .def("set_camera", &ShardStep::set_camera, py::arg("cam"))
+        .def("set_rebalance_every", &ShardStep::set_rebalance_every, py::arg("m"))
+        .def_property_readonly("replans", &ShardStep::replans)
         .def("band_num_rendered", &ShardStep::band_num_rendered)
         .def_property_readonly("rows", &ShardStep::rows)
         .def_property_readonly("pair_cap", &ShardStep::pair_cap)

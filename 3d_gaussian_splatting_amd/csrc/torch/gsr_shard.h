@@ -127,6 +127,14 @@ class ShardStep {
     int64_t band_num_rendered() const;
     // test hook: force a (smaller) pair capacity after plan()
     void set_pair_cap(int pair_cap);
+    // Moving cameras (training, train_utils.cpp:128-145 picks a view per iteration): render from
+    // `cam` (same size) from the next step on -- a captured graph is dropped and re-captured.
+    // The cuts and capacities stay the last plan's until a re-plan: with rebalance_every = M > 0,
+    // step() re-plans (checks the pending steps, then plan() for the camera in use) before every
+    // M-th step; every rank does so at the same step count.
+    void set_camera(const RasterCamera& cam);
+    void set_rebalance_every(int m);
+    int64_t replans() const { return replans_; }
 
    private:
     struct Pool;  // buffers (stable addresses across steps: graph-replayable), streams, events, graph
@@ -154,6 +162,8 @@ class ShardStep {
     int pair_cap_ = 0, capacity_ = 0;
     std::vector<int64_t> band_k_;
     int64_t steps_ = 0;
+    int rebalance_every_ = 0;
+    int64_t replans_ = 0;
     std::unique_ptr<Pool> pool_;
     // overflow ring: gathered status footers (pinned), checked `lag_` steps later
     struct Pending {

@@ -7,7 +7,9 @@ Checks: the gathered image equals the single-process CAbiRasterize
 bit, the radii too, and the leaf gradients gathered from both shards match within 1e-5
 relative L2 (band-order sums vs the single-GPU emission-order sums).  A second run forces
 pair_cap below the true splat counts: every rank must raise ShardOverflowError (strict mode:
-the count check lands before step() returns) instead of returning the truncated render.
+the count check lands before step() returns) instead of returning the truncated render.  A third
+moves the camera (`set_camera`) with `rebalance_every`: the re-plan before the next step cuts
+the bands for the new view, and that step's image equals the single-GPU render of it.
 """
 import os
 import socket
@@ -42,7 +44,17 @@ def _inputs(dev):
     return cam, inputs, t(sc.make_dL_dpix(cam, seed=52))
 
 
-def _worker(rank, port, outdir, force_pair_cap):
+def _moved_camera():
+    """The synthetic camera shifted 0.8 down in view space: the scene's instances crowd into the
+    image's upper rows, so the balanced cuts move."""
+    import math
+    gr = pkg("graphics")
+    fovx = math.radians(60.0)
+    fovy = 2.0 * math.atan(math.tan(fovx / 2.0) * H / W)
+    return gr.make_camera(np.eye(3), np.array([0.0, 0.8, 0.0]), fovx, fovy, W, H)
+
+
+def _worker(rank, port, outdir, force_pair_cap, move=False):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
@@ -51,7 +63,16 @@ def _worker(rank, port, outdir, force_pair_cap):
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
         cam, inputs, dpix = _inputs(dev)
-        step = bands.ShardStep(R.ShardRasterizer(dev), cam, inputs, 3, dist, strict=True).plan()
+        step = bands.ShardStep(R.ShardRasterizer(dev), cam, inputs, 3, dist, strict=True,
+                               rebalance_every=1 if move else 0).plan()
+        if move:
+            step.step(dpix)  # camera A, the initial plan (no re-plan before the first step)
+            rows_a = np.array(step.rows)
+            step.set_camera(_moved_camera())
+            img, g, sh, st = step.step(dpix)  # re-planned for camera B first
+            np.savez(os.path.join(outdir, f"m{rank}.npz"), image=img.cpu().numpy(), rows_a=rows_a,
+                     rows_b=np.array(step.rows), replans=step.replans, radii=sh.radii.cpu().numpy())
+            return
         if force_pair_cap:
             step.pair_cap = 64
             try:
@@ -70,8 +91,8 @@ def _worker(rank, port, outdir, force_pair_cap):
         dist.destroy_process_group()
 
 
-def _run(force_pair_cap, outdir):
-    mp.start_processes(_worker, args=(_free_port(), outdir, force_pair_cap), nprocs=WORLD, join=True,
+def _run(force_pair_cap, outdir, move=False):
+    mp.start_processes(_worker, args=(_free_port(), outdir, force_pair_cap, move), nprocs=WORLD, join=True,
                        start_method="spawn")
 
 
@@ -104,3 +125,21 @@ def test_two_process_overflow_raises():
             assert os.path.exists(f), f"rank {r} returned a truncated step without raising"
             e = np.load(f)
             assert int(e["step"]) == 0 and int(e["counts"].max()) > int(e["pair_cap"]) == 64
+
+
+def test_two_process_camera_move_rebalances():
+    R = pkg("rasterizer")
+    dev = torch.device("cuda", 0)
+    with tempfile.TemporaryDirectory() as outdir:
+        _run(False, outdir, move=True)
+        got = [dict(np.load(os.path.join(outdir, f"m{r}.npz"))) for r in range(WORLD)]
+    _, inputs, _ = _inputs(dev)
+    cam_b = _moved_camera()
+    full = R.CAbiRasterizer(dev).forward(cam_b, **inputs, sh_degree=3)
+    for r in range(WORLD):
+        assert int(got[r]["replans"]) == 1
+        np.testing.assert_array_equal(got[r]["rows_b"], got[0]["rows_b"])  # every rank cut alike
+        np.testing.assert_array_equal(got[r]["image"], full.color.cpu().numpy())
+    assert not np.array_equal(got[0]["rows_a"], got[0]["rows_b"])  # the cuts followed the view
+    radii = np.concatenate([got[r]["radii"] for r in range(WORLD)])
+    np.testing.assert_array_equal(radii, full.radii.cpu().numpy())

@@ -186,3 +186,40 @@ def test_python_binding_rccl_graph(scene, reference):
     np.testing.assert_array_equal(radii.cpu().numpy(), ref_radii)
     for k, c in GRADS:
         assert rel_l2(grads[k].cpu().numpy().reshape(P, -1)[:, :c], g[k].reshape(P, -1)[:, :c]) <= 1e-5, k
+
+
+def test_python_binding_camera_move_rebalances(scene):
+    """A moving camera through the C++ step: set_camera drops the captured graph, and with
+    rebalance_every = 1 the next step re-plans for the new view first; its image and radii equal
+    the single-GPU render of that view, and later steps replay a graph captured for it."""
+    import math
+    cam, s, dpix = scene
+    ext = pkg("native").load_torch_ext()
+    R, gr = pkg("rasterizer"), pkg("graphics")
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.float32), device=dev)
+    inputs = dict(means3D=t(s.means3D), opacities=t(s.opacities), scales=t(s.scales), rotations=t(s.rotations),
+                  sh_dc=t(s.sh_dc).reshape(P, 1, 3), sh_rest=t(s.sh_rest).reshape(P, -1, 3))
+    ex = ext.rccl_exchange(ext.rccl_unique_id(), 0, 1)
+    st = ext.ShardStep(ex, R.ext_camera(cam), inputs, 3, graph=True)
+    st.plan()
+    d = t(dpix)
+    for _ in range(2):
+        st.step(d)
+    assert st.graph_active
+    cam_b = gr.make_camera(np.eye(3), np.array([0.0, 0.8, 0.0]), 2 * math.atan(cam.tanfovx),
+                           2 * math.atan(cam.tanfovy), cam.width, cam.height)
+    st.set_camera(R.ext_camera(cam_b))
+    assert not st.graph_active
+    st.set_rebalance_every(1)
+    img, _, radii = st.step(d)
+    assert st.replans == 1
+    full = R.CAbiRasterizer(dev).forward(cam_b, **inputs, sh_degree=3)
+    np.testing.assert_array_equal(img.cpu().numpy(), full.color.cpu().numpy())
+    np.testing.assert_array_equal(radii.cpu().numpy(), full.radii.cpu().numpy())
+    st.set_rebalance_every(0)
+    img2, _, _ = st.step(d)
+    img3, _, _ = st.step(d)
+    st.check()
+    assert st.graph_active
+    np.testing.assert_array_equal(img3.cpu().numpy(), full.color.cpu().numpy())
