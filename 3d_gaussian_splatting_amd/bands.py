@@ -81,7 +81,9 @@ class ImageGather:
     own stream while the blend backward runs on the compute stream.  Bands are padded to the
     tallest one so a single all_gather_into_tensor (one RCCL call) moves them."""
 
-    def __init__(self, color: torch.Tensor, rows: list, rank: int, dist, group=None):
+    def __init__(self, color: torch.Tensor, rows: list, rank: int, dist, group=None, status=None):
+        """status: an optional int32 device tensor (this rank's overflow words) that rides in a
+        footer row of the gathered bands, so that every rank sees every rank's words."""
         self.world = len(rows) - 1
         _, self.H, W = color.shape
         self.rows = rows
@@ -89,15 +91,26 @@ class ImageGather:
                                                                                      self.H)[0]
                    for r in range(self.world))
         py0, py1 = band_pixel_rows((rows[rank], rows[rank + 1]), self.H)
-        self.mine = color.new_zeros((3, max(tall, 1), W))
+        self.tall = max(tall, 1)
+        self.S = 0 if status is None else int(status.numel())
+        if self.S > W:
+            raise ValueError(f"{self.S} status words do not fit a {W}-pixel footer row")
+        foot = 1 if self.S else 0
+        self.mine = color.new_zeros((3, self.tall + foot, W))
         self.mine[:, : py1 - py0] = color[:, py0:py1]
-        self.buf = color.new_empty((self.world, 3, max(tall, 1), W))
+        if self.S:  # the words' bits in f32 slots (a view, no conversion)
+            self.mine[0, self.tall, : self.S].view(torch.int32).copy_(status.reshape(-1).to(torch.int32))
+        self.buf = color.new_empty((self.world, 3, self.tall + foot, W))
         if dist.get_backend(group) != "gloo":
             self.work = dist.all_gather_into_tensor(self.buf.view(-1), self.mine.view(-1), group=group,
                                                     async_op=True)
         else:
             self.work = dist.all_gather(list(self.buf.unbind(0)), self.mine, group=group, async_op=True)
         self.color = color
+
+    def statuses(self) -> torch.Tensor:
+        """(world, S) int32 device tensor: every rank's status words (after wait())."""
+        return self.buf[:, 0, self.tall, : self.S].contiguous().view(torch.int32)
 
     def wait(self) -> torch.Tensor:
         self.work.wait()
@@ -129,55 +142,63 @@ class ShardOverflowError(RuntimeError):
     rank packed (against ``pair_cap``) and ``band_k`` its band's instance count (against
     ``capacity``).  Re-plan (``ShardStep.plan``) and re-run from that step."""
 
-    def __init__(self, step: int, counts, pair_cap: int, band_k: int, capacity: int):
+    def __init__(self, step: int, counts, pair_cap: int, band_k: int, capacity: int, rank=None):
         self.step, self.counts, self.pair_cap = step, list(counts), pair_cap
-        self.band_k, self.capacity = band_k, capacity
-        super().__init__(f"multi-GPU step {step} overflowed: splats per band {self.counts} vs pair_cap {pair_cap}, "
-                         f"band instances {band_k} vs capacity {capacity}")
+        self.band_k, self.capacity, self.rank = band_k, capacity, rank
+        who = "" if rank is None else f" on rank {rank}"
+        super().__init__(f"multi-GPU step {step} overflowed{who}: splats per band {self.counts} vs pair_cap "
+                         f"{pair_cap}, band instances {band_k} vs capacity {capacity}")
 
 
 class _CountRing:
-    """Each step's per-band splat counts and band instance count, copied to pinned host memory
-    without waiting; read once the copy's event has completed (one or more steps later)."""
+    """Each step's overflow words of EVERY rank -- per-band splat counts and band instance count,
+    (world, nb + 1) int32, gathered with the band images -- copied to pinned host memory without
+    waiting, and checked a fixed number of steps later (``check_upto``), so that every rank checks
+    the same steps at the same calls and raises for the same step."""
 
     def __init__(self, nb: int, device, ring: int = 4):
-        pin = torch.cuda.is_available() and torch.device(device).type == "cuda"
-        self.slots = [torch.zeros(nb + 1, dtype=torch.int32, pin_memory=pin) for _ in range(ring)]
+        self.pin = torch.cuda.is_available() and torch.device(device).type == "cuda"
+        self.ring = ring
+        self.slots: list = []
         self.pending: list = []  # (step, slot, event or None, pair_cap, capacity)
         self.next = 0
 
-    def push(self, step: int, counts: torch.Tensor, band_k: torch.Tensor, pair_cap: int, capacity: int):
-        """counts: (nb,) int32 device view of the send headers; band_k: (1,) int32 device."""
-        if len(self.pending) == len(self.slots):
-            self.wait_oldest()
+    def push(self, step: int, words: torch.Tensor, pair_cap: int, capacity: int):
+        """words: (world, nb + 1) int32 device tensor (every rank's counts, then its band K)."""
+        if len(self.pending) == self.ring:
+            self.check_upto(self.pending[0][0])  # the oldest, at the same step on every rank
+        if len(self.slots) < self.ring or self.slots[self.next].shape != words.shape:
+            slot = torch.zeros(words.shape, dtype=torch.int32, pin_memory=self.pin)
+            if len(self.slots) < self.ring:
+                self.slots.append(slot)
+            else:
+                self.slots[self.next] = slot
         slot = self.slots[self.next]
-        self.next = (self.next + 1) % len(self.slots)
-        nb = slot.numel() - 1
+        self.next = (self.next + 1) % self.ring
+        slot.copy_(words, non_blocking=True)
         ev = None
-        slot[:nb].copy_(counts.reshape(-1), non_blocking=True)  # two small D2H copies, no kernel
-        slot[nb:].copy_(band_k.reshape(-1), non_blocking=True)
-        if counts.is_cuda:
+        if words.is_cuda:
             ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(counts.device))
+            ev.record(torch.cuda.current_stream(words.device))
         self.pending.append((step, slot, ev, pair_cap, capacity))
 
-    def wait_oldest(self):
-        ev = self.pending[0][2]
-        if ev is not None:
-            ev.synchronize()
-        self.poll()
-
-    def poll(self, wait: bool = False):
-        """Check every completed entry (all of them with wait=True); raise on an overflow."""
-        while self.pending and (wait or self.pending[0][2] is None or self.pending[0][2].query()):
+    def check_upto(self, last_step: int):
+        """Wait for and check every entry up to step `last_step`; raise on an overflow."""
+        while self.pending and self.pending[0][0] <= last_step:
             step, slot, ev, pair_cap, capacity = self.pending.pop(0)
             if ev is not None:
                 ev.synchronize()
-            v = [int(x) & 0xFFFFFFFF for x in slot.tolist()]  # u32 counts
-            counts, band_k = v[:-1], v[-1]
-            if max(counts) > pair_cap or band_k > capacity:
-                self.pending.clear()
-                raise ShardOverflowError(step, counts, pair_cap, band_k, capacity)
+            for r, row in enumerate(slot.tolist()):
+                v = [int(x) & 0xFFFFFFFF for x in row]  # u32 counts
+                counts, band_k = v[:-1], v[-1]
+                if max(counts) > pair_cap or band_k > capacity:
+                    self.pending.clear()
+                    raise ShardOverflowError(step, counts, pair_cap, band_k, capacity, rank=r)
+
+    def poll(self, wait: bool = False):
+        """Check every pending entry (wait is kept for the older call sites: always waits)."""
+        if self.pending:
+            self.check_upto(self.pending[-1][0])
 
 
 class ShardStep:
@@ -188,14 +209,14 @@ class ShardStep:
     from the true counts, each with ``headroom``.
 
     Overflow: a step whose splats exceed ``pair_cap`` (any send block's header count) or whose
-    band holds more instances than ``capacity`` is truncated by the kernels.  Every step's
-    counts are copied to pinned memory without a host wait and checked when the copy has landed
-    -- at the next ``step`` / ``check`` call -- which raises ``ShardOverflowError`` naming the
-    step (``strict=True`` checks every step before returning it, at the cost of one host
-    wait per step).  Each rank checks its own counts: a rank that overflowed raises, the
-    others see the error through the collective that the raising rank no longer joins, so
-    re-planning is a job restart (or a caller-level agreement) rather than a silent
-    divergence.
+    band holds more instances than ``capacity`` is truncated by the kernels.  Every rank's
+    overflow words (its per-band splat counts and band instance count) ride in a footer row of
+    the image all-gather, so every rank holds every rank's; they are copied to pinned memory
+    without a host wait and checked ``lag`` steps later (or by ``check``), at the same call on
+    every rank, so all ranks raise ``ShardOverflowError`` for the same step and none is left
+    blocked in a collective (the C++ ``gsr::ShardStep`` does the same).  ``strict=True`` checks
+    every step before returning it, at the cost of one host wait per step.  The caller
+    re-plans (``plan``) and re-runs from that step.
 
     Moving cameras (training): ``set_camera`` renders from another view (same image size) from
     the next step on, and ``rebalance_every`` = M > 0 re-plans before every M-th step -- the
@@ -206,7 +227,7 @@ class ShardStep:
     shard forwards, two all-reduces, one host wait) against that drift."""
 
     def __init__(self, rast, cam, inputs: dict, sh_degree: int, dist, group=None, headroom: float = 1.25,
-                 strict: bool = False, rebalance_every: int = 0):
+                 strict: bool = False, rebalance_every: int = 0, lag: int = 2):
         self.rast, self.cam, self.dist, self.group = rast, cam, dist, group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -216,6 +237,9 @@ class ShardStep:
         if rebalance_every < 0:
             raise ValueError("rebalance_every must be >= 0")
         self.rebalance_every = int(rebalance_every)
+        if lag < 1:
+            raise ValueError("lag must be >= 1")
+        self.lag = int(lag)
         self.replans = 0
         P = int(inputs["means3D"].shape[0])
         self.P = P
@@ -274,12 +298,11 @@ class ShardStep:
         recv = all_to_all_blocks(sh.send, self.world, self.dist, self.group)
         st = self.rast.band_forward(self.cam, self.band, self.world, self.pair_cap, recv, self.capacity,
                                     reuse=self._reuse["band"])
-        self._ring.push(self.steps, sh.counts, st.k_device(), self.pair_cap, self.capacity)
         return sh, st
 
     def check(self, wait: bool = True):
-        """Raise ShardOverflowError if a finished step overflowed (wait=True: every step so far)."""
-        self._ring.poll(wait=wait)
+        """Raise ShardOverflowError if any rank overflowed in a step so far (waits for them)."""
+        self._ring.poll(wait=True)
 
     def step(self, dL_dpix: torch.Tensor):
         """-> (full image, this shard's leaf gradients, shard state, band state).  Raises
@@ -290,14 +313,18 @@ class ShardStep:
             self._ring.poll(wait=True)  # the old plan's pending checks first
             self.plan()
             self.replans += 1
-        self._ring.poll()
+        # the step `lag` steps back, on every rank at this same call (its words have long landed)
+        self._ring.check_upto(self.steps - self.lag)
         sh, st = self.forward()
-        img = ImageGather(st.color, self.rows, self.rank, self.dist, self.group)  # overlaps B1
+        # this rank's overflow words ride in the image all-gather: every rank checks every rank's
+        words = torch.cat([sh.counts.reshape(-1), st.k_device().reshape(-1)]).to(torch.int32)
+        img = ImageGather(st.color, self.rows, self.rank, self.dist, self.group, status=words)  # overlaps B1
         g2 = self.rast.band_backward(st, self.world, self.pair_cap, dL_dpix, reuse=self._reuse["band"])
         back = all_to_all_blocks(g2, self.world, self.dist, self.group)
         grads = self.rast.shard_backward(sh, back, reuse=self._reuse["grads"])
-        self.steps += 1
         out = img.wait(), grads, sh, st
+        self._ring.push(self.steps, img.statuses(), self.pair_cap, self.capacity)
+        self.steps += 1
         if self.strict:
             self._ring.poll(wait=True)
         return out

@@ -7,7 +7,8 @@ Checks: the gathered image equals the single-process CAbiRasterize
 bit, the radii too, and the leaf gradients gathered from both shards match within 1e-5
 relative L2 (band-order sums vs the single-GPU emission-order sums).  A second run forces
 pair_cap below the true splat counts: every rank must raise ShardOverflowError (strict mode:
-the count check lands before step() returns) instead of returning the truncated render.  A third
+the count check lands before step() returns) instead of returning the truncated render; with only
+rank 0 overflowing and lagged checks, both ranks raise for the same step at the same call.  A third
 moves the camera (`set_camera`) with `rebalance_every`: the re-plan before the next step cuts
 the bands for the new view, and that step's image equals the single-GPU render of it.
 """
@@ -54,7 +55,7 @@ def _moved_camera():
     return gr.make_camera(np.eye(3), np.array([0.0, 0.8, 0.0]), fovx, fovy, W, H)
 
 
-def _worker(rank, port, outdir, force_pair_cap, move=False):
+def _worker(rank, port, outdir, force_pair_cap, move=False, one_rank=False):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
@@ -65,6 +66,18 @@ def _worker(rank, port, outdir, force_pair_cap, move=False):
         cam, inputs, dpix = _inputs(dev)
         step = bands.ShardStep(R.ShardRasterizer(dev), cam, inputs, 3, dist, strict=True,
                                rebalance_every=1 if move else 0).plan()
+        if one_rank:  # only rank 0's band overflows; checks lag two steps, not strict
+            step.strict = False
+            if rank == 0:
+                step.capacity = 1024
+            for i in range(5):
+                try:
+                    step.step(dpix)
+                except bands.ShardOverflowError as e:
+                    np.savez(os.path.join(outdir, f"one{rank}.npz"), call=i, step=e.step, rank=e.rank,
+                             band_k=e.band_k, capacity=e.capacity)
+                    break
+            return
         if move:
             step.step(dpix)  # camera A, the initial plan (no re-plan before the first step)
             rows_a = np.array(step.rows)
@@ -91,9 +104,9 @@ def _worker(rank, port, outdir, force_pair_cap, move=False):
         dist.destroy_process_group()
 
 
-def _run(force_pair_cap, outdir, move=False):
-    mp.start_processes(_worker, args=(_free_port(), outdir, force_pair_cap, move), nprocs=WORLD, join=True,
-                       start_method="spawn")
+def _run(force_pair_cap, outdir, move=False, one_rank=False):
+    mp.start_processes(_worker, args=(_free_port(), outdir, force_pair_cap, move, one_rank), nprocs=WORLD,
+                       join=True, start_method="spawn")
 
 
 def test_two_process_shard_step_matches_single_gpu():
@@ -143,3 +156,20 @@ def test_two_process_camera_move_rebalances():
     assert not np.array_equal(got[0]["rows_a"], got[0]["rows_b"])  # the cuts followed the view
     radii = np.concatenate([got[r]["radii"] for r in range(WORLD)])
     np.testing.assert_array_equal(radii, full.radii.cpu().numpy())
+
+
+def test_two_process_overflow_agreed():
+    """Only rank 0's band overflows (its capacity forced small), checks lagging two steps: both
+    ranks raise ShardOverflowError at the same call, for the same step, naming rank 0 -- the
+    overflow words ride in the image all-gather, so the rank whose own counts are fine is not
+    left blocked in a collective."""
+    with tempfile.TemporaryDirectory() as outdir:
+        _run(False, outdir, one_rank=True)
+        got = []
+        for r in range(WORLD):
+            f = os.path.join(outdir, f"one{r}.npz")
+            assert os.path.exists(f), f"rank {r} never raised"
+            got.append(dict(np.load(f)))
+    for g in got:
+        assert int(g["call"]) == 2 and int(g["step"]) == 0 and int(g["rank"]) == 0
+        assert int(g["band_k"]) > int(g["capacity"]) == 1024

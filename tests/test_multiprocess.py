@@ -109,7 +109,9 @@ def _worker(rank, port, outdir):
         gid = got[:, 0].astype(np.int64)
         assert np.all(np.diff(gid) > 0), "splats must reach the band in ascending global id"
         f = _oracle(cam, _unparams(np.ascontiguousarray(got[:, 1:]), M), band)
-        img = bands.ImageGather(torch.from_numpy(f.color), rows, rank, dist)
+        # the overflow words ride in the gather's footer row: every rank receives every rank's
+        words = torch.tensor([counts[s] for s in range(WORLD)] + [1000 + rank, -1], dtype=torch.int32)
+        img = bands.ImageGather(torch.from_numpy(f.color), rows, rank, dist, status=words)
         # backward: the band's gradient of every received Gaussian, back in the received slot layout
         gb = _grad_rows(f.state.backward(dpix), len(gid))
         G = gb.shape[1]
@@ -123,6 +125,11 @@ def _worker(rank, port, outdir):
         for b in range(WORLD):  # band order: deterministic
             acc[sent[b]] += ret[b, :len(sent[b])]
         full = img.wait()
+        allw = img.statuses()
+        assert allw.dtype == torch.int32 and tuple(allw.shape) == (WORLD, WORLD + 2)
+        assert allw[rank].tolist() == words.tolist()
+        assert [int(allw[r, WORLD]) for r in range(WORLD)] == [1000 + r for r in range(WORLD)]
+        assert all(int(allw[r, WORLD + 1]) == -1 for r in range(WORLD))  # bit-exact through the f32 slots
         parts = [torch.zeros((-(-P // WORLD), G)) for _ in range(WORLD)]
         pad = torch.zeros((-(-P // WORLD), G))
         pad[: g1 - g0] = torch.from_numpy(acc)
