@@ -151,8 +151,9 @@ class ShardOverflowError(RuntimeError):
 
 
 class _CountRing:
-    """Each step's overflow words of EVERY rank -- per-band splat counts and band instance count,
-    (world, nb + 1) int32, gathered with the band images -- copied to pinned host memory without
+    """Each step's overflow words of EVERY rank -- per-band splat counts, band instance count and
+    that rank's two capacities, (world, nb + 3) int32, gathered with the band images -- copied to
+    pinned host memory without
     waiting, and checked a fixed number of steps later (``check_upto``), so that every rank checks
     the same steps at the same calls and raises for the same step."""
 
@@ -164,7 +165,8 @@ class _CountRing:
         self.next = 0
 
     def push(self, step: int, words: torch.Tensor, pair_cap: int, capacity: int):
-        """words: (world, nb + 1) int32 device tensor (every rank's counts, then its band K)."""
+        """words: (world, nb + 3) int32 device tensor: every rank's counts, band K, pair_cap and
+        capacity (each rank is checked against its own)."""
         if len(self.pending) == self.ring:
             self.check_upto(self.pending[0][0])  # the oldest, at the same step on every rank
         if len(self.slots) < self.ring or self.slots[self.next].shape != words.shape:
@@ -189,11 +191,12 @@ class _CountRing:
             if ev is not None:
                 ev.synchronize()
             for r, row in enumerate(slot.tolist()):
-                v = [int(x) & 0xFFFFFFFF for x in row]  # u32 counts
-                counts, band_k = v[:-1], v[-1]
-                if max(counts) > pair_cap or band_k > capacity:
+                # rank r's words: its per-band counts, band K, then ITS pair_cap and capacity
+                v = [int(x) & 0xFFFFFFFF for x in row]  # u32
+                counts, band_k, pc, cap = v[:-3], v[-3], v[-2], v[-1]
+                if max(counts) > pc or band_k > cap:
                     self.pending.clear()
-                    raise ShardOverflowError(step, counts, pair_cap, band_k, capacity, rank=r)
+                    raise ShardOverflowError(step, counts, pc, band_k, cap, rank=r)
 
     def poll(self, wait: bool = False):
         """Check every pending entry (wait is kept for the older call sites: always waits)."""
@@ -317,7 +320,11 @@ class ShardStep:
         self._ring.check_upto(self.steps - self.lag)
         sh, st = self.forward()
         # this rank's overflow words ride in the image all-gather: every rank checks every rank's
-        words = torch.cat([sh.counts.reshape(-1), st.k_device().reshape(-1)]).to(torch.int32)
+        key = (self.pair_cap, self.capacity)
+        if getattr(self, "_caps_key", None) != key:  # a device copy of the capacities, made once per plan
+            self._caps = torch.tensor(list(key), dtype=torch.int32, device=sh.counts.device)
+            self._caps_key = key
+        words = torch.cat([sh.counts.reshape(-1), st.k_device().reshape(-1), self._caps]).to(torch.int32)
         img = ImageGather(st.color, self.rows, self.rank, self.dist, self.group, status=words)  # overlaps B1
         g2 = self.rast.band_backward(st, self.world, self.pair_cap, dL_dpix, reuse=self._reuse["band"])
         back = all_to_all_blocks(g2, self.world, self.dist, self.group)
