@@ -150,6 +150,21 @@ class ShardOverflowError(RuntimeError):
                          f"{pair_cap}, band instances {band_k} vs capacity {capacity}")
 
 
+def overflow_ranks(words: torch.Tensor) -> torch.Tensor:
+    """Device-side agreement word: the number of ranks whose step overflowed, as a (1,) int32
+    tensor on the words' device, computed without a host wait.  `words`: (world, nb + 3) int32,
+    every rank's per-band splat counts, band K, pair_cap and capacity (the gathered footer).
+    Every rank computes it from the same gathered words, so every rank holds the same value: a
+    training loop passes it as the guard of its optimizer step (``gsr_adam_step_guarded`` /
+    ``gsr_densify_stats_guarded`` with guard_cap = 0, trainer.adam_step(guard=(word, 0))) so that
+    a truncated step never updates the model on any rank, the step before the lagged host check
+    raises ShardOverflowError."""
+    v = words.to(torch.int64) & 0xFFFFFFFF  # the kernels' u32 counts
+    counts, band_k, pc, cap = v[:, :-3], v[:, -3], v[:, -2], v[:, -1]
+    bad = (counts > pc[:, None]).any(dim=1) | (band_k > cap)
+    return bad.sum().to(torch.int32).reshape(1)
+
+
 class _CountRing:
     """Each step's overflow words of EVERY rank -- per-band splat counts, band instance count and
     that rank's two capacities, (world, nb + 3) int32, gathered with the band images -- copied to
@@ -198,8 +213,8 @@ class _CountRing:
                     self.pending.clear()
                     raise ShardOverflowError(step, counts, pc, band_k, cap, rank=r)
 
-    def poll(self, wait: bool = False):
-        """Check every pending entry (wait is kept for the older call sites: always waits)."""
+    def poll(self):
+        """Check every pending entry (waits for each)."""
         if self.pending:
             self.check_upto(self.pending[-1][0])
 
@@ -217,7 +232,12 @@ class ShardStep:
     the image all-gather, so every rank holds every rank's; they are copied to pinned memory
     without a host wait and checked ``lag`` steps later (or by ``check``), at the same call on
     every rank, so all ranks raise ``ShardOverflowError`` for the same step and none is left
-    blocked in a collective (the C++ ``gsr::ShardStep`` does the same).  ``strict=True`` checks
+    blocked in a collective (the C++ ``gsr::ShardStep`` does the same).  The same words also give
+    ``overflow_guard`` after every step: a (1,) int32 device word, the number of ranks that
+    overflowed in THAT step (``overflow_ranks``), identical on every rank and ready without a host
+    wait.  A training loop passes ``(step.overflow_guard, 0)`` as the guard of its statistics and
+    Adam step, so the truncated step's gradients are never applied on any rank, even before the
+    lagged check raises.  ``strict=True`` checks
     every step before returning it, at the cost of one host wait per step.  The caller
     re-plans (``plan``) and re-runs from that step.
 
@@ -303,9 +323,10 @@ class ShardStep:
                                     reuse=self._reuse["band"])
         return sh, st
 
-    def check(self, wait: bool = True):
-        """Raise ShardOverflowError if any rank overflowed in a step so far (waits for them)."""
-        self._ring.poll(wait=True)
+    def check(self):
+        """Raise ShardOverflowError if any rank overflowed in a step so far.  Always waits for
+        every pending step (a host sync); every rank must call it at the same step count."""
+        self._ring.poll()
 
     def step(self, dL_dpix: torch.Tensor):
         """-> (full image, this shard's leaf gradients, shard state, band state).  Raises
@@ -313,7 +334,7 @@ class ShardStep:
         The returned gradients and states live in buffers the next step reuses: consume them
         (e.g. the optimizer step) before calling step() again."""
         if self.rebalance_every and self.steps and self.steps % self.rebalance_every == 0:
-            self._ring.poll(wait=True)  # the old plan's pending checks first
+            self._ring.poll()  # the old plan's pending checks first
             self.plan()
             self.replans += 1
         # the step `lag` steps back, on every rank at this same call (its words have long landed)
@@ -330,10 +351,15 @@ class ShardStep:
         back = all_to_all_blocks(g2, self.world, self.dist, self.group)
         grads = self.rast.shard_backward(sh, back, reuse=self._reuse["grads"])
         out = img.wait(), grads, sh, st
-        self._ring.push(self.steps, img.statuses(), self.pair_cap, self.capacity)
+        allw = img.statuses()
+        # the step's agreement word on the device (same value on every rank): the optimizer guard
+        if getattr(self, "overflow_guard", None) is None or self.overflow_guard.device != allw.device:
+            self.overflow_guard = torch.zeros(1, dtype=torch.int32, device=allw.device)
+        self.overflow_guard.copy_(overflow_ranks(allw))
+        self._ring.push(self.steps, allw, self.pair_cap, self.capacity)
         self.steps += 1
         if self.strict:
-            self._ring.poll(wait=True)
+            self._ring.poll()
         return out
 
 

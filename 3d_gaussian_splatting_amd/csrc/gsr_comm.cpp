@@ -63,6 +63,16 @@ int gsr_comm_destroy(gsr_comm* comm) {
     return r == ncclSuccess ? 0 : nccl_err(r, "ncclCommDestroy");
 }
 
+int gsr_comm_size(gsr_comm* c, int32_t* world, int32_t* rank) {
+    if (!c || !c->comm || !world || !rank) return gsr::set_error(-1, "gsr_comm_size: null argument");
+    int n = 0, r = 0;
+    if (ncclResult_t e = ncclCommCount(c->comm, &n)) return nccl_err(e, "ncclCommCount");
+    if (ncclResult_t e = ncclCommUserRank(c->comm, &r)) return nccl_err(e, "ncclCommUserRank");
+    *world = n;
+    *rank = r;
+    return 0;
+}
+
 int gsr_comm_all_to_all(gsr_comm* c, const void* send, void* recv, size_t bb, void* stream) {
     if (!c || (!send && bb) || (!recv && bb)) return gsr::set_error(-1, "gsr_comm_all_to_all: null argument");
     const hipStream_t s = (hipStream_t)stream;

@@ -46,6 +46,11 @@ class RcclExchange final : public Exchange {
     int world() const override { return world_; }
     bool capturable() const override { return true; }
     const char* name() const override { return "rccl"; }
+    int comm_world() const override {
+        int32_t n = 0, r = 0;
+        detail::check(gsr_comm_size(comm_, &n, &r), "gsr_comm_size");
+        return n;
+    }
     void all_to_all(const void* send, void* recv, size_t bb, hipStream_t s) override {
         detail::check(gsr_comm_all_to_all(comm_, send, recv, bb, s), "gsr_comm_all_to_all");
     }
@@ -97,8 +102,7 @@ class StoreExchange final : public Exchange {
             std::memcpy(all.data() + (size_t)p * bytes, v.data(), bytes);
         }
         barrier(tag);
-        if (rank_ == 0)
-            for (int p = 0; p < world_; ++p) store_->deleteKey(tag + std::to_string(p));
+        release(tag);
         h2d(recv, all.data(), all.size(), s);
     }
     void all_reduce_i64(int64_t* buf, size_t n, bool max, hipStream_t s) override {
@@ -121,10 +125,19 @@ class StoreExchange final : public Exchange {
             for (size_t i = 0; i < n; ++i) acc[i] = p == 0 ? x[i] : (max ? std::max(acc[i], x[i]) : acc[i] + x[i]);
         }
         barrier(tag);
+        release(tag);
     }
     void barrier(const std::string& tag) {
         store_->add(tag + "done", 1);
         while (store_->add(tag + "done", 0) < world_) std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    // After barrier(tag): every rank has read every payload, so the last rank to leave deletes the
+    // payloads and both counters -- a long run leaves no keys behind in the store.
+    void release(const std::string& tag) {
+        if (store_->add(tag + "left", 1) < world_) return;
+        for (int p = 0; p < world_; ++p) store_->deleteKey(tag + std::to_string(p));
+        store_->deleteKey(tag + "done");
+        store_->deleteKey(tag + "left");
     }
     // synchronous copies on the caller's current stream (the step runs with it set to its own)
     static void d2h(void* h, const void* d, size_t n, hipStream_t) {
@@ -254,6 +267,12 @@ struct ShardStep::Pool {
     std::vector<std::unique_ptr<c10::Event>> ring_ev;
     std::unique_ptr<at::cuda::CUDAGraph> graph;
     const void* graph_dpix = nullptr;
+    // capture only once the camera and dL_dpix have been the same for one eager step: a loop that
+    // changes the camera every iteration then runs eagerly instead of capturing graphs it never
+    // replays
+    const void* last_dpix = nullptr;
+    int eager_since_change = 0;
+    torch::Tensor guard;  // (1,) int32: ranks that overflowed in the last step (device, agreed)
     explicit Pool(torch::Device d)
         : dev(d),
           main(c10::hip::getStreamFromPoolMasqueradingAsCUDA(false, d.index())),
@@ -291,7 +310,10 @@ bool ShardStep::graph_active() const { return pool_ && pool_->graph != nullptr; 
 void ShardStep::drop_graph() {
     pool_->graph.reset();
     pool_->graph_dpix = nullptr;
+    pool_->eager_since_change = 0;
 }
+
+torch::Tensor ShardStep::overflow_guard() const { return pool_->guard; }
 
 gsr_gaussians ShardStep::shard_struct() const {
     gsr_gaussians g{};
@@ -359,6 +381,7 @@ void ShardStep::size_buffers() {
     p.mine = torch::zeros({(int64_t)p.mine_floats}, f32);
     p.gathered = torch::empty({(int64_t)world_, (int64_t)p.mine_floats}, f32);
     p.image = torch::empty({3, cam_.height, cam_.width}, f32);
+    p.guard = torch::zeros({1}, f32.dtype(torch::kInt32));
     auto e = [&](std::initializer_list<int64_t> sh) { return torch::empty(sh, f32); };
     p.grads.clear();
     p.grads["means2D"] = e({Ps, 3});
@@ -514,6 +537,15 @@ void ShardStep::run(const torch::Tensor& dpix) {
                   "gsr_shard_backward");
     // 8. join the all-gather, unpack the bands into the full image
     if (overlap) p.join.block(p.main.unwrap());
+    // the agreed overflow word on the device, from every rank's gathered status: the number of
+    // ranks whose splat counts or band K exceeded the plan's capacities in THIS step (the same on
+    // every rank; the optimizer guard of a training loop, no host wait)
+    {
+        auto all = p.gathered.narrow(1, (int64_t)p.status_off, kStatusWords).view(torch::kInt32);
+        auto v = all.to(torch::kInt64).bitwise_and(0xFFFFFFFFLL);
+        auto bad = v.narrow(1, 0, nb).gt((int64_t)pair_cap_).any(1).logical_or(v.select(1, nb).gt((int64_t)capacity_));
+        p.guard.copy_(bad.sum().to(torch::kInt32).reshape({1}));
+    }
     for (int r = 0; r < world_; ++r) {
         const int a = std::min(rows_[r] * GSR_TILE, H), b = std::min(rows_[r + 1] * GSR_TILE, H);
         if (b > a)
@@ -583,7 +615,10 @@ ShardStep::Result ShardStep::step(const torch::Tensor& dL_dpix) {
             p.graph->replay();
         } else {
             run(dL_dpix);  // this step's result, eagerly
-            if (graph_) {
+            const bool stable = p.eager_since_change > 0 && p.last_dpix == dL_dpix.data_ptr();
+            p.last_dpix = dL_dpix.data_ptr();
+            ++p.eager_since_change;
+            if (graph_ && stable) {
                 // every arena slot now exists: capture the same calls on the same buffers
                 drop_graph();
                 for (Arena* a : {&p.geom, &p.bin, &p.img, &p.scratch}) a->frozen = true;
@@ -642,6 +677,7 @@ void bind_shard(py::module& m) {
         .def_property_readonly("rank", &Exchange::rank)
         .def_property_readonly("world", &Exchange::world)
         .def_property_readonly("name", &Exchange::name)
+        .def_property_readonly("comm_world", &Exchange::comm_world)
         .def_property_readonly("capturable", &Exchange::capturable);
     m.def("rccl_unique_id", []() {
         auto v = rccl_unique_id();
@@ -700,6 +736,9 @@ void bind_shard(py::module& m) {
         .def_property_readonly("band_instances", &ShardStep::band_instances)
         .def_property_readonly("g0", &ShardStep::g0)
         .def_property_readonly("g1", &ShardStep::g1)
+        .def_property_readonly("exchange_world", &ShardStep::exchange_world)
+        .def_property_readonly("overflow_guard", &ShardStep::overflow_guard)
+        .def_property_readonly("exchange_name", &ShardStep::exchange_name)
         .def_property_readonly("graph_active", &ShardStep::graph_active)
         .def_property_readonly("steps", &ShardStep::steps);
 }

@@ -48,6 +48,8 @@ class Exchange {
     virtual int world() const = 0;
     virtual bool capturable() const = 0;  // may be recorded into a hipGraph
     virtual const char* name() const = 0;
+    // the transport's own count of ranks (RCCL: ncclCommCount), for reports
+    virtual int comm_world() const { return world(); }
     // block b of `send` (block_bytes each) -> rank b; block s of `recv` <- rank s
     virtual void all_to_all(const void* send, void* recv, size_t block_bytes, hipStream_t s) = 0;
     // `bytes` from every rank into recv, rank-major
@@ -114,6 +116,12 @@ class ShardStep {
     Result step(const torch::Tensor& dL_dpix);
     // Check every completed step now (waits); raises like step().
     void check();
+    // (1,) int32 device word, written by every step: the number of ranks whose splats or band
+    // instances exceeded the plan's capacities in THAT step, from the gathered status footers --
+    // the same value on every rank, with no host wait.  Pass it as the guard of the optimizer step
+    // (gsr_adam_step_guarded / gsr_densify_stats_guarded with guard_cap 0) so that a truncated
+    // step never updates the model, before the lagged check raises.
+    torch::Tensor overflow_guard() const;
 
     const std::vector<int>& rows() const { return rows_; }
     int pair_cap() const { return pair_cap_; }
@@ -121,6 +129,9 @@ class ShardStep {
     const std::vector<int64_t>& band_instances() const { return band_k_; }
     int64_t g0() const { return g0_; }
     int64_t g1() const { return g1_; }
+    // ranks as the exchange's communicator counts them (RCCL: ncclCommCount)
+    int exchange_world() const { return ex_.comm_world(); }
+    const char* exchange_name() const { return ex_.name(); }
     bool graph_active() const;
     int64_t steps() const { return steps_; }
     // the last step's band instance count K (reads the device counter back: waits)
@@ -128,7 +139,9 @@ class ShardStep {
     // test hook: force a (smaller) pair capacity after plan()
     void set_pair_cap(int pair_cap);
     // Moving cameras (training, train_utils.cpp:128-145 picks a view per iteration): render from
-    // `cam` (same size) from the next step on -- a captured graph is dropped and re-captured.
+    // `cam` (same size) from the next step on -- a captured graph is dropped, and a new one is
+    // captured only after one eager step with the same camera and dL_dpix (a camera that changes
+    // every step runs eagerly, capturing nothing).
     // The cuts and capacities stay the last plan's until a re-plan: with rebalance_every = M > 0,
     // step() re-plans (checks the pending steps, then plan() for the camera in use) before every
     // M-th step; every rank does so at the same step count.

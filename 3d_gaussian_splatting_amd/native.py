@@ -48,7 +48,7 @@ EXPORTS = ["gsr_abi_version", "gsr_last_error", "gsr_forward", "gsr_read_num_ren
 TRAIN_EXPORTS = ["gsr_activate", "gsr_loss_scratch_bytes", "gsr_loss_forward", "gsr_loss_backward", "gsr_adam_step",
                  "gsr_adam_step_guarded", "gsr_densify_stats", "gsr_densify_stats_guarded", "gsr_compact_scratch_bytes", "gsr_compact_index", "gsr_gather_rows",
                  "gsr_knn_scratch_bytes", "gsr_knn_mean_dist2"]
-COMM_EXPORTS = ["gsr_comm_unique_id", "gsr_comm_init", "gsr_comm_destroy", "gsr_comm_all_to_all",
+COMM_EXPORTS = ["gsr_comm_unique_id", "gsr_comm_init", "gsr_comm_destroy", "gsr_comm_size", "gsr_comm_all_to_all",
                 "gsr_comm_all_gather", "gsr_comm_all_reduce_i64"]  # include/gsr/gsr_comm.h
 COMM_ID_BYTES = 128
 ACT_NONE, ACT_EXP, ACT_SIGMOID, ACT_NORMALIZE4 = range(4)

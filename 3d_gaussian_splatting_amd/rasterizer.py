@@ -155,6 +155,30 @@ class ViewsState:
             self.buffers.num_rendered = k.value
         return int(self.buffers.num_rendered)
 
+    def tall_camera(self):
+        """The pass's camera struct: the views stacked as bands of ceil(H / 16) tile rows."""
+        tall = native.Camera()
+        ctypes.memmove(ctypes.byref(tall), ctypes.byref(self.cstructs[0]), ctypes.sizeof(tall))
+        tall.height = len(self.cams) * ((self.cams[0].height + 15) // 16) * 16
+        return tall
+
+    def view(self, what: int, dtype: torch.dtype, count: int) -> torch.Tensor:
+        """Copy of an internal array of the pass (gsr_view over the tall grid and the V * P
+        (view, Gaussian) entries e = v * P + g): sorted tiles are tall-grid tile ids, sorted gids
+        are entry ids."""
+        L = native.load_hip()
+        tall = self.tall_camera()
+        p = L.gsr_view(ctypes.byref(tall), len(self.cams) * self.gauss.P, ctypes.byref(self.buffers), what)
+        if not p or count == 0:
+            return torch.empty(0, dtype=dtype, device=self.color.device)
+        nbytes = count * torch.empty(0, dtype=dtype).element_size()
+        for a in self.allocs:
+            for t in a.tensors:
+                base = t.data_ptr()
+                if base <= p < base + t.numel():
+                    return t[p - base:p - base + nbytes].view(dtype).clone()
+        raise KeyError("pointer not inside a views buffer")
+
 
 class CAbiRasterizer:
     """Thin ctypes front-end of gsr_forward / gsr_backward*."""

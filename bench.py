@@ -167,10 +167,79 @@ class CppShard:
         self.band_instances = list(self.st.band_instances)
         self.g0, self.g1 = self.st.g0, self.st.g1
         self.band = (self.rows[rank], self.rows[rank + 1])
+        self.comm_world = int(self.st.exchange_world)  # ncclCommCount of the step's communicator
+
+    def check(self):  # every pending step's agreed overflow check (waits)
+        self.st.check()
 
     def step(self, dpix):
         img, g, radii = self.st.step(dpix)
         return self._Band(self.st), g, self._Shard(radii)
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_or_refuse(args) -> int | None:
+    """`--gpus N` means N ranks (BASELINE north_star: throughput at 1, 2, 4 and 8 GPUs).
+
+    - Under a launcher (WORLD_SIZE set): WORLD_SIZE must equal --gpus, else exit 2.
+    - No launcher and --gpus N > 1: start N ranks as ONE child process (torch.distributed.run on
+      127.0.0.1, this script with the same arguments) and return its exit code.  Nothing here has
+      touched the GPU (torch.cuda.device_count() does not initialise it on this image), and the
+      parent only waits: no exec from a GPU process.
+    - --gpus N > 1 over RCCL needs N devices: fewer visible devices exit 2 (gloo ranks may share
+      one GPU: the rehearsal).
+    Returns None when this process is the one to run the benchmark."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus < 1:
+        print(f"bench.py: --gpus must be >= 1 (got {args.gpus})", file=sys.stderr)
+        return 2
+    if env_world is not None:
+        if int(env_world) != args.gpus:
+            print(f"bench.py: WORLD_SIZE={env_world} from the launcher but --gpus {args.gpus}: refusing to "
+                  f"report a {env_world}-rank run as {args.gpus} GPUs", file=sys.stderr)
+            return 2
+        return None
+    if args.gpus == 1:
+        return None
+    if args.mode != "render" and not args.launch_check:
+        print(f"bench.py: --mode {args.mode} runs on one GPU; --gpus {args.gpus} refused", file=sys.stderr)
+        return 2
+    if args.dist_backend == "nccl" and not args.launch_check:
+        ndev = torch.cuda.device_count()
+        if ndev < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} over RCCL needs {args.gpus} visible GPUs, found {ndev} "
+                  f"(use --dist-backend gloo --dist-impl python to rehearse ranks sharing a GPU)", file=sys.stderr)
+            return 2
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this pool (RCCL)
+    return subprocess.call(cmd, env=env)
+
+
+def launch_check_main(args):
+    """--launch-check: each rank joins the process group (gloo, no device) and the world is counted
+    by an all-reduce of ones; rank 0 prints the count as n_gpus.  Tests the launch path on a CPU."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    counted = 1
+    if world > 1:
+        dist.init_process_group("gloo")
+        t = torch.ones(1, dtype=torch.int64)
+        dist.all_reduce(t)
+        counted = int(t.item())
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_counted": counted, "gpus_arg": args.gpus}))
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
@@ -205,9 +274,17 @@ def main():
                     help="size the binning from K every step (one host read per forward) instead of a bound")
     ap.add_argument("--lib", default=None, help="load this libgsr_hip.so instead of the in-tree one "
                                                   "(experimental builds: _build.build_variant)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="launcher plumbing only: start the --gpus ranks, join the process group, count the "
+                         "ranks with one all-reduce, print that as a JSON line and exit (no GPU work)")
     args = ap.parse_args()
+    rc = launch_or_refuse(args)
+    if rc is not None:
+        sys.exit(rc)
     if args.lib:
         native.HIP_LIB = os.path.abspath(args.lib)
+    if args.launch_check:
+        return launch_check_main(args)
     if args.mode == "train":
         return train_main(args)
     if args.mode == "views":
@@ -308,6 +385,8 @@ def main():
     elapsed = time.perf_counter() - t0
     live = native.profile_read() if dom_stage is not None else {}
     native.profile_enable(0)
+    if world > 1:
+        plan.check()  # the last `lag` steps' agreed overflow checks, before any count is reported
     if dist:
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -344,7 +423,11 @@ def main():
         result["exchange"] = {"impl": ("C++ gsr::ShardStep over RCCL, hipGraph replay"
                                        if isinstance(plan, CppShard) else "bands.ShardStep over torch.distributed"),
                               "band_rows": plan.rows, "pair_cap": plan.pair_cap, "band_capacity": plan.capacity,
-                              "band_instances": plan.band_instances, "counts_are": "rank 0's shard / band"}
+                              "band_instances": plan.band_instances, "counts_are": "rank 0's shard / band",
+                              "comm_world": (plan.comm_world if isinstance(plan, CppShard) else dist.get_world_size()),
+                              "overflow_checked": "every step, agreed across ranks"}
+        if result["exchange"]["comm_world"] != world:
+            raise SystemExit(f"communicator counts {result['exchange']['comm_world']} ranks, WORLD_SIZE {world}")
     if stages and rank == 0 and dom_stage in live and live[dom_stage][1]:
         result["stage_ms"] = {k: round(ms / args.steps, 4) for k, (ms, n) in stages.items() if n}
         dom = dom_stage

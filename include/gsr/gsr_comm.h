@@ -34,6 +34,9 @@ int gsr_comm_unique_id(uint8_t id[GSR_COMM_ID_BYTES]);
 /* Collective over `world` processes (blocks until all ranks have called it). */
 int gsr_comm_init(gsr_comm** comm, const uint8_t id[GSR_COMM_ID_BYTES], int32_t world, int32_t rank);
 int gsr_comm_destroy(gsr_comm* comm);
+/* The communicator's size and this rank, as RCCL reports them (ncclCommCount / ncclCommUserRank):
+ * what a benchmark line quotes as its GPU count. */
+int gsr_comm_size(gsr_comm* comm, int32_t* world, int32_t* rank);
 
 /* Block b of send (block_bytes each) -> rank b; block s of recv <- rank s. */
 int gsr_comm_all_to_all(gsr_comm* comm, const void* send, void* recv, size_t block_bytes, void* stream);

@@ -124,9 +124,11 @@ int main(int argc, char** argv) {
             for (const char* k : {"means2D", "opacities", "means3D", "sh_dc", "sh_rest", "scales", "rotations"})
                 put_t(o, res.grads.at(k));
         }
-        std::fprintf(stderr, "[gsr_shard_step rank %d/%d] %s exchange, graph %d, %lld steps, pair_cap %d, capacity %d\n",
+        std::fprintf(stderr,
+                     "[gsr_shard_step rank %d/%d] %s exchange, graph %d, %lld steps, pair_cap %d, capacity %d, "
+                     "store_keys %lld\n",
                      rank, world, ex->name(), (int)step.graph_active(), (long long)done, step.pair_cap(),
-                     step.capacity());
+                     step.capacity(), (long long)store->getNumKeys());
         return 0;
     } catch (const std::exception& e) {
         std::fprintf(stderr, "gsr_shard_step failed: %s\n", e.what());

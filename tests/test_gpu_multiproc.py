@@ -70,12 +70,14 @@ def _worker(rank, port, outdir, force_pair_cap, move=False, one_rank=False):
             step.strict = False
             if rank == 0:
                 step.capacity = 1024
+            guards = []
             for i in range(5):
                 try:
                     step.step(dpix)
+                    guards.append(int(step.overflow_guard.item()))  # the device word, before the host check
                 except bands.ShardOverflowError as e:
                     np.savez(os.path.join(outdir, f"one{rank}.npz"), call=i, step=e.step, rank=e.rank,
-                             band_k=e.band_k, capacity=e.capacity)
+                             band_k=e.band_k, capacity=e.capacity, guards=np.array(guards))
                     break
             return
         if move:
@@ -95,6 +97,7 @@ def _worker(rank, port, outdir, force_pair_cap, move=False, one_rank=False):
                          pair_cap=e.pair_cap)
             return
         outs = [step.step(dpix) for _ in range(2)]  # two steps: the lagged count ring is exercised
+        assert int(step.overflow_guard.item()) == 0
         img, g, sh, st = outs[-1]
         assert torch.equal(img, outs[0][0])
         np.savez(os.path.join(outdir, f"r{rank}.npz"), image=img.cpu().numpy(), radii=sh.radii.cpu().numpy(),
@@ -173,3 +176,6 @@ def test_two_process_overflow_agreed():
     for g in got:
         assert int(g["call"]) == 2 and int(g["step"]) == 0 and int(g["rank"]) == 0
         assert int(g["band_k"]) > int(g["capacity"]) == 1024
+        # the device-side agreement word flagged both steps on BOTH ranks before the
+        # lagged host check raised (a guarded optimizer step would have skipped them)
+        assert g["guards"].tolist() == [1, 1]

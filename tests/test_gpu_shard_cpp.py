@@ -15,6 +15,7 @@ per rank, and compares with the single-GPU CAbiRasterizer on the same scene:
 * the same through the Python binding (the benchmark's multi-GPU path).
 """
 import os
+import re
 import socket
 import subprocess
 import tempfile
@@ -113,7 +114,10 @@ def _run(scene_path, world, transport, d, extra=None, graph=False, steps=2):
     for p, log in zip(procs, logs):
         assert p.returncode == 0, log
     print("\n".join(logs))
-    return [_read_out(os.path.join(d, f"out{r}.bin"), world) for r in range(world)]
+    outs = [_read_out(os.path.join(d, f"out{r}.bin"), world) for r in range(world)]
+    for o, log in zip(outs, logs):
+        o["log"] = log
+    return outs
 
 
 def _check_against(outs, reference, world):
@@ -132,8 +136,12 @@ def test_two_processes_store_exchange(scene, reference):
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "scene.bin")
         _write_scene(path, cam, s, dpix)
-        outs = _run(path, 2, "store", d)
-    assert all(o["done"] == 2 and o["ovf_step"] == -1 for o in outs)
+        outs = _run(path, 2, "store", d, steps=6)
+    assert all(o["done"] == 6 and o["ovf_step"] == -1 for o in outs)
+    # the host-staged exchange deletes its payload and barrier keys (the last rank out
+    # of each barrier does): six steps leave no per-step keys in the store (before: >= 12)
+    keys = [int(m) for m in re.findall(r"store_keys (\d+)", outs[0]["log"])]
+    assert keys and max(keys) <= 6, outs[0]["log"]
     assert outs[0]["rows"][1] not in (0, cam.grid[1])  # a real two-band split
     assert [o["g0"] for o in outs] == [0, outs[0]["g1"]] and outs[1]["g1"] == P
     _check_against(outs, reference, 2)
@@ -223,3 +231,42 @@ def test_python_binding_camera_move_rebalances(scene):
     st.check()
     assert st.graph_active
     np.testing.assert_array_equal(img3.cpu().numpy(), full.color.cpu().numpy())
+
+
+def test_python_binding_overflow_guard_skips_adam(scene):
+    """the C++ step's agreed overflow word is on the device after every step
+    (0 for a step within the plan's capacities, the number of overflowing ranks otherwise), and a
+    fused Adam step guarded by it (gsr_adam_step_guarded, guard_cap 0) leaves the parameters
+    untouched for the truncated step -- before the lagged host check raises."""
+    cam, s, dpix = scene
+    ext = pkg("native").load_torch_ext()
+    R, T = pkg("rasterizer"), pkg("trainer")
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.float32), device=dev)
+    inputs = dict(means3D=t(s.means3D), opacities=t(s.opacities), scales=t(s.scales), rotations=t(s.rotations),
+                  sh_dc=t(s.sh_dc).reshape(P, 1, 3), sh_rest=t(s.sh_rest).reshape(P, -1, 3))
+    ex = ext.rccl_exchange(ext.rccl_unique_id(), 0, 1)
+    assert ex.comm_world == 1
+    st = ext.ShardStep(ex, R.ext_camera(cam), inputs, 3, graph=True)
+    st.plan()
+    assert st.exchange_world == 1 and st.exchange_name == "rccl"
+    d = t(dpix)
+    k = T.TrainKernels(dev)
+
+    def adam(grads):
+        p = inputs["means3D"].clone()
+        m, v = torch.zeros_like(p), torch.zeros_like(p)
+        k.adam_step([dict(param=p, grad=grads["means3D"].contiguous(), exp_avg=m, exp_avg_sq=v, act=0, step=1,
+                          lr=1e-3)], guard=(st.overflow_guard, 0))
+        torch.cuda.synchronize()
+        return p
+
+    _, g, _ = st.step(d)
+    assert int(st.overflow_guard.item()) == 0
+    assert not torch.equal(adam(g), inputs["means3D"])  # applied
+    st.set_pair_cap(64)  # far below the true splat counts: the step is truncated
+    _, g, _ = st.step(d)
+    assert int(st.overflow_guard.item()) == 1
+    assert torch.equal(adam(g), inputs["means3D"])  # skipped on the device
+    with pytest.raises(OverflowError):
+        st.check()

@@ -173,3 +173,19 @@ def test_gloo_two_ranks_match_single_process(oracle):
         want = _grad_rows(g, scene.P)
         assert rel_l2(got["grads"], want) < 1e-5
         assert got["rows"][1] not in (0, cam.grid[1])
+
+
+def test_overflow_ranks_word():
+    """bands.overflow_ranks: the device agreement word counts the ranks whose counts exceed their
+    own pair_cap / capacity (u32 counts, each rank against its own capacities)."""
+    bands = pkg("bands")
+    # (world 3, nb 3): counts..., band K, pair_cap, capacity
+    w = torch.tensor([[10, 20, 30, 500, 32, 512],
+                      [10, 40, 30, 500, 32, 512],    # a splat count past pair_cap
+                      [1, 2, 3, 600, 32, 512]], dtype=torch.int32)  # band K past capacity
+    g = bands.overflow_ranks(w)
+    assert g.dtype == torch.int32 and g.shape == (1,) and int(g) == 2
+    ok = torch.tensor([[32, 0, 1, 512, 32, 512]], dtype=torch.int32)
+    assert int(bands.overflow_ranks(ok)) == 0
+    huge = torch.tensor([[-1, 0, 0, 0, 32, 512]], dtype=torch.int32)  # 0xFFFFFFFF as u32
+    assert int(bands.overflow_ranks(huge)) == 1
