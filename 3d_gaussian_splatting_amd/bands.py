@@ -75,6 +75,25 @@ def round_up(x: int, m: int = 256) -> int:
     return -(-int(x) // m) * m
 
 
+def plan_from_stats(inst, starts, ends, world: int):
+    """Band cuts from one step's row statistics (GSR_FLAG_ROW_SPANS): inst[y] = the instances in
+    tile row y over all shards; starts[s][y] / ends[s][y] = shard s's visible Gaussians whose tile
+    rect starts / ends (last row) in row y.  The splats shard s sends to band [r0, r1) are exactly
+    sum_{y<r1} starts[s][y] - sum_{y<r0} ends[s][y] (a rect meets the band iff it starts before r1
+    and does not end before r0), so the needed capacities follow for any cuts.
+    -> (rows, max splats per (shard, band), instances per band).  gsr::plan_from_stats is the
+    same arithmetic in C++."""
+    inst = np.asarray(inst, np.int64)
+    rows = balance_bands(inst, world)
+    band_k = [int(inst[rows[b]:rows[b + 1]].sum()) for b in range(world)]
+    max_splats = 0
+    for s_, e_ in zip(starts, ends):
+        ps = np.concatenate([[0], np.cumsum(np.asarray(s_, np.int64))])
+        pe = np.concatenate([[0], np.cumsum(np.asarray(e_, np.int64))])
+        max_splats = max(max_splats, max(int(ps[rows[b + 1]] - pe[rows[b]]) for b in range(world)))
+    return rows, max_splats, band_k
+
+
 class ImageGather:
     """Asynchronous all-gather of the band images: start it after the band forward, wait() for
     the full (3, H, W) image after the backward -- the collective runs on the communicator's
@@ -150,17 +169,19 @@ class ShardOverflowError(RuntimeError):
                          f"{pair_cap}, band instances {band_k} vs capacity {capacity}")
 
 
-def overflow_ranks(words: torch.Tensor) -> torch.Tensor:
+def overflow_ranks(words: torch.Tensor, nb: int | None = None) -> torch.Tensor:
     """Device-side agreement word: the number of ranks whose step overflowed, as a (1,) int32
     tensor on the words' device, computed without a host wait.  `words`: (world, nb + 3) int32,
-    every rank's per-band splat counts, band K, pair_cap and capacity (the gathered footer).
+    every rank's per-band splat counts, band K, pair_cap and capacity (the gathered footer;
+    `nb` = the number of counts when row statistics follow, else (words.shape[1] - 3)).
     Every rank computes it from the same gathered words, so every rank holds the same value: a
     training loop passes it as the guard of its optimizer step (``gsr_adam_step_guarded`` /
     ``gsr_densify_stats_guarded`` with guard_cap = 0, trainer.adam_step(guard=(word, 0))) so that
     a truncated step never updates the model on any rank, the step before the lagged host check
     raises ShardOverflowError."""
     v = words.to(torch.int64) & 0xFFFFFFFF  # the kernels' u32 counts
-    counts, band_k, pc, cap = v[:, :-3], v[:, -3], v[:, -2], v[:, -1]
+    nb = int(words.shape[1]) - 3 if nb is None else int(nb)
+    counts, band_k, pc, cap = v[:, :nb], v[:, nb], v[:, nb + 1], v[:, nb + 2]
     bad = (counts > pc[:, None]).any(dim=1) | (band_k > cap)
     return bad.sum().to(torch.int32).reshape(1)
 
@@ -174,14 +195,16 @@ class _CountRing:
 
     def __init__(self, nb: int, device, ring: int = 4):
         self.pin = torch.cuda.is_available() and torch.device(device).type == "cuda"
+        self.nb = nb
         self.ring = ring
         self.slots: list = []
         self.pending: list = []  # (step, slot, event or None, pair_cap, capacity)
         self.next = 0
+        self.last = None  # (step, rows of words) of the latest checked step: its row statistics
 
     def push(self, step: int, words: torch.Tensor, pair_cap: int, capacity: int):
-        """words: (world, nb + 3) int32 device tensor: every rank's counts, band K, pair_cap and
-        capacity (each rank is checked against its own)."""
+        """words: (world, nb + 3 [+ 3 grid_y]) int32 device tensor: every rank's counts, band K,
+        pair_cap and capacity (each rank is checked against its own), then its row statistics."""
         if len(self.pending) == self.ring:
             self.check_upto(self.pending[0][0])  # the oldest, at the same step on every rank
         if len(self.slots) < self.ring or self.slots[self.next].shape != words.shape:
@@ -205,13 +228,15 @@ class _CountRing:
             step, slot, ev, pair_cap, capacity = self.pending.pop(0)
             if ev is not None:
                 ev.synchronize()
-            for r, row in enumerate(slot.tolist()):
+            nb = self.nb
+            rows = [[int(x) & 0xFFFFFFFF for x in row] for row in slot.tolist()]  # u32
+            for r, v in enumerate(rows):
                 # rank r's words: its per-band counts, band K, then ITS pair_cap and capacity
-                v = [int(x) & 0xFFFFFFFF for x in row]  # u32
-                counts, band_k, pc, cap = v[:-3], v[-3], v[-2], v[-1]
+                counts, band_k, pc, cap = v[:nb], v[nb], v[nb + 1], v[nb + 2]
                 if max(counts) > pc or band_k > cap:
                     self.pending.clear()
                     raise ShardOverflowError(step, counts, pc, band_k, cap, rank=r)
+            self.last = (step, rows)
 
     def poll(self):
         """Check every pending entry (waits for each)."""
@@ -237,7 +262,13 @@ class ShardStep:
     overflowed in THAT step (``overflow_ranks``), identical on every rank and ready without a host
     wait.  A training loop passes ``(step.overflow_guard, 0)`` as the guard of its statistics and
     Adam step, so the truncated step's gradients are never applied on any rank, even before the
-    lagged check raises.  ``strict=True`` checks
+    lagged check raises.  ``live=True`` re-plans from the steps themselves: every step's shard
+    row statistics (instances per tile row, rect start / end rows: GSR_FLAG_ROW_SPANS) ride in the
+    same footer, and when step s - lag is checked every rank computes the cuts and capacities
+    they call for (``plan_from_stats`` with headroom) and adopts them at that same call if the cuts
+    moved, a capacity is short or one is over twice the need -- no probe, no collective, no wait
+    beyond the lagged check (``live_replans`` counts them; the C++ step does the same).
+    ``strict=True`` checks
     every step before returning it, at the cost of one host wait per step.  The caller
     re-plans (``plan``) and re-runs from that step.
 
@@ -250,7 +281,7 @@ class ShardStep:
     shard forwards, two all-reduces, one host wait) against that drift."""
 
     def __init__(self, rast, cam, inputs: dict, sh_degree: int, dist, group=None, headroom: float = 1.25,
-                 strict: bool = False, rebalance_every: int = 0, lag: int = 2):
+                 strict: bool = False, rebalance_every: int = 0, lag: int = 2, live: bool = False):
         self.rast, self.cam, self.dist, self.group = rast, cam, dist, group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -264,6 +295,9 @@ class ShardStep:
             raise ValueError("lag must be >= 1")
         self.lag = int(lag)
         self.replans = 0
+        self.live = bool(live)
+        self.live_replans = 0
+        self._stats_used = -1
         P = int(inputs["means3D"].shape[0])
         self.P = P
         self.g0, self.g1 = gaussian_shard(P, self.world, self.rank)
@@ -317,7 +351,12 @@ class ShardStep:
         return self.rows[self.rank], self.rows[self.rank + 1]
 
     def forward(self):
-        sh = self._shard_forward(self.pair_cap)
+        # this shard's row statistics ride in the status footer (live re-planning)
+        if getattr(self, "_stats", None) is None:
+            self._stats = torch.zeros(3 * self.gy, dtype=torch.int32, device=self.shard["means3D"].device)
+        self._stats.zero_()
+        sh = self.rast.shard_forward(self.cam, self.rows, self.pair_cap, **self.shard, sh_degree=self.D,
+                                     row_hist=self._stats, row_spans=True, reuse=self._reuse["shard"])
         recv = all_to_all_blocks(sh.send, self.world, self.dist, self.group)
         st = self.rast.band_forward(self.cam, self.band, self.world, self.pair_cap, recv, self.capacity,
                                     reuse=self._reuse["band"])
@@ -327,6 +366,34 @@ class ShardStep:
         """Raise ShardOverflowError if any rank overflowed in a step so far.  Always waits for
         every pending step (a host sync); every rank must call it at the same step count."""
         self._ring.poll()
+
+    def _replan_live(self):
+        """Adopt the cuts / capacities the latest checked step's statistics call for (see the
+        class doc); every rank takes the same decision from the same gathered words."""
+        last = self._ring.last
+        if last is None or last[0] == self._stats_used:
+            return
+        self._stats_used = last[0]
+        nb, gy = self.world, self.gy
+        o = nb + 3
+        inst = np.zeros(gy, np.int64)
+        starts, ends = [], []
+        for v in last[1]:
+            inst += np.asarray(v[o:o + gy], np.int64)
+            starts.append(v[o + gy:o + 2 * gy])
+            ends.append(v[o + 2 * gy:o + 3 * gy])
+        rows, max_splats, band_k = plan_from_stats(inst, starts, ends, nb)
+        pc_need, cap_need = max(max_splats, 1), max(max(band_k), 1)
+        short = pc_need > self.pair_cap or cap_need > self.capacity
+        fat = (self.pair_cap > 2 * round_up(pc_need * self.headroom)
+               or self.capacity > 2 * round_up(cap_need * self.headroom))
+        if rows == self.rows and not short and not fat:
+            return
+        pc, cap = round_up(pc_need * self.headroom), round_up(cap_need * self.headroom)
+        if cap >= 2**31 or pc * self.world >= 2**31:
+            raise ValueError(f"band capacity {cap} / pair_cap {pc} exceed int32: use more ranks")
+        self.rows, self.pair_cap, self.capacity, self.band_instances = rows, pc, cap, band_k
+        self.live_replans += 1
 
     def step(self, dL_dpix: torch.Tensor):
         """-> (full image, this shard's leaf gradients, shard state, band state).  Raises
@@ -339,13 +406,15 @@ class ShardStep:
             self.replans += 1
         # the step `lag` steps back, on every rank at this same call (its words have long landed)
         self._ring.check_upto(self.steps - self.lag)
+        if self.live:
+            self._replan_live()
         sh, st = self.forward()
         # this rank's overflow words ride in the image all-gather: every rank checks every rank's
         key = (self.pair_cap, self.capacity)
         if getattr(self, "_caps_key", None) != key:  # a device copy of the capacities, made once per plan
             self._caps = torch.tensor(list(key), dtype=torch.int32, device=sh.counts.device)
             self._caps_key = key
-        words = torch.cat([sh.counts.reshape(-1), st.k_device().reshape(-1), self._caps]).to(torch.int32)
+        words = torch.cat([sh.counts.reshape(-1), st.k_device().reshape(-1), self._caps, self._stats]).to(torch.int32)
         img = ImageGather(st.color, self.rows, self.rank, self.dist, self.group, status=words)  # overlaps B1
         g2 = self.rast.band_backward(st, self.world, self.pair_cap, dL_dpix, reuse=self._reuse["band"])
         back = all_to_all_blocks(g2, self.world, self.dist, self.group)
@@ -355,7 +424,7 @@ class ShardStep:
         # the step's agreement word on the device (same value on every rank): the optimizer guard
         if getattr(self, "overflow_guard", None) is None or self.overflow_guard.device != allw.device:
             self.overflow_guard = torch.zeros(1, dtype=torch.int32, device=allw.device)
-        self.overflow_guard.copy_(overflow_ranks(allw))
+        self.overflow_guard.copy_(overflow_ranks(allw, self.world))
         self._ring.push(self.steps, allw, self.pair_cap, self.capacity)
         self.steps += 1
         if self.strict:

@@ -450,18 +450,24 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
 // from LDS in fixed quad order and stored straight to the partial arrays at the record's
 // emission index j (8 moments in part8[2j..2j+1], the 9th in part1[j]).
 constexpr int kPark = 4;
-// Parking slot stride: 16 quads x 12 floats, padded by 12 so that the flush's 36 lanes (4 slots
-// x 9 moments) read 36 distinct banks -- at 192 the 4 slots alias (4-way LDS bank conflicts,
-// ~1 conflict cycle per LDS instruction of B1 in the PMC pass).
-constexpr int kParkSlot = 16 * 12 + 12;
+// Parking slot stride and the flush's lane map.  The flush reads with ds_read_b32, whose banks
+// are (address / 4) mod 32 over lane groups {0-31}, {32-63} (MI355X_MICROARCH.md, LDS table).
+// Flush lane l sums moment c = l >> 2 of parked slot s = l & 3 (36 lanes: c < 9), so lanes 0-31
+// are (c 0-7) x (s 0-3) and read word 8 s + c + 12 i (mod 32) for quad i: 32 distinct banks when
+// the slot stride is 8 mod 32 (200 = 16 quads x 12 floats + 8, 16-B aligned for the leaders'
+// float4 stores).  Round 4's map (s = l / 9, c = l mod 9, stride 204 = 12 mod 32) put slots 2 / 3
+// on slot 0's banks: a 2-way conflict on every flush read, the ~9.5e6 SQ_LDS_BANK_CONFLICT cycles
+// per launch of profiles/r04_pmc_summary.txt (16 reads x ~6.3e5 flushes at 1M / 1080p).
+constexpr int kParkSlot = 16 * 12 + 8;
+static_assert(kParkSlot % 32 == 8 && kParkSlot % 4 == 0, "flush banks / float4 alignment");
 // The parked records' batch indices ride in one scalar word (6 bits per slot: `kpack`); the
 // flush lane of slot s reads its record's emission index from the batch's jl table (`sjl`,
 // written once per batch), so a record costs no per-record readlane / LDS write for it.
 __device__ __forceinline__ void park_flush(const float* qpark, const uint32_t* sjl, uint32_t kpack, int parked,
                                            float* p8f, float* p1, uint8_t* fl, int lane) {
     __syncthreads();  // one-wave block: orders the quad leaders' LDS writes before the reads
-    if (lane < parked * 9) {
-        const int slot = lane / 9, c = lane - 9 * slot;
+    const int slot = lane & 3, c = lane >> 2;
+    if (c < 9 && slot < parked) {
         const float* q = qpark + slot * kParkSlot + c;
         // -0 is the identity of IEEE addition, so the first add of each chain folds into a move
         float t[4] = {-0.f, -0.f, -0.f, -0.f};

@@ -141,7 +141,7 @@ int launch_views_sum(const GaussIn& in, int V, const GradOut& out, const GradOut
 // partials: (sort_blocks(P) + 1) * nbands u32.
 int launch_pack_splats(const uint32_t* tiles, const uint4* rect, const uint32_t* depth_key, const float4* rec, int P,
                        const BandRows& br, uint32_t* partials, char* send, int pair_cap, uint32_t* slot_of,
-                       uint32_t* row_hist, int grid_y, hipStream_t s);
+                       uint32_t* row_hist, int grid_y, bool spans, hipStream_t s);
 // Band side: nsrc received blocks -> local arrays of nsrc * pair_cap entries (empty slots: no tiles)
 int launch_unpack_splats(const char* recv, int nsrc, int pair_cap, int ty0, int ty1, float4* rec, uint32_t* depth_key,
                          uint32_t* tiles, uint4* rect, hipStream_t s);

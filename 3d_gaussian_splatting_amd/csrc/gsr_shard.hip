@@ -26,17 +26,22 @@ __device__ inline uint64_t lanemask_lt() {
 }
 
 // Per block: splats per band (partials[b * nblk + blk]); optionally the per-tile-row instance
-// histogram (LDS, then one global add per row).
+// histogram (LDS, then one global add per row).  SPANS: also the per-row counts of the visible
+// Gaussians whose rect starts / ends in that row (row_hist[gy + y]: first tile row y;
+// row_hist[2 gy + y]: last tile row y) -- from which the splats any band cut would receive
+// follow exactly: #(miny < r1) - #(maxy <= r0) (the live re-plan of the multi-GPU step).
+template <bool SPANS>
 __global__ __launch_bounds__(kB) void pack_count_kernel(const uint32_t* __restrict__ tiles,
                                                         const uint4* __restrict__ rect, int P, BandRows br,
                                                         uint32_t* __restrict__ partials, int nblk,
                                                         uint32_t* __restrict__ row_hist, int grid_y) {
     __shared__ uint32_t cnt[kWaves][kMaxBands];
-    __shared__ uint32_t hist[kMaxHistRows];
+    __shared__ uint32_t hist[(SPANS ? 3 : 1) * kMaxHistRows];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const bool do_hist = row_hist != nullptr;
+    const int hrows = (SPANS ? 3 : 1) * grid_y;
     if (do_hist)
-        for (int y = threadIdx.x; y < grid_y; y += kB) hist[y] = 0u;
+        for (int y = threadIdx.x; y < hrows; y += kB) hist[y] = 0u;
     __syncthreads();
     uint32_t c[kMaxBands];
 #pragma unroll
@@ -52,6 +57,10 @@ __global__ __launch_bounds__(kB) void pack_count_kernel(const uint32_t* __restri
             if (do_hist) {
                 const uint32_t wd = (rr.y & 0xFFFF) - (rr.x & 0xFFFF);
                 for (uint32_t y = miny; y < maxy; ++y) atomicAdd(&hist[y], wd);
+                if constexpr (SPANS) {
+                    atomicAdd(&hist[grid_y + miny], 1u);
+                    atomicAdd(&hist[2 * grid_y + maxy - 1], 1u);
+                }
             }
         }
 #pragma unroll
@@ -67,7 +76,7 @@ __global__ __launch_bounds__(kB) void pack_count_kernel(const uint32_t* __restri
         partials[threadIdx.x * nblk + blockIdx.x] = t;
     }
     if (do_hist)
-        for (int y = threadIdx.x; y < grid_y; y += kB)
+        for (int y = threadIdx.x; y < hrows; y += kB)
             if (hist[y]) atomicAdd(row_hist + y, hist[y]);
 }
 
@@ -220,7 +229,7 @@ __global__ __launch_bounds__(256) void unpack_kernel(const char* __restrict__ re
 
 int launch_pack_splats(const uint32_t* tiles, const uint4* rect, const uint32_t* depth_key, const float4* rec, int P,
                        const BandRows& br, uint32_t* partials, char* send, int pair_cap, uint32_t* slot_of,
-                       uint32_t* row_hist, int grid_y, hipStream_t s) {
+                       uint32_t* row_hist, int grid_y, bool spans, hipStream_t s) {
     const size_t bb = exchange_block_bytes(pair_cap);
     if (P <= 0) {  // empty shard: zero headers
         for (int b = 0; b < br.n; ++b)
@@ -228,8 +237,12 @@ int launch_pack_splats(const uint32_t* tiles, const uint4* rect, const uint32_t*
         return 0;
     }
     const int nblk = pack_blocks(P);
-    hipLaunchKernelGGL(pack_count_kernel, dim3(nblk), dim3(kB), 0, s, tiles, rect, P, br, partials, nblk, row_hist,
-                       grid_y);
+    if (spans && row_hist)
+        hipLaunchKernelGGL(pack_count_kernel<true>, dim3(nblk), dim3(kB), 0, s, tiles, rect, P, br, partials, nblk,
+                           row_hist, grid_y);
+    else
+        hipLaunchKernelGGL(pack_count_kernel<false>, dim3(nblk), dim3(kB), 0, s, tiles, rect, P, br, partials, nblk,
+                           row_hist, grid_y);
     hipLaunchKernelGGL(pack_scan_kernel, dim3(br.n), dim3(1024), 0, s, partials, nblk, send, bb);
     hipLaunchKernelGGL(pack_scatter_kernel, dim3(nblk), dim3(kB), 0, s, tiles, rect, depth_key, rec, P, br, partials,
                        nblk, send, bb, pair_cap, slot_of);

@@ -236,6 +236,23 @@ std::vector<int> balance_bands(const std::vector<int64_t>& c, int world) {
     return rows;
 }
 
+StatsPlan plan_from_stats(const std::vector<int64_t>& inst, const std::vector<std::vector<int64_t>>& starts,
+                          const std::vector<std::vector<int64_t>>& ends, int world) {
+    const int gy = (int)inst.size();
+    StatsPlan sp;
+    sp.rows = balance_bands(inst, world);
+    sp.band_k.assign(world, 0);
+    for (int b = 0; b < world; ++b)
+        for (int y = sp.rows[b]; y < sp.rows[b + 1]; ++y) sp.band_k[b] += inst[y];
+    for (size_t s = 0; s < starts.size(); ++s) {
+        std::vector<int64_t> ps(gy + 1, 0), pe(gy + 1, 0);  // prefix sums of starts / ends
+        for (int y = 0; y < gy; ++y) ps[y + 1] = ps[y] + starts[s][y], pe[y + 1] = pe[y] + ends[s][y];
+        for (int b = 0; b < world; ++b)
+            sp.max_splats = std::max(sp.max_splats, ps[sp.rows[b + 1]] - pe[sp.rows[b]]);
+    }
+    return sp;
+}
+
 ShardOverflowError::ShardOverflowError(int64_t step_, int rank_, std::vector<int64_t> counts_, int pair_cap_,
                                        int64_t band_k_, int capacity_)
     : std::overflow_error([&] {
@@ -263,7 +280,7 @@ struct ShardStep::Pool {
     Stream main, side;  // the step's stream (capturable) and the all-gather's
     c10::Event enter{c10::DeviceType::CUDA}, leave{c10::DeviceType::CUDA}, fork{c10::DeviceType::CUDA},
         join{c10::DeviceType::CUDA};
-    std::vector<torch::Tensor> ring;  // pinned (world x kStatusWords) int32 per slot
+    std::vector<torch::Tensor> ring;  // pinned (world x foot_words) int32 per slot
     std::vector<std::unique_ptr<c10::Event>> ring_ev;
     std::unique_ptr<at::cuda::CUDAGraph> graph;
     const void* graph_dpix = nullptr;
@@ -283,6 +300,7 @@ struct ShardStep::Pool {
 };
 
 static constexpr int kStatusWords = 16;  // per rank: nb header counts, band K (nb <= 15)
+// then 3 x grid_y words of row statistics (GSR_FLAG_ROW_SPANS): the footer is foot_words_ long
 
 ShardStep::ShardStep(Exchange& ex, const RasterCamera& cam, const ShardInputs& in, std::array<float, 3> bg,
                      double headroom, bool graph, int lag)
@@ -295,9 +313,10 @@ ShardStep::ShardStep(Exchange& ex, const RasterCamera& cam, const ShardInputs& i
     grid_y_ = (cam.height + GSR_TILE - 1) / GSR_TILE;
     TORCH_CHECK(world_ <= grid_y_, "ShardStep: more ranks than tile rows");
     rows_ = equal_bands(grid_y_, world_);
+    foot_words_ = kStatusWords + 3 * grid_y_;
     pool_ = std::make_unique<Pool>(in.means3D.device());
     for (int i = 0; i < lag_ + 2; ++i) {
-        pool_->ring.push_back(torch::empty({(int64_t)world_, kStatusWords},
+        pool_->ring.push_back(torch::empty({(int64_t)world_, (int64_t)foot_words_},
                                            torch::TensorOptions().dtype(torch::kInt32).pinned_memory(true)));
         pool_->ring_ev.push_back(std::make_unique<c10::Event>(c10::DeviceType::CUDA));
     }
@@ -348,6 +367,7 @@ gsr_raster_settings ShardStep::shard_settings() const {
 
 gsr_raster_settings ShardStep::band_settings() const {
     gsr_raster_settings s = shard_settings();
+    s.flags = 0;
     s.tile_y0 = rows_[rank_];
     s.tile_y1 = rows_[rank_ + 1];
     s.max_rendered = capacity_;
@@ -377,7 +397,7 @@ void ShardStep::size_buffers() {
     }
     p.tall = tall;
     p.status_off = (size_t)3 * tall * cam_.width;
-    p.mine_floats = p.status_off + kStatusWords;
+    p.mine_floats = p.status_off + foot_words_;
     p.mine = torch::zeros({(int64_t)p.mine_floats}, f32);
     p.gathered = torch::empty({(int64_t)world_, (int64_t)p.mine_floats}, f32);
     p.image = torch::empty({3, cam_.height, cam_.width}, f32);
@@ -496,9 +516,15 @@ void ShardStep::run(const torch::Tensor& dpix) {
     const gsr_raster_settings rs = shard_settings(), bs = band_settings();
     std::vector<int32_t> rows32(rows_.begin(), rows_.end());
     for (Arena* a : {&p.geom, &p.bin, &p.img, &p.scratch}) a->next = 0;
-    // 1. F1 on the shard + splat packing
-    detail::check(gsr_shard_forward(&ccam_, &g, &rs, nb, rows32.data(), pair_cap_, p.send.data_ptr(),
-                                    g.P ? p.radii.data_ptr<int32_t>() : nullptr, p.state.data_ptr(), nullptr, s),
+    // 1. F1 on the shard + splat packing; the shard's row statistics (instances per tile row,
+    //    rect start / end rows) go straight into this rank's status footer
+    auto stats = p.mine.narrow(0, (int64_t)(p.status_off + kStatusWords), 3 * (int64_t)grid_y_);
+    stats.zero_();
+    gsr_raster_settings rss = rs;
+    rss.flags |= GSR_FLAG_ROW_SPANS;
+    detail::check(gsr_shard_forward(&ccam_, &g, &rss, nb, rows32.data(), pair_cap_, p.send.data_ptr(),
+                                    g.P ? p.radii.data_ptr<int32_t>() : nullptr, p.state.data_ptr(),
+                                    reinterpret_cast<uint32_t*>(stats.data_ptr<float>()), s),
                   "gsr_shard_forward");
     // 2. splats -> bands
     ex_.all_to_all(p.send.data_ptr(), p.recv.data_ptr(), p.block_bytes, s);
@@ -560,10 +586,10 @@ void ShardStep::push_status() {
     TORCH_CHECK(pending_.size() < p.ring.size(), "ShardStep: overflow ring full");
     const int slot = ring_next_;
     ring_next_ = (ring_next_ + 1) % (int)p.ring.size();
-    auto st = p.gathered.narrow(1, (int64_t)p.status_off, kStatusWords).contiguous().view(torch::kInt32);
+    auto st = p.gathered.narrow(1, (int64_t)p.status_off, foot_words_).contiguous().view(torch::kInt32);
     p.ring[slot].copy_(st, /*non_blocking=*/true);
     p.ring_ev[slot]->record(p.main.unwrap());
-    pending_.push_back({steps_, slot});
+    pending_.push_back({steps_, slot, pair_cap_, capacity_});
 }
 
 void ShardStep::poll(bool wait_all) {
@@ -574,15 +600,50 @@ void ShardStep::poll(bool wait_all) {
         pending_.erase(pending_.begin());
         const int32_t* st = pool_->ring[q.slot].data_ptr<int32_t>();
         for (int r = 0; r < world_; ++r) {
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(st + r * kStatusWords);
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(st + r * foot_words_);
             std::vector<int64_t> counts(w, w + world_);
             const int64_t k = w[world_];
-            if (*std::max_element(counts.begin(), counts.end()) > pair_cap_ || k > capacity_) {
+            if (*std::max_element(counts.begin(), counts.end()) > q.pair_cap || k > q.capacity) {
                 pending_.clear();
-                throw ShardOverflowError(q.step, r, counts, pair_cap_, k, capacity_);
+                throw ShardOverflowError(q.step, r, counts, q.pair_cap, k, q.capacity);
             }
         }
+        last_stats_.assign(st, st + (size_t)world_ * foot_words_);
+        last_stats_step_ = q.step;
     }
+}
+
+void ShardStep::replan_live() {
+    if (last_stats_step_ < 0 || last_stats_step_ == stats_used_step_) return;
+    stats_used_step_ = last_stats_step_;
+    const int gy = grid_y_;
+    std::vector<int64_t> inst(gy, 0);
+    std::vector<std::vector<int64_t>> starts(world_, std::vector<int64_t>(gy)), ends = starts;
+    for (int r = 0; r < world_; ++r) {
+        const uint32_t* f = reinterpret_cast<const uint32_t*>(last_stats_.data() + (size_t)r * foot_words_) + kStatusWords;
+        for (int y = 0; y < gy; ++y) {
+            inst[y] += f[y];
+            starts[r][y] = f[gy + y];
+            ends[r][y] = f[2 * gy + y];
+        }
+    }
+    const StatsPlan sp = plan_from_stats(inst, starts, ends, world_);
+    const int64_t kmax = *std::max_element(sp.band_k.begin(), sp.band_k.end());
+    const int64_t pc_need = std::max<int64_t>(sp.max_splats, 1), cap_need = std::max<int64_t>(kmax, 1);
+    const bool short_caps = pc_need > pair_cap_ || cap_need > capacity_;
+    const bool fat_caps = pair_cap_ > 2 * round_up((int64_t)std::ceil(pc_need * headroom_)) ||
+                          capacity_ > 2 * round_up((int64_t)std::ceil(cap_need * headroom_));
+    if (sp.rows == rows_ && !short_caps && !fat_caps) return;
+    const int64_t pc = round_up((int64_t)std::ceil(pc_need * headroom_));
+    const int64_t cap = round_up((int64_t)std::ceil(cap_need * headroom_));
+    if (cap >= INT32_MAX || pc * world_ >= INT32_MAX)
+        throw std::overflow_error("ShardStep: band capacity / pair_cap exceed int32: use more ranks");
+    rows_ = sp.rows;
+    band_k_ = sp.band_k;
+    pair_cap_ = (int)pc;
+    capacity_ = (int)cap;
+    size_buffers();  // new cuts / capacities: buffers re-sized, the captured graph dropped
+    ++live_replans_;
 }
 
 void ShardStep::check() { poll(true); }
@@ -604,6 +665,7 @@ ShardStep::Result ShardStep::step(const torch::Tensor& dL_dpix) {
         ++replans_;
     }
     poll(false);
+    if (live_) replan_live();
     Pool& p = *pool_;
     // the step runs on its own stream (capturable), ordered after / before the caller's
     const Stream caller = current_stream();
@@ -679,6 +741,14 @@ void bind_shard(py::module& m) {
         .def_property_readonly("name", &Exchange::name)
         .def_property_readonly("comm_world", &Exchange::comm_world)
         .def_property_readonly("capturable", &Exchange::capturable);
+    m.def(
+        "plan_from_stats",
+        [](const std::vector<int64_t>& inst, const std::vector<std::vector<int64_t>>& starts,
+           const std::vector<std::vector<int64_t>>& ends, int world) {
+            const StatsPlan sp = plan_from_stats(inst, starts, ends, world);
+            return py::make_tuple(sp.rows, sp.max_splats, sp.band_k);
+        },
+        py::arg("inst"), py::arg("starts"), py::arg("ends"), py::arg("world"));
     m.def("rccl_unique_id", []() {
         auto v = rccl_unique_id();
         return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
@@ -729,6 +799,8 @@ void bind_shard(py::module& m) {
         .def("set_camera", &ShardStep::set_camera, py::arg("cam"))
         .def("set_rebalance_every", &ShardStep::set_rebalance_every, py::arg("m"))
         .def_property_readonly("replans", &ShardStep::replans)
+        .def("set_live_replan", &ShardStep::set_live_replan, py::arg("on"))
+        .def_property_readonly("live_replans", &ShardStep::live_replans)
         .def("band_num_rendered", &ShardStep::band_num_rendered)
         .def_property_readonly("rows", &ShardStep::rows)
         .def_property_readonly("pair_cap", &ShardStep::pair_cap)

@@ -71,6 +71,20 @@ std::pair<int64_t, int64_t> gaussian_shard(int64_t P, int world, int rank);
 std::vector<int> equal_bands(int grid_y, int world);
 std::vector<int> balance_bands(const std::vector<int64_t>& row_counts, int world);
 
+// Band cuts and capacities from one step's statistics (GSR_FLAG_ROW_SPANS of every shard, summed
+// or per shard): inst[y] = instances in tile row y over all shards; starts[s][y] / ends[s][y] =
+// shard s's visible Gaussians whose rect's first / last tile row is y.  The splats shard s sends
+// to band [r0, r1) are exactly sum_{y<r1} starts[s][y] - sum_{y<r0} ends[s][y], so the needed
+// pair_cap and band capacity (before headroom) follow for any cuts.  Same arithmetic as
+// bands.plan_from_stats.
+struct StatsPlan {
+    std::vector<int> rows;
+    int64_t max_splats = 0;  // largest (shard, band) splat count under `rows`
+    std::vector<int64_t> band_k;
+};
+StatsPlan plan_from_stats(const std::vector<int64_t>& inst, const std::vector<std::vector<int64_t>>& starts,
+                          const std::vector<std::vector<int64_t>>& ends, int world);
+
 class ShardOverflowError : public std::overflow_error {
    public:
     ShardOverflowError(int64_t step, int rank, std::vector<int64_t> counts, int pair_cap, int64_t band_k,
@@ -148,12 +162,21 @@ class ShardStep {
     void set_camera(const RasterCamera& cam);
     void set_rebalance_every(int m);
     int64_t replans() const { return replans_; }
+    // Live re-planning (SURVEY §8e "reuse the previous iteration's counts"): every step carries
+    // its shard's row statistics (GSR_FLAG_ROW_SPANS) in the status footer of the image
+    // all-gather; when step s - lag is checked, every rank computes the cuts and capacities those
+    // statistics call for (plan_from_stats, headroom) and, at that same call, adopts them if the
+    // cuts moved, a capacity is short, or a capacity is over twice what is needed -- no probe
+    // forward, no collective and no host wait beyond the lagged ring.  live_replans() counts them.
+    void set_live_replan(bool on) { live_ = on; }
+    int64_t live_replans() const { return live_replans_; }
 
    private:
     struct Pool;  // buffers (stable addresses across steps: graph-replayable), streams, events, graph
     void run(const torch::Tensor& dpix);
     void push_status();
     void poll(bool wait_all);
+    void replan_live();
     gsr_gaussians shard_struct() const;
     gsr_raster_settings shard_settings() const;
     gsr_raster_settings band_settings() const;
@@ -177,11 +200,17 @@ class ShardStep {
     int64_t steps_ = 0;
     int rebalance_every_ = 0;
     int64_t replans_ = 0;
+    bool live_ = false;
+    int64_t live_replans_ = 0;
+    int foot_words_ = 0;                  // status words + 3 x grid_y row statistics, per rank
+    std::vector<int32_t> last_stats_;     // the latest checked step's footers (world x foot_words_)
+    int64_t last_stats_step_ = -1, stats_used_step_ = -1;
     std::unique_ptr<Pool> pool_;
     // overflow ring: gathered status footers (pinned), checked `lag_` steps later
     struct Pending {
         int64_t step;
         int slot;
+        int pair_cap, capacity;  // the plan the step ran under
     };
     std::vector<Pending> pending_;
     int ring_next_ = 0;

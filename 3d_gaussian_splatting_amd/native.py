@@ -22,6 +22,7 @@ HIP_LIB = os.environ.get("GSR_HIP_LIB") or os.path.join(LIB_DIR, "libgsr_hip.so"
 
 ABI_VERSION = 3
 GSR_FLAG_DEBUG = 1
+GSR_FLAG_ROW_SPANS = 2  # gsr.h: gsr_shard_forward row_hist = 3 x grid_y (instances, rect start rows, end rows)
 GSR_ERR_OVERFLOW = -4
 GSR_GRAD2D_STRIDE = 12
 GSR_MAX_BATCH = 64

@@ -430,9 +430,11 @@ class ShardRasterizer(CAbiRasterizer):
     def shard_forward(self, cam: RasterCamera, band_rows, pair_cap: int, means3D, opacities, scales=None,
                       rotations=None, sh_dc=None, sh_rest=None, sh_degree=0, colors_precomp=None,
                       cov3D_precomp=None, scale_modifier=1.0, row_hist: torch.Tensor | None = None,
-                      debug=False, reuse: dict | None = None) -> ShardState:
+                      debug=False, reuse: dict | None = None, row_spans: bool = False) -> ShardState:
         """`reuse` (a dict the caller keeps across steps): the send / state / radii buffers and the
-        prepared input structs of the previous call with the same sizes are used again."""
+        prepared input structs of the previous call with the same sizes are used again.
+        row_hist (zeroed by the caller) += the instances per tile row; with row_spans it holds
+        3 x grid_y u32: that, then the rect start rows and end rows (GSR_FLAG_ROW_SPANS)."""
         dev = self.device
         srcs = (means3D, opacities, scales, rotations, sh_dc, sh_rest, colors_precomp, cov3D_precomp)
         key = None
@@ -461,6 +463,9 @@ class ShardRasterizer(CAbiRasterizer):
             if reuse is not None:
                 reuse["sizes"], reuse["bufs"] = (nsend, nstate, g.P), (send, state, radii)
         c = self._cam(cam)
+        s.flags = (native.GSR_FLAG_DEBUG if debug else 0) | (native.GSR_FLAG_ROW_SPANS if row_spans else 0)
+        if row_spans and (row_hist is None or row_hist.numel() < 3 * ((cam.height + 15) // 16)):
+            raise ValueError("row_spans needs a row_hist of 3 x grid_y words")
         rc = self.L.gsr_shard_forward(ctypes.byref(c), ctypes.byref(g), ctypes.byref(s), nb, rows, int(pair_cap),
                                       _ptr(send), _ptr(radii) if g.P else None, _ptr(state), _ptr(row_hist),
                                       self._stream())

@@ -103,6 +103,17 @@ def algorithmic_bytes(P, V, K, pix, tiles, M):
     }
 
 
+def stage_bytes(P, V, K, pix, tiles, M):
+    """Algorithmic bytes of EVERY timed stage (the §8d table plus the two stages it folds into
+    others): the per-tile depth sort reads and writes each instance's gid and gathers its 4-B
+    depth key (12 B per instance); the per-Gaussian gather reads each instance's 36-B partial and
+    writes a 48-B grad2d row per visible Gaussian."""
+    b = algorithmic_bytes(P, V, K, pix, tiles, M)
+    b["depth_sort"] = K * 12
+    b["gather_grad2d"] = K * 36 + V * 48
+    return b
+
+
 def lib_stamp() -> str | None:
     """Source stamp of the loaded libgsr_hip.so (sha256 of its sources + flags, _build.py)."""
     path = native.hip_library_path() + ".stamp"
@@ -430,6 +441,11 @@ def main():
             raise SystemExit(f"communicator counts {result['exchange']['comm_world']} ranks, WORLD_SIZE {world}")
     if stages and rank == 0 and dom_stage in live and live[dom_stage][1]:
         result["stage_ms"] = {k: round(ms / args.steps, 4) for k, (ms, n) in stages.items() if n}
+        # every stage's algorithmic bytes over its measured time, as a fraction of 8 TB/s (tracked
+        # per round: VERDICT r04 item 5); the blend stages are bound by VALU issue, not HBM
+        sb = stage_bytes(P_local, V, K, pix_local, tiles_local, M)
+        result["stage_hbm_frac"] = {k: round(sb[k] / (result["stage_ms"][k] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                    for k in sb if result["stage_ms"].get(k)}
         dom = dom_stage
         launches_per_step = max(live[dom][1] // args.steps, 1)
         mean_ms = live[dom][0] / live[dom][1]  # HIP events in the timed loop, launch stream

@@ -55,6 +55,11 @@ extern "C" {
 
 /* flags */
 #define GSR_FLAG_DEBUG 1u /* synchronise + check after every stage */
+/* gsr_shard_forward: row_hist holds 3 x grid_y u32 -- the instances per tile row, then the
+ * visible Gaussians whose tile rect starts in row y, then those whose rect ends (last row) in y:
+ * the splats any band cut [r0, r1) receives are sum_{y<r1} starts - sum_{y<r0} ends, so a
+ * multi-GPU step re-plans its cuts and capacities from a step's own statistics (no probe). */
+#define GSR_FLAG_ROW_SPANS 2u
 #define GSR_ERR_OVERFLOW (-4) /* gsr_read_num_rendered: K exceeded the binning's capacity */
 
 typedef struct gsr_camera {
@@ -218,7 +223,8 @@ size_t gsr_shard_state_bytes(int32_t P, int32_t nbands, int32_t pair_cap);
 
 /* radii: P (shard rows).  shard_state: gsr_shard_state_bytes, kept until gsr_shard_backward.
  * send: nbands exchange blocks.  row_hist (nullable, device, zeroed by the caller): += the
- * instances per tile row of this shard (grid_y u32) -- band balancing for the next step. */
+ * instances per tile row of this shard (grid_y u32) -- band balancing for the next step; with
+ * rs->flags & GSR_FLAG_ROW_SPANS also the rect start / end rows (3 x grid_y u32, see above). */
 int gsr_shard_forward(const gsr_camera* cam, const gsr_gaussians* shard, const gsr_raster_settings* rs,
                       int32_t nbands, const int32_t* band_rows, int32_t pair_cap, void* send,
                       int32_t* radii, void* shard_state, uint32_t* row_hist, void* stream);

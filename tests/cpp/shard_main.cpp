@@ -6,7 +6,11 @@
 //   env RANK, WORLD_SIZE, MASTER_ADDR (default 127.0.0.1), MASTER_PORT: the c10d::TCPStore
 //   rendezvous (rank 0 hosts it); GSR_TRANSPORT = store (host-staged, ranks may share a GPU) |
 //   rccl (one GPU per rank); GSR_GRAPH = 1: capture the step into a hipGraph (rccl only);
-//   GSR_STEPS (default 2); GSR_FORCE_PAIR_CAP > 0: shrink pair_cap after plan() (overflow test).
+//   GSR_STEPS (default 2); GSR_FORCE_PAIR_CAP > 0: shrink pair_cap after plan() (overflow test);
+//   GSR_CAM_PATH = file of cameras (f32 tanfovx, tanfovy, view[16], proj[16], campos[3] each): step i
+//   renders camera i mod n (set_camera before the step); GSR_LIVE = 1: live re-planning;
+//   GSR_ALL_IMAGES = 1: OUT.bin ends with every step's image (steps x 3 x H x W f32);
+//   GSR_TIMING = 1: synchronise after every step and print its wall time (re-plan cost).
 //
 // SCENE.bin ("GSRSHRD1"): int32 P, W, H, sh_degree, M (sh_rest coefficients per Gaussian);
 //   f32 tanfovx, tanfovy, view[16], proj[16], campos[3]; f32 arrays means3D (P,3), opacities (P),
@@ -18,6 +22,7 @@
 #include <torch/csrc/distributed/c10d/TCPStore.hpp>
 #include <torch/torch.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -86,6 +91,27 @@ int main(int argc, char** argv) {
         si.sh_rest = rd({P, M, 3});
         si.sh_degree = D;
         auto dpix = rd({3, H, W});
+        auto read_cam = [&](std::ifstream& f) {
+            gsr::RasterCamera c = cam;
+            f.read(reinterpret_cast<char*>(&c.tanfovx), 4);
+            f.read(reinterpret_cast<char*>(&c.tanfovy), 4);
+            f.read(reinterpret_cast<char*>(c.viewmatrix.data()), 64);
+            f.read(reinterpret_cast<char*>(c.projmatrix.data()), 64);
+            f.read(reinterpret_cast<char*>(c.campos.data()), 12);
+            return c;
+        };
+        std::vector<gsr::RasterCamera> path;
+        if (const std::string pf = env_str("GSR_CAM_PATH", ""); !pf.empty()) {
+            std::ifstream cf(pf, std::ios::binary);
+            while (true) {
+                gsr::RasterCamera c = read_cam(cf);
+                if (!cf) break;
+                path.push_back(c);
+            }
+            if (path.empty()) throw std::runtime_error("empty camera path");
+        }
+        const bool live = env_int("GSR_LIVE", 0) != 0, all_images = env_int("GSR_ALL_IMAGES", 0) != 0,
+                   timing = env_int("GSR_TIMING", 0) != 0;
 
         c10d::TCPStoreOptions opts;
         opts.port = (uint16_t)env_int("MASTER_PORT", 29500);
@@ -95,14 +121,27 @@ int main(int argc, char** argv) {
         std::shared_ptr<c10d::Store> sstore(store.get(), [keep = store](c10d::Store*) mutable { keep.reset(); });
         std::unique_ptr<gsr::Exchange> ex = transport == "rccl" ? gsr::rccl_exchange(*store, rank, world)
                                                                 : gsr::store_exchange(sstore, rank, world);
-        gsr::ShardStep step(*ex, cam, si, {0.f, 0.f, 0.f}, 1.25, graph, 2);
+        gsr::ShardStep step(*ex, path.empty() ? cam : path[0], si, {0.f, 0.f, 0.f}, 1.25, graph, 2);
         step.plan();
         if (force_cap > 0) step.set_pair_cap(force_cap);
+        step.set_live_replan(live);
         gsr::ShardStep::Result res;
         int64_t done = 0, ovf_step = -1, ovf_rank = -1;
+        std::vector<torch::Tensor> images;
         try {
             for (int i = 0; i < steps; ++i) {
+                if (!path.empty()) step.set_camera(path[i % path.size()]);
+                const int64_t lr0 = step.live_replans();
+                const auto t0 = std::chrono::steady_clock::now();
                 res = step.step(dpix);
+                if (timing) {
+                    torch::cuda::synchronize();
+                    const double ms =
+                        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                    std::fprintf(stderr, "{\"rank\": %d, \"step\": %d, \"ms\": %.4f, \"replanned\": %d, \"graph\": %d}\n",
+                                 rank, i, ms, (int)(step.live_replans() > lr0), (int)step.graph_active());
+                }
+                if (all_images) images.push_back(res.image.clone());
                 ++done;
             }
             step.check();
@@ -124,11 +163,12 @@ int main(int argc, char** argv) {
             for (const char* k : {"means2D", "opacities", "means3D", "sh_dc", "sh_rest", "scales", "rotations"})
                 put_t(o, res.grads.at(k));
         }
+        for (const auto& im : images) put_t(o, im);
         std::fprintf(stderr,
                      "[gsr_shard_step rank %d/%d] %s exchange, graph %d, %lld steps, pair_cap %d, capacity %d, "
-                     "store_keys %lld\n",
+                     "store_keys %lld, live_replans %lld\n",
                      rank, world, ex->name(), (int)step.graph_active(), (long long)done, step.pair_cap(),
-                     step.capacity(), (long long)store->getNumKeys());
+                     step.capacity(), (long long)store->getNumKeys(), (long long)step.live_replans());
         return 0;
     } catch (const std::exception& e) {
         std::fprintf(stderr, "gsr_shard_step failed: %s\n", e.what());

@@ -90,7 +90,9 @@ def _read_out(path, world):
         for k, c in GRADS:
             out[k] = np.frombuffer(b, np.float32, n * c, o).reshape(n, c)
             o += 4 * n * c
-        assert o == len(b)
+        rest = (len(b) - o) // 4
+        assert rest % (3 * H * W) == 0
+        out["images"] = np.frombuffer(b, np.float32, rest, o).reshape(-1, 3, H, W)  # GSR_ALL_IMAGES
     return out
 
 
@@ -270,3 +272,54 @@ def test_python_binding_overflow_guard_skips_adam(scene):
     assert torch.equal(adam(g), inputs["means3D"])  # skipped on the device
     with pytest.raises(OverflowError):
         st.check()
+
+
+def _cam_path(cam, n):
+    """A moving camera: yaw -6..6 degrees with the view sliding 0.9 down -- the scene's instances
+    move up the image and the balanced cuts must follow."""
+    import math
+    gr = pkg("graphics")
+    fx, fy = 2 * math.atan(cam.tanfovx), 2 * math.atan(cam.tanfovy)
+    out = []
+    for i in range(n):
+        a = math.radians(-6.0 + 12.0 * i / (n - 1))
+        Rm = np.array([[math.cos(a), 0, math.sin(a)], [0, 1, 0], [-math.sin(a), 0, math.cos(a)]])
+        out.append(gr.make_camera(Rm, np.array([0.0, 0.9 * i / (n - 1), 0.0]), fx, fy, cam.width, cam.height))
+    return out
+
+
+def test_two_processes_live_replan_camera_path(scene):
+    """the C++ step re-cuts its bands from the statistics every step carries
+    (GSR_FLAG_ROW_SPANS rows in the status footer; no probe, no extra collective), here over a
+    24-pose camera path through the host-staged exchange in two processes: no overflow, cuts that
+    move with the view, and every step's gathered image equal to the single-GPU render of its
+    camera bit for bit.  Per-step wall times (synchronised) go to gpurun_out/ for the re-plan
+    cost (profiles/r05_live_replan_*)."""
+    cam, s, dpix = scene
+    path_cams = _cam_path(cam, 24)
+    rast = pkg("rasterizer").CAbiRasterizer("cuda")
+    args = (s.means3D, s.opacities, s.scales, s.rotations, s.sh_dc, s.sh_rest)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "scene.bin")
+        _write_scene(path, cam, s, dpix)
+        cp = os.path.join(d, "cams.bin")
+        with open(cp, "wb") as f:
+            for c in path_cams:
+                f.write(np.concatenate([[c.tanfovx, c.tanfovy], np.asarray(c.viewmatrix, np.float32).ravel(),
+                                        np.asarray(c.projmatrix, np.float32).ravel(),
+                                        np.asarray(c.campos, np.float32).ravel()]).astype(np.float32).tobytes())
+        outs = _run(path, 2, "store", d, steps=24,
+                    extra={"GSR_CAM_PATH": cp, "GSR_LIVE": "1", "GSR_ALL_IMAGES": "1", "GSR_TIMING": "1"})
+    for o in outs:
+        assert o["done"] == 24 and o["ovf_step"] == -1, o["log"]
+        assert o["images"].shape[0] == 24
+    replans = [int(m) for m in re.findall(r"live_replans (\d+)", outs[0]["log"])]
+    assert replans and replans[0] >= 2, outs[0]["log"]  # the cuts followed the view
+    for i, c in enumerate(path_cams):
+        want = rast.forward(c, *args, sh_degree=3).color.cpu().numpy()
+        for o in outs:
+            np.testing.assert_array_equal(o["images"][i], want, err_msg=f"step {i}")
+    timing = [ln for o in outs for ln in o["log"].splitlines() if ln.startswith('{"rank"')]
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "live_replan_timing.jsonl"), "w") as f:
+        f.write("\n".join(timing) + "\n")
