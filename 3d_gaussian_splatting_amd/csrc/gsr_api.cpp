@@ -205,12 +205,14 @@ void band(const gsr_camera* cam, const gsr_raster_settings* rs, int* y0, int* y1
 struct Views {
     uint32_t *depth_key, *tiles, *flags, *offsets, *partials, *lookback;
     bool presort;                                          // gsr_internal.h use_presort
+    bool rb;                                               // gsr_internal.h use_rb_binning
+    uint32_t *rb_histA, *rb_histB, *rb_status;
     uint32_t *dk0, *dv0, *dk1, *dv1, *dhist, *rtiles;      // presort only
     uint4* rrect;
     float4* rec;
     uint4* rect;
     uint2* ranges;
-    uint32_t *counters, *K_dev, *ovf, *ovf2, *done, *term;
+    uint32_t *counters, *K_dev, *ovf, *ovf2, *ovf3, *done, *term;
     float *final_T, *accum;
     float4* ck;  // the checkpoint pool (binning buffer)
     uint32_t *kA, *vA, *kB, *vB, *hist;
@@ -232,6 +234,8 @@ Views views(const gsr_camera* cam, long long n, const gsr_buffers* b) {
     v.partials = at<uint32_t>(b->geom, gl.partials);
     v.lookback = at<uint32_t>(b->geom, gl.lookback);
     v.presort = use_presort(n);
+    v.rb = (b->reserved & kBufRowBucketed) != 0;  // decided by the forward (fwd_phase2)
+    v.rb_histA = at<uint32_t>(b->geom, gl.rb_hist);
     if (v.presort) {
         v.dk0 = at<uint32_t>(b->geom, gl.dk0);
         v.dv0 = at<uint32_t>(b->geom, gl.dv0);
@@ -246,6 +250,8 @@ Views views(const gsr_camera* cam, long long n, const gsr_buffers* b) {
     v.K_dev = v.counters + kTotalSlot;
     v.ovf = at<uint32_t>(b->image, il.ovf);
     v.ovf2 = at<uint32_t>(b->image, il.ovf2);
+    v.ovf3 = at<uint32_t>(b->image, il.ovf3);
+    v.rb_status = at<uint32_t>(b->image, il.rb_status);
     v.done = at<uint32_t>(b->image, il.done);
     v.term = at<uint32_t>(b->image, il.term);
     v.final_T = at<float>(b->image, il.final_T);
@@ -259,8 +265,10 @@ Views views(const gsr_camera* cam, long long n, const gsr_buffers* b) {
         v.vB = at<uint32_t>(b->binning, bl.vB);
         v.hist = at<uint32_t>(b->binning, bl.hist);
         v.mk = at<uint8_t>(b->binning, bl.mk);
+        v.rb_histB = at<uint32_t>(b->binning, bl.rb_hist);
         const int tiles = div_up(cam->width, kTile) * div_up(cam->height, kTile);
-        const bool odd = (tile_passes(tiles) & 1) != 0;  // the sort ends in (kB, vB) after odd passes
+        // the radix sort ends in (kB, vB) after odd passes; the row-bucketed binning writes (kA, vA)
+        const bool odd = !v.rb && (tile_passes(tiles) & 1) != 0;
         v.sorted_tile = odd ? v.kB : v.kA;
         v.sorted_gid = odd ? v.vB : v.vA;
         v.free_k = odd ? v.kA : v.kB;
@@ -330,7 +338,10 @@ int fwd_phase1(FwdJob& j, gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_image, voi
                   "depth presort");
         return 0;
     }
-    GSR_STAGE(GSR_STAGE_SCAN, launch_scan(v.tiles, (int)j.n, v.offsets, v.partials, v.K_dev, stream), "scan");
+    // the row-bucketed binning (maybe taken in phase 2) needs the three-kernel scan's offsets
+    const bool rb_possible = use_rb_binning(j.n, j.gx, j.gy);
+    GSR_STAGE(GSR_STAGE_SCAN, launch_scan(v.tiles, (int)j.n, v.offsets, v.partials, v.K_dev, stream, !rb_possible),
+              "scan");
     return 0;
 }
 
@@ -343,17 +354,34 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
     bufs->capacity = (int32_t)cap;
     bufs->binning = alloc_binning(ctx, BinLayout(cap, (long long)ImgLayout::tile_count(cam->width, cam->height)).total);
     if (!bufs->binning) return fail(-2, "allocation failed (binning, %lld instances)", cap);
-    const Views v = views(cam, j.n, bufs);
     const int tiles = j.gx * j.gy, ntiles = (j.ty1 - j.ty0) * j.gx;
+    // Row-bucketed binning when the image fits it and the register form takes the per-tile depth
+    // order (it leaves a tile's entries unordered, which that form does not mind); recorded in the
+    // buffers so that every later view of them (backward, accessors) finds the same arrays.
+    const bool scanned = use_rb_binning(j.n, j.gx, j.gy);  // phase 1 ran the three-kernel scan
+    if (scanned && cap > 0 && tile_wave_sort_eligible(cap, ntiles)) bufs->reserved |= kBufRowBucketed;
+    const Views v = views(cam, j.n, bufs);
     if (v.presort)
         GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate_ranked(v.rtiles, v.rrect, v.rect, (int)j.n, j.gx, j.ty0,
                                                                v.lookback, v.offsets, v.kA, v.vA, cap, stream),
                   "duplicate (rank order)");
-    else
+    else if (!v.rb)
         GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate(v.tiles, v.rect, (int)j.n, j.gx, j.ty0, v.offsets, v.lookback,
-                                                        v.kA, v.vA, cap, v.K_dev, stream),
+                                                        v.kA, v.vA, cap, v.K_dev, stream, scanned),
                   "duplicate");
-    if (cap > 0) {
+    if (cap > 0 && v.rb) {
+        // F3 + the tile sort + F5 as two counting passes; the pairs ride in (kB, vB)
+        GSR_STAGE(GSR_STAGE_TILE_SORT, launch_rb_binning(v.tiles, v.rect, v.offsets, (int)j.n, j.gx, j.ty0, j.ty1,
+                                                         v.rb_histA, v.rb_histB, v.rb_status, v.kB, v.vB, v.kA, v.vA,
+                                                         v.ranges, cap, stream),
+                  "row-bucketed binning");
+        GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_tile_depth_sort(v.ranges, j.ty0 * j.gx, ntiles, cap, v.depth_key,
+                                                               v.sorted_gid, v.ovf, v.counters + kOvfCountSlot, v.ovf2,
+                                                               v.counters + kOvf2CountSlot, v.ovf3,
+                                                               v.counters + kOvf3CountSlot, v.done, v.free_k,
+                                                               v.free_v, stream, true),
+                  "per-tile depth order");
+    } else if (cap > 0) {
         int which = -1;
         GSR_STAGE(GSR_STAGE_TILE_SORT, radix_sort(v.kA, v.vA, v.kB, v.vB, v.kA, v.vA, cap, v.K_dev, tile_bits(tiles),
                                                   v.hist, &which, stream),
@@ -365,7 +393,8 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
         if (!v.presort)
             GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_tile_depth_sort(v.ranges, j.ty0 * j.gx, ntiles, cap, v.depth_key,
                                                                v.sorted_gid, v.ovf, v.counters + kOvfCountSlot, v.ovf2,
-                                                               v.counters + kOvf2CountSlot, v.done, v.free_k,
+                                                               v.counters + kOvf2CountSlot, v.ovf3,
+                                                               v.counters + kOvf3CountSlot, v.done, v.free_k,
                                                                v.free_v, stream),
                   "per-tile depth order");
     }

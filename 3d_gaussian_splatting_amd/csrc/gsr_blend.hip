@@ -80,6 +80,7 @@ struct BlendGeom {
     uint32_t ck_slots;  // checkpoint slots (gsr_internal.h); the live bytes follow the float4 slots
     int ck_fixed;       // 1: slot = tile * 31 + chunk - 1; 0: from the tile's start in the list
     float bg0, bg1, bg2;
+    uint32_t cap;       // the binning's capacity: B1 writes partial entries j < cap only
 };
 
 // Which of the tile's four 16x4 pixel stripes (slot p = rows 4p..4p+3) can hold a pixel
@@ -474,9 +475,11 @@ __device__ __forceinline__ void park_flush(const float* qpark, const uint32_t* s
 #pragma unroll
         for (int i = 0; i < 16; ++i) t[i & 3] += q[i * 12];
         const uint32_t j = sjl[(kpack >> (6 * slot)) & 63u];
-        float* dst = c < 8 ? p8f + 8 * (size_t)j + c : p1 + j;
-        *dst = (t[0] + t[1]) + (t[2] + t[3]);
-        if (c == 8) fl[j] = 1;  // the gather reads flagged entries only
+        if (j != 0xFFFFFFFFu) {  // an entry past the capacity (binning overflow) has none
+            float* dst = c < 8 ? p8f + 8 * (size_t)j + c : p1 + j;
+            *dst = (t[0] + t[1]) + (t[2] + t[3]);
+            if (c == 8) fl[j] = 1;  // the gather reads flagged entries only
+        }
     }
     __syncthreads();
 }
@@ -671,6 +674,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
             const int minx = rr.x & 0xFFFF, miny = rr.x >> 16, maxx = rr.y & 0xFFFF;
             const int y0 = miny > geo.ty0 ? miny : geo.ty0;
             jl = rr.z + (uint32_t)((ty - y0) * (maxx - minx) + (tx - minx));
+            // past the capacity: an overflowing binning (the row-bucketed one keeps list
+            // positions, not emission indices, below it) -- the entry is not written
+            if (jl >= geo.cap) jl = 0xFFFFFFFFu;
             const float4* r = rec + 3 * (size_t)g;
             srec[3 * lane + 0] = r[0];
             srec[3 * lane + 1] = r[1];
@@ -786,6 +792,7 @@ static BlendGeom make_geo(const gsr_camera& cam, const float bg[3], int ty0, int
     g.bg0 = bg[0];
     g.bg1 = bg[1];
     g.bg2 = bg[2];
+    g.cap = cap > 0 ? (uint32_t)cap : 0u;
     return g;
 }
 

@@ -71,10 +71,21 @@ inline size_t sort_scratch_words(long long n) { return 256 * ((size_t)radix_bloc
 #endif
 constexpr long long kPresortMin = GSR_PRESORT_MIN;
 constexpr int kMaxViews = 8;  // gsr_forward_views: views per call (= GSR_MAX_VIEWS)
+// Row-bucketed binning (gsr_sort.hip): images of at most kRbMaxRows x kRbMaxCols tiles outside
+// presort mode; chunks of kRbChunkPairs (Gaussian, row) pairs in its second pass.
+#ifndef GSR_RB_BIN
+#define GSR_RB_BIN 1
+#endif
+constexpr int kRbMaxRows = 256, kRbMaxCols = 256, kRbChunkPairs = 1024;
+// gsr_buffers.reserved bits (set by the forward): the binning in use
+constexpr int32_t kBufRowBucketed = 1;
+inline bool use_rb_binning(long long n, int gx, int gy) {
+    return GSR_RB_BIN && n < kPresortMin && gx <= kRbMaxCols && gy <= kRbMaxRows;
+}
 inline bool use_presort(long long n) { return n >= kPresortMin; }
 
 struct GeomLayout {
-    size_t depth_key, tiles, flags, rec, rect, offsets, partials, lookback, total;
+    size_t depth_key, tiles, flags, rec, rect, offsets, partials, lookback, rb_hist, total;
     size_t dk0 = 0, dv0 = 0, dk1 = 0, dv1 = 0, dhist = 0, rtiles = 0, rrect = 0;  // presort only
     GeomLayout(long long P) {
         size_t o = 0, n = (size_t)(P > 0 ? P : 1);
@@ -87,6 +98,7 @@ struct GeomLayout {
         offsets = take(4 * n);
         partials = take(4 * ((size_t)sort_blocks(n) + 16));  // three-kernel scan
         lookback = take(4 * (16 + (n + 255) / 256));        // fused scan + duplicate; presort: block sums
+        rb_hist = take(4 * (256 * ((n + 255) / 256) + 256));  // row-bucketed binning: [row][block] + row totals
         if (use_presort(P)) {
             dk0 = take(4 * n);
             dv0 = take(4 * n);
@@ -151,7 +163,7 @@ __host__ __device__ inline size_t ck_slot_of(bool fixed, uint32_t start, int til
 // `tiles` tiles.  The tile-key sort ping-pongs (kA, vA) <-> (kB, vB); F3 emits into (kA, vA).
 // Then the checkpoint slots: ck_slots x 256 float4, and one live byte per (slot, 16x4 stripe).
 struct BinLayout {
-    size_t kA, vA, kB, vB, hist, ck, ckm, mk = 0, total, ck_slots;
+    size_t kA, vA, kB, vB, hist, rb_hist, ck, ckm, mk = 0, total, ck_slots;
     BinLayout(long long cap, long long tiles) {
         size_t o = 0, n = (size_t)(cap > 0 ? cap : 1);
         auto take = [&](size_t bytes) { size_t r = o; o += align_up(bytes); return r; };
@@ -160,6 +172,8 @@ struct BinLayout {
         kB = take(4 * n);
         vB = take(4 * n);
         hist = take(4 * sort_scratch_words(n));
+        // row-bucketed binning: [column][chunk] counts of every row's chunks of kRbChunkPairs pairs
+        rb_hist = take(4 * (size_t)kRbMaxCols * (n / kRbChunkPairs + 1 + kRbMaxRows));
         ck_slots = ck_pool_slots(cap, tiles);
         ck = take(ck_slots * 256 * 16);
         ckm = take(ck_slots * 4);
@@ -171,7 +185,7 @@ struct BinLayout {
 };
 
 struct ImgLayout {
-    size_t ranges, counters, done, ovf, ovf2, term, final_T, accum, total;
+    size_t ranges, counters, rb_status, done, ovf, ovf2, ovf3, term, final_T, accum, total;
     static size_t tile_count(int W, int H) {
         const size_t t = (size_t)div_up(W, kTile) * div_up(H, kTile);
         return t ? t : 1;
@@ -182,10 +196,13 @@ struct ImgLayout {
         const size_t tiles = tile_count(W, H);
         size_t pix = (size_t)W * H;
         ranges = take(8 * tiles);
-        counters = take(4 * (2 * kCountSlots + 16));  // ranges, counters and done are contiguous:
-        done = take(4 * tiles);  // one memset clears them (done: chunks sorted per queued tile)
+        counters = take(4 * (2 * kCountSlots + 16));  // ranges, counters, rb_status and done are
+        rb_status = take(4 * (16 + kRbMaxRows));       // contiguous: one memset clears them
+        done = take(4 * tiles);  // (rb_status: the row-bucketed binning's ticket + look-back words;
+                                 // done: chunks sorted per queued tile)
         ovf = take(4 * tiles);   // tiles the per-tile depth sort hands to its larger
         ovf2 = take(4 * tiles);  // forms (queues: the 8192-entry form, then the 16384-entry / chunked one)
+        ovf3 = take(4 * tiles);  // register form: slices past one wave's 1024 entries (2048-entry waves)
         term = take(4 * tiles * kMaxChunks);  // F6: per tile [termination index, chunk 1..kMaxChunks-1 starts]
         final_T = take(4 * (pix ? pix : 1));
         accum = take(12 * (pix ? pix : 1));  // colour sum without background, 3 x H x W
@@ -244,6 +261,7 @@ struct ShardLayout {
 constexpr int kTotalSlot = 2 * kCountSlots;          // K = sum of tiles_touched, written by the scan
 constexpr int kOvfCountSlot = 2 * kCountSlots + 8;   // tiles queued for the large per-tile depth sort
 constexpr int kOvf2CountSlot = 2 * kCountSlots + 9;  // ... then for its 16384-entry / chunked form
+constexpr int kOvf3CountSlot = 2 * kCountSlots + 10; // register form: past 2048 entries, to the LDS forms
 
 // number of 8-bit LSD passes to sort tile ids of a grid with `tiles` tiles
 inline int tile_bits(int tiles) {

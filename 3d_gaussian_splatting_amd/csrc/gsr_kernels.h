@@ -50,13 +50,22 @@ int radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* k0, u
 // (device), as three kernels for n > kFusedScanMax (nothing to do below: the fused kernel of
 // launch_duplicate scans).  scan_partials_buf: sort_blocks(n) + 16 u32.
 int launch_scan(const uint32_t* tiles, int n, uint32_t* offsets, uint32_t* scan_partials_buf, uint32_t* total_out,
-                hipStream_t s);
+                hipStream_t s, bool fused_ok = true);
 // F3: inst_start (rect[g].z) and the emitted (tile key, gid) pairs in gid order, rect row-major,
 // band rows from ty0 -- at most `cap` of them.  For n <= kFusedScanMax one look-back kernel
 // also does F2 (offsets, *total_out); lookback: 16 + ceil(n / 256) u32.
 int launch_duplicate(const uint32_t* tiles, uint4* rect, int n, int grid_x, int ty0, uint32_t* offsets,
                      uint32_t* lookback, uint32_t* tkey, uint32_t* tgid, long long cap, uint32_t* total_out,
-                     hipStream_t s);
+                     hipStream_t s, bool scanned = false);  // scanned: the three-kernel scan already ran
+
+// Row-bucketed binning (gsr_internal.h use_rb_binning): from the inclusive F2 scan `offsets`, F3
+// (inst_start into rect.z), the stable tile sort of the instances and F5 -- the (tile key, gid)
+// arrays tkey / tgid in (tile, gid) order and `ranges` (cleared beforehand) -- in two counting
+// passes over (Gaussian, tile row) pairs.  histA: GeomLayout.rb_hist; histB: BinLayout.rb_hist;
+// rb_status: ImgLayout.rb_status (cleared); pgid / pxr: cap u32 each of scratch.
+int launch_rb_binning(const uint32_t* tiles, uint4* rect, const uint32_t* offsets, int n, int gx, int ty0, int ty1,
+                      uint32_t* histA, uint32_t* histB, uint32_t* rb_status, uint32_t* pgid, uint32_t* pxr,
+                      uint32_t* tkey, uint32_t* tgid, uint2* ranges, long long cap, hipStream_t s);
 
 // Per-tile depth order: every tile's slice of `gid` (tile-sorted, gid order within a tile) is
 // sorted in place by (depth_key[gid], gid) -- the canonical (tile, depth, gid) order -- with a
@@ -76,10 +85,16 @@ int launch_depth_presort(const uint32_t* depth_key, const uint32_t* tiles, const
 int launch_duplicate_ranked(const uint32_t* rtiles, const uint4* rrect, uint4* rect, int n, int grid_x, int ty0,
                             const uint32_t* bexcl, uint32_t* offsets, uint32_t* tkey, uint32_t* tgid, long long cap,
                             hipStream_t s);
+// Mean slices of up to ~1365 entries use the register form instead (one wave per slice of <= 1024,
+// then a 2048-entry wave per queued slice; longer ones through ovf3 to the 8192-entry blocks).
 int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long K, const uint32_t* depth_key,
                            uint32_t* gid, uint32_t* ovf, uint32_t* ovf_count, uint32_t* ovf2, uint32_t* ovf2_count,
-                           uint32_t* done, uint32_t* scratch_hi, uint32_t* scratch_lo,
-                           hipStream_t s);
+                           uint32_t* ovf3, uint32_t* ovf3_count, uint32_t* done, uint32_t* scratch_hi,
+                           uint32_t* scratch_lo, hipStream_t s, bool unordered = false);
+// unordered: the tiles' entries are in arbitrary order (row-bucketed binning), not gid order --
+// the register form needs nothing else; the LDS forms then also sort by gid (LSD, gid passes first).
+// True when the register form takes the mean slice (the row-bucketed binning is used only then).
+bool tile_wave_sort_eligible(long long K, int ntiles);
 
 // F5: ranges[tile] = [start, end) of the sorted tile keys (K = min(*K_dev, cap))
 int launch_finalize(const uint32_t* sorted_tile, long long cap, const uint32_t* K_dev, uint2* ranges, hipStream_t s);

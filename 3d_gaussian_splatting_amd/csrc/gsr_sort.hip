@@ -587,6 +587,395 @@ __global__ __launch_bounds__(256) void rank_payload_kernel(const uint32_t* __res
     if (threadIdx.x == 0) bsum[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
 }
 
+// ---- row-bucketed binning: F3 + the tile sort + F5 in two counting passes ----
+// The stable tile-key sort of the K emitted instances (two LSD passes over 8-byte records, ~340 MB
+// of traffic at 1M / 1080p) is replaced by two counting passes that each touch far fewer bytes:
+//   A. (Gaussian, tile row) pairs -- ~2.8 per visible Gaussian against ~7.5 instances -- bucketed by
+//      row: a per-block row count (rb_rows_count), the radix column scan, and a placement that
+//      takes each pair's slot from an LDS counter of its row (rb_rows_place).  A pair is
+//      (gid, x0 | x1 << 16): its columns, not expanded.
+//   B. per chunk of kRbChunk pairs of one row: the pairs' columns counted (rb_chunks_count), every
+//      row's [column][chunk] counts scanned flat with a look-back over rows (rb_tiles_scan, which
+//      also writes the tile ranges), and each chunk's instances placed from LDS column counters,
+//      staged in LDS and written as coalesced column runs (rb_chunks_place).
+// Result: every tile's entries contiguous, the ranges F5 would write, the tile keys -- ~140 MB of
+// traffic and no separate F3 / F5 -- but a tile's entries in arbitrary order: the per-tile depth
+// sort that follows orders them by the whole (depth, gid) key (the register form; the LDS forms
+// add gid passes, `unordered`), so the canonical list is the radix path's bit for bit.  Used when
+// the image has at most kRbMaxRows tile rows and kRbMaxCols tile columns (row / column ids fit one
+// byte; views mode's stacked images take the radix path), outside presort mode, and when the
+// register form takes the mean slice (gsr_api.cpp fwd_phase2; recorded in gsr_buffers.reserved).
+constexpr int kRbChunk = kRbChunkPairs;  // pairs per pass-B block (4 per thread)
+static_assert(kRbChunk % 256 == 0 && kRbMaxRows == 256 && kRbMaxCols == 256, "one row / column per thread");
+constexpr int kRbStageA = 2048;  // LDS staging (pairs) of a pass-A block (~720 at 1M / 1080p)
+constexpr int kRbStage = 4096;   // LDS staging (instances) of a pass-B block (~2800 at 1M / 1080p)
+constexpr uint32_t kRbAgg = 1u << 30, kRbInc = 2u << 30, kRbCntMask = kRbAgg - 1u;
+
+// rows of one block's Gaussians -> histA[r * nbA + b]; also writes inst_start (rect.z) from the
+// inclusive F2 scan
+__global__ __launch_bounds__(256) void rb_rows_count(const uint32_t* __restrict__ tiles, uint4* __restrict__ rect,
+                                                     const uint32_t* __restrict__ offsets, int n, int ty0, int ty1,
+                                                     uint32_t* __restrict__ histA, int nbA) {
+    __shared__ uint32_t cnt[kRbMaxRows];
+    const int tid = threadIdx.x, R = ty1 - ty0;
+    cnt[tid] = 0u;
+    __syncthreads();
+    const int g = blockIdx.x * 256 + tid;
+    if (g < n) {
+        const uint32_t nt = tiles[g];
+        if (nt) {
+            const uint4 rr = rect[g];
+            rect[g].z = offsets[g] - nt;  // inst_start: the emission index of the first instance
+            const int miny = (int)(rr.x >> 16), maxy = (int)(rr.y >> 16);
+            const int by0 = miny > ty0 ? miny : ty0, by1 = maxy < ty1 ? maxy : ty1;
+            for (int r = by0; r < by1; ++r) atomicAdd(&cnt[r - ty0], 1u);
+        }
+    }
+    __syncthreads();
+    if (tid < R) histA[(size_t)tid * nbA + blockIdx.x] = cnt[tid];
+}
+
+// Pairs of the block's 256 Gaussians placed row by row: the block counts its pairs per row in
+// LDS, takes each row's global base (the column-scanned counts), and every lane walks its own
+// rows, taking a slot of its row from an LDS counter -- the order of a row's pairs inside the
+// block is arbitrary (the per-tile sort that follows orders each tile by (depth, gid) itself),
+// so no per-row ballot sweep is needed.  Staged in LDS by row, written as coalesced row runs.
+__global__ __launch_bounds__(256) void rb_rows_place(const uint32_t* __restrict__ tiles, const uint4* __restrict__ rect,
+                                                     int n, int ty0, int ty1, const uint32_t* __restrict__ histA,
+                                                     const uint32_t* __restrict__ totA, int nbA,
+                                                     uint32_t* __restrict__ pgid, uint32_t* __restrict__ pxr,
+                                                     long long pcap) {
+    __shared__ uint32_t cnt[kRbMaxRows];  // pairs per row, then the running staging slot
+    __shared__ uint32_t gb[kRbMaxRows];   // global position of the block's first pair of row r
+    __shared__ uint32_t lb[kRbMaxRows];   // staging position of the block's first pair of row r
+    __shared__ uint32_t sg[kRbStageA], sx[kRbStageA];
+    __shared__ uint8_t sr[kRbStageA];
+    __shared__ uint32_t wsum[kWaves];
+    const int tid = threadIdx.x, R = ty1 - ty0;
+    cnt[tid] = 0u;
+    const int g = blockIdx.x * 256 + tid;
+    int by0 = 0, by1 = 0;  // band-relative rows
+    uint32_t xr = 0;
+    if (g < n && tiles[g]) {
+        const uint4 rr = rect[g];
+        const int miny = (int)(rr.x >> 16), maxy = (int)(rr.y >> 16);
+        by0 = (miny > ty0 ? miny : ty0) - ty0;
+        by1 = (maxy < ty1 ? maxy : ty1) - ty0;
+        xr = (rr.x & 0xFFFFu) | (rr.y << 16);
+    }
+    __syncthreads();
+    for (int r = by0; r < by1; ++r) atomicAdd(&cnt[r], 1u);
+    __syncthreads();
+    uint32_t tot;
+    {
+        const uint32_t c = cnt[tid];
+        const uint32_t ta = tid < R ? totA[tid] : 0u;
+        uint32_t sdum;
+        const uint32_t rowbase = block_exclusive_scan(ta, wsum, &sdum);
+        gb[tid] = tid < R ? rowbase + histA[(size_t)tid * nbA + blockIdx.x] : 0u;
+        lb[tid] = block_exclusive_scan(c, wsum, &tot);
+        cnt[tid] = 0u;
+    }
+    __syncthreads();
+    const bool staged = tot <= (uint32_t)kRbStageA;  // block-uniform
+    for (int r = by0; r < by1; ++r) {
+        const uint32_t k = atomicAdd(&cnt[r], 1u);
+        if (staged) {
+            sg[lb[r] + k] = (uint32_t)g;
+            sx[lb[r] + k] = xr;
+            sr[lb[r] + k] = (uint8_t)r;
+        } else {
+            const long long pos = (long long)gb[r] + k;
+            if (pos < pcap) {
+                pgid[pos] = (uint32_t)g;
+                pxr[pos] = xr;
+            }
+        }
+    }
+    if (!staged) return;
+    __syncthreads();
+    for (int i = tid; i < (int)tot; i += 256) {
+        const int rr = sr[i];
+        const long long pos = (long long)gb[rr] + (uint32_t)i - lb[rr];
+        if (pos < pcap) {
+            pgid[pos] = sg[i];
+            pxr[pos] = sx[i];
+        }
+    }
+}
+
+// Pass-B chunk numbering (every pass-B kernel the same): row r holds ceil(pairs_r / kRbChunk)
+// chunks of its pairs (pairs clamped to the pair capacity), numbered in row order.  Each block
+// builds the rows' pair and chunk bases once in LDS (two block scans over the rows) and then finds
+// a chunk's row by a binary search there.
+struct RbRows {
+    uint32_t pbase[kRbMaxRows];  // the row's first pair
+    uint32_t cbase[kRbMaxRows];  // the row's first chunk
+    uint32_t npair[kRbMaxRows];  // the row's pairs (clamped)
+    uint32_t wsum[kWaves];
+    uint32_t nchunks;            // all rows' chunks
+};
+
+__device__ __forceinline__ void rb_rows_table(const uint32_t* __restrict__ totA, int R, long long pcap, RbRows& t) {
+    const int tid = threadIdx.x;
+    const uint32_t ta = tid < R ? totA[tid] : 0u;
+    uint32_t tp;
+    const uint32_t pb = block_exclusive_scan(ta, t.wsum, &tp);
+    const long long avail = pcap - (long long)pb;
+    const uint32_t tc = avail <= 0 ? 0u : (avail < (long long)ta ? (uint32_t)avail : ta);
+    uint32_t tcs;
+    const uint32_t cb = block_exclusive_scan((tc + kRbChunk - 1) / kRbChunk, t.wsum, &tcs);
+    t.pbase[tid] = pb;
+    t.cbase[tid] = tid < R ? cb : 0xFFFFFFFFu;  // rows past R never match
+    t.npair[tid] = tc;
+    if (tid == 0) t.nchunks = tcs;
+    __syncthreads();
+}
+
+struct RbChunk {
+    int r, k, nch;
+    uint32_t p0, p1, cp;  // pairs [p0, p1); cp: the row's first chunk
+};
+
+__device__ __forceinline__ RbChunk rb_chunk(const RbRows& t, uint32_t b) {
+    // the last row whose first chunk is <= b: a row without chunks shares its first chunk number with
+    // the next row that has some, so the last such row is the one holding chunk b
+    int r = 0;
+#pragma unroll
+    for (int step = kRbMaxRows / 2; step > 0; step >>= 1)
+        if (t.cbase[r + step] <= b) r += step;
+    RbChunk ch;
+    ch.r = r;
+    ch.cp = t.cbase[r];
+    ch.k = (int)(b - ch.cp);
+    ch.nch = (int)((t.npair[r] + kRbChunk - 1) / kRbChunk);
+    ch.p0 = t.pbase[r] + (uint32_t)ch.k * kRbChunk;
+    const uint32_t end = t.pbase[r] + t.npair[r];
+    ch.p1 = ch.p0 + kRbChunk < end ? ch.p0 + kRbChunk : end;
+    return ch;
+}
+
+// pass B, counts: instances of each chunk per column -> histB[gx * cp + c * nch + k].  Blocks walk
+// the chunks (grid-stride), so a grid sized for the worst case costs no empty blocks.
+__global__ __launch_bounds__(256) void rb_chunks_count(const uint32_t* __restrict__ pxr, const uint32_t* __restrict__ totA,
+                                                       int R, int gx, long long pcap, uint32_t* __restrict__ histB) {
+    __shared__ RbRows t;
+    __shared__ uint32_t cnt[kRbMaxCols];
+    const int tid = threadIdx.x;
+    rb_rows_table(totA, R, pcap, t);
+    for (uint32_t b = blockIdx.x; b < t.nchunks; b += gridDim.x) {
+        const RbChunk ch = rb_chunk(t, b);
+        cnt[tid] = 0u;
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kRbChunk / 256; ++q) {
+            const uint32_t p = ch.p0 + q * 256 + tid;
+            if (p < ch.p1) {
+                const uint32_t xr = pxr[p];
+                for (uint32_t c = xr & 0xFFFFu; c < (xr >> 16); ++c) atomicAdd(&cnt[c], 1u);
+            }
+        }
+        __syncthreads();
+        if (tid < gx) histB[(size_t)gx * ch.cp + (size_t)tid * ch.nch + ch.k] = cnt[tid];
+    }
+}
+
+// pass B, scan: block r scans row r's [column][chunk] counts flat (exclusive), takes the row's
+// global base by a decoupled look-back over the rows before it, and stores global positions in
+// place; then the tile ranges of row r ((0, 0) for an empty tile, as F5 leaves it; clamped to cap).
+constexpr int kRbScanThreads = 1024;
+__global__ __launch_bounds__(kRbScanThreads) void rb_tiles_scan(const uint32_t* __restrict__ totA, int R, int gx,
+                                                                int ty0, long long pcap, long long cap,
+                                                                uint32_t* __restrict__ histB,
+                                                                uint32_t* __restrict__ status,
+                                                                uint32_t* __restrict__ ticket,
+                                                                uint2* __restrict__ ranges) {
+    __shared__ uint32_t wsum[kRbScanThreads / 64];
+    __shared__ uint32_t tstart[kRbMaxCols];
+    __shared__ uint32_t s_row[2];
+    __shared__ int s_r;
+    __shared__ uint32_t s_base;
+    const int tid = threadIdx.x, lane = tid & 63;
+    if (tid == 0) s_r = (int)atomicAdd(ticket, 1u);  // rows in dispatch order (the look-back's progress)
+    __syncthreads();
+    const int r = s_r;
+    // the row's chunks, as rb_rows_table numbers them
+    {
+        const uint32_t ta = tid < R ? totA[tid] : 0u;
+        uint32_t tp;
+        const uint32_t pb = block_exclusive_scan(ta, wsum, &tp);
+        const long long avail = pcap - (long long)pb;
+        const uint32_t tc = avail <= 0 ? 0u : (avail < (long long)ta ? (uint32_t)avail : ta);
+        const uint32_t nc = (tc + kRbChunk - 1) / kRbChunk;
+        uint32_t tcs;
+        const uint32_t cb = block_exclusive_scan(nc, wsum, &tcs);
+        if (tid == r) {
+            s_row[0] = nc;
+            s_row[1] = cb;
+        }
+        __syncthreads();
+    }
+    const uint32_t nch = s_row[0], cp = s_row[1];
+    uint32_t* const h = histB + (size_t)gx * cp;
+    const uint32_t E = (uint32_t)gx * nch;
+    const bool one = E <= 4u * kRbScanThreads;  // the common case: the row in one round, in registers
+    const uint32_t i0 = 4 * tid;
+    uint32_t cnts[4] = {0u, 0u, 0u, 0u}, excl = 0, carry = 0;
+    if (one) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cnts[q] = i0 + q < E ? h[i0 + q] : 0u;
+        excl = block_exclusive_scan(cnts[0] + cnts[1] + cnts[2] + cnts[3], wsum, &carry);
+    } else {
+        for (uint32_t base = 0; base < E; base += 4 * kRbScanThreads) {
+            const uint32_t j0 = base + i0;
+            uint32_t v[4], sv = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                v[q] = j0 + q < E ? h[j0 + q] : 0u;
+                sv += v[q];
+            }
+            uint32_t tot;
+            uint32_t run = carry + block_exclusive_scan(sv, wsum, &tot);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (j0 + q < E) h[j0 + q] = run;  // row-relative for now
+                run += v[q];
+            }
+            carry += tot;
+        }
+    }
+    // look-back (wave 0): the instances of rows before r
+    if (tid < 64) {
+        uint32_t excl = 0;
+        if (r == 0) {
+            if (lane == 0) __hip_atomic_store(status, kRbInc | carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (lane == 0) __hip_atomic_store(status + r, kRbAgg | carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int pos = r - 1;
+            uint32_t spins = 0;
+            while (true) {
+                const int idx = pos - lane;
+                uint32_t v = kRbInc;
+                if (idx >= 0) v = __hip_atomic_load(status + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                while (__ballot((v & ~kRbCntMask) == 0u)) {
+                    if (++spins > (1u << 24)) break;  // never expected; bounded so a bug cannot hang
+                    __builtin_amdgcn_s_sleep(1);
+                    if (idx >= 0 && (v & ~kRbCntMask) == 0u)
+                        v = __hip_atomic_load(status + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                const uint64_t inc = __ballot((v & kRbInc) != 0u);
+                const int k = inc ? __builtin_ctzll(inc) : 64;
+                uint32_t c = lane <= k ? (v & kRbCntMask) : 0u;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+                excl += c;
+                if (inc || spins > (1u << 24)) break;
+                pos -= 64;
+            }
+            if (lane == 0) __hip_atomic_store(status + r, kRbInc | (excl + carry), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) s_base = excl;
+    }
+    __syncthreads();
+    const uint32_t rowbase = s_base;
+    if (one) {
+        uint32_t run = rowbase + excl;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (i0 + q < E) {
+                h[i0 + q] = run;
+                if ((i0 + q) % nch == 0) tstart[(i0 + q) / nch] = run;
+                run += cnts[q];
+            }
+        }
+    } else {
+        for (uint32_t i = tid; i < E; i += kRbScanThreads) h[i] += rowbase;
+        __syncthreads();
+        if (tid < gx && nch) tstart[tid] = h[(size_t)tid * nch];
+    }
+    __syncthreads();
+    // tile c of the row: [its first chunk's base, the next tile's)
+    if (tid < gx) {
+        const uint32_t a = nch ? tstart[tid] : rowbase, e = tid + 1 < gx && nch ? tstart[tid + 1] : rowbase + carry;
+        const long long a2 = a < cap ? a : cap, e2 = e < cap ? e : cap;
+        ranges[(size_t)(ty0 + r) * gx + tid] = e2 > a2 ? make_uint2((uint32_t)a2, (uint32_t)e2) : make_uint2(0u, 0u);
+    }
+}
+
+// pass B, placement: each chunk's instances, a slot per instance from its column's LDS counter
+// (order inside a tile is free, as in pass A), staged in LDS by column and written as coalesced
+// column runs (tile key and gid).
+__global__ __launch_bounds__(256) void rb_chunks_place(const uint32_t* __restrict__ pgid, const uint32_t* __restrict__ pxr,
+                                                       const uint32_t* __restrict__ totA, int R, int gx, int ty0,
+                                                       long long pcap, long long cap,
+                                                       const uint32_t* __restrict__ histB,
+                                                       uint32_t* __restrict__ tkey, uint32_t* __restrict__ tgid) {
+    __shared__ RbRows t;
+    __shared__ uint32_t cnt[kRbMaxCols];  // instances per column, then the running staging slot
+    __shared__ uint32_t lb[kRbMaxCols];   // staging start of column c
+    __shared__ uint32_t gb[kRbMaxCols];   // global position of the chunk's first instance of column c
+    __shared__ uint32_t sg[kRbStage];
+    __shared__ uint8_t sc[kRbStage];
+    __shared__ uint32_t wsum[kWaves];
+    const int tid = threadIdx.x;
+    rb_rows_table(totA, R, pcap, t);
+    constexpr int kQ = kRbChunk / 256;
+    for (uint32_t b = blockIdx.x; b < t.nchunks; b += gridDim.x) {
+        const RbChunk ch = rb_chunk(t, b);
+        cnt[tid] = 0u;
+        uint32_t xr[kQ], gg[kQ];
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            const uint32_t p = ch.p0 + q * 256 + tid;
+            xr[q] = p < ch.p1 ? pxr[p] : 0u;  // 0: no columns
+            gg[q] = p < ch.p1 ? pgid[p] : 0u;
+        }
+        __syncthreads();  // cnt zeroed (and the previous chunk's staging read out)
+#pragma unroll
+        for (int q = 0; q < kQ; ++q)
+            for (uint32_t c = xr[q] & 0xFFFFu; c < (xr[q] >> 16); ++c) atomicAdd(&cnt[c], 1u);
+        __syncthreads();
+        uint32_t tot;
+        {
+            const uint32_t c = cnt[tid];
+            lb[tid] = block_exclusive_scan(c, wsum, &tot);
+            gb[tid] = tid < gx ? histB[(size_t)gx * ch.cp + (size_t)tid * ch.nch + ch.k] : 0u;
+            cnt[tid] = 0u;
+        }
+        __syncthreads();
+        const bool staged = tot <= (uint32_t)kRbStage;  // block-uniform
+        const uint32_t row_tile = (uint32_t)(ty0 + ch.r) * (uint32_t)gx;
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            for (uint32_t c = xr[q] & 0xFFFFu; c < (xr[q] >> 16); ++c) {
+                const uint32_t k = atomicAdd(&cnt[c], 1u);
+                if (staged) {
+                    sg[lb[c] + k] = gg[q];
+                    sc[lb[c] + k] = (uint8_t)c;
+                } else {
+                    const long long pos = (long long)gb[c] + k;
+                    if (pos < cap) {
+                        tkey[pos] = row_tile + c;
+                        tgid[pos] = gg[q];
+                    }
+                }
+            }
+        }
+        if (staged) {
+            __syncthreads();
+            for (int i = tid; i < (int)tot; i += 256) {
+                const int c = sc[i];
+                const long long pos = (long long)gb[c] + ((uint32_t)i - lb[c]);
+                if (pos < cap) {
+                    tkey[pos] = row_tile + (uint32_t)c;
+                    tgid[pos] = sg[i];
+                }
+            }
+        }
+        __syncthreads();  // cnt / lb / gb / staging reused by the next chunk
+    }
+}
+
 // ---- F5 finalize: tile ranges from the sorted keys ----
 // Four sorted keys per thread (one 16-B load; the sorted array is 16-B aligned), the neighbours
 // across the quad from the adjacent words (cache hits): 0.075 -> ~0.03 ms at 5M / 1080p.
@@ -636,14 +1025,15 @@ template <int NT, int I, int DB>
 struct SliceLds {
     uint32_t wcnt[NT / 64][1 << DB];
     uint32_t lbase[1 << DB];
-    uint32_t red[2][NT / 64];
+    uint32_t red[4][NT / 64];
     uint32_t skey[NT * I];
     uint32_t sval[NT * I];
 };
 
 template <int NT, int I, int DB>
 __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t* __restrict__ depth_key,
-                                                 uint32_t* __restrict__ gid, SliceLds<NT, I, DB>& lds) {
+                                                 uint32_t* __restrict__ gid, SliceLds<NT, I, DB>& lds,
+                                                 bool unordered = false) {
     constexpr int NWV = NT / 64, BINS = 1 << DB;
     constexpr uint32_t DMASK = BINS - 1u;
     auto& wcnt = lds.wcnt;
@@ -659,7 +1049,7 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
     const int base = w * per;
     const int end = base + per < n ? base + per : n;
     uint32_t key[I], val[I], rank[I];
-    uint32_t kor = 0u, kand = 0xFFFFFFFFu;
+    uint32_t kor = 0u, kand = 0xFFFFFFFFu, vor = 0u, vand = 0xFFFFFFFFu;
 #pragma unroll
     for (int r = 0; r < I; ++r) {
         const int idx = base + r * 64 + lane;
@@ -669,6 +1059,8 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
         if (valid) {
             kor |= key[r];
             kand &= key[r];
+            vor |= val[r];
+            vand &= val[r];
         }
     }
     // bits where the slice's keys differ: passes over constant digits are no-ops (stable)
@@ -676,25 +1068,38 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
     for (int o = 32; o > 0; o >>= 1) {
         kor |= __shfl_xor(kor, o, 64);
         kand &= __shfl_xor(kand, o, 64);
+        vor |= __shfl_xor(vor, o, 64);
+        vand &= __shfl_xor(vand, o, 64);
     }
     if (lane == 0) {
         red[0][w] = kor;
         red[1][w] = kand;
+        red[2][w] = vor;
+        red[3][w] = vand;
     }
     __syncthreads();
-    uint32_t diff = 0u;
+    uint32_t diff = 0u, vdiff = 0u;
     {
-        uint32_t o_ = 0u, a_ = 0xFFFFFFFFu;
+        uint32_t o_ = 0u, a_ = 0xFFFFFFFFu, vo = 0u, va = 0xFFFFFFFFu;
 #pragma unroll
         for (int k = 0; k < NWV; ++k) {
             o_ |= red[0][k];
             a_ &= red[1][k];
+            vo |= red[2][k];
+            va &= red[3][k];
         }
         diff = o_ ^ a_;
+        vdiff = unordered ? vo ^ va : 0u;
     }
     const uint64_t lt = lanemask_lt();
-    for (int shift = 0; shift < 32; shift += DB) {
-        if (((diff >> shift) & DMASK) == 0u) continue;  // block-uniform
+    // An unordered slice (the row-bucketed binning leaves a tile's entries in arbitrary order)
+    // first takes LSD passes over the gid bits, so the depth passes that follow end in (depth,
+    // gid) order; a gid-ordered slice needs the depth passes alone.
+    const int gid_passes = (32 + DB - 1) / DB;
+    for (int pass = unordered ? 0 : gid_passes; pass < 2 * gid_passes; ++pass) {
+        const bool by_val = pass < gid_passes;  // block-uniform
+        const int shift = (by_val ? pass : pass - gid_passes) * DB;
+        if ((((by_val ? vdiff : diff) >> shift) & DMASK) == 0u) continue;  // block-uniform
         for (int d = tid; d < NWV * BINS; d += NT) (&wcnt[0][0])[d] = 0u;
         __syncthreads();
 #pragma unroll
@@ -702,7 +1107,7 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
             if (base + r * 64 >= end) break;  // wave-uniform: only the rounds holding keys
             const int idx = base + r * 64 + lane;
             const bool valid = idx < end;
-            const uint32_t d = (key[r] >> shift) & DMASK;
+            const uint32_t d = ((by_val ? val[r] : key[r]) >> shift) & DMASK;
             const uint64_t peers = match_digit<DB>(d, DB, __ballot(valid));
             const uint32_t old = wcnt[w][d];
             rank[r] = old + (uint32_t)__popcll(peers & lt);
@@ -747,7 +1152,7 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
         for (int r = 0; r < I; ++r) {
             const int idx = base + r * 64 + lane;
             if (idx < end) {
-                const uint32_t d = (key[r] >> shift) & DMASK;
+                const uint32_t d = ((by_val ? val[r] : key[r]) >> shift) & DMASK;
                 const uint32_t lp = lbase[d] + wcnt[w][d] + rank[r];
                 skey[lp] = key[r];
                 sval[lp] = val[r];
@@ -772,12 +1177,210 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
     __syncthreads();  // red[] is rewritten by the next slice
 }
 
+// ---- per-tile depth order, register form: one wave per tile ----
+// A slice of n <= 64 E entries (E = 1 .. kWaveSortMaxE, the smallest power of two that holds it)
+// is sorted by one wave in VGPRs as 64-bit (depth << 32 | gid) keys with a bitonic network: lane l
+// holds entries l E .. l E + E - 1, so exchanges at distances below E stay inside a lane and the
+// rest go lane to lane by DPP (lane xor 1 / 2 / 3, row mirrors, row_ror 8), ds_swizzle (xor 4,
+// 16, 31 inside 32-lane halves) and ds_bpermute (across the halves).  The gid in the low word
+// makes every key distinct, so the result is the canonical (depth, gid) order whatever order the
+// slice arrives in (no stability needed), and there is no LDS, no barrier and no per-pass
+// histogram: ~log2(64 E)^2 / 2 compare-exchange stages of 5-6 VALU ops per key pair, against the
+// LDS radix form's dependent counter updates and ~6 barriers per pass (latency-bound per block).
+// "Flip" network (every merge ascending: its first stage pairs i with i ^ (k - 1), mirrored).
+#ifndef GSR_WAVE_SORT_MAX_E
+#define GSR_WAVE_SORT_MAX_E 32
+#endif
+#ifndef GSR_TILE_WAVE_SORT
+#define GSR_TILE_WAVE_SORT 1
+#endif
+constexpr int kWaveSortMaxE = GSR_WAVE_SORT_MAX_E;
+static_assert(kWaveSortMaxE == 16 || kWaveSortMaxE == 32, "wave sort: up to 1024 or 2048 entries");
+
+// x from lane (lane ^ M) of the wave, M = 2^a - 1 (mirror stages) or 2^a (half cleaners)
+template <int M>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t x) {
+    static_assert(M >= 1 && M <= 63, "lane_xor distance");
+    if constexpr (M == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);
+    else if constexpr (M == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);
+    else if constexpr (M == 3) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x1B, 0xF, 0xF, false);
+    else if constexpr (M == 7) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false);
+    else if constexpr (M == 15) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false);
+    else if constexpr (M == 8) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xF, 0xF, false);
+    else if constexpr (M == 4 || M == 16 || M == 31)  // bit mode: and 0x1f, xor M, inside 32-lane halves
+        return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (M << 10));
+    else return (uint32_t)__shfl_xor((int)x, M, 64);  // 32, 63: across the halves
+}
+
+template <int M>
+__device__ __forceinline__ uint64_t lane_xor64(uint64_t x) {
+    return ((uint64_t)lane_xor<M>((uint32_t)(x >> 32)) << 32) | lane_xor<M>((uint32_t)x);
+}
+
+// flip = 0: keep min(a, b); flip = ~0: keep max(a, b).  Keys are below 2^63 (a positive float's
+// bits over a gid; padding 2^63 - 1), so the sign of a - b orders them; the select is a bit
+// insert on that sign -- VALU only (a compare into an SGPR mask and a scalar XOR with the lane
+// side would put a VALU -> SALU -> VALU round trip on every element).
+// (m & x) | (~m & y) in one v_bfi_b32 (written out, the compiler turns it back into a compare
+// into an SGPR mask + v_cndmask, with its s_nop hazard per element)
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t x, uint32_t y) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(x), "v"(y));
+    return r;
+}
+
+__device__ __forceinline__ uint64_t keep_side(uint64_t a, uint64_t b, uint32_t flip) {
+    const uint32_t m = (uint32_t)((int64_t)(a - b) >> 63) ^ flip;  // ~0: keep a
+    return ((uint64_t)bfi(m, (uint32_t)(a >> 32), (uint32_t)(b >> 32)) << 32) | bfi(m, (uint32_t)a, (uint32_t)b);
+}
+
+__device__ __forceinline__ void cas_up(uint64_t& a, uint64_t& b) {
+    const uint32_t m = (uint32_t)((int64_t)(a - b) >> 63);  // ~0: a < b
+    const uint32_t ah = (uint32_t)(a >> 32), al = (uint32_t)a, bh = (uint32_t)(b >> 32), bl = (uint32_t)b;
+    a = ((uint64_t)bfi(m, ah, bh) << 32) | bfi(m, al, bl);
+    b = ((uint64_t)bfi(m, bh, ah) << 32) | bfi(m, bl, al);
+}
+
+// half cleaners of distance J, J / 2, .., 1
+template <int E, int J>
+__device__ __forceinline__ void wave_half_cleaners(uint64_t (&v)[E], int lane) {
+    if constexpr (J >= 1) {
+        if constexpr (J >= E) {
+            constexpr int L = J / E;
+            const uint32_t flip = (lane & L) ? ~0u : 0u;
+#pragma unroll
+            for (int e = 0; e < E; ++e) v[e] = keep_side(v[e], lane_xor64<L>(v[e]), flip);
+        } else {
+#pragma unroll
+            for (int e = 0; e < E; ++e)
+                if ((e & J) == 0) cas_up(v[e], v[e ^ J]);
+        }
+        wave_half_cleaners<E, J / 2>(v, lane);
+    }
+}
+
+// merges of size K, 2K, .., 64 E
+template <int E, int K>
+__device__ __forceinline__ void wave_bitonic(uint64_t (&v)[E], int lane) {
+    if constexpr (K <= 64 * E) {
+        if constexpr (K <= E) {
+#pragma unroll
+            for (int e = 0; e < E; ++e)
+                if ((e & (K / 2)) == 0) cas_up(v[e], v[e ^ (K - 1)]);
+        } else {
+            // entry i = lane E + e pairs with i ^ (K - 1): lane ^ (K / E - 1), entry E - 1 - e
+            constexpr int M = K / E - 1;
+            const uint32_t flip = (lane & (K / (2 * E))) ? ~0u : 0u;
+            if constexpr (E == 1) {
+                v[0] = keep_side(v[0], lane_xor64<M>(v[0]), flip);
+            } else {
+#pragma unroll
+                for (int e = 0; e < E / 2; ++e) {
+                    const uint64_t pa = lane_xor64<M>(v[E - 1 - e]), pb = lane_xor64<M>(v[e]);
+                    v[e] = keep_side(v[e], pa, flip);
+                    v[E - 1 - e] = keep_side(v[E - 1 - e], pb, flip);
+                }
+            }
+        }
+        wave_half_cleaners<E, K / 4>(v, lane);
+        wave_bitonic<E, 2 * K>(v, lane);
+    }
+}
+
+// The slice is read coalesced (entry e * 64 + lane into register e: the network sorts whatever
+// order it is given) and, sorted (rank lane E + e in register e), written back through the wave's
+// LDS rows so the stores are coalesced too (`xs`: 64 E + 64 E / 32 words, rows padded against bank
+// conflicts).
+template <int E>
+__device__ __forceinline__ void wave_sort_slice(const uint2 rg, const uint32_t* __restrict__ depth_key,
+                                                uint32_t* __restrict__ gid, int lane, uint32_t* xs) {
+    const int n = (int)(rg.y - rg.x);
+    uint64_t v[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = e * 64 + lane;
+        uint64_t k = 0x7FFFFFFFFFFFFFFFull;  // padding sorts last (no real key reaches it)
+        if (i < n) {
+            const uint32_t g = gid[rg.x + i];
+            k = ((uint64_t)depth_key[g] << 32) | g;
+        }
+        v[e] = k;
+    }
+    wave_bitonic<E, 2>(v, lane);
+    auto pad = [](int i) { return i + (i >> 5); };
+#pragma unroll
+    for (int e = 0; e < E; ++e) xs[pad(lane * E + e)] = (uint32_t)v[e];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = e * 64 + lane;
+        if (i < n) gid[rg.x + i] = xs[pad(i)];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();  // xs reused by the wave's next slice
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Four tiles per 256-thread block, one per wave; slices longer than 1024 entries go to `ovf`.
+__global__ __launch_bounds__(256) void tile_depth_wave(const uint2* __restrict__ ranges, int tile0, int ntiles,
+                                                      const uint32_t* __restrict__ depth_key,
+                                                      uint32_t* __restrict__ gid, uint32_t* __restrict__ ovf,
+                                                      uint32_t* __restrict__ ovf_count) {
+    __shared__ uint32_t xs_all[4][64 * 16 + 32];
+    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= ntiles) return;
+    const int lane = threadIdx.x & 63;
+    uint32_t* const xs = xs_all[threadIdx.x >> 6];
+    const int tile = tile0 + t;
+    const uint2 rg = ranges[tile];
+    const int n = (int)(rg.y - rg.x);
+    if (n <= 1) return;
+    if (n > 1024) {
+        if (lane == 0) ovf[atomicAdd(ovf_count, 1u)] = (uint32_t)tile;
+        return;
+    }
+    if (n <= 64) wave_sort_slice<1>(rg, depth_key, gid, lane, xs);
+    else if (n <= 128) wave_sort_slice<2>(rg, depth_key, gid, lane, xs);
+    else if (n <= 256) wave_sort_slice<4>(rg, depth_key, gid, lane, xs);
+    else if (n <= 512) wave_sort_slice<8>(rg, depth_key, gid, lane, xs);
+    else wave_sort_slice<16>(rg, depth_key, gid, lane, xs);
+}
+
+// The queued slices of 1025 .. 64 kWaveSortMaxE entries, one wave each (a kernel of its own: the
+// 32-entry-per-lane form needs ~190 VGPRs, which would cap the common form's occupancy at 2 waves
+// per SIMD); longer ones go on to `ovf3` for the LDS forms.  The queue length is on the device.
+__global__ __launch_bounds__(256) void tile_depth_wave_queue(const uint2* __restrict__ ranges,
+                                                            const uint32_t* __restrict__ depth_key,
+                                                            uint32_t* __restrict__ gid,
+                                                            const uint32_t* __restrict__ ovf,
+                                                            const uint32_t* __restrict__ ovf_count,
+                                                            uint32_t* __restrict__ ovf3,
+                                                            uint32_t* __restrict__ ovf3_count) {
+    __shared__ uint32_t xs_all[4][64 * kWaveSortMaxE + 2 * kWaveSortMaxE];
+    const uint32_t cnt = *ovf_count;
+    const int lane = threadIdx.x & 63;
+    uint32_t* const xs = xs_all[threadIdx.x >> 6];
+    for (uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6); q < cnt; q += gridDim.x * 4) {
+        const uint32_t tile = ovf[q];
+        const uint2 rg = ranges[tile];
+        const int n = (int)(rg.y - rg.x);
+        if (n > 64 * kWaveSortMaxE) {
+            if (lane == 0) ovf3[atomicAdd(ovf3_count, 1u)] = tile;
+            continue;  // wave-uniform
+        }
+        if constexpr (kWaveSortMaxE == 32) wave_sort_slice<32>(rg, depth_key, gid, lane, xs);
+        else wave_sort_slice<16>(rg, depth_key, gid, lane, xs);
+    }
+}
+
 // One block per tile of the launch; slices longer than NT * I go to the queue `ovf`.
 template <int NT, int I, int DB>
 __global__ __launch_bounds__(NT) void tile_depth_radix(const uint2* __restrict__ ranges, int tile0,
                                                       const uint32_t* __restrict__ depth_key,
                                                       uint32_t* __restrict__ gid, uint32_t* __restrict__ ovf,
-                                                      uint32_t* __restrict__ ovf_count) {
+                                                      uint32_t* __restrict__ ovf_count, int unordered) {
     const int tile = tile0 + blockIdx.x;
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
@@ -787,7 +1390,7 @@ __global__ __launch_bounds__(NT) void tile_depth_radix(const uint2* __restrict__
         return;
     }
     __shared__ SliceLds<NT, I, DB> lds;
-    radix_sort_slice<NT, I, DB>(rg, depth_key, gid, lds);
+    radix_sort_slice<NT, I, DB>(rg, depth_key, gid, lds, unordered != 0);
 }
 
 // The queued (longer) slices: blocks walk the queue; slices longer than NT * I go on to the
@@ -799,7 +1402,8 @@ __global__ __launch_bounds__(NT) void tile_depth_radix_queue(const uint2* __rest
                                                             uint32_t* __restrict__ gid,
                                                             const uint32_t* __restrict__ ovf,
                                                             const uint32_t* __restrict__ ovf_count,
-                                                            uint32_t* __restrict__ ovf2, uint32_t* __restrict__ ovf2_count) {
+                                                            uint32_t* __restrict__ ovf2, uint32_t* __restrict__ ovf2_count,
+                                                            int unordered) {
     __shared__ SliceLds<NT, I, DB> lds;
     const uint32_t cnt = *ovf_count;
     for (uint32_t q = blockIdx.x; q < cnt; q += gridDim.x) {
@@ -809,7 +1413,7 @@ __global__ __launch_bounds__(NT) void tile_depth_radix_queue(const uint2* __rest
             if (threadIdx.x == 0) ovf2[atomicAdd(ovf2_count, 1u)] = tile;
             continue;  // block-uniform
         }
-        radix_sort_slice<NT, I, DB>(rg, depth_key, gid, lds);
+        radix_sort_slice<NT, I, DB>(rg, depth_key, gid, lds, unordered != 0);
     }
 }
 
@@ -849,8 +1453,8 @@ __shared__ union BigLds {
 } g_big;
 
 __device__ __attribute__((noinline)) void big_slice_sort(const uint2 rg, const uint32_t* __restrict__ depth_key,
-                                                         uint32_t* __restrict__ gid) {
-    radix_sort_slice<1024, 16, 8>(rg, depth_key, gid, g_big.slice);
+                                                         uint32_t* __restrict__ gid, bool unordered) {
+    radix_sort_slice<1024, 16, 8>(rg, depth_key, gid, g_big.slice, unordered);
 }
 
 __device__ __attribute__((noinline)) void merge_sorted_chunks(const uint2 r, const uint32_t* __restrict__ depth_key,
@@ -913,7 +1517,8 @@ __global__ __launch_bounds__(1024) void tile_depth_sort_big(const uint2* __restr
                                                             const uint32_t* __restrict__ ovf,
                                                             const uint32_t* __restrict__ ovf_count,
                                                             uint32_t* __restrict__ done,
-                                                            uint32_t* __restrict__ hi, uint32_t* __restrict__ lo) {
+                                                            uint32_t* __restrict__ hi, uint32_t* __restrict__ lo,
+                                                            int unordered) {
     __shared__ uint32_t last;
     const uint32_t cnt = *ovf_count;
     // item-major: the first cnt work items are every tile's item 0, spread over all blocks
@@ -928,7 +1533,7 @@ __global__ __launch_bounds__(1024) void tile_depth_sort_big(const uint2* __restr
         if (item >= parts) continue;  // block-uniform
         for (uint32_t c0 = r.x + item * kBigChunk; c0 < r.y; c0 += 8u * kBigChunk) {
             const uint32_t c1 = whole || c0 + kBigChunk >= r.y ? r.y : c0 + kBigChunk;
-            big_slice_sort(make_uint2(c0, c1), depth_key, gid);
+            big_slice_sort(make_uint2(c0, c1), depth_key, gid, unordered != 0);
         }
         if (whole) continue;
         __threadfence();  // this item's chunks visible device-wide before it counts itself done
@@ -982,9 +1587,9 @@ int radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* k0, u
 }
 
 int launch_scan(const uint32_t* tiles, int n, uint32_t* offsets, uint32_t* scan_partials_buf, uint32_t* total_out,
-                hipStream_t s) {
+                hipStream_t s, bool fused_ok) {
     if (n <= 0) return (int)hipMemsetAsync(total_out, 0, sizeof(uint32_t), s);
-    if (n <= kFusedScanMax) return 0;  // scanned by the fused kernel in launch_duplicate
+    if (fused_ok && n <= kFusedScanMax) return 0;  // scanned by the fused kernel in launch_duplicate
     const int nb = sort_blocks(n);
     hipLaunchKernelGGL(scan_reduce, dim3(nb), dim3(kB), 0, s, tiles, n, scan_partials_buf);
     hipLaunchKernelGGL(scan_partials, dim3(1), dim3(1024), 0, s, scan_partials_buf, nb, total_out);
@@ -992,11 +1597,35 @@ int launch_scan(const uint32_t* tiles, int n, uint32_t* offsets, uint32_t* scan_
     return (int)hipGetLastError();
 }
 
+int launch_rb_binning(const uint32_t* tiles, uint4* rect, const uint32_t* offsets, int n, int gx, int ty0, int ty1,
+                      uint32_t* histA, uint32_t* histB, uint32_t* rb_status, uint32_t* pgid, uint32_t* pxr,
+                      uint32_t* tkey, uint32_t* tgid, uint2* ranges, long long cap, hipStream_t s) {
+    const int R = ty1 - ty0;
+    if (n <= 0 || R <= 0 || cap <= 0) return 0;  // ranges stay cleared
+    if (R > kRbMaxRows || gx > kRbMaxCols) return (int)hipErrorInvalidValue;
+    const int nbA = div_up(n, 256);
+    uint32_t* const totA = histA + (size_t)256 * nbA;
+    hipLaunchKernelGGL(rb_rows_count, dim3(nbA), dim3(256), 0, s, tiles, rect, offsets, n, ty0, ty1, histA, nbA);
+    hipLaunchKernelGGL(radix_colscan, dim3(R), dim3(kB), 0, s, histA, nbA, totA);
+    hipLaunchKernelGGL(rb_rows_place, dim3(nbA), dim3(256), 0, s, tiles, rect, n, ty0, ty1, histA, totA, nbA, pgid, pxr,
+                       cap);
+    // chunks: at most cap / kRbChunk full ones plus one partial per row; the blocks walk them, so
+    // the grid is capped near what the chip holds at once (no tail of empty blocks)
+    const int nch_max = div_up(cap, kRbChunk) + R;
+    const int gcount = nch_max < 2048 ? nch_max : 2048, gplace = nch_max < 1280 ? nch_max : 1280;
+    hipLaunchKernelGGL(rb_chunks_count, dim3(gcount), dim3(256), 0, s, pxr, totA, R, gx, cap, histB);
+    hipLaunchKernelGGL(rb_tiles_scan, dim3(R), dim3(kRbScanThreads), 0, s, totA, R, gx, ty0, cap, cap, histB,
+                       rb_status + 16, rb_status, ranges);
+    hipLaunchKernelGGL(rb_chunks_place, dim3(gplace), dim3(256), 0, s, pgid, pxr, totA, R, gx, ty0, cap, cap, histB,
+                       tkey, tgid);
+    return (int)hipGetLastError();
+}
+
 int launch_duplicate(const uint32_t* tiles, uint4* rect, int n, int grid_x, int ty0, uint32_t* offsets,
                      uint32_t* lookback, uint32_t* tkey, uint32_t* tgid, long long cap, uint32_t* total_out,
-                     hipStream_t s) {
+                     hipStream_t s, bool scanned) {
     if (n <= 0) return 0;
-    if (n <= kFusedScanMax) {  // fused look-back scan + duplicate
+    if (n <= kFusedScanMax && !scanned) {  // fused look-back scan + duplicate
         const int nb = div_up(n, 256);
         if (hipError_t e = hipMemsetAsync(lookback, 0, sizeof(uint32_t) * (16 + (size_t)nb), s)) return (int)e;
         hipLaunchKernelGGL(scan_duplicate_kernel, dim3(nb), dim3(256), 0, s, tiles, rect, n, grid_x, ty0, offsets,
@@ -1031,22 +1660,44 @@ int launch_duplicate_ranked(const uint32_t* rtiles, const uint4* rrect, uint4* r
     return (int)hipGetLastError();
 }
 
+// the LDS slice capacity the per-tile sort picks for a mean slice of K / ntiles entries
+static int tile_sort_cap(long long K, int ntiles) {
+    const long long mean = ntiles > 0 ? K / ntiles : K;
+    int cap = 1024;
+    while (cap < 4096 && cap < mean + mean / 2) cap <<= 1;
+    return cap;
+}
+
+bool tile_wave_sort_eligible(long long K, int ntiles) { return GSR_TILE_WAVE_SORT && tile_sort_cap(K, ntiles) <= 2048; }
+
 int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long K, const uint32_t* depth_key,
                            uint32_t* gid, uint32_t* ovf, uint32_t* ovf_count, uint32_t* ovf2, uint32_t* ovf2_count,
-                           uint32_t* done, uint32_t* scratch_hi, uint32_t* scratch_lo,
-                           hipStream_t s) {
+                           uint32_t* ovf3, uint32_t* ovf3_count, uint32_t* done, uint32_t* scratch_hi,
+                           uint32_t* scratch_lo, hipStream_t s, bool unordered) {
     if (ntiles <= 0 || K <= 0) return 0;
+    const int uo = unordered ? 1 : 0;
     // one block per tile holding up to cap entries in LDS, a power of two >= 1.5x the mean slice
     // (1024 .. 4096: <= 43 KB of LDS, 3 blocks per CU); longer slices queue for 512-thread blocks
     // of up to 8192 (73 KB: 2 per CU) walking the queue, and beyond that for tile_depth_sort_big
-    const long long mean = K / ntiles;
-    int cap = 1024;
     // (one 8192-entry block per tile at 5M / 1080p: 0.89 ms with 512 threads, 0.79 with 1024,
     // against 0.49 for 4096-entry blocks + the queue: 1 block per CU)
-    while (cap < 4096 && cap < mean + mean / 2) cap <<= 1;
-#define GSR_TILE_RADIX(NT_, I_)                                                                          \
+    const int cap = tile_sort_cap(K, ntiles);
+    // slices of up to 64 kWaveSortMaxE entries sorted in registers, one wave each, whenever the
+    // mean slice leaves most tiles within that (the longer ones queue for the LDS forms below)
+    const bool wave = tile_wave_sort_eligible(K, ntiles);
+    if (wave) {
+        hipLaunchKernelGGL(tile_depth_wave, dim3(div_up(ntiles, 4)), dim3(256), 0, s, ranges, tile0, ntiles, depth_key,
+                           gid, ovf, ovf_count);
+        const int wgrid = ntiles < 2048 ? div_up(ntiles, 4) : 512;
+        hipLaunchKernelGGL(tile_depth_wave_queue, dim3(wgrid), dim3(256), 0, s, ranges, depth_key, gid, ovf, ovf_count,
+                           ovf3, ovf3_count);
+        // the LDS forms below take the slices the register form could not
+        ovf = ovf3;
+        ovf_count = ovf3_count;
+    } else {
+#define GSR_TILE_RADIX(NT_, I_)                                                                       \
     hipLaunchKernelGGL((tile_depth_radix<NT_, I_, 9>), dim3(ntiles), dim3(NT_), 0, s, ranges, tile0, depth_key, \
-                       gid, ovf, ovf_count)
+                       gid, ovf, ovf_count, uo)
 #ifndef GSR_BAND_SORT_NT
 #define GSR_BAND_SORT_NT 512
 #endif
@@ -1075,13 +1726,14 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
     else if (cap == 2048) GSR_TILE_RADIX(256, 8);
     else GSR_TILE_RADIX(256, 16);
 #undef GSR_TILE_RADIX
+    }
     const int qgrid = ntiles < 512 ? ntiles : 512;
     hipLaunchKernelGGL((tile_depth_radix_queue<512, 16, 8>), dim3(qgrid), dim3(512), 0, s, ranges, depth_key, gid, ovf,
-                       ovf_count, ovf2, ovf2_count);
+                       ovf_count, ovf2, ovf2_count, uo);
     // slices beyond 8192: the 16384-entry LDS form and the chunked form (tile_depth_sort_big)
     const int bgrid = ntiles < 256 ? ntiles : 256;
     hipLaunchKernelGGL(tile_depth_sort_big, dim3(bgrid), dim3(1024), 0, s, ranges, depth_key, gid, ovf2, ovf2_count,
-                       done, scratch_hi, scratch_lo);
+                       done, scratch_hi, scratch_lo, uo);
     return (int)hipGetLastError();
 }
 

@@ -444,6 +444,10 @@ def main():
         # every stage's algorithmic bytes over its measured time, as a fraction of 8 TB/s (tracked
         # per round: VERDICT r04 item 5); the blend stages are bound by VALU issue, not HBM
         sb = stage_bytes(P_local, V, K, pix_local, tiles_local, M)
+        if "duplicate" not in result["stage_ms"] and "tile_sort" in result["stage_ms"]:
+            # row-bucketed binning (gsr_sort.hip): F3, the tile sort and F5 are one timed stage
+            sb["tile_sort"] += sb["duplicate"] + sb["finalize"]
+            result["binning"] = "row-bucketed: F3 + tile sort + F5 timed as tile_sort"
         result["stage_hbm_frac"] = {k: round(sb[k] / (result["stage_ms"][k] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
                                     for k in sb if result["stage_ms"].get(k)}
         dom = dom_stage

@@ -120,7 +120,7 @@ typedef struct gsr_buffers {
                                 the device (max_rendered > 0; see gsr_read_num_rendered) */
     int32_t capacity;        /* instances the binning (and the backward's scratch) hold */
     int32_t n_local;         /* Gaussians (or received splat slots, gsr_band_forward) indexed */
-    int32_t reserved;
+    int32_t reserved;        /* set by the forward: the binning in use (keep it with the buffers) */
 } gsr_buffers;
 
 int gsr_abi_version(void);

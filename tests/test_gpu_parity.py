@@ -119,6 +119,8 @@ CONFIGS = [  # (P, W, H, active D, seed)
     (1001, 256, 256, 3, 5),      # P % 4 != 0: the SH rows' DMA pieces of the last block end
     (4097, 300, 200, 3, 6),      #   inside a 16-B piece (F1 and B2 staging)
     (20000, 2400, 1800, 1, 3),   # 16950 tiles: 15 tile bits (8 + 7 per radix pass)
+    (30000, 4096, 512, 1, 7),    # 256 tile columns: the row-bucketed binning's widest image
+    (5000, 4112, 240, 1, 8),     # 257 tile columns: past it, the radix tile sort
 ]
 
 
@@ -140,6 +142,25 @@ def test_synthetic_parity(P, W, H, D, seed, rast, oracle):
     tt = _np(st.view(pkg("native").VIEW_TILES_TOUCHED, torch.int32, P)).view(np.uint32)
     np.testing.assert_array_equal(tt, pre["tiles_touched"])
     _compare(st, f, dpix, rast)
+
+
+@pytest.mark.parametrize("smod", [4.0, 12.0])
+def test_large_splats_vs_oracle(smod, rast, oracle):
+    """Splats spanning many tile rows and columns (scale_modifier 4 / 12 on a 640x480 scene):
+    the row-bucketed binning's blocks overflow their LDS staging (more than 2048 (Gaussian, row)
+    pairs per 256 Gaussians, more than 4096 instances per 1024 pairs) and write straight to HBM;
+    sorted (tile, gid) list, ranges, image and gradients against the oracle as everywhere."""
+    gr, sc = pkg("graphics"), pkg("scene")
+    cam = gr.synthetic_camera(640, 480)
+    s = sc.make_scene(cam, 3000, max_sh_degree=3, seed=9)
+    dpix = sc.make_dL_dpix(cam, seed=10)
+    args = (cam, s.means3D, s.opacities, s.scales, s.rotations, s.sh_dc, s.sh_rest)
+    st = rast.forward(*args, sh_degree=3, scale_modifier=smod)
+    f = oracle.forward(*args, sh_degree=3, scale_modifier=smod)
+    pre = f.state.preprocess()
+    vis = f.radii > 0
+    assert pre["tiles_touched"][vis].mean() > 8  # many instances per splat
+    _compare(st, f, dpix, rast, elem_grads=False)
 
 
 def test_band_render_equals_full(rast):
