@@ -212,7 +212,7 @@ struct Views {
     float4* rec;
     uint4* rect;
     uint2* ranges;
-    uint32_t *counters, *K_dev, *ovf, *ovf2, *ovf3, *done, *term;
+    uint32_t *counters, *K_dev, *ovf, *ovf2, *done, *term;
     float *final_T, *accum;
     float4* ck;  // the checkpoint pool (binning buffer)
     uint32_t *kA, *vA, *kB, *vB, *hist;
@@ -250,7 +250,6 @@ Views views(const gsr_camera* cam, long long n, const gsr_buffers* b) {
     v.K_dev = v.counters + kTotalSlot;
     v.ovf = at<uint32_t>(b->image, il.ovf);
     v.ovf2 = at<uint32_t>(b->image, il.ovf2);
-    v.ovf3 = at<uint32_t>(b->image, il.ovf3);
     v.rb_status = at<uint32_t>(b->image, il.rb_status);
     v.done = at<uint32_t>(b->image, il.done);
     v.term = at<uint32_t>(b->image, il.term);
@@ -299,6 +298,7 @@ struct FwdJob {
     long long n = 0;  // Gaussians (or splat slots) indexed
     int ty0 = 0, ty1 = 0, gx = 0, gy = 0;
     int vgy = 0, vh = 0;  // views mode: tile rows per view band, pixel rows per view (0: one image)
+    bool rows_counted = false;  // F1 wrote the row-bucketed binning's pass-A counts (run_preprocess)
 };
 
 // Allocations (geometry from the caller when geom_ready), range / counter clears, background
@@ -373,12 +373,11 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
         // F3 + the tile sort + F5 as two counting passes; the pairs ride in (kB, vB)
         GSR_STAGE(GSR_STAGE_TILE_SORT, launch_rb_binning(v.tiles, v.rect, v.offsets, (int)j.n, j.gx, j.ty0, j.ty1,
                                                          v.rb_histA, v.rb_histB, v.rb_status, v.kB, v.vB, v.kA, v.vA,
-                                                         v.ranges, cap, stream),
+                                                         v.ranges, cap, stream, j.rows_counted),
                   "row-bucketed binning");
         GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_tile_depth_sort(v.ranges, j.ty0 * j.gx, ntiles, cap, v.depth_key,
                                                                v.sorted_gid, v.ovf, v.counters + kOvfCountSlot, v.ovf2,
-                                                               v.counters + kOvf2CountSlot, v.ovf3,
-                                                               v.counters + kOvf3CountSlot, v.done, v.free_k,
+                                                               v.counters + kOvf2CountSlot, v.done, v.free_k,
                                                                v.free_v, stream, true),
                   "per-tile depth order");
     } else if (cap > 0) {
@@ -393,8 +392,7 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
         if (!v.presort)
             GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_tile_depth_sort(v.ranges, j.ty0 * j.gx, ntiles, cap, v.depth_key,
                                                                v.sorted_gid, v.ovf, v.counters + kOvfCountSlot, v.ovf2,
-                                                               v.counters + kOvf2CountSlot, v.ovf3,
-                                                               v.counters + kOvf3CountSlot, v.done, v.free_k,
+                                                               v.counters + kOvf2CountSlot, v.done, v.free_k,
                                                                v.free_v, stream),
                   "per-tile depth order");
     }
@@ -433,6 +431,8 @@ int run_preprocess(const gsr_camera* cam, const gsr_gaussians* gs, int ty0, int 
     // own Gaussians alone, and B2 recomputes the bits (stored_flags)
     const bool full = ty0 == 0 && ty1 == div_up(cam->height, kTile);
     PreOut po{radii, v.depth_key, v.tiles, v.rec, v.rect, full ? v.flags : nullptr, v.counters};
+    // the row-bucketed binning's pass-A row counts, from F1 itself (fwd_phase2 then skips them)
+    if (use_rb_binning(gs->P, div_up(cam->width, kTile), div_up(cam->height, kTile))) po.rb_hist = v.rb_histA;
     GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess(*cam, gauss_in(gs), ty0, ty1, po, stream), "preprocess");
     return 0;
 }
@@ -575,6 +575,7 @@ int gsr_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raster
     const bool exact = rs->max_rendered == 0;
     if (int e = fwd_phase1(j, alloc_geom, alloc_image, ctx, stream, debug, false, [&](const Views& v) {
             if (int e2 = run_preprocess(cam, gs, j.ty0, j.ty1, radii, v, stream, debug)) return e2;
+            j.rows_counted = true;
             // exact sizing: F1's count partials go to the host while the scan runs
             if (exact && gs->P > 0) GSR_CHECK_HIP(begin_read(v.counters, 2 * kCountSlots, stream), "read counts");
             return 0;
@@ -637,6 +638,7 @@ int gsr_forward_batch(int32_t V, const gsr_camera* cams, const gsr_gaussians* gs
         jobs[v].n = gs->P;
         int32_t* rad = gs->P > 0 ? radii[v] : nullptr;
         if (int e = fwd_phase1(jobs[v], alloc_geom, alloc_image, ctx, stream, debug, false, [&](const Views& vw) {
+                jobs[v].rows_counted = true;
                 return run_preprocess(&cams[v], gs, jobs[v].ty0, jobs[v].ty1, rad, vw, stream, debug);
             }))
             return e;

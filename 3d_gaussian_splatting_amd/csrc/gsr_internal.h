@@ -185,7 +185,7 @@ struct BinLayout {
 };
 
 struct ImgLayout {
-    size_t ranges, counters, rb_status, done, ovf, ovf2, ovf3, term, final_T, accum, total;
+    size_t ranges, counters, rb_status, done, ovf, ovf2, term, final_T, accum, total;
     static size_t tile_count(int W, int H) {
         const size_t t = (size_t)div_up(W, kTile) * div_up(H, kTile);
         return t ? t : 1;
@@ -202,7 +202,6 @@ struct ImgLayout {
                                  // done: chunks sorted per queued tile)
         ovf = take(4 * tiles);   // tiles the per-tile depth sort hands to its larger
         ovf2 = take(4 * tiles);  // forms (queues: the 8192-entry form, then the 16384-entry / chunked one)
-        ovf3 = take(4 * tiles);  // register form: slices past one wave's 1024 entries (2048-entry waves)
         term = take(4 * tiles * kMaxChunks);  // F6: per tile [termination index, chunk 1..kMaxChunks-1 starts]
         final_T = take(4 * (pix ? pix : 1));
         accum = take(12 * (pix ? pix : 1));  // colour sum without background, 3 x H x W
@@ -261,7 +260,6 @@ struct ShardLayout {
 constexpr int kTotalSlot = 2 * kCountSlots;          // K = sum of tiles_touched, written by the scan
 constexpr int kOvfCountSlot = 2 * kCountSlots + 8;   // tiles queued for the large per-tile depth sort
 constexpr int kOvf2CountSlot = 2 * kCountSlots + 9;  // ... then for its 16384-entry / chunked form
-constexpr int kOvf3CountSlot = 2 * kCountSlots + 10; // register form: past 2048 entries, to the LDS forms
 
 // number of 8-bit LSD passes to sort tile ids of a grid with `tiles` tiles
 inline int tile_bits(int tiles) {

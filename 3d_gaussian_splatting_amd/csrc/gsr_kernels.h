@@ -22,6 +22,8 @@ struct PreOut {
     uint32_t* flags;     // nullable: SH clamp bits per Gaussian (B2 recomputes them when absent)
     uint32_t* counters;  // nullable, zeroed: [slot] += Gaussians with tiles in the band,
                          // [kCountSlots + slot] += K (slot = block % kCountSlots)
+    uint32_t* rb_hist = nullptr;  // nullable (one view only): per 256-Gaussian block b, its pairs per
+                                  // band row r at [r * blocks + b] (row-bucketed binning, pass A)
 };
 
 // F1: projection, EWA cov2D, conic, radius, tile rect (clipped to the tile rows [ty0, ty1)),
@@ -65,7 +67,8 @@ int launch_duplicate(const uint32_t* tiles, uint4* rect, int n, int grid_x, int 
 // rb_status: ImgLayout.rb_status (cleared); pgid / pxr: cap u32 each of scratch.
 int launch_rb_binning(const uint32_t* tiles, uint4* rect, const uint32_t* offsets, int n, int gx, int ty0, int ty1,
                       uint32_t* histA, uint32_t* histB, uint32_t* rb_status, uint32_t* pgid, uint32_t* pxr,
-                      uint32_t* tkey, uint32_t* tgid, uint2* ranges, long long cap, hipStream_t s);
+                      uint32_t* tkey, uint32_t* tgid, uint2* ranges, long long cap, hipStream_t s,
+                      bool rows_counted = false);  // rows_counted: F1 wrote histA (PreOut.rb_hist)
 
 // Per-tile depth order: every tile's slice of `gid` (tile-sorted, gid order within a tile) is
 // sorted in place by (depth_key[gid], gid) -- the canonical (tile, depth, gid) order -- with a
@@ -85,12 +88,13 @@ int launch_depth_presort(const uint32_t* depth_key, const uint32_t* tiles, const
 int launch_duplicate_ranked(const uint32_t* rtiles, const uint4* rrect, uint4* rect, int n, int grid_x, int ty0,
                             const uint32_t* bexcl, uint32_t* offsets, uint32_t* tkey, uint32_t* tgid, long long cap,
                             hipStream_t s);
-// Mean slices of up to ~1365 entries use the register form instead (one wave per slice of <= 1024,
-// then a 2048-entry wave per queued slice; longer ones through ovf3 to the 8192-entry blocks).
+// Mean slices of up to ~1365 entries use the register form instead (one wave per slice of <= 1024
+// entries, a 2048-entry wave for the queued longer ones where the mean is near 1024; the rest
+// through the 1024-thread LDS form of tile_depth_sort_big).
 int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long K, const uint32_t* depth_key,
                            uint32_t* gid, uint32_t* ovf, uint32_t* ovf_count, uint32_t* ovf2, uint32_t* ovf2_count,
-                           uint32_t* ovf3, uint32_t* ovf3_count, uint32_t* done, uint32_t* scratch_hi,
-                           uint32_t* scratch_lo, hipStream_t s, bool unordered = false);
+                           uint32_t* done, uint32_t* scratch_hi, uint32_t* scratch_lo, hipStream_t s,
+                           bool unordered = false);
 // unordered: the tiles' entries are in arbitrary order (row-bucketed binning), not gid order --
 // the register form needs nothing else; the LDS forms then also sort by gid (LSD, gid passes first).
 // True when the register form takes the mean slice (the row-bucketed binning is used only then).

@@ -467,6 +467,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void p
         write_record(e, I.opac, G, rgb, clamped, out);
     }
     const uint32_t t = G.tiles;
+    if (NV == 1 && out.rb_hist) {  // grid-uniform: the row-bucketed binning's per-block row counts
+        __shared__ uint32_t rbc[kRbMaxRows];
+        rbc[threadIdx.x] = 0u;
+        __syncthreads();
+        if (t) {
+            const int by0 = G.miny > ty0 ? G.miny : ty0, by1 = G.maxy < ty1 ? G.maxy : ty1;
+            for (int r = by0; r < by1; ++r) atomicAdd(&rbc[r - ty0], 1u);
+        }
+        __syncthreads();
+        if ((int)threadIdx.x < ty1 - ty0) out.rb_hist[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = rbc[threadIdx.x];
+    }
     if (out.counters) {
         uint32_t k = t, c = t ? 1u : 0u;
 #pragma unroll

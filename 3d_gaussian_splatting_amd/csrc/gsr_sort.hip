@@ -611,11 +611,11 @@ constexpr int kRbStageA = 2048;  // LDS staging (pairs) of a pass-A block (~720 
 constexpr int kRbStage = 4096;   // LDS staging (instances) of a pass-B block (~2800 at 1M / 1080p)
 constexpr uint32_t kRbAgg = 1u << 30, kRbInc = 2u << 30, kRbCntMask = kRbAgg - 1u;
 
-// rows of one block's Gaussians -> histA[r * nbA + b]; also writes inst_start (rect.z) from the
-// inclusive F2 scan
-__global__ __launch_bounds__(256) void rb_rows_count(const uint32_t* __restrict__ tiles, uint4* __restrict__ rect,
-                                                     const uint32_t* __restrict__ offsets, int n, int ty0, int ty1,
-                                                     uint32_t* __restrict__ histA, int nbA) {
+// rows of one block's Gaussians -> histA[r * nbA + b] (F1 writes the same counts itself when it
+// ran for these Gaussians: PreOut.rb_hist; this kernel serves the band side, whose splats arrive
+// from the exchange)
+__global__ __launch_bounds__(256) void rb_rows_count(const uint32_t* __restrict__ tiles, const uint4* __restrict__ rect,
+                                                     int n, int ty0, int ty1, uint32_t* __restrict__ histA, int nbA) {
     __shared__ uint32_t cnt[kRbMaxRows];
     const int tid = threadIdx.x, R = ty1 - ty0;
     cnt[tid] = 0u;
@@ -625,7 +625,6 @@ __global__ __launch_bounds__(256) void rb_rows_count(const uint32_t* __restrict_
         const uint32_t nt = tiles[g];
         if (nt) {
             const uint4 rr = rect[g];
-            rect[g].z = offsets[g] - nt;  // inst_start: the emission index of the first instance
             const int miny = (int)(rr.x >> 16), maxy = (int)(rr.y >> 16);
             const int by0 = miny > ty0 ? miny : ty0, by1 = maxy < ty1 ? maxy : ty1;
             for (int r = by0; r < by1; ++r) atomicAdd(&cnt[r - ty0], 1u);
@@ -640,8 +639,9 @@ __global__ __launch_bounds__(256) void rb_rows_count(const uint32_t* __restrict_
 // rows, taking a slot of its row from an LDS counter -- the order of a row's pairs inside the
 // block is arbitrary (the per-tile sort that follows orders each tile by (depth, gid) itself),
 // so no per-row ballot sweep is needed.  Staged in LDS by row, written as coalesced row runs.
-__global__ __launch_bounds__(256) void rb_rows_place(const uint32_t* __restrict__ tiles, const uint4* __restrict__ rect,
-                                                     int n, int ty0, int ty1, const uint32_t* __restrict__ histA,
+__global__ __launch_bounds__(256) void rb_rows_place(const uint32_t* __restrict__ tiles, uint4* __restrict__ rect,
+                                                     const uint32_t* __restrict__ offsets, int n, int ty0, int ty1,
+                                                     const uint32_t* __restrict__ histA,
                                                      const uint32_t* __restrict__ totA, int nbA,
                                                      uint32_t* __restrict__ pgid, uint32_t* __restrict__ pxr,
                                                      long long pcap) {
@@ -653,11 +653,17 @@ __global__ __launch_bounds__(256) void rb_rows_place(const uint32_t* __restrict_
     __shared__ uint32_t wsum[kWaves];
     const int tid = threadIdx.x, R = ty1 - ty0;
     cnt[tid] = 0u;
+    // the row totals and this block's column of the scanned counts: loads issued first (they do
+    // not depend on the Gaussians), waited for at the block scan
+    const uint32_t ta = tid < R ? totA[tid] : 0u;
+    const uint32_t ha = tid < R ? histA[(size_t)tid * nbA + blockIdx.x] : 0u;
     const int g = blockIdx.x * 256 + tid;
     int by0 = 0, by1 = 0;  // band-relative rows
     uint32_t xr = 0;
-    if (g < n && tiles[g]) {
+    const uint32_t nt = g < n ? tiles[g] : 0u;
+    if (nt) {
         const uint4 rr = rect[g];
+        rect[g].z = offsets[g] - nt;  // inst_start: the emission index of the first instance (F3's)
         const int miny = (int)(rr.x >> 16), maxy = (int)(rr.y >> 16);
         by0 = (miny > ty0 ? miny : ty0) - ty0;
         by1 = (maxy < ty1 ? maxy : ty1) - ty0;
@@ -669,10 +675,9 @@ __global__ __launch_bounds__(256) void rb_rows_place(const uint32_t* __restrict_
     uint32_t tot;
     {
         const uint32_t c = cnt[tid];
-        const uint32_t ta = tid < R ? totA[tid] : 0u;
         uint32_t sdum;
         const uint32_t rowbase = block_exclusive_scan(ta, wsum, &sdum);
-        gb[tid] = tid < R ? rowbase + histA[(size_t)tid * nbA + blockIdx.x] : 0u;
+        gb[tid] = tid < R ? rowbase + ha : 0u;
         lb[tid] = block_exclusive_scan(c, wsum, &tot);
         cnt[tid] = 0u;
     }
@@ -920,16 +925,29 @@ __global__ __launch_bounds__(256) void rb_chunks_place(const uint32_t* __restric
     const int tid = threadIdx.x;
     rb_rows_table(totA, R, pcap, t);
     constexpr int kQ = kRbChunk / 256;
+    // the next chunk's pairs are loaded while this one is placed (register double buffer)
+    uint32_t nxr[kQ], ngg[kQ];
+    auto load_pairs = [&](uint32_t b) {
+        const RbChunk c = rb_chunk(t, b);
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            const uint32_t p = c.p0 + q * 256 + tid;
+            nxr[q] = p < c.p1 ? pxr[p] : 0u;  // 0: no columns
+            ngg[q] = p < c.p1 ? pgid[p] : 0u;
+        }
+    };
+    if (blockIdx.x < t.nchunks) load_pairs(blockIdx.x);
     for (uint32_t b = blockIdx.x; b < t.nchunks; b += gridDim.x) {
         const RbChunk ch = rb_chunk(t, b);
         cnt[tid] = 0u;
+        const uint32_t hb = tid < gx ? histB[(size_t)gx * ch.cp + (size_t)tid * ch.nch + ch.k] : 0u;
         uint32_t xr[kQ], gg[kQ];
 #pragma unroll
         for (int q = 0; q < kQ; ++q) {
-            const uint32_t p = ch.p0 + q * 256 + tid;
-            xr[q] = p < ch.p1 ? pxr[p] : 0u;  // 0: no columns
-            gg[q] = p < ch.p1 ? pgid[p] : 0u;
+            xr[q] = nxr[q];
+            gg[q] = ngg[q];
         }
+        if (b + gridDim.x < t.nchunks) load_pairs(b + gridDim.x);
         __syncthreads();  // cnt zeroed (and the previous chunk's staging read out)
 #pragma unroll
         for (int q = 0; q < kQ; ++q)
@@ -939,7 +957,7 @@ __global__ __launch_bounds__(256) void rb_chunks_place(const uint32_t* __restric
         {
             const uint32_t c = cnt[tid];
             lb[tid] = block_exclusive_scan(c, wsum, &tot);
-            gb[tid] = tid < gx ? histB[(size_t)gx * ch.cp + (size_t)tid * ch.nch + ch.k] : 0u;
+            gb[tid] = hb;
             cnt[tid] = 0u;
         }
         __syncthreads();
@@ -1178,7 +1196,7 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
 }
 
 // ---- per-tile depth order, register form: one wave per tile ----
-// A slice of n <= 64 E entries (E = 1 .. kWaveSortMaxE, the smallest power of two that holds it)
+// A slice of n <= 64 E entries (E = 1 .. 16, the smallest power of two that holds it)
 // is sorted by one wave in VGPRs as 64-bit (depth << 32 | gid) keys with a bitonic network: lane l
 // holds entries l E .. l E + E - 1, so exchanges at distances below E stay inside a lane and the
 // rest go lane to lane by DPP (lane xor 1 / 2 / 3, row mirrors, row_ror 8), ds_swizzle (xor 4,
@@ -1188,14 +1206,9 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
 // histogram: ~log2(64 E)^2 / 2 compare-exchange stages of 5-6 VALU ops per key pair, against the
 // LDS radix form's dependent counter updates and ~6 barriers per pass (latency-bound per block).
 // "Flip" network (every merge ascending: its first stage pairs i with i ^ (k - 1), mirrored).
-#ifndef GSR_WAVE_SORT_MAX_E
-#define GSR_WAVE_SORT_MAX_E 32
-#endif
 #ifndef GSR_TILE_WAVE_SORT
 #define GSR_TILE_WAVE_SORT 1
 #endif
-constexpr int kWaveSortMaxE = GSR_WAVE_SORT_MAX_E;
-static_assert(kWaveSortMaxE == 16 || kWaveSortMaxE == 32, "wave sort: up to 1024 or 2048 entries");
 
 // x from lane (lane ^ M) of the wave, M = 2^a - 1 (mirror stages) or 2^a (half cleaners)
 template <int M>
@@ -1348,17 +1361,19 @@ __global__ __launch_bounds__(256) void tile_depth_wave(const uint2* __restrict__
     else wave_sort_slice<16>(rg, depth_key, gid, lane, xs);
 }
 
-// The queued slices of 1025 .. 64 kWaveSortMaxE entries, one wave each (a kernel of its own: the
-// 32-entry-per-lane form needs ~190 VGPRs, which would cap the common form's occupancy at 2 waves
-// per SIMD); longer ones go on to `ovf3` for the LDS forms.  The queue length is on the device.
+// The queued slices of 1025 .. 2048 entries, one wave each (a kernel of its own: the 32-entry-per-
+// lane form needs ~230 VGPRs, which would cap the common form's occupancy at 2 waves per SIMD);
+// longer ones go on to `ovf2` for the LDS form.  Launched only where the mean slice is near one
+// wave's 1024 entries (multi-GPU bands at 1M: ~1060), where a good share of the slices exceed it;
+// the queue length is on the device.
 __global__ __launch_bounds__(256) void tile_depth_wave_queue(const uint2* __restrict__ ranges,
                                                             const uint32_t* __restrict__ depth_key,
                                                             uint32_t* __restrict__ gid,
                                                             const uint32_t* __restrict__ ovf,
                                                             const uint32_t* __restrict__ ovf_count,
-                                                            uint32_t* __restrict__ ovf3,
-                                                            uint32_t* __restrict__ ovf3_count) {
-    __shared__ uint32_t xs_all[4][64 * kWaveSortMaxE + 2 * kWaveSortMaxE];
+                                                            uint32_t* __restrict__ ovf2,
+                                                            uint32_t* __restrict__ ovf2_count) {
+    __shared__ uint32_t xs_all[4][64 * 32 + 64];
     const uint32_t cnt = *ovf_count;
     const int lane = threadIdx.x & 63;
     uint32_t* const xs = xs_all[threadIdx.x >> 6];
@@ -1366,12 +1381,11 @@ __global__ __launch_bounds__(256) void tile_depth_wave_queue(const uint2* __rest
         const uint32_t tile = ovf[q];
         const uint2 rg = ranges[tile];
         const int n = (int)(rg.y - rg.x);
-        if (n > 64 * kWaveSortMaxE) {
-            if (lane == 0) ovf3[atomicAdd(ovf3_count, 1u)] = tile;
+        if (n > 2048) {
+            if (lane == 0) ovf2[atomicAdd(ovf2_count, 1u)] = tile;
             continue;  // wave-uniform
         }
-        if constexpr (kWaveSortMaxE == 32) wave_sort_slice<32>(rg, depth_key, gid, lane, xs);
-        else wave_sort_slice<16>(rg, depth_key, gid, lane, xs);
+        wave_sort_slice<32>(rg, depth_key, gid, lane, xs);
     }
 }
 
@@ -1599,16 +1613,18 @@ int launch_scan(const uint32_t* tiles, int n, uint32_t* offsets, uint32_t* scan_
 
 int launch_rb_binning(const uint32_t* tiles, uint4* rect, const uint32_t* offsets, int n, int gx, int ty0, int ty1,
                       uint32_t* histA, uint32_t* histB, uint32_t* rb_status, uint32_t* pgid, uint32_t* pxr,
-                      uint32_t* tkey, uint32_t* tgid, uint2* ranges, long long cap, hipStream_t s) {
+                      uint32_t* tkey, uint32_t* tgid, uint2* ranges, long long cap, hipStream_t s,
+                      bool rows_counted) {
     const int R = ty1 - ty0;
     if (n <= 0 || R <= 0 || cap <= 0) return 0;  // ranges stay cleared
     if (R > kRbMaxRows || gx > kRbMaxCols) return (int)hipErrorInvalidValue;
     const int nbA = div_up(n, 256);
     uint32_t* const totA = histA + (size_t)256 * nbA;
-    hipLaunchKernelGGL(rb_rows_count, dim3(nbA), dim3(256), 0, s, tiles, rect, offsets, n, ty0, ty1, histA, nbA);
+    if (!rows_counted)
+        hipLaunchKernelGGL(rb_rows_count, dim3(nbA), dim3(256), 0, s, tiles, rect, n, ty0, ty1, histA, nbA);
     hipLaunchKernelGGL(radix_colscan, dim3(R), dim3(kB), 0, s, histA, nbA, totA);
-    hipLaunchKernelGGL(rb_rows_place, dim3(nbA), dim3(256), 0, s, tiles, rect, n, ty0, ty1, histA, totA, nbA, pgid, pxr,
-                       cap);
+    hipLaunchKernelGGL(rb_rows_place, dim3(nbA), dim3(256), 0, s, tiles, rect, offsets, n, ty0, ty1, histA, totA, nbA,
+                       pgid, pxr, cap);
     // chunks: at most cap / kRbChunk full ones plus one partial per row; the blocks walk them, so
     // the grid is capped near what the chip holds at once (no tail of empty blocks)
     const int nch_max = div_up(cap, kRbChunk) + R;
@@ -1672,8 +1688,8 @@ bool tile_wave_sort_eligible(long long K, int ntiles) { return GSR_TILE_WAVE_SOR
 
 int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long K, const uint32_t* depth_key,
                            uint32_t* gid, uint32_t* ovf, uint32_t* ovf_count, uint32_t* ovf2, uint32_t* ovf2_count,
-                           uint32_t* ovf3, uint32_t* ovf3_count, uint32_t* done, uint32_t* scratch_hi,
-                           uint32_t* scratch_lo, hipStream_t s, bool unordered) {
+                           uint32_t* done, uint32_t* scratch_hi, uint32_t* scratch_lo, hipStream_t s,
+                           bool unordered) {
     if (ntiles <= 0 || K <= 0) return 0;
     const int uo = unordered ? 1 : 0;
     // one block per tile holding up to cap entries in LDS, a power of two >= 1.5x the mean slice
@@ -1682,18 +1698,27 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
     // (one 8192-entry block per tile at 5M / 1080p: 0.89 ms with 512 threads, 0.79 with 1024,
     // against 0.49 for 4096-entry blocks + the queue: 1 block per CU)
     const int cap = tile_sort_cap(K, ntiles);
-    // slices of up to 64 kWaveSortMaxE entries sorted in registers, one wave each, whenever the
+    // slices of up to 1024 entries sorted in registers, one wave each, whenever the
     // mean slice leaves most tiles within that (the longer ones queue for the LDS forms below)
-    const bool wave = tile_wave_sort_eligible(K, ntiles);
-    if (wave) {
+    if (tile_wave_sort_eligible(K, ntiles)) {
         hipLaunchKernelGGL(tile_depth_wave, dim3(div_up(ntiles, 4)), dim3(256), 0, s, ranges, tile0, ntiles, depth_key,
                            gid, ovf, ovf_count);
-        const int wgrid = ntiles < 2048 ? div_up(ntiles, 4) : 512;
-        hipLaunchKernelGGL(tile_depth_wave_queue, dim3(wgrid), dim3(256), 0, s, ranges, depth_key, gid, ovf, ovf_count,
-                           ovf3, ovf3_count);
-        // the LDS forms below take the slices the register form could not
-        ovf = ovf3;
-        ovf_count = ovf3_count;
+        // the slices past one wave's 1024 entries: where the mean is near 1024 (bands), many -- a
+        // 2048-entry wave each, the rest on to the LDS form; elsewhere few (none at 1M / 1080p) --
+        // all straight to the 1024-thread LDS form, one launch instead of two more near-empty
+        // ones (~5 us each)
+        const int bgrid = ntiles < 256 ? ntiles : 256;
+        if (K / ntiles > 900) {
+            const int wgrid = ntiles < 2048 ? div_up(ntiles, 4) : 512;
+            hipLaunchKernelGGL(tile_depth_wave_queue, dim3(wgrid), dim3(256), 0, s, ranges, depth_key, gid, ovf,
+                               ovf_count, ovf2, ovf2_count);
+            hipLaunchKernelGGL(tile_depth_sort_big, dim3(bgrid), dim3(1024), 0, s, ranges, depth_key, gid, ovf2,
+                               ovf2_count, done, scratch_hi, scratch_lo, uo);
+        } else {
+            hipLaunchKernelGGL(tile_depth_sort_big, dim3(bgrid), dim3(1024), 0, s, ranges, depth_key, gid, ovf,
+                               ovf_count, done, scratch_hi, scratch_lo, uo);
+        }
+        return (int)hipGetLastError();
     } else {
 #define GSR_TILE_RADIX(NT_, I_)                                                                       \
     hipLaunchKernelGGL((tile_depth_radix<NT_, I_, 9>), dim3(ntiles), dim3(NT_), 0, s, ranges, tile0, depth_key, \
