@@ -338,10 +338,15 @@ int fwd_phase1(FwdJob& j, gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_image, voi
                   "depth presort");
         return 0;
     }
-    // the row-bucketed binning (maybe taken in phase 2) needs the three-kernel scan's offsets
+    // the row-bucketed binning (maybe taken in phase 2) needs the scan's offsets, not the fused
+    // scan + F3; when F1 summed its blocks' tiles (rows_counted), one launch scans those sums and the
+    // per-Gaussian offsets are written in phase 2
     const bool rb_possible = use_rb_binning(j.n, j.gx, j.gy);
-    GSR_STAGE(GSR_STAGE_SCAN, launch_scan(v.tiles, (int)j.n, v.offsets, v.partials, v.K_dev, stream, !rb_possible),
-              "scan");
+    if (rb_possible && j.rows_counted)
+        GSR_STAGE(GSR_STAGE_SCAN, launch_scan_blocks(v.lookback + 16, (int)j.n, v.K_dev, stream), "scan (block sums)");
+    else
+        GSR_STAGE(GSR_STAGE_SCAN, launch_scan(v.tiles, (int)j.n, v.offsets, v.partials, v.K_dev, stream, !rb_possible),
+                  "scan");
     return 0;
 }
 
@@ -365,15 +370,20 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
         GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate_ranked(v.rtiles, v.rrect, v.rect, (int)j.n, j.gx, j.ty0,
                                                                v.lookback, v.offsets, v.kA, v.vA, cap, stream),
                   "duplicate (rank order)");
-    else if (!v.rb)
+    else if (!v.rb) {
+        if (scanned && j.rows_counted)  // phase 1 scanned F1's block sums only
+            GSR_STAGE(GSR_STAGE_SCAN, launch_block_offsets(v.tiles, (int)j.n, v.lookback + 16, v.offsets, stream),
+                      "offsets");
         GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate(v.tiles, v.rect, (int)j.n, j.gx, j.ty0, v.offsets, v.lookback,
                                                         v.kA, v.vA, cap, v.K_dev, stream, scanned),
                   "duplicate");
+    }
     if (cap > 0 && v.rb) {
         // F3 + the tile sort + F5 as two counting passes; the pairs ride in (kB, vB)
         GSR_STAGE(GSR_STAGE_TILE_SORT, launch_rb_binning(v.tiles, v.rect, v.offsets, (int)j.n, j.gx, j.ty0, j.ty1,
                                                          v.rb_histA, v.rb_histB, v.rb_status, v.kB, v.vB, v.kA, v.vA,
-                                                         v.ranges, cap, stream, j.rows_counted),
+                                                         v.ranges, cap, stream, j.rows_counted,
+                                                         j.rows_counted ? v.lookback + 16 : nullptr),
                   "row-bucketed binning");
         GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_tile_depth_sort(v.ranges, j.ty0 * j.gx, ntiles, cap, v.depth_key,
                                                                v.sorted_gid, v.ovf, v.counters + kOvfCountSlot, v.ovf2,
@@ -432,7 +442,10 @@ int run_preprocess(const gsr_camera* cam, const gsr_gaussians* gs, int ty0, int 
     const bool full = ty0 == 0 && ty1 == div_up(cam->height, kTile);
     PreOut po{radii, v.depth_key, v.tiles, v.rec, v.rect, full ? v.flags : nullptr, v.counters};
     // the row-bucketed binning's pass-A row counts, from F1 itself (fwd_phase2 then skips them)
-    if (use_rb_binning(gs->P, div_up(cam->width, kTile), div_up(cam->height, kTile))) po.rb_hist = v.rb_histA;
+    if (use_rb_binning(gs->P, div_up(cam->width, kTile), div_up(cam->height, kTile))) {
+        po.rb_hist = v.rb_histA;
+        po.bsum = v.lookback + 16;  // the F2 scan's block partials (the lookback words are unused here)
+    }
     GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess(*cam, gauss_in(gs), ty0, ty1, po, stream), "preprocess");
     return 0;
 }
@@ -863,9 +876,13 @@ int gsr_band_forward(const gsr_camera* cam, const gsr_raster_settings* rs, int32
     FwdJob j{cam, rs, out_color, bufs};
     j.n = n;
     if (int e = fwd_phase1(j, alloc_geom, alloc_image, ctx, stream, debug, true, [&](const Views& v) {
+            // the row-bucketed binning's pass-A counts and the F2 block sums come with the unpack
+            const bool rb = use_rb_binning(j.n, j.gx, j.gy);
             GSR_STAGE(GSR_STAGE_EXCHANGE, launch_unpack_splats(static_cast<const char*>(recv), nsrc, pair_cap, j.ty0,
-                                                               j.ty1, v.rec, v.depth_key, v.tiles, v.rect, stream),
+                                                               j.ty1, v.rec, v.depth_key, v.tiles, v.rect, stream,
+                                                               rb ? v.rb_histA : nullptr, rb ? v.lookback + 16 : nullptr),
                       "unpack splats");
+            j.rows_counted = rb;
             return 0;
         }))
         return e;

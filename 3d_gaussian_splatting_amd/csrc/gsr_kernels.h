@@ -24,6 +24,8 @@ struct PreOut {
                          // [kCountSlots + slot] += K (slot = block % kCountSlots)
     uint32_t* rb_hist = nullptr;  // nullable (one view only): per 256-Gaussian block b, its pairs per
                                   // band row r at [r * blocks + b] (row-bucketed binning, pass A)
+    uint32_t* bsum = nullptr;     // with rb_hist: per block b, its Gaussians' tiles_touched sum (the
+                                  // F2 scan's block partials: launch_scan_blocks scans them)
 };
 
 // F1: projection, EWA cov2D, conic, radius, tile rect (clipped to the tile rows [ty0, ty1)),
@@ -60,15 +62,22 @@ int launch_duplicate(const uint32_t* tiles, uint4* rect, int n, int grid_x, int 
                      uint32_t* lookback, uint32_t* tkey, uint32_t* tgid, long long cap, uint32_t* total_out,
                      hipStream_t s, bool scanned = false);  // scanned: the three-kernel scan already ran
 
+// F2 from F1's block sums (PreOut.bsum, one per 256 Gaussians): the sums scanned in place
+// (exclusive) and K into *total_out -- one launch; the per-Gaussian offsets then come from
+// rb_rows_place, or from launch_block_offsets when the radix binning runs instead.
+int launch_scan_blocks(uint32_t* bsum, int n, uint32_t* total_out, hipStream_t s);
+int launch_block_offsets(const uint32_t* tiles, int n, const uint32_t* bsum, uint32_t* offsets, hipStream_t s);
 // Row-bucketed binning (gsr_internal.h use_rb_binning): from the inclusive F2 scan `offsets`, F3
 // (inst_start into rect.z), the stable tile sort of the instances and F5 -- the (tile key, gid)
 // arrays tkey / tgid in (tile, gid) order and `ranges` (cleared beforehand) -- in two counting
 // passes over (Gaussian, tile row) pairs.  histA: GeomLayout.rb_hist; histB: BinLayout.rb_hist;
 // rb_status: ImgLayout.rb_status (cleared); pgid / pxr: cap u32 each of scratch.
-int launch_rb_binning(const uint32_t* tiles, uint4* rect, const uint32_t* offsets, int n, int gx, int ty0, int ty1,
+int launch_rb_binning(const uint32_t* tiles, uint4* rect, uint32_t* offsets, int n, int gx, int ty0, int ty1,
                       uint32_t* histA, uint32_t* histB, uint32_t* rb_status, uint32_t* pgid, uint32_t* pxr,
                       uint32_t* tkey, uint32_t* tgid, uint2* ranges, long long cap, hipStream_t s,
-                      bool rows_counted = false);  // rows_counted: F1 wrote histA (PreOut.rb_hist)
+                      bool rows_counted = false,     // rows_counted: F1 wrote histA (PreOut.rb_hist)
+                      const uint32_t* bsum = nullptr);  // with it: F1's scanned block sums -- the
+                                                         // placement writes `offsets` itself
 
 // Per-tile depth order: every tile's slice of `gid` (tile-sorted, gid order within a tile) is
 // sorted in place by (depth_key[gid], gid) -- the canonical (tile, depth, gid) order -- with a
@@ -162,8 +171,11 @@ int launch_pack_splats(const uint32_t* tiles, const uint4* rect, const uint32_t*
                        const BandRows& br, uint32_t* partials, char* send, int pair_cap, uint32_t* slot_of,
                        uint32_t* row_hist, int grid_y, bool spans, hipStream_t s);
 // Band side: nsrc received blocks -> local arrays of nsrc * pair_cap entries (empty slots: no tiles)
+// rb_hist / bsum (nullable, together): the row-bucketed binning's pass-A row counts and the F2 scan's
+// block partials per 256 slots, as F1 writes them for a single-GPU forward (PreOut.rb_hist / bsum)
 int launch_unpack_splats(const char* recv, int nsrc, int pair_cap, int ty0, int ty1, float4* rec, uint32_t* depth_key,
-                         uint32_t* tiles, uint4* rect, hipStream_t s);
+                         uint32_t* tiles, uint4* rect, hipStream_t s, uint32_t* rb_hist = nullptr,
+                         uint32_t* bsum = nullptr);
 
 // the bands [b_lo, b_hi] a rect's tile rows [miny, maxy) overlap (b_lo > b_hi: none)
 __device__ __forceinline__ void band_span(const BandRows& br, uint32_t miny, uint32_t maxy, int& b_lo, int& b_hi) {

@@ -492,6 +492,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void p
         __syncthreads();
         if (threadIdx.x == 0) {  // spread over kCountSlots addresses: one hot word serialises
             const uint32_t K = wk[0] + wk[1] + wk[2] + wk[3], C = wc[0] + wc[1] + wc[2] + wc[3];
+            if (NV == 1 && out.bsum) out.bsum[blockIdx.x] = K;  // the F2 scan's block partial
             const int slot = blockIdx.x & (kCountSlots - 1);
             if (K) atomicAdd(out.counters + kCountSlots + slot, K);
             if (C) atomicAdd(out.counters + slot, C);

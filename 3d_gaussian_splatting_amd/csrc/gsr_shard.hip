@@ -197,11 +197,55 @@ __global__ __launch_bounds__(kB) void pack_scatter_kernel(const uint32_t* __rest
 
 // Band owner: local index i = src * pair_cap + slot.  Live slots get their record, depth key,
 // rect and the tile count of the rect clipped to the band's rows; empty slots get no tiles.
+// Band side.  With rb_hist (the grid then covers every slot once, 256 per block): also each
+// block's splats per band row (the row-bucketed binning's pass-A counts, as F1 writes them on a
+// single GPU) and its tiles_touched sum (the F2 scan's block partial).
 __global__ __launch_bounds__(256) void unpack_kernel(const char* __restrict__ recv, size_t block_bytes, int nsrc,
                                                      int pair_cap, int ty0, int ty1, float4* __restrict__ rec,
                                                      uint32_t* __restrict__ depth_key, uint32_t* __restrict__ tiles,
-                                                     uint4* __restrict__ rect) {
+                                                     uint4* __restrict__ rect, uint32_t* __restrict__ rb_hist,
+                                                     uint32_t* __restrict__ bsum) {
     const long long n = (long long)nsrc * pair_cap;
+    if (rb_hist) {  // grid-uniform
+        __shared__ uint32_t rows[kRbMaxRows];
+        __shared__ uint32_t ws[4];
+        rows[threadIdx.x] = 0u;
+        __syncthreads();
+        const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+        uint32_t nt = 0;
+        if (i < n) {
+            const int src = (int)(i / pair_cap), slot = (int)(i - (long long)src * pair_cap);
+            const char* blk = recv + (size_t)src * block_bytes;
+            const uint32_t count = *reinterpret_cast<const uint32_t*>(blk);
+            if ((uint32_t)slot < count) {
+                const float4* sp = reinterpret_cast<const float4*>(blk + kSplatBytes + (size_t)slot * kSplatBytes);
+                const float4 a = sp[3];
+                rec[3 * i] = sp[0];
+                rec[3 * i + 1] = sp[1];
+                rec[3 * i + 2] = sp[2];
+                const uint32_t lo = __float_as_uint(a.y), hi = __float_as_uint(a.z);
+                depth_key[i] = __float_as_uint(a.x);
+                rect[i] = make_uint4(lo, hi, 0u, 0u);
+                const int miny = (int)(lo >> 16), maxy = (int)(hi >> 16);
+                const int y0 = miny > ty0 ? miny : ty0, y1 = maxy < ty1 ? maxy : ty1;
+                nt = y1 > y0 ? ((hi & 0xFFFF) - (lo & 0xFFFF)) * (uint32_t)(y1 - y0) : 0u;
+                tiles[i] = nt;
+                if (nt)
+                    for (int r = y0; r < y1; ++r) atomicAdd(&rows[r - ty0], 1u);
+            } else {
+                depth_key[i] = 0xFFFFFFFFu;
+                tiles[i] = 0u;
+            }
+        }
+        uint32_t t = nt;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+        if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = t;
+        __syncthreads();
+        if ((int)threadIdx.x < ty1 - ty0) rb_hist[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = rows[threadIdx.x];
+        if (threadIdx.x == 0) bsum[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+        return;
+    }
     for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
         const int src = (int)(i / pair_cap), slot = (int)(i - (long long)src * pair_cap);
         const char* blk = recv + (size_t)src * block_bytes;
@@ -250,12 +294,14 @@ int launch_pack_splats(const uint32_t* tiles, const uint4* rect, const uint32_t*
 }
 
 int launch_unpack_splats(const char* recv, int nsrc, int pair_cap, int ty0, int ty1, float4* rec, uint32_t* depth_key,
-                         uint32_t* tiles, uint4* rect, hipStream_t s) {
+                         uint32_t* tiles, uint4* rect, hipStream_t s, uint32_t* rb_hist, uint32_t* bsum) {
     const long long n = (long long)nsrc * pair_cap;
     if (n <= 0) return 0;
     const long long blocks = (n + 255) / 256;
-    hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0, s, recv,
-                       exchange_block_bytes(pair_cap), nsrc, pair_cap, ty0, ty1, rec, depth_key, tiles, rect);
+    if (rb_hist && ty1 - ty0 > kRbMaxRows) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)(rb_hist || blocks < 8192 ? blocks : 8192)), dim3(256), 0, s, recv,
+                       exchange_block_bytes(pair_cap), nsrc, pair_cap, ty0, ty1, rec, depth_key, tiles, rect, rb_hist,
+                       bsum);
     return (int)hipGetLastError();
 }
 

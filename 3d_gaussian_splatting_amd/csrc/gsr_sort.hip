@@ -640,7 +640,8 @@ __global__ __launch_bounds__(256) void rb_rows_count(const uint32_t* __restrict_
 // block is arbitrary (the per-tile sort that follows orders each tile by (depth, gid) itself),
 // so no per-row ballot sweep is needed.  Staged in LDS by row, written as coalesced row runs.
 __global__ __launch_bounds__(256) void rb_rows_place(const uint32_t* __restrict__ tiles, uint4* __restrict__ rect,
-                                                     const uint32_t* __restrict__ offsets, int n, int ty0, int ty1,
+                                                     uint32_t* __restrict__ offsets, const uint32_t* __restrict__ bsum,
+                                                     int n, int ty0, int ty1,
                                                      const uint32_t* __restrict__ histA,
                                                      const uint32_t* __restrict__ totA, int nbA,
                                                      uint32_t* __restrict__ pgid, uint32_t* __restrict__ pxr,
@@ -661,9 +662,18 @@ __global__ __launch_bounds__(256) void rb_rows_place(const uint32_t* __restrict_
     int by0 = 0, by1 = 0;  // band-relative rows
     uint32_t xr = 0;
     const uint32_t nt = g < n ? tiles[g] : 0u;
+    uint32_t incl;  // F2: the inclusive scan of tiles_touched at g
+    if (bsum) {     // from F1's scanned block sums: this block's base + the in-block scan
+        const uint32_t bb = bsum[blockIdx.x];
+        uint32_t tdum;
+        incl = bb + block_exclusive_scan(nt, wsum, &tdum) + nt;
+        if (g < n) offsets[g] = incl;
+    } else {
+        incl = g < n ? offsets[g] : 0u;  // the three-kernel scan's
+    }
     if (nt) {
         const uint4 rr = rect[g];
-        rect[g].z = offsets[g] - nt;  // inst_start: the emission index of the first instance (F3's)
+        rect[g].z = incl - nt;  // inst_start: the emission index of the first instance (F3's)
         const int miny = (int)(rr.x >> 16), maxy = (int)(rr.y >> 16);
         by0 = (miny > ty0 ? miny : ty0) - ty0;
         by1 = (maxy < ty1 ? maxy : ty1) - ty0;
@@ -1611,10 +1621,34 @@ int launch_scan(const uint32_t* tiles, int n, uint32_t* offsets, uint32_t* scan_
     return (int)hipGetLastError();
 }
 
-int launch_rb_binning(const uint32_t* tiles, uint4* rect, const uint32_t* offsets, int n, int gx, int ty0, int ty1,
+// one block of 256 Gaussians: offsets = its scanned base + the in-block inclusive scan
+__global__ __launch_bounds__(256) void block_offsets_kernel(const uint32_t* __restrict__ tiles, int n,
+                                                            const uint32_t* __restrict__ bsum,
+                                                            uint32_t* __restrict__ offsets) {
+    __shared__ uint32_t wsum[kWaves];
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t nt = g < n ? tiles[g] : 0u;
+    uint32_t tdum;
+    const uint32_t incl = bsum[blockIdx.x] + block_exclusive_scan(nt, wsum, &tdum) + nt;
+    if (g < n) offsets[g] = incl;
+}
+
+int launch_scan_blocks(uint32_t* bsum, int n, uint32_t* total_out, hipStream_t s) {
+    if (n <= 0) return (int)hipMemsetAsync(total_out, 0, sizeof(uint32_t), s);
+    hipLaunchKernelGGL(scan_partials, dim3(1), dim3(1024), 0, s, bsum, div_up(n, 256), total_out);
+    return (int)hipGetLastError();
+}
+
+int launch_block_offsets(const uint32_t* tiles, int n, const uint32_t* bsum, uint32_t* offsets, hipStream_t s) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(block_offsets_kernel, dim3(div_up(n, 256)), dim3(256), 0, s, tiles, n, bsum, offsets);
+    return (int)hipGetLastError();
+}
+
+int launch_rb_binning(const uint32_t* tiles, uint4* rect, uint32_t* offsets, int n, int gx, int ty0, int ty1,
                       uint32_t* histA, uint32_t* histB, uint32_t* rb_status, uint32_t* pgid, uint32_t* pxr,
                       uint32_t* tkey, uint32_t* tgid, uint2* ranges, long long cap, hipStream_t s,
-                      bool rows_counted) {
+                      bool rows_counted, const uint32_t* bsum) {
     const int R = ty1 - ty0;
     if (n <= 0 || R <= 0 || cap <= 0) return 0;  // ranges stay cleared
     if (R > kRbMaxRows || gx > kRbMaxCols) return (int)hipErrorInvalidValue;
@@ -1623,8 +1657,8 @@ int launch_rb_binning(const uint32_t* tiles, uint4* rect, const uint32_t* offset
     if (!rows_counted)
         hipLaunchKernelGGL(rb_rows_count, dim3(nbA), dim3(256), 0, s, tiles, rect, n, ty0, ty1, histA, nbA);
     hipLaunchKernelGGL(radix_colscan, dim3(R), dim3(kB), 0, s, histA, nbA, totA);
-    hipLaunchKernelGGL(rb_rows_place, dim3(nbA), dim3(256), 0, s, tiles, rect, offsets, n, ty0, ty1, histA, totA, nbA,
-                       pgid, pxr, cap);
+    hipLaunchKernelGGL(rb_rows_place, dim3(nbA), dim3(256), 0, s, tiles, rect, offsets, bsum, n, ty0, ty1, histA, totA,
+                       nbA, pgid, pxr, cap);
     // chunks: at most cap / kRbChunk full ones plus one partial per row; the blocks walk them, so
     // the grid is capped near what the chip holds at once (no tail of empty blocks)
     const int nch_max = div_up(cap, kRbChunk) + R;
