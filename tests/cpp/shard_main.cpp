@@ -23,6 +23,7 @@
 #include <torch/torch.h>
 
 #include <chrono>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -164,11 +165,16 @@ int main(int argc, char** argv) {
                 put_t(o, res.grads.at(k));
         }
         for (const auto& im : images) put_t(o, im);
+        const long long store_keys = (long long)store->getNumKeys();
+        // rank 0 hosts the store: it leaves only after every rank is past its last store call
+        store->add("gsr_main/exit", 1);
+        for (int spin = 0; rank == 0 && spin < 30000 && store->add("gsr_main/exit", 0) < world; ++spin)
+            std::this_thread::sleep_for(std::chrono::milliseconds(1));  // (bounded: a failed rank never arrives)
         std::fprintf(stderr,
                      "[gsr_shard_step rank %d/%d] %s exchange, graph %d, %lld steps, pair_cap %d, capacity %d, "
                      "store_keys %lld, live_replans %lld\n",
                      rank, world, ex->name(), (int)step.graph_active(), (long long)done, step.pair_cap(),
-                     step.capacity(), (long long)store->getNumKeys(), (long long)step.live_replans());
+                     step.capacity(), store_keys, (long long)step.live_replans());
         return 0;
     } catch (const std::exception& e) {
         std::fprintf(stderr, "gsr_shard_step failed: %s\n", e.what());
