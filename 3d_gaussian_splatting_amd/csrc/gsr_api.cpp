@@ -364,7 +364,7 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
     // order (it leaves a tile's entries unordered, which that form does not mind); recorded in the
     // buffers so that every later view of them (backward, accessors) finds the same arrays.
     const bool scanned = use_rb_binning(j.n, j.gx, j.gy);  // phase 1 ran the three-kernel scan
-    if (scanned && cap > 0 && tile_wave_sort_eligible(cap, ntiles)) bufs->reserved |= kBufRowBucketed;
+    if (scanned && cap > 0 && (GSR_RB_DEEP || tile_wave_sort_eligible(cap, ntiles))) bufs->reserved |= kBufRowBucketed;
     const Views v = views(cam, j.n, bufs);
     if (v.presort)
         GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate_ranked(v.rtiles, v.rrect, v.rect, (int)j.n, j.gx, j.ty0,

@@ -76,6 +76,10 @@ constexpr int kMaxViews = 8;  // gsr_forward_views: views per call (= GSR_MAX_VI
 #ifndef GSR_RB_BIN
 #define GSR_RB_BIN 1
 #endif
+// GSR_RB_DEEP 0: only where the per-tile sort takes its register form (mean slices <= ~1365)
+#ifndef GSR_RB_DEEP
+#define GSR_RB_DEEP 1
+#endif
 constexpr int kRbMaxRows = 256, kRbMaxCols = 256, kRbChunkPairs = 1024;
 // gsr_buffers.reserved bits (set by the forward): the binning in use
 constexpr int32_t kBufRowBucketed = 1;

@@ -1049,16 +1049,71 @@ __global__ __launch_bounds__(256) void finalize_kernel(const uint32_t* __restric
 // [w * 64 I, (w + 1) * 64 I) of the slice, ranked round by round in index order (stable).
 // One slice [rg.x, rg.y) of n <= NT * I entries, sorted by the whole block.  Ends with every
 // LDS access behind a barrier, so a block may call it again for another slice.
+// Runs of equal depth keys in a depth-sorted slice (skey, sval in LDS, n entries) into gid order.
+// The thread holding a run's first entry sorts the run by insertion when it is at most
+// kTieRunMax long (runs are disjoint, so no two threads touch the same entries); if any run is
+// longer, the whole slice goes through an all-ascending bitonic network on the 64-bit (depth,
+// gid) keys in place (a degenerate slice: many Gaussians at one depth).  Ends behind a barrier.
+constexpr int kTieRunMax = 32;
+__device__ __forceinline__ void tie_fixup(uint32_t* skey, uint32_t* sval, int n, int nt) {
+    int longrun = 0;
+    for (int i = threadIdx.x; i + 1 < n; i += nt) {
+        const uint32_t k = skey[i];
+        if (skey[i + 1] != k || (i > 0 && skey[i - 1] == k)) continue;  // not a run's first entry
+        int e = i + 2;
+        while (e < n && skey[e] == k && e - i <= kTieRunMax) ++e;
+        if (e - i > kTieRunMax) {
+            longrun = 1;
+            continue;
+        }
+        for (int a = i + 1; a < e; ++a) {  // insertion sort of sval[i, e)
+            const uint32_t v = sval[a];
+            int b = a;
+            while (b > i && sval[b - 1] > v) {
+                sval[b] = sval[b - 1];
+                --b;
+            }
+            sval[b] = v;
+        }
+    }
+    if (!__syncthreads_or(longrun)) return;
+    int m = 1;
+    while (m < n) m <<= 1;
+    auto cex = [&](int i, int j) {  // i < j; j >= n is +inf padding
+        if (j >= n) return;
+        const uint64_t a = ((uint64_t)skey[i] << 32) | sval[i], b = ((uint64_t)skey[j] << 32) | sval[j];
+        if (a > b) {
+            skey[i] = (uint32_t)(b >> 32), sval[i] = (uint32_t)b;
+            skey[j] = (uint32_t)(a >> 32), sval[j] = (uint32_t)a;
+        }
+    };
+    for (int size = 2; size <= m; size <<= 1) {
+        for (int d = size >> 1; d >= 1; d >>= 1) {
+            const bool flip = d == (size >> 1);
+            for (int t = threadIdx.x; t < (m >> 1); t += nt) {
+                const int i = ((t & ~(d - 1)) << 1) | (t & (d - 1));
+                cex(i, flip ? (i ^ (size - 1)) : (i + d));
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// out of line for the register-heavy slice kernels (its few live values cross the call)
+__device__ __attribute__((noinline)) void tile_tie_fixup(uint32_t* skey, uint32_t* sval, int n, int nt) {
+    tie_fixup(skey, sval, n, nt);
+}
+
 template <int NT, int I, int DB>
 struct SliceLds {
     uint32_t wcnt[NT / 64][1 << DB];
     uint32_t lbase[1 << DB];
-    uint32_t red[4][NT / 64];
+    uint32_t red[2][NT / 64];
     uint32_t skey[NT * I];
     uint32_t sval[NT * I];
 };
 
-template <int NT, int I, int DB>
+template <int NT, int I, int DB, bool kFixInline = false>
 __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t* __restrict__ depth_key,
                                                  uint32_t* __restrict__ gid, SliceLds<NT, I, DB>& lds,
                                                  bool unordered = false) {
@@ -1077,7 +1132,7 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
     const int base = w * per;
     const int end = base + per < n ? base + per : n;
     uint32_t key[I], val[I], rank[I];
-    uint32_t kor = 0u, kand = 0xFFFFFFFFu, vor = 0u, vand = 0xFFFFFFFFu;
+    uint32_t kor = 0u, kand = 0xFFFFFFFFu;
 #pragma unroll
     for (int r = 0; r < I; ++r) {
         const int idx = base + r * 64 + lane;
@@ -1087,8 +1142,6 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
         if (valid) {
             kor |= key[r];
             kand &= key[r];
-            vor |= val[r];
-            vand &= val[r];
         }
     }
     // bits where the slice's keys differ: passes over constant digits are no-ops (stable)
@@ -1096,38 +1149,32 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
     for (int o = 32; o > 0; o >>= 1) {
         kor |= __shfl_xor(kor, o, 64);
         kand &= __shfl_xor(kand, o, 64);
-        vor |= __shfl_xor(vor, o, 64);
-        vand &= __shfl_xor(vand, o, 64);
     }
     if (lane == 0) {
         red[0][w] = kor;
         red[1][w] = kand;
-        red[2][w] = vor;
-        red[3][w] = vand;
     }
     __syncthreads();
-    uint32_t diff = 0u, vdiff = 0u;
+    uint32_t diff = 0u;
     {
-        uint32_t o_ = 0u, a_ = 0xFFFFFFFFu, vo = 0u, va = 0xFFFFFFFFu;
+        uint32_t o_ = 0u, a_ = 0xFFFFFFFFu;
 #pragma unroll
         for (int k = 0; k < NWV; ++k) {
             o_ |= red[0][k];
             a_ &= red[1][k];
-            vo |= red[2][k];
-            va &= red[3][k];
         }
         diff = o_ ^ a_;
-        vdiff = unordered ? vo ^ va : 0u;
     }
     const uint64_t lt = lanemask_lt();
-    // An unordered slice (the row-bucketed binning leaves a tile's entries in arbitrary order)
-    // first takes LSD passes over the gid bits, so the depth passes that follow end in (depth,
-    // gid) order; a gid-ordered slice needs the depth passes alone.
-    const int gid_passes = (32 + DB - 1) / DB;
-    for (int pass = unordered ? 0 : gid_passes; pass < 2 * gid_passes; ++pass) {
-        const bool by_val = pass < gid_passes;  // block-uniform
-        const int shift = (by_val ? pass : pass - gid_passes) * DB;
-        if ((((by_val ? vdiff : diff) >> shift) & DMASK) == 0u) continue;  // block-uniform
+    // The (stable) depth passes alone: a gid-ordered slice ends in (depth, gid) order.  An
+    // unordered one (the row-bucketed binning leaves a tile's entries in arbitrary order) ends in
+    // depth order with each run of equal depth keys in arbitrary gid order; tile_tie_fixup puts
+    // those runs in gid order afterwards (ties are rare and short: an LSD pass over the gid bits
+    // per 8-9 of them would cost as much as the depth passes again).
+    bool ran = false;
+    for (int shift = 0; shift < 32; shift += DB) {
+        if (((diff >> shift) & DMASK) == 0u) continue;  // block-uniform
+        ran = true;
         for (int d = tid; d < NWV * BINS; d += NT) (&wcnt[0][0])[d] = 0u;
         __syncthreads();
 #pragma unroll
@@ -1135,7 +1182,7 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
             if (base + r * 64 >= end) break;  // wave-uniform: only the rounds holding keys
             const int idx = base + r * 64 + lane;
             const bool valid = idx < end;
-            const uint32_t d = ((by_val ? val[r] : key[r]) >> shift) & DMASK;
+            const uint32_t d = (key[r] >> shift) & DMASK;
             const uint64_t peers = match_digit<DB>(d, DB, __ballot(valid));
             const uint32_t old = wcnt[w][d];
             rank[r] = old + (uint32_t)__popcll(peers & lt);
@@ -1180,7 +1227,7 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
         for (int r = 0; r < I; ++r) {
             const int idx = base + r * 64 + lane;
             if (idx < end) {
-                const uint32_t d = ((by_val ? val[r] : key[r]) >> shift) & DMASK;
+                const uint32_t d = (key[r] >> shift) & DMASK;
                 const uint32_t lp = lbase[d] + wcnt[w][d] + rank[r];
                 skey[lp] = key[r];
                 sval[lp] = val[r];
@@ -1196,6 +1243,24 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
             }
         }
         __syncthreads();  // skey / sval / wcnt are rewritten by the next pass
+    }
+    if (unordered && n > 1) {
+        if (!ran) {  // every key equal: the slice is one run, in LDS for the fix-up
+#pragma unroll
+            for (int r = 0; r < I; ++r) {
+                const int idx = base + r * 64 + lane;
+                if (idx < end) {
+                    skey[idx] = key[r];
+                    sval[idx] = val[r];
+                }
+            }
+            __syncthreads();
+        }
+        if constexpr (kFixInline) tie_fixup(skey, sval, n, NT);
+        else tile_tie_fixup(skey, sval, n, NT);
+        for (int i = tid; i < n; i += NT) gid[rg.x + i] = sval[i];
+        __syncthreads();  // skey / sval / red[] are rewritten by the next slice
+        return;
     }
 #pragma unroll
     for (int r = 0; r < I; ++r) {
@@ -1478,7 +1543,7 @@ __shared__ union BigLds {
 
 __device__ __attribute__((noinline)) void big_slice_sort(const uint2 rg, const uint32_t* __restrict__ depth_key,
                                                          uint32_t* __restrict__ gid, bool unordered) {
-    radix_sort_slice<1024, 16, 8>(rg, depth_key, gid, g_big.slice, unordered);
+    radix_sort_slice<1024, 16, 8, true>(rg, depth_key, gid, g_big.slice, unordered);
 }
 
 __device__ __attribute__((noinline)) void merge_sorted_chunks(const uint2 r, const uint32_t* __restrict__ depth_key,

@@ -372,6 +372,30 @@ def test_dense_tiles_sort_paths(rast, oracle):
     _compare(st, f, sc.make_dL_dpix(cam, seed=14), rast)
 
 
+@pytest.mark.parametrize("levels", [1, 6])
+def test_depth_ties_in_deep_tiles(levels, rast, oracle):
+    """Deep tiles (thousands of entries: the LDS radix forms) whose Gaussians share a few depth
+    values.  The row-bucketed binning hands those forms each tile's entries in arbitrary order;
+    they sort by depth alone and must notice the ties and re-sort with the gid bits, so that the
+    list is the canonical (depth, gid) one.  The synthetic camera has R = I, T = 0, so the
+    view-space depth is the world z exactly; levels = 1 puts every Gaussian at one depth (no
+    depth pass has anything to do)."""
+    gr, sc = pkg("graphics"), pkg("scene")
+    cam = gr.synthetic_camera(96, 64)
+    s = sc.make_scene(cam, 30000, max_sh_degree=1, seed=21)
+    z = s.means3D[:, 2]
+    lo, hi = float(z.min()), float(z.max())
+    q = np.linspace(lo, hi, levels + 2)[1:-1].astype(np.float32)
+    s.means3D[:, 2] = q[np.random.default_rng(22).integers(0, levels, z.shape[0])]
+    args = (cam, s.means3D, s.opacities, s.scales, s.rotations, s.sh_dc, s.sh_rest)
+    st = rast.forward(*args, sh_degree=1)
+    f = oracle.forward(*args, sh_degree=1)
+    tiles = cam.grid[0] * cam.grid[1]
+    rng = _np(st.view(pkg("native").VIEW_RANGES, torch.int32, 2 * tiles)).view(np.uint32).reshape(-1, 2)
+    assert float((rng[:, 1] - rng[:, 0]).mean()) > 1500  # past the register form's slices
+    _compare(st, f, sc.make_dL_dpix(cam, seed=23), rast)
+
+
 def test_empty_and_culled(rast):
     gr, sc = pkg("graphics"), pkg("scene")
     cam = gr.synthetic_camera(64, 48)
