@@ -233,7 +233,7 @@ Views views(const gsr_camera* cam, long long n, const gsr_buffers* b) {
     v.offsets = at<uint32_t>(b->geom, gl.offsets);
     v.partials = at<uint32_t>(b->geom, gl.partials);
     v.lookback = at<uint32_t>(b->geom, gl.lookback);
-    v.presort = use_presort(n);
+    v.presort = use_presort(n, div_up(cam->width, kTile), div_up(cam->height, kTile));
     v.rb = (b->reserved & kBufRowBucketed) != 0;  // decided by the forward (fwd_phase2)
     v.rb_histA = at<uint32_t>(b->geom, gl.rb_hist);
     if (v.presort) {

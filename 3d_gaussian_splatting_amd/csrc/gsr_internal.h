@@ -66,10 +66,19 @@ inline size_t sort_scratch_words(long long n) { return 256 * ((size_t)radix_bloc
 // (its records / grad2d rows are random by gid in rank order) = 0.239 ms, against 0.211 for the
 // per-tile order (0.102 + scan 0.018 + 0.021 + 0.070): it pays only where the per-tile sort's
 // cost grows faster (5M: 0.49 ms), hence the 2^21 threshold.
+// Round 5: with the row-bucketed binning below it, the pre-sort pays only where tiles are deep:
+// it is taken when, besides, there are more than kPresortPerTile Gaussians per tile of the
+// image (a proxy for the mean slice, which is not known before the scan).  Measured (iters/s,
+// pre-sort vs row-bucketed): 5M / 1080p (613 per tile) 344 vs 367; 3M / 1280x832 (721) 577 vs
+// 577; 6M / 1280x832 (1442) 329 vs 281.
 #ifndef GSR_PRESORT_MIN
 #define GSR_PRESORT_MIN ((1 << 21) + 1)
 #endif
+#ifndef GSR_PRESORT_PER_TILE
+#define GSR_PRESORT_PER_TILE 700
+#endif
 constexpr long long kPresortMin = GSR_PRESORT_MIN;
+constexpr long long kPresortPerTile = GSR_PRESORT_PER_TILE;
 constexpr int kMaxViews = 8;  // gsr_forward_views: views per call (= GSR_MAX_VIEWS)
 // Row-bucketed binning (gsr_sort.hip): images of at most kRbMaxRows x kRbMaxCols tiles outside
 // presort mode; chunks of kRbChunkPairs (Gaussian, row) pairs in its second pass.
@@ -83,10 +92,15 @@ constexpr int kMaxViews = 8;  // gsr_forward_views: views per call (= GSR_MAX_VI
 constexpr int kRbMaxRows = 256, kRbMaxCols = 256, kRbChunkPairs = 1024;
 // gsr_buffers.reserved bits (set by the forward): the binning in use
 constexpr int32_t kBufRowBucketed = 1;
-inline bool use_rb_binning(long long n, int gx, int gy) {
-    return GSR_RB_BIN && n < kPresortMin && gx <= kRbMaxCols && gy <= kRbMaxRows;
+// the pre-sort's buffers (GeomLayout: sized from n alone) / the pre-sort itself for an image of
+// gx x gy tiles
+inline bool presort_possible(long long n) { return n >= kPresortMin; }
+inline bool use_presort(long long n, int gx, int gy) {
+    return presort_possible(n) && n > kPresortPerTile * (long long)gx * gy;
 }
-inline bool use_presort(long long n) { return n >= kPresortMin; }
+inline bool use_rb_binning(long long n, int gx, int gy) {
+    return GSR_RB_BIN && !use_presort(n, gx, gy) && gx <= kRbMaxCols && gy <= kRbMaxRows;
+}
 
 struct GeomLayout {
     size_t depth_key, tiles, flags, rec, rect, offsets, partials, lookback, rb_hist, total;
@@ -103,7 +117,7 @@ struct GeomLayout {
         partials = take(4 * ((size_t)sort_blocks(n) + 16));  // three-kernel scan
         lookback = take(4 * (16 + (n + 255) / 256));        // fused scan + duplicate; presort: block sums
         rb_hist = take(4 * (256 * ((n + 255) / 256) + 256));  // row-bucketed binning: [row][block] + row totals
-        if (use_presort(P)) {
+        if (presort_possible(P)) {
             dk0 = take(4 * n);
             dv0 = take(4 * n);
             dk1 = take(4 * n);

@@ -53,6 +53,10 @@ CONFIGS = {
     "100k_800": dict(P=100_000, W=800, H=800, D=3),
     "1m_1080p": dict(P=1_000_000, W=1920, H=1080, D=3),
     "5m_1080p": dict(P=5_000_000, W=1920, H=1080, D=3),
+    # the training loop's image size (BASELINE configs[4]) at two densities: A/B cases for the
+    # binning choice (global depth pre-sort vs row-bucketed binning), not bench lines
+    "3m_1280x832": dict(P=3_000_000, W=1280, H=832, D=3),
+    "6m_1280x832": dict(P=6_000_000, W=1280, H=832, D=3),
 }
 BASELINE_METRIC = "forward+backward iters/s at 1080p, 1M Gaussians; PSNR vs CPU ref"  # BASELINE.json
 

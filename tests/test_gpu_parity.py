@@ -272,15 +272,18 @@ def test_capacity_bound_and_overflow(rast):
     assert bool(torch.isfinite(st.color).all()) and all(bool(torch.isfinite(v).all()) for v in g.values())
 
 
-@pytest.mark.parametrize("P", [600_000, 1_000_000, 2_500_000])  # 2.5M: past the presort threshold
-def test_headline_config_vs_oracle(P, rast, oracle):
+@pytest.mark.parametrize("P,W,H", [(600_000, 1920, 1080), (1_000_000, 1920, 1080), (2_500_000, 1920, 1080),
+                                   (2_200_000, 800, 600)])
+def test_headline_config_vs_oracle(P, W, H, rast, oracle):
     """BASELINE configs[2] at 1920x1080 / SH3: 1M Gaussians is the bench's own workload (the same
-    make_scene seed), 600k a second draw of the same shape (both > 2^19: the three-kernel scan and
-    the per-tile depth sort; 8160 tiles: the two-wave F6), 2.5M past the global depth pre-sort's
-    threshold (rank-order payload, scan and F3), against the oracle: bit-exact keys, sort, ranges;
-    RGB and every gradient within the §8d bars, element-wise included."""
+    make_scene seed), 600k a second draw of the same shape (both > 2^19: the three-kernel scan,
+    the row-bucketed binning and the per-tile depth sort; 8160 tiles: the two-wave F6), 2.5M past
+    the global depth pre-sort's size threshold but below its density one (306 Gaussians per tile:
+    the row-bucketed binning still), 2.2M on 800x600 (1158 per tile) the pre-sort (rank-order
+    payload, scan and F3), against the oracle: bit-exact keys, sort, ranges; RGB and every
+    gradient within the §8d bars, element-wise included."""
     gr, sc = pkg("graphics"), pkg("scene")
-    cam = gr.synthetic_camera(1920, 1080)
+    cam = gr.synthetic_camera(W, H)
     s = sc.make_scene(cam, P, max_sh_degree=3, seed=0)
     dpix = sc.make_dL_dpix(cam, seed=1)
     args = (cam, s.means3D, s.opacities, s.scales, s.rotations, s.sh_dc, s.sh_rest)
