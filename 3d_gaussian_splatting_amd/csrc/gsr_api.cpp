@@ -855,7 +855,8 @@ int gsr_shard_forward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_
     GSR_STAGE(GSR_STAGE_EXCHANGE, launch_pack_splats(tiles, rect, depth_key, rec, P, br,
                                                      at<uint32_t>(shard_state, sl.partials), static_cast<char*>(send),
                                                      pair_cap, at<uint32_t>(shard_state, sl.slot_of), row_hist, gy,
-                                                     (rs->flags & GSR_FLAG_ROW_SPANS) != 0, stream),
+                                                     (rs->flags & GSR_FLAG_ROW_SPANS) != 0, stream,
+                                                     at<uint32_t>(shard_state, gl.rb_hist)),
               "pack splats");
     return 0;
 }

@@ -169,7 +169,7 @@ int launch_views_sum(const GaussIn& in, int V, const GradOut& out, const GradOut
 // partials: (sort_blocks(P) + 1) * nbands u32.
 int launch_pack_splats(const uint32_t* tiles, const uint4* rect, const uint32_t* depth_key, const float4* rec, int P,
                        const BandRows& br, uint32_t* partials, char* send, int pair_cap, uint32_t* slot_of,
-                       uint32_t* row_hist, int grid_y, bool spans, hipStream_t s);
+                       uint32_t* row_hist, int grid_y, bool spans, hipStream_t s, uint32_t* rowpart = nullptr);
 // Band side: nsrc received blocks -> local arrays of nsrc * pair_cap entries (empty slots: no tiles)
 // rb_hist / bsum (nullable, together): the row-bucketed binning's pass-A row counts and the F2 scan's
 // block partials per 256 slots, as F1 writes them for a single-GPU forward (PreOut.rb_hist / bsum)

@@ -30,11 +30,16 @@ __device__ inline uint64_t lanemask_lt() {
 // Gaussians whose rect starts / ends in that row (row_hist[gy + y]: first tile row y;
 // row_hist[2 gy + y]: last tile row y) -- from which the splats any band cut would receive
 // follow exactly: #(miny < r1) - #(maxy <= r0) (the live re-plan of the multi-GPU step).
+// With rowpart (at most 256 histogram rows), each block stores its rows there ([row][block],
+// the F1 row-count region, unused by a shard) and pack_scan_kernel sums them: one global atomic
+// per row instead of one per (block, row) -- thousands of blocks adding to the same ~200
+// addresses serialise at the L2 (~20 us at 625k Gaussians per shard).
 template <bool SPANS>
 __global__ __launch_bounds__(kB) void pack_count_kernel(const uint32_t* __restrict__ tiles,
                                                         const uint4* __restrict__ rect, int P, BandRows br,
                                                         uint32_t* __restrict__ partials, int nblk,
-                                                        uint32_t* __restrict__ row_hist, int grid_y) {
+                                                        uint32_t* __restrict__ row_hist, int grid_y,
+                                                        uint32_t* __restrict__ rowpart) {
     __shared__ uint32_t cnt[kWaves][kMaxBands];
     __shared__ uint32_t hist[(SPANS ? 3 : 1) * kMaxHistRows];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -75,18 +80,40 @@ __global__ __launch_bounds__(kB) void pack_count_kernel(const uint32_t* __restri
         for (int k = 0; k < kWaves; ++k) t += cnt[k][threadIdx.x];
         partials[threadIdx.x * nblk + blockIdx.x] = t;
     }
-    if (do_hist)
+    if (do_hist && rowpart)
+        for (int y = threadIdx.x; y < hrows; y += kB) rowpart[(size_t)y * nblk + blockIdx.x] = hist[y];
+    else if (do_hist)
         for (int y = threadIdx.x; y < hrows; y += kB)
             if (hist[y]) atomicAdd(row_hist + y, hist[y]);
 }
 
 // Block b: exclusive scan of band b's per-block counts in place; the band's total into its send
 // block's header (the true count, which may exceed pair_cap).
+// Blocks past the bands: histogram row (blockIdx.x - nbands) summed over the count blocks
+// (rowpart), added to row_hist.
 __global__ __launch_bounds__(1024) void pack_scan_kernel(uint32_t* __restrict__ partials, int nblk,
-                                                         char* __restrict__ send, size_t block_bytes) {
+                                                         char* __restrict__ send, size_t block_bytes, int nbands,
+                                                         const uint32_t* __restrict__ rowpart,
+                                                         uint32_t* __restrict__ row_hist) {
     __shared__ uint32_t wsum[16];
-    uint32_t* col = partials + (size_t)blockIdx.x * nblk;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    if ((int)blockIdx.x >= nbands) {  // block-uniform
+        const int y = (int)blockIdx.x - nbands;
+        const uint32_t* row = rowpart + (size_t)y * nblk;
+        uint32_t t = 0;
+        for (int i = tid; i < nblk; i += 1024) t += row[i];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+        if (lane == 0) wsum[w] = t;
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t sum = 0;
+            for (int k = 0; k < 16; ++k) sum += wsum[k];
+            if (sum) atomicAdd(row_hist + y, sum);
+        }
+        return;
+    }
+    uint32_t* col = partials + (size_t)blockIdx.x * nblk;
     uint32_t carry = 0;
     for (int base = 0; base < nblk; base += 1024) {
         const int i = base + tid;
@@ -273,7 +300,7 @@ __global__ __launch_bounds__(256) void unpack_kernel(const char* __restrict__ re
 
 int launch_pack_splats(const uint32_t* tiles, const uint4* rect, const uint32_t* depth_key, const float4* rec, int P,
                        const BandRows& br, uint32_t* partials, char* send, int pair_cap, uint32_t* slot_of,
-                       uint32_t* row_hist, int grid_y, bool spans, hipStream_t s) {
+                       uint32_t* row_hist, int grid_y, bool spans, hipStream_t s, uint32_t* rowpart) {
     const size_t bb = exchange_block_bytes(pair_cap);
     if (P <= 0) {  // empty shard: zero headers
         for (int b = 0; b < br.n; ++b)
@@ -281,13 +308,16 @@ int launch_pack_splats(const uint32_t* tiles, const uint4* rect, const uint32_t*
         return 0;
     }
     const int nblk = pack_blocks(P);
+    const int hrows = row_hist ? (spans ? 3 : 1) * grid_y : 0;
+    uint32_t* rp = hrows > 0 && hrows <= kRbMaxRows ? rowpart : nullptr;  // rowpart: [256][nblk] words
     if (spans && row_hist)
         hipLaunchKernelGGL(pack_count_kernel<true>, dim3(nblk), dim3(kB), 0, s, tiles, rect, P, br, partials, nblk,
-                           row_hist, grid_y);
+                           row_hist, grid_y, rp);
     else
         hipLaunchKernelGGL(pack_count_kernel<false>, dim3(nblk), dim3(kB), 0, s, tiles, rect, P, br, partials, nblk,
-                           row_hist, grid_y);
-    hipLaunchKernelGGL(pack_scan_kernel, dim3(br.n), dim3(1024), 0, s, partials, nblk, send, bb);
+                           row_hist, grid_y, rp);
+    hipLaunchKernelGGL(pack_scan_kernel, dim3(br.n + (rp ? hrows : 0)), dim3(1024), 0, s, partials, nblk, send, bb,
+                       br.n, rp, row_hist);
     hipLaunchKernelGGL(pack_scatter_kernel, dim3(nblk), dim3(kB), 0, s, tiles, rect, depth_key, rec, P, br, partials,
                        nblk, send, bb, pair_cap, slot_of);
     return (int)hipGetLastError();
