@@ -1411,6 +1411,175 @@ __device__ __forceinline__ void wave_sort_slice(const uint2 rg, const uint32_t* 
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// ---- the same network on 32-bit keys (slices of <= 1024 entries) ----
+// Key = the slice's top 22 differing depth bits over the entry's slice position (10 bits): half
+// the cross-lane traffic of the 64-bit key (one DPP / swizzle / bpermute per exchange, not two)
+// and a compare-exchange of one v_min_u32 + one v_max_u32.  Entries whose truncated depths are
+// equal (the depth bits below the top 22 differing ones, or the whole depth, tie) come out in
+// slice-position order; they are put in (depth, gid) order afterwards from the full keys -- in
+// place by the lane holding a run's first entry when the run is short, else by the 64-bit form.
+constexpr int kWaveKeyBits = 22, kWaveRunMax = 16;
+
+__device__ __forceinline__ void cas_up32(uint32_t& a, uint32_t& b) {
+    const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+    a = lo;
+    b = hi;
+}
+
+__device__ __forceinline__ uint32_t keep_side32(uint32_t a, uint32_t b, uint32_t flip) {
+    return bfi(flip, a > b ? a : b, a < b ? a : b);  // flip = ~0: max
+}
+
+template <int E, int J>
+__device__ __forceinline__ void wave_half_cleaners32(uint32_t (&v)[E], int lane) {
+    if constexpr (J >= 1) {
+        if constexpr (J >= E) {
+            constexpr int L = J / E;
+            const uint32_t flip = (lane & L) ? ~0u : 0u;
+#pragma unroll
+            for (int e = 0; e < E; ++e) v[e] = keep_side32(v[e], lane_xor<L>(v[e]), flip);
+        } else {
+#pragma unroll
+            for (int e = 0; e < E; ++e)
+                if ((e & J) == 0) cas_up32(v[e], v[e ^ J]);
+        }
+        wave_half_cleaners32<E, J / 2>(v, lane);
+    }
+}
+
+template <int E, int K>
+__device__ __forceinline__ void wave_bitonic32(uint32_t (&v)[E], int lane) {
+    if constexpr (K <= 64 * E) {
+        if constexpr (K <= E) {
+#pragma unroll
+            for (int e = 0; e < E; ++e)
+                if ((e & (K / 2)) == 0) cas_up32(v[e], v[e ^ (K - 1)]);
+        } else {
+            constexpr int M = K / E - 1;
+            const uint32_t flip = (lane & (K / (2 * E))) ? ~0u : 0u;
+            if constexpr (E == 1) {
+                v[0] = keep_side32(v[0], lane_xor<M>(v[0]), flip);
+            } else {
+#pragma unroll
+                for (int e = 0; e < E / 2; ++e) {
+                    const uint32_t pa = lane_xor<M>(v[E - 1 - e]), pb = lane_xor<M>(v[e]);
+                    v[e] = keep_side32(v[e], pa, flip);
+                    v[E - 1 - e] = keep_side32(v[E - 1 - e], pb, flip);
+                }
+            }
+        }
+        wave_half_cleaners32<E, K / 4>(v, lane);
+        wave_bitonic32<E, 2 * K>(v, lane);
+    }
+}
+
+template <int E>
+__device__ __forceinline__ void wave_sort_slice32(const uint2 rg, const uint32_t* __restrict__ depth_key,
+                                                  uint32_t* __restrict__ gid, int lane, uint32_t* xs) {
+    static_assert(64 * E <= (1 << (32 - kWaveKeyBits)), "slice position bits");
+    constexpr uint32_t kPos = (1u << (32 - kWaveKeyBits)) - 1u;
+    const int n = (int)(rg.y - rg.x);
+    uint32_t v[E], dk[E];
+    uint32_t kor = 0u, kand = ~0u;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = e * 64 + lane;
+        dk[e] = 0u;
+        if (i < n) {
+            dk[e] = depth_key[gid[rg.x + i]];
+            kor |= dk[e];
+            kand &= dk[e];
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        kor |= __shfl_xor(kor, o, 64);
+        kand &= __shfl_xor(kand, o, 64);
+    }
+    const uint32_t dif = kor ^ kand;
+    const int top = dif ? 32 - __clz(dif) : 0;  // differing bits [0, top)
+    const int sh = top > kWaveKeyBits ? top - kWaveKeyBits : 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = e * 64 + lane;
+        // padding ~0 sorts last: a real key reaches it only as the last of 1024 entries
+        v[e] = i < n ? (((dk[e] >> sh) & ((1u << kWaveKeyBits) - 1u)) << (32 - kWaveKeyBits)) | (uint32_t)i : ~0u;
+    }
+    wave_bitonic32<E, 2>(v, lane);
+    auto pad = [](int i) { return i + (i >> 5); };
+#pragma unroll
+    for (int e = 0; e < E; ++e) xs[pad(lane * E + e)] = v[e];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // runs of equal truncated keys: the lane holding a run's first entry orders it by the full
+    // (depth, gid) key (insertion; the slice's gids are still in place in gid[])
+    auto full = [&](uint32_t x) {
+        const uint32_t g = gid[rg.x + (x & kPos)];
+        return ((uint64_t)depth_key[g] << 32) | g;
+    };
+    bool tie = false, longrun = false;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int r = lane * E + e;
+        if (r + 1 < n && (v[e] >> (32 - kWaveKeyBits)) == (xs[pad(r + 1)] >> (32 - kWaveKeyBits))) tie = true;
+    }
+    if (__ballot(tie)) {  // wave-uniform; rare
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int r = lane * E + e;
+            const uint32_t top_r = v[e] >> (32 - kWaveKeyBits);
+            if (r + 1 >= n || (xs[pad(r + 1)] >> (32 - kWaveKeyBits)) != top_r) continue;
+            if (r > 0 && (xs[pad(r - 1)] >> (32 - kWaveKeyBits)) == top_r) continue;  // not the run's first
+            int end = r + 2;
+            while (end < n && (xs[pad(end)] >> (32 - kWaveKeyBits)) == top_r && end - r <= kWaveRunMax) ++end;
+            if (end - r > kWaveRunMax) {
+                longrun = true;
+                continue;
+            }
+            for (int a = r + 1; a < end; ++a) {
+                const uint32_t x = xs[pad(a)];
+                const uint64_t fx = full(x);
+                int b = a;
+                while (b > r && full(xs[pad(b - 1)]) > fx) {
+                    xs[pad(b)] = xs[pad(b - 1)];
+                    --b;
+                }
+                xs[pad(b)] = x;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (__ballot(longrun)) {  // many entries at one truncated depth: the 64-bit form
+            wave_sort_slice<E>(rg, depth_key, gid, lane, xs);
+            return;
+        }
+    }
+    // every read of the slice's gids completes before the first store over them (the compiler
+    // would otherwise store each result as soon as its own load returned, while later loads of the
+    // same slice were still in flight)
+    uint32_t og[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = e * 64 + lane;
+        og[e] = i < n ? gid[rg.x + (xs[pad(i)] & kPos)] : 0u;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = e * 64 + lane;
+        if (i < n) gid[rg.x + i] = og[e];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();  // xs reused by the wave's next slice
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+#ifndef GSR_WAVE_KEY32
+#define GSR_WAVE_KEY32 1
+#endif
+
 // Four tiles per 256-thread block, one per wave; slices longer than 1024 entries go to `ovf`.
 __global__ __launch_bounds__(256) void tile_depth_wave(const uint2* __restrict__ ranges, int tile0, int ntiles,
                                                       const uint32_t* __restrict__ depth_key,
@@ -1427,6 +1596,14 @@ __global__ __launch_bounds__(256) void tile_depth_wave(const uint2* __restrict__
     if (n <= 1) return;
     if (n > 1024) {
         if (lane == 0) ovf[atomicAdd(ovf_count, 1u)] = (uint32_t)tile;
+        return;
+    }
+    if (GSR_WAVE_KEY32) {
+        if (n <= 64) wave_sort_slice32<1>(rg, depth_key, gid, lane, xs);
+        else if (n <= 128) wave_sort_slice32<2>(rg, depth_key, gid, lane, xs);
+        else if (n <= 256) wave_sort_slice32<4>(rg, depth_key, gid, lane, xs);
+        else if (n <= 512) wave_sort_slice32<8>(rg, depth_key, gid, lane, xs);
+        else wave_sort_slice32<16>(rg, depth_key, gid, lane, xs);
         return;
     }
     if (n <= 64) wave_sort_slice<1>(rg, depth_key, gid, lane, xs);
