@@ -301,20 +301,46 @@ __global__ __launch_bounds__(kB) void scan_reduce(const uint32_t* __restrict__ i
     if (threadIdx.x == 0) partials[blockIdx.x] = tot;
 }
 
+// Exclusive scan of n words in place by one block of 1024 threads, kScanQ contiguous words per
+// thread per round (all of a round's loads issued before its block scan): one load latency and
+// one block scan per 8192 words, not per 1024 (the F2 block sums at 5M: 19.5k words).
+constexpr int kScanQ = 8;
+__device__ __forceinline__ uint32_t wide_block_scan(uint32_t* __restrict__ a, int n, uint32_t* wsum) {
+    uint32_t carry = 0;
+    for (int base = 0; base < n; base += 1024 * kScanQ) {
+        const int i0 = base + (int)threadIdx.x * kScanQ;
+        uint32_t v[kScanQ], sv = 0;
+#pragma unroll
+        for (int q = 0; q < kScanQ; ++q) {
+            v[q] = i0 + q < n ? a[i0 + q] : 0u;
+            sv += v[q];
+        }
+        uint32_t tot;
+        uint32_t run = carry + block_exclusive_scan(sv, wsum, &tot);
+#pragma unroll
+        for (int q = 0; q < kScanQ; ++q) {
+            if (i0 + q < n) a[i0 + q] = run;
+            run += v[q];
+        }
+        carry += tot;
+    }
+    return carry;
+}
+
 // exclusive scan of the nb block totals in place; the grand total to *total_out
 __global__ __launch_bounds__(1024) void scan_partials(uint32_t* __restrict__ partials, int nb,
                                                       uint32_t* __restrict__ total_out) {
     __shared__ uint32_t wsum[16];
-    uint32_t carry = 0;
-    for (int base = 0; base < nb; base += 1024) {
-        const int i = base + threadIdx.x;
-        const uint32_t v = i < nb ? partials[i] : 0u;
-        uint32_t tot;
-        const uint32_t ex = block_exclusive_scan(v, wsum, &tot);
-        if (i < nb) partials[i] = carry + ex;
-        carry += tot;
-    }
+    const uint32_t carry = wide_block_scan(partials, nb, wsum);
     if (threadIdx.x == 0 && total_out) *total_out = carry;
+}
+
+// the row-bucketed binning's column scan: row r's per-block pair counts (histA[r][*]) in place,
+// the row total to totA[r]; one 1024-thread block per row
+__global__ __launch_bounds__(1024) void rb_colscan(uint32_t* __restrict__ hist, int nb, uint32_t* __restrict__ totals) {
+    __shared__ uint32_t wsum[16];
+    const uint32_t carry = wide_block_scan(hist + (size_t)blockIdx.x * nb, nb, wsum);
+    if (threadIdx.x == 0) totals[blockIdx.x] = carry;
 }
 
 __global__ __launch_bounds__(kB) void scan_downsweep(const uint32_t* __restrict__ in, int n,
@@ -1898,7 +1924,7 @@ int launch_rb_binning(const uint32_t* tiles, uint4* rect, uint32_t* offsets, int
     uint32_t* const totA = histA + (size_t)256 * nbA;
     if (!rows_counted)
         hipLaunchKernelGGL(rb_rows_count, dim3(nbA), dim3(256), 0, s, tiles, rect, n, ty0, ty1, histA, nbA);
-    hipLaunchKernelGGL(radix_colscan, dim3(R), dim3(kB), 0, s, histA, nbA, totA);
+    hipLaunchKernelGGL(rb_colscan, dim3(R), dim3(1024), 0, s, histA, nbA, totA);
     hipLaunchKernelGGL(rb_rows_place, dim3(nbA), dim3(256), 0, s, tiles, rect, offsets, bsum, n, ty0, ty1, histA, totA,
                        nbA, pgid, pxr, cap);
     // chunks: at most cap / kRbChunk full ones plus one partial per row; the blocks walk them, so
