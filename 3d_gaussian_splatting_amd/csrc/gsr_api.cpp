@@ -380,8 +380,10 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
     }
     if (cap > 0 && v.rb) {
         // F3 + the tile sort + F5 as two counting passes; the pairs ride in (kB, vB)
+        // (the tile keys are left to the GSR_VIEW_SORTED_TILE accessor: nothing in the step reads them)
         GSR_STAGE(GSR_STAGE_TILE_SORT, launch_rb_binning(v.tiles, v.rect, v.offsets, (int)j.n, j.gx, j.ty0, j.ty1,
-                                                         v.rb_histA, v.rb_histB, v.rb_status, v.kB, v.vB, v.kA, v.vA,
+                                                         v.rb_histA, v.rb_histB, v.rb_status, v.kB, v.vB,
+                                                         GSR_RB_TILE_KEYS ? v.kA : nullptr, v.vA,
                                                          v.ranges, cap, stream, j.rows_counted,
                                                          j.rows_counted ? v.lookback + 16 : nullptr),
                   "row-bucketed binning");
@@ -976,7 +978,16 @@ const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, 
     const Views v = views(cam, bufs->n_local > 0 ? bufs->n_local : P, bufs);
     switch (what) {
         case GSR_VIEW_SORTED_GID: return v.sorted_gid;
-        case GSR_VIEW_SORTED_TILE: return v.sorted_tile;
+        case GSR_VIEW_SORTED_TILE:
+            if (v.rb && !GSR_RB_TILE_KEYS && bufs->binning && bufs->capacity > 0) {
+                // filled here from the ranges, on the null stream (ordered after the forward's
+                // stream work), and waited for: the accessor returns a finished array
+                if (launch_tile_keys_from_ranges(v.ranges, ImgLayout::tile_count(cam->width, cam->height),
+                                                 bufs->capacity, v.sorted_tile, nullptr) ||
+                    hipStreamSynchronize(nullptr) != hipSuccess)
+                    return nullptr;
+            }
+            return v.sorted_tile;
         case GSR_VIEW_RANGES: return v.ranges;
         case GSR_VIEW_FINAL_T: return v.final_T;
         case GSR_VIEW_N_CONTRIB: return nullptr;  // retired: B1 re-derives termination from T

@@ -85,6 +85,11 @@ constexpr int kMaxViews = 8;  // gsr_forward_views: views per call (= GSR_MAX_VI
 #ifndef GSR_RB_BIN
 #define GSR_RB_BIN 1
 #endif
+// GSR_RB_TILE_KEYS 1: the row-bucketed placement writes every instance's tile key in the step
+// (0: the GSR_VIEW_SORTED_TILE accessor fills them from the ranges when asked)
+#ifndef GSR_RB_TILE_KEYS
+#define GSR_RB_TILE_KEYS 0
+#endif
 // GSR_RB_DEEP 0: only where the per-tile sort takes its register form (mean slices <= ~1365)
 #ifndef GSR_RB_DEEP
 #define GSR_RB_DEEP 1

@@ -110,6 +110,7 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
 bool tile_wave_sort_eligible(long long K, int ntiles);
 
 // F5: ranges[tile] = [start, end) of the sorted tile keys (K = min(*K_dev, cap))
+int launch_tile_keys_from_ranges(const uint2* ranges, int tiles, long long cap, uint32_t* tkey, hipStream_t s);
 int launch_finalize(const uint32_t* sorted_tile, long long cap, const uint32_t* K_dev, uint2* ranges, hipStream_t s);
 
 // F6: per-tile front-to-back blend -> colour, final T, colour sum without background, the

@@ -1009,7 +1009,7 @@ __global__ __launch_bounds__(256) void rb_chunks_place(const uint32_t* __restric
                 } else {
                     const long long pos = (long long)gb[c] + k;
                     if (pos < cap) {
-                        tkey[pos] = row_tile + c;
+                        if (tkey) tkey[pos] = row_tile + c;
                         tgid[pos] = gg[q];
                     }
                 }
@@ -1021,7 +1021,7 @@ __global__ __launch_bounds__(256) void rb_chunks_place(const uint32_t* __restric
                 const int c = sc[i];
                 const long long pos = (long long)gb[c] + ((uint32_t)i - lb[c]);
                 if (pos < cap) {
-                    tkey[pos] = row_tile + (uint32_t)c;
+                    if (tkey) tkey[pos] = row_tile + (uint32_t)c;
                     tgid[pos] = sg[i];
                 }
             }
@@ -2061,6 +2061,21 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
     const int bgrid = ntiles < 256 ? ntiles : 256;
     hipLaunchKernelGGL(tile_depth_sort_big, dim3(bgrid), dim3(1024), 0, s, ranges, depth_key, gid, ovf2, ovf2_count,
                        done, scratch_hi, scratch_lo, uo);
+    return (int)hipGetLastError();
+}
+
+// The tile key of every listed instance from the ranges (the row-bucketed binning does not write
+// them in the step: only the GSR_VIEW_SORTED_TILE accessor reads them)
+__global__ __launch_bounds__(256) void tile_keys_from_ranges(const uint2* __restrict__ ranges, long long cap,
+                                                             uint32_t* __restrict__ tkey) {
+    const uint2 rg = ranges[blockIdx.x];
+    const uint32_t e = rg.y < cap ? rg.y : (uint32_t)cap;
+    for (uint32_t i = rg.x + threadIdx.x; i < e; i += 256) tkey[i] = blockIdx.x;
+}
+
+int launch_tile_keys_from_ranges(const uint2* ranges, int tiles, long long cap, uint32_t* tkey, hipStream_t s) {
+    if (tiles <= 0 || cap <= 0) return 0;
+    hipLaunchKernelGGL(tile_keys_from_ranges, dim3(tiles), dim3(256), 0, s, ranges, cap, tkey);
     return (int)hipGetLastError();
 }
 

@@ -252,7 +252,7 @@ int gsr_shard_backward(const gsr_camera* cam, const gsr_gaussians* shard, const 
 /* Introspection for tests / the benchmark (all device pointers into the caller's buffers,
  * or NULL when not applicable).  `what`: see gsr_view_* below. */
 #define GSR_VIEW_SORTED_GID 1       /* uint32[K]: Gaussian id of sorted instance i       */
-#define GSR_VIEW_SORTED_TILE 2      /* uint32[K]: tile id of sorted instance i             */
+#define GSR_VIEW_SORTED_TILE 2      /* uint32[K]: tile id of sorted instance i (row-bucketed binning: filled from the ranges by this call, on the null stream, synchronously) */
 #define GSR_VIEW_RANGES 3           /* uint32[2*tiles]: [start,end) per tile               */
 #define GSR_VIEW_FINAL_T 4          /* float[H*W]                                          */
 #define GSR_VIEW_N_CONTRIB 5        /* retired (always NULL): the blend no longer keeps a   
