@@ -76,18 +76,26 @@ def build_hip(verbose: bool = False, force: bool = False) -> str:
     if not force and os.path.exists(so) and os.path.exists(stamp_file) and open(stamp_file).read() == stamp:
         return so
     hipcc = _hipcc()
-    objs = []
+    obj_dir = os.path.join(LIB, "obj_hip")
+    os.makedirs(obj_dir, exist_ok=True)
 
     def compile_one(name):
+        # per-object content stamp (its source, the shared headers, its flags): an edit of one
+        # kernel file recompiles that file only
         src = os.path.join(CSRC, name)
-        obj = os.path.join(LIB, name + ".o")
+        obj = os.path.join(obj_dir, name + ".o")
         lang = ["-x", "hip"] if name.endswith(".cpp") else []
         cmd = [hipcc] + COMMON + HIP_SOURCES[name] + lang + ["-c", src, "-o", obj]
+        ostamp = _stamp([src] + _headers(), " ".join(cmd))
+        if not force and os.path.exists(obj) and os.path.exists(obj + ".stamp") and open(obj + ".stamp").read() == ostamp:
+            return obj
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {name}:\n{r.stdout}\n{r.stderr}")
         if verbose and r.stderr.strip():
             print(r.stderr)
+        with open(obj + ".stamp", "w") as fh:
+            fh.write(ostamp)
         return obj
 
     with cf.ThreadPoolExecutor(max_workers=min(8, len(HIP_SOURCES))) as ex:
@@ -96,8 +104,6 @@ def build_hip(verbose: bool = False, force: bool = False) -> str:
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
-    for o in objs:
-        os.remove(o)
     with open(stamp_file, "w") as fh:
         fh.write(stamp)
     return so

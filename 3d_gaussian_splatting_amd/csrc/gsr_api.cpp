@@ -221,6 +221,36 @@ struct Views {
     uint32_t *free_k, *free_v;           // the other ping-pong pair (scratch after the sort)
 };
 
+// The layout word a forward of n entries over gx x gy tiles, `ntiles` of them binned, with a
+// binning of `cap` instances writes (fwd_phase2): the row-bucketed binning where the image fits
+// it and the per-tile depth order can take it, the pre-sort on dense images.
+uint32_t expected_layout(long long n, int gx, int gy, long long cap, int ntiles) {
+    uint32_t w = GSR_LAYOUT_TAG;
+    if (use_presort(n, gx, gy)) w |= kBufPresort;
+    if (use_rb_binning(n, gx, gy) && cap > 0 && (GSR_RB_DEEP || tile_wave_sort_eligible(cap, ntiles)))
+        w |= kBufRowBucketed;
+    return w;
+}
+
+// Every use of a forward's buffers after the forward checks the layout word: missing tag (a
+// struct rebuilt without the field) or bits that disagree with what the forward of these sizes
+// chose would make the backward read the wrong arrays -- refused instead (ABI 4).
+int check_layout(const gsr_camera* cam, int ty0, int ty1, const gsr_buffers* b) {
+    if ((b->layout & GSR_LAYOUT_TAG_MASK) != GSR_LAYOUT_TAG)
+        return fail(GSR_ERR_LAYOUT,
+                    "gsr_buffers.layout = 0x%08x is not a forward's (ABI %d): pass the forward's gsr_buffers "
+                    "unchanged",
+                    b->layout, GSR_ABI_VERSION);
+    const int gx = div_up(cam->width, kTile), gy = div_up(cam->height, kTile);
+    const uint32_t want = expected_layout(b->n_local, gx, gy, b->capacity, (ty1 - ty0) * gx);
+    if (b->layout != want)
+        return fail(GSR_ERR_LAYOUT,
+                    "gsr_buffers.layout = 0x%08x disagrees with the buffers (0x%08x for %d entries, capacity %d, "
+                    "tile rows [%d, %d) of %d x %d)",
+                    b->layout, want, b->n_local, b->capacity, ty0, ty1, gx, gy);
+    return 0;
+}
+
 Views views(const gsr_camera* cam, long long n, const gsr_buffers* b) {
     Views v{};
     const GeomLayout gl(n);
@@ -234,7 +264,7 @@ Views views(const gsr_camera* cam, long long n, const gsr_buffers* b) {
     v.partials = at<uint32_t>(b->geom, gl.partials);
     v.lookback = at<uint32_t>(b->geom, gl.lookback);
     v.presort = use_presort(n, div_up(cam->width, kTile), div_up(cam->height, kTile));
-    v.rb = (b->reserved & kBufRowBucketed) != 0;  // decided by the forward (fwd_phase2)
+    v.rb = (b->layout & kBufRowBucketed) != 0;  // decided by the forward (fwd_phase2), checked by check_layout
     v.rb_histA = at<uint32_t>(b->geom, gl.rb_hist);
     if (v.presort) {
         v.dk0 = at<uint32_t>(b->geom, gl.dk0);
@@ -315,6 +345,7 @@ int fwd_phase1(FwdJob& j, gsr_alloc_fn alloc_geom, gsr_alloc_fn alloc_image, voi
     j.gy = div_up(H, kTile);
     band(cam, rs, &j.ty0, &j.ty1);
     std::memset(bufs, 0, sizeof *bufs);
+    bufs->layout = GSR_LAYOUT_TAG | (use_presort(j.n, j.gx, j.gy) ? kBufPresort : 0u);
     bufs->num_rendered = -1;
     bufs->n_local = (int32_t)j.n;
     bufs->geom = alloc_geom(ctx, GeomLayout(j.n).total);
@@ -364,7 +395,7 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
     // order (it leaves a tile's entries unordered, which that form does not mind); recorded in the
     // buffers so that every later view of them (backward, accessors) finds the same arrays.
     const bool scanned = use_rb_binning(j.n, j.gx, j.gy);  // phase 1 ran the three-kernel scan
-    if (scanned && cap > 0 && (GSR_RB_DEEP || tile_wave_sort_eligible(cap, ntiles))) bufs->reserved |= kBufRowBucketed;
+    bufs->layout = expected_layout(j.n, j.gx, j.gy, cap, ntiles);
     const Views v = views(cam, j.n, bufs);
     if (v.presort)
         GSR_STAGE(GSR_STAGE_DUPLICATE, launch_duplicate_ranked(v.rtiles, v.rrect, v.rect, (int)j.n, j.gx, j.ty0,
@@ -462,6 +493,7 @@ int blend_backward(const gsr_camera* cam, const gsr_raster_settings* rs, const g
     if (n <= 0) return 0;
     int ty0, ty1;
     band(cam, rs, &ty0, &ty1);
+    if (int e = check_layout(cam, ty0, ty1, bufs)) return e;
     const Views v = views(cam, n, bufs);
     if (!alloc_scratch) return fail(-1, "null scratch allocator");
     float* partial = static_cast<float*>(alloc_scratch(ctx, PartLayout(cap).total));
@@ -739,6 +771,7 @@ int gsr_backward_views(int32_t V, const gsr_camera* cams, const gsr_gaussians* g
     if (int e = check_grads(gs, grads)) return e;
     const long long n = (long long)V * gs->P;
     if (!bufs || bufs->n_local != n) return fail(-1, "forward buffers do not match V * P view entries");
+    if (int e = check_layout(&tall, 0, div_up(tall.height, kTile), bufs)) return e;
     if (!alloc_scratch) return fail(-1, "null scratch allocator");
     hipStream_t stream = (hipStream_t)stream_;
     const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
@@ -787,6 +820,11 @@ int gsr_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr_raste
     if (gs->P == 0) return 0;
     if (int e = check_grads(gs, grads)) return e;
     if (!bufs || bufs->n_local != gs->P) return fail(-1, "forward buffers do not match the Gaussians");
+    {
+        int ty0, ty1;
+        band(cam, rs, &ty0, &ty1);
+        if (int e = check_layout(cam, ty0, ty1, bufs)) return e;  // before any allocation
+    }
     hipStream_t stream = (hipStream_t)stream_;
     const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
     if (!alloc_scratch) return fail(-1, "null scratch allocator");
@@ -974,18 +1012,28 @@ const char* gsr_stage_name(int stage) {
 }
 
 const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, int what) {
+    g_err.clear();
     if (!cam || !bufs || !bufs->geom || !bufs->image) return nullptr;
+    if ((bufs->layout & GSR_LAYOUT_TAG_MASK) != GSR_LAYOUT_TAG) {
+        fail(GSR_ERR_LAYOUT, "gsr_view: gsr_buffers.layout = 0x%08x is not a forward's", bufs->layout);
+        return nullptr;
+    }
     const Views v = views(cam, bufs->n_local > 0 ? bufs->n_local : P, bufs);
     switch (what) {
         case GSR_VIEW_SORTED_GID: return v.sorted_gid;
         case GSR_VIEW_SORTED_TILE:
             if (v.rb && !GSR_RB_TILE_KEYS && bufs->binning && bufs->capacity > 0) {
-                // filled here from the ranges, on the null stream (ordered after the forward's
-                // stream work), and waited for: the accessor returns a finished array
-                if (launch_tile_keys_from_ranges(v.ranges, ImgLayout::tile_count(cam->width, cam->height),
+                // filled here from the ranges between two device-wide waits: the forward may have
+                // run on any stream, blocking or not (a torch pool stream, torch.cuda.stream(s)), and
+                // the null stream alone is not ordered after a non-blocking one; both
+                // waits fail during a stream capture, and the accessor then returns NULL
+                if (hipDeviceSynchronize() != hipSuccess ||
+                    launch_tile_keys_from_ranges(v.ranges, ImgLayout::tile_count(cam->width, cam->height),
                                                  bufs->capacity, v.sorted_tile, nullptr) ||
-                    hipStreamSynchronize(nullptr) != hipSuccess)
+                    hipDeviceSynchronize() != hipSuccess) {
+                    fail(-10, "gsr_view(GSR_VIEW_SORTED_TILE): device synchronisation failed (stream capture?)");
                     return nullptr;
+                }
             }
             return v.sorted_tile;
         case GSR_VIEW_RANGES: return v.ranges;

@@ -95,8 +95,10 @@ constexpr int kMaxViews = 8;  // gsr_forward_views: views per call (= GSR_MAX_VI
 #define GSR_RB_DEEP 1
 #endif
 constexpr int kRbMaxRows = 256, kRbMaxCols = 256, kRbChunkPairs = 1024;
-// gsr_buffers.reserved bits (set by the forward): the binning in use
-constexpr int32_t kBufRowBucketed = 1;
+// gsr_buffers.layout (set by the forward, checked by every later use of the buffers): the tag
+// and the binning in use (gsr.h GSR_LAYOUT_*)
+constexpr uint32_t kBufRowBucketed = GSR_LAYOUT_ROW_BUCKETED;
+constexpr uint32_t kBufPresort = GSR_LAYOUT_PRESORT;
 // the pre-sort's buffers (GeomLayout: sized from n alone) / the pre-sort itself for an image of
 // gx x gy tiles
 inline bool presort_possible(long long n) { return n >= kPresortMin; }

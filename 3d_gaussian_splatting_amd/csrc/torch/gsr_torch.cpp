@@ -138,9 +138,9 @@ FwdResult forward_impl(const RasterCamera& cam, const RasterSettings& rs, const 
 }
 
 gsr_buffers buffers_of(const torch::Tensor& geom, const torch::Tensor& binning, const torch::Tensor& image,
-                       int32_t K, int32_t cap, int32_t n_local, int32_t mode) {
+                       int32_t K, int32_t cap, int32_t n_local, uint32_t layout) {
     gsr_buffers b{};
-    b.reserved = mode;  // the binning the forward used (gsr.h)
+    b.layout = layout;  // the forward's layout word (gsr.h): the backward checks it
     b.geom = geom.data_ptr();
     b.binning = binning.defined() ? binning.data_ptr() : nullptr;
     b.image = image.data_ptr();
@@ -166,7 +166,7 @@ class RasterizeGaussians : public torch::autograd::Function<RasterizeGaussians> 
         ctx->saved_data["K"] = (int64_t)r.bufs.num_rendered;
         ctx->saved_data["cap"] = (int64_t)r.bufs.capacity;
         ctx->saved_data["n_local"] = (int64_t)r.bufs.n_local;
-        ctx->saved_data["bufmode"] = (int64_t)r.bufs.reserved;
+        ctx->saved_data["layout"] = (int64_t)r.bufs.layout;
         ctx->saved_data["cam_w"] = (int64_t)cam.width;
         ctx->saved_data["cam_h"] = (int64_t)cam.height;
         ctx->saved_data["cam_tx"] = (double)cam.tanfovx;
@@ -213,7 +213,7 @@ class RasterizeGaussians : public torch::autograd::Function<RasterizeGaussians> 
         const int32_t K = (int32_t)ctx->saved_data["K"].toInt();
         const int32_t cap = (int32_t)ctx->saved_data["cap"].toInt();
         const int32_t n_local = (int32_t)ctx->saved_data["n_local"].toInt();
-        const int32_t bufmode = (int32_t)ctx->saved_data["bufmode"].toInt();
+        const uint32_t layout = (uint32_t)ctx->saved_data["layout"].toInt();
         auto dL_dcolor = grad_out[0].contiguous();
         const int64_t P = means3D.size(0);
         auto fo = means3D.options();
@@ -248,7 +248,7 @@ class RasterizeGaussians : public torch::autograd::Function<RasterizeGaussians> 
         const gsr_camera c = cam.to_c();
         const gsr_gaussians g = make_gaussians(rs, means3D, sh_dc, sh_rest, colors, opac, scales, rots, cov3D);
         const gsr_raster_settings s = make_settings(rs);
-        const gsr_buffers b = buffers_of(geom, binning, image, K, cap, n_local, bufmode);
+        const gsr_buffers b = buffers_of(geom, binning, image, K, cap, n_local, layout);
         AllocCtx scratch{means3D.device(), {}};
         check(gsr_backward(&c, &g, &s, &b, dL_dcolor.data_ptr<float>(), alloc_cb, &scratch, &gg, cur_stream()),
               "gsr_backward");

@@ -20,7 +20,7 @@ LIB_DIR = os.path.join(PKG, "lib")
 # GSR_HIP_LIB: an experiment build (lib/variants/<name>/libgsr_hip.so) instead of the shipped one
 HIP_LIB = os.environ.get("GSR_HIP_LIB") or os.path.join(LIB_DIR, "libgsr_hip.so")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 GSR_FLAG_DEBUG = 1
 GSR_FLAG_ROW_SPANS = 2  # gsr.h: gsr_shard_forward row_hist = 3 x grid_y (instances, rect start rows, end rows)
 GSR_ERR_OVERFLOW = -4
@@ -87,7 +87,7 @@ class Grads(ctypes.Structure):
 class Buffers(ctypes.Structure):
     _fields_ = [("geom", ctypes.c_void_p), ("binning", ctypes.c_void_p), ("image", ctypes.c_void_p),
                 ("num_rendered", ctypes.c_int32), ("capacity", ctypes.c_int32), ("n_local", ctypes.c_int32),
-                ("reserved", ctypes.c_int32)]
+                ("layout", ctypes.c_uint32)]
 
 
 class AdamGroup(ctypes.Structure):

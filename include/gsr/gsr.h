@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 3
+#define GSR_ABI_VERSION 4
 #define GSR_TILE 16 /* screen tiles are GSR_TILE x GSR_TILE pixels */
 #define GSR_GRAD2D_STRIDE 12 /* floats per Gaussian in a grad2d buffer (9 used) */
 
@@ -120,8 +120,17 @@ typedef struct gsr_buffers {
                                 the device (max_rendered > 0; see gsr_read_num_rendered) */
     int32_t capacity;        /* instances the binning (and the backward's scratch) hold */
     int32_t n_local;         /* Gaussians (or received splat slots, gsr_band_forward) indexed */
-    int32_t reserved;        /* set by the forward: the binning in use (keep it with the buffers) */
+    uint32_t layout;         /* set by the forward: GSR_LAYOUT_TAG | GSR_LAYOUT_* bits, which arrays of
+                                the binning hold the sorted list.  Pass the forward's gsr_buffers to the
+                                backward / gsr_view unchanged: a word without the tag (e.g. a struct
+                                rebuilt with this field zeroed) or with bits that disagree with the
+                                buffers' sizes is refused (< 0, gsr_last_error), never read blindly */
 } gsr_buffers;
+#define GSR_LAYOUT_TAG 0x47530000u      /* 'G' 'S' in the upper half: written by a forward (ABI 4) */
+#define GSR_LAYOUT_TAG_MASK 0xFFFF0000u
+#define GSR_LAYOUT_ROW_BUCKETED 1u      /* row-bucketed binning (tile keys not stored in the step) */
+#define GSR_LAYOUT_PRESORT 2u           /* global depth pre-sort (rank-order payload) */
+#define GSR_ERR_LAYOUT (-13)            /* gsr_buffers.layout missing or inconsistent */
 
 int gsr_abi_version(void);
 const char* gsr_last_error(void);
@@ -252,7 +261,10 @@ int gsr_shard_backward(const gsr_camera* cam, const gsr_gaussians* shard, const 
 /* Introspection for tests / the benchmark (all device pointers into the caller's buffers,
  * or NULL when not applicable).  `what`: see gsr_view_* below. */
 #define GSR_VIEW_SORTED_GID 1       /* uint32[K]: Gaussian id of sorted instance i       */
-#define GSR_VIEW_SORTED_TILE 2      /* uint32[K]: tile id of sorted instance i (row-bucketed binning: filled from the ranges by this call, on the null stream, synchronously) */
+#define GSR_VIEW_SORTED_TILE 2      /* uint32[K]: tile id of sorted instance i (row-bucketed binning:
+                                       filled from the ranges by this call between two device-wide
+                                       synchronisations, so it follows the forward on whatever stream
+                                       ran it, blocking or not; NULL while a stream is being captured) */
 #define GSR_VIEW_RANGES 3           /* uint32[2*tiles]: [start,end) per tile               */
 #define GSR_VIEW_FINAL_T 4          /* float[H*W]                                          */
 #define GSR_VIEW_N_CONTRIB 5        /* retired (always NULL): the blend no longer keeps a   
@@ -274,6 +286,7 @@ int gsr_shard_backward(const gsr_camera* cam, const gsr_gaussians* shard, const 
                                        = the tile's first index in the sorted list          */
 #define GSR_VIEW_RECORDS 8          /* float4[3*P]: {x,y,a',b'},{c',o,r,g},{b,ext_x,ext_y,log2 o};
                                        a',b',c' = -log2(e) * (A/2, B, C/2) of the conic */
+/* NULL (and gsr_last_error set) for buffers whose layout word is not a forward's. */
 const void* gsr_view(const gsr_camera* cam, int32_t P, const gsr_buffers* bufs, int what);
 
 /* Optional stage profiler (off by default; process-wide, mutex-protected).  When enabled,
@@ -298,7 +311,7 @@ int gsr_profile_read(double* ms, uint32_t* counts);
 const char* gsr_stage_name(int stage);
 
 /* Byte sizes the allocation callbacks will be asked for (for pre-sizing pools).  The binning
- * buffer holds the instance arrays for `capacity` instances and the B1 checkpoint slots (ABI 3:
+ * buffer holds the instance arrays for `capacity` instances and the B1 checkpoint slots (ABI >= 3:
  * min(31 per tile, capacity / 48 + tiles + 1) slots of 4 KB -- a chunk opens only after 192
  * visited (record, stripe) pairs, so a tile of n instances opens at most n / 48 -- instead of a
  * fixed 31 per tile in the image buffer). */

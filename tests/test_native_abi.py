@@ -90,7 +90,7 @@ def test_library_exports_every_symbol():
 def test_library_loads_and_reports_sizes():
     native = pkg("native")
     L = native.load_hip()
-    assert L.gsr_abi_version() == native.ABI_VERSION == 3
+    assert L.gsr_abi_version() == native.ABI_VERSION == 4
     assert L.gsr_geom_bytes(1000) > 1000 * 64
     assert L.gsr_binning_bytes(10, 64, 64) >= 10 * 24
     assert L.gsr_image_bytes(1920, 1080) >= 1920 * 1080 * 8
@@ -188,7 +188,7 @@ def test_validation_rejects_bad_arguments_without_gpu():
 def test_torch_extension_loads():
     native = pkg("native")
     ext = native.load_torch_ext()
-    assert ext.abi_version() == 3
+    assert ext.abi_version() == 4
     cam = ext.RasterCamera(16, 16, 0.5, 0.5, [0.0] * 16, [0.0] * 16, [0.0] * 3)
     assert cam.width == 16
 
@@ -232,3 +232,52 @@ def test_bench_metric_names():
     names = {bench.config_metric(k) for k in bench.CONFIGS}
     assert len(names) == len(bench.CONFIGS)
     assert "5M Gaussians" in bench.config_metric("5m_1080p")
+
+
+def test_backward_refuses_bad_layout_word():
+    """ABI 4: gsr_buffers.layout carries the forward's binning choice; a
+    backward handed a struct whose word is zeroed (rebuilt without the field) or disagrees with
+    what a forward of these buffers chooses returns GSR_ERR_LAYOUT with the reason, before any
+    allocation or launch -- it never reads the other binning's arrays.  gsr_view returns NULL."""
+    native = pkg("native")
+    L = native.load_hip()
+    text = open(HEADER).read()
+    hexval = lambda name: int(re.search(rf"#define {name} (0x[0-9A-Fa-f]+|\d+)u?", text).group(1), 0)
+    TAG, RB = hexval("GSR_LAYOUT_TAG"), hexval("GSR_LAYOUT_ROW_BUCKETED")
+    err = int(re.search(r"#define GSR_ERR_LAYOUT \((-\d+)\)", text).group(1))
+    c = native.Camera()
+    c.width, c.height = 64, 48
+    g = native.Gaussians()
+    g.P, g.sh_degree = 5, 0
+    fake = ctypes.c_void_p(1 << 20)  # never dereferenced: the check comes first
+    g.means3D = g.opacities = g.sh_dc = g.scales = g.rotations = fake
+    s = native.Settings()
+    s.tile_y1 = 2**31 - 1
+    gr = native.Grads()
+    gr.dL_dmeans2D = gr.dL_dopacity = gr.dL_dmeans3D = gr.dL_dsh_dc = gr.dL_dscales = gr.dL_drotations = fake
+    calls = []
+    alloc = native.ALLOC_FN(lambda _c, n: calls.append(n) or 0)
+
+    def backward(layout, capacity):
+        b = native.Buffers()
+        b.geom = b.binning = b.image = fake
+        b.n_local, b.capacity, b.num_rendered, b.layout = 5, capacity, capacity, layout
+        return L.gsr_backward(ctypes.byref(c), ctypes.byref(g), ctypes.byref(s), ctypes.byref(b), fake, alloc, None,
+                              ctypes.byref(gr), None), b
+
+    rc, b = backward(0, 64)  # a struct rebuilt with the word zeroed
+    assert rc == err and "not a forward's" in native.last_error(), native.last_error()
+    rc, _ = backward(TAG, 64)  # tagged, but a 4 x 3-tile image of 5 Gaussians takes the row-bucketed binning
+    assert rc == err and "disagrees" in native.last_error(), native.last_error()
+    rc, _ = backward(TAG | RB, 0)  # an empty binning never takes it
+    assert rc == err and "disagrees" in native.last_error(), native.last_error()
+    assert calls == [], "nothing may be allocated before the layout check"
+    b.layout = 0
+    L.gsr_view.restype = ctypes.c_void_p
+    assert L.gsr_view(ctypes.byref(c), 5, ctypes.byref(b), 1) is None
+    assert "layout" in native.last_error()
+    # gsr_backward_blend / gsr_band_backward share the check (blend_backward)
+    grad2d = fake
+    rc = L.gsr_backward_blend(ctypes.byref(c), ctypes.byref(g), ctypes.byref(s), ctypes.byref(b), fake, alloc, None,
+                              grad2d, None)
+    assert rc == err and calls == []
