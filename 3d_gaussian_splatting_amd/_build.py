@@ -154,10 +154,9 @@ def build_variant(name: str, defines: list, verbose: bool = False, csrc: str | N
     os.makedirs(out_dir, exist_ok=True)
     so = os.path.join(out_dir, "libgsr_hip.so")
     hipcc = _hipcc()
-    objs = []
-    for src_name, flags in HIP_SOURCES.items():
-        if not os.path.exists(os.path.join(src_dir, src_name)):  # an older commit's sources
-            continue
+
+    def one(src_name):
+        flags = HIP_SOURCES[src_name]
         obj = os.path.join(out_dir, src_name + ".o")
         lang = ["-x", "hip"] if src_name.endswith(".cpp") else []
         cmd = [hipcc] + COMMON + flags + ["-D" + d for d in defines] + lang + ["-I" + src_dir, "-c",
@@ -165,7 +164,11 @@ def build_variant(name: str, defines: list, verbose: bool = False, csrc: str | N
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src_name}:\n{r.stderr}")
-        objs.append(obj)
+        return obj
+
+    names = [n for n in HIP_SOURCES if os.path.exists(os.path.join(src_dir, n))]  # an older commit's sources
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(names))) as ex:
+        objs = list(ex.map(one, names))
     r = subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", so] + objs + LINK_LIBS,
                        capture_output=True, text=True)
     if r.returncode != 0:

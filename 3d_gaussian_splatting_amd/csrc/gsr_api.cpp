@@ -8,6 +8,7 @@
 // No persistent allocations; every scratch buffer comes from the caller's callbacks.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 #include <cstdlib>
 #include <cstdarg>
@@ -496,17 +497,21 @@ int blend_backward(const gsr_camera* cam, const gsr_raster_settings* rs, const g
     if (int e = check_layout(cam, ty0, ty1, bufs)) return e;
     const Views v = views(cam, n, bufs);
     if (!alloc_scratch) return fail(-1, "null scratch allocator");
-    float* partial = static_cast<float*>(alloc_scratch(ctx, PartLayout(cap).total));
+    // band launches split each (tile, chunk) of B1 over `split` waves by stripe, one partial
+    // entry per (instance, part)
+    int split = b1_split(cam->width, cam->height, ty0, ty1, vgy);
+    if (cap * split > (long long)UINT32_MAX) split = 1;  // entry indices are u32
+    float* partial = static_cast<float*>(alloc_scratch(ctx, PartLayout(cap * split).total));
     if (!partial) return fail(-2, "allocation failed (scratch, %lld instances)", cap);
     // only the per-entry flag bytes are zeroed: the gather reads the entries B1 flagged
-    GSR_STAGE(GSR_STAGE_MISC, launch_clear_flags(partial, cap, stream), "clear partial flags");
+    GSR_STAGE(GSR_STAGE_MISC, launch_clear_flags(partial, cap * split, stream), "clear partial flags");
     GSR_STAGE(GSR_STAGE_BLEND_BWD, launch_blend_backward(*cam, rs->bg, ty0, ty1, v.ranges, v.sorted_gid, v.rect, v.rec,
                                                          v.final_T, v.accum, dL_dpix, partial, cap, v.term, v.ck,
-                                                         stream, vgy, vh, v.mk),
+                                                         stream, vgy, vh, v.mk, split),
               "blend backward");
     GSR_STAGE(GSR_STAGE_GATHER, launch_gather_grad2d(v.offsets, partial, v.rec, cam->width, vgy > 0 ? vh : cam->height,
                                                      cap, (int)n,
-                                                     v.presort ? v.rrect : nullptr, grad2d, stream),
+                                                     v.presort ? v.rrect : nullptr, grad2d, stream, split),
               "gather grad2d");
     return 0;
 }
@@ -965,6 +970,52 @@ int gsr_shard_backward(const gsr_camera* cam, const gsr_gaussians* gs, const gsr
                                                                           at<uint32_t>(shard_state, gl.flags), bs,
                                                                           grad_out(grads), stream),
               "preprocess backward (band sum)");
+    return 0;
+}
+
+int gsr_band_publish(const gsr_camera* cam, const gsr_raster_settings* rs, int32_t tall, const float* out_color,
+                     int32_t nbands, const void* send, int32_t pair_cap, const gsr_buffers* bufs, float* row,
+                     int64_t status_off, void* stream_) {
+    g_err.clear();
+    if (!cam || !rs || !out_color || !send || !bufs || !bufs->image || !row) return fail(-1, "publish: null argument");
+    if (cam->width <= 0 || cam->height <= 0) return fail(-1, "publish: bad image size");
+    if (nbands < 1 || nbands > kMaxBands || pair_cap < 0) return fail(-1, "publish: bad nbands / pair_cap");
+    int ty0, ty1;
+    band(cam, rs, &ty0, &ty1);
+    const int py0 = std::min(ty0 * kTile, cam->height), py1 = std::min(ty1 * kTile, cam->height);
+    if (tall < py1 - py0) return fail(-1, "publish: tall (%d) below the band's %d pixel rows", tall, py1 - py0);
+    if (status_off < 3LL * tall * cam->width) return fail(-1, "publish: status words overlap the pixels");
+    const ImgLayout il(cam->width, cam->height);
+    const uint32_t* K_dev = at<uint32_t>(bufs->image, il.counters) + kTotalSlot;
+    hipStream_t stream = (hipStream_t)stream_;
+    const bool debug = (rs->flags & GSR_FLAG_DEBUG) != 0;
+    GSR_STAGE(GSR_STAGE_EXCHANGE, launch_band_publish(out_color, cam->width, cam->height, py0, py1, tall, row,
+                                                      status_off, static_cast<const char*>(send),
+                                                      exchange_block_bytes(pair_cap), nbands, K_dev, stream),
+              "band publish");
+    return 0;
+}
+
+int gsr_gather_finish(const gsr_camera* cam, int32_t world, const int32_t* band_rows, int32_t tall,
+                      const float* gathered, int64_t row_floats, int64_t status_off, int32_t pair_cap,
+                      int32_t capacity, float* image, int32_t* guard, float* zero, int64_t nzero, void* stream_) {
+    g_err.clear();
+    if (!cam || !gathered || !image || !guard || (nzero > 0 && !zero)) return fail(-1, "gather finish: null argument");
+    if (cam->width <= 0 || cam->height <= 0) return fail(-1, "gather finish: bad image size");
+    BandRows br;
+    if (int e = band_rows_of(world, band_rows, div_up(cam->height, kTile), br)) return e;
+    for (int r = 0; r < world; ++r)
+        if (std::min(br.row[r + 1] * kTile, cam->height) - std::min(br.row[r] * kTile, cam->height) > tall)
+            return fail(-1, "gather finish: band %d is taller than tall (%d)", r, tall);
+    if (status_off < 3LL * tall * cam->width || status_off + world + 1 > row_floats || nzero < 0 || nzero > INT32_MAX)
+        return fail(-1, "gather finish: bad row layout");
+    hipStream_t stream = (hipStream_t)stream_;
+    const bool debug = false;
+    GSR_STAGE(GSR_STAGE_EXCHANGE, launch_gather_finish(gathered, row_floats, status_off, world, br, cam->width,
+                                                       cam->height, tall, image, (uint32_t)std::max(pair_cap, 0),
+                                                       (uint32_t)std::max(capacity, 0), guard, zero, (int)nzero,
+                                                       stream),
+              "gather finish");
     return 0;
 }
 

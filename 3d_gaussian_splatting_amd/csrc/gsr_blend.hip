@@ -514,7 +514,15 @@ __device__ __forceinline__ void park_flush(const float* qpark, const uint32_t* s
 // entries are mostly culled, e.g. after an opacity reset -- fewer serial window loads).
 constexpr int kB1Win = GSR_B1_WIN;
 static_assert(kB1Win == 4 || kB1Win == 16, "B1 window: 4 or 16 mask bytes per lane");
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void blend_backward_kernel(const BlendGeom geo,
+// SPW: the 16x4 stripes one wave owns.  4 (full images): one wave per (tile, chunk) and one
+// partial entry per (tile, instance).  2 or 1 (band launches, b1_split): the (tile, chunk) is
+// split over 4 / SPW one-wave blocks by stripe ("parts"), each running the same front-to-back
+// loop over its own pixels only -- its own termination, its own visit filter -- and writing
+// its own partial entry j * parts + part, which the gather sums with the others in part order.
+// A band of 1/8 of the tiles then still fills the chip (~3.3 chunks per tile leave ~3 one-wave
+// blocks per SIMD otherwise), at the price of per-record work repeated per part.
+template <int SPW>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SPW == 4 ? 6 : 8))) void blend_backward_kernel(const BlendGeom geo,
                                                             const uint2* __restrict__ ranges,
                                                             const uint32_t* __restrict__ sorted_gid,
                                                             const uint4* __restrict__ rect,
@@ -540,11 +548,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
     float4* const srec = lds.srec;
     uint32_t* const sjl = lds.sjl;
     float* const qpark = lds.qpark;
+    constexpr int S = kPPL / SPW;  // parts per (tile, chunk)
+    static_assert(SPW == 4 || SPW == 2 || SPW == 1, "stripes per wave");
     const int lane = threadIdx.x;
     float* const qlane = qpark + (lane >> 2) * 12;  // this quad's parking row
     int tl, chunk;
+    const int part = (int)((blockIdx.x / 8) % S);  // the (tile, chunk)'s parts are neighbours
+    const int sp0 = part * SPW;                      // this wave's first stripe
     {
-        const int q = geo.nwg / 8, r = geo.nwg % 8, xcd = blockIdx.x % 8, local = blockIdx.x / 8;
+        const int q = geo.nwg / 8, r = geo.nwg % 8, xcd = blockIdx.x % 8, local = (int)((blockIdx.x / 8) / S);
         const int t0 = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q, nt = q + (xcd < r ? 1 : 0);
         const int per = q + 1;  // padded tiles per XCD
         chunk = local / per;
@@ -579,10 +591,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
     accum += (size_t)view * 3 * npix;
     dL_dpix += (size_t)view * 3 * npix;
     // R = S . dL/dpix - Sp + T_final bg . dL/dpix: the colour term behind the current record
-    float pfy[kPPL], T[kPPL], R[kPPL], dp0[kPPL], dp1[kPPL], dp2[kPPL];
+    float pfy[SPW], T[SPW], R[SPW], dp0[SPW], dp1[SPW], dp2[SPW];
 #pragma unroll
-    for (int p = 0; p < kPPL; ++p) {
-        const int pyl = tyl * kTile + row + 4 * p;
+    for (int p = 0; p < SPW; ++p) {
+        const int pyl = tyl * kTile + row + 4 * (sp0 + p);
         pfy[p] = (float)pyl;
         const bool in = px < geo.W && pyl < geo.vh;
         const size_t pix = in ? (size_t)pyl * geo.W + px : 0;
@@ -602,9 +614,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
         const uint32_t on = *reinterpret_cast<const uint32_t*>(
             reinterpret_cast<const uint8_t*>(ck + (size_t)geo.ck_slots * 256) + 4 * slot);
 #pragma unroll
-        for (int p = 0; p < kPPL; ++p) {
-            if ((on >> (8 * p)) & 0xFFu) {  // wave-uniform
-                const float4 c4 = src[64 * p + col + 16 * row];  // F6's lane of this pixel
+        for (int p = 0; p < SPW; ++p) {
+            if ((on >> (8 * (sp0 + p))) & 0xFFu) {  // wave-uniform
+                const float4 c4 = src[64 * (sp0 + p) + col + 16 * row];  // F6's lane of this pixel
                 T[p] = c4.x;
                 R[p] -= fmaf(c4.y, dp0[p], fmaf(c4.z, dp1[p], c4.w * dp2[p]));
             } else {
@@ -616,9 +628,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
     // past tend no pixel is live
     const int n_lim = n < (int)tend ? n : (int)tend;
     for (int base = start; base < n_lim;) {
-        uint32_t live = 0;
+        uint32_t live = 0;  // in stripe positions (the mask bytes' bits)
 #pragma unroll
-        for (int p = 0; p < kPPL; ++p) live |= __any(T[p] > 0.0f) ? (1u << p) : 0u;
+        for (int p = 0; p < SPW; ++p) live |= __any(T[p] > 0.0f) ? (1u << (sp0 + p)) : 0u;
         if (live == 0) break;
         // the batch: up to 64 entries with a live stripe among the next 256 (four mask bytes
         // per lane from one aligned word), in list order; the next batch starts after the last
@@ -676,7 +688,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
             jl = rr.z + (uint32_t)((ty - y0) * (maxx - minx) + (tx - minx));
             // past the capacity: an overflowing binning (the row-bucketed one keeps list
             // positions, not emission indices, below it) -- the entry is not written
-            if (jl >= geo.cap) jl = 0xFFFFFFFFu;
+            jl = jl >= geo.cap ? 0xFFFFFFFFu : jl * S + part;  // this part's entry
             const float4* r = rec + 3 * (size_t)g;
             srec[3 * lane + 0] = r[0];
             srec[3 * lane + 1] = r[1];
@@ -701,8 +713,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
             float s0 = -0.f, sy = -0.f, syy = -0.f, g0 = -0.f, g1 = -0.f, g2 = -0.f;
             bool any = false;
 #pragma unroll
-            for (int p = 0; p < kPPL; ++p) {
-                if (!(m & (1u << p))) continue;  // wave-uniform
+            for (int p = 0; p < SPW; ++p) {
+                if (!(m & (1u << (sp0 + p)))) continue;  // wave-uniform
                 const float dy = r0.y - pfy[p];
                 const float e = fmaf(fmaf(r1.x, dy, bdx), dy, K);
                 float oG;
@@ -751,7 +763,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void bl
             if ((++visited & 7) == 0) {
                 uint32_t lv = 0;
 #pragma unroll
-                for (int p = 0; p < kPPL; ++p) lv |= __any(T[p] > 0.0f) ? (1u << p) : 0u;
+                for (int p = 0; p < SPW; ++p) lv |= __any(T[p] > 0.0f) ? (1u << (sp0 + p)) : 0u;
                 live = lv;
                 if (live == 0) return true;
             }
@@ -814,21 +826,49 @@ int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int 
     return (int)hipGetLastError();
 }
 
+// B1 parts per (tile, chunk) (blend_backward_kernel's 4 / SPW) on launches of fewer than
+// GSR_B1_SPLIT_TILES tiles of one image (multi-GPU bands).  Measured at 1M / 1080p, N = 8
+// (rehearsal kernel trace, mean band B1 / gather; profiles/r06_experiments/b1_split_1m_w8.txt):
+// 1 part 101.8 / 24.7 us, 2 parts 101.4 / 50.9, 4 parts 130.0 / 115.4 -- a part repeats the
+// record's set-up, batch loads and reduction for fewer stripes, and the per-chunk chain is set
+// by that per-record work, not by the stripes; so the split is built but off (1).
+#ifndef GSR_B1_SPLIT_TILES
+#define GSR_B1_SPLIT_TILES 4096
+#endif
+#ifndef GSR_B1_BAND_SPLIT
+#define GSR_B1_BAND_SPLIT 1
+#endif
+int b1_split(int W, int H, int ty0, int ty1, int vgy) {
+    (void)H;
+    const long long gx = div_up(W, kTile);
+    const long long sel = vgy > 0 ? (long long)vgy * gx : (long long)(ty1 - ty0) * gx;  // one image's tiles
+    return sel < GSR_B1_SPLIT_TILES ? GSR_B1_BAND_SPLIT : 1;
+}
+
 int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int ty1,
                           const uint2* ranges, const uint32_t* sorted_gid, const uint4* rect,
                           const float4* rec, const float* final_T,
                           const float* accum, const float* dL_dpix, float* partial, long long cap,
                           const uint32_t* term, const float4* ck, hipStream_t s, int vgy, int vh,
-                          const uint8_t* mk) {
+                          const uint8_t* mk, int split) {
     const BlendGeom geo = make_geo(cam, bg, ty0, ty1, cap, vgy, vh);
     if (geo.nwg <= 0) return 0;
-    const PartLayout pl(cap);
+    if (split != 1 && split != 2 && split != 4) return (int)hipErrorInvalidValue;
+    const PartLayout pl(cap * split);  // one entry per (instance, part)
     char* base = reinterpret_cast<char*>(partial);
-    const int blocks = 8 * (geo.nwg / 8 + 1) * kMaxChunks;
-    hipLaunchKernelGGL(blend_backward_kernel, dim3(blocks), dim3(64), 0, s, geo, ranges, sorted_gid, rect, rec,
-                       final_T, accum, dL_dpix, reinterpret_cast<float*>(base + pl.p8),
-                       reinterpret_cast<float*>(base + pl.p1), reinterpret_cast<uint8_t*>(base + pl.fl), term, ck,
-                       mk);
+    const int blocks = 8 * (geo.nwg / 8 + 1) * kMaxChunks * split;
+    auto* p8 = reinterpret_cast<float*>(base + pl.p8);
+    auto* p1 = reinterpret_cast<float*>(base + pl.p1);
+    auto* fl = reinterpret_cast<uint8_t*>(base + pl.fl);
+    if (split == 1)
+        hipLaunchKernelGGL(blend_backward_kernel<4>, dim3(blocks), dim3(64), 0, s, geo, ranges, sorted_gid, rect, rec,
+                           final_T, accum, dL_dpix, p8, p1, fl, term, ck, mk);
+    else if (split == 2)
+        hipLaunchKernelGGL(blend_backward_kernel<2>, dim3(blocks), dim3(64), 0, s, geo, ranges, sorted_gid, rect, rec,
+                           final_T, accum, dL_dpix, p8, p1, fl, term, ck, mk);
+    else
+        hipLaunchKernelGGL(blend_backward_kernel<1>, dim3(blocks), dim3(64), 0, s, geo, ranges, sorted_gid, rect, rec,
+                           final_T, accum, dL_dpix, p8, p1, fl, term, ck, mk);
     return (int)hipGetLastError();
 }
 

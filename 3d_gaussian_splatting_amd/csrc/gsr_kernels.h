@@ -133,7 +133,11 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
                           const float4* rec, const float* final_T,
                           const float* accum, const float* dL_dpix, float* partial, long long cap,
                           const uint32_t* term, const float4* ck, hipStream_t s, int vgy = 0, int vh = 0,
-                          const uint8_t* mk = nullptr);
+                          const uint8_t* mk = nullptr, int split = 1);
+// B1 parts per (tile, chunk) for a launch over tile rows [ty0, ty1) (views mode: vgy rows per
+// view): 1 on full images, GSR_B1_BAND_SPLIT on band launches; the partial block then holds
+// cap * split entries (entry j * split + part) and the gather sums them (launch_gather_grad2d)
+int b1_split(int W, int H, int ty0, int ty1, int vgy);
 // (vgy, vh: views mode -- bands of vgy tile rows per view, vh valid pixel rows each; 0 = one image)
 
 // record layout constants shared by preprocess and the blend kernels
@@ -143,7 +147,7 @@ constexpr float kLn2 = 0.6931471805599453f;  // conic A = -2 ln2 a', B = -ln2 b'
 // culled Gaussians).  offsets: the inclusive tile scan in gid order; partial: PartLayout(cap).
 // rrect: the rank-order payload in presort mode (offsets then in rank order), else nullptr
 int launch_gather_grad2d(const uint32_t* offsets, const float* partial, const float4* rec, int W, int H,
-                         long long cap, int P, const uint4* rrect, float* grad2d, hipStream_t s);
+                         long long cap, int P, const uint4* rrect, float* grad2d, hipStream_t s, int split = 1);
 
 struct GradOut {
     float *means2D, *conic, *opac, *colors, *means3D, *sh_dc, *sh_rest, *scales, *rots, *cov3D;
@@ -177,6 +181,14 @@ int launch_pack_splats(const uint32_t* tiles, const uint4* rect, const uint32_t*
 int launch_unpack_splats(const char* recv, int nsrc, int pair_cap, int ty0, int ty1, float4* rec, uint32_t* depth_key,
                          uint32_t* tiles, uint4* rect, hipStream_t s, uint32_t* rb_hist = nullptr,
                          uint32_t* bsum = nullptr);
+
+// The step's glue around the exchanges (gsr.h gsr_band_publish / gsr_gather_finish)
+int launch_band_publish(const float* color, int W, int H, int py0, int py1, int tall, float* mine,
+                        long long status_off, const char* send, size_t block_bytes, int nbands, const uint32_t* K_dev,
+                        hipStream_t s);
+int launch_gather_finish(const float* gathered, long long row_floats, long long status_off, int world,
+                         const BandRows& br, int W, int H, int tall, float* image, uint32_t pair_cap,
+                         uint32_t capacity, int32_t* guard, float* zero, int nzero, hipStream_t s);
 
 // the bands [b_lo, b_hi] a rect's tile rows [miny, maxy) overlap (b_lo > b_hi: none)
 __device__ __forceinline__ void band_span(const BandRows& br, uint32_t miny, uint32_t maxy, int& b_lo, int& b_hi) {

@@ -47,14 +47,15 @@ __global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __re
                                                             const uint8_t* __restrict__ fl,
                                                             const float4* __restrict__ rec, float hw, float hh,
                                                             int P, uint32_t cap, const uint4* __restrict__ rrect,
-                                                            float* __restrict__ grad2d) {
+                                                            float* __restrict__ grad2d, uint32_t split) {
     __shared__ float4 w8[2 * kGatherWin];
     __shared__ float w1[kGatherWin];
     __shared__ uint32_t wv[kGatherWin / 4];
     const int g0 = blockIdx.x * 256, g = g0 + threadIdx.x;
     const int gl = (P - g0 < 256 ? P - g0 : 256) + g0;  // one past the block's last Gaussian
-    // emission indices past the binning's capacity were never emitted (overflow): clamped
-    auto off = [&](int i) { const uint32_t o = offsets[i]; return o < cap ? o : cap; };
+    // emission indices past the binning's capacity were never emitted (overflow): clamped; a
+    // split B1 (band launches) wrote `split` consecutive entries per instance, summed in order
+    auto off = [&](int i) { const uint32_t o = offsets[i]; return (o < cap ? o : cap) * split; };
     const uint32_t J0 = g0 ? off(g0 - 1) : 0u, J1 = off(gl - 1);
     const uint32_t s = g < P ? (g ? off(g - 1) : 0u) : 0u;
     const uint32_t e = g < P ? off(g) : 0u;
@@ -539,14 +540,14 @@ __global__ __launch_bounds__(256) void preprocess_backward_kernel(
 }  // namespace
 
 int launch_gather_grad2d(const uint32_t* offsets, const float* partial, const float4* rec, int W, int H,
-                         long long cap, int P, const uint4* rrect, float* grad2d, hipStream_t s) {
+                         long long cap, int P, const uint4* rrect, float* grad2d, hipStream_t s, int split) {
     if (P <= 0) return 0;
-    const PartLayout pl(cap);
+    const PartLayout pl(cap * split);
     const char* base = reinterpret_cast<const char*>(partial);
     hipLaunchKernelGGL(gather_grad2d_kernel, dim3(div_up(P, 256)), dim3(256), 0, s, offsets,
                        reinterpret_cast<const float4*>(base + pl.p8), reinterpret_cast<const float*>(base + pl.p1),
                        reinterpret_cast<const uint8_t*>(base + pl.fl), rec, 0.5f * (float)W, 0.5f * (float)H, P,
-                       (uint32_t)cap, rrect, grad2d);
+                       (uint32_t)cap, rrect, grad2d, (uint32_t)split);
     return (int)hipGetLastError();
 }
 

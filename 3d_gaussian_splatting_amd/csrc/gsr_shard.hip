@@ -296,7 +296,86 @@ __global__ __launch_bounds__(256) void unpack_kernel(const char* __restrict__ re
     }
 }
 
+// ---- the multi-GPU step's glue around the exchanges (gsr.h gsr_band_publish / gsr_gather_finish):
+// one launch each instead of ~20 small copies, reductions and clears per step ----
+
+// This rank's all-gather row: its band's pixel rows [py0, py1) of the 3 x H x W image into the
+// row's 3 x tall x W head, then the status words (send-header counts, band K) at status_off.
+__global__ __launch_bounds__(256) void band_publish_kernel(const float* __restrict__ color, int W, int H, int py0,
+                                                          int py1, int tall, float* __restrict__ mine,
+                                                          long long status_off, const char* __restrict__ send,
+                                                          size_t block_bytes, int nbands,
+                                                          const uint32_t* __restrict__ K_dev) {
+    const long long per = (long long)(py1 - py0) * W, total = 3 * per;
+    const long long stride = (long long)gridDim.x * 256;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += stride) {
+        const long long c = i / per, r = i - c * per;
+        mine[c * (long long)tall * W + r] = color[c * (long long)H * W + (long long)py0 * W + r];
+    }
+    if (blockIdx.x == 0 && threadIdx.x <= nbands) {
+        uint32_t* st = reinterpret_cast<uint32_t*>(mine + status_off);
+        st[threadIdx.x] = threadIdx.x < nbands
+                              ? *reinterpret_cast<const uint32_t*>(send + (size_t)threadIdx.x * block_bytes)
+                              : *K_dev;
+    }
+}
+
+// From the gathered rows (world x row_floats): every rank's band into the image, the agreed
+// overflow word (ranks whose header counts exceed pair_cap or whose K exceeds the capacity, read
+// from every rank's status words: the same value on every rank) and the next step's row
+// statistics cleared (the statistics words of this rank's own row).
+__global__ __launch_bounds__(256) void gather_finish_kernel(const float* __restrict__ gathered, long long row_floats,
+                                                           long long status_off, int world, BandRows br, int W, int H,
+                                                           int tall, float* __restrict__ image, uint32_t pair_cap,
+                                                           uint32_t capacity, int32_t* __restrict__ guard,
+                                                           float* __restrict__ zero, int nzero) {
+    const int r = blockIdx.y;
+    const int a = br.row[r] * kTile < H ? br.row[r] * kTile : H;
+    const int b = br.row[r + 1] * kTile < H ? br.row[r + 1] * kTile : H;
+    const long long per = (long long)(b - a) * W, total = 3 * per;
+    const float* src = gathered + (long long)r * row_floats;
+    const long long stride = (long long)gridDim.x * 256;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += stride) {
+        const long long c = i / per, q = i - c * per;
+        image[c * (long long)H * W + (long long)a * W + q] = src[c * (long long)tall * W + q];
+    }
+    if (blockIdx.x == 0 && r == 0) {
+        if (threadIdx.x < 64) {  // one lane per rank
+            bool bad = false;
+            if ((int)threadIdx.x < world) {
+                const uint32_t* st = reinterpret_cast<const uint32_t*>(gathered + (long long)threadIdx.x * row_floats +
+                                                                       status_off);
+                for (int k = 0; k < world; ++k) bad |= st[k] > pair_cap;
+                bad |= st[world] > capacity;
+            }
+            const uint64_t m = __ballot(bad);
+            if (threadIdx.x == 0) guard[0] = (int32_t)__popcll(m);
+        }
+        for (int i = threadIdx.x; i < nzero; i += 256) zero[i] = 0.0f;
+    }
+}
+
 }  // namespace
+
+int launch_band_publish(const float* color, int W, int H, int py0, int py1, int tall, float* mine,
+                        long long status_off, const char* send, size_t block_bytes, int nbands, const uint32_t* K_dev,
+                        hipStream_t s) {
+    const long long total = 3LL * (py1 > py0 ? py1 - py0 : 0) * W;
+    const long long blocks = total > 0 ? ((total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048) : 1;
+    hipLaunchKernelGGL(band_publish_kernel, dim3((unsigned)blocks), dim3(256), 0, s, color, W, H, py0,
+                       py1 > py0 ? py1 : py0, tall, mine, status_off, send, block_bytes, nbands, K_dev);
+    return (int)hipGetLastError();
+}
+
+int launch_gather_finish(const float* gathered, long long row_floats, long long status_off, int world,
+                         const BandRows& br, int W, int H, int tall, float* image, uint32_t pair_cap,
+                         uint32_t capacity, int32_t* guard, float* zero, int nzero, hipStream_t s) {
+    const long long total = 3LL * tall * W;
+    const long long blocks = total > 0 ? ((total + 255) / 256 < 512 ? (total + 255) / 256 : 512) : 1;
+    hipLaunchKernelGGL(gather_finish_kernel, dim3((unsigned)blocks, world), dim3(256), 0, s, gathered, row_floats,
+                       status_off, world, br, W, H, tall, image, pair_cap, capacity, guard, zero, nzero);
+    return (int)hipGetLastError();
+}
 
 int launch_pack_splats(const uint32_t* tiles, const uint4* rect, const uint32_t* depth_key, const float4* rec, int P,
                        const BandRows& br, uint32_t* partials, char* send, int pair_cap, uint32_t* slot_of,

@@ -11,6 +11,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <exception>
+#include <mutex>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -21,6 +24,7 @@ namespace gsr {
 namespace {
 
 int64_t round_up(int64_t x, int64_t m = 256) { return (x + m - 1) / m * m; }
+constexpr int kMaxLocalRanks = 16;
 
 using Stream = c10::hip::HIPStreamMasqueradingAsCUDA;
 // c10's device-generic guard and events (they dispatch through the registered HIP guard
@@ -69,25 +73,34 @@ class RcclExchange final : public Exchange {
 // ---- host-staged exchange through a c10d::Store (ranks sharing one GPU) ----
 class StoreExchange final : public Exchange {
    public:
+    // Every rank announces itself under this exchange's join key (exchanges are created in the
+    // same order on every rank, so the per-process counter names the same key everywhere) and
+    // waits until `world` ranks have: comm_world() is then the store's own count of the ranks
+    // that joined, not the number the caller claimed.
     StoreExchange(std::shared_ptr<c10d::Store> store, int rank, int world)
-        : store_(std::move(store)), rank_(rank), world_(world) {}
+        : store_(std::move(store)), rank_(rank), world_(world) {
+        static int instances = 0;
+        join_key_ = "gsr/join/" + std::to_string(instances++);
+        store_->add(join_key_, 1);
+        for (int spin = 0; store_->add(join_key_, 0) < world_; ++spin) {
+            if (spin > 600000) throw std::runtime_error("store exchange: ranks did not join within 120 s");
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
+        }
+    }
     int rank() const override { return rank_; }
     int world() const override { return world_; }
     bool capturable() const override { return false; }
     const char* name() const override { return "store"; }
+    int comm_world() const override { return (int)store_->add(join_key_, 0); }
     void all_to_all(const void* send, void* recv, size_t bb, hipStream_t s) override {
         const std::string tag = "gsr/a2a/" + std::to_string(seq_++) + "/";
         std::vector<uint8_t> h((size_t)world_ * bb);
         d2h(h.data(), send, h.size(), s);
         for (int p = 0; p < world_; ++p)
-            store_->set(tag + std::to_string(rank_) + ">" + std::to_string(p),
-                        std::vector<uint8_t>(h.begin() + (size_t)p * bb, h.begin() + (size_t)(p + 1) * bb));
+            put(tag + std::to_string(rank_) + ">" + std::to_string(p), h.data() + (size_t)p * bb, bb);
         for (int p = 0; p < world_; ++p) {
             const std::string key = tag + std::to_string(p) + ">" + std::to_string(rank_);
-            auto v = store_->get(key);
-            if (v.size() != bb) throw std::runtime_error("store exchange: block size mismatch");
-            std::memcpy(h.data() + (size_t)p * bb, v.data(), bb);
-            store_->deleteKey(key);
+            take(key, h.data() + (size_t)p * bb, bb, /*erase=*/true);
         }
         h2d(recv, h.data(), h.size(), s);
     }
@@ -95,14 +108,11 @@ class StoreExchange final : public Exchange {
         const std::string tag = "gsr/ag/" + std::to_string(seq_++) + "/";
         std::vector<uint8_t> h(bytes);
         d2h(h.data(), send, bytes, s);
-        store_->set(tag + std::to_string(rank_), h);
+        put(tag + std::to_string(rank_), h.data(), bytes);
         std::vector<uint8_t> all((size_t)world_ * bytes);
-        for (int p = 0; p < world_; ++p) {
-            auto v = store_->get(tag + std::to_string(p));
-            std::memcpy(all.data() + (size_t)p * bytes, v.data(), bytes);
-        }
+        for (int p = 0; p < world_; ++p) take(tag + std::to_string(p), all.data() + (size_t)p * bytes, bytes, false);
         barrier(tag);
-        release(tag);
+        release(tag, bytes);
         h2d(recv, all.data(), all.size(), s);
     }
     void all_reduce_i64(int64_t* buf, size_t n, bool max, hipStream_t s) override {
@@ -133,11 +143,38 @@ class StoreExchange final : public Exchange {
     }
     // After barrier(tag): every rank has read every payload, so the last rank to leave deletes the
     // payloads and both counters -- a long run leaves no keys behind in the store.
-    void release(const std::string& tag) {
+    void release(const std::string& tag, size_t bytes = 0) {
         if (store_->add(tag + "left", 1) < world_) return;
-        for (int p = 0; p < world_; ++p) store_->deleteKey(tag + std::to_string(p));
+        for (int p = 0; p < world_; ++p) {
+            if (bytes == 0) {
+                store_->deleteKey(tag + std::to_string(p));
+            } else {
+                for (size_t c = 0; c < chunks(bytes); ++c) store_->deleteKey(tag + std::to_string(p) + "#" + std::to_string(c));
+            }
+        }
         store_->deleteKey(tag + "done");
         store_->deleteKey(tag + "left");
+    }
+    // Values go through the store in pieces of at most kChunk bytes (the libuv TCPStore refuses
+    // payloads above 8 MiB; a 1M / 1080p splat block for 2 ranks is 17.8 MB).  The reader knows the
+    // size, hence the number of pieces.
+    static constexpr size_t kChunk = 4u << 20;
+    static size_t chunks(size_t n) { return n == 0 ? 1 : (n + kChunk - 1) / kChunk; }
+    void put(const std::string& key, const uint8_t* data, size_t n) {
+        for (size_t c = 0; c < chunks(n); ++c) {
+            const size_t a = c * kChunk, b = std::min(n, a + kChunk);
+            store_->set(key + "#" + std::to_string(c), std::vector<uint8_t>(data + a, data + b));
+        }
+    }
+    void take(const std::string& key, uint8_t* out, size_t n, bool erase) {
+        for (size_t c = 0; c < chunks(n); ++c) {
+            const std::string k = key + "#" + std::to_string(c);
+            auto v = store_->get(k);
+            const size_t a = c * kChunk, want = std::min(n, a + kChunk) - a;
+            if (v.size() != want) throw std::runtime_error("store exchange: block size mismatch");
+            std::memcpy(out + a, v.data(), want);
+            if (erase) store_->deleteKey(k);
+        }
     }
     // synchronous copies on the caller's current stream (the step runs with it set to its own)
     static void d2h(void* h, const void* d, size_t n, hipStream_t) {
@@ -151,7 +188,149 @@ class StoreExchange final : public Exchange {
     std::shared_ptr<c10d::Store> store_;
     int rank_, world_;
     int64_t seq_ = 0;
+    std::string join_key_;
 };
+
+}  // namespace
+
+// ---- in-process rank group (one-GPU rehearsal; gsr_shard.h) ----
+class LocalGroup {
+   public:
+    explicit LocalGroup(int world) : world_(world), pub_(world), fin_(world), host_(world) {}
+    int world() const { return world_; }
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu_);
+        const int64_t gen = gen_;
+        if (++count_ == world_) {
+            count_ = 0;
+            ++gen_;
+            cv_.notify_all();
+        } else {
+            cv_.wait(lk, [&] { return gen_ != gen; });
+        }
+    }
+    struct Pub {
+        const void* ptr = nullptr;
+        c10::Event* ev = nullptr;
+    };
+    std::vector<Pub> pub_;             // per rank: its send buffer and the event after it was written
+    std::vector<c10::Event*> fin_;     // per rank: the event after its copies from the peers
+    std::vector<std::vector<int64_t>> host_;  // all-reduce contributions
+
+   private:
+    int world_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    int count_ = 0;
+    int64_t gen_ = 0;
+};
+
+namespace {
+class LocalExchange final : public Exchange {
+   public:
+    LocalExchange(std::shared_ptr<LocalGroup> g, int rank) : g_(std::move(g)), rank_(rank) {
+        if (rank < 0 || rank >= g_->world()) throw std::invalid_argument("local exchange: rank out of range");
+    }
+    int rank() const override { return rank_; }
+    int world() const override { return g_->world(); }
+    bool capturable() const override { return replay_; }
+    const char* name() const override { return replay_ ? "local-replay" : "local"; }
+    // copies = false: replay without moving any bytes -- the step's receive buffers still hold
+    // the last delivery, so the results are the same and the time is the rank's compute + glue
+    void set_replay(bool on, bool copies) {
+        if (on && snap_.size() < 3) throw std::runtime_error("local exchange: replay needs one live step first");
+        replay_ = on;
+        replay_copies_ = copies;
+    }
+    void all_to_all(const void* send, void* recv, size_t bb, hipStream_t s) override {
+        const int w = g_->world();
+        deliver(s, send, recv, (size_t)w * bb, /*always=*/false, [&](int p, const char* src) {
+            copy(static_cast<char*>(recv) + (size_t)p * bb, src + (size_t)rank_ * bb, bb);
+        });
+    }
+    // (the image all-gather runs on the step's side stream, overlapping B1: replayed with its
+    // copy in both replay modes, as RCCL's would overlap -- and so that the side stream's branch
+    // of a captured graph is never empty)
+    void all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+        deliver(s, send, recv, (size_t)g_->world() * bytes, /*always=*/true, [&](int p, const char* src) {
+            copy(static_cast<char*>(recv) + (size_t)p * bytes, src, bytes);
+        });
+    }
+    void all_reduce_i64(int64_t* buf, size_t n, bool max, hipStream_t) override {
+        auto d = dev_view(buf, (int64_t)(n * sizeof(int64_t)), torch::kUInt8);
+        std::vector<int64_t> mine(n);
+        torch::from_blob(mine.data(), {(int64_t)(n * sizeof(int64_t))}, torch::kUInt8).copy_(d);
+        g_->host_[rank_] = mine;
+        g_->barrier();
+        std::vector<int64_t> acc = g_->host_[0];
+        for (int p = 1; p < g_->world(); ++p)
+            for (size_t i = 0; i < n; ++i) acc[i] = max ? std::max(acc[i], g_->host_[p][i]) : acc[i] + g_->host_[p][i];
+        g_->barrier();  // everyone has read every contribution
+        d.copy_(torch::from_blob(acc.data(), {(int64_t)(n * sizeof(int64_t))}, torch::kUInt8));
+        current_stream().unwrap().synchronize();  // acc is a host buffer of this call
+    }
+
+   private:
+    static void copy(void* dst, const void* src, size_t n) {
+        dev_view(dst, (int64_t)n, torch::kUInt8).copy_(dev_view(const_cast<void*>(src), (int64_t)n, torch::kUInt8));
+    }
+    // A step makes three calls in a fixed order (splats all-to-all, image all-gather, gradient
+    // all-to-all): call k % 3 keeps its delivery for replay.  Every copy and event is on the
+    // stream the step passed (its main stream, or the side stream of the overlapped all-gather).
+    template <class F>
+    void deliver(hipStream_t s, const void* send, void* recv, size_t total, bool always, F&& from_peer) {
+        const int k = (int)(calls_++ % 3);
+        const Stream cs = s ? c10::hip::getStreamFromExternalMasqueradingAsCUDA(s, c10::hip::current_device())
+                            : current_stream();
+        StreamGuard on(cs.unwrap());
+        if (replay_) {
+            if (replay_copies_ || always) copy(recv, snap_[k].data_ptr(), total);
+            return;
+        }
+        ready_.record(cs.unwrap());
+        g_->pub_[rank_] = {send, &ready_};
+        g_->barrier();  // every rank's send buffer is published
+        for (int p = 0; p < g_->world(); ++p) {
+            g_->pub_[p].ev->block(cs.unwrap());
+            from_peer(p, static_cast<const char*>(g_->pub_[p].ptr));
+        }
+        done_.record(cs.unwrap());
+        g_->fin_[rank_] = &done_;
+        g_->barrier();  // every rank has issued its copies (pub_ may be reused after the next barrier)
+        for (int p = 0; p < g_->world(); ++p) g_->fin_[p]->block(cs.unwrap());  // peers done reading my send
+        g_->barrier();  // fin_ read by everyone
+        if ((int)snap_.size() <= k) snap_.resize(k + 1);
+        if (!snap_[k].defined() || (size_t)snap_[k].numel() != total)
+            snap_[k] = torch::empty({(int64_t)total}, torch::TensorOptions().dtype(torch::kUInt8).device(
+                                                           torch::kCUDA, c10::hip::current_device()));
+        copy(snap_[k].data_ptr(), recv, total);
+    }
+    std::shared_ptr<LocalGroup> g_;
+    int rank_;
+    bool replay_ = false, replay_copies_ = true;
+    int64_t calls_ = 0;
+    c10::Event ready_{c10::DeviceType::CUDA}, done_{c10::DeviceType::CUDA};
+    std::vector<torch::Tensor> snap_;
+};
+
+template <class F>
+void run_threads(const std::vector<ShardStep*>& steps, F&& body) {
+    std::vector<std::thread> th;
+    std::vector<std::exception_ptr> err(steps.size());
+    const c10::Device dev(c10::DeviceType::CUDA, c10::hip::current_device());
+    for (size_t r = 0; r < steps.size(); ++r)
+        th.emplace_back([&, r] {
+            try {
+                c10::DeviceGuard g(dev);
+                body(*steps[r]);
+            } catch (...) {
+                err[r] = std::current_exception();
+            }
+        });
+    for (auto& t : th) t.join();
+    for (auto& e : err)
+        if (e) std::rethrow_exception(e);
+}
 
 // Fixed-address arena behind one gsr_alloc_fn role: the i-th request of a step gets slot i,
 // grown only when a request is larger (never during a captured step: capacities are fixed).
@@ -200,6 +379,28 @@ std::unique_ptr<Exchange> rccl_exchange(c10d::Store& store, int rank, int world)
 
 std::unique_ptr<Exchange> store_exchange(std::shared_ptr<c10d::Store> store, int rank, int world) {
     return std::make_unique<StoreExchange>(std::move(store), rank, world);
+}
+
+std::shared_ptr<LocalGroup> local_group(int world) {
+    if (world < 1 || world > kMaxLocalRanks) throw std::invalid_argument("local group: 1..16 ranks");
+    return std::make_shared<LocalGroup>(world);
+}
+std::unique_ptr<Exchange> local_exchange(std::shared_ptr<LocalGroup> group, int rank) {
+    return std::make_unique<LocalExchange>(std::move(group), rank);
+}
+void local_exchange_set_replay(Exchange& ex, bool on, bool copies) {
+    auto* l = dynamic_cast<LocalExchange*>(&ex);
+    if (!l) throw std::invalid_argument("not a local exchange");
+    l->set_replay(on, copies);
+}
+void run_ranks_plan(const std::vector<ShardStep*>& steps) {
+    run_threads(steps, [](ShardStep& s) { s.plan(); });
+}
+void run_ranks_steps(const std::vector<ShardStep*>& steps, const torch::Tensor& dpix, int n) {
+    run_threads(steps, [&](ShardStep& s) {
+        for (int i = 0; i < n; ++i) s.step(dpix);
+        s.check();
+    });
 }
 
 // ---- partition: the same arithmetic as bands.py ----
@@ -516,15 +717,15 @@ void ShardStep::run(const torch::Tensor& dpix) {
     const gsr_raster_settings rs = shard_settings(), bs = band_settings();
     std::vector<int32_t> rows32(rows_.begin(), rows_.end());
     for (Arena* a : {&p.geom, &p.bin, &p.img, &p.scratch}) a->next = 0;
-    // 1. F1 on the shard + splat packing; the shard's row statistics (instances per tile row,
-    //    rect start / end rows) go straight into this rank's status footer
-    auto stats = p.mine.narrow(0, (int64_t)(p.status_off + kStatusWords), 3 * (int64_t)grid_y_);
-    stats.zero_();
+    // 1. F1 on the shard + splat packing; with live re-planning the shard's row statistics
+    //    (instances per tile row, rect start / end rows) go straight into this rank's status
+    //    footer (zeroed by the previous step's gsr_gather_finish, or by size_buffers)
+    float* const stats = p.mine.data_ptr<float>() + p.status_off + kStatusWords;
     gsr_raster_settings rss = rs;
-    rss.flags |= GSR_FLAG_ROW_SPANS;
+    if (live_) rss.flags |= GSR_FLAG_ROW_SPANS;
     detail::check(gsr_shard_forward(&ccam_, &g, &rss, nb, rows32.data(), pair_cap_, p.send.data_ptr(),
                                     g.P ? p.radii.data_ptr<int32_t>() : nullptr, p.state.data_ptr(),
-                                    reinterpret_cast<uint32_t*>(stats.data_ptr<float>()), s),
+                                    live_ ? reinterpret_cast<uint32_t*>(stats) : nullptr, s),
                   "gsr_shard_forward");
     // 2. splats -> bands
     ex_.all_to_all(p.send.data_ptr(), p.recv.data_ptr(), p.block_bytes, s);
@@ -533,16 +734,10 @@ void ShardStep::run(const torch::Tensor& dpix) {
                                    Pool::geom_cb, Pool::bin_cb, Pool::img_cb, &p, &p.bufs, s),
                   "gsr_band_forward");
     // 4. the band's pixels + status footer (send-header counts, band K) -> all-gather on the side
-    //    stream, overlapping B1
-    const int W = cam_.width, H = cam_.height;
-    const int py0 = std::min(rows_[rank_] * GSR_TILE, H), py1 = std::min(rows_[rank_ + 1] * GSR_TILE, H);
-    auto mine_img = p.mine.narrow(0, 0, (int64_t)p.status_off).view({3, p.tall, W});
-    if (py1 > py0) mine_img.narrow(1, 0, py1 - py0).copy_(p.color.narrow(1, py0, py1 - py0));
-    auto status = p.mine.narrow(0, (int64_t)p.status_off, kStatusWords).view(torch::kInt32);
-    status.narrow(0, 0, nb).copy_(p.send.view(torch::kInt32).view({nb, (int64_t)p.block_bytes / 4}).select(1, 0));
-    void* kdev = const_cast<void*>(gsr_view(&ccam_, nb * pair_cap_, &p.bufs, GSR_VIEW_COUNTS));
-    TORCH_CHECK(kdev != nullptr, "ShardStep: no K counter");
-    status.narrow(0, nb, 1).copy_(dev_view(kdev, 1, torch::kInt32));
+    //    stream, overlapping B1 (one launch: gsr_band_publish)
+    detail::check(gsr_band_publish(&ccam_, &bs, p.tall, p.color.data_ptr<float>(), nb, p.send.data_ptr(), pair_cap_,
+                                   &p.bufs, p.mine.data_ptr<float>(), (int64_t)p.status_off, s),
+                  "gsr_band_publish");
     const bool overlap = ex_.capturable();
     if (overlap) {
         p.fork.record(p.main.unwrap());
@@ -561,23 +756,29 @@ void ShardStep::run(const torch::Tensor& dpix) {
     detail::check(gsr_shard_backward(&ccam_, &g, &rs, nb, rows32.data(), pair_cap_, p.state.data_ptr(),
                                      p.back.data_ptr(), &p.gg, s),
                   "gsr_shard_backward");
-    // 8. join the all-gather, unpack the bands into the full image
+    // 8. join the all-gather; one launch (gsr_gather_finish) unpacks the bands into the full image,
+    //    writes the agreed overflow word (the number of ranks whose splat counts or band K exceeded
+    //    the plan's capacities in THIS step, the same on every rank; the optimizer guard of a
+    //    training loop, no host wait) and clears this rank's row statistics for the next step
     if (overlap) p.join.block(p.main.unwrap());
-    // the agreed overflow word on the device, from every rank's gathered status: the number of
-    // ranks whose splat counts or band K exceeded the plan's capacities in THIS step (the same on
-    // every rank; the optimizer guard of a training loop, no host wait)
-    {
-        auto all = p.gathered.narrow(1, (int64_t)p.status_off, kStatusWords).view(torch::kInt32);
-        auto v = all.to(torch::kInt64).bitwise_and(0xFFFFFFFFLL);
-        auto bad = v.narrow(1, 0, nb).gt((int64_t)pair_cap_).any(1).logical_or(v.select(1, nb).gt((int64_t)capacity_));
-        p.guard.copy_(bad.sum().to(torch::kInt32).reshape({1}));
-    }
-    for (int r = 0; r < world_; ++r) {
-        const int a = std::min(rows_[r] * GSR_TILE, H), b = std::min(rows_[r + 1] * GSR_TILE, H);
-        if (b > a)
-            p.image.narrow(1, a, b - a).copy_(
-                p.gathered.select(0, r).narrow(0, 0, (int64_t)p.status_off).view({3, p.tall, W}).narrow(1, 0, b - a));
-    }
+    detail::check(gsr_gather_finish(&ccam_, world_, rows32.data(), p.tall, p.gathered.data_ptr<float>(),
+                                    (int64_t)p.mine_floats, (int64_t)p.status_off, pair_cap_, capacity_,
+                                    p.image.data_ptr<float>(), p.guard.data_ptr<int32_t>(), stats,
+                                    live_ ? 3 * (int64_t)grid_y_ : 0, s),
+                  "gsr_gather_finish");
+}
+
+void ShardStep::set_graph(bool on) {
+    const bool g = on && ex_.capturable();
+    if (g == graph_) return;
+    graph_ = g;
+    drop_graph();
+}
+
+void ShardStep::set_live_replan(bool on) {
+    if (on == live_) return;
+    live_ = on;
+    drop_graph();  // the captured pack collects the statistics or not
 }
 
 void ShardStep::push_status() {
@@ -589,7 +790,7 @@ void ShardStep::push_status() {
     auto st = p.gathered.narrow(1, (int64_t)p.status_off, foot_words_).contiguous().view(torch::kInt32);
     p.ring[slot].copy_(st, /*non_blocking=*/true);
     p.ring_ev[slot]->record(p.main.unwrap());
-    pending_.push_back({steps_, slot, pair_cap_, capacity_});
+    pending_.push_back({steps_, slot, pair_cap_, capacity_, live_});
 }
 
 void ShardStep::poll(bool wait_all) {
@@ -608,8 +809,10 @@ void ShardStep::poll(bool wait_all) {
                 throw ShardOverflowError(q.step, r, counts, q.pair_cap, k, q.capacity);
             }
         }
-        last_stats_.assign(st, st + (size_t)world_ * foot_words_);
-        last_stats_step_ = q.step;
+        if (q.stats) {  // a step without statistics (live re-planning off) leaves the last ones
+            last_stats_.assign(st, st + (size_t)world_ * foot_words_);
+            last_stats_step_ = q.step;
+        }
     }
 }
 
@@ -760,6 +963,29 @@ void bind_shard(py::module& m) {
             return rccl_exchange(std::vector<uint8_t>(b.begin(), b.end()), rank, world);
         },
         py::arg("unique_id"), py::arg("rank"), py::arg("world"));
+    // host-staged exchange through a torch.distributed Store (e.g. the default group's,
+    // torch.distributed.distributed_c10d._get_default_store()): ranks may share a GPU (rehearsal)
+    m.def(
+        "store_exchange",
+        [](const c10::intrusive_ptr<c10d::Store>& store, int rank, int world) {
+            std::shared_ptr<c10d::Store> s(store.get(), [keep = store](c10d::Store*) mutable { keep.reset(); });
+            py::gil_scoped_release nogil;  // the join waits for the other ranks
+            return store_exchange(std::move(s), rank, world);
+        },
+        py::arg("store"), py::arg("rank"), py::arg("world"));
+    py::class_<LocalGroup, std::shared_ptr<LocalGroup>>(m, "LocalGroup")
+        .def(py::init([](int world) { return local_group(world); }), py::arg("world"))
+        .def_property_readonly("world", &LocalGroup::world);
+    m.def("local_exchange", &local_exchange, py::arg("group"), py::arg("rank"), py::keep_alive<0, 1>());
+    m.def("local_exchange_set_replay", &local_exchange_set_replay, py::arg("exchange"), py::arg("on"),
+          py::arg("copies") = true);
+    m.def(
+        "run_ranks_plan", [](const std::vector<ShardStep*>& steps) { run_ranks_plan(steps); }, py::arg("steps"),
+        py::call_guard<py::gil_scoped_release>());
+    m.def(
+        "run_ranks_steps",
+        [](const std::vector<ShardStep*>& steps, const torch::Tensor& dpix, int n) { run_ranks_steps(steps, dpix, n); },
+        py::arg("steps"), py::arg("dL_dpix"), py::arg("n"), py::call_guard<py::gil_scoped_release>());
     py::class_<ShardStep>(m, "ShardStep")
         .def(py::init([](Exchange& ex, const RasterCamera& cam, py::dict inputs, int sh_degree,
                          std::array<float, 3> bg, double headroom, bool graph, int lag) {
@@ -800,6 +1026,7 @@ void bind_shard(py::module& m) {
         .def("set_rebalance_every", &ShardStep::set_rebalance_every, py::arg("m"))
         .def_property_readonly("replans", &ShardStep::replans)
         .def("set_live_replan", &ShardStep::set_live_replan, py::arg("on"))
+        .def("set_graph", &ShardStep::set_graph, py::arg("on"))
         .def_property_readonly("live_replans", &ShardStep::live_replans)
         .def("band_num_rendered", &ShardStep::band_num_rendered)
         .def_property_readonly("rows", &ShardStep::rows)

@@ -66,6 +66,23 @@ std::unique_ptr<Exchange> rccl_exchange(c10d::Store& store, int rank, int world)
 // Host-staged through a c10d::Store (device -> host -> store -> host -> device); not capturable.
 std::unique_ptr<Exchange> store_exchange(std::shared_ptr<c10d::Store> store, int rank, int world);
 
+// In-process rank group (one-GPU rehearsal of the N-rank step, scripts/band_sim.py --cpp): every
+// rank's ShardStep runs in its own host thread on the same device, and the collectives are
+// device-to-device copies between the ranks' own buffers, ordered by events and host barriers.
+// After a live step each exchange keeps what it delivered (recv blocks, gathered rows, gradient
+// blocks); in replay mode it copies those instead of waiting for peers, so ONE rank's whole C++
+// step (glue, graph replay and exchange-sized copies included) can be timed alone on the GPU.
+class LocalGroup;
+std::shared_ptr<LocalGroup> local_group(int world);
+std::unique_ptr<Exchange> local_exchange(std::shared_ptr<LocalGroup> group, int rank);
+// replay: copy the last live step's deliveries (copies) or move nothing (the receive buffers
+// still hold them); throws unless ex is a local exchange
+void local_exchange_set_replay(Exchange& ex, bool on, bool copies = true);
+class ShardStep;
+// steps[r].plan() / steps[r].step(dpix) x n in one host thread per rank (exceptions rethrown)
+void run_ranks_plan(const std::vector<ShardStep*>& steps);
+void run_ranks_steps(const std::vector<ShardStep*>& steps, const torch::Tensor& dpix, int n);
+
 // ---- partition (bands.py) -------------------------------------------------------------------
 std::pair<int64_t, int64_t> gaussian_shard(int64_t P, int world, int rank);
 std::vector<int> equal_bands(int grid_y, int world);
@@ -168,7 +185,12 @@ class ShardStep {
     // statistics call for (plan_from_stats, headroom) and, at that same call, adopts them if the
     // cuts moved, a capacity is short, or a capacity is over twice what is needed -- no probe
     // forward, no collective and no host wait beyond the lagged ring.  live_replans() counts them.
-    void set_live_replan(bool on) { live_ = on; }
+    // The statistics are collected only while live re-planning is on (the pack then takes its
+    // row-spans form); switching it drops a captured graph.
+    void set_live_replan(bool on);
+    // Graph capture on / off after construction (on only with a capturable exchange; a local
+    // exchange becomes capturable in replay mode).
+    void set_graph(bool on);
     int64_t live_replans() const { return live_replans_; }
 
    private:
@@ -211,6 +233,7 @@ class ShardStep {
         int64_t step;
         int slot;
         int pair_cap, capacity;  // the plan the step ran under
+        bool stats;              // the step collected row statistics (live re-planning on)
     };
     std::vector<Pending> pending_;
     int ring_next_ = 0;

@@ -44,7 +44,7 @@ EXPORTS = ["gsr_abi_version", "gsr_last_error", "gsr_forward", "gsr_read_num_ren
            "gsr_band_forward", "gsr_band_backward", "gsr_shard_backward", "gsr_exchange_block_bytes",
            "gsr_shard_state_bytes", "gsr_view", "gsr_geom_bytes", "gsr_binning_bytes",
            "gsr_image_bytes", "gsr_scratch_bytes", "gsr_ck_pool_slots", "gsr_profile_enable", "gsr_profile_read",
-           "gsr_stage_name"]
+           "gsr_stage_name", "gsr_band_publish", "gsr_gather_finish"]
 # include/gsr/gsr_train.h (training-step kernels)
 TRAIN_EXPORTS = ["gsr_activate", "gsr_loss_scratch_bytes", "gsr_loss_forward", "gsr_loss_backward", "gsr_adam_step",
                  "gsr_adam_step_guarded", "gsr_densify_stats", "gsr_densify_stats_guarded", "gsr_compact_scratch_bytes", "gsr_compact_index", "gsr_gather_rows",

@@ -154,9 +154,12 @@ def cpu_model() -> str:
 
 
 class CppShard:
-    """bench's view of the C++ multi-GPU step (ext.ShardStep over ext.rccl_exchange): the same
-    attributes bands.ShardStep offers the reporting code below.  The RCCL unique id travels over
-    the torch.distributed group that the launcher already set up."""
+    """bench's view of the C++ multi-GPU step (ext.ShardStep): the same attributes bands.ShardStep
+    offers the reporting code below.  Over RCCL (--dist-backend nccl, one GPU per rank, the step
+    captured into a hipGraph) the unique id travels over the torch.distributed group that the
+    launcher already set up; with --dist-backend gloo the exchange is the host-staged
+    ext.store_exchange over that group's c10d store -- the same C++ step, ranks may share one GPU
+    (the rehearsal of the driver's N-GPU line; not capturable, so every step runs eagerly)."""
 
     class _Band:  # num_rendered of the band (read back after the timed loop)
         def __init__(self, st):
@@ -170,11 +173,14 @@ class CppShard:
         def __init__(self, radii):
             self.radii = radii
 
-    def __init__(self, cam, inputs, D, dist, rank, world):
+    def __init__(self, cam, inputs, D, dist, rank, world, backend="nccl"):
         ext = native.load_torch_ext()
-        uid = [ext.rccl_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        self.exchange = ext.rccl_exchange(uid[0], rank, world)
+        if backend == "nccl":
+            uid = [ext.rccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            self.exchange = ext.rccl_exchange(uid[0], rank, world)
+        else:
+            self.exchange = ext.store_exchange(dist.distributed_c10d._get_default_store(), rank, world)
         self.st = ext.ShardStep(self.exchange, R.ext_camera(cam), inputs, D, graph=True)
         self.st.plan()
         self.rank = rank
@@ -182,7 +188,12 @@ class CppShard:
         self.band_instances = list(self.st.band_instances)
         self.g0, self.g1 = self.st.g0, self.st.g1
         self.band = (self.rows[rank], self.rows[rank + 1])
-        self.comm_world = int(self.st.exchange_world)  # ncclCommCount of the step's communicator
+        # ranks as the transport counts them: ncclCommCount of the step's communicator (RCCL), the
+        # ranks that joined the exchange's store key (store)
+        self.comm_world = int(self.st.exchange_world)
+        self.impl = ("C++ gsr::ShardStep over RCCL, hipGraph replay" if backend == "nccl" else
+                     "C++ gsr::ShardStep over a host-staged c10d store exchange (rehearsal: ranks may share a "
+                     "GPU; device->host->store copies instead of RCCL's xGMI transfers, eager steps, no graph)")
 
     def check(self):  # every pending step's agreed overflow check (waits)
         self.st.check()
@@ -229,7 +240,7 @@ def launch_or_refuse(args) -> int | None:
         ndev = torch.cuda.device_count()
         if ndev < args.gpus:
             print(f"bench.py: --gpus {args.gpus} over RCCL needs {args.gpus} visible GPUs, found {ndev} "
-                  f"(use --dist-backend gloo --dist-impl python to rehearse ranks sharing a GPU)", file=sys.stderr)
+                  f"(use --dist-backend gloo to rehearse ranks sharing a GPU)", file=sys.stderr)
             return 2
     import subprocess
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
@@ -283,8 +294,9 @@ def main():
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank) or gloo (rehearsal: ranks may share a GPU)")
     ap.add_argument("--dist-impl", default="cpp", choices=("cpp", "python"),
-                    help="N > 1 with --dist-backend nccl: the C++ gsr::ShardStep over RCCL with hipGraph "
-                         "replay (cpp), or bands.ShardStep over torch.distributed (python; always with gloo)")
+                    help="N > 1: the C++ gsr::ShardStep (cpp: over RCCL with hipGraph replay, or with "
+                         "--dist-backend gloo over the host-staged store exchange), or bands.ShardStep over "
+                         "torch.distributed (python)")
     ap.add_argument("--exact-k", action="store_true",
                     help="size the binning from K every step (one host read per forward) instead of a bound")
     ap.add_argument("--lib", default=None, help="load this libgsr_hip.so instead of the in-tree one "
@@ -331,10 +343,11 @@ def main():
                   rotations=t(scene.rotations), sh_dc=t(scene.sh_dc), sh_rest=t(scene.sh_rest))
     dpix = t(dpix_np)
     gx, gy = cam.grid
-    if world > 1 and args.dist_impl == "cpp" and args.dist_backend == "nccl":
+    if world > 1 and args.dist_impl == "cpp":
         # the C++ step (csrc/torch/gsr_shard.h) over RCCL, captured into a hipGraph on its first
-        # step and replayed: one graph launch per rank and step
-        plan = CppShard(cam, inputs, D, dist, rank, world)
+        # step and replayed: one graph launch per rank and step (gloo: the same step over the
+        # host-staged store exchange)
+        plan = CppShard(cam, inputs, D, dist, rank, world, backend=args.dist_backend)
         band = plan.band
 
         def step():
@@ -435,8 +448,9 @@ def main():
         "counts": {"visible": V, "num_rendered": K, "tiles": tiles},
     }
     if world > 1:
-        result["exchange"] = {"impl": ("C++ gsr::ShardStep over RCCL, hipGraph replay"
-                                       if isinstance(plan, CppShard) else "bands.ShardStep over torch.distributed"),
+        result["exchange"] = {"impl": (plan.impl if isinstance(plan, CppShard) else
+                                       f"bands.ShardStep over torch.distributed ({args.dist_backend})"),
+                              "backend": args.dist_backend,
                               "band_rows": plan.rows, "pair_cap": plan.pair_cap, "band_capacity": plan.capacity,
                               "band_instances": plan.band_instances, "counts_are": "rank 0's shard / band",
                               "comm_world": (plan.comm_world if isinstance(plan, CppShard) else dist.get_world_size()),

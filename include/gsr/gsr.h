@@ -258,6 +258,25 @@ int gsr_shard_backward(const gsr_camera* cam, const gsr_gaussians* shard, const 
                        int32_t nbands, const int32_t* band_rows, int32_t pair_cap, void* shard_state,
                        const void* grad_recv, const gsr_grads* grads, void* stream);
 
+/* The step's glue around the exchanges, one launch each (what a caller would otherwise do with
+ * ~20 small copies, reductions and clears per step):
+ *   gsr_band_publish   this rank's row of the image all-gather: the band's pixel rows of
+ *                      out_color (3 x H x W; tile rows rs->tile_y0..tile_y1) into row[0, 3*tall*W)
+ *                      laid out 3 x tall x W, then at row + status_off (u32 words) the nbands
+ *                      send-block header counts and the band's K (bufs: the band forward's)
+ *   gsr_gather_finish  from `gathered` (world rows of row_floats floats, as the all-gather left
+ *                      them): every rank's band pixels into image (3 x H x W); into *guard (device
+ *                      int32) the number of ranks whose header counts exceed pair_cap or whose K
+ *                      exceeds capacity -- the agreed overflow word, the same on every rank; and
+ *                      nzero floats at `zero` cleared (e.g. the next step's row statistics, which
+ *                      gsr_shard_forward accumulates into).  0 <= status_off, world <= 16 ranks. */
+int gsr_band_publish(const gsr_camera* cam, const gsr_raster_settings* rs, int32_t tall, const float* out_color,
+                     int32_t nbands, const void* send, int32_t pair_cap, const gsr_buffers* bufs, float* row,
+                     int64_t status_off, void* stream);
+int gsr_gather_finish(const gsr_camera* cam, int32_t world, const int32_t* band_rows, int32_t tall,
+                      const float* gathered, int64_t row_floats, int64_t status_off, int32_t pair_cap,
+                      int32_t capacity, float* image, int32_t* guard, float* zero, int64_t nzero, void* stream);
+
 /* Introspection for tests / the benchmark (all device pointers into the caller's buffers,
  * or NULL when not applicable).  `what`: see gsr_view_* below. */
 #define GSR_VIEW_SORTED_GID 1       /* uint32[K]: Gaussian id of sorted instance i       */

@@ -6,7 +6,15 @@ gsr_shard_forward (F1 + splat pack), gsr_band_forward (unpack + F2..F6), gsr_ban
 launch stream, median over --steps runs, and reports the slowest rank's total: the per-step
 compute an N-GPU run adds to its communication.  Also the bytes each rank moves per step
 (splat blocks out, gradient blocks back, its image band), for the xGMI estimate in DESIGN §7.
-usage: band_sim.py [--worlds 1,2,4,8] [--steps 5] [--config 5m_1080p]"""
+usage: band_sim.py [--worlds 1,2,4,8] [--steps 5] [--config 5m_1080p] [--cpp]
+
+--cpp: the C++ gsr::ShardStep instead (what bench.py --gpus N runs): N ranks in one process, one
+host thread each, over an in-process exchange (ext.LocalGroup: device copies between the ranks'
+buffers); after two live steps every rank's WHOLE step -- the four C-ABI calls, the glue around
+the exchanges (gsr_band_publish / gsr_gather_finish), the exchange-sized copies and the hipGraph
+replay -- is timed alone on the GPU, with the copies ("with_copies") and without the all-to-all copies
+("compute": the image all-gather's copy stays, overlapped with B1 on the side stream as RCCL's
+would be), and its image is checked against the single-GPU render."""
 import argparse
 import importlib
 import json
@@ -33,6 +41,9 @@ def main():
     ap.add_argument("--config", default="5m_1080p", choices=sorted(bench.CONFIGS))
     ap.add_argument("--no-single", action="store_true", help="skip the single-GPU reference step (kernel traces)")
     ap.add_argument("--lib", default=None, help="an experimental libgsr_hip.so (_build.build_variant)")
+    ap.add_argument("--cpp", action="store_true", help="time the C++ ShardStep per rank (see above)")
+    ap.add_argument("--cpp-graph", type=int, default=1, help="--cpp: replay each rank's step as a hipGraph (1) "
+                                                            "or eagerly (0)")
     args = ap.parse_args()
     if args.lib:
         importlib.import_module(f"{PKG}.native").HIP_LIB = os.path.abspath(args.lib)
@@ -65,6 +76,10 @@ def main():
     one_gpu = float(np.median(ref)) if ref else float("nan")
     print(json.dumps({"config": args.config, "world": 1, "path": "single-GPU gsr_forward + gsr_backward",
                       "ms_per_step": round(one_gpu, 4)}), flush=True)
+    if args.cpp:
+        for world in [int(w) for w in args.worlds.split(",")]:
+            cpp_rehearsal(args, cam, inputs, D, dpix, world, one_gpu, None if args.no_single else st.color)
+        return
     for world in [int(w) for w in args.worlds.split(",")]:
         plan = None
         runs = []
@@ -100,6 +115,52 @@ def main():
             "bytes_per_rank": {"splats_out": world * (pc + 1) * 64, "grads_back": world * pc * 48,
                                "image_band": 12 * max(band_px)},
         }), flush=True)
+
+
+def cpp_rehearsal(args, cam, inputs, D, dpix, world, one_gpu, color):
+    """Every rank's whole C++ step (gsr::ShardStep) timed alone, after live steps in threads."""
+    ext = importlib.import_module(f"{PKG}.native").load_torch_ext()
+    grp = ext.LocalGroup(world)
+    exs = [ext.local_exchange(grp, r) for r in range(world)]
+    ecam = R.ext_camera(cam)
+    steps = [ext.ShardStep(exs[r], ecam, inputs, D, graph=False) for r in range(world)]
+    ext.run_ranks_plan(steps)
+    ext.run_ranks_steps(steps, dpix, 2)  # live: every rank's collectives with the others
+    torch.cuda.synchronize()
+    out = {"config": args.config, "world": world,
+           "impl": "C++ gsr::ShardStep, in-process exchange, " + ("graph replay" if args.cpp_graph else "eager steps"),
+           "rows": list(steps[0].rows), "pair_cap": steps[0].pair_cap, "band_capacity": steps[0].capacity,
+           "band_instances": list(steps[0].band_instances)}
+    for mode in ("with_copies", "compute"):
+        rank_ms, equal, graphs = {}, [], []
+        for r in range(world):
+            ext.local_exchange_set_replay(exs[r], True, mode == "with_copies")
+            steps[r].set_graph(False)  # drop a graph captured in the other mode
+            steps[r].set_graph(args.cpp_graph == 1)
+            for _ in range(3):  # eager, capture, replay
+                img, g, radii = steps[r].step(dpix)
+            torch.cuda.synchronize()
+            times = []
+            for _ in range(args.steps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                img, g, radii = steps[r].step(dpix)
+                e1.record()
+                torch.cuda.synchronize()
+                times.append(e0.elapsed_time(e1))
+            steps[r].check()
+            rank_ms[r] = float(np.median(times))
+            graphs.append(bool(steps[r].graph_active))
+            if color is not None:
+                equal.append(bool(torch.equal(img, color)))
+        slow = max(rank_ms, key=rank_ms.get)
+        out[mode] = {"rank_ms": {r: round(v, 4) for r, v in rank_ms.items()}, "slowest_rank": slow,
+                     "slowest_rank_ms": round(rank_ms[slow], 4), "graph_replay": all(graphs),
+                     "compute_speedup": round(one_gpu / rank_ms[slow], 3) if one_gpu == one_gpu else None}
+        if equal:
+            out[mode]["image_equals_single_gpu"] = all(equal)
+    out["single_gpu_ms"] = round(one_gpu, 4)
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

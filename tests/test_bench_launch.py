@@ -65,3 +65,34 @@ def test_rccl_needs_n_devices():
 
 def test_bad_gpu_count_refused():
     assert _run(["--gpus", "0", "--launch-check"]).returncode == 2
+
+
+def test_store_exchange_counts_the_ranks_that_joined(tmp_path):
+    """bench.py --dist-backend gloo --dist-impl cpp runs the C++ gsr::ShardStep over
+    ext.store_exchange on the launcher's c10d store; its comm_world, which the
+    bench line reports next to n_gpus, is the store's own count of the ranks that joined the
+    exchange -- checked here with two real ranks (gloo, no device: the join needs none)."""
+    script = tmp_path / "se.py"
+    script.write_text(
+        "import importlib, json, sys\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "import torch.distributed as dist\n"
+        "native = importlib.import_module('3d_gaussian_splatting_amd.native')\n"
+        "dist.init_process_group('gloo')\n"
+        "r, w = dist.get_rank(), dist.get_world_size()\n"
+        "ext = native.load_torch_ext()\n"
+        "a = ext.store_exchange(dist.distributed_c10d._get_default_store(), r, w)\n"
+        "b = ext.store_exchange(dist.distributed_c10d._get_default_store(), r, w)\n"
+        "print(json.dumps({'rank': r, 'name': a.name, 'world': a.world, 'comm_world': a.comm_world,\n"
+        "                  'second': b.comm_world, 'capturable': a.capturable}), flush=True)\n"
+        "dist.destroy_process_group()\n")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr=127.0.0.1", "--master-port=29571", str(script)], env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rows = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert sorted(x["rank"] for x in rows) == [0, 1]
+    for x in rows:
+        assert x["name"] == "store" and x["world"] == 2 and x["comm_world"] == 2 and x["second"] == 2
+        assert x["capturable"] is False
