@@ -1080,26 +1080,32 @@ __global__ __launch_bounds__(256) void finalize_kernel(const uint32_t* __restric
 // kTieRunMax long (runs are disjoint, so no two threads touch the same entries); if any run is
 // longer, the whole slice goes through an all-ascending bitonic network on the 64-bit (depth,
 // gid) keys in place (a degenerate slice: many Gaussians at one depth).  Ends behind a barrier.
+// lo_bit > 0 (a truncated sort, radix_sort_slice): the slice was ordered by the key bits at and
+// above lo_bit only, so a run is a group of equal TRUNCATED keys, and it is insertion-sorted by the
+// whole (depth, gid) pair (lo_bit = 0: runs of equal keys, sorted by gid -- the same thing).
 constexpr int kTieRunMax = 32;
-__device__ __forceinline__ void tie_fixup(uint32_t* skey, uint32_t* sval, int n, int nt) {
+__device__ __forceinline__ void tie_fixup(uint32_t* skey, uint32_t* sval, int n, int nt, int lo_bit = 0) {
     int longrun = 0;
     for (int i = threadIdx.x; i + 1 < n; i += nt) {
-        const uint32_t k = skey[i];
-        if (skey[i + 1] != k || (i > 0 && skey[i - 1] == k)) continue;  // not a run's first entry
+        const uint32_t k = skey[i] >> lo_bit;
+        if ((skey[i + 1] >> lo_bit) != k || (i > 0 && (skey[i - 1] >> lo_bit) == k)) continue;  // not a run start
         int e = i + 2;
-        while (e < n && skey[e] == k && e - i <= kTieRunMax) ++e;
+        while (e < n && (skey[e] >> lo_bit) == k && e - i <= kTieRunMax) ++e;
         if (e - i > kTieRunMax) {
             longrun = 1;
             continue;
         }
-        for (int a = i + 1; a < e; ++a) {  // insertion sort of sval[i, e)
-            const uint32_t v = sval[a];
+        for (int a = i + 1; a < e; ++a) {  // insertion sort of (skey, sval)[i, e) by the 64-bit pair
+            const uint32_t ka = skey[a], va = sval[a];
+            const uint64_t x = ((uint64_t)ka << 32) | va;
             int b = a;
-            while (b > i && sval[b - 1] > v) {
+            while (b > i && ((((uint64_t)skey[b - 1]) << 32) | sval[b - 1]) > x) {
+                skey[b] = skey[b - 1];
                 sval[b] = sval[b - 1];
                 --b;
             }
-            sval[b] = v;
+            skey[b] = ka;
+            sval[b] = va;
         }
     }
     if (!__syncthreads_or(longrun)) return;
@@ -1126,9 +1132,20 @@ __device__ __forceinline__ void tie_fixup(uint32_t* skey, uint32_t* sval, int n,
 }
 
 // out of line for the register-heavy slice kernels (its few live values cross the call)
-__device__ __attribute__((noinline)) void tile_tie_fixup(uint32_t* skey, uint32_t* sval, int n, int nt) {
-    tie_fixup(skey, sval, n, nt);
+__device__ __attribute__((noinline)) void tile_tie_fixup(uint32_t* skey, uint32_t* sval, int n, int nt, int lo_bit) {
+    tie_fixup(skey, sval, n, nt, lo_bit);
 }
+
+// Truncated passes (unordered slices only): the LSD passes cover the top slice_passes(cap) * DB
+// differing key bits and tie_fixup orders the groups of equal truncated keys by the whole
+// (depth, gid) pair -- at 5M / 1080p (~4000-entry slices, 25 differing depth bits) two 9-bit
+// passes instead of three leave ~3 % of the entries in groups of 2-3.  Longer slices keep more
+// bits (a 8192-entry slice 3 x 8, so its groups stay as short); the 16384-entry form keeps all.
+// GSR_SLICE_TRUNC 0: every differing bit everywhere.
+#ifndef GSR_SLICE_TRUNC
+#define GSR_SLICE_TRUNC 1
+#endif
+__host__ __device__ constexpr int slice_passes(int cap) { return !GSR_SLICE_TRUNC ? 0 : cap <= 4096 ? 2 : cap <= 8192 ? 3 : 0; }
 
 template <int NT, int I, int DB>
 struct SliceLds {
@@ -1196,9 +1213,14 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
     // unordered one (the row-bucketed binning leaves a tile's entries in arbitrary order) ends in
     // depth order with each run of equal depth keys in arbitrary gid order; tile_tie_fixup puts
     // those runs in gid order afterwards (ties are rare and short: an LSD pass over the gid bits
-    // per 8-9 of them would cost as much as the depth passes again).
+    // per 8-9 of them would cost as much as the depth passes again).  An unordered slice is also
+    // sorted on its top slice_passes * DB differing bits only (lo_bit): the fix-up then orders the
+    // groups of equal truncated keys by the whole pair.
+    const int hb = diff ? 31 - __clz(diff) : 0;  // the highest differing bit
+    constexpr int KB = slice_passes(NT * I) * DB;  // kept bits (0: all)
+    const int lo_bit = (unordered && KB > 0 && hb + 1 > KB) ? hb + 1 - KB : 0;
     bool ran = false;
-    for (int shift = 0; shift < 32; shift += DB) {
+    for (int shift = lo_bit; shift < 32 && shift <= hb; shift += DB) {
         if (((diff >> shift) & DMASK) == 0u) continue;  // block-uniform
         ran = true;
         for (int d = tid; d < NWV * BINS; d += NT) (&wcnt[0][0])[d] = 0u;
@@ -1282,8 +1304,8 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
             }
             __syncthreads();
         }
-        if constexpr (kFixInline) tie_fixup(skey, sval, n, NT);
-        else tile_tie_fixup(skey, sval, n, NT);
+        if constexpr (kFixInline) tie_fixup(skey, sval, n, NT, lo_bit);
+        else tile_tie_fixup(skey, sval, n, NT, lo_bit);
         for (int i = tid; i < n; i += NT) gid[rg.x + i] = sval[i];
         __syncthreads();  // skey / sval / red[] are rewritten by the next slice
         return;

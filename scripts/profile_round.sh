@@ -5,16 +5,17 @@
 #      SQ issue counters, FETCH_SIZE, WRITE_SIZE
 #   3. the FETCH_SIZE / WRITE_SIZE calibration (scripts/ubench/fetch_calib) on known byte counts
 # then summarise into gpurun_out/$TAG/ (copy what is to be committed into profiles/).
-# usage: scripts/profile_round.sh TAG
+# usage: [PROF_CONFIG=5m_1080p] scripts/profile_round.sh TAG
 set -u
 TAG=${1:-prof}
+CFG=${PROF_CONFIG:-1m_1080p}
 R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp
 export TMPDIR=/tmp
-BENCH="python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline"
-PBENCH="python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-stage-events"
+BENCH="python3 $R/bench.py --config $CFG --steps 20 --warmup 5 --no-cpu-baseline"
+PBENCH="python3 $R/bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline --no-stage-events"
 CAL=$R/scripts/ubench/fetch_calib
 step() {
   echo "=== $*"
@@ -33,6 +34,6 @@ step timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE -d $OUT/cal_write -o cal_writ
 rc=$?
 STAMP=$(cat $R/3d_gaussian_splatting_amd/lib/libgsr_hip.so.stamp)
 python3 $R/scripts/pmc_summary.py $OUT/sq1 $OUT/sq2 $OUT/fetch $OUT/write --calib $OUT/cal_fetch $OUT/cal_write \
-  --lib-stamp $STAMP --traffic $OUT/pmc_traffic.json > $OUT/pmc_summary.txt 2>&1
+  --lib-stamp $STAMP --workload $CFG --traffic $OUT/pmc_traffic.json > $OUT/pmc_summary.txt 2>&1
 find $OUT/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
 exit $rc

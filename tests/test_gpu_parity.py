@@ -376,6 +376,8 @@ def test_dense_tiles_sort_paths(rast, oracle):
 
 
 @pytest.mark.parametrize("levels,P,W,H,deep", [(1, 30000, 96, 64, True), (6, 30000, 96, 64, True),
+                                                (0, 30000, 96, 64, True), (-8, 30000, 96, 64, True),
+                                                (0, 60000, 96, 64, True),
                                                 (1, 20000, 640, 360, False), (40, 20000, 640, 360, False)])
 def test_depth_ties_in_deep_tiles(levels, P, W, H, deep, rast, oracle):
     """Tiles whose Gaussians share a few depth values.  The row-bucketed binning hands the per-tile
@@ -384,14 +386,26 @@ def test_depth_ties_in_deep_tiles(levels, P, W, H, deep, rast, oracle):
     (<= 1024: the register form on 32-bit keys) tie on their truncated keys and must do the same
     (in place for short runs, by the 64-bit form for long ones), so that every list is the
     canonical (depth, gid) one.  The synthetic camera has R = I, T = 0, so the view-space depth is
-    the world z exactly; levels = 1 puts every Gaussian at one depth."""
+    the world z exactly; levels = 1 puts every Gaussian at one depth.  levels = 0 keeps the
+    scene's continuous depths: the LDS forms sort deep slices on their top differing bits only
+    (two 9-bit passes at <= 4096 entries, three 8-bit ones at <= 8192) and order the groups of
+    equal truncated keys by the whole (depth, gid) pair -- P = 60000 puts most slices past 4096.
+    levels = -8: eight depth values, each Gaussian's a few ulps off its level, so the truncated
+    keys tie in groups of thousands that differ only below the kept bits (the long-group path)."""
     gr, sc = pkg("graphics"), pkg("scene")
     cam = gr.synthetic_camera(W, H)
     s = sc.make_scene(cam, P, max_sh_degree=1, seed=21)
     z = s.means3D[:, 2]
     lo, hi = float(z.min()), float(z.max())
-    q = np.linspace(lo, hi, levels + 2)[1:-1].astype(np.float32)
-    s.means3D[:, 2] = q[np.random.default_rng(22).integers(0, levels, z.shape[0])]
+    rng_ = np.random.default_rng(22)
+    if levels > 0:
+        q = np.linspace(lo, hi, levels + 2)[1:-1].astype(np.float32)
+        s.means3D[:, 2] = q[rng_.integers(0, levels, z.shape[0])]
+    elif levels < 0:
+        q = np.linspace(lo, hi, -levels + 2)[1:-1].astype(np.float32)
+        zq = q[rng_.integers(0, -levels, z.shape[0])]
+        ulps = rng_.integers(0, 64, z.shape[0]).astype(np.int32)
+        s.means3D[:, 2] = (zq.view(np.int32) + ulps).view(np.float32)
     args = (cam, s.means3D, s.opacities, s.scales, s.rotations, s.sh_dc, s.sh_rest)
     st = rast.forward(*args, sh_degree=1)
     f = oracle.forward(*args, sh_degree=1)
