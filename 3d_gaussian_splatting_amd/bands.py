@@ -351,12 +351,15 @@ class ShardStep:
         return self.rows[self.rank], self.rows[self.rank + 1]
 
     def forward(self):
-        # this shard's row statistics ride in the status footer (live re-planning)
+        # with live re-planning this shard's row statistics ride in the status footer (zeros
+        # otherwise: the pack then skips its row-spans form)
         if getattr(self, "_stats", None) is None:
             self._stats = torch.zeros(3 * self.gy, dtype=torch.int32, device=self.shard["means3D"].device)
-        self._stats.zero_()
+        if self.live:
+            self._stats.zero_()
         sh = self.rast.shard_forward(self.cam, self.rows, self.pair_cap, **self.shard, sh_degree=self.D,
-                                     row_hist=self._stats, row_spans=True, reuse=self._reuse["shard"])
+                                     row_hist=self._stats if self.live else None, row_spans=self.live,
+                                     reuse=self._reuse["shard"])
         recv = all_to_all_blocks(sh.send, self.world, self.dist, self.group)
         st = self.rast.band_forward(self.cam, self.band, self.world, self.pair_cap, recv, self.capacity,
                                     reuse=self._reuse["band"])

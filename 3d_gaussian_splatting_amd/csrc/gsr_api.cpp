@@ -228,7 +228,8 @@ struct Views {
 uint32_t expected_layout(long long n, int gx, int gy, long long cap, int ntiles) {
     uint32_t w = GSR_LAYOUT_TAG;
     if (use_presort(n, gx, gy)) w |= kBufPresort;
-    if (use_rb_binning(n, gx, gy) && cap > 0 && (GSR_RB_DEEP || tile_wave_sort_eligible(cap, ntiles)))
+    if (use_rb_binning(n, gx, gy) && cap > 0 && cap < kRbMaxCap &&
+        (GSR_RB_DEEP || tile_wave_sort_eligible(cap, ntiles)))
         w |= kBufRowBucketed;
     return w;
 }
@@ -417,7 +418,7 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
                                                          v.rb_histA, v.rb_histB, v.rb_status, v.kB, v.vB,
                                                          GSR_RB_TILE_KEYS ? v.kA : nullptr, v.vA,
                                                          v.ranges, cap, stream, j.rows_counted,
-                                                         j.rows_counted ? v.lookback + 16 : nullptr),
+                                                         j.rows_counted ? v.lookback + 16 : nullptr, v.K_dev),
                   "row-bucketed binning");
         GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_tile_depth_sort(v.ranges, j.ty0 * j.gx, ntiles, cap, v.depth_key,
                                                                v.sorted_gid, v.ovf, v.counters + kOvfCountSlot, v.ovf2,
@@ -660,6 +661,9 @@ int gsr_read_num_rendered(const gsr_camera* cam, const gsr_buffers* bufs, int32_
         if (int e = end_read(v.K_dev, &K, 1, stream)) return fail(-10, "read K: %s", hipGetErrorString((hipError_t)e));
     }
     if (num_rendered) *num_rendered = (int32_t)(K > (uint32_t)INT32_MAX ? INT32_MAX : K);
+    if (K == 0xFFFFFFFFu && bufs->capacity < INT32_MAX)
+        return fail(GSR_ERR_OVERFLOW, "binning void: the row-bucketed binning's look-back did not complete "
+                                      "(K marked UINT32_MAX); re-run the forward");
     if ((long long)K > (long long)bufs->capacity)
         return fail(GSR_ERR_OVERFLOW, "binning overflow: K = %u instances, capacity %d", K, bufs->capacity);
     return 0;

@@ -95,6 +95,7 @@ constexpr int kMaxViews = 8;  // gsr_forward_views: views per call (= GSR_MAX_VI
 #define GSR_RB_DEEP 1
 #endif
 constexpr int kRbMaxRows = 256, kRbMaxCols = 256, kRbChunkPairs = 1024;
+constexpr long long kRbMaxCap = 1LL << 30;  // the look-back's 30-bit counts (rb_tiles_scan)
 // gsr_buffers.layout (set by the forward, checked by every later use of the buffers): the tag
 // and the binning in use (gsr.h GSR_LAYOUT_*)
 constexpr uint32_t kBufRowBucketed = GSR_LAYOUT_ROW_BUCKETED;

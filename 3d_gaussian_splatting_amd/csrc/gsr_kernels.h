@@ -76,8 +76,9 @@ int launch_rb_binning(const uint32_t* tiles, uint4* rect, uint32_t* offsets, int
                       uint32_t* histA, uint32_t* histB, uint32_t* rb_status, uint32_t* pgid, uint32_t* pxr,
                       uint32_t* tkey, uint32_t* tgid, uint2* ranges, long long cap, hipStream_t s,
                       bool rows_counted = false,     // rows_counted: F1 wrote histA (PreOut.rb_hist)
-                      const uint32_t* bsum = nullptr);  // with it: F1's scanned block sums -- the
+                      const uint32_t* bsum = nullptr,  // with it: F1's scanned block sums -- the
                                                          // placement writes `offsets` itself
+                      uint32_t* K_dev = nullptr);      // set to UINT32_MAX if the look-back times out
 
 // Per-tile depth order: every tile's slice of `gid` (tile-sorted, gid order within a tile) is
 // sorted in place by (depth_key[gid], gid) -- the canonical (tile, depth, gid) order -- with a

@@ -629,8 +629,9 @@ __global__ __launch_bounds__(256) void rank_payload_kernel(const uint32_t* __res
 // sort that follows orders them by the whole (depth, gid) key (the register form; the LDS forms
 // add gid passes, `unordered`), so the canonical list is the radix path's bit for bit.  Used when
 // the image has at most kRbMaxRows tile rows and kRbMaxCols tile columns (row / column ids fit one
-// byte; views mode's stacked images take the radix path), outside presort mode, and when the
-// register form takes the mean slice (gsr_api.cpp fwd_phase2; recorded in gsr_buffers.reserved).
+// byte; tall grids of at most kRbMaxRows tile rows -- views mode's stacked images included -- take
+// it too), outside presort mode, below kRbMaxCap instances (gsr_api.cpp expected_layout; recorded
+// in gsr_buffers.layout).
 constexpr int kRbChunk = kRbChunkPairs;  // pairs per pass-B block (4 per thread)
 static_assert(kRbChunk % 256 == 0 && kRbMaxRows == 256 && kRbMaxCols == 256, "one row / column per thread");
 constexpr int kRbStageA = 2048;  // LDS staging (pairs) of a pass-A block (~720 at 1M / 1080p)
@@ -825,12 +826,18 @@ __global__ __launch_bounds__(256) void rb_chunks_count(const uint32_t* __restric
 // global base by a decoupled look-back over the rows before it, and stores global positions in
 // place; then the tile ranges of row r ((0, 0) for an empty tile, as F5 leaves it; clamped to cap).
 constexpr int kRbScanThreads = 1024;
+// The look-back's status words pack a 30-bit count: the layout word keeps this binning to
+// capacities below 2^30 (gsr_api.cpp expected_layout), so a step within its capacity never
+// counts past it.  A look-back that spins past its bound (never expected) publishes what it has
+// and marks the step: K_dev = UINT32_MAX, which every reader of K takes for an overflow
+// (gsr_read_num_rendered names the cause), so the ranges it leaves are never trusted silently.
 __global__ __launch_bounds__(kRbScanThreads) void rb_tiles_scan(const uint32_t* __restrict__ totA, int R, int gx,
                                                                 int ty0, long long pcap, long long cap,
                                                                 uint32_t* __restrict__ histB,
                                                                 uint32_t* __restrict__ status,
                                                                 uint32_t* __restrict__ ticket,
-                                                                uint2* __restrict__ ranges) {
+                                                                uint2* __restrict__ ranges,
+                                                                uint32_t* __restrict__ K_dev) {
     __shared__ uint32_t wsum[kRbScanThreads / 64];
     __shared__ uint32_t tstart[kRbMaxCols];
     __shared__ uint32_t s_row[2];
@@ -914,6 +921,7 @@ __global__ __launch_bounds__(kRbScanThreads) void rb_tiles_scan(const uint32_t* 
                 pos -= 64;
             }
             if (lane == 0) __hip_atomic_store(status + r, kRbInc | (excl + carry), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (spins > (1u << 24) && lane == 0 && K_dev) *K_dev = 0xFFFFFFFFu;  // the step is void
         }
         if (lane == 0) s_base = excl;
     }
@@ -1938,10 +1946,10 @@ int launch_block_offsets(const uint32_t* tiles, int n, const uint32_t* bsum, uin
 int launch_rb_binning(const uint32_t* tiles, uint4* rect, uint32_t* offsets, int n, int gx, int ty0, int ty1,
                       uint32_t* histA, uint32_t* histB, uint32_t* rb_status, uint32_t* pgid, uint32_t* pxr,
                       uint32_t* tkey, uint32_t* tgid, uint2* ranges, long long cap, hipStream_t s,
-                      bool rows_counted, const uint32_t* bsum) {
+                      bool rows_counted, const uint32_t* bsum, uint32_t* K_dev) {
     const int R = ty1 - ty0;
     if (n <= 0 || R <= 0 || cap <= 0) return 0;  // ranges stay cleared
-    if (R > kRbMaxRows || gx > kRbMaxCols) return (int)hipErrorInvalidValue;
+    if (R > kRbMaxRows || gx > kRbMaxCols || cap >= kRbMaxCap) return (int)hipErrorInvalidValue;
     const int nbA = div_up(n, 256);
     uint32_t* const totA = histA + (size_t)256 * nbA;
     if (!rows_counted)
@@ -1955,7 +1963,7 @@ int launch_rb_binning(const uint32_t* tiles, uint4* rect, uint32_t* offsets, int
     const int gcount = nch_max < 2048 ? nch_max : 2048, gplace = nch_max < 1280 ? nch_max : 1280;
     hipLaunchKernelGGL(rb_chunks_count, dim3(gcount), dim3(256), 0, s, pxr, totA, R, gx, cap, histB);
     hipLaunchKernelGGL(rb_tiles_scan, dim3(R), dim3(kRbScanThreads), 0, s, totA, R, gx, ty0, cap, cap, histB,
-                       rb_status + 16, rb_status, ranges);
+                       rb_status + 16, rb_status, ranges, K_dev);
     hipLaunchKernelGGL(rb_chunks_place, dim3(gplace), dim3(256), 0, s, pgid, pxr, totA, R, gx, ty0, cap, cap, histB,
                        tkey, tgid);
     return (int)hipGetLastError();

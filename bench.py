@@ -80,13 +80,16 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 # rate is the only issue ceiling reported (a measured FMA-stream rate is not a ceiling: the
 # blend kernels exceed it with their mix of moves, selects and DPP adds).
 VALU_ISSUE_PER_S = 256 * 4 * 2.4e9 / 2
-# SURVEY §8d secondary bound for F6 + B1: exact (pixel, list-entry) pairs from the CPU oracle x
-# VALU lane-ops per pair, over 256 CU x 4 SIMD x 32 lanes x 2.4 GHz.  The lane-ops per pair are
-# MEASURED: each kernel's PMC SQ_INSTS_VALU per launch (wave64 instructions) x 64 / the oracle's
-# pairs (profiles/pmc_traffic.json, this build only) -- all of the kernel's VALU work, per-record
-# overhead and culled-stripe savings included, so the floor is the issue-bound time of the
-# instruction streams the kernels actually run.
-VALU_LANE_OPS_PER_S = 256 * 4 * 32 * 2.4e9
+# SURVEY §8d secondary bound for F6 + B1, from the ISA: the wave64 VALU
+# instructions of the kernels' per-stripe loop bodies in the shipped gfx950 code x the
+# number of times the culled loops must run them, counted exactly by the CPU oracle
+# (gsr_oracle.State.blend_work: the kernels' box + ellipse stripe masks, exact per-pixel
+# termination -- lower bounds of the kernels' own counts) -- over the spec issue peak.  Per-record
+# set-up, batch loads, reductions and loop control are left out, so floor / measured is the share
+# of the blend time the unavoidable arithmetic would take at full issue rate.
+F6_VISIT_VALU = 32        # blend_forward_kernel<2>: one wave's visit of a record, its two stripes
+B1_STRIPE_VALU = 12       # blend_backward_kernel<4>: one stripe evaluation (exp, alpha, T update)
+B1_CONTRIB_VALU = 16      # ... plus the contribution block when a lane of the stripe contributes
 
 
 ALG_STAGES = ("preprocess", "scan", "duplicate", "tile_sort", "finalize", "blend_fwd", "blend_bwd",
@@ -535,18 +538,27 @@ def main():
                                   # the whole machine.  A whole-machine figure is an estimate,
                                   # linear in threads (an upper bound for the CPU):
                                   "full_machine_linear_estimate": round(os.cpu_count() / cores / cpu_s, 4)}
-        f6, b1 = pmc_record("blend_forward_kernel", args.config), pmc_record("blend_backward_kernel", args.config)
-        if "roofline" in result and "valu_insts_per_launch" in f6 and "valu_insts_per_launch" in b1:
-            pairs = f.state.forward_pairs()
-            c_f6 = f6["valu_insts_per_launch"] * 64 / pairs
-            c_b1 = b1["valu_insts_per_launch"] * 64 / pairs
-            floor_ms = pairs * (c_f6 + c_b1) / VALU_LANE_OPS_PER_S * 1e3
+        if "roofline" in result:
+            work = f.state.blend_work()
+            floor_insts = (work["f6_wave_visits"] * F6_VISIT_VALU + work["b1_stripe_evals"] * B1_STRIPE_VALU +
+                           work["b1_contrib_evals"] * B1_CONTRIB_VALU)
+            floor_ms = floor_insts / VALU_ISSUE_PER_S * 1e3
             meas = sum(result.get("stage_ms", {}).get(k, 0.0) for k in ("blend_fwd", "blend_bwd"))
-            result["roofline"]["valu_pair_bound"] = {
-                "pairs": pairs, "lane_ops_per_pair": {"f6": round(c_f6, 3), "b1": round(c_b1, 3)},
-                "lane_ops_source": "PMC SQ_INSTS_VALU x 64 / oracle pairs (profiles/pmc_traffic.json)",
-                "peak_lane_ops_per_s": VALU_LANE_OPS_PER_S, "floor_ms_f6_b1": round(floor_ms, 4),
-                "measured_ms_f6_b1": round(meas, 4), "frac": round(floor_ms / meas, 4) if meas else None}
+            vb = {"pairs": f.state.forward_pairs(), "work": work,
+                  "body_valu": {"f6_per_wave_visit": F6_VISIT_VALU, "b1_per_stripe_eval": B1_STRIPE_VALU,
+                                "b1_contribution": B1_CONTRIB_VALU},
+                  "source": "ISA loop bodies (DESIGN §6) x oracle-counted culled evaluations (lower bounds)",
+                  "floor_insts": int(floor_insts), "peak_insts_per_s": VALU_ISSUE_PER_S,
+                  "floor_ms_f6_b1": round(floor_ms, 4), "measured_ms_f6_b1": round(meas, 4),
+                  "frac": round(floor_ms / meas, 4) if meas else None}
+            f6, b1 = pmc_record("blend_forward_kernel", args.config), pmc_record("blend_backward_kernel", args.config)
+            if "valu_insts_per_launch" in f6 and "valu_insts_per_launch" in b1:
+                # the instructions the kernels issue beyond the floor bodies (set-up, loads,
+                # reductions, loop control): this build's PMC counts
+                issued = f6["valu_insts_per_launch"] + b1["valu_insts_per_launch"]
+                vb["pmc_valu_insts_f6_b1"] = issued
+                vb["overhead_share_of_issued"] = round(1.0 - floor_insts / issued, 4)
+            result["roofline"]["valu_pair_bound"] = vb
         result["parity"] = {"psnr_db_vs_cpu": round(10 * math.log10(1.0 / mse), 2) if mse > 0 else float("inf"),
                             "rgb_rel_l2": float(np.linalg.norm(col - f.color) / np.linalg.norm(f.color)),
                             "grad_rel_l2_max": max(rel.values()),

@@ -808,6 +808,115 @@ void gsro_get_preprocess(const gsro_state* st, float* xy, float* depth, float* c
 
 uint64_t gsro_forward_pairs(const gsro_state* st) { return st->pairs; }
 
+/* ------------------------------------------------------------------ */
+/* Work statistics of the blend kernels' stripe culling (analysis and    */
+/* the benchmark's VALU floor; not part of the algorithm)               */
+/* ------------------------------------------------------------------ */
+/* The 16x4 stripes of tile (bx0, by0) that entry g's alpha >= 1/255 footprint reaches, as the
+ * kernels decide it (gsr_blend.hip stripe_mask, restated from the oracle's conic/opacity: the padded
+ * box, then the footprint ellipse against each stripe's pixel-centre rectangle). */
+static float edge_min_q(float a, float b, float c, float k, float u, float v0, float v1) {
+    float vs = fminf(fmaxf(k * u, v0), v1);
+    return fmaf(fmaf(c, vs, b * u), vs, a * u * u);
+}
+static unsigned stripe_mask_of(const gsro_state* st, int g, float bx0, float by0) {
+    const float kL2E = 1.4426950408889634f;
+    const float* co = st->conic_o + 4 * g;
+    const float A0 = co[0], B0 = co[1], C0 = co[2], o = co[3];
+    float det = A0 * C0 - B0 * B0;
+    if (det == 0.0f) det = 1.0f;
+    const float cov_a = C0 / det, cov_c = A0 / det;
+    const float tthr = 2.0f * logf(255.0f * o);
+    const float ex = tthr > 0.0f ? sqrtf(tthr * cov_a) * 1.02f + 0.5f : -1.0f;
+    const float ey = tthr > 0.0f ? sqrtf(tthr * cov_c) * 1.02f + 0.5f : -1.0f;
+    const float x = st->xy[2 * g], y = st->xy[2 * g + 1];
+    if (!(ex >= 0.0f) || x + ex < bx0 || x - ex > bx0 + 15.0f) return 0u;
+    const float A = 0.5f * kL2E * A0, B = kL2E * B0, C = 0.5f * kL2E * C0; /* the PD form */
+    const int pd = A > 0.0f && C > 0.0f && 4.0f * A * C - B * B > 0.0f;
+    const float bound = fmaf(fmaxf(log2f(o) + 7.99435343f, 0.0f), 1.02f, 0.05f);
+    const float x0 = bx0 - x, x1 = bx0 + 15.0f - x;
+    const float kc = -B / (2.0f * C), ka = -B / (2.0f * A);
+    unsigned m = 0;
+    for (int p = 0; p < 4; ++p) {
+        const float s0 = by0 + 4.0f * p;
+        int hit = y + ey >= s0 && y - ey <= s0 + 3.0f;
+        if (hit && pd) {
+            const float y0 = s0 - y, y1 = s0 + 3.0f - y;
+            const int inside = x0 <= 0.0f && x1 >= 0.0f && y0 <= 0.0f && y1 >= 0.0f;
+            const float q = fminf(fminf(edge_min_q(A, B, C, kc, x0, y0, y1), edge_min_q(A, B, C, kc, x1, y0, y1)),
+                                  fminf(edge_min_q(C, B, A, ka, y0, x0, x1), edge_min_q(C, B, A, ka, y1, x0, x1)));
+            hit = inside || q <= bound;
+        }
+        m |= hit ? (1u << p) : 0u;
+    }
+    return m;
+}
+
+/* out[0]: F6 (two-wave form) wave visits -- (entry, wave) pairs where the entry's stripe mask meets
+ *         a live stripe of the wave's two (stripes 2w, 2w + 1);
+ * out[1]: B1 stripe evaluations -- popcount(mask & live) summed over entries;
+ * out[2]: those of out[1] with a contributing pixel (alpha >= 1/255, not past termination);
+ * out[3]: B1 visited entries (mask & live != 0).
+ * A stripe is live at entry e while some pixel of it has not terminated before e (terminated at
+ * e: still live there).  Exact liveness -- the kernels refresh theirs every 8 entries -- so the
+ * counts are lower bounds of the kernels' own. */
+void gsro_blend_work(const gsro_state* st, uint64_t out[4]) {
+    uint64_t f6 = 0, evals = 0, contrib = 0, recs = 0;
+    const int W = st->cam.width, H = st->cam.height;
+    const int t0 = st->tile_y0 * st->grid_x, t1 = st->tile_y1 * st->grid_x;
+#pragma omp parallel for schedule(dynamic, 4) reduction(+ : f6, evals, contrib, recs)
+    for (int t = t0; t < t1; ++t) {
+        const uint32_t beg = st->ranges[2 * t], end = st->ranges[2 * t + 1], n = end - beg;
+        if (n == 0) continue;
+        const int tx = t % st->grid_x, ty = t / st->grid_x;
+        uint8_t* cb = (uint8_t*)calloc(n, 1); /* stripes with a contributing pixel, per entry */
+        uint32_t last[4] = {0, 0, 0, 0};      /* per stripe: live through entry last[p] - 1 */
+        for (int ly = 0; ly < TILE; ++ly)
+            for (int lx = 0; lx < TILE; ++lx) {
+                const int pxi = tx * TILE + lx, pyi = ty * TILE + ly, p = ly >> 2;
+                if (pxi >= W || pyi >= H) continue;
+                const float pfx = (float)pxi, pfy = (float)pyi;
+                float T = 1.0f;
+                uint32_t e = 0;
+                for (; e < n; ++e) {
+                    const uint32_t g = st->s_gid[beg + e];
+                    const float* co = st->conic_o + 4 * g;
+                    const float dx = st->xy[2 * g] - pfx, dy = st->xy[2 * g + 1] - pfy;
+                    const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                    if (power > 0.0f) continue;
+                    const float alpha = fminf(0.99f, co[3] * expf(power));
+                    if (alpha < 1.0f / 255.0f) continue;
+                    const float test_T = T * (1.0f - alpha);
+                    if (test_T < 0.0001f) break;
+                    cb[e] |= (uint8_t)(1u << p);
+                    T = test_T;
+                }
+                const uint32_t live_to = e < n ? e + 1 : n; /* the terminating entry is still visited */
+                if (live_to > last[p]) last[p] = live_to;
+            }
+        const float bx0 = (float)(tx * TILE), by0 = (float)(ty * TILE);
+        for (uint32_t e = 0; e < n; ++e) {
+            unsigned live = 0;
+            for (int p = 0; p < 4; ++p) live |= (e < last[p]) ? (1u << p) : 0u;
+            if (!live) break;
+            const unsigned mm = stripe_mask_of(st, (int)st->s_gid[beg + e], bx0, by0) & live;
+            if (!mm) continue;
+            recs++;
+            f6 += ((mm & 3u) != 0) + ((mm & 12u) != 0);
+            for (int p = 0; p < 4; ++p)
+                if (mm & (1u << p)) {
+                    evals++;
+                    contrib += (cb[e] >> p) & 1u;
+                }
+        }
+        free(cb);
+    }
+    out[0] = f6;
+    out[1] = evals;
+    out[2] = contrib;
+    out[3] = recs;
+}
+
 void gsro_get_examined(const gsro_state* st, uint32_t* examined) {
     memcpy(examined, st->examined, (size_t)st->cam.width * st->cam.height * 4);
 }

@@ -86,6 +86,9 @@ void gsro_get_preprocess(const gsro_state* st, float* xy, float* depth, float* c
                          float* rgb, uint32_t* tiles_touched);
 /* count of (pixel, list entry) evaluations the forward made (VALU-bound proxy) */
 uint64_t gsro_forward_pairs(const gsro_state* st);
+/* blend kernels' stripe-culling work statistics (F6 wave visits, B1 stripe evaluations, those
+ * with a contributing pixel, B1 visited entries): lower bounds, see gsr_oracle.c */
+void gsro_blend_work(const gsro_state* st, uint64_t out[4]);
 /* per pixel: list entries examined by the forward before termination */
 void gsro_get_examined(const gsro_state* st, uint32_t* examined);
 

@@ -55,6 +55,7 @@ def lib():
         L.gsro_forward_pairs.argtypes = [vp]
         L.gsro_get_examined.argtypes = [vp, up]
         L.gsro_forward_pairs.restype = ctypes.c_uint64
+        L.gsro_blend_work.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
         L.gsro_build_rotation.argtypes = [fp, fp]
         L.gsro_covariance.argtypes = [fp, ctypes.c_float, fp, fp]
         _lib = L
@@ -148,6 +149,14 @@ class OracleState:
 
     def forward_pairs(self) -> int:
         return int(lib().gsro_forward_pairs(self.ptr))
+
+    def blend_work(self) -> dict:
+        """The blend kernels' culled work (gsro_blend_work): lower bounds of F6's wave visits and
+        B1's stripe evaluations (all / with a contributing pixel) and visited entries."""
+        w = (ctypes.c_uint64 * 4)()
+        lib().gsro_blend_work(self.ptr, w)
+        return dict(f6_wave_visits=int(w[0]), b1_stripe_evals=int(w[1]), b1_contrib_evals=int(w[2]),
+                    b1_records=int(w[3]))
 
     def backward(self, dL_dpix: np.ndarray) -> dict:
         P, Mr = self.P, self.M_rest

@@ -149,3 +149,96 @@ def test_occlusion_order(oracle):
                        rotations=np.array([[1.0, 0, 0, 0]] * 2), colors_precomp=cols)
     c = f.color[:, 15, 15]
     assert c[1] > c[0] > 0  # green (near) dominates red (far)
+
+
+def test_blend_work_counts_match_a_python_restatement(oracle):
+    """gsro_blend_work (the counts behind bench.py's ISA VALU floor) against a direct numpy
+    restatement of the same rules on a small scene: per tile, the stripes each entry's footprint
+    box / ellipse reaches, against the stripes some pixel of which is still live there, and the
+    stripes with a contributing pixel (alpha >= 1/255 before termination)."""
+    gr, sc = pkg("graphics"), pkg("scene")
+    cam = gr.synthetic_camera(96, 64)
+    s = sc.make_scene(cam, 1500, max_sh_degree=1, seed=5)
+    f = oracle.forward(cam, s.means3D, s.opacities, s.scales, s.rotations, s.sh_dc, s.sh_rest, sh_degree=1)
+    w = f.state.blend_work()
+    pre = f.state.preprocess()
+    _, _, gid = f.state.sorted()
+    rng = f.state.ranges().reshape(-1, 2)
+    xy, co = pre["xy"].astype(np.float32), pre["conic_o"].astype(np.float32)
+    L2E = np.float32(1.4426950408889634)
+    gx = cam.grid[0]
+    f6 = evals = contrib = recs = 0
+    for t, (a, b) in enumerate(rng):
+        if b <= a:
+            continue
+        tx, ty = t % gx, t // gx
+        g = gid[a:b]
+        n = b - a
+        cb = np.zeros(n, np.int64)
+        last = [0, 0, 0, 0]
+        for ly in range(16):
+            for lx in range(16):
+                px, py = tx * 16 + lx, ty * 16 + ly
+                if px >= cam.width or py >= cam.height:
+                    continue
+                T = np.float32(1.0)
+                e = 0
+                while e < n:
+                    A, B, C, o = co[g[e]]
+                    dx, dy = xy[g[e], 0] - np.float32(px), xy[g[e], 1] - np.float32(py)
+                    power = np.float32(-0.5) * (A * dx * dx + C * dy * dy) - B * dx * dy
+                    if power <= 0:
+                        alpha = min(np.float32(0.99), o * np.float32(np.exp(np.float32(power))))
+                        if alpha >= np.float32(1.0 / 255.0):
+                            tt = T * (np.float32(1.0) - alpha)
+                            if tt < np.float32(1e-4):
+                                break
+                            cb[e] |= 1 << (ly >> 2)
+                            T = tt
+                    e += 1
+                last[ly >> 2] = max(last[ly >> 2], e + 1 if e < n else n)
+        bx0, by0 = np.float32(tx * 16), np.float32(ty * 16)
+        for e in range(n):
+            live = sum(1 << p for p in range(4) if e < last[p])
+            if not live:
+                break
+            A0, B0, C0, o = co[g[e]]
+            det = A0 * C0 - B0 * B0
+            det = det if det != 0 else np.float32(1)
+            tthr = np.float32(2) * np.float32(np.log(np.float32(255) * o))
+            ex = np.sqrt(tthr * C0 / det) * np.float32(1.02) + np.float32(0.5) if tthr > 0 else -1
+            ey = np.sqrt(tthr * A0 / det) * np.float32(1.02) + np.float32(0.5) if tthr > 0 else -1
+            x, y = xy[g[e]]
+            m = 0
+            if ex >= 0 and not (x + ex < bx0 or x - ex > bx0 + 15):
+                A, B, C = np.float32(0.5) * L2E * A0, L2E * B0, np.float32(0.5) * L2E * C0
+                pd = A > 0 and C > 0 and 4 * A * C - B * B > 0
+                bound = max(np.float32(np.log2(o)) + np.float32(7.99435343), 0) * np.float32(1.02) + np.float32(0.05)
+                for p in range(4):
+                    s0 = by0 + 4 * p
+                    hit = y + ey >= s0 and y - ey <= s0 + 3
+                    if hit and pd:
+                        # minimum of the PD form over the stripe's pixel-centre rectangle (dense grid:
+                        # a superset check of the kernels' exact edge minimum)
+                        xs = np.linspace(bx0 - x, bx0 + 15 - x, 61, dtype=np.float32)
+                        ys = np.linspace(s0 - y, s0 + 3 - y, 13, dtype=np.float32)
+                        X, Y = np.meshgrid(xs, ys)
+                        q = (A * X * X + B * X * Y + C * Y * Y).min()
+                        hit = q <= bound * 1.0005 + 1e-4
+                    m |= (1 << p) if hit else 0
+            mm = m & live
+            if not mm:
+                continue
+            recs += 1
+            f6 += int((mm & 3) != 0) + int((mm & 12) != 0)
+            for p in range(4):
+                if mm >> p & 1:
+                    evals += 1
+                    contrib += int(cb[e] >> p & 1)
+    # the grid minimum (with its small pad) and numpy's float32 rounding can decide a borderline
+    # stripe differently from the C code's exact edge minimum: agreement within a hair
+    assert abs(w["b1_stripe_evals"] - evals) <= max(3, evals // 200), (w, evals)
+    assert abs(w["b1_records"] - recs) <= max(3, recs // 200), (w, recs)
+    assert abs(w["f6_wave_visits"] - f6) <= max(3, f6 // 200), (w, f6)
+    assert abs(w["b1_contrib_evals"] - contrib) <= max(3, contrib // 200), (w, contrib)
+    assert w["b1_contrib_evals"] <= w["b1_stripe_evals"] and w["f6_wave_visits"] <= 2 * w["b1_records"]
