@@ -521,8 +521,12 @@ static_assert(kB1Win == 4 || kB1Win == 16, "B1 window: 4 or 16 mask bytes per la
 // its own partial entry j * parts + part, which the gather sums with the others in part order.
 // A band of 1/8 of the tiles then still fills the chip (~3.3 chunks per tile leave ~3 one-wave
 // blocks per SIMD otherwise), at the price of per-record work repeated per part.
-template <int SPW>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SPW == 4 ? 6 : 8))) void blend_backward_kernel(const BlendGeom geo,
+// PF (band launches, GSR_B1_BAND_PREFETCH): each visited record's LDS reads are issued before the
+// previous record's work (2x unrolled, no register copies) -- with ~3 one-wave blocks per SIMD on a
+// band's 1020 tiles the LDS latency per record is exposed, where on full images other waves hide
+// it (round 4: the same prefetch at full occupancy measured 0.456 vs 0.447 ms).
+template <int SPW, bool PF = false>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PF ? 4 : (SPW == 4 ? 6 : 8)))) void blend_backward_kernel(const BlendGeom geo,
                                                             const uint2* __restrict__ ranges,
                                                             const uint32_t* __restrict__ sorted_gid,
                                                             const uint4* __restrict__ rect,
@@ -769,10 +773,37 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SPW == 4 ? 6
             }
             return false;
         };
-        while (todo) {
-            const int k = __builtin_ctzll(todo);
-            todo &= todo - 1;
-            if (record(k, srec[3 * k + 0], srec[3 * k + 1], srec[3 * k + 2])) break;
+        if constexpr (PF) {
+            if (todo) {
+                int ka = __builtin_ctzll(todo);
+                todo &= todo - 1;
+                float4 a0 = srec[3 * ka + 0], a1 = srec[3 * ka + 1], a2 = srec[3 * ka + 2];
+                float4 b0, b1, b2;
+                while (true) {
+                    const int kb = todo ? __builtin_ctzll(todo) : -1;  // wave-uniform
+                    if (kb >= 0) {
+                        todo &= todo - 1;
+                        b0 = srec[3 * kb + 0];
+                        b1 = srec[3 * kb + 1];
+                        b2 = srec[3 * kb + 2];
+                    }
+                    if (record(ka, a0, a1, a2) || kb < 0) break;
+                    ka = todo ? __builtin_ctzll(todo) : -1;
+                    if (ka >= 0) {
+                        todo &= todo - 1;
+                        a0 = srec[3 * ka + 0];
+                        a1 = srec[3 * ka + 1];
+                        a2 = srec[3 * ka + 2];
+                    }
+                    if (record(kb, b0, b1, b2) || ka < 0) break;
+                }
+            }
+        } else {
+            while (todo) {
+                const int k = __builtin_ctzll(todo);
+                todo &= todo - 1;
+                if (record(k, srec[3 * k + 0], srec[3 * k + 1], srec[3 * k + 2])) break;
+            }
         }
         if (parked) park_flush(qpark, sjl, kpack, parked, p8f, p1, fl, lane);
         __syncthreads();  // srec / qpark are rewritten by the next batch
@@ -835,6 +866,9 @@ int launch_blend_forward(const gsr_camera& cam, const float bg[3], int ty0, int 
 #ifndef GSR_B1_SPLIT_TILES
 #define GSR_B1_SPLIT_TILES 4096
 #endif
+#ifndef GSR_B1_BAND_PREFETCH
+#define GSR_B1_BAND_PREFETCH 1
+#endif
 #ifndef GSR_B1_BAND_SPLIT
 #define GSR_B1_BAND_SPLIT 1
 #endif
@@ -860,7 +894,11 @@ int launch_blend_backward(const gsr_camera& cam, const float bg[3], int ty0, int
     auto* p8 = reinterpret_cast<float*>(base + pl.p8);
     auto* p1 = reinterpret_cast<float*>(base + pl.p1);
     auto* fl = reinterpret_cast<uint8_t*>(base + pl.fl);
-    if (split == 1)
+    const long long sel = vgy > 0 ? (long long)geo.vgy * geo.grid_x : geo.nwg;  // one image's tiles
+    if (split == 1 && GSR_B1_BAND_PREFETCH && sel < kF6BandTiles)
+        hipLaunchKernelGGL((blend_backward_kernel<4, true>), dim3(blocks), dim3(64), 0, s, geo, ranges, sorted_gid,
+                           rect, rec, final_T, accum, dL_dpix, p8, p1, fl, term, ck, mk);
+    else if (split == 1)
         hipLaunchKernelGGL(blend_backward_kernel<4>, dim3(blocks), dim3(64), 0, s, geo, ranges, sorted_gid, rect, rec,
                            final_T, accum, dL_dpix, p8, p1, fl, term, ck, mk);
     else if (split == 2)

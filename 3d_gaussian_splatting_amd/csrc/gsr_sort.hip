@@ -1153,7 +1153,12 @@ __device__ __attribute__((noinline)) void tile_tie_fixup(uint32_t* skey, uint32_
 #ifndef GSR_SLICE_TRUNC
 #define GSR_SLICE_TRUNC 1
 #endif
-__host__ __device__ constexpr int slice_passes(int cap) { return !GSR_SLICE_TRUNC ? 0 : cap <= 4096 ? 2 : cap <= 8192 ? 3 : 0; }
+#ifndef GSR_SLICE_PASSES_8K
+#define GSR_SLICE_PASSES_8K 3
+#endif
+__host__ __device__ constexpr int slice_passes(int cap) {
+    return !GSR_SLICE_TRUNC ? 0 : cap <= 4096 ? 2 : cap <= 8192 ? GSR_SLICE_PASSES_8K : 0;
+}
 
 template <int NT, int I, int DB>
 struct SliceLds {
