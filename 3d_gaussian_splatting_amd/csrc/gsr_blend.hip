@@ -512,6 +512,9 @@ __device__ __forceinline__ void park_flush(const float* qpark, const uint32_t* s
 // 0.552 ms vs 0.564 at the compiler's own 85 VGPRs (5 waves); 7 and 8 waves spill.
 // Mask bytes per lane in one batch window (4: 256 entries per window; 16: 1024, for lists whose
 // entries are mostly culled, e.g. after an opacity reset -- fewer serial window loads).
+#ifndef GSR_B1_PAIRS
+#define GSR_B1_PAIRS 0
+#endif
 constexpr int kB1Win = GSR_B1_WIN;
 static_assert(kB1Win == 4 || kB1Win == 16, "B1 window: 4 or 16 mask bytes per lane");
 // SPW: the 16x4 stripes one wave owns.  4 (full images): one wave per (tile, chunk) and one
@@ -716,33 +719,67 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PF ? 4 : (SP
             // without fast-math; +0 would keep them (0 + -0 = +0)
             float s0 = -0.f, sy = -0.f, syy = -0.f, g0 = -0.f, g1 = -0.f, g2 = -0.f;
             bool any = false;
+            // one contributing (pixel, record) pair of stripe p into the record's moments
+            auto contribute = [&](const int p, const float a, const float w, const float oG, const float dy) {
+                any = true;
+                const float one_m = 1.0f - a;
+                const float cdp = fmaf(r1.z, dp0[p], fmaf(r1.w, dp1[p], r2.x * dp2[p]));
+                R[p] = fmaf(-w, cdp, R[p]);
+                const float dLda = fmaf(T[p], cdp, -R[p] * __builtin_amdgcn_rcpf(one_m));
+                g0 = fmaf(w, dp0[p], g0);
+                g1 = fmaf(w, dp1[p], g1);
+                g2 = fmaf(w, dp2[p], g2);
+                const float sv = oG * dLda;
+                s0 += sv;
+                const float svy = sv * dy;
+                sy += svy;
+                syy = fmaf(svy, dy, syy);
+            };
+#if GSR_B1_PAIRS
+            if constexpr (SPW >= 2) {
+                // Stripes in pairs (2q, 2q + 1): the two alpha / transmittance chains of a visited
+                // pair in one block, interleaved (the exp latency of one covers the other), the
+                // contributions still behind exec-mask branches.  A stripe of the pair that the
+                // record does not visit runs with L = -inf: keep is false, so alpha = 0, T stays
+                // (live T >= 1e-4, dead T < 0) and nothing is added -- bit-identical to skipping it.
 #pragma unroll
-            for (int p = 0; p < SPW; ++p) {
-                if (!(m & (1u << (sp0 + p)))) continue;  // wave-uniform
-                const float dy = r0.y - pfy[p];
-                const float e = fmaf(fmaf(r1.x, dy, bdx), dy, K);
-                float oG;
-                bool keep;
-                const float a = pair_alpha_keep(e, r2.w, oG, keep);
-                const float w = a * T[p];
-                const float tT = T[p] - w;
-                const bool ok = tT >= 0.0001f;
-                if (ok && keep) {
-                    any = true;
-                    const float one_m = 1.0f - a;
-                    const float cdp = fmaf(r1.z, dp0[p], fmaf(r1.w, dp1[p], r2.x * dp2[p]));
-                    R[p] = fmaf(-w, cdp, R[p]);
-                    const float dLda = fmaf(T[p], cdp, -R[p] * __builtin_amdgcn_rcpf(one_m));
-                    g0 = fmaf(w, dp0[p], g0);
-                    g1 = fmaf(w, dp1[p], g1);
-                    g2 = fmaf(w, dp2[p], g2);
-                    const float sv = oG * dLda;
-                    s0 += sv;
-                    const float svy = sv * dy;
-                    sy += svy;
-                    syy = fmaf(svy, dy, syy);
+                for (int q = 0; q < SPW / 2; ++q) {
+                    const int pa = 2 * q, pb = 2 * q + 1;
+                    const uint32_t pm = (m >> (sp0 + pa)) & 3u;
+                    if (!pm) continue;  // wave-uniform
+                    const float La = (pm & 1u) ? r2.w : -INFINITY, Lb = (pm & 2u) ? r2.w : -INFINITY;
+                    const float dya = r0.y - pfy[pa], dyb = r0.y - pfy[pb];
+                    const float ea = fmaf(fmaf(r1.x, dya, bdx), dya, K);
+                    const float eb = fmaf(fmaf(r1.x, dyb, bdx), dyb, K);
+                    float oGa, oGb;
+                    bool keepa, keepb;
+                    const float aa = pair_alpha_keep(ea, La, oGa, keepa);
+                    const float ab = pair_alpha_keep(eb, Lb, oGb, keepb);
+                    const float wa = aa * T[pa], wb = ab * T[pb];
+                    const float tTa = T[pa] - wa, tTb = T[pb] - wb;
+                    const bool oka = tTa >= 0.0001f, okb = tTb >= 0.0001f;
+                    if (oka && keepa) contribute(pa, aa, wa, oGa, dya);
+                    T[pa] = oka ? tTa : -fabsf(T[pa]);
+                    if (okb && keepb) contribute(pb, ab, wb, oGb, dyb);
+                    T[pb] = okb ? tTb : -fabsf(T[pb]);
                 }
-                T[p] = ok ? tT : -fabsf(T[p]);
+            } else
+#endif
+            {
+#pragma unroll
+                for (int p = 0; p < SPW; ++p) {
+                    if (!(m & (1u << (sp0 + p)))) continue;  // wave-uniform
+                    const float dy = r0.y - pfy[p];
+                    const float e = fmaf(fmaf(r1.x, dy, bdx), dy, K);
+                    float oG;
+                    bool keep;
+                    const float a = pair_alpha_keep(e, r2.w, oG, keep);
+                    const float w = a * T[p];
+                    const float tT = T[p] - w;
+                    const bool ok = tT >= 0.0001f;
+                    if (ok && keep) contribute(p, a, w, oG, dy);
+                    T[p] = ok ? tT : -fabsf(T[p]);
+                }
             }
             if (__any(any)) {
                 // the quad shares dx: reduce the six column sums (12 DPP adds, not 18 for the

@@ -492,6 +492,13 @@ def main():
                               # PMC passes are of the N = 1 launch; a band launch has no committed counts
                               "traffic": pmc.get("hbm_bytes_per_launch") if world == 1 else None, "mean_launch_ms": round(mean_ms, 4),
                               "algorithmic_bytes_per_launch": int(bytes_launch)}
+        if "write_size_kib" in pmc and world == 1:
+            # B1's partial-entry writes against the algorithmic 36 B per visible Gaussian (VERDICT r05
+            # item 5): the per-(tile, instance) partials the deterministic hand-off costs
+            wb = pmc["write_size_kib"] * 1024
+            result["roofline"]["write_bytes_per_launch"] = int(wb)
+            if dom == "blend_bwd":
+                result["roofline"]["write_over_algorithmic"] = round(wb / (V * 36), 3) if V else None
         if "valu_insts_per_launch" in pmc and world == 1:  # PMC counts are of the N = 1 launch
             # F6/B1 are bound by VALU issue, not HBM: the kernel's measured
             # instruction count over its measured duration, against the spec issue peak (1024
