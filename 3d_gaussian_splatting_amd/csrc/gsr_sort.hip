@@ -1092,11 +1092,11 @@ __global__ __launch_bounds__(256) void finalize_kernel(const uint32_t* __restric
 // above lo_bit only, so a run is a group of equal TRUNCATED keys, and it is insertion-sorted by the
 // whole (depth, gid) pair (lo_bit = 0: runs of equal keys, sorted by gid -- the same thing).
 constexpr int kTieRunMax = 32;
-// Returns true (and leaves the slice as it is) when a truncated sort (lo_bit > 0, allow_resort)
-// meets a group longer than kTieRunMax: the caller re-sorts on every bit instead of the bitonic
-// fallback (clustered depths: thousands of keys within one truncated step).
-__device__ __forceinline__ bool tie_fixup(uint32_t* skey, uint32_t* sval, int n, int nt, int lo_bit = 0,
-                                          bool allow_resort = false) {
+// (A truncated sort that meets a long group -- clustered depths, thousands of keys within one
+// truncated step -- takes the bitonic fallback on the whole pair as well.  Re-sorting such a slice
+// on every bit from the registers instead was tried in round 6 and faulted on the GPU in the
+// clustered-depth parity test; it is not used.)
+__device__ __forceinline__ void tie_fixup(uint32_t* skey, uint32_t* sval, int n, int nt, int lo_bit = 0) {
     int longrun = 0;
     for (int i = threadIdx.x; i + 1 < n; i += nt) {
         const uint32_t k = skey[i] >> lo_bit;
@@ -1120,8 +1120,7 @@ __device__ __forceinline__ bool tie_fixup(uint32_t* skey, uint32_t* sval, int n,
             sval[b] = va;
         }
     }
-    if (!__syncthreads_or(longrun)) return false;
-    if (allow_resort && lo_bit > 0) return true;
+    if (!__syncthreads_or(longrun)) return;
     int m = 1;
     while (m < n) m <<= 1;
     auto cex = [&](int i, int j) {  // i < j; j >= n is +inf padding
@@ -1142,13 +1141,11 @@ __device__ __forceinline__ bool tie_fixup(uint32_t* skey, uint32_t* sval, int n,
             __syncthreads();
         }
     }
-    return false;
 }
 
 // out of line for the register-heavy slice kernels (its few live values cross the call)
-__device__ __attribute__((noinline)) bool tile_tie_fixup(uint32_t* skey, uint32_t* sval, int n, int nt, int lo_bit,
-                                                         bool allow_resort) {
-    return tie_fixup(skey, sval, n, nt, lo_bit, allow_resort);
+__device__ __attribute__((noinline)) void tile_tie_fixup(uint32_t* skey, uint32_t* sval, int n, int nt, int lo_bit) {
+    tie_fixup(skey, sval, n, nt, lo_bit);
 }
 
 // Truncated passes (unordered slices only): the LSD passes cover the top slice_passes(cap) * DB
@@ -1239,10 +1236,8 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
     const int hb = diff ? 31 - __clz(diff) : 0;  // the highest differing bit
     constexpr int KB = slice_passes(NT * I) * DB;  // kept bits (0: all)
     const int lo_bit = (unordered && KB > 0 && hb + 1 > KB) ? hb + 1 - KB : 0;
-    int lo = lo_bit;
-  sort_again:  // (a truncated sort whose groups turned out long: once more on every bit)
     bool ran = false;
-    for (int shift = lo; shift < 32 && shift <= hb; shift += DB) {
+    for (int shift = lo_bit; shift < 32 && shift <= hb; shift += DB) {
         if (((diff >> shift) & DMASK) == 0u) continue;  // block-uniform
         ran = true;
         for (int d = tid; d < NWV * BINS; d += NT) (&wcnt[0][0])[d] = 0u;
@@ -1326,13 +1321,8 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
             }
             __syncthreads();
         }
-        bool resort;
-        if constexpr (kFixInline) resort = tie_fixup(skey, sval, n, NT, lo, lo > 0);
-        else resort = tile_tie_fixup(skey, sval, n, NT, lo, lo > 0);
-        if (resort) {  // block-uniform; the registers still hold the slice (in top-bit order)
-            lo = 0;
-            goto sort_again;
-        }
+        if constexpr (kFixInline) tie_fixup(skey, sval, n, NT, lo_bit);
+        else tile_tie_fixup(skey, sval, n, NT, lo_bit);
         for (int i = tid; i < n; i += NT) gid[rg.x + i] = sval[i];
         __syncthreads();  // skey / sval / red[] are rewritten by the next slice
         return;
