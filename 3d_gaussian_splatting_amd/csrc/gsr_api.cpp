@@ -216,6 +216,7 @@ struct Views {
     uint32_t *counters, *K_dev, *ovf, *ovf2, *done, *term;
     float *final_T, *accum;
     float4* ck;  // the checkpoint pool (binning buffer)
+    size_t ck_bytes;
     uint32_t *kA, *vA, *kB, *vB, *hist;
     uint8_t* mk;                         // F6's per-entry stripe masks (B1's visit filter)
     uint32_t *sorted_tile, *sorted_gid;  // where the tile sort's result lands
@@ -290,6 +291,7 @@ Views views(const gsr_camera* cam, long long n, const gsr_buffers* b) {
     if (b->binning) {
         const BinLayout bl(b->capacity, (long long)ImgLayout::tile_count(cam->width, cam->height));
         v.ck = at<float4>(b->binning, bl.ck);
+        v.ck_bytes = bl.ckm - bl.ck;
         v.kA = at<uint32_t>(b->binning, bl.kA);
         v.vA = at<uint32_t>(b->binning, bl.vA);
         v.kB = at<uint32_t>(b->binning, bl.kB);
@@ -413,17 +415,23 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
     }
     if (cap > 0 && v.rb) {
         // F3 + the tile sort + F5 as two counting passes; the pairs ride in (kB, vB)
-        // (the tile keys are left to the GSR_VIEW_SORTED_TILE accessor: nothing in the step reads them)
+        // (the tile keys are left to the GSR_VIEW_SORTED_TILE accessor: nothing in the step reads them;
+        // kA carries the instances' depth keys from the placement to the per-tile sort instead)
+        // and the pairs' keys ride in the checkpoint pool, which F6 fills only after the sort (when it
+        // holds cap words: every image with a few KB of list per tile)
+        const bool rb_keys = GSR_RB_SORT_KEYS && !GSR_RB_TILE_KEYS && v.ck_bytes >= 4 * (size_t)cap;
         GSR_STAGE(GSR_STAGE_TILE_SORT, launch_rb_binning(v.tiles, v.rect, v.offsets, (int)j.n, j.gx, j.ty0, j.ty1,
                                                          v.rb_histA, v.rb_histB, v.rb_status, v.kB, v.vB,
                                                          GSR_RB_TILE_KEYS ? v.kA : nullptr, v.vA,
                                                          v.ranges, cap, stream, j.rows_counted,
-                                                         j.rows_counted ? v.lookback + 16 : nullptr, v.K_dev),
+                                                         j.rows_counted ? v.lookback + 16 : nullptr, v.K_dev,
+                                                         v.depth_key, rb_keys ? reinterpret_cast<uint32_t*>(v.ck) : nullptr,
+                                                         rb_keys ? v.kA : nullptr),
                   "row-bucketed binning");
         GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_tile_depth_sort(v.ranges, j.ty0 * j.gx, ntiles, cap, v.depth_key,
                                                                v.sorted_gid, v.ovf, v.counters + kOvfCountSlot, v.ovf2,
                                                                v.counters + kOvf2CountSlot, v.done, v.free_k,
-                                                               v.free_v, stream, true),
+                                                               v.free_v, stream, true, rb_keys ? v.kA : nullptr),
                   "per-tile depth order");
     } else if (cap > 0) {
         int which = -1;

@@ -90,6 +90,12 @@ constexpr int kMaxViews = 8;  // gsr_forward_views: views per call (= GSR_MAX_VI
 #ifndef GSR_RB_TILE_KEYS
 #define GSR_RB_TILE_KEYS 0
 #endif
+// GSR_RB_SORT_KEYS 1: the row-bucketed placement writes every instance's depth key beside its gid
+// (into the tile-key array kA, free in that mode), so the per-tile sort that follows reads its keys
+// coalesced instead of through a dependent depth_key[gid] gather per entry (round 6)
+#ifndef GSR_RB_SORT_KEYS
+#define GSR_RB_SORT_KEYS 1
+#endif
 // GSR_RB_DEEP 0: only where the per-tile sort takes its register form (mean slices <= ~1365)
 #ifndef GSR_RB_DEEP
 #define GSR_RB_DEEP 1

@@ -672,11 +672,12 @@ __global__ __launch_bounds__(256) void rb_rows_place(const uint32_t* __restrict_
                                                      const uint32_t* __restrict__ histA,
                                                      const uint32_t* __restrict__ totA, int nbA,
                                                      uint32_t* __restrict__ pgid, uint32_t* __restrict__ pxr,
-                                                     long long pcap) {
+                                                     long long pcap, const uint32_t* __restrict__ depth_key,
+                                                     uint32_t* __restrict__ pkey) {
     __shared__ uint32_t cnt[kRbMaxRows];  // pairs per row, then the running staging slot
     __shared__ uint32_t gb[kRbMaxRows];   // global position of the block's first pair of row r
     __shared__ uint32_t lb[kRbMaxRows];   // staging position of the block's first pair of row r
-    __shared__ uint32_t sg[kRbStageA], sx[kRbStageA];
+    __shared__ uint32_t sg[kRbStageA], sx[kRbStageA], sk[kRbStageA];
     __shared__ uint8_t sr[kRbStageA];
     __shared__ uint32_t wsum[kWaves];
     const int tid = threadIdx.x, R = ty1 - ty0;
@@ -706,6 +707,7 @@ __global__ __launch_bounds__(256) void rb_rows_place(const uint32_t* __restrict_
         by1 = (maxy < ty1 ? maxy : ty1) - ty0;
         xr = (rr.x & 0xFFFFu) | (rr.y << 16);
     }
+    const uint32_t dk = pkey && nt ? depth_key[g] : 0u;  // the pair's depth key (pkey: for pass B)
     __syncthreads();
     for (int r = by0; r < by1; ++r) atomicAdd(&cnt[r], 1u);
     __syncthreads();
@@ -725,12 +727,14 @@ __global__ __launch_bounds__(256) void rb_rows_place(const uint32_t* __restrict_
         if (staged) {
             sg[lb[r] + k] = (uint32_t)g;
             sx[lb[r] + k] = xr;
+            if (pkey) sk[lb[r] + k] = dk;
             sr[lb[r] + k] = (uint8_t)r;
         } else {
             const long long pos = (long long)gb[r] + k;
             if (pos < pcap) {
                 pgid[pos] = (uint32_t)g;
                 pxr[pos] = xr;
+                if (pkey) pkey[pos] = dk;
             }
         }
     }
@@ -742,6 +746,7 @@ __global__ __launch_bounds__(256) void rb_rows_place(const uint32_t* __restrict_
         if (pos < pcap) {
             pgid[pos] = sg[i];
             pxr[pos] = sx[i];
+            if (pkey) pkey[pos] = sk[i];
         }
     }
 }
@@ -953,24 +958,32 @@ __global__ __launch_bounds__(kRbScanThreads) void rb_tiles_scan(const uint32_t* 
 
 // pass B, placement: each chunk's instances, a slot per instance from its column's LDS counter
 // (order inside a tile is free, as in pass A), staged in LDS by column and written as coalesced
-// column runs (tile key and gid).
+// column runs (tile key and gid; with tdk also the depth key, which pass A wrote beside each pair
+// (pkey), so the per-tile sort that follows reads its keys coalesced instead of gathering one
+// behind every gid load).  The staging holds each instance's pair index (u16) and column; the
+// chunk's pairs (gid, key) sit in LDS beside it.
 __global__ __launch_bounds__(256) void rb_chunks_place(const uint32_t* __restrict__ pgid, const uint32_t* __restrict__ pxr,
                                                        const uint32_t* __restrict__ totA, int R, int gx, int ty0,
                                                        long long pcap, long long cap,
                                                        const uint32_t* __restrict__ histB,
-                                                       uint32_t* __restrict__ tkey, uint32_t* __restrict__ tgid) {
+                                                       uint32_t* __restrict__ tkey, uint32_t* __restrict__ tgid,
+                                                       const uint32_t* __restrict__ pkey,
+                                                       uint32_t* __restrict__ tdk) {
     __shared__ RbRows t;
     __shared__ uint32_t cnt[kRbMaxCols];  // instances per column, then the running staging slot
     __shared__ uint32_t lb[kRbMaxCols];   // staging start of column c
     __shared__ uint32_t gb[kRbMaxCols];   // global position of the chunk's first instance of column c
-    __shared__ uint32_t sg[kRbStage];
+    __shared__ uint32_t pg[kRbChunk], pk[kRbChunk];  // the chunk's pairs: gid, depth key
+    __shared__ uint16_t sp[kRbStage];                 // staged instance: its pair (index in the chunk)
     __shared__ uint8_t sc[kRbStage];
     __shared__ uint32_t wsum[kWaves];
+    static_assert(kRbChunk <= 65536, "u16 pair index");
     const int tid = threadIdx.x;
+    const bool keys = tdk != nullptr;  // launch-uniform
     rb_rows_table(totA, R, pcap, t);
     constexpr int kQ = kRbChunk / 256;
     // the next chunk's pairs are loaded while this one is placed (register double buffer)
-    uint32_t nxr[kQ], ngg[kQ];
+    uint32_t nxr[kQ], ngg[kQ], nkk[kQ];
     auto load_pairs = [&](uint32_t b) {
         const RbChunk c = rb_chunk(t, b);
 #pragma unroll
@@ -978,6 +991,7 @@ __global__ __launch_bounds__(256) void rb_chunks_place(const uint32_t* __restric
             const uint32_t p = c.p0 + q * 256 + tid;
             nxr[q] = p < c.p1 ? pxr[p] : 0u;  // 0: no columns
             ngg[q] = p < c.p1 ? pgid[p] : 0u;
+            nkk[q] = keys && p < c.p1 ? pkey[p] : 0u;
         }
     };
     if (blockIdx.x < t.nchunks) load_pairs(blockIdx.x);
@@ -985,11 +999,12 @@ __global__ __launch_bounds__(256) void rb_chunks_place(const uint32_t* __restric
         const RbChunk ch = rb_chunk(t, b);
         cnt[tid] = 0u;
         const uint32_t hb = tid < gx ? histB[(size_t)gx * ch.cp + (size_t)tid * ch.nch + ch.k] : 0u;
-        uint32_t xr[kQ], gg[kQ];
+        uint32_t xr[kQ], gg[kQ], kk[kQ];
 #pragma unroll
         for (int q = 0; q < kQ; ++q) {
             xr[q] = nxr[q];
             gg[q] = ngg[q];
+            kk[q] = nkk[q];
         }
         if (b + gridDim.x < t.nchunks) load_pairs(b + gridDim.x);
         __syncthreads();  // cnt zeroed (and the previous chunk's staging read out)
@@ -1007,17 +1022,25 @@ __global__ __launch_bounds__(256) void rb_chunks_place(const uint32_t* __restric
         __syncthreads();
         const bool staged = tot <= (uint32_t)kRbStage;  // block-uniform
         const uint32_t row_tile = (uint32_t)(ty0 + ch.r) * (uint32_t)gx;
+        if (staged) {
+#pragma unroll
+            for (int q = 0; q < kQ; ++q) {
+                pg[q * 256 + tid] = gg[q];
+                if (keys) pk[q * 256 + tid] = kk[q];
+            }
+        }
 #pragma unroll
         for (int q = 0; q < kQ; ++q) {
             for (uint32_t c = xr[q] & 0xFFFFu; c < (xr[q] >> 16); ++c) {
                 const uint32_t k = atomicAdd(&cnt[c], 1u);
                 if (staged) {
-                    sg[lb[c] + k] = gg[q];
+                    sp[lb[c] + k] = (uint16_t)(q * 256 + tid);
                     sc[lb[c] + k] = (uint8_t)c;
                 } else {
                     const long long pos = (long long)gb[c] + k;
                     if (pos < cap) {
                         if (tkey) tkey[pos] = row_tile + c;
+                        if (keys) tdk[pos] = kk[q];
                         tgid[pos] = gg[q];
                     }
                 }
@@ -1030,7 +1053,9 @@ __global__ __launch_bounds__(256) void rb_chunks_place(const uint32_t* __restric
                 const long long pos = (long long)gb[c] + ((uint32_t)i - lb[c]);
                 if (pos < cap) {
                     if (tkey) tkey[pos] = row_tile + (uint32_t)c;
-                    tgid[pos] = sg[i];
+                    const int pi = sp[i];
+                    if (keys) tdk[pos] = pk[pi];
+                    tgid[pos] = pg[pi];
                 }
             }
         }
@@ -1176,7 +1201,7 @@ struct SliceLds {
 template <int NT, int I, int DB, bool kFixInline = false>
 __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t* __restrict__ depth_key,
                                                  uint32_t* __restrict__ gid, SliceLds<NT, I, DB>& lds,
-                                                 bool unordered = false) {
+                                                 bool unordered = false, const uint32_t* __restrict__ pkey = nullptr) {
     constexpr int NWV = NT / 64, BINS = 1 << DB;
     constexpr uint32_t DMASK = BINS - 1u;
     auto& wcnt = lds.wcnt;
@@ -1198,7 +1223,8 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
         const int idx = base + r * 64 + lane;
         const bool valid = idx < end;
         val[r] = valid ? gid[rg.x + idx] : 0u;
-        key[r] = valid ? depth_key[val[r]] : 0xFFFFFFFFu;
+        // the placed keys beside the gids (pkey: one coalesced load, not a gather behind the gid's)
+        key[r] = valid ? (pkey ? pkey[rg.x + idx] : depth_key[val[r]]) : 0xFFFFFFFFu;
         if (valid) {
             kor |= key[r];
             kand &= key[r];
@@ -1446,7 +1472,8 @@ __device__ __forceinline__ void wave_bitonic(uint64_t (&v)[E], int lane) {
 // conflicts).
 template <int E>
 __device__ __forceinline__ void wave_sort_slice(const uint2 rg, const uint32_t* __restrict__ depth_key,
-                                                uint32_t* __restrict__ gid, int lane, uint32_t* xs) {
+                                                uint32_t* __restrict__ gid, int lane, uint32_t* xs,
+                                                const uint32_t* __restrict__ pkey = nullptr) {
     const int n = (int)(rg.y - rg.x);
     uint64_t v[E];
 #pragma unroll
@@ -1455,7 +1482,7 @@ __device__ __forceinline__ void wave_sort_slice(const uint2 rg, const uint32_t* 
         uint64_t k = 0x7FFFFFFFFFFFFFFFull;  // padding sorts last (no real key reaches it)
         if (i < n) {
             const uint32_t g = gid[rg.x + i];
-            k = ((uint64_t)depth_key[g] << 32) | g;
+            k = ((uint64_t)(pkey ? pkey[rg.x + i] : depth_key[g]) << 32) | g;
         }
         v[e] = k;
     }
@@ -1540,7 +1567,8 @@ __device__ __forceinline__ void wave_bitonic32(uint32_t (&v)[E], int lane) {
 
 template <int E>
 __device__ __forceinline__ void wave_sort_slice32(const uint2 rg, const uint32_t* __restrict__ depth_key,
-                                                  uint32_t* __restrict__ gid, int lane, uint32_t* xs) {
+                                                  uint32_t* __restrict__ gid, int lane, uint32_t* xs,
+                                                  const uint32_t* __restrict__ pkey = nullptr) {
     static_assert(64 * E <= (1 << (32 - kWaveKeyBits)), "slice position bits");
     constexpr uint32_t kPos = (1u << (32 - kWaveKeyBits)) - 1u;
     const int n = (int)(rg.y - rg.x);
@@ -1551,7 +1579,7 @@ __device__ __forceinline__ void wave_sort_slice32(const uint2 rg, const uint32_t
         const int i = e * 64 + lane;
         dk[e] = 0u;
         if (i < n) {
-            dk[e] = depth_key[gid[rg.x + i]];
+            dk[e] = pkey ? pkey[rg.x + i] : depth_key[gid[rg.x + i]];
             kor |= dk[e];
             kand &= dk[e];
         }
@@ -1617,7 +1645,7 @@ __device__ __forceinline__ void wave_sort_slice32(const uint2 rg, const uint32_t
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (__ballot(longrun)) {  // many entries at one truncated depth: the 64-bit form
-            wave_sort_slice<E>(rg, depth_key, gid, lane, xs);
+            wave_sort_slice<E>(rg, depth_key, gid, lane, xs, pkey);
             return;
         }
     }
@@ -1649,7 +1677,8 @@ __device__ __forceinline__ void wave_sort_slice32(const uint2 rg, const uint32_t
 __global__ __launch_bounds__(256) void tile_depth_wave(const uint2* __restrict__ ranges, int tile0, int ntiles,
                                                       const uint32_t* __restrict__ depth_key,
                                                       uint32_t* __restrict__ gid, uint32_t* __restrict__ ovf,
-                                                      uint32_t* __restrict__ ovf_count) {
+                                                      uint32_t* __restrict__ ovf_count,
+                                                      const uint32_t* __restrict__ pkey) {
     __shared__ uint32_t xs_all[4][64 * 16 + 32];
     const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (t >= ntiles) return;
@@ -1664,18 +1693,18 @@ __global__ __launch_bounds__(256) void tile_depth_wave(const uint2* __restrict__
         return;
     }
     if (GSR_WAVE_KEY32) {
-        if (n <= 64) wave_sort_slice32<1>(rg, depth_key, gid, lane, xs);
-        else if (n <= 128) wave_sort_slice32<2>(rg, depth_key, gid, lane, xs);
-        else if (n <= 256) wave_sort_slice32<4>(rg, depth_key, gid, lane, xs);
-        else if (n <= 512) wave_sort_slice32<8>(rg, depth_key, gid, lane, xs);
-        else wave_sort_slice32<16>(rg, depth_key, gid, lane, xs);
+        if (n <= 64) wave_sort_slice32<1>(rg, depth_key, gid, lane, xs, pkey);
+        else if (n <= 128) wave_sort_slice32<2>(rg, depth_key, gid, lane, xs, pkey);
+        else if (n <= 256) wave_sort_slice32<4>(rg, depth_key, gid, lane, xs, pkey);
+        else if (n <= 512) wave_sort_slice32<8>(rg, depth_key, gid, lane, xs, pkey);
+        else wave_sort_slice32<16>(rg, depth_key, gid, lane, xs, pkey);
         return;
     }
-    if (n <= 64) wave_sort_slice<1>(rg, depth_key, gid, lane, xs);
-    else if (n <= 128) wave_sort_slice<2>(rg, depth_key, gid, lane, xs);
-    else if (n <= 256) wave_sort_slice<4>(rg, depth_key, gid, lane, xs);
-    else if (n <= 512) wave_sort_slice<8>(rg, depth_key, gid, lane, xs);
-    else wave_sort_slice<16>(rg, depth_key, gid, lane, xs);
+    if (n <= 64) wave_sort_slice<1>(rg, depth_key, gid, lane, xs, pkey);
+    else if (n <= 128) wave_sort_slice<2>(rg, depth_key, gid, lane, xs, pkey);
+    else if (n <= 256) wave_sort_slice<4>(rg, depth_key, gid, lane, xs, pkey);
+    else if (n <= 512) wave_sort_slice<8>(rg, depth_key, gid, lane, xs, pkey);
+    else wave_sort_slice<16>(rg, depth_key, gid, lane, xs, pkey);
 }
 
 // The queued slices of 1025 .. 2048 entries, one wave each (a kernel of its own: the 32-entry-per-
@@ -1689,7 +1718,8 @@ __global__ __launch_bounds__(256) void tile_depth_wave_queue(const uint2* __rest
                                                             const uint32_t* __restrict__ ovf,
                                                             const uint32_t* __restrict__ ovf_count,
                                                             uint32_t* __restrict__ ovf2,
-                                                            uint32_t* __restrict__ ovf2_count) {
+                                                            uint32_t* __restrict__ ovf2_count,
+                                                            const uint32_t* __restrict__ pkey) {
     __shared__ uint32_t xs_all[4][64 * 32 + 64];
     const uint32_t cnt = *ovf_count;
     const int lane = threadIdx.x & 63;
@@ -1702,7 +1732,215 @@ __global__ __launch_bounds__(256) void tile_depth_wave_queue(const uint2* __rest
             if (lane == 0) ovf2[atomicAdd(ovf2_count, 1u)] = tile;
             continue;  // wave-uniform
         }
-        wave_sort_slice<32>(rg, depth_key, gid, lane, xs);
+        wave_sort_slice<32>(rg, depth_key, gid, lane, xs, pkey);
+    }
+}
+
+// ---- per-tile depth order, block form: slices of 1025 .. NW x 1024 entries (round 6) ----
+// Each of the block's NW waves sorts 1024 entries of the slice with the register network on
+// 32-bit keys (the slice's top differing depth bits over the entry's slice position, as the
+// one-wave form: 20 bits over 12 at 4096 entries, 19 over 13 at 8192); the waves' runs are then
+// merged by the same all-ascending network, its stages at distances >= 1024 exchanged through LDS
+// (one write, a barrier and one read per entry; padded rows: conflict-free) and
+// the rest inside each wave.  Against the LDS radix form (two or three counting passes of ~6
+// barriers each, the digit-peer ballots, latency-bound per block, PMC round 6): ~log2(n)^2 / 2
+// register stages, 3 (4096) or 6 (8192) LDS exchanges.  Runs of equal truncated keys are put in
+// (depth, gid) order from the full keys by the thread holding a run's first entry; a run longer
+// than kWaveRunMax (depths clustered inside one truncated step) leaves the slice untouched and
+// hands the tile on (`false`) to the next queue, whose forms sort every bit.
+constexpr int kBlkE = 16;  // entries per lane
+__host__ __device__ constexpr int blk_pad(int i) { return i + (i >> 5); }
+template <int NW>
+struct BlockSortLds {
+    uint32_t xs[blk_pad(NW * 1024)];
+    uint32_t red[2][NW];
+};
+
+template <int NW>
+__device__ __forceinline__ bool block_sort_slice(const uint2 rg, const uint32_t* __restrict__ depth_key,
+                                                 uint32_t* __restrict__ gid, const uint32_t* __restrict__ pkey,
+                                                 BlockSortLds<NW>& L) {
+    constexpr int CAP = NW * 1024, NT = NW * 64;
+    constexpr int PB = NW == 2 ? 11 : NW == 4 ? 12 : 13;  // position bits
+    constexpr int KB = 32 - PB;                           // truncated depth bits
+    static_assert((1 << PB) == CAP, "position bits");
+    constexpr uint32_t kPos = CAP - 1u;
+    const int n = (int)(rg.y - rg.x);
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    // active waves: the power of two whose runs cover the slice (the rest only meet the barriers)
+    const int nwa = n <= 1024 ? 1 : n <= 2048 ? 2 : n <= 4096 ? 4 : 8;
+    const bool act = w < nwa;
+    uint32_t v[kBlkE];
+    uint32_t kor = 0u, kand = ~0u;
+#pragma unroll
+    for (int e = 0; e < kBlkE; ++e) {
+        const int i = w * 1024 + e * 64 + lane;
+        v[e] = 0u;
+        if (i < n) {
+            v[e] = pkey ? pkey[rg.x + i] : depth_key[gid[rg.x + i]];
+            kor |= v[e];
+            kand &= v[e];
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        kor |= __shfl_xor(kor, o, 64);
+        kand &= __shfl_xor(kand, o, 64);
+    }
+    if (lane == 0) {
+        L.red[0][w] = kor;
+        L.red[1][w] = kand;
+    }
+    __syncthreads();
+    {
+        uint32_t o_ = 0u, a_ = ~0u;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            o_ |= L.red[0][k];
+            a_ &= L.red[1][k];
+        }
+        kor = o_;
+        kand = a_;
+    }
+    const uint32_t dif = kor ^ kand;
+    const int top = dif ? 32 - __clz(dif) : 0;  // differing bits [0, top)
+    const int sh = top > KB ? top - KB : 0;
+#pragma unroll
+    for (int e = 0; e < kBlkE; ++e) {
+        const int i = w * 1024 + e * 64 + lane;
+        // padding ~0 sorts last: a real key reaches it only at position CAP - 1, i.e. n = CAP
+        v[e] = i < n ? (((v[e] >> sh) & ((1u << KB) - 1u)) << PB) | (uint32_t)i : ~0u;
+    }
+    if (act) wave_bitonic32<kBlkE, 2>(v, lane);  // each active wave's 1024 entries, ascending
+    // merges of the waves' runs: entry i = w 1024 + 16 lane + e
+    const int i0 = w * 1024 + lane * kBlkE;
+    uint32_t* const xs = L.xs;
+    auto lds_stage = [&](int x, int h) {  // i <-> i ^ x, the lower of the pair (i & h == 0) keeps the min
+        if (act) {
+#pragma unroll
+            for (int e = 0; e < kBlkE; ++e) xs[blk_pad(i0 + e)] = v[e];
+        }
+        __syncthreads();
+        if (act) {
+            const bool hi = (i0 & h) != 0;  // the same for the lane's 16 entries (h >= 1024)
+#pragma unroll
+            for (int e = 0; e < kBlkE; ++e) {
+                const uint32_t o = xs[blk_pad((i0 + e) ^ x)];
+                v[e] = hi ? (v[e] > o ? v[e] : o) : (v[e] < o ? v[e] : o);
+            }
+        }
+        __syncthreads();  // xs is rewritten by the next stage
+    };
+    for (int K = 2048; K <= nwa * 1024; K <<= 1) {  // block-uniform
+        lds_stage(K - 1, K >> 1);                     // the mirror stage
+        for (int J = K >> 2; J >= 1024; J >>= 1) lds_stage(J, J);
+        if (act) wave_half_cleaners32<kBlkE, 512>(v, lane);
+    }
+    // the sorted keys by rank, then the runs of equal truncated keys
+    if (act) {
+#pragma unroll
+        for (int e = 0; e < kBlkE; ++e) xs[blk_pad(i0 + e)] = v[e];
+    }
+    __syncthreads();
+    bool tie = false;
+    if (act) {
+#pragma unroll
+        for (int e = 0; e < kBlkE; ++e) {
+            const int r = i0 + e;
+            if (r + 1 < n && (v[e] >> PB) == (xs[blk_pad(r + 1)] >> PB)) tie = true;
+        }
+    }
+    if (__syncthreads_or(tie)) {  // block-uniform
+        auto full = [&](uint32_t x) {
+            const uint32_t g = gid[rg.x + (x & kPos)];
+            return ((uint64_t)(pkey ? pkey[rg.x + (x & kPos)] : depth_key[g]) << 32) | g;
+        };
+        bool longrun = false;
+        if (act) {
+#pragma unroll
+            for (int e = 0; e < kBlkE; ++e) {
+                const int r = i0 + e;
+                const uint32_t top_r = v[e] >> PB;
+                if (r + 1 >= n || (xs[blk_pad(r + 1)] >> PB) != top_r) continue;
+                if (r > 0 && (xs[blk_pad(r - 1)] >> PB) == top_r) continue;  // not the run's first
+                int end = r + 2;
+                while (end < n && (xs[blk_pad(end)] >> PB) == top_r && end - r <= kWaveRunMax) ++end;
+                if (end - r > kWaveRunMax) {
+                    longrun = true;
+                    continue;
+                }
+                for (int a = r + 1; a < end; ++a) {  // insertion by the full (depth, gid) key
+                    const uint32_t x = xs[blk_pad(a)];
+                    const uint64_t fx = full(x);
+                    int b = a;
+                    while (b > r && full(xs[blk_pad(b - 1)]) > fx) {
+                        xs[blk_pad(b)] = xs[blk_pad(b - 1)];
+                        --b;
+                    }
+                    xs[blk_pad(b)] = x;
+                }
+            }
+        }
+        if (__syncthreads_or(longrun)) return false;  // nothing written: the next form sorts it
+    }
+    // out in rank order: every thread's reads of the slice's gids complete, block-wide, before the
+    // first store over them
+    uint32_t og[CAP / NT];
+#pragma unroll
+    for (int k = 0; k < CAP / NT; ++k) {
+        const int r = k * NT + tid;
+        og[k] = r < n ? gid[rg.x + (xs[blk_pad(r)] & kPos)] : 0u;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < CAP / NT; ++k) {
+        const int r = k * NT + tid;
+        if (r < n) gid[rg.x + r] = og[k];
+    }
+    __syncthreads();  // xs / red are rewritten by the block's next slice
+    return true;
+}
+
+#ifndef GSR_TILE_BLOCK_SORT
+#define GSR_TILE_BLOCK_SORT 1
+#endif
+
+// One block of four waves per tile of the launch (slices of up to 4096 entries); longer slices, and
+// those with long runs of equal truncated keys, go to the queue `ovf`.
+__global__ __launch_bounds__(256) void tile_depth_block(const uint2* __restrict__ ranges, int tile0,
+                                                       const uint32_t* __restrict__ depth_key,
+                                                       uint32_t* __restrict__ gid, uint32_t* __restrict__ ovf,
+                                                       uint32_t* __restrict__ ovf_count,
+                                                       const uint32_t* __restrict__ pkey) {
+    __shared__ BlockSortLds<4> lds;
+    const int tile = tile0 + blockIdx.x;
+    const uint2 rg = ranges[tile];
+    const int n = (int)(rg.y - rg.x);
+    if (n <= 1) return;
+    if (n > 4096 || !block_sort_slice<4>(rg, depth_key, gid, pkey, lds)) {
+        if (threadIdx.x == 0) ovf[atomicAdd(ovf_count, 1u)] = (uint32_t)tile;
+    }
+}
+
+// The queued slices of up to 8192 entries, eight waves per block, one queued tile per block (the
+// grid covers every tile; blocks past the queue's length exit at once); longer ones and those with
+// long truncated-key runs go on to `ovf2` (tile_depth_sort_big sorts every bit).
+__global__ __launch_bounds__(512) void tile_depth_block_queue(const uint2* __restrict__ ranges,
+                                                             const uint32_t* __restrict__ depth_key,
+                                                             uint32_t* __restrict__ gid,
+                                                             const uint32_t* __restrict__ ovf,
+                                                             const uint32_t* __restrict__ ovf_count,
+                                                             uint32_t* __restrict__ ovf2,
+                                                             uint32_t* __restrict__ ovf2_count,
+                                                             const uint32_t* __restrict__ pkey) {
+    __shared__ BlockSortLds<8> lds;
+    if (blockIdx.x >= *ovf_count) return;
+    const uint32_t tile = ovf[blockIdx.x];
+    const uint2 rg = ranges[tile];
+    const int n = (int)(rg.y - rg.x);
+    if (n > 8192 || !block_sort_slice<8>(rg, depth_key, gid, pkey, lds)) {  // block-uniform
+        if (threadIdx.x == 0) ovf2[atomicAdd(ovf2_count, 1u)] = tile;
     }
 }
 
@@ -1711,7 +1949,8 @@ template <int NT, int I, int DB>
 __global__ __launch_bounds__(NT) void tile_depth_radix(const uint2* __restrict__ ranges, int tile0,
                                                       const uint32_t* __restrict__ depth_key,
                                                       uint32_t* __restrict__ gid, uint32_t* __restrict__ ovf,
-                                                      uint32_t* __restrict__ ovf_count, int unordered) {
+                                                      uint32_t* __restrict__ ovf_count, int unordered,
+                                                      const uint32_t* __restrict__ pkey) {
     const int tile = tile0 + blockIdx.x;
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
@@ -1721,7 +1960,7 @@ __global__ __launch_bounds__(NT) void tile_depth_radix(const uint2* __restrict__
         return;
     }
     __shared__ SliceLds<NT, I, DB> lds;
-    radix_sort_slice<NT, I, DB>(rg, depth_key, gid, lds, unordered != 0);
+    radix_sort_slice<NT, I, DB>(rg, depth_key, gid, lds, unordered != 0, pkey);
 }
 
 // The queued (longer) slices: blocks walk the queue; slices longer than NT * I go on to the
@@ -1734,7 +1973,7 @@ __global__ __launch_bounds__(NT) void tile_depth_radix_queue(const uint2* __rest
                                                             const uint32_t* __restrict__ ovf,
                                                             const uint32_t* __restrict__ ovf_count,
                                                             uint32_t* __restrict__ ovf2, uint32_t* __restrict__ ovf2_count,
-                                                            int unordered) {
+                                                            int unordered, const uint32_t* __restrict__ pkey) {
     __shared__ SliceLds<NT, I, DB> lds;
     const uint32_t cnt = *ovf_count;
     for (uint32_t q = blockIdx.x; q < cnt; q += gridDim.x) {
@@ -1744,7 +1983,7 @@ __global__ __launch_bounds__(NT) void tile_depth_radix_queue(const uint2* __rest
             if (threadIdx.x == 0) ovf2[atomicAdd(ovf2_count, 1u)] = tile;
             continue;  // block-uniform
         }
-        radix_sort_slice<NT, I, DB>(rg, depth_key, gid, lds, unordered != 0);
+        radix_sort_slice<NT, I, DB>(rg, depth_key, gid, lds, unordered != 0, pkey);
     }
 }
 
@@ -1955,8 +2194,10 @@ int launch_block_offsets(const uint32_t* tiles, int n, const uint32_t* bsum, uin
 int launch_rb_binning(const uint32_t* tiles, uint4* rect, uint32_t* offsets, int n, int gx, int ty0, int ty1,
                       uint32_t* histA, uint32_t* histB, uint32_t* rb_status, uint32_t* pgid, uint32_t* pxr,
                       uint32_t* tkey, uint32_t* tgid, uint2* ranges, long long cap, hipStream_t s,
-                      bool rows_counted, const uint32_t* bsum, uint32_t* K_dev) {
+                      bool rows_counted, const uint32_t* bsum, uint32_t* K_dev, const uint32_t* depth_key,
+                      uint32_t* pkey, uint32_t* tdk) {
     const int R = ty1 - ty0;
+    if (!depth_key || !pkey || !tdk) pkey = tdk = nullptr;
     if (n <= 0 || R <= 0 || cap <= 0) return 0;  // ranges stay cleared
     if (R > kRbMaxRows || gx > kRbMaxCols || cap >= kRbMaxCap) return (int)hipErrorInvalidValue;
     const int nbA = div_up(n, 256);
@@ -1965,7 +2206,7 @@ int launch_rb_binning(const uint32_t* tiles, uint4* rect, uint32_t* offsets, int
         hipLaunchKernelGGL(rb_rows_count, dim3(nbA), dim3(256), 0, s, tiles, rect, n, ty0, ty1, histA, nbA);
     hipLaunchKernelGGL(rb_colscan, dim3(R), dim3(1024), 0, s, histA, nbA, totA);
     hipLaunchKernelGGL(rb_rows_place, dim3(nbA), dim3(256), 0, s, tiles, rect, offsets, bsum, n, ty0, ty1, histA, totA,
-                       nbA, pgid, pxr, cap);
+                       nbA, pgid, pxr, cap, depth_key, pkey);
     // chunks: at most cap / kRbChunk full ones plus one partial per row; the blocks walk them, so
     // the grid is capped near what the chip holds at once (no tail of empty blocks)
     const int nch_max = div_up(cap, kRbChunk) + R;
@@ -1974,7 +2215,7 @@ int launch_rb_binning(const uint32_t* tiles, uint4* rect, uint32_t* offsets, int
     hipLaunchKernelGGL(rb_tiles_scan, dim3(R), dim3(kRbScanThreads), 0, s, totA, R, gx, ty0, cap, cap, histB,
                        rb_status + 16, rb_status, ranges, K_dev);
     hipLaunchKernelGGL(rb_chunks_place, dim3(gplace), dim3(256), 0, s, pgid, pxr, totA, R, gx, ty0, cap, cap, histB,
-                       tkey, tgid);
+                       tkey, tgid, pkey, tdk);
     return (int)hipGetLastError();
 }
 
@@ -2030,7 +2271,7 @@ bool tile_wave_sort_eligible(long long K, int ntiles) { return GSR_TILE_WAVE_SOR
 int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long K, const uint32_t* depth_key,
                            uint32_t* gid, uint32_t* ovf, uint32_t* ovf_count, uint32_t* ovf2, uint32_t* ovf2_count,
                            uint32_t* done, uint32_t* scratch_hi, uint32_t* scratch_lo, hipStream_t s,
-                           bool unordered) {
+                           bool unordered, const uint32_t* pkey) {
     if (ntiles <= 0 || K <= 0) return 0;
     const int uo = unordered ? 1 : 0;
     // one block per tile holding up to cap entries in LDS, a power of two >= 1.5x the mean slice
@@ -2043,7 +2284,7 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
     // mean slice leaves most tiles within that (the longer ones queue for the LDS forms below)
     if (tile_wave_sort_eligible(K, ntiles)) {
         hipLaunchKernelGGL(tile_depth_wave, dim3(div_up(ntiles, 4)), dim3(256), 0, s, ranges, tile0, ntiles, depth_key,
-                           gid, ovf, ovf_count);
+                           gid, ovf, ovf_count, pkey);
         // the slices past one wave's 1024 entries: where the mean is near 1024 (bands), many -- a
         // 2048-entry wave each, the rest on to the LDS form; elsewhere few (none at 1M / 1080p) --
         // all straight to the 1024-thread LDS form, one launch instead of two more near-empty
@@ -2052,7 +2293,7 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
         if (K / ntiles > 900) {
             const int wgrid = ntiles < 2048 ? div_up(ntiles, 4) : 512;
             hipLaunchKernelGGL(tile_depth_wave_queue, dim3(wgrid), dim3(256), 0, s, ranges, depth_key, gid, ovf,
-                               ovf_count, ovf2, ovf2_count);
+                               ovf_count, ovf2, ovf2_count, pkey);
             hipLaunchKernelGGL(tile_depth_sort_big, dim3(bgrid), dim3(1024), 0, s, ranges, depth_key, gid, ovf2,
                                ovf2_count, done, scratch_hi, scratch_lo, uo);
         } else {
@@ -2063,7 +2304,7 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
     } else {
 #define GSR_TILE_RADIX(NT_, I_)                                                                       \
     hipLaunchKernelGGL((tile_depth_radix<NT_, I_, 9>), dim3(ntiles), dim3(NT_), 0, s, ranges, tile0, depth_key, \
-                       gid, ovf, ovf_count, uo)
+                       gid, ovf, ovf_count, uo, pkey)
 #ifndef GSR_BAND_SORT_NT
 #define GSR_BAND_SORT_NT 512
 #endif
@@ -2072,6 +2313,16 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
 #ifndef GSR_FULL_SORT_NT
 #define GSR_FULL_SORT_NT 0
 #endif
+    if (GSR_TILE_BLOCK_SORT && cap == 4096) {  // deep slices: the block form, then its 8192-entry queue
+        hipLaunchKernelGGL(tile_depth_block, dim3(ntiles), dim3(256), 0, s, ranges, tile0, depth_key, gid, ovf,
+                           ovf_count, pkey);
+        hipLaunchKernelGGL(tile_depth_block_queue, dim3(ntiles), dim3(512), 0, s, ranges, depth_key, gid, ovf,
+                           ovf_count, ovf2, ovf2_count, pkey);
+        const int bgrid = ntiles < 256 ? ntiles : 256;
+        hipLaunchKernelGGL(tile_depth_sort_big, dim3(bgrid), dim3(1024), 0, s, ranges, depth_key, gid, ovf2,
+                           ovf2_count, done, scratch_hi, scratch_lo, uo);
+        return (int)hipGetLastError();
+    }
     if (ntiles < 4096 && GSR_BAND_SORT_NT == 512) {  // band launches: fewer tiles, wider blocks
         if (cap == 1024) GSR_TILE_RADIX(512, 2);
         else if (cap == 2048) GSR_TILE_RADIX(512, 4);
@@ -2095,7 +2346,7 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
     }
     const int qgrid = ntiles < 512 ? ntiles : 512;
     hipLaunchKernelGGL((tile_depth_radix_queue<512, 16, 8>), dim3(qgrid), dim3(512), 0, s, ranges, depth_key, gid, ovf,
-                       ovf_count, ovf2, ovf2_count, uo);
+                       ovf_count, ovf2, ovf2_count, uo, pkey);
     // slices beyond 8192: the 16384-entry LDS form and the chunked form (tile_depth_sort_big)
     const int bgrid = ntiles < 256 ? ntiles : 256;
     hipLaunchKernelGGL(tile_depth_sort_big, dim3(bgrid), dim3(1024), 0, s, ranges, depth_key, gid, ovf2, ovf2_count,
