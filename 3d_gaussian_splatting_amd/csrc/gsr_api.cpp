@@ -417,21 +417,25 @@ int fwd_phase2(FwdJob& j, long long cap, gsr_alloc_fn alloc_binning, void* ctx, 
         // F3 + the tile sort + F5 as two counting passes; the pairs ride in (kB, vB)
         // (the tile keys are left to the GSR_VIEW_SORTED_TILE accessor: nothing in the step reads them;
         // kA carries the instances' depth keys from the placement to the per-tile sort instead)
-        // and the pairs' keys ride in the checkpoint pool, which F6 fills only after the sort (when it
-        // holds cap words: every image with a few KB of list per tile)
+        // With the depth keys placed (rb_keys): pass A's pairs as (gid, key) over kA..vA with their
+        // columns in the checkpoint pool (which F6 fills only after the sort; used when it holds cap
+        // words), pass B's instances as (gid, key) over kB..vB, and the per-tile sort writes the
+        // ordered gids to vA -- one 8-B store per pair / instance and no key gather in the sort.
         const bool rb_keys = GSR_RB_SORT_KEYS && !GSR_RB_TILE_KEYS && v.ck_bytes >= 4 * (size_t)cap;
+        uint2* const ppair = rb_keys ? reinterpret_cast<uint2*>(v.kA) : nullptr;
+        uint2* const tpair = rb_keys ? reinterpret_cast<uint2*>(v.kB) : nullptr;
+        uint32_t* const pxr = rb_keys ? reinterpret_cast<uint32_t*>(v.ck) : v.vB;
         GSR_STAGE(GSR_STAGE_TILE_SORT, launch_rb_binning(v.tiles, v.rect, v.offsets, (int)j.n, j.gx, j.ty0, j.ty1,
-                                                         v.rb_histA, v.rb_histB, v.rb_status, v.kB, v.vB,
+                                                         v.rb_histA, v.rb_histB, v.rb_status, v.kB, pxr,
                                                          GSR_RB_TILE_KEYS ? v.kA : nullptr, v.vA,
                                                          v.ranges, cap, stream, j.rows_counted,
                                                          j.rows_counted ? v.lookback + 16 : nullptr, v.K_dev,
-                                                         v.depth_key, rb_keys ? reinterpret_cast<uint32_t*>(v.ck) : nullptr,
-                                                         rb_keys ? v.kA : nullptr),
+                                                         v.depth_key, ppair, tpair),
                   "row-bucketed binning");
         GSR_STAGE(GSR_STAGE_DEPTH_SORT, launch_tile_depth_sort(v.ranges, j.ty0 * j.gx, ntiles, cap, v.depth_key,
                                                                v.sorted_gid, v.ovf, v.counters + kOvfCountSlot, v.ovf2,
                                                                v.counters + kOvf2CountSlot, v.done, v.free_k,
-                                                               v.free_v, stream, true, rb_keys ? v.kA : nullptr),
+                                                               v.free_v, stream, true, tpair),
                   "per-tile depth order");
     } else if (cap > 0) {
         int which = -1;

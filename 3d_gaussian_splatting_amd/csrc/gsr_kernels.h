@@ -79,9 +79,9 @@ int launch_rb_binning(const uint32_t* tiles, uint4* rect, uint32_t* offsets, int
                       const uint32_t* bsum = nullptr,  // with it: F1's scanned block sums -- the
                                                          // placement writes `offsets` itself
                       uint32_t* K_dev = nullptr,       // set to UINT32_MAX if the look-back times out
-                      const uint32_t* depth_key = nullptr,  // with pkey and tdk: every placed instance's
-                      uint32_t* pkey = nullptr,             // depth key beside its gid (tdk[i] for tgid[i]),
-                      uint32_t* tdk = nullptr);             // via pkey (cap u32 of scratch) beside the pairs
+                      const uint32_t* depth_key = nullptr,  // with ppair and tpair: the pairs go to ppair as
+                      uint2* ppair = nullptr,               // (gid, depth key) (pgid unused; pxr any cap u32)
+                      uint2* tpair = nullptr);              // and the instances to tpair as (gid, key), not tgid
 
 // Per-tile depth order: every tile's slice of `gid` (tile-sorted, gid order within a tile) is
 // sorted in place by (depth_key[gid], gid) -- the canonical (tile, depth, gid) order -- with a
@@ -107,9 +107,10 @@ int launch_duplicate_ranked(const uint32_t* rtiles, const uint4* rrect, uint4* r
 int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long K, const uint32_t* depth_key,
                            uint32_t* gid, uint32_t* ovf, uint32_t* ovf_count, uint32_t* ovf2, uint32_t* ovf2_count,
                            uint32_t* done, uint32_t* scratch_hi, uint32_t* scratch_lo, hipStream_t s,
-                           bool unordered = false, const uint32_t* skey = nullptr);
-// skey (optional): the slices' depth keys in place beside `gid` (the row-bucketed placement's tdk),
-// read coalesced instead of gathered through depth_key[gid] (which the rare paths still use).
+                           bool unordered = false, const uint2* src = nullptr);
+// src (optional): the slices as placed (gid, depth key) pairs (the row-bucketed placement's tpair):
+// the sort reads them coalesced, instead of gathering depth_key[gid], and writes the ordered gids
+// to `gid` (the forms that sort in place get their slices' gids copied there first).
 // unordered: the tiles' entries are in arbitrary order (row-bucketed binning), not gid order --
 // the register form needs nothing else; the LDS forms then also sort by gid (LSD, gid passes first).
 // True when the register form takes the mean slice (the row-bucketed binning is used only then).

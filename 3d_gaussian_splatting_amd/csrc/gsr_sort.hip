@@ -673,7 +673,7 @@ __global__ __launch_bounds__(256) void rb_rows_place(const uint32_t* __restrict_
                                                      const uint32_t* __restrict__ totA, int nbA,
                                                      uint32_t* __restrict__ pgid, uint32_t* __restrict__ pxr,
                                                      long long pcap, const uint32_t* __restrict__ depth_key,
-                                                     uint32_t* __restrict__ pkey) {
+                                                     uint2* __restrict__ ppair) {
     __shared__ uint32_t cnt[kRbMaxRows];  // pairs per row, then the running staging slot
     __shared__ uint32_t gb[kRbMaxRows];   // global position of the block's first pair of row r
     __shared__ uint32_t lb[kRbMaxRows];   // staging position of the block's first pair of row r
@@ -707,7 +707,7 @@ __global__ __launch_bounds__(256) void rb_rows_place(const uint32_t* __restrict_
         by1 = (maxy < ty1 ? maxy : ty1) - ty0;
         xr = (rr.x & 0xFFFFu) | (rr.y << 16);
     }
-    const uint32_t dk = pkey && nt ? depth_key[g] : 0u;  // the pair's depth key (pkey: for pass B)
+    const uint32_t dk = ppair && nt ? depth_key[g] : 0u;  // the pair's depth key (ppair: for pass B)
     __syncthreads();
     for (int r = by0; r < by1; ++r) atomicAdd(&cnt[r], 1u);
     __syncthreads();
@@ -727,14 +727,14 @@ __global__ __launch_bounds__(256) void rb_rows_place(const uint32_t* __restrict_
         if (staged) {
             sg[lb[r] + k] = (uint32_t)g;
             sx[lb[r] + k] = xr;
-            if (pkey) sk[lb[r] + k] = dk;
+            if (ppair) sk[lb[r] + k] = dk;
             sr[lb[r] + k] = (uint8_t)r;
         } else {
             const long long pos = (long long)gb[r] + k;
             if (pos < pcap) {
-                pgid[pos] = (uint32_t)g;
+                if (ppair) ppair[pos] = make_uint2((uint32_t)g, dk);
+                else pgid[pos] = (uint32_t)g;
                 pxr[pos] = xr;
-                if (pkey) pkey[pos] = dk;
             }
         }
     }
@@ -744,9 +744,9 @@ __global__ __launch_bounds__(256) void rb_rows_place(const uint32_t* __restrict_
         const int rr = sr[i];
         const long long pos = (long long)gb[rr] + (uint32_t)i - lb[rr];
         if (pos < pcap) {
-            pgid[pos] = sg[i];
+            if (ppair) ppair[pos] = make_uint2(sg[i], sk[i]);
+            else pgid[pos] = sg[i];
             pxr[pos] = sx[i];
-            if (pkey) pkey[pos] = sk[i];
         }
     }
 }
@@ -958,17 +958,17 @@ __global__ __launch_bounds__(kRbScanThreads) void rb_tiles_scan(const uint32_t* 
 
 // pass B, placement: each chunk's instances, a slot per instance from its column's LDS counter
 // (order inside a tile is free, as in pass A), staged in LDS by column and written as coalesced
-// column runs (tile key and gid; with tdk also the depth key, which pass A wrote beside each pair
-// (pkey), so the per-tile sort that follows reads its keys coalesced instead of gathering one
-// behind every gid load).  The staging holds each instance's pair index (u16) and column; the
-// chunk's pairs (gid, key) sit in LDS beside it.
+// column runs (tile key and gid; with tpair the (gid, depth key) pair, the key from pass A's
+// ppair, so the per-tile sort that follows reads its keys coalesced instead of gathering one
+// behind every gid load, one 8-B store per instance).  The staging holds each instance's pair
+// index (u16) and column; the chunk's pairs (gid, key) sit in LDS beside it.
 __global__ __launch_bounds__(256) void rb_chunks_place(const uint32_t* __restrict__ pgid, const uint32_t* __restrict__ pxr,
                                                        const uint32_t* __restrict__ totA, int R, int gx, int ty0,
                                                        long long pcap, long long cap,
                                                        const uint32_t* __restrict__ histB,
                                                        uint32_t* __restrict__ tkey, uint32_t* __restrict__ tgid,
-                                                       const uint32_t* __restrict__ pkey,
-                                                       uint32_t* __restrict__ tdk) {
+                                                       const uint2* __restrict__ ppair,
+                                                       uint2* __restrict__ tpair) {
     __shared__ RbRows t;
     __shared__ uint32_t cnt[kRbMaxCols];  // instances per column, then the running staging slot
     __shared__ uint32_t lb[kRbMaxCols];   // staging start of column c
@@ -979,7 +979,7 @@ __global__ __launch_bounds__(256) void rb_chunks_place(const uint32_t* __restric
     __shared__ uint32_t wsum[kWaves];
     static_assert(kRbChunk <= 65536, "u16 pair index");
     const int tid = threadIdx.x;
-    const bool keys = tdk != nullptr;  // launch-uniform
+    const bool keys = tpair != nullptr;  // launch-uniform
     rb_rows_table(totA, R, pcap, t);
     constexpr int kQ = kRbChunk / 256;
     // the next chunk's pairs are loaded while this one is placed (register double buffer)
@@ -990,8 +990,14 @@ __global__ __launch_bounds__(256) void rb_chunks_place(const uint32_t* __restric
         for (int q = 0; q < kQ; ++q) {
             const uint32_t p = c.p0 + q * 256 + tid;
             nxr[q] = p < c.p1 ? pxr[p] : 0u;  // 0: no columns
-            ngg[q] = p < c.p1 ? pgid[p] : 0u;
-            nkk[q] = keys && p < c.p1 ? pkey[p] : 0u;
+            if (keys) {
+                const uint2 pp = p < c.p1 ? ppair[p] : make_uint2(0u, 0u);
+                ngg[q] = pp.x;
+                nkk[q] = pp.y;
+            } else {
+                ngg[q] = p < c.p1 ? pgid[p] : 0u;
+                nkk[q] = 0u;
+            }
         }
     };
     if (blockIdx.x < t.nchunks) load_pairs(blockIdx.x);
@@ -1040,8 +1046,8 @@ __global__ __launch_bounds__(256) void rb_chunks_place(const uint32_t* __restric
                     const long long pos = (long long)gb[c] + k;
                     if (pos < cap) {
                         if (tkey) tkey[pos] = row_tile + c;
-                        if (keys) tdk[pos] = kk[q];
-                        tgid[pos] = gg[q];
+                        if (keys) tpair[pos] = make_uint2(gg[q], kk[q]);
+                        else tgid[pos] = gg[q];
                     }
                 }
             }
@@ -1054,8 +1060,8 @@ __global__ __launch_bounds__(256) void rb_chunks_place(const uint32_t* __restric
                 if (pos < cap) {
                     if (tkey) tkey[pos] = row_tile + (uint32_t)c;
                     const int pi = sp[i];
-                    if (keys) tdk[pos] = pk[pi];
-                    tgid[pos] = pg[pi];
+                    if (keys) tpair[pos] = make_uint2(pg[pi], pk[pi]);
+                    else tgid[pos] = pg[pi];
                 }
             }
         }
@@ -1201,7 +1207,7 @@ struct SliceLds {
 template <int NT, int I, int DB, bool kFixInline = false>
 __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t* __restrict__ depth_key,
                                                  uint32_t* __restrict__ gid, SliceLds<NT, I, DB>& lds,
-                                                 bool unordered = false, const uint32_t* __restrict__ pkey = nullptr) {
+                                                 bool unordered = false) {
     constexpr int NWV = NT / 64, BINS = 1 << DB;
     constexpr uint32_t DMASK = BINS - 1u;
     auto& wcnt = lds.wcnt;
@@ -1223,8 +1229,7 @@ __device__ __forceinline__ void radix_sort_slice(const uint2 rg, const uint32_t*
         const int idx = base + r * 64 + lane;
         const bool valid = idx < end;
         val[r] = valid ? gid[rg.x + idx] : 0u;
-        // the placed keys beside the gids (pkey: one coalesced load, not a gather behind the gid's)
-        key[r] = valid ? (pkey ? pkey[rg.x + idx] : depth_key[val[r]]) : 0xFFFFFFFFu;
+        key[r] = valid ? depth_key[val[r]] : 0xFFFFFFFFu;
         if (valid) {
             kor |= key[r];
             kand &= key[r];
@@ -1473,7 +1478,7 @@ __device__ __forceinline__ void wave_bitonic(uint64_t (&v)[E], int lane) {
 template <int E>
 __device__ __forceinline__ void wave_sort_slice(const uint2 rg, const uint32_t* __restrict__ depth_key,
                                                 uint32_t* __restrict__ gid, int lane, uint32_t* xs,
-                                                const uint32_t* __restrict__ pkey = nullptr) {
+                                                const uint2* __restrict__ src = nullptr) {
     const int n = (int)(rg.y - rg.x);
     uint64_t v[E];
 #pragma unroll
@@ -1481,8 +1486,13 @@ __device__ __forceinline__ void wave_sort_slice(const uint2 rg, const uint32_t* 
         const int i = e * 64 + lane;
         uint64_t k = 0x7FFFFFFFFFFFFFFFull;  // padding sorts last (no real key reaches it)
         if (i < n) {
-            const uint32_t g = gid[rg.x + i];
-            k = ((uint64_t)(pkey ? pkey[rg.x + i] : depth_key[g]) << 32) | g;
+            if (src) {  // the placed (gid, key) pairs
+                const uint2 p = src[rg.x + i];
+                k = ((uint64_t)p.y << 32) | p.x;
+            } else {
+                const uint32_t g = gid[rg.x + i];
+                k = ((uint64_t)depth_key[g] << 32) | g;
+            }
         }
         v[e] = k;
     }
@@ -1568,7 +1578,7 @@ __device__ __forceinline__ void wave_bitonic32(uint32_t (&v)[E], int lane) {
 template <int E>
 __device__ __forceinline__ void wave_sort_slice32(const uint2 rg, const uint32_t* __restrict__ depth_key,
                                                   uint32_t* __restrict__ gid, int lane, uint32_t* xs,
-                                                  const uint32_t* __restrict__ pkey = nullptr) {
+                                                  const uint2* __restrict__ src = nullptr) {
     static_assert(64 * E <= (1 << (32 - kWaveKeyBits)), "slice position bits");
     constexpr uint32_t kPos = (1u << (32 - kWaveKeyBits)) - 1u;
     const int n = (int)(rg.y - rg.x);
@@ -1579,7 +1589,7 @@ __device__ __forceinline__ void wave_sort_slice32(const uint2 rg, const uint32_t
         const int i = e * 64 + lane;
         dk[e] = 0u;
         if (i < n) {
-            dk[e] = pkey ? pkey[rg.x + i] : depth_key[gid[rg.x + i]];
+            dk[e] = src ? src[rg.x + i].y : depth_key[gid[rg.x + i]];
             kor |= dk[e];
             kand &= dk[e];
         }
@@ -1608,6 +1618,10 @@ __device__ __forceinline__ void wave_sort_slice32(const uint2 rg, const uint32_t
     // runs of equal truncated keys: the lane holding a run's first entry orders it by the full
     // (depth, gid) key (insertion; the slice's gids are still in place in gid[])
     auto full = [&](uint32_t x) {
+        if (src) {
+            const uint2 p = src[rg.x + (x & kPos)];
+            return ((uint64_t)p.y << 32) | p.x;
+        }
         const uint32_t g = gid[rg.x + (x & kPos)];
         return ((uint64_t)depth_key[g] << 32) | g;
     };
@@ -1645,7 +1659,7 @@ __device__ __forceinline__ void wave_sort_slice32(const uint2 rg, const uint32_t
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (__ballot(longrun)) {  // many entries at one truncated depth: the 64-bit form
-            wave_sort_slice<E>(rg, depth_key, gid, lane, xs, pkey);
+            wave_sort_slice<E>(rg, depth_key, gid, lane, xs, src);
             return;
         }
     }
@@ -1656,7 +1670,8 @@ __device__ __forceinline__ void wave_sort_slice32(const uint2 rg, const uint32_t
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int i = e * 64 + lane;
-        og[e] = i < n ? gid[rg.x + (xs[pad(i)] & kPos)] : 0u;
+        const uint32_t at = rg.x + (xs[pad(i)] & kPos);
+        og[e] = i < n ? (src ? src[at].x : gid[at]) : 0u;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
@@ -1678,7 +1693,7 @@ __global__ __launch_bounds__(256) void tile_depth_wave(const uint2* __restrict__
                                                       const uint32_t* __restrict__ depth_key,
                                                       uint32_t* __restrict__ gid, uint32_t* __restrict__ ovf,
                                                       uint32_t* __restrict__ ovf_count,
-                                                      const uint32_t* __restrict__ pkey) {
+                                                      const uint2* __restrict__ src) {
     __shared__ uint32_t xs_all[4][64 * 16 + 32];
     const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (t >= ntiles) return;
@@ -1687,24 +1702,26 @@ __global__ __launch_bounds__(256) void tile_depth_wave(const uint2* __restrict__
     const int tile = tile0 + t;
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
-    if (n <= 1) return;
-    if (n > 1024) {
-        if (lane == 0) ovf[atomicAdd(ovf_count, 1u)] = (uint32_t)tile;
+    if (n <= 1 || n > 1024) {
+        // src: the later forms sort in place in gid[] -- the slice's gids go there first
+        if (src)
+            for (int i = lane; i < n; i += 64) gid[rg.x + i] = src[rg.x + i].x;
+        if (n > 1 && lane == 0) ovf[atomicAdd(ovf_count, 1u)] = (uint32_t)tile;
         return;
     }
     if (GSR_WAVE_KEY32) {
-        if (n <= 64) wave_sort_slice32<1>(rg, depth_key, gid, lane, xs, pkey);
-        else if (n <= 128) wave_sort_slice32<2>(rg, depth_key, gid, lane, xs, pkey);
-        else if (n <= 256) wave_sort_slice32<4>(rg, depth_key, gid, lane, xs, pkey);
-        else if (n <= 512) wave_sort_slice32<8>(rg, depth_key, gid, lane, xs, pkey);
-        else wave_sort_slice32<16>(rg, depth_key, gid, lane, xs, pkey);
+        if (n <= 64) wave_sort_slice32<1>(rg, depth_key, gid, lane, xs, src);
+        else if (n <= 128) wave_sort_slice32<2>(rg, depth_key, gid, lane, xs, src);
+        else if (n <= 256) wave_sort_slice32<4>(rg, depth_key, gid, lane, xs, src);
+        else if (n <= 512) wave_sort_slice32<8>(rg, depth_key, gid, lane, xs, src);
+        else wave_sort_slice32<16>(rg, depth_key, gid, lane, xs, src);
         return;
     }
-    if (n <= 64) wave_sort_slice<1>(rg, depth_key, gid, lane, xs, pkey);
-    else if (n <= 128) wave_sort_slice<2>(rg, depth_key, gid, lane, xs, pkey);
-    else if (n <= 256) wave_sort_slice<4>(rg, depth_key, gid, lane, xs, pkey);
-    else if (n <= 512) wave_sort_slice<8>(rg, depth_key, gid, lane, xs, pkey);
-    else wave_sort_slice<16>(rg, depth_key, gid, lane, xs, pkey);
+    if (n <= 64) wave_sort_slice<1>(rg, depth_key, gid, lane, xs, src);
+    else if (n <= 128) wave_sort_slice<2>(rg, depth_key, gid, lane, xs, src);
+    else if (n <= 256) wave_sort_slice<4>(rg, depth_key, gid, lane, xs, src);
+    else if (n <= 512) wave_sort_slice<8>(rg, depth_key, gid, lane, xs, src);
+    else wave_sort_slice<16>(rg, depth_key, gid, lane, xs, src);
 }
 
 // The queued slices of 1025 .. 2048 entries, one wave each (a kernel of its own: the 32-entry-per-
@@ -1718,8 +1735,7 @@ __global__ __launch_bounds__(256) void tile_depth_wave_queue(const uint2* __rest
                                                             const uint32_t* __restrict__ ovf,
                                                             const uint32_t* __restrict__ ovf_count,
                                                             uint32_t* __restrict__ ovf2,
-                                                            uint32_t* __restrict__ ovf2_count,
-                                                            const uint32_t* __restrict__ pkey) {
+                                                            uint32_t* __restrict__ ovf2_count) {
     __shared__ uint32_t xs_all[4][64 * 32 + 64];
     const uint32_t cnt = *ovf_count;
     const int lane = threadIdx.x & 63;
@@ -1732,7 +1748,7 @@ __global__ __launch_bounds__(256) void tile_depth_wave_queue(const uint2* __rest
             if (lane == 0) ovf2[atomicAdd(ovf2_count, 1u)] = tile;
             continue;  // wave-uniform
         }
-        wave_sort_slice<32>(rg, depth_key, gid, lane, xs, pkey);
+        wave_sort_slice<32>(rg, depth_key, gid, lane, xs);
     }
 }
 
@@ -1758,7 +1774,7 @@ struct BlockSortLds {
 
 template <int NW>
 __device__ __forceinline__ bool block_sort_slice(const uint2 rg, const uint32_t* __restrict__ depth_key,
-                                                 uint32_t* __restrict__ gid, const uint32_t* __restrict__ pkey,
+                                                 uint32_t* __restrict__ gid, const uint2* __restrict__ src,
                                                  BlockSortLds<NW>& L) {
     constexpr int CAP = NW * 1024, NT = NW * 64;
     constexpr int PB = NW == 2 ? 11 : NW == 4 ? 12 : 13;  // position bits
@@ -1777,7 +1793,7 @@ __device__ __forceinline__ bool block_sort_slice(const uint2 rg, const uint32_t*
         const int i = w * 1024 + e * 64 + lane;
         v[e] = 0u;
         if (i < n) {
-            v[e] = pkey ? pkey[rg.x + i] : depth_key[gid[rg.x + i]];
+            v[e] = src ? src[rg.x + i].y : depth_key[gid[rg.x + i]];
             kor |= v[e];
             kand &= v[e];
         }
@@ -1852,8 +1868,12 @@ __device__ __forceinline__ bool block_sort_slice(const uint2 rg, const uint32_t*
     }
     if (__syncthreads_or(tie)) {  // block-uniform
         auto full = [&](uint32_t x) {
+            if (src) {
+                const uint2 p = src[rg.x + (x & kPos)];
+                return ((uint64_t)p.y << 32) | p.x;
+            }
             const uint32_t g = gid[rg.x + (x & kPos)];
-            return ((uint64_t)(pkey ? pkey[rg.x + (x & kPos)] : depth_key[g]) << 32) | g;
+            return ((uint64_t)depth_key[g] << 32) | g;
         };
         bool longrun = false;
         if (act) {
@@ -1883,16 +1903,19 @@ __device__ __forceinline__ bool block_sort_slice(const uint2 rg, const uint32_t*
         }
         if (__syncthreads_or(longrun)) return false;  // nothing written: the next form sorts it
     }
-    // out in rank order: every thread's reads of the slice's gids complete, block-wide, before the
-    // first store over them
+    // out in rank order (in place without src: every thread's reads of the slice's gids complete,
+    // block-wide, before the first store over them)
     uint32_t og[CAP / NT];
 #pragma unroll
     for (int k = 0; k < CAP / NT; ++k) {
         const int r = k * NT + tid;
-        og[k] = r < n ? gid[rg.x + (xs[blk_pad(r)] & kPos)] : 0u;
+        const uint32_t at = rg.x + (xs[blk_pad(r < n ? r : 0)] & kPos);
+        og[k] = r < n ? (src ? src[at].x : gid[at]) : 0u;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (!src) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
 #pragma unroll
     for (int k = 0; k < CAP / NT; ++k) {
         const int r = k * NT + tid;
@@ -1912,13 +1935,17 @@ __global__ __launch_bounds__(256) void tile_depth_block(const uint2* __restrict_
                                                        const uint32_t* __restrict__ depth_key,
                                                        uint32_t* __restrict__ gid, uint32_t* __restrict__ ovf,
                                                        uint32_t* __restrict__ ovf_count,
-                                                       const uint32_t* __restrict__ pkey) {
+                                                       const uint2* __restrict__ src) {
     __shared__ BlockSortLds<4> lds;
     const int tile = tile0 + blockIdx.x;
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
-    if (n <= 1) return;
-    if (n > 4096 || !block_sort_slice<4>(rg, depth_key, gid, pkey, lds)) {
+    if (n <= 1) {
+        if (n == 1 && src && threadIdx.x == 0) gid[rg.x] = src[rg.x].x;
+        return;
+    }
+    // (the queue reads src too: a handed-on slice is not copied here)
+    if (n > 4096 || !block_sort_slice<4>(rg, depth_key, gid, src, lds)) {
         if (threadIdx.x == 0) ovf[atomicAdd(ovf_count, 1u)] = (uint32_t)tile;
     }
 }
@@ -1933,13 +1960,16 @@ __global__ __launch_bounds__(512) void tile_depth_block_queue(const uint2* __res
                                                              const uint32_t* __restrict__ ovf_count,
                                                              uint32_t* __restrict__ ovf2,
                                                              uint32_t* __restrict__ ovf2_count,
-                                                             const uint32_t* __restrict__ pkey) {
+                                                             const uint2* __restrict__ src) {
     __shared__ BlockSortLds<8> lds;
     if (blockIdx.x >= *ovf_count) return;
     const uint32_t tile = ovf[blockIdx.x];
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
-    if (n > 8192 || !block_sort_slice<8>(rg, depth_key, gid, pkey, lds)) {  // block-uniform
+    if (n > 8192 || !block_sort_slice<8>(rg, depth_key, gid, src, lds)) {  // block-uniform
+        // tile_depth_sort_big sorts in place in gid[]: the slice's gids go there first
+        if (src)
+            for (int i = threadIdx.x; i < n; i += 512) gid[rg.x + i] = src[rg.x + i].x;
         if (threadIdx.x == 0) ovf2[atomicAdd(ovf2_count, 1u)] = tile;
     }
 }
@@ -1949,8 +1979,7 @@ template <int NT, int I, int DB>
 __global__ __launch_bounds__(NT) void tile_depth_radix(const uint2* __restrict__ ranges, int tile0,
                                                       const uint32_t* __restrict__ depth_key,
                                                       uint32_t* __restrict__ gid, uint32_t* __restrict__ ovf,
-                                                      uint32_t* __restrict__ ovf_count, int unordered,
-                                                      const uint32_t* __restrict__ pkey) {
+                                                      uint32_t* __restrict__ ovf_count, int unordered) {
     const int tile = tile0 + blockIdx.x;
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
@@ -1960,7 +1989,7 @@ __global__ __launch_bounds__(NT) void tile_depth_radix(const uint2* __restrict__
         return;
     }
     __shared__ SliceLds<NT, I, DB> lds;
-    radix_sort_slice<NT, I, DB>(rg, depth_key, gid, lds, unordered != 0, pkey);
+    radix_sort_slice<NT, I, DB>(rg, depth_key, gid, lds, unordered != 0);
 }
 
 // The queued (longer) slices: blocks walk the queue; slices longer than NT * I go on to the
@@ -1973,7 +2002,7 @@ __global__ __launch_bounds__(NT) void tile_depth_radix_queue(const uint2* __rest
                                                             const uint32_t* __restrict__ ovf,
                                                             const uint32_t* __restrict__ ovf_count,
                                                             uint32_t* __restrict__ ovf2, uint32_t* __restrict__ ovf2_count,
-                                                            int unordered, const uint32_t* __restrict__ pkey) {
+                                                            int unordered) {
     __shared__ SliceLds<NT, I, DB> lds;
     const uint32_t cnt = *ovf_count;
     for (uint32_t q = blockIdx.x; q < cnt; q += gridDim.x) {
@@ -1983,7 +2012,7 @@ __global__ __launch_bounds__(NT) void tile_depth_radix_queue(const uint2* __rest
             if (threadIdx.x == 0) ovf2[atomicAdd(ovf2_count, 1u)] = tile;
             continue;  // block-uniform
         }
-        radix_sort_slice<NT, I, DB>(rg, depth_key, gid, lds, unordered != 0, pkey);
+        radix_sort_slice<NT, I, DB>(rg, depth_key, gid, lds, unordered != 0);
     }
 }
 
@@ -2195,9 +2224,9 @@ int launch_rb_binning(const uint32_t* tiles, uint4* rect, uint32_t* offsets, int
                       uint32_t* histA, uint32_t* histB, uint32_t* rb_status, uint32_t* pgid, uint32_t* pxr,
                       uint32_t* tkey, uint32_t* tgid, uint2* ranges, long long cap, hipStream_t s,
                       bool rows_counted, const uint32_t* bsum, uint32_t* K_dev, const uint32_t* depth_key,
-                      uint32_t* pkey, uint32_t* tdk) {
+                      uint2* ppair, uint2* tpair) {
     const int R = ty1 - ty0;
-    if (!depth_key || !pkey || !tdk) pkey = tdk = nullptr;
+    if (!depth_key || !ppair || !tpair) ppair = tpair = nullptr;
     if (n <= 0 || R <= 0 || cap <= 0) return 0;  // ranges stay cleared
     if (R > kRbMaxRows || gx > kRbMaxCols || cap >= kRbMaxCap) return (int)hipErrorInvalidValue;
     const int nbA = div_up(n, 256);
@@ -2206,7 +2235,7 @@ int launch_rb_binning(const uint32_t* tiles, uint4* rect, uint32_t* offsets, int
         hipLaunchKernelGGL(rb_rows_count, dim3(nbA), dim3(256), 0, s, tiles, rect, n, ty0, ty1, histA, nbA);
     hipLaunchKernelGGL(rb_colscan, dim3(R), dim3(1024), 0, s, histA, nbA, totA);
     hipLaunchKernelGGL(rb_rows_place, dim3(nbA), dim3(256), 0, s, tiles, rect, offsets, bsum, n, ty0, ty1, histA, totA,
-                       nbA, pgid, pxr, cap, depth_key, pkey);
+                       nbA, pgid, pxr, cap, depth_key, ppair);
     // chunks: at most cap / kRbChunk full ones plus one partial per row; the blocks walk them, so
     // the grid is capped near what the chip holds at once (no tail of empty blocks)
     const int nch_max = div_up(cap, kRbChunk) + R;
@@ -2215,7 +2244,7 @@ int launch_rb_binning(const uint32_t* tiles, uint4* rect, uint32_t* offsets, int
     hipLaunchKernelGGL(rb_tiles_scan, dim3(R), dim3(kRbScanThreads), 0, s, totA, R, gx, ty0, cap, cap, histB,
                        rb_status + 16, rb_status, ranges, K_dev);
     hipLaunchKernelGGL(rb_chunks_place, dim3(gplace), dim3(256), 0, s, pgid, pxr, totA, R, gx, ty0, cap, cap, histB,
-                       tkey, tgid, pkey, tdk);
+                       tkey, tgid, ppair, tpair);
     return (int)hipGetLastError();
 }
 
@@ -2258,6 +2287,13 @@ int launch_duplicate_ranked(const uint32_t* rtiles, const uint4* rrect, uint4* r
     return (int)hipGetLastError();
 }
 
+// the gids of placed (gid, depth key) pairs, for the forms that sort gid[] in place
+__global__ __launch_bounds__(256) void copy_pair_gids(const uint2* __restrict__ src, long long n,
+                                                      uint32_t* __restrict__ gid) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) gid[i] = src[i].x;
+}
+
 // the LDS slice capacity the per-tile sort picks for a mean slice of K / ntiles entries
 static int tile_sort_cap(long long K, int ntiles) {
     const long long mean = ntiles > 0 ? K / ntiles : K;
@@ -2271,7 +2307,7 @@ bool tile_wave_sort_eligible(long long K, int ntiles) { return GSR_TILE_WAVE_SOR
 int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long K, const uint32_t* depth_key,
                            uint32_t* gid, uint32_t* ovf, uint32_t* ovf_count, uint32_t* ovf2, uint32_t* ovf2_count,
                            uint32_t* done, uint32_t* scratch_hi, uint32_t* scratch_lo, hipStream_t s,
-                           bool unordered, const uint32_t* pkey) {
+                           bool unordered, const uint2* src) {
     if (ntiles <= 0 || K <= 0) return 0;
     const int uo = unordered ? 1 : 0;
     // one block per tile holding up to cap entries in LDS, a power of two >= 1.5x the mean slice
@@ -2284,7 +2320,7 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
     // mean slice leaves most tiles within that (the longer ones queue for the LDS forms below)
     if (tile_wave_sort_eligible(K, ntiles)) {
         hipLaunchKernelGGL(tile_depth_wave, dim3(div_up(ntiles, 4)), dim3(256), 0, s, ranges, tile0, ntiles, depth_key,
-                           gid, ovf, ovf_count, pkey);
+                           gid, ovf, ovf_count, src);
         // the slices past one wave's 1024 entries: where the mean is near 1024 (bands), many -- a
         // 2048-entry wave each, the rest on to the LDS form; elsewhere few (none at 1M / 1080p) --
         // all straight to the 1024-thread LDS form, one launch instead of two more near-empty
@@ -2293,7 +2329,7 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
         if (K / ntiles > 900) {
             const int wgrid = ntiles < 2048 ? div_up(ntiles, 4) : 512;
             hipLaunchKernelGGL(tile_depth_wave_queue, dim3(wgrid), dim3(256), 0, s, ranges, depth_key, gid, ovf,
-                               ovf_count, ovf2, ovf2_count, pkey);
+                               ovf_count, ovf2, ovf2_count);
             hipLaunchKernelGGL(tile_depth_sort_big, dim3(bgrid), dim3(1024), 0, s, ranges, depth_key, gid, ovf2,
                                ovf2_count, done, scratch_hi, scratch_lo, uo);
         } else {
@@ -2304,7 +2340,7 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
     } else {
 #define GSR_TILE_RADIX(NT_, I_)                                                                       \
     hipLaunchKernelGGL((tile_depth_radix<NT_, I_, 9>), dim3(ntiles), dim3(NT_), 0, s, ranges, tile0, depth_key, \
-                       gid, ovf, ovf_count, uo, pkey)
+                       gid, ovf, ovf_count, uo)
 #ifndef GSR_BAND_SORT_NT
 #define GSR_BAND_SORT_NT 512
 #endif
@@ -2313,11 +2349,15 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
 #ifndef GSR_FULL_SORT_NT
 #define GSR_FULL_SORT_NT 0
 #endif
+    if (src && !(GSR_TILE_BLOCK_SORT && cap == 4096)) {  // the radix forms sort in place: gids first
+        hipLaunchKernelGGL(copy_pair_gids, dim3(div_up(K, 256)), dim3(256), 0, s, src, K, gid);
+        src = nullptr;
+    }
     if (GSR_TILE_BLOCK_SORT && cap == 4096) {  // deep slices: the block form, then its 8192-entry queue
         hipLaunchKernelGGL(tile_depth_block, dim3(ntiles), dim3(256), 0, s, ranges, tile0, depth_key, gid, ovf,
-                           ovf_count, pkey);
+                           ovf_count, src);
         hipLaunchKernelGGL(tile_depth_block_queue, dim3(ntiles), dim3(512), 0, s, ranges, depth_key, gid, ovf,
-                           ovf_count, ovf2, ovf2_count, pkey);
+                           ovf_count, ovf2, ovf2_count, src);
         const int bgrid = ntiles < 256 ? ntiles : 256;
         hipLaunchKernelGGL(tile_depth_sort_big, dim3(bgrid), dim3(1024), 0, s, ranges, depth_key, gid, ovf2,
                            ovf2_count, done, scratch_hi, scratch_lo, uo);
@@ -2346,7 +2386,7 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
     }
     const int qgrid = ntiles < 512 ? ntiles : 512;
     hipLaunchKernelGGL((tile_depth_radix_queue<512, 16, 8>), dim3(qgrid), dim3(512), 0, s, ranges, depth_key, gid, ovf,
-                       ovf_count, ovf2, ovf2_count, uo, pkey);
+                       ovf_count, ovf2, ovf2_count, uo);
     // slices beyond 8192: the 16384-entry LDS form and the chunked form (tile_depth_sort_big)
     const int bgrid = ntiles < 256 ? ntiles : 256;
     hipLaunchKernelGGL(tile_depth_sort_big, dim3(bgrid), dim3(1024), 0, s, ranges, depth_key, gid, ovf2, ovf2_count,
