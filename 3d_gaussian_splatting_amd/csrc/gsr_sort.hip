@@ -1889,6 +1889,37 @@ __device__ __forceinline__ bool block_sort_slice(const uint2 rg, const uint32_t*
                     longrun = true;
                     continue;
                 }
+                if (end - r <= 4) {
+                    // the common run (2 - 3 entries at 5M / 1080p): its full keys loaded together --
+                    // one global round trip, not one per insertion step -- and a 4-entry network
+                    uint32_t xx[4];
+                    uint64_t fk[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const bool in = r + j < end;
+                        xx[j] = in ? xs[blk_pad(r + j)] : 0u;
+                        fk[j] = in ? full(xx[j]) : ~0ull;
+                    }
+                    auto cx = [&](int a, int b) {
+                        if (fk[b] < fk[a]) {
+                            const uint64_t t = fk[a];
+                            fk[a] = fk[b];
+                            fk[b] = t;
+                            const uint32_t u = xx[a];
+                            xx[a] = xx[b];
+                            xx[b] = u;
+                        }
+                    };
+                    cx(0, 1);
+                    cx(2, 3);
+                    cx(0, 2);
+                    cx(1, 3);
+                    cx(1, 2);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (r + j < end) xs[blk_pad(r + j)] = xx[j];
+                    continue;
+                }
                 for (int a = r + 1; a < end; ++a) {  // insertion by the full (depth, gid) key
                     const uint32_t x = xs[blk_pad(a)];
                     const uint64_t fx = full(x);
@@ -1928,15 +1959,23 @@ __device__ __forceinline__ bool block_sort_slice(const uint2 rg, const uint32_t*
 #ifndef GSR_TILE_BLOCK_SORT
 #define GSR_TILE_BLOCK_SORT 1
 #endif
+// launches of fewer tiles (multi-GPU bands) sort every deep slice with the 8-wave form in one round
+#ifndef GSR_BLOCK8_TILES
+#define GSR_BLOCK8_TILES 4096
+#endif
 
-// One block of four waves per tile of the launch (slices of up to 4096 entries); longer slices, and
-// those with long runs of equal truncated keys, go to the queue `ovf`.
-__global__ __launch_bounds__(256) void tile_depth_block(const uint2* __restrict__ ranges, int tile0,
-                                                       const uint32_t* __restrict__ depth_key,
-                                                       uint32_t* __restrict__ gid, uint32_t* __restrict__ ovf,
-                                                       uint32_t* __restrict__ ovf_count,
-                                                       const uint2* __restrict__ src) {
-    __shared__ BlockSortLds<4> lds;
+// One block of NW waves per tile of the launch (slices of up to NW x 1024 entries); longer slices,
+// and those with long runs of equal truncated keys, go to `ovf`: NW = 4 (full images) hands them to
+// the 8-wave queue below, which reads src too; NW = 8 (band launches, ~1000 tiles: one round of
+// blocks instead of two, the first one's 4096-entry sorts and then the queued longer ones) hands
+// them to tile_depth_sort_big, which sorts in place -- their gids are copied to gid[] first.
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void tile_depth_block(const uint2* __restrict__ ranges, int tile0,
+                                                           const uint32_t* __restrict__ depth_key,
+                                                           uint32_t* __restrict__ gid, uint32_t* __restrict__ ovf,
+                                                           uint32_t* __restrict__ ovf_count,
+                                                           const uint2* __restrict__ src) {
+    __shared__ BlockSortLds<NW> lds;
     const int tile = tile0 + blockIdx.x;
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
@@ -1944,8 +1983,9 @@ __global__ __launch_bounds__(256) void tile_depth_block(const uint2* __restrict_
         if (n == 1 && src && threadIdx.x == 0) gid[rg.x] = src[rg.x].x;
         return;
     }
-    // (the queue reads src too: a handed-on slice is not copied here)
-    if (n > 4096 || !block_sort_slice<4>(rg, depth_key, gid, src, lds)) {
+    if (n > NW * 1024 || !block_sort_slice<NW>(rg, depth_key, gid, src, lds)) {  // block-uniform
+        if (NW == 8 && src)
+            for (int i = threadIdx.x; i < n; i += NW * 64) gid[rg.x + i] = src[rg.x + i].x;
         if (threadIdx.x == 0) ovf[atomicAdd(ovf_count, 1u)] = (uint32_t)tile;
     }
 }
@@ -2353,8 +2393,16 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
         hipLaunchKernelGGL(copy_pair_gids, dim3(div_up(K, 256)), dim3(256), 0, s, src, K, gid);
         src = nullptr;
     }
+    if (GSR_TILE_BLOCK_SORT && cap == 4096 && ntiles < GSR_BLOCK8_TILES) {  // bands: 8 waves per tile
+        hipLaunchKernelGGL(tile_depth_block<8>, dim3(ntiles), dim3(512), 0, s, ranges, tile0, depth_key, gid, ovf2,
+                           ovf2_count, src);
+        const int bgrid = ntiles < 256 ? ntiles : 256;
+        hipLaunchKernelGGL(tile_depth_sort_big, dim3(bgrid), dim3(1024), 0, s, ranges, depth_key, gid, ovf2,
+                           ovf2_count, done, scratch_hi, scratch_lo, uo);
+        return (int)hipGetLastError();
+    }
     if (GSR_TILE_BLOCK_SORT && cap == 4096) {  // deep slices: the block form, then its 8192-entry queue
-        hipLaunchKernelGGL(tile_depth_block, dim3(ntiles), dim3(256), 0, s, ranges, tile0, depth_key, gid, ovf,
+        hipLaunchKernelGGL(tile_depth_block<4>, dim3(ntiles), dim3(256), 0, s, ranges, tile0, depth_key, gid, ovf,
                            ovf_count, src);
         hipLaunchKernelGGL(tile_depth_block_queue, dim3(ntiles), dim3(512), 0, s, ranges, depth_key, gid, ovf,
                            ovf_count, ovf2, ovf2_count, src);
