@@ -304,8 +304,32 @@ __global__ __launch_bounds__(kB) void scan_reduce(const uint32_t* __restrict__ i
 // Exclusive scan of n words in place by one block of 1024 threads, kScanQ contiguous words per
 // thread per round (all of a round's loads issued before its block scan): one load latency and
 // one block scan per 8192 words, not per 1024 (the F2 block sums at 5M: 19.5k words).
-constexpr int kScanQ = 8;
+// Up to kScanQ1 x 1024 words (5M: 19.5k) in one round: Q = ceil(n / 1024) consecutive words per
+// thread, one load latency, one block scan, one store pass (three serial rounds of 8192 took
+// ~7 us each at 5M).
+#ifndef GSR_SCAN_ONE_ROUND
+#define GSR_SCAN_ONE_ROUND 1
+#endif
+constexpr int kScanQ = 8, kScanQ1 = 32;
 __device__ __forceinline__ uint32_t wide_block_scan(uint32_t* __restrict__ a, int n, uint32_t* wsum) {
+    if (GSR_SCAN_ONE_ROUND && n <= 1024 * kScanQ1) {
+        const int Q = (n + 1023) / 1024;
+        const int i0 = (int)threadIdx.x * Q;
+        uint32_t v[kScanQ1], sv = 0;
+#pragma unroll
+        for (int q = 0; q < kScanQ1; ++q) {
+            v[q] = q < Q && i0 + q < n ? a[i0 + q] : 0u;
+            sv += v[q];
+        }
+        uint32_t tot;
+        uint32_t run = block_exclusive_scan(sv, wsum, &tot);
+#pragma unroll
+        for (int q = 0; q < kScanQ1; ++q) {
+            if (q < Q && i0 + q < n) a[i0 + q] = run;
+            run += v[q];
+        }
+        return tot;
+    }
     uint32_t carry = 0;
     for (int base = 0; base < n; base += 1024 * kScanQ) {
         const int i0 = base + (int)threadIdx.x * kScanQ;
@@ -830,7 +854,7 @@ __global__ __launch_bounds__(256) void rb_chunks_count(const uint32_t* __restric
 // pass B, scan: block r scans row r's [column][chunk] counts flat (exclusive), takes the row's
 // global base by a decoupled look-back over the rows before it, and stores global positions in
 // place; then the tile ranges of row r ((0, 0) for an empty tile, as F5 leaves it; clamped to cap).
-constexpr int kRbScanThreads = 1024;
+constexpr int kRbScanThreads = 1024, kRbScanQ = 32;
 // The look-back's status words pack a 30-bit count: the layout word keeps this binning to
 // capacities below 2^30 (gsr_api.cpp expected_layout), so a step within its capacity never
 // counts past it.  A look-back that spins past its bound (never expected) publishes what it has
@@ -871,16 +895,24 @@ __global__ __launch_bounds__(kRbScanThreads) void rb_tiles_scan(const uint32_t* 
     const uint32_t nch = s_row[0], cp = s_row[1];
     uint32_t* const h = histB + (size_t)gx * cp;
     const uint32_t E = (uint32_t)gx * nch;
-    const bool one = E <= 4u * kRbScanThreads;  // the common case: the row in one round, in registers
-    const uint32_t i0 = 4 * tid;
-    uint32_t cnts[4] = {0u, 0u, 0u, 0u}, excl = 0, carry = 0;
+    // the common case: the row's counts in registers, Q consecutive ones per thread (up to
+    // kRbScanQ x 1024: 5M / 1080p rows hold ~26k), one block scan and one write of the final
+    // positions -- a row's scan was serial rounds of 4096 and a second pass before (22 us at 5M)
+    const uint32_t Q = (E + kRbScanThreads - 1) / kRbScanThreads;
+    const bool one = Q <= (uint32_t)(GSR_SCAN_ONE_ROUND ? kRbScanQ : 4);
+    const uint32_t i0 = Q * tid;
+    uint32_t cnts[kRbScanQ], excl = 0, carry = 0;
     if (one) {
+        uint32_t sv = 0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) cnts[q] = i0 + q < E ? h[i0 + q] : 0u;
-        excl = block_exclusive_scan(cnts[0] + cnts[1] + cnts[2] + cnts[3], wsum, &carry);
+        for (int q = 0; q < kRbScanQ; ++q) {
+            cnts[q] = (uint32_t)q < Q && i0 + q < E ? h[i0 + q] : 0u;
+            sv += cnts[q];
+        }
+        excl = block_exclusive_scan(sv, wsum, &carry);
     } else {
         for (uint32_t base = 0; base < E; base += 4 * kRbScanThreads) {
-            const uint32_t j0 = base + i0;
+            const uint32_t j0 = base + 4 * tid;  // (rows past kRbScanQ x 1024 counts: rounds of 4 per thread)
             uint32_t v[4], sv = 0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -934,12 +966,14 @@ __global__ __launch_bounds__(kRbScanThreads) void rb_tiles_scan(const uint32_t* 
     const uint32_t rowbase = s_base;
     if (one) {
         uint32_t run = rowbase + excl;
+        uint32_t c = i0 / (nch ? nch : 1u), k = i0 - c * nch;  // column and chunk of element i0
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            if (i0 + q < E) {
+        for (int q = 0; q < kRbScanQ; ++q) {
+            if ((uint32_t)q < Q && i0 + q < E) {
                 h[i0 + q] = run;
-                if ((i0 + q) % nch == 0) tstart[(i0 + q) / nch] = run;
+                if (k == 0) tstart[c] = run;
                 run += cnts[q];
+                if (++k == nch) k = 0, ++c;
             }
         }
     } else {
