@@ -1798,11 +1798,18 @@ __global__ __launch_bounds__(256) void tile_depth_wave_queue(const uint2* __rest
 // (depth, gid) order from the full keys by the thread holding a run's first entry; a run longer
 // than kWaveRunMax (depths clustered inside one truncated step) leaves the slice untouched and
 // hands the tile on (`false`) to the next queue, whose forms sort every bit.
-constexpr int kBlkE = 16;  // entries per lane
+// E: entries per lane (16: 1024 per wave; 8: 512 per wave, twice the waves per slice and one more
+// level of LDS merges, for a shorter chain per block)
+#ifndef GSR_BLOCK_E
+#define GSR_BLOCK_E 16
+#endif
+constexpr int kBlkE = GSR_BLOCK_E;
 __host__ __device__ constexpr int blk_pad(int i) { return i + (i >> 5); }
+__host__ __device__ constexpr int ilog2c(int x) { return x <= 1 ? 0 : 1 + ilog2c(x >> 1); }
+constexpr int kBlkW = 4096 / (64 * kBlkE), kBlkQW = 8192 / (64 * kBlkE);  // waves: <= 4096 / <= 8192
 template <int NW>
 struct BlockSortLds {
-    uint32_t xs[blk_pad(NW * 1024)];
+    uint32_t xs[blk_pad(NW * 64 * kBlkE)];
     uint32_t red[2][NW];
 };
 
@@ -1810,21 +1817,23 @@ template <int NW>
 __device__ __forceinline__ bool block_sort_slice(const uint2 rg, const uint32_t* __restrict__ depth_key,
                                                  uint32_t* __restrict__ gid, const uint2* __restrict__ src,
                                                  BlockSortLds<NW>& L) {
-    constexpr int CAP = NW * 1024, NT = NW * 64;
-    constexpr int PB = NW == 2 ? 11 : NW == 4 ? 12 : 13;  // position bits
+    constexpr int WE = 64 * kBlkE;  // entries per wave
+    constexpr int CAP = NW * WE, NT = NW * 64;
+    constexpr int PB = ilog2c(CAP);  // position bits
     constexpr int KB = 32 - PB;                           // truncated depth bits
     static_assert((1 << PB) == CAP, "position bits");
     constexpr uint32_t kPos = CAP - 1u;
     const int n = (int)(rg.y - rg.x);
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     // active waves: the power of two whose runs cover the slice (the rest only meet the barriers)
-    const int nwa = n <= 1024 ? 1 : n <= 2048 ? 2 : n <= 4096 ? 4 : 8;
+    int nwa = 1;
+    while (nwa * WE < n) nwa <<= 1;
     const bool act = w < nwa;
     uint32_t v[kBlkE];
     uint32_t kor = 0u, kand = ~0u;
 #pragma unroll
     for (int e = 0; e < kBlkE; ++e) {
-        const int i = w * 1024 + e * 64 + lane;
+        const int i = w * WE + e * 64 + lane;
         v[e] = 0u;
         if (i < n) {
             v[e] = src ? src[rg.x + i].y : depth_key[gid[rg.x + i]];
@@ -1857,13 +1866,13 @@ __device__ __forceinline__ bool block_sort_slice(const uint2 rg, const uint32_t*
     const int sh = top > KB ? top - KB : 0;
 #pragma unroll
     for (int e = 0; e < kBlkE; ++e) {
-        const int i = w * 1024 + e * 64 + lane;
+        const int i = w * WE + e * 64 + lane;
         // padding ~0 sorts last: a real key reaches it only at position CAP - 1, i.e. n = CAP
         v[e] = i < n ? (((v[e] >> sh) & ((1u << KB) - 1u)) << PB) | (uint32_t)i : ~0u;
     }
-    if (act) wave_bitonic32<kBlkE, 2>(v, lane);  // each active wave's 1024 entries, ascending
-    // merges of the waves' runs: entry i = w 1024 + 16 lane + e
-    const int i0 = w * 1024 + lane * kBlkE;
+    if (act) wave_bitonic32<kBlkE, 2>(v, lane);  // each active wave's WE entries, ascending
+    // merges of the waves' runs: entry i = w WE + E lane + e
+    const int i0 = w * WE + lane * kBlkE;
     uint32_t* const xs = L.xs;
     auto lds_stage = [&](int x, int h) {  // i <-> i ^ x, the lower of the pair (i & h == 0) keeps the min
         if (act) {
@@ -1872,7 +1881,7 @@ __device__ __forceinline__ bool block_sort_slice(const uint2 rg, const uint32_t*
         }
         __syncthreads();
         if (act) {
-            const bool hi = (i0 & h) != 0;  // the same for the lane's 16 entries (h >= 1024)
+            const bool hi = (i0 & h) != 0;  // the same for the lane's E entries (h >= WE)
 #pragma unroll
             for (int e = 0; e < kBlkE; ++e) {
                 const uint32_t o = xs[blk_pad((i0 + e) ^ x)];
@@ -1881,10 +1890,10 @@ __device__ __forceinline__ bool block_sort_slice(const uint2 rg, const uint32_t*
         }
         __syncthreads();  // xs is rewritten by the next stage
     };
-    for (int K = 2048; K <= nwa * 1024; K <<= 1) {  // block-uniform
+    for (int K = 2 * WE; K <= nwa * WE; K <<= 1) {  // block-uniform
         lds_stage(K - 1, K >> 1);                     // the mirror stage
-        for (int J = K >> 2; J >= 1024; J >>= 1) lds_stage(J, J);
-        if (act) wave_half_cleaners32<kBlkE, 512>(v, lane);
+        for (int J = K >> 2; J >= WE; J >>= 1) lds_stage(J, J);
+        if (act) wave_half_cleaners32<kBlkE, WE / 2>(v, lane);
     }
     // the sorted keys by rank, then the runs of equal truncated keys
     if (act) {
@@ -2017,8 +2026,8 @@ __global__ __launch_bounds__(NW * 64) void tile_depth_block(const uint2* __restr
         if (n == 1 && src && threadIdx.x == 0) gid[rg.x] = src[rg.x].x;
         return;
     }
-    if (n > NW * 1024 || !block_sort_slice<NW>(rg, depth_key, gid, src, lds)) {  // block-uniform
-        if (NW == 8 && src)
+    if (n > NW * 64 * kBlkE || !block_sort_slice<NW>(rg, depth_key, gid, src, lds)) {  // block-uniform
+        if (NW == kBlkQW && src)
             for (int i = threadIdx.x; i < n; i += NW * 64) gid[rg.x + i] = src[rg.x + i].x;
         if (threadIdx.x == 0) ovf[atomicAdd(ovf_count, 1u)] = (uint32_t)tile;
     }
@@ -2027,7 +2036,7 @@ __global__ __launch_bounds__(NW * 64) void tile_depth_block(const uint2* __restr
 // The queued slices of up to 8192 entries, eight waves per block, one queued tile per block (the
 // grid covers every tile; blocks past the queue's length exit at once); longer ones and those with
 // long truncated-key runs go on to `ovf2` (tile_depth_sort_big sorts every bit).
-__global__ __launch_bounds__(512) void tile_depth_block_queue(const uint2* __restrict__ ranges,
+__global__ __launch_bounds__(64 * kBlkQW) void tile_depth_block_queue(const uint2* __restrict__ ranges,
                                                              const uint32_t* __restrict__ depth_key,
                                                              uint32_t* __restrict__ gid,
                                                              const uint32_t* __restrict__ ovf,
@@ -2035,15 +2044,15 @@ __global__ __launch_bounds__(512) void tile_depth_block_queue(const uint2* __res
                                                              uint32_t* __restrict__ ovf2,
                                                              uint32_t* __restrict__ ovf2_count,
                                                              const uint2* __restrict__ src) {
-    __shared__ BlockSortLds<8> lds;
+    __shared__ BlockSortLds<kBlkQW> lds;
     if (blockIdx.x >= *ovf_count) return;
     const uint32_t tile = ovf[blockIdx.x];
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
-    if (n > 8192 || !block_sort_slice<8>(rg, depth_key, gid, src, lds)) {  // block-uniform
+    if (n > 8192 || !block_sort_slice<kBlkQW>(rg, depth_key, gid, src, lds)) {  // block-uniform
         // tile_depth_sort_big sorts in place in gid[]: the slice's gids go there first
         if (src)
-            for (int i = threadIdx.x; i < n; i += 512) gid[rg.x + i] = src[rg.x + i].x;
+            for (int i = threadIdx.x; i < n; i += 64 * kBlkQW) gid[rg.x + i] = src[rg.x + i].x;
         if (threadIdx.x == 0) ovf2[atomicAdd(ovf2_count, 1u)] = tile;
     }
 }
@@ -2428,7 +2437,7 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
         src = nullptr;
     }
     if (GSR_TILE_BLOCK_SORT && cap == 4096 && ntiles < GSR_BLOCK8_TILES) {  // bands: 8 waves per tile
-        hipLaunchKernelGGL(tile_depth_block<8>, dim3(ntiles), dim3(512), 0, s, ranges, tile0, depth_key, gid, ovf2,
+        hipLaunchKernelGGL(tile_depth_block<kBlkQW>, dim3(ntiles), dim3(64 * kBlkQW), 0, s, ranges, tile0, depth_key, gid, ovf2,
                            ovf2_count, src);
         const int bgrid = ntiles < 256 ? ntiles : 256;
         hipLaunchKernelGGL(tile_depth_sort_big, dim3(bgrid), dim3(1024), 0, s, ranges, depth_key, gid, ovf2,
@@ -2436,9 +2445,9 @@ int launch_tile_depth_sort(const uint2* ranges, int tile0, int ntiles, long long
         return (int)hipGetLastError();
     }
     if (GSR_TILE_BLOCK_SORT && cap == 4096) {  // deep slices: the block form, then its 8192-entry queue
-        hipLaunchKernelGGL(tile_depth_block<4>, dim3(ntiles), dim3(256), 0, s, ranges, tile0, depth_key, gid, ovf,
+        hipLaunchKernelGGL(tile_depth_block<kBlkW>, dim3(ntiles), dim3(64 * kBlkW), 0, s, ranges, tile0, depth_key, gid, ovf,
                            ovf_count, src);
-        hipLaunchKernelGGL(tile_depth_block_queue, dim3(ntiles), dim3(512), 0, s, ranges, depth_key, gid, ovf,
+        hipLaunchKernelGGL(tile_depth_block_queue, dim3(ntiles), dim3(64 * kBlkQW), 0, s, ranges, depth_key, gid, ovf,
                            ovf_count, ovf2, ovf2_count, src);
         const int bgrid = ntiles < 256 ? ntiles : 256;
         hipLaunchKernelGGL(tile_depth_sort_big, dim3(bgrid), dim3(1024), 0, s, ranges, depth_key, gid, ovf2,
