@@ -657,6 +657,11 @@ __global__ __launch_bounds__(256) void rank_payload_kernel(const uint32_t* __res
 // it too), outside presort mode, below kRbMaxCap instances (gsr_api.cpp expected_layout; recorded
 // in gsr_buffers.layout).
 constexpr int kRbChunk = kRbChunkPairs;  // pairs per pass-B block (4 per thread)
+// GSR_RB_STAGE32 1: pass B stages (pair index | column << 16) as one word per instance (no
+// sub-dword LDS stores from neighbouring lanes into one dword)
+#ifndef GSR_RB_STAGE32
+#define GSR_RB_STAGE32 1
+#endif
 static_assert(kRbChunk % 256 == 0 && kRbMaxRows == 256 && kRbMaxCols == 256, "one row / column per thread");
 constexpr int kRbStageA = 2048;  // LDS staging (pairs) of a pass-A block (~720 at 1M / 1080p)
 constexpr int kRbStage = 4096;   // LDS staging (instances) of a pass-B block (~2800 at 1M / 1080p)
@@ -1008,8 +1013,12 @@ __global__ __launch_bounds__(256) void rb_chunks_place(const uint32_t* __restric
     __shared__ uint32_t lb[kRbMaxCols];   // staging start of column c
     __shared__ uint32_t gb[kRbMaxCols];   // global position of the chunk's first instance of column c
     __shared__ uint32_t pg[kRbChunk], pk[kRbChunk];  // the chunk's pairs: gid, depth key
+#if GSR_RB_STAGE32
+    __shared__ uint32_t spc[kRbStage];                // staged instance: pair index | column << 16
+#else
     __shared__ uint16_t sp[kRbStage];                 // staged instance: its pair (index in the chunk)
     __shared__ uint8_t sc[kRbStage];
+#endif
     __shared__ uint32_t wsum[kWaves];
     static_assert(kRbChunk <= 65536, "u16 pair index");
     const int tid = threadIdx.x;
@@ -1074,8 +1083,12 @@ __global__ __launch_bounds__(256) void rb_chunks_place(const uint32_t* __restric
             for (uint32_t c = xr[q] & 0xFFFFu; c < (xr[q] >> 16); ++c) {
                 const uint32_t k = atomicAdd(&cnt[c], 1u);
                 if (staged) {
+#if GSR_RB_STAGE32
+                    spc[lb[c] + k] = (uint32_t)(q * 256 + tid) | (c << 16);
+#else
                     sp[lb[c] + k] = (uint16_t)(q * 256 + tid);
                     sc[lb[c] + k] = (uint8_t)c;
+#endif
                 } else {
                     const long long pos = (long long)gb[c] + k;
                     if (pos < cap) {
@@ -1089,11 +1102,20 @@ __global__ __launch_bounds__(256) void rb_chunks_place(const uint32_t* __restric
         if (staged) {
             __syncthreads();
             for (int i = tid; i < (int)tot; i += 256) {
+#if GSR_RB_STAGE32
+                const uint32_t pc = spc[i];
+                const int c = (int)(pc >> 16);
+#else
                 const int c = sc[i];
+#endif
                 const long long pos = (long long)gb[c] + ((uint32_t)i - lb[c]);
                 if (pos < cap) {
                     if (tkey) tkey[pos] = row_tile + (uint32_t)c;
+#if GSR_RB_STAGE32
+                    const int pi = (int)(pc & 0xFFFFu);
+#else
                     const int pi = sp[i];
+#endif
                     if (keys) tpair[pos] = make_uint2(pg[pi], pk[pi]);
                     else tgid[pos] = pg[pi];
                 }
