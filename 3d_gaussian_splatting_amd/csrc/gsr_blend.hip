@@ -173,8 +173,16 @@ __device__ __forceinline__ float pair_alpha_keep(float e, float L, float& oG, bo
 #ifndef GSR_F6_BATCH4
 #define GSR_F6_BATCH4 256
 #endif
+#ifndef GSR_F6_GID_AHEAD
+#define GSR_F6_GID_AHEAD 1
+#endif
+// two-wave (full-image) F6 held to 8 waves per SIMD (64 VGPRs): the gid-ahead register would
+// otherwise take it to 65 and 7 waves
+#ifndef GSR_F6_WPE
+#define GSR_F6_WPE 8
+#endif
 template <int NW>
-__global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom geo,
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW == 2 ? GSR_F6_WPE : 1))) void blend_forward_kernel(const BlendGeom geo,
                                                                 const uint2* __restrict__ ranges,
                                                                 const uint32_t* __restrict__ sorted_gid,
                                                                 const float4* __restrict__ rec,
@@ -266,6 +274,9 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
 #else
     constexpr int quota = kCW;
 #endif
+    // GSR_F6_GID_AHEAD: each batch's gid is loaded one batch ahead (one VGPR), so a batch start
+    // waits for its record loads only, not for the gid load they depend on as well
+    uint32_t g_next = GSR_F6_GID_AHEAD && tid < BATCH && tid < n ? sorted_gid[range.x + tid] : 0u;
     for (int base = 0; base < n; base += BATCH) {
         uint32_t live = 0;
 #pragma unroll
@@ -278,7 +289,8 @@ __global__ __launch_bounds__(64 * NW) void blend_forward_kernel(const BlendGeom 
         }
 #endif
         if (tid < BATCH && base + tid < n) {
-            const uint32_t g = sorted_gid[range.x + base + tid];
+            const uint32_t g = GSR_F6_GID_AHEAD ? g_next : sorted_gid[range.x + base + tid];
+            if (GSR_F6_GID_AHEAD && base + BATCH + tid < n) g_next = sorted_gid[range.x + base + BATCH + tid];
             const float4* r = rec + 3 * (size_t)g;
             const float4 r0 = r[0], r1 = r[1], r2 = r[2];
             srec[3 * tid + 0] = r0;
