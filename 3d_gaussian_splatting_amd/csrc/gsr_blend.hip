@@ -527,6 +527,11 @@ __device__ __forceinline__ void park_flush(const float* qpark, const uint32_t* s
 #ifndef GSR_B1_PAIRS
 #define GSR_B1_PAIRS 0
 #endif
+// GSR_B1_GID_WIN: B1 loads the batch window's gids with its mask bytes (one 16-B load per lane),
+// so a batch's record loads do not wait on a gid load first
+#ifndef GSR_B1_GID_WIN
+#define GSR_B1_GID_WIN 1
+#endif
 constexpr int kB1Win = GSR_B1_WIN;
 static_assert(kB1Win == 4 || kB1Win == 16, "B1 window: 4 or 16 mask bytes per lane");
 // SPW: the 16x4 stripes one wave owns.  4 (full images): one wave per (tile, chunk) and one
@@ -563,6 +568,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PF ? 4 : (SP
         float qpark[kPark * kParkSlot];    // [slot][quad][9 of 12]
         uint32_t sidx[64];                 // the batch's entries (list offsets), in list order
         uint32_t smv[64];                  // and their stripe masks
+#if GSR_B1_GID_WIN
+        uint32_t sgd[64];                  // and their gids (loaded with the window's mask bytes)
+#endif
     } lds;
     float4* const srec = lds.srec;
     uint32_t* const sjl = lds.sjl;
@@ -663,6 +671,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PF ? 4 : (SP
         } else {
             wd[0] = *reinterpret_cast<const uint32_t*>(mk + a0 + 4 * lane);
         }
+#if GSR_B1_GID_WIN
+        static_assert(kB1Win == 4, "gids with the mask window: 4 entries per lane");
+        // the window's gids beside its mask bytes (one 16-B load per lane; the list array is
+        // followed by the rest of the binning buffer, so the window's tail past the list is
+        // readable and never used): the batch's record loads then wait for no gid load
+        const uint4 gw = *reinterpret_cast<const uint4*>(sorted_gid + a0 + 4 * lane);
+        const uint32_t gwa[4] = {gw.x, gw.y, gw.z, gw.w};
+#endif
         uint32_t vis = 0;
 #pragma unroll
         for (int i = 0; i < kB1Win; ++i) {
@@ -687,6 +703,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PF ? 4 : (SP
                 if (pos < 64u) {
                     lds.sidx[pos] = a0 + kB1Win * lane + i - range.x;
                     lds.smv[pos] = (wd[i >> 2] >> (8 * (i & 3))) & 0xFu;
+#if GSR_B1_GID_WIN
+                    lds.sgd[pos] = gwa[i];
+#endif
                 }
                 ++pos;
             }
@@ -700,7 +719,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PF ? 4 : (SP
         }
         uint32_t jl = 0, smask = 0;
         if (lane < cnt) {
+#if GSR_B1_GID_WIN
+            const uint32_t g = lds.sgd[lane];
+#else
             const uint32_t g = sorted_gid[range.x + lds.sidx[lane]];
+#endif
             const uint4 rr = rect[g];
             const int minx = rr.x & 0xFFFF, miny = rr.x >> 16, maxx = rr.y & 0xFFFF;
             const int y0 = miny > geo.ty0 ? miny : geo.ty0;
