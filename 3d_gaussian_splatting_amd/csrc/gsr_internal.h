@@ -101,6 +101,11 @@ constexpr int kMaxViews = 8;  // gsr_forward_views: views per call (= GSR_MAX_VI
 #define GSR_RB_DEEP 1
 #endif
 constexpr int kRbMaxRows = 256, kRbMaxCols = 256, kRbChunkPairs = 1024;
+// the binning's row scan splits a row into at most this many column partitions (gsr_sort.hip)
+#ifndef GSR_RB_SCAN_SPLIT
+#define GSR_RB_SCAN_SPLIT 16
+#endif
+constexpr int kRbScanSplit = GSR_RB_SCAN_SPLIT;
 constexpr long long kRbMaxCap = 1LL << 30;  // the look-back's 30-bit counts (rb_tiles_scan)
 // gsr_buffers.layout (set by the forward, checked by every later use of the buffers): the tag
 // and the binning in use (gsr.h GSR_LAYOUT_*)
@@ -229,7 +234,7 @@ struct ImgLayout {
         size_t pix = (size_t)W * H;
         ranges = take(8 * tiles);
         counters = take(4 * (2 * kCountSlots + 16));  // ranges, counters, rb_status and done are
-        rb_status = take(4 * (16 + kRbMaxRows));       // contiguous: one memset clears them
+        rb_status = take(4 * (16 + kRbMaxRows * kRbScanSplit));  // contiguous: one memset clears them
         done = take(4 * tiles);  // (rb_status: the row-bucketed binning's ticket + look-back words;
                                  // done: chunks sorted per queued tile)
         ovf = take(4 * tiles);   // tiles the per-tile depth sort hands to its larger

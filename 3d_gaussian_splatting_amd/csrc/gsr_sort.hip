@@ -856,9 +856,13 @@ __global__ __launch_bounds__(256) void rb_chunks_count(const uint32_t* __restric
     }
 }
 
-// pass B, scan: block r scans row r's [column][chunk] counts flat (exclusive), takes the row's
-// global base by a decoupled look-back over the rows before it, and stores global positions in
-// place; then the tile ranges of row r ((0, 0) for an empty tile, as F5 leaves it; clamped to cap).
+// pass B, scan: the [column][chunk] counts of every row, flat, in R x G partitions -- partition
+// p = r G + g holds columns [g gx / G, (g + 1) gx / G) of row r, contiguous in the flat order.
+// Each block scans one partition (exclusive), takes its global base by a decoupled look-back over
+// the partitions before it (in dispatch order: a ticket), and stores global positions in place;
+// then the tile ranges of its columns ((0, 0) for an empty tile, as F5 leaves it; clamped to
+// cap).  G > 1 spreads a row over several CUs: a band of 8 tile rows was 8 blocks on the chip
+// (~22 us at 5M, the same as 68 rows of the full image).
 constexpr int kRbScanThreads = 1024, kRbScanQ = 32;
 // The look-back's status words pack a 30-bit count: the layout word keeps this binning to
 // capacities below 2^30 (gsr_api.cpp expected_layout), so a step within its capacity never
@@ -871,16 +875,17 @@ __global__ __launch_bounds__(kRbScanThreads) void rb_tiles_scan(const uint32_t* 
                                                                 uint32_t* __restrict__ status,
                                                                 uint32_t* __restrict__ ticket,
                                                                 uint2* __restrict__ ranges,
-                                                                uint32_t* __restrict__ K_dev) {
+                                                                uint32_t* __restrict__ K_dev, int G) {
     __shared__ uint32_t wsum[kRbScanThreads / 64];
     __shared__ uint32_t tstart[kRbMaxCols];
     __shared__ uint32_t s_row[2];
-    __shared__ int s_r;
+    __shared__ int s_p;
     __shared__ uint32_t s_base;
     const int tid = threadIdx.x, lane = tid & 63;
-    if (tid == 0) s_r = (int)atomicAdd(ticket, 1u);  // rows in dispatch order (the look-back's progress)
+    if (tid == 0) s_p = (int)atomicAdd(ticket, 1u);  // partitions in dispatch order (the look-back's progress)
     __syncthreads();
-    const int r = s_r;
+    const int p = s_p, r = p / G, gi = p - r * G;
+    const int c0 = gi * gx / G, c1 = (gi + 1) * gx / G;  // this partition's columns
     // the row's chunks, as rb_rows_table numbers them
     {
         const uint32_t ta = tid < R ? totA[tid] : 0u;
@@ -898,11 +903,10 @@ __global__ __launch_bounds__(kRbScanThreads) void rb_tiles_scan(const uint32_t* 
         __syncthreads();
     }
     const uint32_t nch = s_row[0], cp = s_row[1];
-    uint32_t* const h = histB + (size_t)gx * cp;
-    const uint32_t E = (uint32_t)gx * nch;
-    // the common case: the row's counts in registers, Q consecutive ones per thread (up to
-    // kRbScanQ x 1024: 5M / 1080p rows hold ~26k), one block scan and one write of the final
-    // positions -- a row's scan was serial rounds of 4096 and a second pass before (22 us at 5M)
+    uint32_t* const h = histB + (size_t)gx * cp + (size_t)c0 * nch;  // the partition's counts
+    const uint32_t E = (uint32_t)(c1 - c0) * nch;
+    // the common case: the partition's counts in registers, Q consecutive ones per thread (up to
+    // kRbScanQ x 1024), one block scan and one write of the final positions
     const uint32_t Q = (E + kRbScanThreads - 1) / kRbScanThreads;
     const bool one = Q <= (uint32_t)(GSR_SCAN_ONE_ROUND ? kRbScanQ : 4);
     const uint32_t i0 = Q * tid;
@@ -917,7 +921,7 @@ __global__ __launch_bounds__(kRbScanThreads) void rb_tiles_scan(const uint32_t* 
         excl = block_exclusive_scan(sv, wsum, &carry);
     } else {
         for (uint32_t base = 0; base < E; base += 4 * kRbScanThreads) {
-            const uint32_t j0 = base + 4 * tid;  // (rows past kRbScanQ x 1024 counts: rounds of 4 per thread)
+            const uint32_t j0 = base + 4 * tid;  // (partitions past kRbScanQ x 1024 counts: rounds of 4 per thread)
             uint32_t v[4], sv = 0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -928,20 +932,20 @@ __global__ __launch_bounds__(kRbScanThreads) void rb_tiles_scan(const uint32_t* 
             uint32_t run = carry + block_exclusive_scan(sv, wsum, &tot);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                if (j0 + q < E) h[j0 + q] = run;  // row-relative for now
+                if (j0 + q < E) h[j0 + q] = run;  // partition-relative for now
                 run += v[q];
             }
             carry += tot;
         }
     }
-    // look-back (wave 0): the instances of rows before r
+    // look-back (wave 0): the instances of the partitions before p
     if (tid < 64) {
         uint32_t excl = 0;
-        if (r == 0) {
+        if (p == 0) {
             if (lane == 0) __hip_atomic_store(status, kRbInc | carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            if (lane == 0) __hip_atomic_store(status + r, kRbAgg | carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int pos = r - 1;
+            if (lane == 0) __hip_atomic_store(status + p, kRbAgg | carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int pos = p - 1;
             uint32_t spins = 0;
             while (true) {
                 const int idx = pos - lane;
@@ -962,34 +966,35 @@ __global__ __launch_bounds__(kRbScanThreads) void rb_tiles_scan(const uint32_t* 
                 if (inc || spins > (1u << 24)) break;
                 pos -= 64;
             }
-            if (lane == 0) __hip_atomic_store(status + r, kRbInc | (excl + carry), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) __hip_atomic_store(status + p, kRbInc | (excl + carry), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (spins > (1u << 24) && lane == 0 && K_dev) *K_dev = 0xFFFFFFFFu;  // the step is void
         }
         if (lane == 0) s_base = excl;
     }
     __syncthreads();
-    const uint32_t rowbase = s_base;
+    const uint32_t pbase = s_base;  // the global position of the partition's first instance
     if (one) {
-        uint32_t run = rowbase + excl;
-        uint32_t c = i0 / (nch ? nch : 1u), k = i0 - c * nch;  // column and chunk of element i0
+        uint32_t run = pbase + excl;
+        uint32_t c = i0 / (nch ? nch : 1u), k = i0 - c * nch;  // column (partition-relative) and chunk of i0
 #pragma unroll
         for (int q = 0; q < kRbScanQ; ++q) {
             if ((uint32_t)q < Q && i0 + q < E) {
                 h[i0 + q] = run;
-                if (k == 0) tstart[c] = run;
+                if (k == 0) tstart[c0 + c] = run;
                 run += cnts[q];
                 if (++k == nch) k = 0, ++c;
             }
         }
     } else {
-        for (uint32_t i = tid; i < E; i += kRbScanThreads) h[i] += rowbase;
+        for (uint32_t i = tid; i < E; i += kRbScanThreads) h[i] += pbase;
         __syncthreads();
-        if (tid < gx && nch) tstart[tid] = h[(size_t)tid * nch];
+        if (tid >= c0 && tid < c1 && nch) tstart[tid] = h[(size_t)(tid - c0) * nch];
     }
     __syncthreads();
-    // tile c of the row: [its first chunk's base, the next tile's)
-    if (tid < gx) {
-        const uint32_t a = nch ? tstart[tid] : rowbase, e = tid + 1 < gx && nch ? tstart[tid + 1] : rowbase + carry;
+    // tile c of the partition: [its first chunk's base, the next tile's); the partition's last
+    // tile ends where the next partition starts (flat order)
+    if (tid >= c0 && tid < c1) {
+        const uint32_t a = nch ? tstart[tid] : pbase, e = tid + 1 < c1 && nch ? tstart[tid + 1] : pbase + carry;
         const long long a2 = a < cap ? a : cap, e2 = e < cap ? e : cap;
         ranges[(size_t)(ty0 + r) * gx + tid] = e2 > a2 ? make_uint2((uint32_t)a2, (uint32_t)e2) : make_uint2(0u, 0u);
     }
@@ -2346,8 +2351,11 @@ int launch_rb_binning(const uint32_t* tiles, uint4* rect, uint32_t* offsets, int
     const int nch_max = div_up(cap, kRbChunk) + R;
     const int gcount = nch_max < 2048 ? nch_max : 2048, gplace = nch_max < 1280 ? nch_max : 1280;
     hipLaunchKernelGGL(rb_chunks_count, dim3(gcount), dim3(256), 0, s, pxr, totA, R, gx, cap, histB);
-    hipLaunchKernelGGL(rb_tiles_scan, dim3(R), dim3(kRbScanThreads), 0, s, totA, R, gx, ty0, cap, cap, histB,
-                       rb_status + 16, rb_status, ranges, K_dev);
+    // partitions per row: enough to spread a band's few rows over the chip, at most kRbScanSplit
+    int G = kRbScanSplit < 256 / R ? kRbScanSplit : 256 / R;
+    G = G < 1 ? 1 : G > gx ? gx : G;
+    hipLaunchKernelGGL(rb_tiles_scan, dim3(R * G), dim3(kRbScanThreads), 0, s, totA, R, gx, ty0, cap, cap, histB,
+                       rb_status + 16, rb_status, ranges, K_dev, G);
     hipLaunchKernelGGL(rb_chunks_place, dim3(gplace), dim3(256), 0, s, pgid, pxr, totA, R, gx, ty0, cap, cap, histB,
                        tkey, tgid, ppair, tpair);
     return (int)hipGetLastError();
