@@ -787,13 +787,11 @@ void ShardStep::push_status() {
     TORCH_CHECK(pending_.size() < p.ring.size(), "ShardStep: overflow ring full");
     const int slot = ring_next_;
     ring_next_ = (ring_next_ + 1) % (int)p.ring.size();
-    // every rank's footer (a strided column block of the gathered rows) straight into the pinned
-    // slot: one 2-D copy, not a gather kernel into a contiguous temporary and then a copy
-    const size_t fb = (size_t)foot_words_ * sizeof(int32_t);
-    const hipError_t e = hipMemcpy2DAsync(p.ring[slot].data_ptr<int32_t>(), fb, p.gathered.data_ptr<float>() + p.status_off,
-                                          (size_t)p.mine_floats * sizeof(float), fb, (size_t)world_,
-                                          hipMemcpyDeviceToHost, p.main.stream());
-    TORCH_CHECK(e == hipSuccess, "ShardStep: status copy: ", hipGetErrorString(e));
+    // (a hipMemcpy2DAsync straight into the pinned slot would skip the gather into a contiguous
+    // temporary, but it makes this object reference the HIP runtime directly, which the C++
+    // executables must not link a second copy of: _build._exe_flags)
+    auto st = p.gathered.narrow(1, (int64_t)p.status_off, foot_words_).contiguous().view(torch::kInt32);
+    p.ring[slot].copy_(st, /*non_blocking=*/true);
     p.ring_ev[slot]->record(p.main.unwrap());
     pending_.push_back({steps_, slot, pair_cap_, capacity_, live_});
 }
