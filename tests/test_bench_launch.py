@@ -87,8 +87,12 @@ def test_store_exchange_counts_the_ranks_that_joined(tmp_path):
         "                  'second': b.comm_world, 'capturable': a.capturable}), flush=True)\n"
         "dist.destroy_process_group()\n")
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    import socket
+    with socket.socket() as sk:  # a free port (a fixed one can still be held by an earlier run)
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-                        "--master-addr=127.0.0.1", "--master-port=29571", str(script)], env=env,
+                        "--master-addr=127.0.0.1", f"--master-port={port}", str(script)], env=env,
                        stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=240, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     rows = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
