@@ -663,7 +663,12 @@ constexpr int kRbChunk = kRbChunkPairs;  // pairs per pass-B block (4 per thread
 #define GSR_RB_STAGE32 1
 #endif
 static_assert(kRbChunk % 256 == 0 && kRbMaxRows == 256 && kRbMaxCols == 256, "one row / column per thread");
-constexpr int kRbStageA = 2048;  // LDS staging (pairs) of a pass-A block (~720 at 1M / 1080p)
+#ifndef GSR_RB_STAGE_A
+#define GSR_RB_STAGE_A 1024
+#endif
+// LDS staging (pairs) of a pass-A block (~720 at 1M / 1080p; a block past it writes unstaged):
+// 1024 keeps the block at 16 KB, 8 waves per SIMD (2048: 30 KB, 5)
+constexpr int kRbStageA = GSR_RB_STAGE_A;
 constexpr int kRbStage = 4096;   // LDS staging (instances) of a pass-B block (~2800 at 1M / 1080p)
 constexpr uint32_t kRbAgg = 1u << 30, kRbInc = 2u << 30, kRbCntMask = kRbAgg - 1u;
 
@@ -1006,7 +1011,10 @@ __global__ __launch_bounds__(kRbScanThreads) void rb_tiles_scan(const uint32_t* 
 // ppair, so the per-tile sort that follows reads its keys coalesced instead of gathering one
 // behind every gid load, one 8-B store per instance).  The staging holds each instance's pair
 // index (u16) and column; the chunk's pairs (gid, key) sit in LDS beside it.
-__global__ __launch_bounds__(256) void rb_chunks_place(const uint32_t* __restrict__ pgid, const uint32_t* __restrict__ pxr,
+#ifndef GSR_RB_PLACE_WPE
+#define GSR_RB_PLACE_WPE 1
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_RB_PLACE_WPE))) void rb_chunks_place(const uint32_t* __restrict__ pgid, const uint32_t* __restrict__ pxr,
                                                        const uint32_t* __restrict__ totA, int R, int gx, int ty0,
                                                        long long pcap, long long cap,
                                                        const uint32_t* __restrict__ histB,
