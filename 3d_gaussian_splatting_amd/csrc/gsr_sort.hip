@@ -669,7 +669,10 @@ static_assert(kRbChunk % 256 == 0 && kRbMaxRows == 256 && kRbMaxCols == 256, "on
 // LDS staging (pairs) of a pass-A block (~720 at 1M / 1080p; a block past it writes unstaged):
 // 1024 keeps the block at 16 KB, 8 waves per SIMD (2048: 30 KB, 5)
 constexpr int kRbStageA = GSR_RB_STAGE_A;
-constexpr int kRbStage = 4096;   // LDS staging (instances) of a pass-B block (~2800 at 1M / 1080p)
+#ifndef GSR_RB_STAGE_B
+#define GSR_RB_STAGE_B 4096
+#endif
+constexpr int kRbStage = GSR_RB_STAGE_B;  // LDS staging (instances) of a pass-B block (~2800 at 1M / 1080p)
 constexpr uint32_t kRbAgg = 1u << 30, kRbInc = 2u << 30, kRbCntMask = kRbAgg - 1u;
 
 // rows of one block's Gaussians -> histA[r * nbA + b] (F1 writes the same counts itself when it
