@@ -38,6 +38,9 @@ constexpr float kC1 = 0.4886025119029199f;
 // conversion runs once on the per-Gaussian sum, with the Gaussian's own conic and opacity from
 // its blend record.  The 48-B result lands at grad2d[gid].
 constexpr int kGatherWin = 512;
+#ifndef GSR_GATHER_FLAG_AHEAD
+#define GSR_GATHER_FLAG_AHEAD 1
+#endif
 
 // rrect (presort mode): index i is a depth rank whose emission range the rank-order offsets give;
 // its Gaussian (record read, grad2d row written) is rrect[i].z.  nullptr: i is the gid itself.
@@ -70,10 +73,33 @@ __global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __re
 #pragma unroll
     for (int k = 0; k < 9; ++k) a[k] = 0.f;
     const uint8_t* wvb = reinterpret_cast<const uint8_t*>(wv);
+#if GSR_GATHER_FLAG_AHEAD
+    // each window's flags are loaded during the previous window's entry loads (two per thread in
+    // registers), so a window waits for one load round, not two
+    static_assert(kGatherWin == 512, "two flags per thread");
+    uint32_t fa = 0u, fb = 0u;
+    {
+        const uint32_t n0 = J1 - J0 < (uint32_t)kGatherWin ? J1 - J0 : (uint32_t)kGatherWin;
+        if (threadIdx.x < n0) fa = fl[(size_t)J0 + threadIdx.x];
+        if (threadIdx.x + 256 < n0) fb = fl[(size_t)J0 + threadIdx.x + 256];
+    }
+#endif
     for (uint32_t W = J0; W < J1; W += kGatherWin) {
         const uint32_t n = J1 - W < (uint32_t)kGatherWin ? J1 - W : (uint32_t)kGatherWin;
+#if GSR_GATHER_FLAG_AHEAD
+        if (threadIdx.x < n) reinterpret_cast<uint8_t*>(wv)[threadIdx.x] = (uint8_t)fa;
+        if (threadIdx.x + 256 < n) reinterpret_cast<uint8_t*>(wv)[threadIdx.x + 256] = (uint8_t)fb;
+        __syncthreads();
+        {
+            const uint32_t W2 = W + kGatherWin;
+            const uint32_t n2 = W2 < J1 ? (J1 - W2 < (uint32_t)kGatherWin ? J1 - W2 : (uint32_t)kGatherWin) : 0u;
+            fa = threadIdx.x < n2 ? fl[(size_t)W2 + threadIdx.x] : 0u;
+            fb = threadIdx.x + 256 < n2 ? fl[(size_t)W2 + threadIdx.x + 256] : 0u;
+        }
+#else
         for (uint32_t i = threadIdx.x; i < n; i += 256) reinterpret_cast<uint8_t*>(wv)[i] = fl[(size_t)W + i];
         __syncthreads();
+#endif
         for (uint32_t i = threadIdx.x; i < 2 * n; i += 256)
             w8[i] = wvb[i >> 1] ? p8[2 * (size_t)W + i] : make_float4(0.f, 0.f, 0.f, 0.f);
         for (uint32_t i = threadIdx.x; i < n; i += 256) w1[i] = wvb[i] ? p1[(size_t)W + i] : 0.f;
