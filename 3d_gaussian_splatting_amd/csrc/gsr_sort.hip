@@ -351,21 +351,58 @@ __device__ __forceinline__ uint32_t wide_block_scan(uint32_t* __restrict__ a, in
     return carry;
 }
 
+// The single-round scan through LDS (dynamic LDS of n words, n <= kScanQ1 x 1024): the array is
+// loaded and stored coalesced (word i by thread i mod 1024), and each thread scans its Q
+// consecutive words out of LDS -- the direct form's loads of Q consecutive words per thread touch
+// a different cache line in every lane of every load instruction.
+#ifndef GSR_SCAN_LDS
+#define GSR_SCAN_LDS 1
+#endif
+__device__ __forceinline__ uint32_t wide_block_scan_lds(uint32_t* __restrict__ a, int n, uint32_t* wsum,
+                                                        uint32_t* buf) {
+    for (int i = (int)threadIdx.x; i < n; i += 1024) buf[i] = a[i];
+    __syncthreads();
+    const int Q = (n + 1023) / 1024;
+    const int i0 = (int)threadIdx.x * Q;
+    uint32_t v[kScanQ1], sv = 0;
+#pragma unroll
+    for (int q = 0; q < kScanQ1; ++q) {
+        v[q] = q < Q && i0 + q < n ? buf[i0 + q] : 0u;
+        sv += v[q];
+    }
+    uint32_t tot;
+    uint32_t run = block_exclusive_scan(sv, wsum, &tot);
+#pragma unroll
+    for (int q = 0; q < kScanQ1; ++q) {
+        if (q < Q && i0 + q < n) buf[i0 + q] = run;
+        run += v[q];
+    }
+    __syncthreads();
+    for (int i = (int)threadIdx.x; i < n; i += 1024) a[i] = buf[i];
+    return tot;
+}
+__host__ __device__ constexpr bool scan_lds_fits(long long n) { return GSR_SCAN_LDS && n <= 1024LL * kScanQ1; }
+
 // exclusive scan of the nb block totals in place; the grand total to *total_out
 __global__ __launch_bounds__(1024) void scan_partials(uint32_t* __restrict__ partials, int nb,
                                                       uint32_t* __restrict__ total_out) {
+    extern __shared__ uint32_t sbuf[];
     __shared__ uint32_t wsum[16];
-    const uint32_t carry = wide_block_scan(partials, nb, wsum);
+    const uint32_t carry = scan_lds_fits(nb) ? wide_block_scan_lds(partials, nb, wsum, sbuf)
+                                             : wide_block_scan(partials, nb, wsum);
     if (threadIdx.x == 0 && total_out) *total_out = carry;
 }
 
 // the row-bucketed binning's column scan: row r's per-block pair counts (histA[r][*]) in place,
 // the row total to totA[r]; one 1024-thread block per row
 __global__ __launch_bounds__(1024) void rb_colscan(uint32_t* __restrict__ hist, int nb, uint32_t* __restrict__ totals) {
+    extern __shared__ uint32_t sbuf[];
     __shared__ uint32_t wsum[16];
-    const uint32_t carry = wide_block_scan(hist + (size_t)blockIdx.x * nb, nb, wsum);
+    uint32_t* const a = hist + (size_t)blockIdx.x * nb;
+    const uint32_t carry = scan_lds_fits(nb) ? wide_block_scan_lds(a, nb, wsum, sbuf) : wide_block_scan(a, nb, wsum);
     if (threadIdx.x == 0) totals[blockIdx.x] = carry;
 }
+static size_t scan_lds_bytes(long long n) { return scan_lds_fits(n) ? sizeof(uint32_t) * (size_t)n : 0; }
 
 __global__ __launch_bounds__(kB) void scan_downsweep(const uint32_t* __restrict__ in, int n,
                                                      const uint32_t* __restrict__ partials,
@@ -2312,7 +2349,7 @@ int launch_scan(const uint32_t* tiles, int n, uint32_t* offsets, uint32_t* scan_
     if (fused_ok && n <= kFusedScanMax) return 0;  // scanned by the fused kernel in launch_duplicate
     const int nb = sort_blocks(n);
     hipLaunchKernelGGL(scan_reduce, dim3(nb), dim3(kB), 0, s, tiles, n, scan_partials_buf);
-    hipLaunchKernelGGL(scan_partials, dim3(1), dim3(1024), 0, s, scan_partials_buf, nb, total_out);
+    hipLaunchKernelGGL(scan_partials, dim3(1), dim3(1024), scan_lds_bytes(nb), s, scan_partials_buf, nb, total_out);
     hipLaunchKernelGGL(scan_downsweep, dim3(nb), dim3(kB), 0, s, tiles, n, scan_partials_buf, offsets);
     return (int)hipGetLastError();
 }
@@ -2331,7 +2368,8 @@ __global__ __launch_bounds__(256) void block_offsets_kernel(const uint32_t* __re
 
 int launch_scan_blocks(uint32_t* bsum, int n, uint32_t* total_out, hipStream_t s) {
     if (n <= 0) return (int)hipMemsetAsync(total_out, 0, sizeof(uint32_t), s);
-    hipLaunchKernelGGL(scan_partials, dim3(1), dim3(1024), 0, s, bsum, div_up(n, 256), total_out);
+    hipLaunchKernelGGL(scan_partials, dim3(1), dim3(1024), scan_lds_bytes(div_up(n, 256)), s, bsum, div_up(n, 256),
+                       total_out);
     return (int)hipGetLastError();
 }
 
@@ -2354,7 +2392,7 @@ int launch_rb_binning(const uint32_t* tiles, uint4* rect, uint32_t* offsets, int
     uint32_t* const totA = histA + (size_t)256 * nbA;
     if (!rows_counted)
         hipLaunchKernelGGL(rb_rows_count, dim3(nbA), dim3(256), 0, s, tiles, rect, n, ty0, ty1, histA, nbA);
-    hipLaunchKernelGGL(rb_colscan, dim3(R), dim3(1024), 0, s, histA, nbA, totA);
+    hipLaunchKernelGGL(rb_colscan, dim3(R), dim3(1024), scan_lds_bytes(nbA), s, histA, nbA, totA);
     hipLaunchKernelGGL(rb_rows_place, dim3(nbA), dim3(256), 0, s, tiles, rect, offsets, bsum, n, ty0, ty1, histA, totA,
                        nbA, pgid, pxr, cap, depth_key, ppair);
     // chunks: at most cap / kRbChunk full ones plus one partial per row; the blocks walk them, so
@@ -2398,7 +2436,7 @@ int launch_depth_presort(const uint32_t* depth_key, const uint32_t* tiles, const
     const int nb = div_up(n, 256);
     hipLaunchKernelGGL(rank_payload_kernel, dim3(nb), dim3(256), 0, s, sgid, tiles, rect, n, rtiles, rrect, bsum);
     // the 256-rank blocks' exclusive offsets and K: F3 (launch_duplicate_ranked) scans inside them
-    hipLaunchKernelGGL(scan_partials, dim3(1), dim3(1024), 0, s, bsum, nb, total_out);
+    hipLaunchKernelGGL(scan_partials, dim3(1), dim3(1024), scan_lds_bytes(nb), s, bsum, nb, total_out);
     return (int)hipGetLastError();
 }
 
