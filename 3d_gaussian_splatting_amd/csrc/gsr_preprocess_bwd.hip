@@ -41,6 +41,9 @@ constexpr int kGatherWin = 512;
 #ifndef GSR_GATHER_FLAG_AHEAD
 #define GSR_GATHER_FLAG_AHEAD 1
 #endif
+#ifndef GSR_GATHER_DATA_AHEAD
+#define GSR_GATHER_DATA_AHEAD 1
+#endif
 
 // rrect (presort mode): index i is a depth rank whose emission range the rank-order offsets give;
 // its Gaussian (record read, grad2d row written) is rrect[i].z.  nullptr: i is the gid itself.
@@ -73,6 +76,76 @@ __global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __re
 #pragma unroll
     for (int k = 0; k < 9; ++k) a[k] = 0.f;
     const uint8_t* wvb = reinterpret_cast<const uint8_t*>(wv);
+#if GSR_GATHER_DATA_AHEAD
+    // Each window's entries are loaded into registers during the previous window's sums (4 float4 +
+    // 2 floats per thread), and its flags a window earlier still (double-buffered in LDS): after
+    // the first window no window waits on a load round at all.
+    static_assert(kGatherWin == 512, "two entries per thread");
+    __shared__ uint32_t wvd[2][kGatherWin / 4];
+    (void)wvb;
+    auto nwin = [&](uint32_t W) -> uint32_t {
+        return W < J1 ? (J1 - W < (uint32_t)kGatherWin ? J1 - W : (uint32_t)kGatherWin) : 0u;
+    };
+    float4 d8[4];
+    float d1[2];
+    auto load_data = [&](uint32_t Wx, uint32_t nx, const uint8_t* fb) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t i = threadIdx.x + 256u * k;
+            d8[k] = i < 2 * nx && fb[i >> 1] ? p8[2 * (size_t)Wx + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t i = threadIdx.x + 256u * k;
+            d1[k] = i < nx && fb[i] ? p1[(size_t)Wx + i] : 0.f;
+        }
+    };
+    uint32_t fa = 0u, fb2 = 0u;  // flags of the window after the next
+    if (J0 < J1) {
+        const uint32_t n0 = nwin(J0);
+        uint8_t* f0 = reinterpret_cast<uint8_t*>(wvd[0]);
+        if (threadIdx.x < n0) f0[threadIdx.x] = fl[(size_t)J0 + threadIdx.x];
+        if (threadIdx.x + 256 < n0) f0[threadIdx.x + 256] = fl[(size_t)J0 + threadIdx.x + 256];
+        __syncthreads();
+        load_data(J0, n0, f0);
+        const uint32_t n1 = nwin(J0 + kGatherWin);
+        if (threadIdx.x < n1) fa = fl[(size_t)J0 + kGatherWin + threadIdx.x];
+        if (threadIdx.x + 256 < n1) fb2 = fl[(size_t)J0 + kGatherWin + threadIdx.x + 256];
+    }
+    int buf = 0;
+    for (uint32_t W = J0; W < J1; W += kGatherWin, buf ^= 1) {
+        const uint32_t n = nwin(W);
+        // this window's entries -> LDS; the next window's flags -> the other flag buffer
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t i = threadIdx.x + 256u * k;
+            if (i < 2 * n) w8[i] = d8[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t i = threadIdx.x + 256u * k;
+            if (i < n) w1[i] = d1[k];
+        }
+        uint8_t* const fnx = reinterpret_cast<uint8_t*>(wvd[buf ^ 1]);
+        const uint32_t n1 = nwin(W + kGatherWin);
+        if (threadIdx.x < n1) fnx[threadIdx.x] = (uint8_t)fa;
+        if (threadIdx.x + 256 < n1) fnx[threadIdx.x + 256] = (uint8_t)fb2;
+        __syncthreads();
+        // the next window's entries and the flags after it stay in flight during this window's sums
+        if (n1) load_data(W + kGatherWin, n1, fnx);
+        const uint32_t n2 = nwin(W + 2 * kGatherWin);
+        fa = threadIdx.x < n2 ? fl[(size_t)W + 2 * kGatherWin + threadIdx.x] : 0u;
+        fb2 = threadIdx.x + 256 < n2 ? fl[(size_t)W + 2 * kGatherWin + threadIdx.x + 256] : 0u;
+        const uint32_t lo = s > W ? s : W, hi = e < W + n ? e : W + n;
+        for (uint32_t j = lo; j < hi; ++j) {
+            const float4 u = w8[2 * (j - W)], v = w8[2 * (j - W) + 1];
+            a[0] += u.x; a[1] += u.y; a[2] += u.z; a[3] += u.w;
+            a[4] += v.x; a[5] += v.y; a[6] += v.z; a[7] += v.w;
+            a[8] += w1[j - W];
+        }
+        __syncthreads();
+    }
+#else
 #if GSR_GATHER_FLAG_AHEAD
     // each window's flags are loaded during the previous window's entry loads (two per thread in
     // registers), so a window waits for one load round, not two
@@ -113,6 +186,7 @@ __global__ __launch_bounds__(256) void gather_grad2d_kernel(const uint32_t* __re
         }
         __syncthreads();
     }
+#endif
     if (g >= P) return;
     // moments -> d mean2D (NDC), d conic, d opacity (sum G dL/dalpha = S0 / o), d colour
     const float A = -2.0f * kLn2 * q0.z, B = -kLn2 * q0.w, C = -2.0f * kLn2 * q1.x;
